@@ -1,0 +1,287 @@
+/*
+ * lgx.h — C ABI of liblgx.so, the MI355X-native vectorised legged-robot env step.
+ *
+ * This ABI replaces, for the env-step hot path, the calls the reference makes into
+ * Isaac Gym (closed PhysX binary) plus the eager-torch post-physics pipeline:
+ *
+ *   lgx_step        replaces LeggedRobot.step()            legged_robot.py:67-100
+ *                   (clip → 4× {_compute_torques :440-478, gym.simulate :82,
+ *                    refresh_dof_state :85} → post_physics_step → clip obs :91-95)
+ *                   with Go2Robot.post_physics_step          go2.py:345-387
+ *                   or LeggedRobot.post_physics_step         legged_robot.py:103-138
+ *   lgx_post_physics  the post-physics half alone (physics state supplied by the
+ *                   caller) — used for parity against the reference's tensor code
+ *   lgx_reset_envs  replaces BaseTask.reset → reset_idx(all)  base_task.py:131-135,
+ *                   go2.py:207-263 / legged_robot.py:157-213 (+ set_*_tensor_indexed
+ *                   legged_robot.py:504-506,530-532)
+ *   lgx_episode_stats  extras['episode'] means over reset envs without a host sync
+ *                   (go2.py:246-249) — reduced on device
+ *
+ * Conventions: every buffer is env-major (row = one env), fp32 unless stated, owned
+ * by the caller (PyTorch caching allocator) and bound once with lgx_bind (re-bind when
+ * a tensor is replaced). Quaternions are xyzw as in the reference (legged_robot.py:640).
+ * All work is stream-ordered on the stream passed in; no call synchronises the host.
+ * Return value: 0 = ok, <0 = error; lgx_last_error() gives the message.
+ */
+#ifndef LGX_H
+#define LGX_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LGX_ABI_VERSION 1
+
+#define LGX_MAX_DOF 12
+#define LGX_MAX_LINKS 16          /* dynamic links: base + 12 leg links (+spare) */
+#define LGX_MAX_BODIES 24         /* reported rigid bodies (Go2: 19, ANYmal: 17) */
+#define LGX_MAX_FEET 4
+#define LGX_MAX_PROPRIO 240       /* Go2 52, ANYmal 235 */
+#define LGX_MAX_HEIGHT_POINTS 192 /* Go2 132, ANYmal 187 */
+#define LGX_MAX_REWARDS 40
+#define LGX_MAX_CANDIDATES 64     /* contact candidate points, one per lane */
+#define LGX_MAX_CONTACTS 16       /* active contact points solved per substep */
+#define LGX_MAX_PENALISED 24
+#define LGX_MAX_TERMINATION 8
+
+/* task flavour: which post_physics_step / compute_observations the step follows */
+enum lgx_task_kind {
+  LGX_TASK_LEGGED = 0, /* LeggedRobot (ANYmal): legged_robot.py:103-273 */
+  LGX_TASK_GO2 = 1     /* Go2Robot: go2.py:186-574 */
+};
+
+enum lgx_mesh_type { LGX_MESH_PLANE = 0, LGX_MESH_HEIGHTFIELD = 1, LGX_MESH_TRIMESH = 2 };
+
+enum lgx_control_type { LGX_CONTROL_P = 0, LGX_CONTROL_V = 1, LGX_CONTROL_T = 2 };
+
+/* reward terms; the host passes them in the reference's order (alphabetical,
+ * helpers.py:45 class_to_dict → dir()) with scales already multiplied by dt
+ * (legged_robot.py:735-750). Names = the `_reward_<name>` methods. */
+enum lgx_reward_id {
+  LGX_REW_ACTION_RATE = 0,      /* legged_robot.py:1079 */
+  LGX_REW_ANG_VEL_XY,           /* legged_robot.py:1042 */
+  LGX_REW_BASE_HEIGHT,          /* legged_robot.py:1054 */
+  LGX_REW_CALF_COLLISION,       /* go2.py:689 */
+  LGX_REW_CALF_POS,             /* go2.py:613 */
+  LGX_REW_CALF_SYMMETRY,        /* go2.py:724 */
+  LGX_REW_COLLISION,            /* legged_robot.py:1085 */
+  LGX_REW_DELTA_TORQUES,        /* go2.py:578 */
+  LGX_REW_DOF_ACC,              /* legged_robot.py:1073 */
+  LGX_REW_DOF_ERROR,            /* go2.py:584 */
+  LGX_REW_DOF_POS_LIMITS,       /* legged_robot.py:1097 */
+  LGX_REW_DOF_VEL,              /* legged_robot.py:1067 */
+  LGX_REW_DOF_VEL_LIMITS,       /* legged_robot.py:1105 */
+  LGX_REW_FEET_AIR_TIME,        /* go2.py:819 (stateful) */
+  LGX_REW_FEET_CONTACT_FORCES,  /* legged_robot.py:1145 */
+  LGX_REW_HEADING_ALIGNMENT,    /* go2.py:734 */
+  LGX_REW_HIP_POS,              /* go2.py:599 */
+  LGX_REW_JUMP_ZONE_FORWARD_VEL,/* go2.py:768 */
+  LGX_REW_JUMP_ZONE_UPWARD_VEL, /* go2.py:782 */
+  LGX_REW_LIN_VEL_Z,            /* legged_robot.py:1036 */
+  LGX_REW_MIN_HEIGHT,           /* go2.py:795 */
+  LGX_REW_ORIENTATION,          /* legged_robot.py:1048 */
+  LGX_REW_PHASE_CONTACT_MATCH,  /* go2.py:621 */
+  LGX_REW_PHASE_FOOT_LIFTING,   /* go2.py:647 */
+  LGX_REW_REVERSE_PENALTY,      /* go2.py:759 */
+  LGX_REW_STAND_STILL,          /* legged_robot.py:1139 */
+  LGX_REW_STUMBLE_CALVES,       /* go2.py:681 */
+  LGX_REW_STUMBLE_FEET,         /* legged_robot.py:1132 */
+  LGX_REW_THIGH_POS,            /* go2.py:606 */
+  LGX_REW_THIGH_SYMMETRY,       /* go2.py:715 */
+  LGX_REW_TORQUE_LIMITS,        /* legged_robot.py:1112 */
+  LGX_REW_TORQUES,              /* legged_robot.py:1061 */
+  LGX_REW_TRACKING_ANG_VEL,     /* legged_robot.py:1125 */
+  LGX_REW_TRACKING_LIN_VEL,     /* legged_robot.py:1118 */
+  LGX_REW_TRACKING_PITCH,       /* go2.py:697 */
+  LGX_REW_TRACKING_ROLL,        /* go2.py:706 */
+  LGX_REW_ZERO_CMD_DOF_ERROR,   /* go2.py:809 (second definition wins, Q27) */
+  LGX_REW_COUNT
+};
+
+/* ---------------------------------------------------------------------------
+ * Rigid-body model (built on the host from the URDF, collapse_fixed_joints=True,
+ * legged_robot_config.py:95). Dynamic links: link 0 = floating base; every other
+ * link hangs off its parent through one revolute joint (dof index = link-1).
+ * ------------------------------------------------------------------------- */
+typedef struct lgx_model {
+  int32_t num_links;                      /* 1 + num_dof */
+  int32_t num_bodies;                     /* reported rigid bodies (body_names order) */
+  int32_t num_candidates;                 /* contact candidate points */
+  int32_t link_parent[LGX_MAX_LINKS];     /* -1 for the base */
+  float joint_origin[LGX_MAX_LINKS][3];   /* joint anchor in the parent link frame */
+  float joint_axis[LGX_MAX_LINKS][3];     /* unit axis in the joint (= child) frame */
+  float joint_rot[LGX_MAX_LINKS][9];      /* joint frame rotation in the parent link frame (row-major) */
+  float joint_lower[LGX_MAX_LINKS];       /* hard URDF limits (PhysX enforces) */
+  float joint_upper[LGX_MAX_LINKS];
+  int32_t joint_has_limits[LGX_MAX_LINKS];
+  float link_mass[LGX_MAX_LINKS];         /* collapsed (fixed children merged) */
+  float link_com[LGX_MAX_LINKS][3];       /* COM in link frame */
+  float link_inertia[LGX_MAX_LINKS][6];   /* about COM, link frame: xx yy zz xy xz yz */
+  /* reported bodies: pose = link pose * fixed offset */
+  int32_t body_link[LGX_MAX_BODIES];
+  float body_offset[LGX_MAX_BODIES][3];
+  float body_rot[LGX_MAX_BODIES][9];      /* fixed rotation of the body in its link frame */
+  /* contact candidates: sphere centre (radius >= 0) in its link frame */
+  int32_t cand_link[LGX_MAX_CANDIDATES];
+  int32_t cand_body[LGX_MAX_CANDIDATES];  /* reported body that receives the force */
+  float cand_pos[LGX_MAX_CANDIDATES][3];
+  float cand_radius[LGX_MAX_CANDIDATES];
+} lgx_model;
+
+typedef struct lgx_task_params {
+  int32_t abi_version;
+  int32_t task_kind;                      /* enum lgx_task_kind */
+  int32_t num_envs;                       /* envs in this shard */
+  int32_t num_envs_total;                 /* global N (terrain_types, legged_robot.py:914) */
+  int32_t env_id_offset;                  /* global id of this shard's env 0 (RNG key) */
+  int32_t num_dof, num_bodies, num_actions, num_feet;
+  int32_t num_proprio, history_len, num_obs, num_priv, num_est, num_scan, num_critic;
+  int32_t num_height_points;
+  int32_t num_reward_terms;
+  int32_t decimation;
+  float sim_dt, dt;                       /* dt = decimation * sim_dt (legged_robot.py:946) */
+  /* actions / actuator: legged_robot.py:440-478 */
+  float action_scale, clip_actions, clip_obs;
+  int32_t control_type;
+  int32_t randomize_kp_kd;
+  float p_gains[LGX_MAX_DOF];
+  float d_gains[LGX_MAX_DOF];
+  float default_dof_pos[LGX_MAX_DOF];
+  float torque_limits[LGX_MAX_DOF];
+  float dof_pos_limits[LGX_MAX_DOF][2];   /* soft limits (legged_robot.py:354-357) */
+  float dof_vel_limits[LGX_MAX_DOF];
+  float soft_dof_vel_limit, soft_torque_limit;
+  /* observations */
+  float obs_scale_lin_vel, obs_scale_ang_vel, obs_scale_dof_pos, obs_scale_dof_vel, obs_scale_height;
+  int32_t add_noise;
+  float noise_vec[LGX_MAX_PROPRIO];
+  int32_t measure_heights;                /* LEGGED: heights in obs (legged_robot.py:254) */
+  float height_points[LGX_MAX_HEIGHT_POINTS][2]; /* base-frame (x,y), meshgrid(x,y) order */
+  /* commands: go2.py:413-464 / legged_robot.py:406-437 */
+  int32_t heading_command, zero_command, resample_interval, has_user_command;
+  float cmd_lin_vel_x[2], cmd_lin_vel_y[2], cmd_ang_vel_yaw[2], cmd_heading[2];
+  float heading_error_gain, zero_command_prob;
+  float user_command[4];
+  float commands_scale[3];
+  /* gait phase: go2.py:279-290 */
+  float period, offset_fl, offset_fr, offset_bl, offset_br;
+  /* termination: go2.py:186-204 */
+  int32_t max_episode_length;             /* ceil(T/dt), legged_robot.py:954 */
+  float max_episode_length_s;
+  int32_t parkour;
+  int32_t n_termination;
+  int32_t termination_idx[LGX_MAX_TERMINATION];
+  int32_t n_penalised;
+  int32_t penalised_idx[LGX_MAX_PENALISED];
+  int32_t feet_idx[LGX_MAX_FEET];
+  int32_t calf_idx[LGX_MAX_FEET];
+  int32_t hip_joint_idx[LGX_MAX_FEET], thigh_joint_idx[LGX_MAX_FEET], calf_joint_idx[LGX_MAX_FEET];
+  /* rewards */
+  int32_t reward_ids[LGX_MAX_REWARDS];
+  float reward_scales[LGX_MAX_REWARDS];
+  int32_t only_positive_rewards;
+  int32_t has_termination_reward;
+  float termination_scale;
+  float tracking_sigma, base_height_target, max_foot_height, percent_time_on_ground;
+  float max_contact_force, pitch_deg_target, roll_deg_target;
+  /* domain randomisation events: legged_robot.py:535-540 */
+  int32_t push_robots, push_interval;
+  float max_push_vel_xy;
+  /* reset: legged_robot.py:481-532 */
+  float base_init_state[13];
+  int32_t custom_origins;
+  /* terrain: legged_robot.py:997-1032 (height_samples int16 [rows, cols]) */
+  int32_t mesh_type;
+  float horizontal_scale, vertical_scale, border_size;
+  int32_t hf_rows, hf_cols;
+  int32_t curriculum;
+  float terrain_length, promote_threshold, demote_threshold;
+  int32_t max_terrain_level, num_terrain_rows, num_terrain_cols;
+  /* physics (this build's solver; replaces PhysX TGS, legged_robot_config.py:183-200) */
+  float gravity[3];
+  float ground_friction;                  /* terrain static/dynamic friction (plane 1.0) */
+  int32_t solver_iterations;              /* projected Gauss-Seidel sweeps per substep */
+  float baumgarte, slop, max_depenetration_vel, contact_margin, limit_margin;
+} lgx_task_params;
+
+/* Every per-env buffer the step reads/writes. NULL = not present. */
+typedef struct lgx_buffers {
+  /* physics state (the reference's gym state tensors, legged_robot.py:640-646) */
+  float* root_states;          /* [N,13] pos, quat xyzw, world lin vel, world ang vel */
+  float* dof_state;            /* [N,D,2] pos, vel */
+  float* contact_forces;       /* [N,B,3] world-frame net contact force per body */
+  float* rigid_body_states;    /* [N,B,13] */
+  /* actuation */
+  const float* actions_in;     /* [N,A] raw policy actions */
+  float* actions;              /* [N,A] clipped actions (self.actions) */
+  float* torques;              /* [N,D] last-substep torques */
+  /* carried post-physics state */
+  float* last_actions;         /* [N,A] */
+  float* last_dof_vel;         /* [N,D] */
+  float* last_root_vel;        /* [N,6] */
+  float* last_base_lin_vel;    /* [N,3] */
+  float* last_torques;         /* [N,D] */
+  float* commands;             /* [N,4] vx vy wz heading */
+  int64_t* episode_length;     /* [N] int64 (torch.long) */
+  float* episode_sums;         /* [K,N] per reward term (+ termination last if present) */
+  float* obs_history;          /* [N,H,P] */
+  uint8_t* last_contacts;      /* [N,F] bool */
+  float* last_contact_heights; /* [N,F] */
+  float* feet_air_time;        /* [N,F] */
+  /* outputs */
+  float* obs;                  /* [N,O] */
+  float* priv;                 /* [N,num_priv] */
+  float* critic;               /* [N,C] */
+  float* est;                  /* [N,num_est] */
+  float* scan;                 /* [N,num_scan] */
+  float* rew;                  /* [N] */
+  uint8_t* reset;              /* [N] bool */
+  uint8_t* time_out;           /* [N] bool */
+  float* base_lin_vel;         /* [N,3] */
+  float* base_ang_vel;         /* [N,3] */
+  float* projected_gravity;    /* [N,3] */
+  float* rpy_phase;            /* [N,8] roll pitch yaw phase_fl phase_fr phase_bl phase_br jump_flag */
+  float* measured_heights;     /* [N,num_height_points] */
+  /* setup-time per-env parameters (domain randomisation, legged_robot.py:306-380) */
+  const float* friction;       /* [N] */
+  const float* mass_params;    /* [N,4] added base mass, added com xyz */
+  const float* kp_kd;          /* [2,N,D] */
+  float* env_origins;          /* [N,3] */
+  int64_t* terrain_levels;     /* [N] */
+  const int64_t* terrain_types;/* [N] */
+  const float* terrain_origins;/* [rows,cols,3] */
+  const int16_t* height_samples; /* [hf_rows, hf_cols] */
+  /* device-side reductions for extras['episode'] (go2.py:246-249): [K+1] sums + count */
+  float* episode_stats;
+} lgx_buffers;
+
+typedef struct lgx_env lgx_env;
+
+int32_t lgx_abi_version(void);
+int64_t lgx_sizeof_model(void);
+int64_t lgx_sizeof_task_params(void);
+int64_t lgx_sizeof_buffers(void);
+
+/* device >= 0: HIP device ordinal. */
+int lgx_create(const lgx_model* model, const lgx_task_params* params, int32_t device, lgx_env** out);
+int lgx_bind(lgx_env* env, const lgx_buffers* buffers);
+/* one env step: decimation physics substeps + post-physics. step_counter is the
+ * reference's common_step_counter AFTER its increment (legged_robot.py:112). */
+int lgx_step(lgx_env* env, uint64_t seed, uint64_t step_counter, void* hip_stream);
+/* post-physics only: the caller has written the physics state (root/dof/contact/
+ * rigid-body) and torques; otherwise identical to the tail of lgx_step. */
+int lgx_post_physics(lgx_env* env, uint64_t seed, uint64_t step_counter, void* hip_stream);
+/* physics substeps only (decimation × {PD torque, dynamics, contacts}). */
+int lgx_physics(lgx_env* env, void* hip_stream);
+/* reset_idx for the envs with env_mask[i] != 0 (device pointer, uint8 [N]);
+ * reset_call numbers external reset calls for the RNG stream. */
+int lgx_reset_envs(lgx_env* env, const uint8_t* env_mask, uint64_t seed, uint64_t reset_call, void* hip_stream);
+const char* lgx_last_error(const lgx_env* env);
+void lgx_destroy(lgx_env* env);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LGX_H */

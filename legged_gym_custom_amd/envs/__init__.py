@@ -1,0 +1,13 @@
+"""Task registration (drop-in for legged_gym/envs/__init__.py:19-24)."""
+from legged_gym_custom_amd.envs.base.legged_robot_config import LeggedRobotCfg, LeggedRobotCfgPPO  # noqa: F401
+from legged_gym_custom_amd.envs.go2.go2_config import Go2Cfg, Go2CfgPPO
+
+_CONFIGS = {
+    "go2": (Go2Cfg, Go2CfgPPO),
+}
+
+
+def task_registry_configs(name):
+    """Fresh (env_cfg, train_cfg) instances for a registered task name."""
+    e, t = _CONFIGS[name]
+    return e(), t()

@@ -1,0 +1,173 @@
+"""Drop-in helpers (legged_gym/utils/helpers.py:41-214): config <-> dict, seeding,
+checkpoint discovery, CLI parsing, TorchScript export.
+
+`get_args` re-implements the Isaac Gym CLI surface the reference exposes
+(gymutil.parse_arguments + the custom flags at helpers.py:152-178) with argparse, so
+`train.py --task=go2 --headless --sim_device=cuda:0 --rl_device=cuda:0` parses the same.
+"""
+import argparse
+import copy
+import os
+import random
+
+import numpy as np
+import torch
+
+
+def class_to_dict(obj) -> dict:
+    """Recursive config -> dict; keys in dir() (alphabetical) order (helpers.py:41-56)."""
+    if not hasattr(obj, "__dict__"):
+        return obj
+    out = {}
+    for key in dir(obj):
+        if key.startswith("_"):
+            continue
+        val = getattr(obj, key)
+        if isinstance(val, list):
+            out[key] = [class_to_dict(v) for v in val]
+        else:
+            out[key] = class_to_dict(val)
+    return out
+
+
+def update_class_from_dict(obj, d):
+    for key, val in d.items():
+        attr = getattr(obj, key, None)
+        if isinstance(attr, type):
+            update_class_from_dict(attr, val)
+        else:
+            setattr(obj, key, val)
+
+
+def set_seed(seed):
+    if seed == -1:
+        seed = np.random.randint(0, 10000)
+    print("Setting seed: {}".format(seed))
+    random.seed(seed)
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+    os.environ["PYTHONHASHSEED"] = str(seed)
+    if torch.cuda.is_available():
+        torch.cuda.manual_seed(seed)
+        torch.cuda.manual_seed_all(seed)
+
+
+class SimParams:
+    """Stand-in for gymapi.SimParams: the fields the env reads."""
+
+    def __init__(self, sim_cfg=None):
+        self.dt = 0.005
+        self.substeps = 1
+        self.gravity = [0.0, 0.0, -9.81]
+        self.up_axis = 1
+        self.use_gpu_pipeline = True
+        self.physx = argparse.Namespace(num_threads=10, solver_type=1, num_position_iterations=4,
+                                        num_velocity_iterations=0, contact_offset=0.01, rest_offset=0.0,
+                                        bounce_threshold_velocity=0.5, max_depenetration_velocity=1.0,
+                                        use_gpu=True, num_subscenes=0)
+        if sim_cfg:
+            for k, v in sim_cfg.items():
+                if k == "physx":
+                    for pk, pv in v.items():
+                        setattr(self.physx, pk, pv)
+                else:
+                    setattr(self, k, v)
+
+
+def parse_sim_params(args, cfg):
+    sp = SimParams(cfg.get("sim") if isinstance(cfg, dict) else None)
+    sp.use_gpu_pipeline = getattr(args, "use_gpu_pipeline", True)
+    if getattr(args, "num_threads", 0) > 0:
+        sp.physx.num_threads = args.num_threads
+    return sp
+
+
+def get_load_path(root, load_run=-1, checkpoint=-1):
+    try:
+        runs = sorted(os.listdir(root))
+        if "exported" in runs:
+            runs.remove("exported")
+        last_run = os.path.join(root, runs[-1])
+    except Exception:
+        raise ValueError("No runs in this directory: " + root)
+    load_run = last_run if load_run == -1 else os.path.join(root, load_run)
+    if checkpoint == -1:
+        models = sorted([f for f in os.listdir(load_run) if "model" in f], key=lambda m: "{0:0>15}".format(m))
+        model = models[-1]
+    else:
+        model = "model_{}.pt".format(checkpoint)
+    return os.path.join(load_run, model)
+
+
+def update_cfg_from_args(env_cfg, cfg_train, args):
+    if env_cfg is not None and args.num_envs is not None:
+        env_cfg.env.num_envs = args.num_envs
+    if cfg_train is not None:
+        if args.seed is not None:
+            cfg_train.seed = args.seed
+        if args.max_iterations is not None:
+            cfg_train.runner.max_iterations = args.max_iterations
+        if args.resume:
+            cfg_train.runner.resume = args.resume
+        if args.experiment_name is not None:
+            cfg_train.runner.experiment_name = args.experiment_name
+        if args.run_name is not None:
+            cfg_train.runner.run_name = args.run_name
+        if args.load_run is not None:
+            cfg_train.runner.load_run = args.load_run
+        if args.checkpoint is not None:
+            cfg_train.runner.checkpoint = args.checkpoint
+    return env_cfg, cfg_train
+
+
+def _str2bool(v):
+    return str(v).lower() in ("1", "true", "yes", "y")
+
+
+def get_args(argv=None):
+    p = argparse.ArgumentParser(description="RL Policy")
+    # custom flags (helpers.py:153-166)
+    p.add_argument("--task", type=str, default="anymal_c_flat")
+    p.add_argument("--resume", action="store_true", default=False)
+    p.add_argument("--experiment_name", type=str)
+    p.add_argument("--run_name", type=str)
+    p.add_argument("--load_run", type=str)
+    p.add_argument("--checkpoint", type=int)
+    p.add_argument("--headless", action="store_true", default=False)
+    p.add_argument("--horovod", action="store_true", default=False)
+    p.add_argument("--rl_device", type=str, default="cuda:0")
+    p.add_argument("--num_envs", type=int)
+    p.add_argument("--seed", type=int)
+    p.add_argument("--max_iterations", type=int)
+    # Isaac Gym's own flags (gymutil.parse_arguments) the reference reads
+    p.add_argument("--sim_device", type=str, default="cuda:0")
+    p.add_argument("--pipeline", type=str, default="gpu")
+    p.add_argument("--graphics_device_id", type=int, default=0)
+    p.add_argument("--physx", action="store_true", default=True)
+    p.add_argument("--flex", action="store_true", default=False)
+    p.add_argument("--num_threads", type=int, default=0)
+    p.add_argument("--subscenes", type=int, default=0)
+    p.add_argument("--slices", type=int)
+    args = p.parse_args(argv)
+    args.sim_device_type = args.sim_device.split(":")[0]
+    args.compute_device_id = int(args.sim_device.split(":")[1]) if ":" in args.sim_device else 0
+    args.use_gpu_pipeline = args.pipeline in ("gpu", "GPU")
+    args.use_gpu = args.sim_device_type == "cuda"
+    args.physics_engine = 1  # SIM_PHYSX (value kept for API compatibility)
+    args.device = args.sim_device_type
+    # name alignment (helpers.py:174-177)
+    args.sim_device_id = args.compute_device_id
+    args.sim_device = args.sim_device_type
+    if args.sim_device == "cuda":
+        args.sim_device += f":{args.sim_device_id}"
+    return args
+
+
+def export_policy_as_jit(actor_critic, estimator, path):
+    """helpers.py:180-214: policy.pt, adaptation_module.pt, estimator.pt, scan_encoder.pt."""
+    os.makedirs(path, exist_ok=True)
+    for fname, module in (("policy.pt", actor_critic.actor), ("adaptation_module.pt", actor_critic.adaptation_encoder_),
+                          ("estimator.pt", estimator), ("scan_encoder.pt", actor_critic.scan_encoder)):
+        m = copy.deepcopy(module).to("cpu")
+        torch.jit.script(m).save(os.path.join(path, fname))
+        print(f"Exported {fname} to: {path}")
