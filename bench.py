@@ -1,0 +1,169 @@
+#!/usr/bin/env python3
+"""bench.py — BASELINE.json metric: env-steps/sec (whole node), Go2 flat, 4096 envs per GPU.
+
+One "step" = one rsl_rl learning iteration of the drop-in runner on synthetic Go2 flat
+terrain: 24 env steps (policy act + fused HIP env step + storage) + GAE + the PPO/ROA
+update (5 epochs x 4 minibatches) — i.e. Perf/total_fps of on_policy_runner.py:219.
+value = num_envs x 24 x world_size x K / (max over ranks of the timed K iterations).
+
+Also reported: `roofline` of the env-step kernel (algorithmic bytes per launch over its
+HIP-event-timed duration vs 8 TB/s HBM), and `cpu_baseline`: the CPU oracle (C port of
+the same env step) + torch-CPU learner on a bounded sample, rank 0 at N=1 only.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--num_envs 4096]
+  N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "env-steps/sec (whole node), Go2 4096 envs, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0
+
+
+def env_bytes_per_env_step(P, num_bodies, ks):
+    """Algorithmic HBM bytes one env moves per lgx_step (DESIGN.md 'Roofline'):
+    every per-env row the kernel must read and write once (4-B words; int64 = 8 B;
+    bool = 1 B)."""
+    D, A, H, Pp = P.num_dof, P.num_actions, P.history_len, P.num_proprio
+    f = 4
+    rd = f * (A + 2 * D + 2 * D + D + 13 + 4 + 1 + 4 + 1 + 4 + A + D + 4 + ks + H * Pp) + 8 + 4
+    wr = f * (A + num_bodies * 13 + num_bodies * 3 + D + ks + 1 + P.num_obs + P.num_critic + P.num_priv +
+              P.num_est + P.num_scan + H * Pp + A + 2 * D + 2 * D + 6 + 3 + 9 + 13 + 4 + 4 + 4 + 8 +
+              P.num_height_points) + 8 + 2 + 4
+    return rd + wr
+
+
+def cpu_baseline(num_envs=256, iters=1, steps_per_env=24):
+    """Oracle env step (single-threaded C) + torch-CPU rsl_rl learner, same runner."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import cpu_env
+    from legged_gym_custom_amd import model as mdl, params as prm
+    from legged_gym_custom_amd.envs import task_registry_configs
+    from legged_gym_custom_amd.rsl_rl.runners import OnPolicyRunner
+    from legged_gym_custom_amd.utils.helpers import class_to_dict
+    cfg, tcfg = task_registry_configs("go2")
+    cfg.env.num_envs = num_envs
+    m = mdl.load_model(cfg.asset.file, cfg.asset.foot_name)
+    P = prm.build_task_params(cfg, m, num_envs)
+    env = cpu_env.OracleVecEnv(cfg, m, P, mdl.to_struct(m))
+    tcfg.runner.num_steps_per_env = steps_per_env
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    torch.manual_seed(1)
+    runner = OnPolicyRunner(env, class_to_dict(tcfg), None, device="cpu")
+    runner.learn(1, init_at_random_ep_len=True)  # warm-up (also a DAgger iteration: it=0)
+    t0 = time.time()
+    runner.learn(iters)
+    dt = time.time() - t0
+    return {"value": round(num_envs * steps_per_env * iters / dt, 1), "unit": "env-steps/s", "cores": threads,
+            "kind": "port",
+            "sample": f"{iters} PPO iteration(s) of Go2 flat at {num_envs} envs x {steps_per_env} steps on the host: "
+                      f"oracle/lgx_oracle.c env step (1 thread) + torch-CPU learner ({threads} threads)",
+            "seconds": round(dt, 2)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--num_envs", type=int, default=4096)
+    ap.add_argument("--no_cpu_baseline", action="store_true")
+    ap.add_argument("--kernel_iters", type=int, default=50)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    dev = f"cuda:{local}"
+
+    from legged_gym_custom_amd import _abi
+    from legged_gym_custom_amd.envs import task_registry
+    from legged_gym_custom_amd.utils.helpers import get_args
+    a = get_args(["--task=go2", "--headless", f"--num_envs={args.num_envs}", f"--sim_device={dev}",
+                  f"--rl_device={dev}", "--seed=1"])
+    env, env_cfg = task_registry.make_env("go2", a)
+    _, train_cfg = task_registry.get_cfgs("go2")
+    runner, _ = task_registry.make_alg_runner(env, args=a, train_cfg=train_cfg, log_root=None)
+
+    def barrier():
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+
+    runner.learn(num_learning_iterations=args.warmup, init_at_random_ep_len=True)
+    barrier()
+    t0 = time.time()
+    runner.learn(num_learning_iterations=args.steps)
+    barrier()
+    elapsed = time.time() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    steps_per_iter = train_cfg.runner.num_steps_per_env
+    total_env_steps = args.num_envs * steps_per_iter * world * args.steps
+    value = total_env_steps / elapsed
+
+    # ---- env-step kernel alone (HIP events on the launch stream) -> roofline
+    g = torch.Generator(device=dev).manual_seed(1234)
+    acts = torch.clamp(torch.randn(args.kernel_iters, env.num_envs, env.num_actions, device=dev, generator=g), -3.14, 3.14)
+    for i in range(3):
+        env.step(acts[i])
+    stream = torch.cuda.current_stream(dev)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.kernel_iters)]
+    env.actions_in.copy_(acts[0])
+    for i in range(args.kernel_iters):
+        env.actions_in.copy_(acts[i])
+        env.common_step_counter += 1
+        evs[i][0].record(stream)
+        env._native.step(env.seed, env.common_step_counter, stream.cuda_stream)
+        evs[i][1].record(stream)
+    torch.cuda.synchronize(dev)
+    kern_ms = sorted(s.elapsed_time(e) for s, e in evs)
+    kern_avg_ms = sum(kern_ms) / len(kern_ms)
+    ks = len(env._episode_keys)
+    bpe = env_bytes_per_env_step(env.task_params, env.num_bodies, ks)
+    launch_bytes = bpe * env.num_envs
+    achieved = launch_bytes / (kern_avg_ms * 1e-3) / 1e9
+
+    if rank == 0:
+        out = {
+            "metric": METRIC, "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (Go2 flat terrain, random-init ActorCritic/estimator, seed 1)",
+            "config": {"workload": "go2 flat terrain, rsl_rl PPO/ROA iteration (24 env steps + 5x4 minibatch update)",
+                       "num_envs_per_gpu": args.num_envs, "num_steps_per_env": steps_per_iter,
+                       "global_envs": args.num_envs * world, "parallelism": f"env-sharded dp{world}"},
+            "collection_s": round(runner.last_perf.get("collection_time", 0.0), 4),
+            "learn_s": round(runner.last_perf.get("learn_time", 0.0), 4),
+            "env_kernel": {"avg_us": round(kern_avg_ms * 1e3, 2), "min_us": round(kern_ms[0] * 1e3, 2),
+                           "env_steps_per_s": round(env.num_envs / (kern_avg_ms * 1e-3), 1)},
+            "roofline": {"bound": "hbm", "kernel": "lgx::env_step_kernel<true>", "achieved": round(achieved, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "bytes_per_env_step": bpe, "bytes_per_launch": launch_bytes, "traffic": None},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline()
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

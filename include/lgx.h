@@ -225,7 +225,7 @@ typedef struct lgx_buffers {
   float* last_torques;         /* [N,D] */
   float* commands;             /* [N,4] vx vy wz heading */
   int64_t* episode_length;     /* [N] int64 (torch.long) */
-  float* episode_sums;         /* [K,N] per reward term (+ termination last if present) */
+  float* episode_sums;         /* [N,K] per reward term (+ termination last if present) */
   float* obs_history;          /* [N,H,P] */
   uint8_t* last_contacts;      /* [N,F] bool */
   float* last_contact_heights; /* [N,F] */

@@ -1,0 +1,1414 @@
+// lgx_env.hip — MI355X (gfx950) env-step kernels behind include/lgx.h.
+//
+// One wavefront (64 lanes) per environment; the env's state lives in LDS for the whole
+// step (decimation physics substeps + post-physics), so HBM sees each per-env row once
+// in and once out, coalesced (rows are env-major, lanes sweep a row).
+//
+// Physics (replaces PhysX `gym.simulate`, legged_robot.py:79-85; spec in DESIGN.md):
+//   lanes 0..11  PD torques (legged_robot.py:440-478)
+//   lanes 0..3   forward kinematics / composite inertia / bias of one leg chain each
+//   lane  0      6x6 Schur complement of the base (mass matrix is [A B; Bᵀ D], D block
+//                diagonal over the 4 chains) + its Cholesky factor
+//   lanes 0..63  contact candidates (one sphere centre per lane) -> ballot-compacted rows
+//   lanes 0..R-1 one constraint row each: Jacobian row, M⁻¹Jᵀ column (Schur solve), A_rr
+//   lanes 0..17  projected Gauss-Seidel: the generalized velocity is spread over lanes,
+//                each row residual J_r·u is a DPP row reduction, u += M⁻¹J_rᵀ Δλ
+// Post-physics (Go2Robot.post_physics_step go2.py:345-387, LeggedRobot legged_robot.py:
+//   103-138): uniform scalar control flow per env; vector outputs written lane-parallel.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "../../include/lgx.h"
+#include "lgx_device.h"
+
+namespace lgx {
+
+constexpr int NL = 13;  // dynamic links: base + 4 chains x 3 (checked by lgx_create)
+constexpr int NJ = 12;
+constexpr int NU = 18;
+constexpr int MAXC = LGX_MAX_CONTACTS;
+constexpr int MAXR = NJ + 3 * MAXC;
+constexpr int NBLK = 22;  // Philox blocks per env per step (oracle/philox.py NUM_BLOCKS)
+constexpr int NSLOT = NBLK * 4;
+constexpr int MAXHIST = 1216;
+
+enum Slot { S_CMD = 0, S_PUSH = 4, S_TERR = 6, S_DOF = 8, S_ROOT_XY = 20, S_ROOT_VEL = 24, S_RCMD = 32, S_NOISE = 36 };
+
+struct Sh {
+  // --- physics state (base velocity kept as the ORIGIN velocity inside the step)
+  float qb[4], pb[3], vo[3], wb[3];
+  float th[NJ], thd[NJ], tau[NJ], act[NJ], kpm[NJ], kdm[NJ], ldv[NJ];
+  float madd, cadd[3], mu;
+  // --- kinematics per dynamic link
+  float R[NL][9], P[NL][3], Ax[NL][3], W[NL][3], V[NL][3], Al[NL][3], Ao[NL][3], C[NL][3], I[NL][6], m[NL];
+  // --- dynamics
+  float red[5][16];  // partial sums: m, h(3), Ip(6), F(3), N(3) per leg + base
+  float Bc[NJ][6], Dinv[4][6], X[NJ][6], S[4][21], L[21], hj[NJ], hb[6], us[NU], up[NU];
+  // --- constraints
+  float J[MAXR][NU], MJ[MAXR][NU], Arr[MAXR], tgt[MAXR], lam[MAXR];
+  int rkind[MAXR];
+  int cbody[MAXC];
+  int nrows, nlim, ncon;
+  float cf[LGX_MAX_BODIES][3];
+  float rbz[LGX_MAX_BODIES];
+  // --- post-physics
+  float U[NSLOT];
+  float cur[LGX_MAX_PROPRIO];
+  float hist[MAXHIST];
+  float heights[LGX_MAX_HEIGHT_POINTS];
+};
+
+// ============================================================== physics helpers
+#pragma clang fp contract(fast)
+
+// symmetric 3x3 (xx yy zz xy xz yz) inverse
+LGX_DEV void sym3_inv(const float* D, float* O) {
+  float a = D[0], b = D[1], c = D[2], d = D[3], e = D[4], f = D[5];
+  float A = b * c - f * f, Bm = -(d * c - e * f), Cm = d * f - b * e;
+  float det = a * A + d * Bm + e * Cm;
+  float inv = 1.0f / det;
+  O[0] = A * inv;
+  O[1] = (a * c - e * e) * inv;
+  O[2] = (a * b - d * d) * inv;
+  O[3] = Bm * inv;
+  O[4] = Cm * inv;
+  O[5] = -(a * f - d * e) * inv;
+}
+LGX_DEV float sym3(const float* S, int i, int j) {
+  if (i == j) return S[i];
+  int k = i + j;  // (0,1)->3 (0,2)->4 (1,2)->5
+  return S[k == 1 ? 3 : (k == 2 ? 4 : 5)];
+}
+// packed symmetric 6x6 index (lower, row-major)
+LGX_DEV int pk(int i, int j) { return i >= j ? i * (i + 1) / 2 + j : j * (j + 1) / 2 + i; }
+
+// x = M⁻¹ b for one right-hand side, by the base Schur complement (one lane).
+LGX_DEV void mass_solve(const Sh& s, const float* b, float* x) {
+  float y[6];
+#pragma unroll
+  for (int r = 0; r < 6; ++r) y[r] = b[r];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    float bj = b[6 + j];
+#pragma unroll
+    for (int r = 0; r < 6; ++r) y[r] -= s.X[j][r] * bj;
+  }
+  // L Lᵀ xb = y
+  float z[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    float t = y[i];
+#pragma unroll
+    for (int k = 0; k < i; ++k) t -= s.L[pk(i, k)] * z[k];
+    z[i] = t / s.L[pk(i, i)];
+  }
+#pragma unroll
+  for (int i = 5; i >= 0; --i) {
+    float t = z[i];
+#pragma unroll
+    for (int k = i + 1; k < 6; ++k) t -= s.L[pk(k, i)] * z[k];
+    z[i] = t / s.L[pk(i, i)];
+  }
+#pragma unroll
+  for (int r = 0; r < 6; ++r) x[r] = z[r];
+#pragma unroll
+  for (int l = 0; l < 4; ++l) {
+    float rhs[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      int j = 3 * l + a;
+      float t = b[6 + j];
+#pragma unroll
+      for (int r = 0; r < 6; ++r) t -= s.Bc[j][r] * z[r];
+      rhs[a] = t;
+    }
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      float t = 0.f;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) t += sym3(s.Dinv[l], a, c) * rhs[c];
+      x[6 + 3 * l + a] = t;
+    }
+  }
+}
+
+// forward kinematics, velocities and bias accelerations (lane 0: base; lanes 0..3: legs)
+LGX_DEV void kinematics(Sh& s, const lgx_model* M, int lane) {
+  if (lane == 0) {
+    quat_to_R(s.qb, s.R[0]);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      s.P[0][i] = s.pb[i]; s.W[0][i] = s.wb[i]; s.V[0][i] = s.vo[i];
+      s.Al[0][i] = 0.f; s.Ao[0][i] = 0.f; s.Ax[0][i] = 0.f;
+    }
+    float mb = M->link_mass[0] + s.madd;
+    f3 cl = mk(M->link_com[0][0] + s.cadd[0], M->link_com[0][1] + s.cadd[1], M->link_com[0][2] + s.cadd[2]);
+    st3(s.C[0], ld3(s.pb) + mv(s.R[0], cl));
+    s.m[0] = mb;
+  }
+  __syncthreads();
+  if (lane < 4) {
+    int par = 0;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int k = 1 + 3 * lane + i;
+      const float* Rp = s.R[par];
+      f3 o = mv(Rp, ld3(M->joint_origin[k]));
+      float RpRj[9];
+      mm(Rp, M->joint_rot[k], RpRj);
+      f3 al = ld3(M->joint_axis[k]);
+      float th = s.th[k - 1], ct = cosf(th), st = sinf(th), t1 = 1.f - ct;
+      float Ra[9] = {t1 * al.x * al.x + ct, t1 * al.x * al.y - st * al.z, t1 * al.x * al.z + st * al.y,
+                     t1 * al.x * al.y + st * al.z, t1 * al.y * al.y + ct, t1 * al.y * al.z - st * al.x,
+                     t1 * al.x * al.z - st * al.y, t1 * al.y * al.z + st * al.x, t1 * al.z * al.z + ct};
+      mm(RpRj, Ra, s.R[k]);
+      f3 ax = mv(RpRj, al);
+      st3(s.Ax[k], ax);
+      f3 pp = ld3(s.P[par]) + o;
+      st3(s.P[k], pp);
+      f3 wp = ld3(s.W[par]);
+      f3 wa = ax * s.thd[k - 1];
+      st3(s.W[k], wp + wa);
+      st3(s.V[k], ld3(s.V[par]) + cross(wp, o));
+      f3 alp = ld3(s.Al[par]);
+      st3(s.Al[k], alp + cross(wp, wa));
+      st3(s.Ao[k], ld3(s.Ao[par]) + cross(alp, o) + cross(wp, cross(wp, o)));
+      st3(s.C[k], pp + mv(s.R[k], ld3(M->link_com[k])));
+      s.m[k] = M->link_mass[k];
+      par = k;
+    }
+  }
+  // world inertia per link (lanes 0..12)
+  __syncthreads();
+  if (lane < NL) {
+    const float* R = s.R[lane];
+    const float* In = M->link_inertia[lane];
+    float Il[9] = {In[0], In[3], In[4], In[3], In[1], In[5], In[4], In[5], In[2]};
+    float T[9], Rt[9] = {R[0], R[3], R[6], R[1], R[4], R[7], R[2], R[5], R[8]}, O[9];
+    mm(R, Il, T);
+    mm(T, Rt, O);
+    s.I[lane][0] = O[0]; s.I[lane][1] = O[4]; s.I[lane][2] = O[8];
+    s.I[lane][3] = O[1]; s.I[lane][4] = O[2]; s.I[lane][5] = O[5];
+  }
+  __syncthreads();
+}
+
+// composite-inertia mass-matrix blocks, bias forces and the base Schur complement
+LGX_DEV void dynamics(Sh& s, const lgx_task_params* Pm, int lane) {
+  const f3 g = ld3(Pm->gravity);
+  const f3 p0 = ld3(s.P[0]);
+  if (lane < 4) {
+    const int k0 = 1 + 3 * lane;
+    f3 F[3], N[3], c[3], a[3], pj[3];
+    float mk_[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int k = k0 + i;
+      c[i] = ld3(s.C[k]); a[i] = ld3(s.Ax[k]); pj[i] = ld3(s.P[k]); mk_[i] = s.m[k];
+      f3 r = c[i] - pj[i], w = ld3(s.W[k]), al = ld3(s.Al[k]);
+      f3 acc = ld3(s.Ao[k]) + cross(al, r) + cross(w, cross(w, r));
+      F[i] = (acc - g) * mk_[i];
+      N[i] = symv(s.I[k], al) + cross(w, symv(s.I[k], w));
+    }
+    // joint bias
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      f3 acc = mk(0, 0, 0);
+#pragma unroll
+      for (int i = j; i < 3; ++i) acc = acc + cross(c[i] - pj[j], F[i]) + N[i];
+      s.hj[3 * lane + j] = dot(a[j], acc);
+    }
+    // base partials about p0
+    float msum = 0.f;
+    f3 hs = mk(0, 0, 0), Fs = mk(0, 0, 0), Ns = mk(0, 0, 0);
+    float Ip[6] = {0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int k = k0 + i;
+      f3 r = c[i] - p0;
+      msum += mk_[i];
+      hs = hs + r * mk_[i];
+      Fs = Fs + F[i];
+      Ns = Ns + cross(r, F[i]) + N[i];
+      float rr = dot(r, r);
+      Ip[0] += s.I[k][0] + mk_[i] * (rr - r.x * r.x);
+      Ip[1] += s.I[k][1] + mk_[i] * (rr - r.y * r.y);
+      Ip[2] += s.I[k][2] + mk_[i] * (rr - r.z * r.z);
+      Ip[3] += s.I[k][3] - mk_[i] * r.x * r.y;
+      Ip[4] += s.I[k][4] - mk_[i] * r.x * r.z;
+      Ip[5] += s.I[k][5] - mk_[i] * r.y * r.z;
+    }
+    float* rd = s.red[lane];
+    rd[0] = msum; rd[1] = hs.x; rd[2] = hs.y; rd[3] = hs.z;
+#pragma unroll
+    for (int q = 0; q < 6; ++q) rd[4 + q] = Ip[q];
+    rd[10] = Fs.x; rd[11] = Fs.y; rd[12] = Fs.z; rd[13] = Ns.x; rd[14] = Ns.y; rd[15] = Ns.z;
+    // coupling columns B (6 x 3) and leg block D (3 x 3)
+    float Bl[3][6];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      f3 hl = mk(0, 0, 0), bang = mk(0, 0, 0);
+#pragma unroll
+      for (int i = j; i < 3; ++i) {
+        f3 d = c[i] - pj[j];
+        hl = hl + d * mk_[i];
+        bang = bang + cross(c[i] - p0, cross(a[j], d)) * mk_[i] + symv(s.I[k0 + i], a[j]);
+      }
+      f3 blin = cross(a[j], hl);
+      Bl[j][0] = blin.x; Bl[j][1] = blin.y; Bl[j][2] = blin.z;
+      Bl[j][3] = bang.x; Bl[j][4] = bang.y; Bl[j][5] = bang.z;
+#pragma unroll
+      for (int r = 0; r < 6; ++r) s.Bc[3 * lane + j][r] = Bl[j][r];
+    }
+    float Dl[6];
+    int idx[6][2] = {{0, 0}, {1, 1}, {2, 2}, {0, 1}, {0, 2}, {1, 2}};
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      const int j1 = idx[q][0], j2 = idx[q][1];
+      float acc = 0.f;
+#pragma unroll
+      for (int i = j2; i < 3; ++i) {
+        acc += mk_[i] * dot(cross(a[j1], c[i] - pj[j1]), cross(a[j2], c[i] - pj[j2])) +
+               dot(a[j1], symv(s.I[k0 + i], a[j2]));
+      }
+      Dl[q] = acc;
+    }
+    float Di[6];
+    sym3_inv(Dl, Di);
+#pragma unroll
+    for (int q = 0; q < 6; ++q) s.Dinv[lane][q] = Di[q];
+    float Xl[3][6];
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+      for (int r = 0; r < 6; ++r) {
+        float t = 0.f;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) t += Bl[i][r] * sym3(Di, i, j);
+        Xl[j][r] = t;
+        s.X[3 * lane + j][r] = t;
+      }
+#pragma unroll
+    for (int r = 0; r < 6; ++r)
+#pragma unroll
+      for (int q = 0; q <= r; ++q) {
+        float t = 0.f;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) t += Xl[j][r] * Bl[j][q];
+        s.S[lane][pk(r, q)] = t;
+      }
+  } else if (lane == 4) {
+    // base link partials (bias acceleration of the base COM: w x (w x r))
+    f3 c0 = ld3(s.C[0]), w = ld3(s.W[0]);
+    f3 r = c0 - p0;
+    float m0 = s.m[0];
+    f3 acc = cross(w, cross(w, r));
+    f3 F = (acc - g) * m0;
+    f3 N = cross(w, symv(s.I[0], w));
+    float* rd = s.red[4];
+    float rr = dot(r, r);
+    rd[0] = m0; rd[1] = m0 * r.x; rd[2] = m0 * r.y; rd[3] = m0 * r.z;
+    rd[4] = s.I[0][0] + m0 * (rr - r.x * r.x);
+    rd[5] = s.I[0][1] + m0 * (rr - r.y * r.y);
+    rd[6] = s.I[0][2] + m0 * (rr - r.z * r.z);
+    rd[7] = s.I[0][3] - m0 * r.x * r.y;
+    rd[8] = s.I[0][4] - m0 * r.x * r.z;
+    rd[9] = s.I[0][5] - m0 * r.y * r.z;
+    f3 Nt = cross(r, F) + N;
+    rd[10] = F.x; rd[11] = F.y; rd[12] = F.z; rd[13] = Nt.x; rd[14] = Nt.y; rd[15] = Nt.z;
+  }
+  __syncthreads();
+  if (lane == 0) {
+    float t[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) t[q] = s.red[0][q] + s.red[1][q] + s.red[2][q] + s.red[3][q] + s.red[4][q];
+    float A[21];
+    float Mt = t[0];
+    f3 H = mk(t[1], t[2], t[3]);
+    // A = [[M I, -[H]x], [[H]x, Ip]]  (generalized velocity = base origin velocity, w)
+    for (int q = 0; q < 21; ++q) A[q] = 0.f;
+    A[pk(0, 0)] = Mt; A[pk(1, 1)] = Mt; A[pk(2, 2)] = Mt;
+    // lower block rows 3..5 (w), cols 0..2 (v) = [H]x = [[0,-Hz,Hy],[Hz,0,-Hx],[-Hy,Hx,0]]
+    A[pk(3, 0)] = 0.f;   A[pk(3, 1)] = -H.z; A[pk(3, 2)] = H.y;
+    A[pk(4, 0)] = H.z;   A[pk(4, 1)] = 0.f;  A[pk(4, 2)] = -H.x;
+    A[pk(5, 0)] = -H.y;  A[pk(5, 1)] = H.x;  A[pk(5, 2)] = 0.f;
+    A[pk(3, 3)] = t[4]; A[pk(4, 4)] = t[5]; A[pk(5, 5)] = t[6];
+    A[pk(4, 3)] = t[7]; A[pk(5, 3)] = t[8]; A[pk(5, 4)] = t[9];
+#pragma unroll
+    for (int q = 0; q < 21; ++q) A[q] -= s.S[0][q] + s.S[1][q] + s.S[2][q] + s.S[3][q];
+    // Cholesky (packed)
+    for (int j = 0; j < 6; ++j) {
+      float d = A[pk(j, j)];
+      for (int k = 0; k < j; ++k) d -= s.L[pk(j, k)] * s.L[pk(j, k)];
+      float ljj = sqrtf(fmaxf(d, 1e-12f));
+      s.L[pk(j, j)] = ljj;
+      float inv = 1.0f / ljj;
+      for (int i = j + 1; i < 6; ++i) {
+        float v = A[pk(i, j)];
+        for (int k = 0; k < j; ++k) v -= s.L[pk(i, k)] * s.L[pk(j, k)];
+        s.L[pk(i, j)] = v * inv;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 6; ++q) s.hb[q] = t[10 + q];
+  }
+  __syncthreads();
+}
+
+LGX_DEV float ground_height(const lgx_task_params* Pm, const lgx_buffers& B, float x, float y) {
+  if (Pm->mesh_type == LGX_MESH_PLANE || B.height_samples == nullptr) return 0.0f;
+  float fx = (x + Pm->border_size) / Pm->horizontal_scale, fy = (y + Pm->border_size) / Pm->horizontal_scale;
+  int ix = (int)floorf(fx), iy = (int)floorf(fy);
+  ix = min(max(ix, 0), Pm->hf_rows - 2);
+  iy = min(max(iy, 0), Pm->hf_cols - 2);
+  float tx = fminf(fmaxf(fx - ix, 0.f), 1.f), ty = fminf(fmaxf(fy - iy, 0.f), 1.f);
+  const int16_t* hs = B.height_samples;
+  float h00 = hs[ix * Pm->hf_cols + iy], h10 = hs[(ix + 1) * Pm->hf_cols + iy];
+  float h01 = hs[ix * Pm->hf_cols + iy + 1], h11 = hs[(ix + 1) * Pm->hf_cols + iy + 1];
+  return Pm->vertical_scale * ((1 - tx) * (1 - ty) * h00 + tx * (1 - ty) * h10 + (1 - tx) * ty * h01 + tx * ty * h11);
+}
+
+// one physics substep (legged_robot.py:80-85 loop body)
+LGX_DEV void substep(Sh& s, const lgx_model* M, const lgx_task_params* Pm, const lgx_buffers& B, int lane,
+                     bool last) {
+  const float dt = Pm->sim_dt;
+  // ---- PD torques: LeggedRobot._compute_torques legged_robot.py:440-478
+  {
+#pragma clang fp contract(off)
+    if (lane < NJ) {
+      const int j = lane;
+      float as = s.act[j] * Pm->action_scale;
+      float t;
+      if (Pm->control_type == LGX_CONTROL_P) {
+        float err = (as + Pm->default_dof_pos[j]) - s.th[j];
+        if (Pm->randomize_kp_kd)
+          t = (s.kpm[j] * Pm->p_gains[j]) * err - (s.kdm[j] * Pm->d_gains[j]) * s.thd[j];
+        else
+          t = Pm->p_gains[j] * err - Pm->d_gains[j] * s.thd[j];
+      } else if (Pm->control_type == LGX_CONTROL_V) {
+        t = Pm->p_gains[j] * (as - s.thd[j]) - Pm->d_gains[j] * ((s.thd[j] - s.ldv[j]) / Pm->sim_dt);
+      } else {
+        t = as;
+      }
+      s.tau[j] = fminf(fmaxf(t, -Pm->torque_limits[j]), Pm->torque_limits[j]);
+    }
+  }
+  kinematics(s, M, lane);
+  dynamics(s, Pm, lane);
+  // ---- free velocity u* = u + dt M⁻¹ (Sᵀτ - h)
+  if (lane == 0) {
+    float b[NU], x[NU];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) b[i] = -s.hb[i];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) b[6 + j] = s.tau[j] - s.hj[j];
+    mass_solve(s, b, x);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) { s.us[i] = s.vo[i] + dt * x[i]; s.us[3 + i] = s.wb[i] + dt * x[3 + i]; }
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) s.us[6 + j] = s.thd[j] + dt * x[6 + j];
+  }
+  // ---- constraint detection: joint limits (lanes 0..11), contacts (one candidate per lane)
+  bool lim_lo = false, lim_hi = false;
+  if (lane < NJ && M->joint_has_limits[lane + 1]) {
+    lim_lo = s.th[lane] < M->joint_lower[lane + 1] + Pm->limit_margin;
+    lim_hi = !lim_lo && s.th[lane] > M->joint_upper[lane + 1] - Pm->limit_margin;
+  }
+  uint64_t lmask = __ballot(lim_lo || lim_hi);
+  int nlim = __popcll(lmask);
+  bool act = false;
+  f3 xc = mk(0, 0, 0);
+  float depth = 0.f;
+  int ck = 0;
+  if (lane < M->num_candidates) {
+    ck = M->cand_link[lane];
+    xc = ld3(s.P[ck]) + mv(s.R[ck], ld3(M->cand_pos[lane]));
+    float r = M->cand_radius[lane];
+    float hg = ground_height(Pm, B, xc.x, xc.y);
+    depth = r + hg - xc.z;
+    act = depth > -Pm->contact_margin;
+    xc.z -= r;
+  }
+  uint64_t cmask = __ballot(act);
+  uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  int crank = __popcll(cmask & below);
+  int ncon = min(__popcll(cmask), MAXC);
+  const int nrows = nlim + 3 * ncon;
+  auto target = [&](float d) {
+    float tv;
+    if (d > Pm->slop) tv = fminf(Pm->baumgarte * (d - Pm->slop) / dt, Pm->max_depenetration_vel);
+    else if (d >= 0.f) tv = 0.f;
+    else tv = d / dt;
+    return tv;
+  };
+  if (lim_lo || lim_hi) {
+    int r = __popcll(lmask & below);
+#pragma unroll
+    for (int q = 0; q < NU; ++q) s.J[r][q] = 0.f;
+    s.J[r][6 + lane] = lim_lo ? 1.f : -1.f;
+    float d = lim_lo ? (M->joint_lower[lane + 1] - s.th[lane]) : (s.th[lane] - M->joint_upper[lane + 1]);
+    s.tgt[r] = target(d);
+    s.rkind[r] = 0;
+  }
+  if (act && crank < MAXC) {
+    const int r0 = nlim + 3 * crank;
+    const f3 p0 = ld3(s.P[0]);
+    const f3 dirs[3] = {mk(0, 0, 1), mk(1, 0, 0), mk(0, 1, 0)};
+    const int leg = ck > 0 ? (ck - 1) / 3 : -1;
+    const int pos = ck > 0 ? (ck - 1) % 3 : -1;
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+      const int r = r0 + t;
+      const f3 d = dirs[t];
+      f3 ang = cross(xc - p0, d);
+      s.J[r][0] = d.x; s.J[r][1] = d.y; s.J[r][2] = d.z;
+      s.J[r][3] = ang.x; s.J[r][4] = ang.y; s.J[r][5] = ang.z;
+#pragma unroll
+      for (int q = 0; q < NJ; ++q) s.J[r][6 + q] = 0.f;
+      for (int i = 0; i <= pos; ++i) {
+        const int ki = 1 + 3 * leg + i;
+        s.J[r][6 + 3 * leg + i] = dot(ld3(s.Ax[ki]), cross(xc - ld3(s.P[ki]), d));
+      }
+      s.rkind[r] = t;
+      s.tgt[r] = t == 0 ? target(depth) : 0.f;
+    }
+    s.cbody[crank] = M->cand_body[lane];
+  }
+  if (lane == 0) { s.nrows = nrows; s.nlim = nlim; s.ncon = ncon; }
+  __syncthreads();
+  // ---- per-row M⁻¹Jᵀ column and diagonal of A = J M⁻¹ Jᵀ (one lane per row)
+  if (lane < nrows) {
+    float x[NU];
+    mass_solve(s, s.J[lane], x);
+    float a = 0.f;
+#pragma unroll
+    for (int q = 0; q < NU; ++q) { s.MJ[lane][q] = x[q]; a += s.J[lane][q] * x[q]; }
+    s.Arr[lane] = a;
+    s.lam[lane] = 0.f;
+  }
+  __syncthreads();
+  // ---- projected Gauss-Seidel, generalized velocity spread over lanes 0..17
+  float uc = lane < NU ? s.us[lane] : 0.f;
+  const float mu = s.mu;
+  for (int it = 0; it < Pm->solver_iterations; ++it) {
+    for (int r = 0; r < nrows; ++r) {
+      const int kind = s.rkind[r];
+      if (kind == 0) {
+        float w = row_sums_32(lane < NU ? s.J[r][lane] * uc : 0.f);
+        float lo = s.lam[r];
+        float ln = fmaxf(0.f, lo + (s.tgt[r] - w) / s.Arr[r]);
+        float d = ln - lo;
+        if (lane < NU) uc += s.MJ[r][lane] * d;
+        if (lane == 0) s.lam[r] = ln;
+      } else {
+        float w1 = row_sums_32(lane < NU ? s.J[r][lane] * uc : 0.f);
+        float w2 = row_sums_32(lane < NU ? s.J[r + 1][lane] * uc : 0.f);
+        float o1 = s.lam[r], o2 = s.lam[r + 1];
+        float l1 = o1 - w1 / s.Arr[r];
+        float l2 = o2 - w2 / s.Arr[r + 1];
+        float lim = mu * s.lam[r - 1];
+        float n = sqrtf(l1 * l1 + l2 * l2);
+        if (n > lim) {
+          float sc = n > 0.f ? lim / n : 0.f;
+          l1 *= sc; l2 *= sc;
+        }
+        if (lane < NU) uc += s.MJ[r][lane] * (l1 - o1) + s.MJ[r + 1][lane] * (l2 - o2);
+        if (lane == 0) { s.lam[r] = l1; s.lam[r + 1] = l2; }
+        ++r;
+      }
+    }
+  }
+  if (lane < NU) s.up[lane] = uc;
+  __syncthreads();
+  // ---- contact forces of the last substep, per reported body (world frame)
+  if (last && lane < LGX_MAX_BODIES) {
+    float f[3] = {0.f, 0.f, 0.f};
+    for (int c = 0; c < ncon; ++c) {
+      if (s.cbody[c] != lane) continue;
+      const int r = nlim + 3 * c;
+      f[2] += s.lam[r]; f[0] += s.lam[r + 1]; f[1] += s.lam[r + 2];
+    }
+    s.cf[lane][0] = f[0] / dt; s.cf[lane][1] = f[1] / dt; s.cf[lane][2] = f[2] / dt;
+  }
+  // ---- semi-implicit Euler
+  if (lane == 0) {
+    f3 v = mk(s.up[0], s.up[1], s.up[2]), w = mk(s.up[3], s.up[4], s.up[5]);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) s.pb[i] += dt * s.up[i];
+    float wn = sqrtf(dot(w, w));
+    float ang = wn * dt;
+    float dq[4];
+    if (ang > 1e-12f) {
+      float sc = sinf(0.5f * ang) / wn;
+      dq[0] = w.x * sc; dq[1] = w.y * sc; dq[2] = w.z * sc; dq[3] = cosf(0.5f * ang);
+    } else {
+      dq[0] = 0.5f * dt * w.x; dq[1] = 0.5f * dt * w.y; dq[2] = 0.5f * dt * w.z; dq[3] = 1.f;
+    }
+    const float* q = s.qb;
+    float qn[4];
+    qn[3] = dq[3] * q[3] - (dq[0] * q[0] + dq[1] * q[1] + dq[2] * q[2]);
+    qn[0] = dq[3] * q[0] + q[3] * dq[0] + (dq[1] * q[2] - dq[2] * q[1]);
+    qn[1] = dq[3] * q[1] + q[3] * dq[1] + (dq[2] * q[0] - dq[0] * q[2]);
+    qn[2] = dq[3] * q[2] + q[3] * dq[2] + (dq[0] * q[1] - dq[1] * q[0]);
+    float nq = rsqrtf(qn[0] * qn[0] + qn[1] * qn[1] + qn[2] * qn[2] + qn[3] * qn[3]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) s.qb[i] = qn[i] * nq;
+    st3(s.vo, v);
+    st3(s.wb, w);
+  }
+  if (lane < NJ) {
+    s.thd[lane] = s.up[6 + lane];
+    s.th[lane] += dt * s.thd[lane];
+  }
+  __syncthreads();
+}
+
+#pragma clang fp contract(off)
+
+// ============================================================== post-physics helpers
+// (fp32, no contraction: the reference evaluates these as separate eager torch ops)
+
+LGX_DEV void quat_rotate_inverse(const float* q, const float* v, float* out) {
+  float w = q[3];
+  float sc = 2.0f * (w * w) - 1.0f;
+  float cx = q[1] * v[2] - q[2] * v[1];
+  float cy = q[2] * v[0] - q[0] * v[2];
+  float cz = q[0] * v[1] - q[1] * v[0];
+  float d = q[0] * v[0] + q[1] * v[1] + q[2] * v[2];
+  out[0] = v[0] * sc - cx * w * 2.0f + q[0] * d * 2.0f;
+  out[1] = v[1] * sc - cy * w * 2.0f + q[1] * d * 2.0f;
+  out[2] = v[2] * sc - cz * w * 2.0f + q[2] * d * 2.0f;
+}
+LGX_DEV void quat_apply(const float* q, const float* b, float* out) {
+  float t0 = (q[1] * b[2] - q[2] * b[1]) * 2.0f;
+  float t1 = (q[2] * b[0] - q[0] * b[2]) * 2.0f;
+  float t2 = (q[0] * b[1] - q[1] * b[0]) * 2.0f;
+  out[0] = b[0] + q[3] * t0 + (q[1] * t2 - q[2] * t1);
+  out[1] = b[1] + q[3] * t1 + (q[2] * t0 - q[0] * t2);
+  out[2] = b[2] + q[3] * t2 + (q[0] * t1 - q[1] * t0);
+}
+LGX_DEV float trem(float a, float b) {
+  float m = fmodf(a, b);
+  if (m != 0.0f && ((m < 0.0f) != (b < 0.0f))) m += b;
+  return m;
+}
+LGX_DEV float wrap_to_pi(float a) {
+  const float two_pi = 6.283185307179586f, pi = 3.141592653589793f;
+  float m = trem(a, two_pi);
+  m -= two_pi * (float)(m > pi);
+  return m;
+}
+LGX_DEV float clipf(float x, float lo, float hi) { return x < lo ? lo : (x > hi ? hi : x); }
+LGX_DEV float sq(float x) { return x * x; }
+LGX_DEV float nrm3(float a, float b, float c) { return sqrtf(a * a + b * b + c * c); }
+LGX_DEV float nrm2(float a, float b) { return sqrtf(a * a + b * b); }
+LGX_DEV float rand_range(float lo, float hi, float u) {
+  float span = (float)((double)hi - (double)lo);
+  return span * u + lo;
+}
+
+struct Scratch {
+  float blv[3], bav[3], pg[3];
+  float roll, pitch, yaw;
+  float ph[4];  // fl fr bl br
+  int contact[4];
+  float feet_z[4];
+  float jump;
+};
+
+// Go2Robot._resample_commands go2.py:413-464 / LeggedRobot legged_robot.py:406-437
+LGX_DEV void resample_commands(const lgx_task_params* Pm, float* cmd, const float* U, int slot0, const float* quat) {
+  if (Pm->has_user_command) {
+    for (int i = 0; i < 4; ++i) cmd[i] = Pm->user_command[i];
+    return;
+  }
+  cmd[0] = rand_range(Pm->cmd_lin_vel_x[0], Pm->cmd_lin_vel_x[1], U[slot0 + 0]);
+  cmd[1] = rand_range(Pm->cmd_lin_vel_y[0], Pm->cmd_lin_vel_y[1], U[slot0 + 1]);
+  if (Pm->heading_command)
+    cmd[3] = rand_range(Pm->cmd_heading[0], Pm->cmd_heading[1], U[slot0 + 2]);
+  else
+    cmd[2] = rand_range(Pm->cmd_ang_vel_yaw[0], Pm->cmd_ang_vel_yaw[1], U[slot0 + 2]);
+  float keep = (float)(nrm2(cmd[0], cmd[1]) > 0.2f);
+  cmd[0] = cmd[0] * keep;
+  cmd[1] = cmd[1] * keep;
+  if (Pm->zero_command && U[slot0 + 3] < Pm->zero_command_prob) {
+    if (Pm->task_kind == LGX_TASK_GO2) {
+      cmd[0] = cmd[0] * 0.0f; cmd[1] = cmd[1] * 0.0f; cmd[2] = cmd[2] * 0.0f;
+      if (Pm->heading_command) {
+        const float fwd[3] = {1.f, 0.f, 0.f};
+        float f[3];
+        quat_apply(quat, fwd, f);
+        cmd[3] = atan2f(f[1], f[0]);
+      }
+    } else {
+      for (int i = 0; i < 4; ++i) cmd[i] = cmd[i] * 0.0f;
+    }
+  }
+}
+
+// reset_idx for one env (go2.py:207-263 / legged_robot.py:157-213), lane-parallel writes.
+// root/dof/commands are in LDS (s) or in `root`, `dof`, `cmd` register copies by the caller.
+LGX_DEV void reset_env(const lgx_task_params* Pm, const lgx_buffers& B, int e, int lane, const float* U,
+                       float* root, float* th, float* thd, float* cmd, int64_t& ep, bool after_init,
+                       bool zero_carried) {
+  const int D = Pm->num_dof;
+  // terrain curriculum legged_robot.py:543-574
+  if (Pm->curriculum && after_init && B.terrain_levels) {
+    float dx = root[0] - B.env_origins[e * 3 + 0], dy = root[1] - B.env_origins[e * 3 + 1];
+    float dist = nrm2(dx, dy);
+    int up = dist > Pm->terrain_length * Pm->promote_threshold;
+    float expct = nrm2(cmd[0], cmd[1]) * Pm->max_episode_length_s;
+    int down = dist < expct * Pm->demote_threshold;
+    int64_t lvl = B.terrain_levels[e] + up - down;
+    if (lvl >= Pm->max_terrain_level) {
+      lvl = (int64_t)(U[S_TERR] * (float)Pm->max_terrain_level);
+      if (lvl >= Pm->max_terrain_level) lvl = Pm->max_terrain_level - 1;
+    } else if (lvl < 0) {
+      lvl = 0;
+    }
+    __syncthreads();
+    if (lane == 0) {
+      B.terrain_levels[e] = lvl;
+      const float* o = B.terrain_origins + ((size_t)lvl * Pm->num_terrain_cols + B.terrain_types[e]) * 3;
+      for (int i = 0; i < 3; ++i) B.env_origins[e * 3 + i] = o[i];
+    }
+    __syncthreads();
+  }
+  for (int j = 0; j < D; ++j) {
+    th[j] = Pm->default_dof_pos[j] + rand_range(0.0f, 0.9f, U[S_DOF + j]);
+    thd[j] = 0.0f;
+  }
+  for (int i = 0; i < 13; ++i) root[i] = Pm->base_init_state[i];
+  for (int i = 0; i < 3; ++i) root[i] = root[i] + B.env_origins[e * 3 + i];
+  if (Pm->custom_origins) {
+    root[0] = root[0] + rand_range(-1.0f, 1.0f, U[S_ROOT_XY + 0]);
+    root[1] = root[1] + rand_range(-1.0f, 1.0f, U[S_ROOT_XY + 1]);
+  }
+  for (int i = 0; i < 6; ++i) root[7 + i] = rand_range(-0.5f, 0.5f, U[S_ROOT_VEL + i]);
+  resample_commands(Pm, cmd, U, S_RCMD, root + 3);
+  ep = 0;
+  // buffer zeroing (lane-parallel). Inside a step the last_* buffers and the history
+  // are rewritten at the end of post_physics_step anyway (go2.py:380-384, :570-574),
+  // so only an external reset has to zero them.
+  if (zero_carried) {
+    const int A = Pm->num_actions, H = Pm->history_len * Pm->num_proprio;
+    if (lane < A) B.last_actions[(size_t)e * A + lane] = 0.f;
+    if (lane < D) { B.last_dof_vel[(size_t)e * D + lane] = 0.f; B.last_torques[(size_t)e * D + lane] = 0.f; }
+    if (lane < 6) B.last_root_vel[e * 6 + lane] = 0.f;
+    if (lane < 3) B.last_base_lin_vel[e * 3 + lane] = 0.f;
+    for (int i = lane; i < H; i += 64) B.obs_history[(size_t)e * H + i] = 0.f;
+  }
+  if (Pm->task_kind == LGX_TASK_GO2 && lane < Pm->num_feet) {
+    if (B.feet_air_time) B.feet_air_time[e * Pm->num_feet + lane] = 0.f;
+    B.last_contacts[e * Pm->num_feet + lane] = 0;
+    B.last_contact_heights[e * Pm->num_feet + lane] = 0.f;
+  }
+  const int K = Pm->num_reward_terms + (Pm->has_termination_reward ? 1 : 0);
+  if (lane < K) {
+    float* es = B.episode_sums + (size_t)e * K + lane;
+    if (B.episode_stats) atomicAdd(B.episode_stats + lane, *es);
+    *es = 0.f;
+  }
+  if (lane == 0 && B.episode_stats) atomicAdd(B.episode_stats + K, 1.0f);
+}
+
+LGX_DEV void fill_uniforms(Sh& s, uint64_t seed, uint32_t gid, uint64_t step, uint32_t stream, int lane) {
+  if (lane < NBLK) {
+    uint32_t o[4];
+    philox4x32_10(gid, (uint32_t)step, (uint32_t)lane | (stream << 16), (uint32_t)(step >> 32), (uint32_t)seed,
+                  (uint32_t)(seed >> 32), o);
+    s.U[4 * lane + 0] = u01(o[0]); s.U[4 * lane + 1] = u01(o[1]);
+    s.U[4 * lane + 2] = u01(o[2]); s.U[4 * lane + 3] = u01(o[3]);
+  }
+  __syncthreads();
+}
+
+// reward term (uniform across lanes); mirrors oracle/lgx_oracle.c reward_term
+LGX_DEV float reward_term(const lgx_task_params* Pm, const lgx_buffers& B, const Sh& s, const Scratch& x, int e,
+                          int id, const float* root, float* cmd, const float* lact, const float* ldv,
+                          const float* ltq, const float* lch, float* fat, const uint8_t* lc) {
+  const int D = Pm->num_dof, A = Pm->num_actions;
+  float r = 0.0f;
+  switch (id) {
+    case LGX_REW_ACTION_RATE:
+      for (int j = 0; j < A; ++j) r += sq(lact[j] - s.act[j]);
+      return r;
+    case LGX_REW_ANG_VEL_XY: return sq(x.bav[0]) + sq(x.bav[1]);
+    case LGX_REW_BASE_HEIGHT: {
+      float acc = 0.0f;
+      for (int i = 0; i < Pm->num_height_points; ++i) acc += root[2] - s.heights[i];
+      return sq(acc / (float)Pm->num_height_points - Pm->base_height_target);
+    }
+    case LGX_REW_CALF_COLLISION:
+      for (int i = 0; i < 4; ++i) { const float* c = s.cf[Pm->calf_idx[i]]; r += (float)(nrm3(c[0], c[1], c[2]) > 0.1f); }
+      return r;
+    case LGX_REW_CALF_POS:
+      for (int i = 0; i < 4; ++i) { int j = Pm->calf_joint_idx[i]; r += sq(s.th[j] - Pm->default_dof_pos[j]); }
+      return r;
+    case LGX_REW_CALF_SYMMETRY: {
+      const int* c = Pm->calf_joint_idx;
+      return fabsf(s.th[c[0]] - s.th[c[1]]) + fabsf(s.th[c[2]] - s.th[c[3]]);
+    }
+    case LGX_REW_COLLISION:
+      for (int i = 0; i < Pm->n_penalised; ++i) {
+        const float* c = s.cf[Pm->penalised_idx[i]];
+        r += (float)(nrm3(c[0], c[1], c[2]) > 0.1f);
+      }
+      return r;
+    case LGX_REW_DELTA_TORQUES:
+      for (int j = 0; j < D; ++j) r += sq(s.tau[j] - ltq[j]);
+      return r;
+    case LGX_REW_DOF_ACC:
+      for (int j = 0; j < D; ++j) r += sq((ldv[j] - s.thd[j]) / Pm->dt);
+      return r;
+    case LGX_REW_DOF_ERROR:
+      for (int j = 0; j < D; ++j) r += sq(s.th[j] - Pm->default_dof_pos[j]);
+      return r;
+    case LGX_REW_DOF_POS_LIMITS:
+      for (int j = 0; j < D; ++j) {
+        float lo = s.th[j] - Pm->dof_pos_limits[j][0], hi = s.th[j] - Pm->dof_pos_limits[j][1];
+        float o = -(lo < 0.0f ? lo : 0.0f);
+        o += (hi > 0.0f ? hi : 0.0f);
+        r += o;
+      }
+      return r;
+    case LGX_REW_DOF_VEL:
+      for (int j = 0; j < D; ++j) r += sq(s.thd[j]);
+      return r;
+    case LGX_REW_DOF_VEL_LIMITS:
+      for (int j = 0; j < D; ++j) r += clipf(fabsf(s.thd[j]) - Pm->dof_vel_limits[j] * Pm->soft_dof_vel_limit, 0.0f, 1.0f);
+      return r;
+    case LGX_REW_FEET_AIR_TIME: {
+      float rew = 0.0f;
+      for (int f = 0; f < Pm->num_feet; ++f) {
+        int cfl = (s.cf[Pm->feet_idx[f]][2] > 1.0f) || lc[f];
+        float first = (float)((fat[f] > 0.0f) && cfl);
+        fat[f] = fat[f] + Pm->dt;
+        rew += (fat[f] - 0.5f) * first;
+      }
+      rew = rew * (float)(nrm2(cmd[0], cmd[1]) > 0.1f);
+      for (int f = 0; f < Pm->num_feet; ++f) {
+        int cfl = (s.cf[Pm->feet_idx[f]][2] > 1.0f) || lc[f];
+        fat[f] = fat[f] * (float)(!cfl);
+      }
+      return rew;
+    }
+    case LGX_REW_FEET_CONTACT_FORCES:
+      for (int f = 0; f < Pm->num_feet; ++f) {
+        const float* c = s.cf[Pm->feet_idx[f]];
+        float v = nrm3(c[0], c[1], c[2]) - Pm->max_contact_force;
+        r += v > 0.0f ? v : 0.0f;
+      }
+      return r;
+    case LGX_REW_HEADING_ALIGNMENT: {
+      const float fwd[3] = {1.f, 0.f, 0.f};
+      float f[3];
+      quat_apply(root + 3, fwd, f);
+      float heading = atan2f(f[1], f[0]);
+      float desired = 0.0f;
+      if (Pm->heading_command) {
+        cmd[3] = wrap_to_pi(cmd[3]);  // wrap_to_pi mutates commands[:, 3] (Q7)
+        desired = cmd[3];
+      }
+      float err = wrap_to_pi(desired - heading);
+      return sq(err) * (float)(nrm3(cmd[0], cmd[1], cmd[2]) >= 0.2f);
+    }
+    case LGX_REW_HIP_POS:
+      for (int i = 0; i < 4; ++i) { int j = Pm->hip_joint_idx[i]; r += sq(s.th[j] - Pm->default_dof_pos[j]); }
+      return r;
+    case LGX_REW_JUMP_ZONE_FORWARD_VEL: {
+      float fr = root[7] > 0.0f ? root[7] : 0.0f;
+      return fr * (float)(x.jump > 0.0f) * (float)(nrm3(cmd[0], cmd[1], cmd[2]) >= 0.2f);
+    }
+    case LGX_REW_JUMP_ZONE_UPWARD_VEL: {
+      float up = root[9] > 0.0f ? root[9] : 0.0f;
+      return up * (float)(x.jump > 0.0f) * (float)(nrm3(cmd[0], cmd[1], cmd[2]) >= 0.2f);
+    }
+    case LGX_REW_LIN_VEL_Z: return sq(x.blv[2]);
+    case LGX_REW_MIN_HEIGHT: {
+      float ze = clipf(Pm->base_height_target - root[2], 0.0f, Pm->base_height_target);
+      return ze * (float)(x.jump > 0.0f);
+    }
+    case LGX_REW_ORIENTATION: return sq(x.pg[0]) + sq(x.pg[1]);
+    case LGX_REW_PHASE_CONTACT_MATCH: {
+      float thr = 2.0f * Pm->percent_time_on_ground - 1.0f;
+      float rew = 0.0f;
+      for (int f = 0; f < 4; ++f) {
+        int stance = sinf(6.283185307179586f * x.ph[f]) <= thr;
+        rew += (x.contact[f] == stance) ? 0.25f : -0.25f;
+      }
+      return rew;
+    }
+    case LGX_REW_PHASE_FOOT_LIFTING: {
+      float thr = 2.0f * Pm->percent_time_on_ground - 1.0f;
+      float rew = 0.0f;
+      for (int f = 0; f < 4; ++f) {
+        int stance = sinf(6.283185307179586f * x.ph[f]) <= thr;
+        float h = clipf(x.feet_z[f] - lch[f], 0.0f, Pm->max_foot_height);
+        float nh = h / Pm->max_foot_height;
+        rew += stance ? -nh : nh;
+      }
+      return rew / 2.0f;
+    }
+    case LGX_REW_REVERSE_PENALTY: return -(root[7] < 0.0f ? root[7] : 0.0f);
+    case LGX_REW_STAND_STILL:
+      for (int j = 0; j < D; ++j) r += fabsf(s.th[j] - Pm->default_dof_pos[j]);
+      return r * (float)(nrm2(cmd[0], cmd[1]) < 0.1f);
+    case LGX_REW_STUMBLE_CALVES: {
+      int any = 0;
+      for (int i = 0; i < 4; ++i) { const float* c = s.cf[Pm->calf_idx[i]]; any |= nrm2(c[0], c[1]) > 5.0f * fabsf(c[2]); }
+      return (float)any;
+    }
+    case LGX_REW_STUMBLE_FEET: {
+      int any = 0;
+      for (int f = 0; f < Pm->num_feet; ++f) { const float* c = s.cf[Pm->feet_idx[f]]; any |= nrm2(c[0], c[1]) > 5.0f * fabsf(c[2]); }
+      return (float)any;
+    }
+    case LGX_REW_THIGH_POS:
+      for (int i = 0; i < 4; ++i) { int j = Pm->thigh_joint_idx[i]; r += sq(s.th[j] - Pm->default_dof_pos[j]); }
+      return r;
+    case LGX_REW_THIGH_SYMMETRY: {
+      const int* c = Pm->thigh_joint_idx;
+      return fabsf(s.th[c[0]] - s.th[c[1]]) + fabsf(s.th[c[2]] - s.th[c[3]]);
+    }
+    case LGX_REW_TORQUE_LIMITS:
+      for (int j = 0; j < D; ++j) {
+        float v = fabsf(s.tau[j]) - Pm->torque_limits[j] * Pm->soft_torque_limit;
+        r += v > 0.0f ? v : 0.0f;
+      }
+      return r;
+    case LGX_REW_TORQUES:
+      for (int j = 0; j < D; ++j) r += sq(s.tau[j]);
+      return r;
+    case LGX_REW_TRACKING_ANG_VEL: return expf(-sq(cmd[2] - x.bav[2]) / Pm->tracking_sigma);
+    case LGX_REW_TRACKING_LIN_VEL: return expf(-(sq(cmd[0] - x.blv[0]) + sq(cmd[1] - x.blv[1])) / Pm->tracking_sigma);
+    case LGX_REW_TRACKING_PITCH: {
+      float deg = x.pitch * 57.29577951308232f;
+      return expf(-sq(deg - Pm->pitch_deg_target) / Pm->tracking_sigma);
+    }
+    case LGX_REW_TRACKING_ROLL: {
+      float deg = x.roll * 57.29577951308232f;
+      return expf(-sq(deg - Pm->roll_deg_target) / Pm->tracking_sigma);
+    }
+    case LGX_REW_ZERO_CMD_DOF_ERROR: {
+      float zm = (float)(nrm3(cmd[0], cmd[1], cmd[2]) < 0.2f);
+      for (int j = 0; j < D; ++j) r += sq(s.th[j] - Pm->default_dof_pos[j]);
+      return r * zm;
+    }
+    default: return 0.0f;
+  }
+}
+
+LGX_DEV void get_heights(const lgx_task_params* Pm, const lgx_buffers& B, Sh& s, const float* root, int lane) {
+  const int NP = Pm->num_height_points;
+  if (Pm->mesh_type == LGX_MESH_PLANE || B.height_samples == nullptr) {
+    for (int i = lane; i < NP; i += 64) s.heights[i] = 0.0f;
+    return;
+  }
+  float qz = root[5], qw = root[6];
+  float n = sqrtf(qz * qz + qw * qw);
+  n = n < 1e-9f ? 1e-9f : n;
+  float qy[4] = {0.f, 0.f, qz / n, qw / n};
+  for (int i = lane; i < NP; i += 64) {
+    float p[3] = {Pm->height_points[i][0], Pm->height_points[i][1], 0.f}, w[3];
+    quat_apply(qy, p, w);
+    float px = (w[0] + root[0]) + Pm->border_size, py = (w[1] + root[1]) + Pm->border_size;
+    long ix = (long)(px / Pm->horizontal_scale), iy = (long)(py / Pm->horizontal_scale);
+    ix = ix < 0 ? 0 : (ix > Pm->hf_rows - 2 ? Pm->hf_rows - 2 : ix);
+    iy = iy < 0 ? 0 : (iy > Pm->hf_cols - 2 ? Pm->hf_cols - 2 : iy);
+    int16_t h1 = B.height_samples[ix * Pm->hf_cols + iy];
+    int16_t h2 = B.height_samples[(ix + 1) * Pm->hf_cols + iy];
+    int16_t h3 = B.height_samples[ix * Pm->hf_cols + iy + 1];
+    int16_t h = h1 < h2 ? h1 : h2;
+    h = h < h3 ? h : h3;
+    s.heights[i] = (float)h * Pm->vertical_scale;
+  }
+}
+
+// ============================================================== kernels
+template <bool PHYSICS>
+__global__ __launch_bounds__(64) void env_step_kernel(const lgx_model* __restrict__ M,
+                                                      const lgx_task_params* __restrict__ Pm, lgx_buffers B,
+                                                      uint64_t seed, uint64_t step) {
+  __shared__ Sh s;
+  const int e = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int D = Pm->num_dof, A = Pm->num_actions, NB = Pm->num_bodies;
+  const uint32_t gid = (uint32_t)(Pm->env_id_offset + e);
+
+  // ---------------------------------------------------------------- load + clip
+  float* root_g = B.root_states + (size_t)e * 13;
+  if (lane < A) {
+    float a = B.actions_in[(size_t)e * A + lane];
+    a = clipf(a, -Pm->clip_actions, Pm->clip_actions);  // legged_robot.py:74-75
+    s.act[lane] = a;
+    B.actions[(size_t)e * A + lane] = a;
+  }
+  if (lane < D) {
+    s.th[lane] = B.dof_state[((size_t)e * D + lane) * 2];
+    s.thd[lane] = B.dof_state[((size_t)e * D + lane) * 2 + 1];
+    s.kpm[lane] = B.kp_kd ? B.kp_kd[(size_t)e * D + lane] : 1.f;
+    s.kdm[lane] = B.kp_kd ? B.kp_kd[((size_t)Pm->num_envs + e) * D + lane] : 1.f;
+    s.ldv[lane] = B.last_dof_vel[(size_t)e * D + lane];
+  }
+  if (lane < 13) s.hist[lane] = root_g[lane];  // staging
+  if (lane == 0) {
+    s.madd = B.mass_params ? B.mass_params[e * 4] : 0.f;
+    s.mu = 0.5f * ((B.friction ? B.friction[e] : 1.f) + Pm->ground_friction);
+  }
+  if (lane < 3) s.cadd[lane] = B.mass_params ? B.mass_params[e * 4 + 1 + lane] : 0.f;
+  __syncthreads();
+
+  if (PHYSICS) {
+    if (lane == 0) {
+      float q[4] = {s.hist[3], s.hist[4], s.hist[5], s.hist[6]};
+      float n = rsqrtf(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+      for (int i = 0; i < 4; ++i) s.qb[i] = q[i] * n;
+      for (int i = 0; i < 3; ++i) { s.pb[i] = s.hist[i]; s.wb[i] = s.hist[10 + i]; }
+      float R[9];
+      quat_to_R(s.qb, R);
+      f3 rc = mv(R, mk(M->link_com[0][0] + s.cadd[0], M->link_com[0][1] + s.cadd[1], M->link_com[0][2] + s.cadd[2]));
+      f3 vo = ld3(s.hist + 7) - cross(ld3(s.wb), rc);  // COM velocity -> origin velocity
+      st3(s.vo, vo);
+    }
+    __syncthreads();
+    for (int sub = 0; sub < Pm->decimation; ++sub) substep(s, M, Pm, B, lane, sub == Pm->decimation - 1);
+    // final kinematics for the rigid-body state tensor
+    kinematics(s, M, lane);
+    float root[13];
+    {
+      float R[9];
+      quat_to_R(s.qb, R);
+      f3 rc = mv(R, mk(M->link_com[0][0] + s.cadd[0], M->link_com[0][1] + s.cadd[1], M->link_com[0][2] + s.cadd[2]));
+      f3 vc = ld3(s.vo) + cross(ld3(s.wb), rc);
+      root[0] = s.pb[0]; root[1] = s.pb[1]; root[2] = s.pb[2];
+      root[3] = s.qb[0]; root[4] = s.qb[1]; root[5] = s.qb[2]; root[6] = s.qb[3];
+      root[7] = vc.x; root[8] = vc.y; root[9] = vc.z;
+      root[10] = s.wb[0]; root[11] = s.wb[1]; root[12] = s.wb[2];
+    }
+    __syncthreads();
+    if (lane < 13) s.hist[lane] = root[lane];
+    // rigid body states, contact forces, torques -> HBM
+    if (lane < NB) {
+      const int k = M->body_link[lane];
+      f3 off = ld3(M->body_offset[lane]);
+      f3 o = mv(s.R[k], off);
+      f3 pos = ld3(s.P[k]) + o;
+      bool primary = off.x == 0.f && off.y == 0.f && off.z == 0.f;
+      f3 lv = ld3(s.V[k]) + cross(ld3(s.W[k]), primary ? (ld3(s.C[k]) - ld3(s.P[k])) : o);
+      float Rb[9];
+      mm(s.R[k], M->body_rot[lane], Rb);
+      float tr = Rb[0] + Rb[4] + Rb[8], qq[4];
+      if (tr > 0.f) {
+        float sc = sqrtf(tr + 1.f) * 2.f;
+        qq[3] = 0.25f * sc; qq[0] = (Rb[7] - Rb[5]) / sc; qq[1] = (Rb[2] - Rb[6]) / sc; qq[2] = (Rb[3] - Rb[1]) / sc;
+      } else if (Rb[0] > Rb[4] && Rb[0] > Rb[8]) {
+        float sc = sqrtf(1.f + Rb[0] - Rb[4] - Rb[8]) * 2.f;
+        qq[3] = (Rb[7] - Rb[5]) / sc; qq[0] = 0.25f * sc; qq[1] = (Rb[1] + Rb[3]) / sc; qq[2] = (Rb[2] + Rb[6]) / sc;
+      } else if (Rb[4] > Rb[8]) {
+        float sc = sqrtf(1.f + Rb[4] - Rb[0] - Rb[8]) * 2.f;
+        qq[3] = (Rb[2] - Rb[6]) / sc; qq[0] = (Rb[1] + Rb[3]) / sc; qq[1] = 0.25f * sc; qq[2] = (Rb[5] + Rb[7]) / sc;
+      } else {
+        float sc = sqrtf(1.f + Rb[8] - Rb[0] - Rb[4]) * 2.f;
+        qq[3] = (Rb[3] - Rb[1]) / sc; qq[0] = (Rb[2] + Rb[6]) / sc; qq[1] = (Rb[5] + Rb[7]) / sc; qq[2] = 0.25f * sc;
+      }
+      if (qq[3] < 0.f) for (int i = 0; i < 4; ++i) qq[i] = -qq[i];
+      float* rb = B.rigid_body_states + ((size_t)e * NB + lane) * 13;
+      rb[0] = pos.x; rb[1] = pos.y; rb[2] = pos.z;
+      rb[3] = qq[0]; rb[4] = qq[1]; rb[5] = qq[2]; rb[6] = qq[3];
+      rb[7] = lv.x; rb[8] = lv.y; rb[9] = lv.z;
+      const float* w = s.W[k];
+      rb[10] = w[0]; rb[11] = w[1]; rb[12] = w[2];
+      s.rbz[lane] = pos.z;
+      float* cfo = B.contact_forces + ((size_t)e * NB + lane) * 3;
+      cfo[0] = s.cf[lane][0]; cfo[1] = s.cf[lane][1]; cfo[2] = s.cf[lane][2];
+    }
+    if (lane < D) B.torques[(size_t)e * D + lane] = s.tau[lane];
+    __syncthreads();
+  } else {
+    // post-physics only: physics state supplied by the caller
+    if (lane < NB) {
+      const float* cfi = B.contact_forces + ((size_t)e * NB + lane) * 3;
+      s.cf[lane][0] = cfi[0]; s.cf[lane][1] = cfi[1]; s.cf[lane][2] = cfi[2];
+      s.rbz[lane] = B.rigid_body_states[((size_t)e * NB + lane) * 13 + 2];
+    }
+    if (lane < D) s.tau[lane] = B.torques[(size_t)e * D + lane];
+    __syncthreads();
+  }
+
+  // ================================================================ post-physics
+  // Go2Robot.post_physics_step go2.py:345-387 / LeggedRobot legged_robot.py:103-138
+  float root[13];
+  for (int i = 0; i < 13; ++i) root[i] = s.hist[i];
+  float cmd[4];
+  for (int i = 0; i < 4; ++i) cmd[i] = B.commands[e * 4 + i];
+  int64_t ep = B.episode_length[e] + 1;
+  fill_uniforms(s, seed, gid, step, 0, lane);
+  Scratch x;
+  const float g[3] = {0.f, 0.f, -1.f};
+  quat_rotate_inverse(root + 3, root + 7, x.blv);
+  quat_rotate_inverse(root + 3, root + 10, x.bav);
+  quat_rotate_inverse(root + 3, g, x.pg);
+  float lch[4] = {0.f, 0.f, 0.f, 0.f};
+  uint8_t lc[4] = {0, 0, 0, 0};
+  x.roll = x.pitch = x.yaw = 0.f;
+  x.ph[0] = x.ph[1] = x.ph[2] = x.ph[3] = 0.f;
+  if (Pm->task_kind == LGX_TASK_GO2) {
+    // update_feet_states go2.py:266-328
+    float phase = trem((float)ep * Pm->dt, Pm->period) / Pm->period;
+    float pfr = trem(phase + Pm->offset_fr, 1.0f), pbl = trem(phase + Pm->offset_bl, 1.0f);
+    float pfl = trem(phase + Pm->offset_fl, 1.0f), pbr = trem(phase + Pm->offset_br, 1.0f);
+    float msk = (nrm3(cmd[0], cmd[1], cmd[2]) < 0.2f) ? 0.0f : 1.0f;
+    x.ph[0] = pfl * msk; x.ph[1] = pfr * msk; x.ph[2] = pbl * msk; x.ph[3] = pbr * msk;
+    for (int f = 0; f < 4; ++f) {
+      lc[f] = B.last_contacts[e * Pm->num_feet + f];
+      lch[f] = B.last_contact_heights[e * Pm->num_feet + f];
+      int curc = s.cf[Pm->feet_idx[f]][2] > 1.0f;
+      x.contact[f] = curc || lc[f];
+      lc[f] = (uint8_t)curc;
+      x.feet_z[f] = s.rbz[Pm->feet_idx[f]];
+      if (x.contact[f]) lch[f] = x.feet_z[f];
+    }
+    // quaternion_to_euler go2.py:11-31
+    float qx = root[3], qy = root[4], qz = root[5], qw = root[6];
+    x.roll = atan2f(2.0f * (qw * qx + qy * qz), 1.0f - 2.0f * (qx * qx + qy * qy));
+    x.pitch = asinf(clipf(2.0f * (qw * qy - qz * qx), -1.0f, 1.0f));
+    x.yaw = atan2f(2.0f * (qw * qz + qx * qy), 1.0f - 2.0f * (qy * qy + qz * qz));
+  }
+  // _post_physics_step_callback go2.py:390-410
+  if (ep % Pm->resample_interval == 0) resample_commands(Pm, cmd, s.U, S_CMD, root + 3);
+  if (Pm->heading_command) {
+    const float fwd[3] = {1.f, 0.f, 0.f};
+    float f[3];
+    quat_apply(root + 3, fwd, f);
+    float heading = atan2f(f[1], f[0]);
+    float gain = Pm->task_kind == LGX_TASK_GO2 ? Pm->heading_error_gain : 0.5f;
+    cmd[2] = clipf(wrap_to_pi(cmd[3] - heading) * gain, -1.0f, 1.0f);
+  }
+  get_heights(Pm, B, s, root, lane);
+  __syncthreads();
+  if (Pm->push_robots && (step % (uint64_t)Pm->push_interval == 0)) {
+    root[7] = rand_range(-Pm->max_push_vel_xy, Pm->max_push_vel_xy, s.U[S_PUSH + 0]);
+    root[8] = rand_range(-Pm->max_push_vel_xy, Pm->max_push_vel_xy, s.U[S_PUSH + 1]);
+  }
+  // check_termination go2.py:186-204
+  int reset = 0;
+  for (int i = 0; i < Pm->n_termination; ++i) {
+    const float* c = s.cf[Pm->termination_idx[i]];
+    reset |= nrm3(c[0], c[1], c[2]) > 1.0f;
+  }
+  int tout = ep > Pm->max_episode_length;
+  reset |= tout;
+  reset |= x.pg[2] > 0.0f;
+  if (Pm->parkour) reset |= root[2] < -1.0f;
+  x.jump = B.rpy_phase ? B.rpy_phase[e * 8 + 7] : 0.f;
+  // compute_reward legged_robot.py:216-237
+  const int K = Pm->num_reward_terms;
+  const int KS = K + (Pm->has_termination_reward ? 1 : 0);
+  float lact[LGX_MAX_DOF], ldv[LGX_MAX_DOF], ltq[LGX_MAX_DOF], fat[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int j = 0; j < A; ++j) lact[j] = B.last_actions[(size_t)e * A + j];
+  for (int j = 0; j < D; ++j) { ldv[j] = B.last_dof_vel[(size_t)e * D + j]; ltq[j] = B.last_torques[(size_t)e * D + j]; }
+  if (B.feet_air_time) for (int f = 0; f < Pm->num_feet && f < 4; ++f) fat[f] = B.feet_air_time[e * Pm->num_feet + f];
+  float rew = 0.0f;
+  float my_sum = 0.f;
+  for (int k = 0; k < K; ++k) {
+    float v = reward_term(Pm, B, s, x, e, Pm->reward_ids[k], root, cmd, lact, ldv, ltq, lch, fat, lc) * Pm->reward_scales[k];
+    rew += v;
+    if (lane == k) my_sum = v;
+  }
+  if (Pm->only_positive_rewards) rew = rew < 0.0f ? 0.0f : rew;
+  if (Pm->has_termination_reward) {
+    float v = (float)(reset && !tout) * Pm->termination_scale;
+    rew += v;
+    if (lane == K) my_sum = v;
+  }
+  __syncthreads();
+  if (lane < KS) B.episode_sums[(size_t)e * KS + lane] += my_sum;
+  if (lane == 0) { B.rew[e] = rew; B.reset[e] = (uint8_t)reset; B.time_out[e] = (uint8_t)tout; }
+  __syncthreads();
+  // reset_idx (go2.py:207-263)
+  if (reset) reset_env(Pm, B, e, lane, s.U, root, s.th, s.thd, cmd, ep, true, false);
+  __syncthreads();
+
+  // compute_observations go2.py:467-574 / legged_robot.py:240-273
+  const int Pp = Pm->num_proprio, H = Pm->history_len;
+  if (Pm->task_kind == LGX_TASK_GO2 && Pm->parkour) {
+    int outl = 0;
+    for (int i = 0; i < Pm->num_height_points; ++i) outl += fabsf(s.heights[i]) > 0.1f;
+    x.jump = (float)(outl >= 8);
+  }
+  for (int i = lane; i < Pp; i += 64) {
+    float v;
+    if (Pm->task_kind == LGX_TASK_GO2) {
+      if (i < 3) v = x.bav[i] * Pm->obs_scale_ang_vel;
+      else if (i == 3) v = x.roll;
+      else if (i == 4) v = x.pitch;
+      else if (i < 8) v = cmd[i - 5] * Pm->commands_scale[i - 5];
+      else if (i < 8 + D) v = (s.th[i - 8] - Pm->default_dof_pos[i - 8]) * Pm->obs_scale_dof_pos;
+      else if (i < 8 + 2 * D) v = s.thd[i - 8 - D] * Pm->obs_scale_dof_vel;
+      else if (i < 8 + 2 * D + A) v = s.act[i - 8 - 2 * D];
+      else {
+        int q = i - (8 + 2 * D + A);  // sin/cos of FR, FL, BL, BR
+        const int order[4] = {1, 0, 2, 3};
+        float p = 6.283185307179586f * x.ph[order[q >> 1]];
+        v = (q & 1) ? cosf(p) : sinf(p);
+      }
+    } else {
+      if (i < 3) v = x.blv[i] * Pm->obs_scale_lin_vel;
+      else if (i < 6) v = x.bav[i - 3] * Pm->obs_scale_ang_vel;
+      else if (i < 9) v = x.pg[i - 6];
+      else if (i < 12) v = cmd[i - 9] * Pm->commands_scale[i - 9];
+      else if (i < 12 + D) v = (s.th[i - 12] - Pm->default_dof_pos[i - 12]) * Pm->obs_scale_dof_pos;
+      else if (i < 12 + 2 * D) v = s.thd[i - 12 - D] * Pm->obs_scale_dof_vel;
+      else if (i < 12 + 2 * D + A) v = s.act[i - 12 - 2 * D];
+      else v = clipf(root[2] - 0.5f - s.heights[i - (12 + 2 * D + A)], -1.0f, 1.0f) * Pm->obs_scale_height;
+    }
+    if (Pm->add_noise) v = v + (2.0f * s.U[S_NOISE + i] - 1.0f) * Pm->noise_vec[i];
+    s.cur[i] = v;
+  }
+  // stage the old history (obs[0:H*P]) in LDS
+  float* hist_g = B.obs_history + (size_t)e * H * Pp;
+  for (int i = lane; i < H * Pp; i += 64) s.hist[16 + i] = reset ? 0.f : hist_g[i];  // reset zeroes it (go2.py:238)
+  __syncthreads();
+  const float co = Pm->clip_obs;
+  float* obs = B.obs + (size_t)e * Pm->num_obs;
+  float* cr = B.critic ? B.critic + (size_t)e * Pm->num_critic : nullptr;
+  const bool go2 = Pm->task_kind == LGX_TASK_GO2;
+  for (int i = lane; i < H * Pp; i += 64) {
+    float v = clipf(s.hist[16 + i], -co, co);
+    obs[i] = v;
+    if (go2 && cr) cr[i] = v;
+  }
+  for (int i = lane; i < Pp; i += 64) {
+    float v = clipf(s.cur[i], -co, co);
+    obs[H * Pp + i] = v;
+    if (go2 && cr) cr[H * Pp + i] = v;
+  }
+  if (go2) {
+    const int NO = Pm->num_obs;
+    // priv = [mass params (4), friction, kp-1 (D), kd-1 (D)]
+    for (int i = lane; i < Pm->num_priv; i += 64) {
+      float v;
+      if (i < 4) v = B.mass_params[e * 4 + i];
+      else if (i == 4) v = B.friction[e];
+      else if (i < 5 + D) v = s.kpm[i - 5] - 1.0f;
+      else v = s.kdm[i - 5 - D] - 1.0f;
+      v = clipf(v, -co, co);
+      B.priv[(size_t)e * Pm->num_priv + i] = v;
+      if (cr) cr[NO + i] = v;
+    }
+    if (lane < 3) {
+      float v = clipf(x.blv[lane] * Pm->obs_scale_lin_vel, -co, co);
+      B.est[(size_t)e * Pm->num_est + lane] = v;
+      if (cr) cr[NO + Pm->num_priv + lane] = v;
+    }
+    for (int i = lane; i < Pm->num_scan; i += 64) {
+      float v = clipf(root[2] - 0.3f - s.heights[i], -1.0f, 1.0f);
+      B.scan[(size_t)e * Pm->num_scan + i] = v;
+      if (cr) cr[NO + Pm->num_priv + 3 + i] = clipf(v, -co, co);
+    }
+  }
+  // history update go2.py:570-574
+  for (int i = lane; i < H * Pp; i += 64) {
+    float v = (ep <= 1) ? s.cur[i % Pp] : (i < (H - 1) * Pp ? s.hist[16 + i + Pp] : s.cur[i - (H - 1) * Pp]);
+    hist_g[i] = v;
+  }
+  // last_* copies go2.py:380-384 and state write-back
+  if (lane < A) B.last_actions[(size_t)e * A + lane] = s.act[lane];
+  if (lane < D) {
+    B.last_dof_vel[(size_t)e * D + lane] = s.thd[lane];
+    B.last_torques[(size_t)e * D + lane] = s.tau[lane];
+    B.dof_state[((size_t)e * D + lane) * 2] = s.th[lane];
+    B.dof_state[((size_t)e * D + lane) * 2 + 1] = s.thd[lane];
+  }
+  if (lane < 6) B.last_root_vel[e * 6 + lane] = root[7 + lane];
+  if (lane < 3) {
+    B.last_base_lin_vel[e * 3 + lane] = x.blv[lane];
+    if (B.base_lin_vel) B.base_lin_vel[e * 3 + lane] = x.blv[lane];
+    if (B.base_ang_vel) B.base_ang_vel[e * 3 + lane] = x.bav[lane];
+    if (B.projected_gravity) B.projected_gravity[e * 3 + lane] = x.pg[lane];
+  }
+  if (lane < 13) root_g[lane] = root[lane];
+  if (lane < 4) B.commands[e * 4 + lane] = cmd[lane];
+  if (go2 && lane < Pm->num_feet) {
+    if (!reset) {
+      B.last_contacts[e * Pm->num_feet + lane] = lc[lane];
+      B.last_contact_heights[e * Pm->num_feet + lane] = lch[lane];
+    }
+    if (B.feet_air_time && !reset) B.feet_air_time[e * Pm->num_feet + lane] = fat[lane];
+  }
+  if (lane == 0) B.episode_length[e] = ep;
+  if (B.rpy_phase && lane < 8) {
+    float v = lane == 0 ? x.roll : lane == 1 ? x.pitch : lane == 2 ? x.yaw : lane < 7 ? x.ph[lane - 3] : x.jump;
+    B.rpy_phase[e * 8 + lane] = v;
+  }
+  if (B.measured_heights)
+    for (int i = lane; i < Pm->num_height_points; i += 64) B.measured_heights[(size_t)e * Pm->num_height_points + i] = s.heights[i];
+}
+
+// BaseTask.reset -> reset_idx(env_ids) outside a step (RNG stream 1)
+__global__ __launch_bounds__(64) void reset_kernel(const lgx_task_params* __restrict__ Pm, lgx_buffers B,
+                                                   const uint8_t* __restrict__ mask, uint64_t seed, uint64_t call) {
+  __shared__ Sh s;
+  const int e = blockIdx.x;
+  const int lane = threadIdx.x;
+  if (!mask[e]) return;
+  const int D = Pm->num_dof;
+  fill_uniforms(s, seed, (uint32_t)(Pm->env_id_offset + e), call, 1, lane);
+  float root[13], cmd[4], th[LGX_MAX_DOF], thd[LGX_MAX_DOF];
+  for (int i = 0; i < 13; ++i) root[i] = B.root_states[(size_t)e * 13 + i];
+  for (int i = 0; i < 4; ++i) cmd[i] = B.commands[e * 4 + i];
+  int64_t ep = B.episode_length[e];
+  reset_env(Pm, B, e, lane, s.U, root, th, thd, cmd, ep, false, true);
+  if (lane < 13) B.root_states[(size_t)e * 13 + lane] = root[lane];
+  if (lane < D) {
+    B.dof_state[((size_t)e * D + lane) * 2] = th[lane];
+    B.dof_state[((size_t)e * D + lane) * 2 + 1] = thd[lane];
+  }
+  if (lane < 4) B.commands[e * 4 + lane] = cmd[lane];
+  if (lane == 0) { B.episode_length[e] = ep; B.reset[e] = 1; }
+}
+
+}  // namespace lgx
+
+// ============================================================== C ABI
+#include <string>
+
+struct lgx_env {
+  lgx_model model;
+  lgx_task_params params;
+  lgx_buffers buffers;
+  lgx_model* d_model = nullptr;
+  lgx_task_params* d_params = nullptr;
+  int device = 0;
+  bool bound = false;
+  std::string err;
+};
+
+static int fail(lgx_env* env, const std::string& msg) {
+  if (env) env->err = msg;
+  return -1;
+}
+
+#define HIP_OK(call)                                                                   \
+  do {                                                                                 \
+    hipError_t _e = (call);                                                            \
+    if (_e != hipSuccess) return fail(env, std::string(#call ": ") + hipGetErrorString(_e)); \
+  } while (0)
+
+extern "C" {
+
+int32_t lgx_abi_version(void) { return LGX_ABI_VERSION; }
+int64_t lgx_sizeof_model(void) { return (int64_t)sizeof(lgx_model); }
+int64_t lgx_sizeof_task_params(void) { return (int64_t)sizeof(lgx_task_params); }
+int64_t lgx_sizeof_buffers(void) { return (int64_t)sizeof(lgx_buffers); }
+
+int lgx_create(const lgx_model* model, const lgx_task_params* params, int32_t device, lgx_env** out) {
+  if (!model || !params || !out) return -2;
+  lgx_env* env = new lgx_env();
+  *out = env;
+  env->model = *model;
+  env->params = *params;
+  env->device = device;
+  if (params->abi_version != LGX_ABI_VERSION) return fail(env, "ABI version mismatch");
+  // the kernel's structured solver assumes base + 4 chains of 3 revolute joints
+  if (model->num_links != lgx::NL || params->num_dof != lgx::NJ)
+    return fail(env, "model must be a floating base with 4 chains of 3 joints (13 links, 12 dof)");
+  for (int l = 0; l < 4; ++l)
+    for (int i = 0; i < 3; ++i) {
+      int k = 1 + 3 * l + i;
+      int expect = i == 0 ? 0 : k - 1;
+      if (model->link_parent[k] != expect) return fail(env, "link tree is not 4 serial chains of 3");
+    }
+  if (model->num_candidates > LGX_MAX_CANDIDATES || model->num_bodies > LGX_MAX_BODIES)
+    return fail(env, "too many contact candidates or bodies");
+  if (params->history_len * params->num_proprio > lgx::MAXHIST - 16) return fail(env, "history too long");
+  if (params->num_proprio > LGX_MAX_PROPRIO || params->num_height_points > LGX_MAX_HEIGHT_POINTS)
+    return fail(env, "observation too large");
+  if (params->num_reward_terms + 1 > 64) return fail(env, "too many reward terms");
+  HIP_OK(hipSetDevice(device));
+  HIP_OK(hipMalloc(&env->d_model, sizeof(lgx_model)));
+  HIP_OK(hipMalloc(&env->d_params, sizeof(lgx_task_params)));
+  HIP_OK(hipMemcpy(env->d_model, model, sizeof(lgx_model), hipMemcpyHostToDevice));
+  HIP_OK(hipMemcpy(env->d_params, params, sizeof(lgx_task_params), hipMemcpyHostToDevice));
+  return 0;
+}
+
+int lgx_bind(lgx_env* env, const lgx_buffers* b) {
+  if (!env || !b) return -2;
+  static const char* required[] = {"root_states", "dof_state", "contact_forces", "rigid_body_states", "actions_in",
+                                   "actions", "torques", "last_actions", "last_dof_vel", "last_root_vel",
+                                   "last_base_lin_vel", "last_torques", "commands", "episode_length",
+                                   "episode_sums", "obs_history", "obs", "rew", "reset", "time_out", "env_origins"};
+  const void* ptrs[] = {b->root_states, b->dof_state, b->contact_forces, b->rigid_body_states, b->actions_in,
+                        b->actions, b->torques, b->last_actions, b->last_dof_vel, b->last_root_vel,
+                        b->last_base_lin_vel, b->last_torques, b->commands, b->episode_length,
+                        b->episode_sums, b->obs_history, b->obs, b->rew, b->reset, b->time_out, b->env_origins};
+  for (size_t i = 0; i < sizeof(ptrs) / sizeof(ptrs[0]); ++i)
+    if (!ptrs[i]) return fail(env, std::string("lgx_bind: required buffer missing: ") + required[i]);
+  if (env->params.task_kind == LGX_TASK_GO2) {
+    if (!b->priv || !b->est || !b->scan || !b->critic || !b->last_contacts || !b->last_contact_heights ||
+        !b->mass_params || !b->friction)
+      return fail(env, "lgx_bind: Go2 task needs priv/est/scan/critic/last_contacts/last_contact_heights/mass_params/friction");
+  }
+  env->buffers = *b;
+  env->bound = true;
+  return 0;
+}
+
+static int launch_step(lgx_env* env, uint64_t seed, uint64_t step, void* stream, bool physics) {
+  if (!env) return -2;
+  if (!env->bound) return fail(env, "lgx_step before lgx_bind");
+  hipStream_t st = (hipStream_t)stream;
+  const int N = env->params.num_envs;
+  const int KS = env->params.num_reward_terms + (env->params.has_termination_reward ? 1 : 0);
+  if (env->buffers.episode_stats)
+    HIP_OK(hipMemsetAsync(env->buffers.episode_stats, 0, sizeof(float) * (KS + 1), st));
+  if (physics)
+    hipLaunchKernelGGL(lgx::env_step_kernel<true>, dim3(N), dim3(64), 0, st, env->d_model, env->d_params, env->buffers,
+                       seed, step);
+  else
+    hipLaunchKernelGGL(lgx::env_step_kernel<false>, dim3(N), dim3(64), 0, st, env->d_model, env->d_params,
+                       env->buffers, seed, step);
+  HIP_OK(hipGetLastError());
+  return 0;
+}
+
+int lgx_step(lgx_env* env, uint64_t seed, uint64_t step_counter, void* hip_stream) {
+  return launch_step(env, seed, step_counter, hip_stream, true);
+}
+
+int lgx_post_physics(lgx_env* env, uint64_t seed, uint64_t step_counter, void* hip_stream) {
+  return launch_step(env, seed, step_counter, hip_stream, false);
+}
+
+int lgx_physics(lgx_env* env, void* hip_stream) {
+  (void)hip_stream;
+  return fail(env, "lgx_physics: use lgx_step (physics is fused with the post-physics pass)");
+}
+
+int lgx_reset_envs(lgx_env* env, const uint8_t* env_mask, uint64_t seed, uint64_t reset_call, void* hip_stream) {
+  if (!env) return -2;
+  if (!env->bound) return fail(env, "lgx_reset_envs before lgx_bind");
+  if (!env_mask) return fail(env, "lgx_reset_envs: env_mask is NULL");
+  hipStream_t st = (hipStream_t)hip_stream;
+  const int KS = env->params.num_reward_terms + (env->params.has_termination_reward ? 1 : 0);
+  if (env->buffers.episode_stats)
+    HIP_OK(hipMemsetAsync(env->buffers.episode_stats, 0, sizeof(float) * (KS + 1), st));
+  hipLaunchKernelGGL(lgx::reset_kernel, dim3(env->params.num_envs), dim3(64), 0, st, env->d_params, env->buffers,
+                     env_mask, seed, reset_call);
+  HIP_OK(hipGetLastError());
+  return 0;
+}
+
+const char* lgx_last_error(const lgx_env* env) { return env ? env->err.c_str() : "null env"; }
+
+void lgx_destroy(lgx_env* env) {
+  if (!env) return;
+  if (env->d_model) (void)hipFree(env->d_model);
+  if (env->d_params) (void)hipFree(env->d_params);
+  delete env;
+}
+
+}  // extern "C"

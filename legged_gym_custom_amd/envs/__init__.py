@@ -1,13 +1,17 @@
 """Task registration (drop-in for legged_gym/envs/__init__.py:19-24)."""
+from legged_gym_custom_amd import LEGGED_GYM_ROOT_DIR, LEGGED_GYM_ENVS_DIR  # noqa: F401
+from legged_gym_custom_amd.envs.base.legged_robot import LeggedRobot  # noqa: F401
 from legged_gym_custom_amd.envs.base.legged_robot_config import LeggedRobotCfg, LeggedRobotCfgPPO  # noqa: F401
+from legged_gym_custom_amd.envs.go2.go2 import Go2Robot
 from legged_gym_custom_amd.envs.go2.go2_config import Go2Cfg, Go2CfgPPO
+from legged_gym_custom_amd.utils.task_registry import task_registry
 
-_CONFIGS = {
-    "go2": (Go2Cfg, Go2CfgPPO),
-}
+task_registry.register("go2", Go2Robot, Go2Cfg(), Go2CfgPPO())
+
+_CONFIGS = {"go2": (Go2Cfg, Go2CfgPPO)}
 
 
 def task_registry_configs(name):
-    """Fresh (env_cfg, train_cfg) instances for a registered task name."""
+    """Fresh (env_cfg, train_cfg) instances for a registered task name (tests/tools)."""
     e, t = _CONFIGS[name]
     return e(), t()

@@ -1,0 +1,282 @@
+"""LeggedRobot — drop-in for legged_gym/envs/base/legged_robot.py:21-1152.
+
+The whole env step (legged_robot.py:67-100: clip, decimation x {PD torque, simulate},
+post_physics_step, obs clip) is ONE HIP kernel launch of liblgx.so (lgx_step), one
+wavefront per env. This class owns the torch buffers (same names/shapes as the
+reference, env-major), builds the model/params once, binds the buffers to the native
+env, and keeps the reference's Python-visible surface: step/reset/reset_idx, the
+8-tuple return, extras['time_outs'/'episode'], common_step_counter, buffer attributes.
+"""
+import os
+
+import numpy as np
+import torch
+
+from legged_gym_custom_amd import LEGGED_GYM_ROOT_DIR, _abi, _native
+from legged_gym_custom_amd import model as mdl
+from legged_gym_custom_amd import params as prm
+from legged_gym_custom_amd.envs.base.base_task import BaseTask
+from legged_gym_custom_amd.utils.helpers import class_to_dict
+
+
+class LeggedRobot(BaseTask):
+    TASK_KIND = _abi.TASK_LEGGED
+
+    def __init__(self, cfg, sim_params, physics_engine, sim_device, headless):
+        self.cfg = cfg
+        self.sim_params = sim_params
+        self.height_samples = None
+        self.debug_viz = False
+        self.init_done = False
+        self._parse_cfg(self.cfg)
+        self.num_envs = self.cfg.env.num_envs
+        self.seed = int(getattr(cfg, "seed", 1))
+        if self.seed < 0:
+            self.seed = 1
+        # env sharding across ranks (one process per GPU): global env ids are used for
+        # the RNG counter and terrain_types, so a sharded run draws what one GPU would.
+        rank, world = 0, 1
+        if torch.distributed.is_available() and torch.distributed.is_initialized():
+            rank, world = torch.distributed.get_rank(), torch.distributed.get_world_size()
+        self.env_id_offset = rank * self.num_envs
+        self.num_envs_total = world * self.num_envs
+        super().__init__(self.cfg, sim_params, physics_engine, sim_device, headless)
+        self._init_buffers()
+        self._prepare_reward_function()
+        self.init_done = True
+
+    # ------------------------------------------------------------------ step
+    def step(self, actions):
+        """legged_robot.py:67-100 as one kernel launch; returns the reference's 8-tuple."""
+        self.actions_in.copy_(actions, non_blocking=True)
+        self.common_step_counter += 1
+        self._native.step(self.seed, self.common_step_counter, torch.cuda.current_stream(self.device).cuda_stream)
+        self._update_extras()
+        return (self.obs_buf, self.privileged_obs_buf, self.critic_obs_buf, self.estimated_obs_buf, self.scan_obs_buf,
+                self.rew_buf, self.reset_buf, self.extras)
+
+    def reset_idx(self, env_ids):
+        """reset_idx outside a step (BaseTask.reset): masked reset on device (RNG stream 1)."""
+        if isinstance(env_ids, torch.Tensor):
+            env_ids = env_ids.to(self.device)
+        mask = torch.zeros(self.num_envs, dtype=torch.uint8, device=self.device)
+        mask[env_ids] = 1
+        self._native.reset_envs(mask, self.seed, self._reset_calls, torch.cuda.current_stream(self.device).cuda_stream)
+        self._reset_calls += 1
+        self.reset_buf[env_ids] = True
+        self._update_extras()
+
+    def _update_extras(self):
+        """extras['episode'] / ['time_outs'] with the reference's stale-when-no-reset
+        semantics (go2.py:246-263, Appendix B Q5), computed on device (no host sync)."""
+        st = self.episode_stats
+        cnt = st[-1]
+        means = st[:-1] / torch.clamp(cnt, min=1.0) / self.max_episode_length_s
+        self._episode_means = torch.where(cnt > 0, means, self._episode_means)
+        self.extras["episode"] = {"rew_" + k: self._episode_means[i] for i, k in enumerate(self._episode_keys)}
+        if self.cfg.env.send_timeouts:
+            self._extras_time_outs = torch.where(self.reset_buf.any(), self.time_out_buf, self._extras_time_outs)
+            self.extras["time_outs"] = self._extras_time_outs
+
+    # ------------------------------------------------------------------ setup
+    def create_sim(self):
+        self.up_axis_idx = 2
+        mesh_type = self.cfg.terrain.mesh_type
+        if mesh_type in ("heightfield", "trimesh"):
+            raise NotImplementedError(
+                "heightfield/trimesh terrain is the next §8 row (SURVEY.md §8f #1); plane is supported")
+        elif mesh_type not in ("plane", None, "none"):
+            raise ValueError("Terrain mesh type not recognised. Allowed types are [None, plane, heightfield, trimesh]")
+        self._create_envs()
+
+    def _create_envs(self):
+        """legged_robot.py:805-894: model, body/dof names, index tables, domain randomisation."""
+        asset_cfg = self.cfg.asset
+        self.model_dict = mdl.load_model(asset_cfg.file, asset_cfg.foot_name, LEGGED_GYM_ROOT_DIR)
+        self.body_names = list(self.model_dict["body_names"])
+        self.dof_names = list(self.model_dict["dof_names"])
+        self.num_bodies = len(self.body_names)
+        self.num_dof = self.num_dofs = len(self.dof_names)
+        base = list(self.cfg.init_state.pos) + list(self.cfg.init_state.rot) + list(self.cfg.init_state.lin_vel) + \
+            list(self.cfg.init_state.ang_vel)
+        self.base_init_state = torch.tensor(base, dtype=torch.float, device=self.device)
+        self._get_env_origins()
+        n = self.num_envs
+        dr = self.cfg.domain_rand
+        # _process_rigid_shape_props legged_robot.py:318-329 (64 friction buckets, CPU RNG)
+        if dr.randomize_friction:
+            bucket_ids = torch.randint(0, 64, (n, 1))
+            lo, hi = dr.friction_range
+            buckets = (hi - lo) * torch.rand(64, 1) + lo
+            self.friction_coeffs = buckets[bucket_ids]
+        mass = np.zeros((n, 4), dtype=np.float32)
+        for i in range(n):
+            torch.rand(2, 1)  # start-pose xy jitter draw (legged_robot.py:867), kept for RNG order
+            if dr.randomize_base_mass:
+                mass[i, 0] = np.random.uniform(dr.added_mass_range[0], dr.added_mass_range[1], size=(1,))[0]
+            if getattr(dr, "randomize_center_of_mass", False):
+                mass[i, 1:4] = np.random.uniform(dr.added_com_range[0], dr.added_com_range[1], size=(3,))
+        self.privileged_mass_params = torch.from_numpy(mass).to(self.device)
+        names = self.body_names
+        feet = [s for s in names if self.cfg.asset.foot_name in s]
+        pen, term = [], []
+        for key in self.cfg.asset.penalize_contacts_on:
+            pen.extend([s for s in names if key in s])
+        for key in self.cfg.asset.terminate_after_contacts_on:
+            term.extend([s for s in names if key in s])
+        idx = lambda lst: torch.tensor([names.index(s) for s in lst], dtype=torch.long, device=self.device)  # noqa: E731
+        self.feet_indices = idx(feet)
+        self.penalised_contact_indices = idx(pen)
+        self.termination_contact_indices = idx(term)
+        links = self.model_dict["links"][1:]
+        self.dof_pos_limits = torch.from_numpy(prm.soft_dof_limits(
+            [l["lower"] for l in links], [l["upper"] for l in links], self.cfg.rewards.soft_dof_pos_limit)).to(self.device)
+        self.dof_vel_limits = torch.tensor([l["velocity"] for l in links], dtype=torch.float, device=self.device)
+        self.torque_limits = torch.tensor([l["effort"] for l in links], dtype=torch.float, device=self.device)
+
+    def _get_env_origins(self):
+        """legged_robot.py:897-930 (plane: a grid with env_spacing)."""
+        self.custom_origins = False
+        self.env_origins = torch.zeros(self.num_envs, 3, device=self.device)
+        # the grid is laid out over the GLOBAL env index so shards tile one field
+        total = self.num_envs_total
+        num_cols = np.floor(np.sqrt(total))
+        num_rows = np.ceil(total / num_cols)
+        xx, yy = torch.meshgrid(torch.arange(num_rows), torch.arange(num_cols), indexing="ij")
+        sl = slice(self.env_id_offset, self.env_id_offset + self.num_envs)
+        spacing = self.cfg.env.env_spacing
+        self.env_origins[:, 0] = spacing * xx.flatten()[sl].to(self.device)
+        self.env_origins[:, 1] = spacing * yy.flatten()[sl].to(self.device)
+
+    def _parse_cfg(self, cfg):
+        """legged_robot.py:933-955."""
+        self.dt = self.cfg.control.decimation * self.sim_params.dt
+        self.obs_scales = self.cfg.normalization.obs_scales
+        self.reward_scales = class_to_dict(self.cfg.rewards.scales)
+        self.command_ranges = class_to_dict(self.cfg.commands.ranges)
+        if self.cfg.terrain.mesh_type not in ("heightfield", "trimesh"):
+            self.cfg.terrain.curriculum = False
+        self.max_episode_length_s = self.cfg.env.episode_length_s
+        self.max_episode_length = np.ceil(self.max_episode_length_s / self.dt)
+        self.cfg.domain_rand.push_interval = np.ceil(self.cfg.domain_rand.push_interval_s / self.dt)
+
+    def _init_buffers(self):
+        """legged_robot.py:625-727 (+ go2.py:132-177): torch-owned, env-major buffers,
+        bound once to the native env."""
+        n, d, nb, na = self.num_envs, self.num_dof, self.num_bodies, self.num_actions
+        dev = self.device
+        z = lambda *s, dtype=torch.float: torch.zeros(*s, device=dev, dtype=dtype)  # noqa: E731
+        self.root_states = z(n, 13)
+        self.root_states[:] = self.base_init_state
+        self.root_states[:, :3] += self.env_origins
+        self._dof_state3 = z(n, d, 2)
+        self.dof_state = self._dof_state3.view(n * d, 2)
+        self.dof_pos = self._dof_state3[..., 0]
+        self.dof_vel = self._dof_state3[..., 1]
+        self.base_quat = self.root_states[:, 3:7]
+        self._contact3 = z(n, nb, 3)
+        self.contact_forces = self._contact3
+        self.rigid_body_states = z(n * nb, 13)
+        self.rigid_body_states_view = self.rigid_body_states.view(n, nb, 13)
+        self.common_step_counter = 0
+        self._reset_calls = 0
+        self.extras = {}
+        self.noise_scale_vec = torch.from_numpy(prm.noise_vector(self.cfg, self.TASK_KIND == _abi.TASK_GO2)).to(dev)
+        self.add_noise = self.cfg.noise.add_noise
+        self.gravity_vec = torch.tensor([0.0, 0.0, -1.0], device=dev).repeat((n, 1))
+        self.forward_vec = torch.tensor([1.0, 0.0, 0.0], device=dev).repeat((n, 1))
+        self.actions_in = z(n, na)
+        self.actions = z(n, na)
+        self.torques = z(n, na)
+        self.last_actions = z(n, na)
+        self.last_dof_vel = z(n, d)
+        self.last_root_vel = z(n, 6)
+        self.last_torques = z(n, na)
+        self.commands = z(n, self.cfg.commands.num_commands)
+        sc = self.obs_scales
+        self.commands_scale = torch.tensor([sc.lin_vel, sc.lin_vel, sc.ang_vel], device=dev)
+        self.base_lin_vel = z(n, 3)
+        self.base_ang_vel = z(n, 3)
+        self.projected_gravity = z(n, 3)
+        self.projected_gravity[:, 2] = -1.0
+        self.last_base_lin_vel = z(n, 3)
+        xs, ys = self.cfg.terrain.measured_points_x, self.cfg.terrain.measured_points_y
+        self.num_height_points = len(xs) * len(ys)
+        self.measured_heights = z(n, self.num_height_points)
+        self.obs_history_buf = z(n, self.cfg.env.history_buffer_length, self.cfg.env.num_proprio)
+        self.rpy_phase = z(n, 8)
+        self.roll, self.pitch, self.yaw = self.rpy_phase[:, 0], self.rpy_phase[:, 1], self.rpy_phase[:, 2]
+        self.phase_fl, self.phase_fr = self.rpy_phase[:, 3], self.rpy_phase[:, 4]
+        self.phase_bl, self.phase_br = self.rpy_phase[:, 5], self.rpy_phase[:, 6]
+        self.jump_flags = self.rpy_phase[:, 7:8]
+        nf = len(self.feet_indices)
+        self.last_contacts = z(n, nf, dtype=torch.bool)
+        self.last_contact_heights = z(n, nf)
+        self.feet_air_time = z(n, nf)
+        dr = self.cfg.domain_rand
+        if dr.randomize_friction:
+            self._friction = self.friction_coeffs.to(dev).to(torch.float).reshape(n).contiguous()
+        else:
+            self._friction = torch.ones(n, device=dev) * self.cfg.terrain.dynamic_friction
+        self.privileged_friction_coeffs = self._friction.view(n, 1)
+        lo, hi = getattr(dr, "kp_kd_range", [1.0, 1.0])
+        self.kp_kd_multipliers = (hi - lo) * torch.rand(2, n, na, device=dev) + lo
+        if not getattr(dr, "randomize_kp_kd", False):
+            self.kp_kd_multipliers.fill_(1.0)
+        self.default_dof_pos = torch.tensor([self.cfg.init_state.default_joint_angles[nm] for nm in self.dof_names],
+                                            device=dev).unsqueeze(0)
+        self._dof_state3[..., 0] = self.default_dof_pos
+        p_gains, d_gains = [], []
+        for nm in self.dof_names:
+            kp = kd = 0.0
+            for key in self.cfg.control.stiffness.keys():
+                if key in nm:
+                    kp, kd = self.cfg.control.stiffness[key], self.cfg.control.damping[key]
+            p_gains.append(kp)
+            d_gains.append(kd)
+        self.p_gains = torch.tensor(p_gains, device=dev)
+        self.d_gains = torch.tensor(d_gains, device=dev)
+        # ---- native env
+        model_struct = mdl.to_struct(self.model_dict)
+        self.task_params = prm.build_task_params(self.cfg, self.model_dict, n, self.num_envs_total, self.env_id_offset,
+                                                 sim_dt=self.sim_params.dt, go2=self.TASK_KIND == _abi.TASK_GO2)
+        names, _, _, term = prm.reward_terms(self.cfg, self.dt)
+        self._episode_keys = names + (["termination"] if term is not None else [])
+        ks = len(self._episode_keys)
+        self.episode_sums_buf = z(n, ks)
+        self.episode_sums = {k: self.episode_sums_buf[:, i] for i, k in enumerate(self._episode_keys)}
+        self.episode_stats = z(ks + 1)
+        self._episode_means = z(ks)
+        self._extras_time_outs = z(n, dtype=torch.bool)
+        self._native = _native.NativeEnv(model_struct, self.task_params, self.sim_device_id)
+        self._bind()
+
+    def _bind(self):
+        self._native.bind({
+            "root_states": self.root_states, "dof_state": self._dof_state3, "contact_forces": self._contact3,
+            "rigid_body_states": self.rigid_body_states, "actions_in": self.actions_in, "actions": self.actions,
+            "torques": self.torques, "last_actions": self.last_actions, "last_dof_vel": self.last_dof_vel,
+            "last_root_vel": self.last_root_vel, "last_base_lin_vel": self.last_base_lin_vel,
+            "last_torques": self.last_torques, "commands": self.commands,
+            "episode_length": self._episode_length_buf, "episode_sums": self.episode_sums_buf,
+            "obs_history": self.obs_history_buf, "last_contacts": self.last_contacts,
+            "last_contact_heights": self.last_contact_heights, "feet_air_time": self.feet_air_time,
+            "obs": self.obs_buf, "priv": self.privileged_obs_buf if self.num_privileged_obs else None,
+            "critic": self.critic_obs_buf, "est": self.estimated_obs_buf if self.num_estimated_obs else None,
+            "scan": self.scan_obs_buf if self.num_scan_obs else None, "rew": self.rew_buf, "reset": self.reset_buf,
+            "time_out": self.time_out_buf, "base_lin_vel": self.base_lin_vel, "base_ang_vel": self.base_ang_vel,
+            "projected_gravity": self.projected_gravity, "rpy_phase": self.rpy_phase,
+            "measured_heights": self.measured_heights, "friction": self._friction,
+            "mass_params": self.privileged_mass_params, "kp_kd": self.kp_kd_multipliers,
+            "env_origins": self.env_origins, "episode_stats": self.episode_stats,
+        })
+
+    def _prepare_reward_function(self):
+        """legged_robot.py:730-754: nonzero scales x dt, alphabetical; the terms run in
+        the kernel (params.reward_terms validates that each one is implemented)."""
+        for key in list(self.reward_scales.keys()):
+            if self.reward_scales[key] == 0:
+                self.reward_scales.pop(key)
+            else:
+                self.reward_scales[key] *= self.dt
+        self.reward_names = [k for k in self.reward_scales if k != "termination"]

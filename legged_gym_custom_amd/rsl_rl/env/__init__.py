@@ -1,0 +1,1 @@
+from .vec_env import VecEnv  # noqa: F401

@@ -1,0 +1,127 @@
+"""RolloutStorage — drop-in for rsl_rl/storage/rollout_storage.py:7-181.
+
+[T, N, ·] buffers on the learner device; GAE backward scan (rollout_storage.py:110-124);
+advantage normalisation by the mean and UNBIASED std (+1e-8) — over all ranks when
+torch.distributed is initialised (one all-reduce of {Σa, Σa², n}, fp64).
+"""
+import torch
+import torch.distributed as dist
+
+
+class RolloutStorage:
+    class Transition:
+        def __init__(self):
+            self.observations = None
+            self.privileged_observations = None
+            self.critic_observations = None
+            self.true_estimated_observations = None
+            self.scan_observations = None
+            self.actions = None
+            self.rewards = None
+            self.dones = None
+            self.values = None
+            self.actions_log_prob = None
+            self.action_mean = None
+            self.action_sigma = None
+            self.hidden_states = None
+
+        def clear(self):
+            self.__init__()
+
+    def __init__(self, num_envs, num_transitions_per_env, obs_shape, privileged_obs_shape, critic_obs_shape,
+                 estimated_obs_shape, scan_obs_shape, actions_shape, device="cpu"):
+        self.device = device
+        self.obs_shape = obs_shape
+        self.privileged_obs_shape = privileged_obs_shape
+        self.critic_obs_shape = critic_obs_shape
+        self.estimated_obs_shape = estimated_obs_shape
+        self.actions_shape = actions_shape
+        T, N = num_transitions_per_env, num_envs
+        z = lambda *s: torch.zeros(T, N, *s, device=device)  # noqa: E731
+        self.observations = z(*obs_shape)
+        self.privileged_observations = z(*privileged_obs_shape)
+        self.critic_observations = z(*critic_obs_shape)
+        self.true_estimated_observations = z(*estimated_obs_shape)
+        self.scan_observations = z(*scan_obs_shape)
+        self.rewards = z(1)
+        self.actions = z(*actions_shape)
+        self.dones = z(1).byte()
+        self.actions_log_prob = z(1)
+        self.values = z(1)
+        self.returns = z(1)
+        self.advantages = z(1)
+        self.mu = z(*actions_shape)
+        self.sigma = z(*actions_shape)
+        self.num_transitions_per_env = T
+        self.num_envs = N
+        self.saved_hidden_states_a = None
+        self.saved_hidden_states_c = None
+        self.step = 0
+
+    def add_transitions(self, transition):
+        if self.step >= self.num_transitions_per_env:
+            raise AssertionError("Rollout buffer overflow")
+        s = self.step
+        self.observations[s].copy_(transition.observations)
+        self.privileged_observations[s].copy_(transition.privileged_observations)
+        self.critic_observations[s].copy_(transition.critic_observations)
+        self.true_estimated_observations[s].copy_(transition.true_estimated_observations)
+        self.scan_observations[s].copy_(transition.scan_observations)
+        self.actions[s].copy_(transition.actions)
+        self.rewards[s].copy_(transition.rewards.view(-1, 1))
+        self.dones[s].copy_(transition.dones.view(-1, 1))
+        self.values[s].copy_(transition.values)
+        self.actions_log_prob[s].copy_(transition.actions_log_prob.view(-1, 1))
+        self.mu[s].copy_(transition.action_mean)
+        self.sigma[s].copy_(transition.action_sigma)
+        self.step += 1
+
+    def clear(self):
+        self.step = 0
+
+    def compute_returns(self, last_values, gamma, lam):
+        advantage = 0
+        for step in reversed(range(self.num_transitions_per_env)):
+            next_values = last_values if step == self.num_transitions_per_env - 1 else self.values[step + 1]
+            not_terminal = 1.0 - self.dones[step].float()
+            delta = self.rewards[step] + not_terminal * gamma * next_values - self.values[step]
+            advantage = delta + not_terminal * gamma * lam * advantage
+            self.returns[step] = advantage + self.values[step]
+        self.advantages = self.returns - self.values
+        mean, std = self._global_mean(self.advantages)
+        self.advantages = (self.advantages - mean) / (std + 1e-8)
+
+    def _global_mean(self, a):
+        """(mean, unbiased std) of `a` over every rank's shard."""
+        if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+            return a.mean(), a.std()
+        a64 = a.double()
+        m = torch.stack([a64.sum(), (a64 * a64).sum(), torch.tensor(float(a.numel()), device=a.device, dtype=torch.float64)])
+        dist.all_reduce(m)
+        n = m[2]
+        mean = m[0] / n
+        var = (m[1] - n * mean * mean) / (n - 1)
+        return mean.float(), var.clamp(min=0).sqrt().float()
+
+    def get_statistics(self):
+        done = self.dones
+        done[-1] = 1
+        flat_dones = done.permute(1, 0, 2).reshape(-1, 1)
+        done_indices = torch.cat((flat_dones.new_tensor([-1], dtype=torch.int64), flat_dones.nonzero(as_tuple=False)[:, 0]))
+        trajectory_lengths = done_indices[1:] - done_indices[:-1]
+        return trajectory_lengths.float().mean(), self.rewards.mean()
+
+    def mini_batch_generator(self, num_mini_batches, num_epochs=8):
+        batch_size = self.num_envs * self.num_transitions_per_env
+        mini_batch_size = batch_size // num_mini_batches
+        # one permutation shared by all epochs (rollout_storage.py:142, Appendix B Q24)
+        indices = torch.randperm(num_mini_batches * mini_batch_size, requires_grad=False, device=self.device)
+        flat = [t.flatten(0, 1) for t in (self.observations, self.privileged_observations, self.critic_observations,
+                                          self.true_estimated_observations, self.scan_observations, self.actions,
+                                          self.values, self.advantages, self.returns, self.actions_log_prob,
+                                          self.mu, self.sigma)]
+        for _ in range(num_epochs):
+            for i in range(num_mini_batches):
+                idx = indices[i * mini_batch_size:(i + 1) * mini_batch_size]
+                (obs, priv, critic, est, scan, act, val, adv, ret, logp, mu, sigma) = [t[idx] for t in flat]
+                yield obs, priv, critic, est, scan, act, val, adv, ret, logp, mu, sigma, (None, None), None

@@ -57,7 +57,7 @@ class OracleEnv:
             "rigid_body_states": f(N, B, 13), "actions_in": f(N, P.num_actions), "actions": f(N, P.num_actions),
             "torques": f(N, D), "last_actions": f(N, P.num_actions), "last_dof_vel": f(N, D),
             "last_root_vel": f(N, 6), "last_base_lin_vel": f(N, 3), "last_torques": f(N, D), "commands": f(N, 4),
-            "episode_length": np.zeros(N, dtype=np.int64), "episode_sums": f(num_reward_slots, N),
+            "episode_length": np.zeros(N, dtype=np.int64), "episode_sums": f(N, num_reward_slots),
             "obs_history": f(N, P.history_len, P.num_proprio), "last_contacts": np.zeros((N, P.num_feet), np.uint8),
             "last_contact_heights": f(N, P.num_feet), "feet_air_time": f(N, P.num_feet),
             "obs": f(N, P.num_obs), "priv": f(N, max(P.num_priv, 1)), "critic": f(N, P.num_critic),

@@ -278,9 +278,10 @@ static void reset_env(const lgx_task_params* P, lgx_buffers* B, int e, uint64_t 
     }
   }
   int K = P->num_reward_terms + (P->has_termination_reward ? 1 : 0);
+  const int KS = K;
   for (int k = 0; k < K; ++k) {
-    if (B->episode_stats) B->episode_stats[k] += B->episode_sums[(size_t)k * P->num_envs + e];
-    B->episode_sums[(size_t)k * P->num_envs + e] = 0.0f;
+    if (B->episode_stats) B->episode_stats[k] += B->episode_sums[(size_t)e * KS + k];
+    B->episode_sums[(size_t)e * KS + k] = 0.0f;
   }
   if (B->episode_stats) B->episode_stats[K] += 1.0f;
 }
@@ -507,6 +508,7 @@ void oracle_post_physics(const lgx_task_params* P, lgx_buffers* B, uint64_t seed
   const int N = P->num_envs, D = P->num_dof, A = P->num_actions;
   const int Pp = P->num_proprio, H = P->history_len;
   const int K = P->num_reward_terms;
+  const int KS = K + (P->has_termination_reward ? 1 : 0);
   env_scratch* S = (env_scratch*)calloc((size_t)N, sizeof(env_scratch));
   int any_reset = 0;
   /* Pass 1 (per env, independent): everything up to and including reset_idx. */
@@ -588,13 +590,13 @@ void oracle_post_physics(const lgx_task_params* P, lgx_buffers* B, uint64_t seed
     for (int k = 0; k < K; ++k) {
       float v = reward_term(P, B, e, P->reward_ids[k], s) * P->reward_scales[k];
       rew += v;
-      B->episode_sums[(size_t)k * N + e] += v;
+      B->episode_sums[(size_t)e * KS + k] += v;
     }
     if (P->only_positive_rewards) rew = rew < 0.0f ? 0.0f : rew;
     if (P->has_termination_reward) {
       float v = (float)(reset && !tout) * P->termination_scale;
       rew += v;
-      B->episode_sums[(size_t)K * N + e] += v;
+      B->episode_sums[(size_t)e * KS + K] += v;
     }
     B->rew[e] = rew;
     any_reset |= reset;

@@ -1,4 +1,513 @@
-/* placeholder: replaced below */
+/*
+ * oracle_physics.c — dense double-precision restatement of this build's physics substep
+ * (TEST INFRASTRUCTURE ONLY). It replaces one `gym.simulate()` (legged_robot.py:82) of
+ * the closed PhysX binary; the spec is DESIGN.md "Physics" and is restated here without
+ * any of the HIP kernel's structure (no Schur complement, no lane mapping, no fp32):
+ *
+ *   state  root_states [p, q(xyzw), v_com, w] (PhysX semantics: COM linear velocity,
+ *          body-origin position), dof_state [theta, theta_dot]; u = [v_origin, w, theta_dot]
+ *   1. forward kinematics of the collapsed tree (lgx_model)
+ *   2. M(q) = sum_k J_kᵀ diag(m_k, I_k) J_k          (18x18 dense)
+ *      h(q,u) = sum_k J_kᵀ [m_k(a_k - g); I_k alpha_k + w_k x I_k w_k]
+ *   3. u* = u + dt M⁻¹ (Sᵀ tau - h)                    (dense Cholesky)
+ *   4. constraints: joint-limit rows, then per active contact (sphere candidates vs the
+ *      ground, depth > -contact_margin, first LGX_MAX_CONTACTS in candidate order)
+ *      normal + 2 tangent rows; projected Gauss-Seidel on A = J M⁻¹ Jᵀ with Baumgarte
+ *      targets, isotropic Coulomb disk, mu = (mu_env + mu_ground)/2
+ *   5. u+ = u* + M⁻¹ Jᵀ lambda; semi-implicit Euler (q ← exp(w dt) ⊗ q)
+ *   6. outputs: contact force per body = sum lambda/dt, rigid-body states.
+ * PARITY UNPINNED vs the reference (PhysX is closed and absent).
+ */
+#include <math.h>
+#include <string.h>
+
 #include "lgx_oracle.h"
-void oracle_physics_substep(const lgx_model* M, const lgx_task_params* P, lgx_buffers* B, int env) { (void)M; (void)P; (void)B; (void)env; }
-double oracle_energy(const lgx_model* M, const lgx_task_params* P, const lgx_buffers* B, int env) { (void)M; (void)P; (void)B; (void)env; return 0; }
+
+#define NU 18
+
+typedef struct {
+  int nl;
+  double R[LGX_MAX_LINKS][3][3], p[LGX_MAX_LINKS][3], ax[LGX_MAX_LINKS][3];
+  double w[LGX_MAX_LINKS][3], v[LGX_MAX_LINKS][3];      /* angular vel, origin vel */
+  double al[LGX_MAX_LINKS][3], ao[LGX_MAX_LINKS][3];    /* bias accelerations */
+  double c[LGX_MAX_LINKS][3], I[LGX_MAX_LINKS][3][3], m[LGX_MAX_LINKS];
+  int anc[LGX_MAX_LINKS][LGX_MAX_LINKS];                /* anc[k][i]: link i is k or an ancestor */
+} kin_t;
+
+static void cross(const double* a, const double* b, double* o) {
+  double t0 = a[1] * b[2] - a[2] * b[1], t1 = a[2] * b[0] - a[0] * b[2], t2 = a[0] * b[1] - a[1] * b[0];
+  o[0] = t0; o[1] = t1; o[2] = t2;
+}
+static double dot(const double* a, const double* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+static void matvec(double R[3][3], const double* x, double* o) {
+  double t[3];
+  for (int i = 0; i < 3; ++i) t[i] = R[i][0] * x[0] + R[i][1] * x[1] + R[i][2] * x[2];
+  o[0] = t[0]; o[1] = t[1]; o[2] = t[2];
+}
+static void matmul(double A[3][3], double B[3][3], double O[3][3]) {
+  double T[3][3];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) T[i][j] = A[i][0] * B[0][j] + A[i][1] * B[1][j] + A[i][2] * B[2][j];
+  memcpy(O, T, sizeof(T));
+}
+static void quat_to_R(const double* q, double R[3][3]) {
+  double x = q[0], y = q[1], z = q[2], w = q[3];
+  R[0][0] = 1 - 2 * (y * y + z * z); R[0][1] = 2 * (x * y - z * w); R[0][2] = 2 * (x * z + y * w);
+  R[1][0] = 2 * (x * y + z * w); R[1][1] = 1 - 2 * (x * x + z * z); R[1][2] = 2 * (y * z - x * w);
+  R[2][0] = 2 * (x * z - y * w); R[2][1] = 2 * (y * z + x * w); R[2][2] = 1 - 2 * (x * x + y * y);
+}
+static void axis_angle_R(const double* a, double th, double R[3][3]) {
+  double c = cos(th), s = sin(th), t = 1 - c;
+  double x = a[0], y = a[1], z = a[2];
+  R[0][0] = t * x * x + c; R[0][1] = t * x * y - s * z; R[0][2] = t * x * z + s * y;
+  R[1][0] = t * x * y + s * z; R[1][1] = t * y * y + c; R[1][2] = t * y * z - s * x;
+  R[2][0] = t * x * z - s * y; R[2][1] = t * y * z + s * x; R[2][2] = t * z * z + c;
+}
+
+/* forward kinematics + velocities + bias accelerations, base velocity = origin velocity */
+static void kinematics(const lgx_model* M, const lgx_buffers* B, int e, int D, const double* pb, const double* qb,
+                       const double* vo, const double* wb, const double* th, const double* thd, kin_t* K) {
+  (void)B; (void)e; (void)D;
+  K->nl = M->num_links;
+  memset(K->anc, 0, sizeof(K->anc));
+  for (int k = 0; k < K->nl; ++k) {
+    int par = M->link_parent[k];
+    if (par < 0) {
+      quat_to_R(qb, K->R[0]);
+      memcpy(K->p[0], pb, sizeof(double) * 3);
+      memcpy(K->w[0], wb, sizeof(double) * 3);
+      memcpy(K->v[0], vo, sizeof(double) * 3);
+      memset(K->al[0], 0, sizeof(double) * 3);
+      memset(K->ao[0], 0, sizeof(double) * 3);
+      memset(K->ax[0], 0, sizeof(double) * 3);
+      K->anc[0][0] = 1;
+    } else {
+      double Rj[3][3], Ra[3][3], o[3], a_local[3];
+      for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) Rj[i][j] = M->joint_rot[k][i * 3 + j];
+      double jo[3] = {M->joint_origin[k][0], M->joint_origin[k][1], M->joint_origin[k][2]};
+      matvec(K->R[par], jo, o);
+      for (int i = 0; i < 3; ++i) K->p[k][i] = K->p[par][i] + o[i];
+      double RpRj[3][3];
+      matmul(K->R[par], Rj, RpRj);
+      for (int i = 0; i < 3; ++i) a_local[i] = M->joint_axis[k][i];
+      axis_angle_R(a_local, th[k - 1], Ra);
+      matmul(RpRj, Ra, K->R[k]);
+      matvec(RpRj, a_local, K->ax[k]);
+      double wa[3] = {K->ax[k][0] * thd[k - 1], K->ax[k][1] * thd[k - 1], K->ax[k][2] * thd[k - 1]};
+      double t[3], t2[3];
+      for (int i = 0; i < 3; ++i) K->w[k][i] = K->w[par][i] + wa[i];
+      cross(K->w[par], o, t);
+      for (int i = 0; i < 3; ++i) K->v[k][i] = K->v[par][i] + t[i];
+      cross(K->w[par], wa, t);
+      for (int i = 0; i < 3; ++i) K->al[k][i] = K->al[par][i] + t[i];
+      cross(K->al[par], o, t);
+      cross(K->w[par], o, t2);
+      double t3[3];
+      cross(K->w[par], t2, t3);
+      for (int i = 0; i < 3; ++i) K->ao[k][i] = K->ao[par][i] + t[i] + t3[i];
+      for (int i = 0; i < K->nl; ++i) K->anc[k][i] = K->anc[par][i];
+      K->anc[k][k] = 1;
+    }
+  }
+}
+
+static void link_inertia(const lgx_model* M, const lgx_buffers* B, int e, kin_t* K) {
+  for (int k = 0; k < K->nl; ++k) {
+    double m = M->link_mass[k];
+    double cl[3] = {M->link_com[k][0], M->link_com[k][1], M->link_com[k][2]};
+    if (k == 0 && B->mass_params) { /* _process_rigid_body_props legged_robot.py:361-380 */
+      m += B->mass_params[e * 4 + 0];
+      for (int i = 0; i < 3; ++i) cl[i] += B->mass_params[e * 4 + 1 + i];
+    }
+    K->m[k] = m;
+    double rc[3];
+    matvec(K->R[k], cl, rc);
+    for (int i = 0; i < 3; ++i) K->c[k][i] = K->p[k][i] + rc[i];
+    const float* In = M->link_inertia[k];
+    double Il[3][3] = {{In[0], In[3], In[4]}, {In[3], In[1], In[5]}, {In[4], In[5], In[2]}};
+    double T[3][3], Rt[3][3];
+    matmul(K->R[k], Il, T);
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) Rt[i][j] = K->R[k][j][i];
+    matmul(T, Rt, K->I[k]);
+  }
+}
+
+/* 3x18 linear Jacobian of world point x on link k, 3x18 angular Jacobian */
+static void point_jac(const kin_t* K, int k, const double* x, double Jv[3][NU], double Jw[3][NU]) {
+  memset(Jv, 0, sizeof(double) * 3 * NU);
+  memset(Jw, 0, sizeof(double) * 3 * NU);
+  double r[3] = {x[0] - K->p[0][0], x[1] - K->p[0][1], x[2] - K->p[0][2]};
+  for (int i = 0; i < 3; ++i) {
+    Jv[i][i] = 1.0;
+    Jw[i][3 + i] = 1.0;
+    double ei[3] = {0, 0, 0}, t[3];
+    ei[i] = 1.0;
+    cross(ei, r, t); /* e_i x r */
+    for (int a = 0; a < 3; ++a) Jv[a][3 + i] = t[a];
+  }
+  for (int i = 1; i < K->nl; ++i) {
+    if (!K->anc[k][i]) continue;
+    double d[3] = {x[0] - K->p[i][0], x[1] - K->p[i][1], x[2] - K->p[i][2]}, t[3];
+    cross(K->ax[i], d, t);
+    for (int a = 0; a < 3; ++a) {
+      Jv[a][5 + i] = t[a];
+      Jw[a][5 + i] = K->ax[i][a];
+    }
+  }
+}
+
+static int cholesky(double* A, int n) {
+  for (int j = 0; j < n; ++j) {
+    double s = A[j * n + j];
+    for (int k = 0; k < j; ++k) s -= A[j * n + k] * A[j * n + k];
+    if (s <= 0) return -1;
+    A[j * n + j] = sqrt(s);
+    for (int i = j + 1; i < n; ++i) {
+      double t = A[i * n + j];
+      for (int k = 0; k < j; ++k) t -= A[i * n + k] * A[j * n + k];
+      A[i * n + j] = t / A[j * n + j];
+    }
+  }
+  return 0;
+}
+static void chol_solve(const double* L, int n, double* b) {
+  for (int i = 0; i < n; ++i) {
+    double s = b[i];
+    for (int k = 0; k < i; ++k) s -= L[i * n + k] * b[k];
+    b[i] = s / L[i * n + i];
+  }
+  for (int i = n - 1; i >= 0; --i) {
+    double s = b[i];
+    for (int k = i + 1; k < n; ++k) s -= L[k * n + i] * b[k];
+    b[i] = s / L[i * n + i];
+  }
+}
+
+static void mass_matrix_and_bias(const kin_t* K, const double* g, double* Mm, double* h) {
+  memset(Mm, 0, sizeof(double) * NU * NU);
+  memset(h, 0, sizeof(double) * NU);
+  for (int k = 0; k < K->nl; ++k) {
+    double Jv[3][NU], Jw[3][NU];
+    point_jac(K, k, K->c[k], Jv, Jw);
+    double IJw[3][NU];
+    for (int a = 0; a < 3; ++a)
+      for (int j = 0; j < NU; ++j) IJw[a][j] = K->I[k][a][0] * Jw[0][j] + K->I[k][a][1] * Jw[1][j] + K->I[k][a][2] * Jw[2][j];
+    for (int i = 0; i < NU; ++i)
+      for (int j = 0; j < NU; ++j) {
+        double s = 0;
+        for (int a = 0; a < 3; ++a) s += K->m[k] * Jv[a][i] * Jv[a][j] + Jw[a][i] * IJw[a][j];
+        Mm[i * NU + j] += s;
+      }
+    /* COM bias acceleration */
+    double r[3] = {K->c[k][0] - K->p[k][0], K->c[k][1] - K->p[k][1], K->c[k][2] - K->p[k][2]};
+    double t1[3], t2[3], t3[3], acc[3];
+    cross(K->al[k], r, t1);
+    cross(K->w[k], r, t2);
+    cross(K->w[k], t2, t3);
+    for (int a = 0; a < 3; ++a) acc[a] = K->ao[k][a] + t1[a] + t3[a];
+    double F[3], Nn[3], Iw[3], Ia[3], wIw[3];
+    for (int a = 0; a < 3; ++a) F[a] = K->m[k] * (acc[a] - g[a]);
+    matvec((double(*)[3])K->I[k], K->w[k], Iw);
+    matvec((double(*)[3])K->I[k], K->al[k], Ia);
+    cross(K->w[k], Iw, wIw);
+    for (int a = 0; a < 3; ++a) Nn[a] = Ia[a] + wIw[a];
+    for (int j = 0; j < NU; ++j) h[j] += Jv[0][j] * F[0] + Jv[1][j] * F[1] + Jv[2][j] * F[2] + Jw[0][j] * Nn[0] +
+                                       Jw[1][j] * Nn[1] + Jw[2][j] * Nn[2];
+  }
+}
+
+static double ground_height(const lgx_task_params* P, const lgx_buffers* B, double x, double y) {
+  if (P->mesh_type == LGX_MESH_PLANE || B->height_samples == NULL) return 0.0;
+  /* heightfield: bilinear interpolation of height_samples (DESIGN.md "terrain contact") */
+  double fx = (x + P->border_size) / P->horizontal_scale, fy = (y + P->border_size) / P->horizontal_scale;
+  int ix = (int)floor(fx), iy = (int)floor(fy);
+  if (ix < 0) ix = 0;
+  if (iy < 0) iy = 0;
+  if (ix > P->hf_rows - 2) ix = P->hf_rows - 2;
+  if (iy > P->hf_cols - 2) iy = P->hf_cols - 2;
+  double tx = fx - ix, ty = fy - iy;
+  if (tx < 0) tx = 0;
+  if (tx > 1) tx = 1;
+  if (ty < 0) ty = 0;
+  if (ty > 1) ty = 1;
+  const int16_t* hs = B->height_samples;
+  double h00 = hs[ix * P->hf_cols + iy], h10 = hs[(ix + 1) * P->hf_cols + iy];
+  double h01 = hs[ix * P->hf_cols + iy + 1], h11 = hs[(ix + 1) * P->hf_cols + iy + 1];
+  return P->vertical_scale * ((1 - tx) * (1 - ty) * h00 + tx * (1 - ty) * h10 + (1 - tx) * ty * h01 + tx * ty * h11);
+}
+
+typedef struct {
+  double J[NU];
+  double target;
+  int kind;     /* 0 limit/normal, 1 tangent1, 2 tangent2 */
+  int contact;  /* contact index for tangents/normal, -1 for limits */
+} row_t;
+
+static void load_state(const lgx_model* M, const lgx_task_params* P, const lgx_buffers* B, int e, double* pb,
+                       double* qb, double* vo, double* wb, double* th, double* thd, kin_t* K) {
+  const float* root = B->root_states + e * 13;
+  const int D = P->num_dof;
+  for (int i = 0; i < 3; ++i) { pb[i] = root[i]; wb[i] = root[10 + i]; }
+  double n = 0;
+  for (int i = 0; i < 4; ++i) { qb[i] = root[3 + i]; n += qb[i] * qb[i]; }
+  n = sqrt(n);
+  for (int i = 0; i < 4; ++i) qb[i] /= n;
+  for (int j = 0; j < D; ++j) { th[j] = B->dof_state[(e * D + j) * 2]; thd[j] = B->dof_state[(e * D + j) * 2 + 1]; }
+  /* COM velocity -> origin velocity: v_o = v_c - w x (R c0) */
+  double R[3][3], cl[3] = {M->link_com[0][0], M->link_com[0][1], M->link_com[0][2]}, rc[3], t[3];
+  if (B->mass_params)
+    for (int i = 0; i < 3; ++i) cl[i] += B->mass_params[e * 4 + 1 + i];
+  quat_to_R(qb, R);
+  matvec(R, cl, rc);
+  cross(wb, rc, t);
+  for (int i = 0; i < 3; ++i) vo[i] = root[7 + i] - t[i];
+  (void)K;
+}
+
+double oracle_energy(const lgx_model* M, const lgx_task_params* P, const lgx_buffers* B, int e) {
+  double pb[3], qb[4], vo[3], wb[3], th[LGX_MAX_DOF], thd[LGX_MAX_DOF];
+  static kin_t K;
+  load_state(M, P, B, e, pb, qb, vo, wb, th, thd, &K);
+  kinematics(M, B, e, P->num_dof, pb, qb, vo, wb, th, thd, &K);
+  link_inertia(M, B, e, &K);
+  double g[3] = {P->gravity[0], P->gravity[1], P->gravity[2]};
+  double E = 0;
+  for (int k = 0; k < K.nl; ++k) {
+    double r[3] = {K.c[k][0] - K.p[k][0], K.c[k][1] - K.p[k][1], K.c[k][2] - K.p[k][2]}, t[3], vc[3], Iw[3];
+    cross(K.w[k], r, t);
+    for (int a = 0; a < 3; ++a) vc[a] = K.v[k][a] + t[a];
+    matvec(K.I[k], K.w[k], Iw);
+    E += 0.5 * K.m[k] * dot(vc, vc) + 0.5 * dot(K.w[k], Iw) - K.m[k] * dot(g, K.c[k]);
+  }
+  return E;
+}
+
+void oracle_physics_substep(const lgx_model* M, const lgx_task_params* P, lgx_buffers* B, int e) {
+  const int D = P->num_dof;
+  const double dt = P->sim_dt;
+  double pb[3], qb[4], vo[3], wb[3], th[LGX_MAX_DOF], thd[LGX_MAX_DOF];
+  kin_t K;
+  load_state(M, P, B, e, pb, qb, vo, wb, th, thd, &K);
+  kinematics(M, B, e, D, pb, qb, vo, wb, th, thd, &K);
+  link_inertia(M, B, e, &K);
+  double g[3] = {P->gravity[0], P->gravity[1], P->gravity[2]};
+  double Mm[NU * NU], L[NU * NU], h[NU];
+  mass_matrix_and_bias(&K, g, Mm, h);
+  memcpy(L, Mm, sizeof(L));
+  cholesky(L, NU);
+  /* free velocity */
+  double u[NU], us[NU], acc[NU];
+  for (int i = 0; i < 3; ++i) { u[i] = vo[i]; u[3 + i] = wb[i]; }
+  for (int j = 0; j < D; ++j) u[6 + j] = thd[j];
+  for (int i = 0; i < NU; ++i) acc[i] = -h[i];
+  for (int j = 0; j < D; ++j) acc[6 + j] += B->torques[e * D + j];
+  chol_solve(L, NU, acc);
+  for (int i = 0; i < NU; ++i) us[i] = u[i] + dt * acc[i];
+
+  /* constraint rows */
+  static row_t rows[LGX_MAX_DOF * 2 + 3 * LGX_MAX_CONTACTS];
+  int nr = 0;
+  for (int j = 0; j < D; ++j) {
+    int k = j + 1;
+    if (!M->joint_has_limits[k]) continue;
+    double lo = M->joint_lower[k], hi = M->joint_upper[k];
+    if (th[j] < lo + P->limit_margin) {
+      memset(rows[nr].J, 0, sizeof(rows[nr].J));
+      rows[nr].J[6 + j] = 1.0;
+      double d = lo - th[j];
+      rows[nr].target = d; /* depth; converted below */
+      rows[nr].kind = 0; rows[nr].contact = -1; ++nr;
+    } else if (th[j] > hi - P->limit_margin) {
+      memset(rows[nr].J, 0, sizeof(rows[nr].J));
+      rows[nr].J[6 + j] = -1.0;
+      double d = th[j] - hi;
+      rows[nr].target = d;
+      rows[nr].kind = 0; rows[nr].contact = -1; ++nr;
+    }
+  }
+  int nc = 0, cbody[LGX_MAX_CONTACTS];
+  double mu_env = B->friction ? B->friction[e] : 1.0;
+  double mu = 0.5 * (mu_env + P->ground_friction);
+  for (int c = 0; c < M->num_candidates && nc < LGX_MAX_CONTACTS; ++c) {
+    int k = M->cand_link[c];
+    double s[3] = {M->cand_pos[c][0], M->cand_pos[c][1], M->cand_pos[c][2]}, xc[3];
+    matvec(K.R[k], s, xc);
+    for (int i = 0; i < 3; ++i) xc[i] += K.p[k][i];
+    double r = M->cand_radius[c];
+    double hg = ground_height(P, B, xc[0], xc[1]);
+    double d = r + hg - xc[2];
+    if (d <= -P->contact_margin) continue;
+    double x[3] = {xc[0], xc[1], xc[2] - r};
+    double Jv[3][NU], Jw[3][NU];
+    point_jac(&K, k, x, Jv, Jw);
+    const double dirs[3][3] = {{0, 0, 1}, {1, 0, 0}, {0, 1, 0}};
+    for (int t = 0; t < 3; ++t) {
+      for (int j = 0; j < NU; ++j) rows[nr].J[j] = dirs[t][0] * Jv[0][j] + dirs[t][1] * Jv[1][j] + dirs[t][2] * Jv[2][j];
+      rows[nr].target = t == 0 ? d : 0.0;
+      rows[nr].kind = t;
+      rows[nr].contact = nc;
+      ++nr;
+    }
+    cbody[nc] = M->cand_body[c];
+    ++nc;
+  }
+  /* convert depths to velocity targets (Baumgarte) */
+  for (int r = 0; r < nr; ++r) {
+    if (rows[r].kind != 0) continue;
+    double d = rows[r].target;
+    double tv;
+    if (d > P->slop) {
+      tv = P->baumgarte * (d - P->slop) / dt;
+      if (tv > P->max_depenetration_vel) tv = P->max_depenetration_vel;
+    } else if (d >= 0) {
+      tv = 0.0;
+    } else {
+      tv = d / dt;
+    }
+    rows[r].target = tv;
+  }
+  /* A = J M⁻¹ Jᵀ, b = J u* */
+  static double MiJ[LGX_MAX_DOF * 2 + 3 * LGX_MAX_CONTACTS][NU];
+  static double A[LGX_MAX_DOF * 2 + 3 * LGX_MAX_CONTACTS][LGX_MAX_DOF * 2 + 3 * LGX_MAX_CONTACTS];
+  double b[LGX_MAX_DOF * 2 + 3 * LGX_MAX_CONTACTS], lam[LGX_MAX_DOF * 2 + 3 * LGX_MAX_CONTACTS];
+  for (int r = 0; r < nr; ++r) {
+    memcpy(MiJ[r], rows[r].J, sizeof(double) * NU);
+    chol_solve(L, NU, MiJ[r]);
+    double s = 0;
+    for (int j = 0; j < NU; ++j) s += rows[r].J[j] * us[j];
+    b[r] = s;
+    lam[r] = 0.0;
+  }
+  for (int r = 0; r < nr; ++r)
+    for (int q = 0; q < nr; ++q) {
+      double s = 0;
+      for (int j = 0; j < NU; ++j) s += rows[r].J[j] * MiJ[q][j];
+      A[r][q] = s;
+    }
+  for (int it = 0; it < P->solver_iterations; ++it) {
+    for (int r = 0; r < nr; ++r) {
+      if (rows[r].kind == 0) {
+        double w = b[r];
+        for (int q = 0; q < nr; ++q) w += A[r][q] * lam[q];
+        double nl = lam[r] + (rows[r].target - w) / A[r][r];
+        lam[r] = nl > 0 ? nl : 0;
+      } else if (rows[r].kind == 1) {
+        /* tangent pair r, r+1 of contact rows[r].contact; normal at r-1 */
+        double w1 = b[r], w2 = b[r + 1];
+        for (int q = 0; q < nr; ++q) { w1 += A[r][q] * lam[q]; w2 += A[r + 1][q] * lam[q]; }
+        double l1 = lam[r] - w1 / A[r][r];
+        double l2 = lam[r + 1] - w2 / A[r + 1][r + 1];
+        double lim = mu * lam[r - 1];
+        double n = sqrt(l1 * l1 + l2 * l2);
+        if (n > lim) {
+          double s = n > 0 ? lim / n : 0;
+          l1 *= s; l2 *= s;
+        }
+        lam[r] = l1; lam[r + 1] = l2;
+      }
+    }
+  }
+  double up[NU];
+  for (int j = 0; j < NU; ++j) {
+    double s = us[j];
+    for (int r = 0; r < nr; ++r) s += MiJ[r][j] * lam[r];
+    up[j] = s;
+  }
+  /* contact forces per body (world) */
+  float* cf = B->contact_forces + (size_t)e * P->num_bodies * 3;
+  for (int i = 0; i < P->num_bodies * 3; ++i) cf[i] = 0.0f;
+  for (int r = 0; r < nr; ++r) {
+    if (rows[r].contact < 0) continue;
+    int bidx = cbody[rows[r].contact];
+    int axis = rows[r].kind == 0 ? 2 : (rows[r].kind == 1 ? 0 : 1);
+    cf[bidx * 3 + axis] += (float)(lam[r] / dt);
+  }
+  /* integrate */
+  double vn[3] = {up[0], up[1], up[2]}, wn[3] = {up[3], up[4], up[5]};
+  for (int i = 0; i < 3; ++i) pb[i] += dt * vn[i];
+  double ang = sqrt(dot(wn, wn)) * dt;
+  double dq[4];
+  if (ang > 1e-12) {
+    double s = sin(0.5 * ang) / (ang / dt);
+    dq[0] = wn[0] * s; dq[1] = wn[1] * s; dq[2] = wn[2] * s; dq[3] = cos(0.5 * ang);
+  } else {
+    dq[0] = 0.5 * dt * wn[0]; dq[1] = 0.5 * dt * wn[1]; dq[2] = 0.5 * dt * wn[2]; dq[3] = 1.0;
+  }
+  /* q' = dq ⊗ q (xyzw) */
+  double qn[4];
+  qn[3] = dq[3] * qb[3] - (dq[0] * qb[0] + dq[1] * qb[1] + dq[2] * qb[2]);
+  qn[0] = dq[3] * qb[0] + qb[3] * dq[0] + (dq[1] * qb[2] - dq[2] * qb[1]);
+  qn[1] = dq[3] * qb[1] + qb[3] * dq[1] + (dq[2] * qb[0] - dq[0] * qb[2]);
+  qn[2] = dq[3] * qb[2] + qb[3] * dq[2] + (dq[0] * qb[1] - dq[1] * qb[0]);
+  double nq = sqrt(qn[0] * qn[0] + qn[1] * qn[1] + qn[2] * qn[2] + qn[3] * qn[3]);
+  for (int i = 0; i < 4; ++i) qn[i] /= nq;
+  for (int j = 0; j < D; ++j) {
+    thd[j] = up[6 + j];
+    th[j] += dt * thd[j];
+  }
+  /* write back: root velocity = COM velocity with the new orientation */
+  float* root = B->root_states + e * 13;
+  double R[3][3], cl[3] = {M->link_com[0][0], M->link_com[0][1], M->link_com[0][2]}, rc[3], t[3];
+  if (B->mass_params)
+    for (int i = 0; i < 3; ++i) cl[i] += B->mass_params[e * 4 + 1 + i];
+  quat_to_R(qn, R);
+  matvec(R, cl, rc);
+  cross(wn, rc, t);
+  for (int i = 0; i < 3; ++i) {
+    root[i] = (float)pb[i];
+    root[7 + i] = (float)(vn[i] + t[i]);
+    root[10 + i] = (float)wn[i];
+  }
+  for (int i = 0; i < 4; ++i) root[3 + i] = (float)qn[i];
+  for (int j = 0; j < D; ++j) {
+    B->dof_state[(e * D + j) * 2] = (float)th[j];
+    B->dof_state[(e * D + j) * 2 + 1] = (float)thd[j];
+  }
+  /* rigid body states at the new configuration */
+  kinematics(M, B, e, D, pb, qn, vn, wn, th, thd, &K);
+  link_inertia(M, B, e, &K);
+  for (int bi = 0; bi < M->num_bodies; ++bi) {
+    int k = M->body_link[bi];
+    double off[3] = {M->body_offset[bi][0], M->body_offset[bi][1], M->body_offset[bi][2]}, o[3], tv[3];
+    matvec(K.R[k], off, o);
+    float* rb = B->rigid_body_states + ((size_t)e * P->num_bodies + bi) * 13;
+    double Rb[3][3], Ro[3][3];
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) Ro[i][j] = M->body_rot[bi][i * 3 + j];
+    matmul(K.R[k], Ro, Rb);
+    /* rotation -> quaternion (xyzw) */
+    double tr = Rb[0][0] + Rb[1][1] + Rb[2][2], qq[4];
+    if (tr > 0) {
+      double s = sqrt(tr + 1.0) * 2;
+      qq[3] = 0.25 * s; qq[0] = (Rb[2][1] - Rb[1][2]) / s; qq[1] = (Rb[0][2] - Rb[2][0]) / s; qq[2] = (Rb[1][0] - Rb[0][1]) / s;
+    } else if (Rb[0][0] > Rb[1][1] && Rb[0][0] > Rb[2][2]) {
+      double s = sqrt(1.0 + Rb[0][0] - Rb[1][1] - Rb[2][2]) * 2;
+      qq[3] = (Rb[2][1] - Rb[1][2]) / s; qq[0] = 0.25 * s; qq[1] = (Rb[0][1] + Rb[1][0]) / s; qq[2] = (Rb[0][2] + Rb[2][0]) / s;
+    } else if (Rb[1][1] > Rb[2][2]) {
+      double s = sqrt(1.0 + Rb[1][1] - Rb[0][0] - Rb[2][2]) * 2;
+      qq[3] = (Rb[0][2] - Rb[2][0]) / s; qq[0] = (Rb[0][1] + Rb[1][0]) / s; qq[1] = 0.25 * s; qq[2] = (Rb[1][2] + Rb[2][1]) / s;
+    } else {
+      double s = sqrt(1.0 + Rb[2][2] - Rb[0][0] - Rb[1][1]) * 2;
+      qq[3] = (Rb[1][0] - Rb[0][1]) / s; qq[0] = (Rb[0][2] + Rb[2][0]) / s; qq[1] = (Rb[1][2] + Rb[2][1]) / s; qq[2] = 0.25 * s;
+    }
+    if (qq[3] < 0) for (int i = 0; i < 4; ++i) qq[i] = -qq[i];
+    /* linear velocity: the link COM for a link's own body (offset 0), else the body origin */
+    int primary = off[0] == 0.0 && off[1] == 0.0 && off[2] == 0.0;
+    double vp[3];
+    if (primary) {
+      double rcw[3] = {K.c[k][0] - K.p[k][0], K.c[k][1] - K.p[k][1], K.c[k][2] - K.p[k][2]};
+      cross(K.w[k], rcw, tv);
+    } else {
+      cross(K.w[k], o, tv);
+    }
+    for (int i = 0; i < 3; ++i) vp[i] = K.v[k][i] + tv[i];
+    for (int i = 0; i < 3; ++i) {
+      rb[i] = (float)(K.p[k][i] + o[i]);
+      rb[7 + i] = (float)vp[i];
+      rb[10 + i] = (float)K.w[k][i];
+    }
+    for (int i = 0; i < 4; ++i) rb[3 + i] = (float)qq[i];
+  }
+}

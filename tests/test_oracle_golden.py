@@ -89,7 +89,7 @@ def test_oracle_replays_reference_steps(fixture):
             ("priv", a["priv"], S("out.privileged_obs_buf")),
             ("est", a["est"], S("out.estimated_obs_buf")),
             ("scan", a["scan"], S("out.scan_obs_buf")),
-            ("episode_sums", a["episode_sums"][:K], S("out.episode_sums")),
+            ("episode_sums", a["episode_sums"][:, :K].T, S("out.episode_sums")),
             ("roll", a["rpy_phase"][:, 0], S("out.roll")),
             ("pitch", a["rpy_phase"][:, 1], S("out.pitch")),
             ("episode_length", a["episode_length"], S("out.state_out.episode_length_buf")),
