@@ -89,6 +89,9 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
     dev = f"cuda:{local}"
+    # the reference's own training precision (legged_gym/scripts/train.py:39): fp32
+    # storage, hipBLASLt's reduced-precision fp32 GEMM path allowed
+    torch.set_float32_matmul_precision("high")
 
     from legged_gym_custom_amd import _abi
     from legged_gym_custom_amd.envs import task_registry

@@ -6,7 +6,7 @@ import os
 
 from . import _abi
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "liblgx.so")
+LIB_PATH = os.environ.get("LGX_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "liblgx.so")
 _lib = None
 
 

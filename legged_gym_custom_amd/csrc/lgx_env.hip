@@ -35,7 +35,23 @@ constexpr int MAXHIST = 1216;
 
 enum Slot { S_CMD = 0, S_PUSH = 4, S_TERR = 6, S_DOF = 8, S_ROOT_XY = 20, S_ROOT_VEL = 24, S_RCMD = 32, S_NOISE = 36 };
 
+struct Scratch {  // per-env post-physics scalars (go2.py:357-367, 279-328)
+  float blv[3], bav[3], pg[3];
+  float roll, pitch, yaw;
+  float ph[4];  // fl fr bl br
+  int contact[4];
+  float feet_z[4];
+  float jump;
+};
+
 struct Sh {
+  // --- post-physics per-env scalars (written by lane 0, read by all lanes)
+  Scratch x;
+  float root[13], cmd[4], fat[4], lch[4];
+  int lc[4];
+  float rterm[64];
+  long long ep;
+  int reset, tout;
   // --- physics state (base velocity kept as the ORIGIN velocity inside the step)
   float qb[4], pb[3], vo[3], wb[3];
   float th[NJ], thd[NJ], tau[NJ], act[NJ], kpm[NJ], kdm[NJ], ldv[NJ];
@@ -43,7 +59,10 @@ struct Sh {
   // --- kinematics per dynamic link
   float R[NL][9], P[NL][3], Ax[NL][3], W[NL][3], V[NL][3], Al[NL][3], Ao[NL][3], C[NL][3], I[NL][6], m[NL];
   // --- dynamics
-  float red[5][16];  // partial sums: m, h(3), Ip(6), F(3), N(3) per leg + base
+  float red[NL][16];  // per-link partials about p0: m, h(3), Ip(6), F(3), N(3)
+  float tot[16];
+  float Fw[NL][3], Nw[NL][3];  // per-link COM wrench (bias)
+  float Dl[4][6];
   float Bc[NJ][6], Dinv[4][6], X[NJ][6], S[4][21], L[21], hj[NJ], hb[6], us[NU], up[NU];
   // --- constraints
   float J[MAXR][NU], MJ[MAXR][NU], Arr[MAXR], tgt[MAXR], lam[MAXR];
@@ -84,21 +103,22 @@ LGX_DEV float sym3(const float* S, int i, int j) {
 LGX_DEV int pk(int i, int j) { return i >= j ? i * (i + 1) / 2 + j : j * (j + 1) / 2 + i; }
 
 // x = M⁻¹ b for one right-hand side, by the base Schur complement (one lane).
-LGX_DEV void mass_solve(const Sh& s, const float* b, float* x) {
-  float y[6];
-#pragma unroll
-  for (int r = 0; r < 6; ++r) y[r] = b[r];
-#pragma unroll
+// Loops over joints/legs are deliberately NOT unrolled: unrolled, the compiler hoists
+// all ~190 LDS operands into VGPRs and the kernel drops to one wave per SIMD.
+LGX_DEV void mass_solve(const Sh& s, const float* b, float* x) {  // b may alias x
+  float y0 = b[0], y1 = b[1], y2 = b[2], y3 = b[3], y4 = b[4], y5 = b[5];
+#pragma unroll 1
   for (int j = 0; j < NJ; ++j) {
-    float bj = b[6 + j];
-#pragma unroll
-    for (int r = 0; r < 6; ++r) y[r] -= s.X[j][r] * bj;
+    const float bj = b[6 + j];
+    const float* Xj = s.X[j];
+    y0 -= Xj[0] * bj; y1 -= Xj[1] * bj; y2 -= Xj[2] * bj;
+    y3 -= Xj[3] * bj; y4 -= Xj[4] * bj; y5 -= Xj[5] * bj;
   }
-  // L Lᵀ xb = y
-  float z[6];
+  // L Lᵀ z = y (packed lower Cholesky factor)
+  float z[6] = {y0, y1, y2, y3, y4, y5};
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
-    float t = y[i];
+    float t = z[i];
 #pragma unroll
     for (int k = 0; k < i; ++k) t -= s.L[pk(i, k)] * z[k];
     z[i] = t / s.L[pk(i, i)];
@@ -112,24 +132,19 @@ LGX_DEV void mass_solve(const Sh& s, const float* b, float* x) {
   }
 #pragma unroll
   for (int r = 0; r < 6; ++r) x[r] = z[r];
-#pragma unroll
+#pragma unroll 1
   for (int l = 0; l < 4; ++l) {
     float rhs[3];
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
-      int j = 3 * l + a;
-      float t = b[6 + j];
-#pragma unroll
-      for (int r = 0; r < 6; ++r) t -= s.Bc[j][r] * z[r];
-      rhs[a] = t;
+      const int j = 3 * l + a;
+      const float* Bj = s.Bc[j];
+      rhs[a] = b[6 + j] - (Bj[0] * z[0] + Bj[1] * z[1] + Bj[2] * z[2] + Bj[3] * z[3] + Bj[4] * z[4] + Bj[5] * z[5]);
     }
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-      float t = 0.f;
-#pragma unroll
-      for (int c = 0; c < 3; ++c) t += sym3(s.Dinv[l], a, c) * rhs[c];
-      x[6 + 3 * l + a] = t;
-    }
+    const float* Di = s.Dinv[l];
+    x[6 + 3 * l + 0] = Di[0] * rhs[0] + Di[3] * rhs[1] + Di[4] * rhs[2];
+    x[6 + 3 * l + 1] = Di[3] * rhs[0] + Di[1] * rhs[1] + Di[5] * rhs[2];
+    x[6 + 3 * l + 2] = Di[4] * rhs[0] + Di[5] * rhs[1] + Di[2] * rhs[2];
   }
 }
 
@@ -150,7 +165,7 @@ LGX_DEV void kinematics(Sh& s, const lgx_model* M, int lane) {
   __syncthreads();
   if (lane < 4) {
     int par = 0;
-#pragma unroll
+#pragma unroll 1
     for (int i = 0; i < 3; ++i) {
       const int k = 1 + 3 * lane + i;
       const float* Rp = s.R[par];
@@ -194,160 +209,123 @@ LGX_DEV void kinematics(Sh& s, const lgx_model* M, int lane) {
   __syncthreads();
 }
 
-// composite-inertia mass-matrix blocks, bias forces and the base Schur complement
-LGX_DEV void dynamics(Sh& s, const lgx_task_params* Pm, int lane) {
+// composite-inertia mass-matrix blocks, bias forces and the base Schur complement.
+// Spread over lanes so that no lane holds more than one link/joint/entry worth of state:
+//   D1 lanes 0..12  per-link COM wrench (F, N) and base partials about p0
+//   D2 lanes 0..11  joint bias h_j and coupling column B_j;  lanes 16..39  leg block D
+//   D3 lanes 0..3   D_l⁻¹, X_l = B_l D_l⁻¹, Schur term X_l B_lᵀ;  lane 4  base sums
+//   D4 lane 0       S = A_bb - Σ X_l B_lᵀ and its Cholesky factor
+__device__ __noinline__ void dynamics(Sh& s, const lgx_task_params* Pm, int lane) {
   const f3 g = ld3(Pm->gravity);
   const f3 p0 = ld3(s.P[0]);
-  if (lane < 4) {
-    const int k0 = 1 + 3 * lane;
-    f3 F[3], N[3], c[3], a[3], pj[3];
-    float mk_[3];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      const int k = k0 + i;
-      c[i] = ld3(s.C[k]); a[i] = ld3(s.Ax[k]); pj[i] = ld3(s.P[k]); mk_[i] = s.m[k];
-      f3 r = c[i] - pj[i], w = ld3(s.W[k]), al = ld3(s.Al[k]);
-      f3 acc = ld3(s.Ao[k]) + cross(al, r) + cross(w, cross(w, r));
-      F[i] = (acc - g) * mk_[i];
-      N[i] = symv(s.I[k], al) + cross(w, symv(s.I[k], w));
-    }
-    // joint bias
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      f3 acc = mk(0, 0, 0);
-#pragma unroll
-      for (int i = j; i < 3; ++i) acc = acc + cross(c[i] - pj[j], F[i]) + N[i];
-      s.hj[3 * lane + j] = dot(a[j], acc);
-    }
-    // base partials about p0
-    float msum = 0.f;
-    f3 hs = mk(0, 0, 0), Fs = mk(0, 0, 0), Ns = mk(0, 0, 0);
-    float Ip[6] = {0, 0, 0, 0, 0, 0};
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      const int k = k0 + i;
-      f3 r = c[i] - p0;
-      msum += mk_[i];
-      hs = hs + r * mk_[i];
-      Fs = Fs + F[i];
-      Ns = Ns + cross(r, F[i]) + N[i];
-      float rr = dot(r, r);
-      Ip[0] += s.I[k][0] + mk_[i] * (rr - r.x * r.x);
-      Ip[1] += s.I[k][1] + mk_[i] * (rr - r.y * r.y);
-      Ip[2] += s.I[k][2] + mk_[i] * (rr - r.z * r.z);
-      Ip[3] += s.I[k][3] - mk_[i] * r.x * r.y;
-      Ip[4] += s.I[k][4] - mk_[i] * r.x * r.z;
-      Ip[5] += s.I[k][5] - mk_[i] * r.y * r.z;
-    }
-    float* rd = s.red[lane];
-    rd[0] = msum; rd[1] = hs.x; rd[2] = hs.y; rd[3] = hs.z;
-#pragma unroll
-    for (int q = 0; q < 6; ++q) rd[4 + q] = Ip[q];
-    rd[10] = Fs.x; rd[11] = Fs.y; rd[12] = Fs.z; rd[13] = Ns.x; rd[14] = Ns.y; rd[15] = Ns.z;
-    // coupling columns B (6 x 3) and leg block D (3 x 3)
-    float Bl[3][6];
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      f3 hl = mk(0, 0, 0), bang = mk(0, 0, 0);
-#pragma unroll
-      for (int i = j; i < 3; ++i) {
-        f3 d = c[i] - pj[j];
-        hl = hl + d * mk_[i];
-        bang = bang + cross(c[i] - p0, cross(a[j], d)) * mk_[i] + symv(s.I[k0 + i], a[j]);
-      }
-      f3 blin = cross(a[j], hl);
-      Bl[j][0] = blin.x; Bl[j][1] = blin.y; Bl[j][2] = blin.z;
-      Bl[j][3] = bang.x; Bl[j][4] = bang.y; Bl[j][5] = bang.z;
-#pragma unroll
-      for (int r = 0; r < 6; ++r) s.Bc[3 * lane + j][r] = Bl[j][r];
-    }
-    float Dl[6];
-    int idx[6][2] = {{0, 0}, {1, 1}, {2, 2}, {0, 1}, {0, 2}, {1, 2}};
-#pragma unroll
-    for (int q = 0; q < 6; ++q) {
-      const int j1 = idx[q][0], j2 = idx[q][1];
-      float acc = 0.f;
-#pragma unroll
-      for (int i = j2; i < 3; ++i) {
-        acc += mk_[i] * dot(cross(a[j1], c[i] - pj[j1]), cross(a[j2], c[i] - pj[j2])) +
-               dot(a[j1], symv(s.I[k0 + i], a[j2]));
-      }
-      Dl[q] = acc;
-    }
-    float Di[6];
-    sym3_inv(Dl, Di);
-#pragma unroll
-    for (int q = 0; q < 6; ++q) s.Dinv[lane][q] = Di[q];
-    float Xl[3][6];
-#pragma unroll
-    for (int j = 0; j < 3; ++j)
-#pragma unroll
-      for (int r = 0; r < 6; ++r) {
-        float t = 0.f;
-#pragma unroll
-        for (int i = 0; i < 3; ++i) t += Bl[i][r] * sym3(Di, i, j);
-        Xl[j][r] = t;
-        s.X[3 * lane + j][r] = t;
-      }
-#pragma unroll
-    for (int r = 0; r < 6; ++r)
-#pragma unroll
-      for (int q = 0; q <= r; ++q) {
-        float t = 0.f;
-#pragma unroll
-        for (int j = 0; j < 3; ++j) t += Xl[j][r] * Bl[j][q];
-        s.S[lane][pk(r, q)] = t;
-      }
-  } else if (lane == 4) {
-    // base link partials (bias acceleration of the base COM: w x (w x r))
-    f3 c0 = ld3(s.C[0]), w = ld3(s.W[0]);
-    f3 r = c0 - p0;
-    float m0 = s.m[0];
-    f3 acc = cross(w, cross(w, r));
-    f3 F = (acc - g) * m0;
-    f3 N = cross(w, symv(s.I[0], w));
-    float* rd = s.red[4];
+  if (lane < NL) {  // ---- D1
+    const int k = lane;
+    f3 c = ld3(s.C[k]), w = ld3(s.W[k]), al = ld3(s.Al[k]);
+    f3 rl = c - ld3(s.P[k]);
+    f3 acc = ld3(s.Ao[k]) + cross(al, rl) + cross(w, cross(w, rl));
+    const float m = s.m[k];
+    f3 F = (acc - g) * m;
+    f3 N = symv(s.I[k], al) + cross(w, symv(s.I[k], w));
+    st3(s.Fw[k], F);
+    st3(s.Nw[k], N);
+    f3 r = c - p0;
     float rr = dot(r, r);
-    rd[0] = m0; rd[1] = m0 * r.x; rd[2] = m0 * r.y; rd[3] = m0 * r.z;
-    rd[4] = s.I[0][0] + m0 * (rr - r.x * r.x);
-    rd[5] = s.I[0][1] + m0 * (rr - r.y * r.y);
-    rd[6] = s.I[0][2] + m0 * (rr - r.z * r.z);
-    rd[7] = s.I[0][3] - m0 * r.x * r.y;
-    rd[8] = s.I[0][4] - m0 * r.x * r.z;
-    rd[9] = s.I[0][5] - m0 * r.y * r.z;
+    float* rd = s.red[k];
+    rd[0] = m; rd[1] = m * r.x; rd[2] = m * r.y; rd[3] = m * r.z;
+    rd[4] = s.I[k][0] + m * (rr - r.x * r.x);
+    rd[5] = s.I[k][1] + m * (rr - r.y * r.y);
+    rd[6] = s.I[k][2] + m * (rr - r.z * r.z);
+    rd[7] = s.I[k][3] - m * r.x * r.y;
+    rd[8] = s.I[k][4] - m * r.x * r.z;
+    rd[9] = s.I[k][5] - m * r.y * r.z;
     f3 Nt = cross(r, F) + N;
     rd[10] = F.x; rd[11] = F.y; rd[12] = F.z; rd[13] = Nt.x; rd[14] = Nt.y; rd[15] = Nt.z;
   }
   __syncthreads();
-  if (lane == 0) {
-    float t[16];
+  if (lane < NJ) {  // ---- D2a: joint j (leg l, chain position a)
+    const int j = lane, l = j / 3, a = j % 3;
+    const int kj = 1 + j;
+    const f3 ax = ld3(s.Ax[kj]), pj = ld3(s.P[kj]);
+    f3 acc = mk(0, 0, 0), hl = mk(0, 0, 0), bang = mk(0, 0, 0);
+#pragma unroll 1
+    for (int i = a; i < 3; ++i) {
+      const int k = 1 + 3 * l + i;
+      const f3 c = ld3(s.C[k]);
+      const f3 d = c - pj;
+      const float m = s.m[k];
+      acc = acc + cross(d, ld3(s.Fw[k])) + ld3(s.Nw[k]);
+      hl = hl + d * m;
+      bang = bang + cross(c - p0, cross(ax, d)) * m + symv(s.I[k], ax);
+    }
+    s.hj[j] = dot(ax, acc);
+    f3 blin = cross(ax, hl);
+    float* Bj = s.Bc[j];
+    Bj[0] = blin.x; Bj[1] = blin.y; Bj[2] = blin.z; Bj[3] = bang.x; Bj[4] = bang.y; Bj[5] = bang.z;
+  } else if (lane >= 16 && lane < 40) {  // ---- D2b: leg block entry (xx yy zz xy xz yz)
+    const int q = lane - 16, l = q / 6, e = q % 6;
+    const int j1 = e < 3 ? e : (e == 5 ? 1 : 0);
+    const int j2 = e < 3 ? e : (e == 3 ? 1 : 2);
+    const int k1 = 1 + 3 * l + j1, k2 = 1 + 3 * l + j2;
+    const f3 a1 = ld3(s.Ax[k1]), a2 = ld3(s.Ax[k2]), p1 = ld3(s.P[k1]), p2 = ld3(s.P[k2]);
+    float acc = 0.f;
+#pragma unroll 1
+    for (int i = j2; i < 3; ++i) {
+      const int k = 1 + 3 * l + i;
+      const f3 c = ld3(s.C[k]);
+      acc += s.m[k] * dot(cross(a1, c - p1), cross(a2, c - p2)) + dot(a1, symv(s.I[k], a2));
+    }
+    s.Dl[l][e] = acc;
+  }
+  __syncthreads();
+  if (lane < 4) {  // ---- D3: leg l (operands streamed from LDS, not held in VGPRs)
+    const int l = lane;
+    float Di[6];
+    sym3_inv(s.Dl[l], Di);
 #pragma unroll
-    for (int q = 0; q < 16; ++q) t[q] = s.red[0][q] + s.red[1][q] + s.red[2][q] + s.red[3][q] + s.red[4][q];
-    float A[21];
-    float Mt = t[0];
-    f3 H = mk(t[1], t[2], t[3]);
+    for (int q = 0; q < 6; ++q) s.Dinv[l][q] = Di[q];
+#pragma unroll 1
+    for (int r = 0; r < 6; ++r) {
+      const float b0 = s.Bc[3 * l][r], b1 = s.Bc[3 * l + 1][r], b2 = s.Bc[3 * l + 2][r];
+      s.X[3 * l + 0][r] = b0 * Di[0] + b1 * Di[3] + b2 * Di[4];
+      s.X[3 * l + 1][r] = b0 * Di[3] + b1 * Di[1] + b2 * Di[5];
+      s.X[3 * l + 2][r] = b0 * Di[4] + b1 * Di[5] + b2 * Di[2];
+    }
+#pragma unroll 1
+    for (int r = 0; r < 6; ++r) {
+      const float x0 = s.X[3 * l][r], x1 = s.X[3 * l + 1][r], x2 = s.X[3 * l + 2][r];
+#pragma unroll 1
+      for (int q = 0; q <= r; ++q)
+        s.S[l][pk(r, q)] = x0 * s.Bc[3 * l][q] + x1 * s.Bc[3 * l + 1][q] + x2 * s.Bc[3 * l + 2][q];
+    }
+  } else if (lane >= 16 && lane < 32) {  // base sums over the 13 links, one quantity per lane
+    const int q = lane - 16;
+    float t = 0.f;
+#pragma unroll 1
+    for (int k = 0; k < NL; ++k) t += s.red[k][q];
+    s.tot[q] = t;
+  }
+  __syncthreads();
+  if (lane == 0) {  // ---- D4: A_bb - Σ S_l into s.L, then in-place packed Cholesky
+    const float* t = s.tot;
+    float* L = s.L;
+    const float Mt = t[0], Hx = t[1], Hy = t[2], Hz = t[3];
     // A = [[M I, -[H]x], [[H]x, Ip]]  (generalized velocity = base origin velocity, w)
-    for (int q = 0; q < 21; ++q) A[q] = 0.f;
-    A[pk(0, 0)] = Mt; A[pk(1, 1)] = Mt; A[pk(2, 2)] = Mt;
     // lower block rows 3..5 (w), cols 0..2 (v) = [H]x = [[0,-Hz,Hy],[Hz,0,-Hx],[-Hy,Hx,0]]
-    A[pk(3, 0)] = 0.f;   A[pk(3, 1)] = -H.z; A[pk(3, 2)] = H.y;
-    A[pk(4, 0)] = H.z;   A[pk(4, 1)] = 0.f;  A[pk(4, 2)] = -H.x;
-    A[pk(5, 0)] = -H.y;  A[pk(5, 1)] = H.x;  A[pk(5, 2)] = 0.f;
-    A[pk(3, 3)] = t[4]; A[pk(4, 4)] = t[5]; A[pk(5, 5)] = t[6];
-    A[pk(4, 3)] = t[7]; A[pk(5, 3)] = t[8]; A[pk(5, 4)] = t[9];
-#pragma unroll
-    for (int q = 0; q < 21; ++q) A[q] -= s.S[0][q] + s.S[1][q] + s.S[2][q] + s.S[3][q];
-    // Cholesky (packed)
+    const float A[21] = {Mt, 0.f, Mt, 0.f, 0.f, Mt, 0.f, -Hz, Hy, t[4], Hz, 0.f, -Hx, t[7], t[5],
+                         -Hy, Hx, 0.f, t[8], t[9], t[6]};
+#pragma unroll 1
+    for (int q = 0; q < 21; ++q) L[q] = A[q] - (s.S[0][q] + s.S[1][q] + s.S[2][q] + s.S[3][q]);
+#pragma unroll 1
     for (int j = 0; j < 6; ++j) {
-      float d = A[pk(j, j)];
-      for (int k = 0; k < j; ++k) d -= s.L[pk(j, k)] * s.L[pk(j, k)];
-      float ljj = sqrtf(fmaxf(d, 1e-12f));
-      s.L[pk(j, j)] = ljj;
-      float inv = 1.0f / ljj;
+      float d = L[pk(j, j)];
+      for (int k = 0; k < j; ++k) d -= L[pk(j, k)] * L[pk(j, k)];
+      const float ljj = sqrtf(fmaxf(d, 1e-12f));
+      L[pk(j, j)] = ljj;
+      const float inv = 1.0f / ljj;
       for (int i = j + 1; i < 6; ++i) {
-        float v = A[pk(i, j)];
-        for (int k = 0; k < j; ++k) v -= s.L[pk(i, k)] * s.L[pk(j, k)];
-        s.L[pk(i, j)] = v * inv;
+        float v = L[pk(i, j)];
+        for (int k = 0; k < j; ++k) v -= L[pk(i, k)] * L[pk(j, k)];
+        L[pk(i, j)] = v * inv;
       }
     }
 #pragma unroll
@@ -395,19 +373,23 @@ LGX_DEV void substep(Sh& s, const lgx_model* M, const lgx_task_params* Pm, const
     }
   }
   kinematics(s, M, lane);
+#if defined(LGX_DBG_STAGE) && LGX_DBG_STAGE == 1
+  return;
+#endif
   dynamics(s, Pm, lane);
-  // ---- free velocity u* = u + dt M⁻¹ (Sᵀτ - h)
-  if (lane == 0) {
-    float b[NU], x[NU];
-#pragma unroll
-    for (int i = 0; i < 6; ++i) b[i] = -s.hb[i];
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) b[6 + j] = s.tau[j] - s.hj[j];
-    mass_solve(s, b, x);
-#pragma unroll
-    for (int i = 0; i < 3; ++i) { s.us[i] = s.vo[i] + dt * x[i]; s.us[3 + i] = s.wb[i] + dt * x[3 + i]; }
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) s.us[6 + j] = s.thd[j] + dt * x[6 + j];
+#if defined(LGX_DBG_STAGE) && LGX_DBG_STAGE == 2
+  return;
+#endif
+  // ---- free velocity u* = u + dt M⁻¹ (Sᵀτ - h): rhs assembled lane-parallel, solved in
+  //      place in LDS by lane 0, then scaled lane-parallel
+  if (lane < 6) s.us[lane] = -s.hb[lane];
+  else if (lane < NU) s.us[lane] = s.tau[lane - 6] - s.hj[lane - 6];
+  __syncthreads();
+  if (lane == 0) mass_solve(s, s.us, s.us);
+  __syncthreads();
+  if (lane < NU) {
+    const float u0 = lane < 3 ? s.vo[lane] : (lane < 6 ? s.wb[lane - 3] : s.thd[lane - 6]);
+    s.us[lane] = u0 + dt * s.us[lane];
   }
   // ---- constraint detection: joint limits (lanes 0..11), contacts (one candidate per lane)
   bool lim_lo = false, lim_hi = false;
@@ -457,14 +439,14 @@ LGX_DEV void substep(Sh& s, const lgx_model* M, const lgx_task_params* Pm, const
     const f3 dirs[3] = {mk(0, 0, 1), mk(1, 0, 0), mk(0, 1, 0)};
     const int leg = ck > 0 ? (ck - 1) / 3 : -1;
     const int pos = ck > 0 ? (ck - 1) % 3 : -1;
-#pragma unroll
+#pragma unroll 1
     for (int t = 0; t < 3; ++t) {
       const int r = r0 + t;
       const f3 d = dirs[t];
       f3 ang = cross(xc - p0, d);
       s.J[r][0] = d.x; s.J[r][1] = d.y; s.J[r][2] = d.z;
       s.J[r][3] = ang.x; s.J[r][4] = ang.y; s.J[r][5] = ang.z;
-#pragma unroll
+#pragma unroll 4
       for (int q = 0; q < NJ; ++q) s.J[r][6 + q] = 0.f;
       for (int i = 0; i <= pos; ++i) {
         const int ki = 1 + 3 * leg + i;
@@ -477,17 +459,22 @@ LGX_DEV void substep(Sh& s, const lgx_model* M, const lgx_task_params* Pm, const
   }
   if (lane == 0) { s.nrows = nrows; s.nlim = nlim; s.ncon = ncon; }
   __syncthreads();
+#if defined(LGX_DBG_STAGE) && LGX_DBG_STAGE == 3
+  return;
+#endif
   // ---- per-row M⁻¹Jᵀ column and diagonal of A = J M⁻¹ Jᵀ (one lane per row)
   if (lane < nrows) {
-    float x[NU];
-    mass_solve(s, s.J[lane], x);
+    mass_solve(s, s.J[lane], s.MJ[lane]);
     float a = 0.f;
-#pragma unroll
-    for (int q = 0; q < NU; ++q) { s.MJ[lane][q] = x[q]; a += s.J[lane][q] * x[q]; }
+#pragma unroll 1
+    for (int q = 0; q < NU; ++q) a += s.J[lane][q] * s.MJ[lane][q];
     s.Arr[lane] = a;
     s.lam[lane] = 0.f;
   }
   __syncthreads();
+#if defined(LGX_DBG_STAGE) && LGX_DBG_STAGE == 4
+  return;
+#endif
   // ---- projected Gauss-Seidel, generalized velocity spread over lanes 0..17
   float uc = lane < NU ? s.us[lane] : 0.f;
   const float mu = s.mu;
@@ -608,15 +595,6 @@ LGX_DEV float rand_range(float lo, float hi, float u) {
   return span * u + lo;
 }
 
-struct Scratch {
-  float blv[3], bav[3], pg[3];
-  float roll, pitch, yaw;
-  float ph[4];  // fl fr bl br
-  int contact[4];
-  float feet_z[4];
-  float jump;
-};
-
 // Go2Robot._resample_commands go2.py:413-464 / LeggedRobot legged_robot.py:406-437
 LGX_DEV void resample_commands(const lgx_task_params* Pm, float* cmd, const float* U, int slot0, const float* quat) {
   if (Pm->has_user_command) {
@@ -647,50 +625,53 @@ LGX_DEV void resample_commands(const lgx_task_params* Pm, float* cmd, const floa
   }
 }
 
-// reset_idx for one env (go2.py:207-263 / legged_robot.py:157-213), lane-parallel writes.
-// root/dof/commands are in LDS (s) or in `root`, `dof`, `cmd` register copies by the caller.
-LGX_DEV void reset_env(const lgx_task_params* Pm, const lgx_buffers& B, int e, int lane, const float* U,
-                       float* root, float* th, float* thd, float* cmd, int64_t& ep, bool after_init,
+// reset_idx for one env (go2.py:207-263 / legged_robot.py:157-213). The env's root/dof/
+// command state is in LDS (s.root, s.th, s.thd, s.cmd, s.ep): lane 0 does the scalar part,
+// lanes write the per-env buffer rows. Called under a uniform branch.
+LGX_DEV void reset_env(const lgx_task_params* Pm, const lgx_buffers& B, Sh& s, int e, int lane, bool after_init,
                        bool zero_carried) {
   const int D = Pm->num_dof;
-  // terrain curriculum legged_robot.py:543-574
-  if (Pm->curriculum && after_init && B.terrain_levels) {
-    float dx = root[0] - B.env_origins[e * 3 + 0], dy = root[1] - B.env_origins[e * 3 + 1];
-    float dist = nrm2(dx, dy);
-    int up = dist > Pm->terrain_length * Pm->promote_threshold;
-    float expct = nrm2(cmd[0], cmd[1]) * Pm->max_episode_length_s;
-    int down = dist < expct * Pm->demote_threshold;
-    int64_t lvl = B.terrain_levels[e] + up - down;
-    if (lvl >= Pm->max_terrain_level) {
-      lvl = (int64_t)(U[S_TERR] * (float)Pm->max_terrain_level);
-      if (lvl >= Pm->max_terrain_level) lvl = Pm->max_terrain_level - 1;
-    } else if (lvl < 0) {
-      lvl = 0;
-    }
-    __syncthreads();
-    if (lane == 0) {
+  const float* U = s.U;
+  if (lane == 0) {
+    float* root = s.root;
+    float* cmd = s.cmd;
+    // terrain curriculum legged_robot.py:543-574
+    if (Pm->curriculum && after_init && B.terrain_levels) {
+      float dx = root[0] - B.env_origins[e * 3 + 0], dy = root[1] - B.env_origins[e * 3 + 1];
+      float dist = nrm2(dx, dy);
+      int up = dist > Pm->terrain_length * Pm->promote_threshold;
+      float expct = nrm2(cmd[0], cmd[1]) * Pm->max_episode_length_s;
+      int down = dist < expct * Pm->demote_threshold;
+      int64_t lvl = B.terrain_levels[e] + up - down;
+      if (lvl >= Pm->max_terrain_level) {
+        lvl = (int64_t)(U[S_TERR] * (float)Pm->max_terrain_level);
+        if (lvl >= Pm->max_terrain_level) lvl = Pm->max_terrain_level - 1;
+      } else if (lvl < 0) {
+        lvl = 0;
+      }
       B.terrain_levels[e] = lvl;
       const float* o = B.terrain_origins + ((size_t)lvl * Pm->num_terrain_cols + B.terrain_types[e]) * 3;
       for (int i = 0; i < 3; ++i) B.env_origins[e * 3 + i] = o[i];
     }
-    __syncthreads();
+    // _reset_root_states legged_robot.py:509-532
+    for (int i = 0; i < 13; ++i) root[i] = Pm->base_init_state[i];
+    for (int i = 0; i < 3; ++i) root[i] = root[i] + B.env_origins[e * 3 + i];
+    if (Pm->custom_origins) {
+      root[0] = root[0] + rand_range(-1.0f, 1.0f, U[S_ROOT_XY + 0]);
+      root[1] = root[1] + rand_range(-1.0f, 1.0f, U[S_ROOT_XY + 1]);
+    }
+    for (int i = 0; i < 6; ++i) root[7 + i] = rand_range(-0.5f, 0.5f, U[S_ROOT_VEL + i]);
+    resample_commands(Pm, cmd, U, S_RCMD, root + 3);
+    s.ep = 0;
   }
-  for (int j = 0; j < D; ++j) {
-    th[j] = Pm->default_dof_pos[j] + rand_range(0.0f, 0.9f, U[S_DOF + j]);
-    thd[j] = 0.0f;
+  // _reset_dofs legged_robot.py:481-506: q = q0 + U(0, 0.9), qd = 0
+  if (lane < D) {
+    s.th[lane] = Pm->default_dof_pos[lane] + rand_range(0.0f, 0.9f, U[S_DOF + lane]);
+    s.thd[lane] = 0.0f;
   }
-  for (int i = 0; i < 13; ++i) root[i] = Pm->base_init_state[i];
-  for (int i = 0; i < 3; ++i) root[i] = root[i] + B.env_origins[e * 3 + i];
-  if (Pm->custom_origins) {
-    root[0] = root[0] + rand_range(-1.0f, 1.0f, U[S_ROOT_XY + 0]);
-    root[1] = root[1] + rand_range(-1.0f, 1.0f, U[S_ROOT_XY + 1]);
-  }
-  for (int i = 0; i < 6; ++i) root[7 + i] = rand_range(-0.5f, 0.5f, U[S_ROOT_VEL + i]);
-  resample_commands(Pm, cmd, U, S_RCMD, root + 3);
-  ep = 0;
-  // buffer zeroing (lane-parallel). Inside a step the last_* buffers and the history
-  // are rewritten at the end of post_physics_step anyway (go2.py:380-384, :570-574),
-  // so only an external reset has to zero them.
+  // buffer zeroing. Inside a step the last_* buffers and the history are rewritten at the
+  // end of post_physics_step anyway (go2.py:380-384, 570-574); only an external reset
+  // has to zero them.
   if (zero_carried) {
     const int A = Pm->num_actions, H = Pm->history_len * Pm->num_proprio;
     if (lane < A) B.last_actions[(size_t)e * A + lane] = 0.f;
@@ -711,6 +692,7 @@ LGX_DEV void reset_env(const lgx_task_params* Pm, const lgx_buffers& B, int e, i
     *es = 0.f;
   }
   if (lane == 0 && B.episode_stats) atomicAdd(B.episode_stats + K, 1.0f);
+  __syncthreads();
 }
 
 LGX_DEV void fill_uniforms(Sh& s, uint64_t seed, uint32_t gid, uint64_t step, uint32_t stream, int lane) {
@@ -724,11 +706,20 @@ LGX_DEV void fill_uniforms(Sh& s, uint64_t seed, uint32_t gid, uint64_t step, ui
   __syncthreads();
 }
 
-// reward term (uniform across lanes); mirrors oracle/lgx_oracle.c reward_term
-LGX_DEV float reward_term(const lgx_task_params* Pm, const lgx_buffers& B, const Sh& s, const Scratch& x, int e,
-                          int id, const float* root, float* cmd, const float* lact, const float* ldv,
-                          const float* ltq, const float* lch, float* fat, const uint8_t* lc) {
+// one reward term (lane k computes term k); mirrors oracle/lgx_oracle.c reward_term.
+// Side effects (kept from the reference): feet_air_time (go2.py:827-830) and the in-place
+// wrap of commands[:, 3] (go2.py:744, Q7) are written back to LDS by the owning lane.
+LGX_DEV float reward_term(const lgx_task_params* Pm, const lgx_buffers& B, Sh& s, int e, int id) {
   const int D = Pm->num_dof, A = Pm->num_actions;
+  const Scratch& x = s.x;
+  const float* root = s.root;
+  float* cmd = s.cmd;
+  const float* lact = B.last_actions + (size_t)e * A;
+  const float* ldv = s.ldv;
+  const float* ltq = B.last_torques + (size_t)e * D;
+  const float* lch = s.lch;
+  float* fat = s.fat;
+  const int* lc = s.lc;
   float r = 0.0f;
   switch (id) {
     case LGX_REW_ACTION_RATE:
@@ -900,8 +891,9 @@ LGX_DEV float reward_term(const lgx_task_params* Pm, const lgx_buffers& B, const
   }
 }
 
-LGX_DEV void get_heights(const lgx_task_params* Pm, const lgx_buffers& B, Sh& s, const float* root, int lane) {
+LGX_DEV void get_heights(const lgx_task_params* Pm, const lgx_buffers& B, Sh& s, int lane) {
   const int NP = Pm->num_height_points;
+  const float* root = s.root;
   if (Pm->mesh_type == LGX_MESH_PLANE || B.height_samples == nullptr) {
     for (int i = lane; i < NP; i += 64) s.heights[i] = 0.0f;
     return;
@@ -927,8 +919,11 @@ LGX_DEV void get_heights(const lgx_task_params* Pm, const lgx_buffers& B, Sh& s,
 }
 
 // ============================================================== kernels
+#ifndef LGX_WAVES_PER_EU
+#define LGX_WAVES_PER_EU 1
+#endif
 template <bool PHYSICS>
-__global__ __launch_bounds__(64) void env_step_kernel(const lgx_model* __restrict__ M,
+__global__ __launch_bounds__(64, LGX_WAVES_PER_EU) void env_step_kernel(const lgx_model* __restrict__ M,
                                                       const lgx_task_params* __restrict__ Pm, lgx_buffers B,
                                                       uint64_t seed, uint64_t step) {
   __shared__ Sh s;
@@ -1037,144 +1032,152 @@ __global__ __launch_bounds__(64) void env_step_kernel(const lgx_model* __restric
     __syncthreads();
   }
 
+#ifdef LGX_DEBUG_SKIP_POST
+  return;
+#endif
   // ================================================================ post-physics
-  // Go2Robot.post_physics_step go2.py:345-387 / LeggedRobot legged_robot.py:103-138
-  float root[13];
-  for (int i = 0; i < 13; ++i) root[i] = s.hist[i];
-  float cmd[4];
-  for (int i = 0; i < 4; ++i) cmd[i] = B.commands[e * 4 + i];
-  int64_t ep = B.episode_length[e] + 1;
+  // Go2Robot.post_physics_step go2.py:345-387 / LeggedRobot legged_robot.py:103-138.
+  // Per-env scalars: lane 0, into LDS. Vectors: lane-parallel from LDS.
   fill_uniforms(s, seed, gid, step, 0, lane);
-  Scratch x;
-  const float g[3] = {0.f, 0.f, -1.f};
-  quat_rotate_inverse(root + 3, root + 7, x.blv);
-  quat_rotate_inverse(root + 3, root + 10, x.bav);
-  quat_rotate_inverse(root + 3, g, x.pg);
-  float lch[4] = {0.f, 0.f, 0.f, 0.f};
-  uint8_t lc[4] = {0, 0, 0, 0};
-  x.roll = x.pitch = x.yaw = 0.f;
-  x.ph[0] = x.ph[1] = x.ph[2] = x.ph[3] = 0.f;
-  if (Pm->task_kind == LGX_TASK_GO2) {
-    // update_feet_states go2.py:266-328
-    float phase = trem((float)ep * Pm->dt, Pm->period) / Pm->period;
-    float pfr = trem(phase + Pm->offset_fr, 1.0f), pbl = trem(phase + Pm->offset_bl, 1.0f);
-    float pfl = trem(phase + Pm->offset_fl, 1.0f), pbr = trem(phase + Pm->offset_br, 1.0f);
-    float msk = (nrm3(cmd[0], cmd[1], cmd[2]) < 0.2f) ? 0.0f : 1.0f;
-    x.ph[0] = pfl * msk; x.ph[1] = pfr * msk; x.ph[2] = pbl * msk; x.ph[3] = pbr * msk;
-    for (int f = 0; f < 4; ++f) {
-      lc[f] = B.last_contacts[e * Pm->num_feet + f];
-      lch[f] = B.last_contact_heights[e * Pm->num_feet + f];
-      int curc = s.cf[Pm->feet_idx[f]][2] > 1.0f;
-      x.contact[f] = curc || lc[f];
-      lc[f] = (uint8_t)curc;
-      x.feet_z[f] = s.rbz[Pm->feet_idx[f]];
-      if (x.contact[f]) lch[f] = x.feet_z[f];
+  const bool go2 = Pm->task_kind == LGX_TASK_GO2;
+  if (lane == 0) {
+    Scratch& x = s.x;
+    float* root = s.root;
+    float* cmd = s.cmd;
+    for (int i = 0; i < 13; ++i) root[i] = s.hist[i];
+    for (int i = 0; i < 4; ++i) cmd[i] = B.commands[e * 4 + i];
+    const long long ep = B.episode_length[e] + 1;
+    s.ep = ep;
+    const float g[3] = {0.f, 0.f, -1.f};
+    quat_rotate_inverse(root + 3, root + 7, x.blv);
+    quat_rotate_inverse(root + 3, root + 10, x.bav);
+    quat_rotate_inverse(root + 3, g, x.pg);
+    x.roll = x.pitch = x.yaw = 0.f;
+    x.ph[0] = x.ph[1] = x.ph[2] = x.ph[3] = 0.f;
+    for (int f = 0; f < 4; ++f) { x.contact[f] = 0; x.feet_z[f] = 0.f; s.lc[f] = 0; s.lch[f] = 0.f; s.fat[f] = 0.f; }
+    if (go2) {
+      // update_feet_states go2.py:266-328
+      float phase = trem((float)ep * Pm->dt, Pm->period) / Pm->period;
+      float pfr = trem(phase + Pm->offset_fr, 1.0f), pbl = trem(phase + Pm->offset_bl, 1.0f);
+      float pfl = trem(phase + Pm->offset_fl, 1.0f), pbr = trem(phase + Pm->offset_br, 1.0f);
+      float msk = (nrm3(cmd[0], cmd[1], cmd[2]) < 0.2f) ? 0.0f : 1.0f;
+      x.ph[0] = pfl * msk; x.ph[1] = pfr * msk; x.ph[2] = pbl * msk; x.ph[3] = pbr * msk;
+      for (int f = 0; f < 4; ++f) {
+        int lcf = B.last_contacts[e * Pm->num_feet + f];
+        float lch = B.last_contact_heights[e * Pm->num_feet + f];
+        int curc = s.cf[Pm->feet_idx[f]][2] > 1.0f;
+        x.contact[f] = curc || lcf;
+        s.lc[f] = curc;
+        x.feet_z[f] = s.rbz[Pm->feet_idx[f]];
+        s.lch[f] = x.contact[f] ? x.feet_z[f] : lch;
+        if (B.feet_air_time) s.fat[f] = B.feet_air_time[e * Pm->num_feet + f];
+      }
+      // quaternion_to_euler go2.py:11-31
+      float qx = root[3], qy = root[4], qz = root[5], qw = root[6];
+      x.roll = atan2f(2.0f * (qw * qx + qy * qz), 1.0f - 2.0f * (qx * qx + qy * qy));
+      x.pitch = asinf(clipf(2.0f * (qw * qy - qz * qx), -1.0f, 1.0f));
+      x.yaw = atan2f(2.0f * (qw * qz + qx * qy), 1.0f - 2.0f * (qy * qy + qz * qz));
     }
-    // quaternion_to_euler go2.py:11-31
-    float qx = root[3], qy = root[4], qz = root[5], qw = root[6];
-    x.roll = atan2f(2.0f * (qw * qx + qy * qz), 1.0f - 2.0f * (qx * qx + qy * qy));
-    x.pitch = asinf(clipf(2.0f * (qw * qy - qz * qx), -1.0f, 1.0f));
-    x.yaw = atan2f(2.0f * (qw * qz + qx * qy), 1.0f - 2.0f * (qy * qy + qz * qz));
+    // _post_physics_step_callback go2.py:390-410
+    if (ep % Pm->resample_interval == 0) resample_commands(Pm, cmd, s.U, S_CMD, root + 3);
+    if (Pm->heading_command) {
+      const float fwd[3] = {1.f, 0.f, 0.f};
+      float f[3];
+      quat_apply(root + 3, fwd, f);
+      float heading = atan2f(f[1], f[0]);
+      float gain = go2 ? Pm->heading_error_gain : 0.5f;
+      cmd[2] = clipf(wrap_to_pi(cmd[3] - heading) * gain, -1.0f, 1.0f);
+    }
+    if (Pm->push_robots && (step % (uint64_t)Pm->push_interval == 0)) {
+      root[7] = rand_range(-Pm->max_push_vel_xy, Pm->max_push_vel_xy, s.U[S_PUSH + 0]);
+      root[8] = rand_range(-Pm->max_push_vel_xy, Pm->max_push_vel_xy, s.U[S_PUSH + 1]);
+    }
+    // check_termination go2.py:186-204
+    int reset = 0;
+    for (int i = 0; i < Pm->n_termination; ++i) {
+      const float* c = s.cf[Pm->termination_idx[i]];
+      reset |= nrm3(c[0], c[1], c[2]) > 1.0f;
+    }
+    int tout = ep > Pm->max_episode_length;
+    reset |= tout;
+    reset |= x.pg[2] > 0.0f;
+    if (Pm->parkour) reset |= root[2] < -1.0f;
+    s.reset = reset;
+    s.tout = tout;
+    x.jump = B.rpy_phase ? B.rpy_phase[e * 8 + 7] : 0.f;  // set by the previous step's observations
   }
-  // _post_physics_step_callback go2.py:390-410
-  if (ep % Pm->resample_interval == 0) resample_commands(Pm, cmd, s.U, S_CMD, root + 3);
-  if (Pm->heading_command) {
-    const float fwd[3] = {1.f, 0.f, 0.f};
-    float f[3];
-    quat_apply(root + 3, fwd, f);
-    float heading = atan2f(f[1], f[0]);
-    float gain = Pm->task_kind == LGX_TASK_GO2 ? Pm->heading_error_gain : 0.5f;
-    cmd[2] = clipf(wrap_to_pi(cmd[3] - heading) * gain, -1.0f, 1.0f);
-  }
-  get_heights(Pm, B, s, root, lane);
   __syncthreads();
-  if (Pm->push_robots && (step % (uint64_t)Pm->push_interval == 0)) {
-    root[7] = rand_range(-Pm->max_push_vel_xy, Pm->max_push_vel_xy, s.U[S_PUSH + 0]);
-    root[8] = rand_range(-Pm->max_push_vel_xy, Pm->max_push_vel_xy, s.U[S_PUSH + 1]);
-  }
-  // check_termination go2.py:186-204
-  int reset = 0;
-  for (int i = 0; i < Pm->n_termination; ++i) {
-    const float* c = s.cf[Pm->termination_idx[i]];
-    reset |= nrm3(c[0], c[1], c[2]) > 1.0f;
-  }
-  int tout = ep > Pm->max_episode_length;
-  reset |= tout;
-  reset |= x.pg[2] > 0.0f;
-  if (Pm->parkour) reset |= root[2] < -1.0f;
-  x.jump = B.rpy_phase ? B.rpy_phase[e * 8 + 7] : 0.f;
-  // compute_reward legged_robot.py:216-237
+  get_heights(Pm, B, s, lane);
+  __syncthreads();
+  // compute_reward legged_robot.py:216-237: lane k evaluates term k (alphabetical order)
   const int K = Pm->num_reward_terms;
   const int KS = K + (Pm->has_termination_reward ? 1 : 0);
-  float lact[LGX_MAX_DOF], ldv[LGX_MAX_DOF], ltq[LGX_MAX_DOF], fat[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int j = 0; j < A; ++j) lact[j] = B.last_actions[(size_t)e * A + j];
-  for (int j = 0; j < D; ++j) { ldv[j] = B.last_dof_vel[(size_t)e * D + j]; ltq[j] = B.last_torques[(size_t)e * D + j]; }
-  if (B.feet_air_time) for (int f = 0; f < Pm->num_feet && f < 4; ++f) fat[f] = B.feet_air_time[e * Pm->num_feet + f];
-  float rew = 0.0f;
-  float my_sum = 0.f;
-  for (int k = 0; k < K; ++k) {
-    float v = reward_term(Pm, B, s, x, e, Pm->reward_ids[k], root, cmd, lact, ldv, ltq, lch, fat, lc) * Pm->reward_scales[k];
-    rew += v;
-    if (lane == k) my_sum = v;
-  }
-  if (Pm->only_positive_rewards) rew = rew < 0.0f ? 0.0f : rew;
-  if (Pm->has_termination_reward) {
-    float v = (float)(reset && !tout) * Pm->termination_scale;
-    rew += v;
-    if (lane == K) my_sum = v;
+  if (lane < K) s.rterm[lane] = reward_term(Pm, B, s, e, Pm->reward_ids[lane]) * Pm->reward_scales[lane];
+  __syncthreads();
+  const int reset = s.reset;
+  if (lane == 0) {
+    float rew = 0.0f;
+    for (int k = 0; k < K; ++k) rew += s.rterm[k];  // sequential, the reference's order
+    if (Pm->only_positive_rewards) rew = rew < 0.0f ? 0.0f : rew;
+    if (Pm->has_termination_reward) {
+      float v = (float)(reset && !s.tout) * Pm->termination_scale;
+      rew += v;
+      s.rterm[K] = v;
+    }
+    B.rew[e] = rew;
+    B.reset[e] = (uint8_t)reset;
+    B.time_out[e] = (uint8_t)s.tout;
   }
   __syncthreads();
-  if (lane < KS) B.episode_sums[(size_t)e * KS + lane] += my_sum;
-  if (lane == 0) { B.rew[e] = rew; B.reset[e] = (uint8_t)reset; B.time_out[e] = (uint8_t)tout; }
+  if (lane < KS) B.episode_sums[(size_t)e * KS + lane] += s.rterm[lane];
   __syncthreads();
   // reset_idx (go2.py:207-263)
-  if (reset) reset_env(Pm, B, e, lane, s.U, root, s.th, s.thd, cmd, ep, true, false);
-  __syncthreads();
+  if (reset) reset_env(Pm, B, s, e, lane, true, false);
 
   // compute_observations go2.py:467-574 / legged_robot.py:240-273
   const int Pp = Pm->num_proprio, H = Pm->history_len;
-  if (Pm->task_kind == LGX_TASK_GO2 && Pm->parkour) {
+  const Scratch& x = s.x;
+  if (go2 && Pm->parkour && lane == 0) {
     int outl = 0;
     for (int i = 0; i < Pm->num_height_points; ++i) outl += fabsf(s.heights[i]) > 0.1f;
-    x.jump = (float)(outl >= 8);
+    s.x.jump = (float)(outl >= 8);
   }
   for (int i = lane; i < Pp; i += 64) {
     float v;
-    if (Pm->task_kind == LGX_TASK_GO2) {
+    if (go2) {
       if (i < 3) v = x.bav[i] * Pm->obs_scale_ang_vel;
       else if (i == 3) v = x.roll;
       else if (i == 4) v = x.pitch;
-      else if (i < 8) v = cmd[i - 5] * Pm->commands_scale[i - 5];
+      else if (i < 8) v = s.cmd[i - 5] * Pm->commands_scale[i - 5];
       else if (i < 8 + D) v = (s.th[i - 8] - Pm->default_dof_pos[i - 8]) * Pm->obs_scale_dof_pos;
       else if (i < 8 + 2 * D) v = s.thd[i - 8 - D] * Pm->obs_scale_dof_vel;
       else if (i < 8 + 2 * D + A) v = s.act[i - 8 - 2 * D];
       else {
         int q = i - (8 + 2 * D + A);  // sin/cos of FR, FL, BL, BR
-        const int order[4] = {1, 0, 2, 3};
-        float p = 6.283185307179586f * x.ph[order[q >> 1]];
+        int leg = (q >> 1) == 0 ? 1 : ((q >> 1) == 1 ? 0 : (q >> 1));
+        float p = 6.283185307179586f * x.ph[leg];
         v = (q & 1) ? cosf(p) : sinf(p);
       }
     } else {
       if (i < 3) v = x.blv[i] * Pm->obs_scale_lin_vel;
       else if (i < 6) v = x.bav[i - 3] * Pm->obs_scale_ang_vel;
       else if (i < 9) v = x.pg[i - 6];
-      else if (i < 12) v = cmd[i - 9] * Pm->commands_scale[i - 9];
+      else if (i < 12) v = s.cmd[i - 9] * Pm->commands_scale[i - 9];
       else if (i < 12 + D) v = (s.th[i - 12] - Pm->default_dof_pos[i - 12]) * Pm->obs_scale_dof_pos;
       else if (i < 12 + 2 * D) v = s.thd[i - 12 - D] * Pm->obs_scale_dof_vel;
       else if (i < 12 + 2 * D + A) v = s.act[i - 12 - 2 * D];
-      else v = clipf(root[2] - 0.5f - s.heights[i - (12 + 2 * D + A)], -1.0f, 1.0f) * Pm->obs_scale_height;
+      else v = clipf(s.root[2] - 0.5f - s.heights[i - (12 + 2 * D + A)], -1.0f, 1.0f) * Pm->obs_scale_height;
     }
     if (Pm->add_noise) v = v + (2.0f * s.U[S_NOISE + i] - 1.0f) * Pm->noise_vec[i];
     s.cur[i] = v;
   }
-  // stage the old history (obs[0:H*P]) in LDS
+  // stage the old history (obs[0:H*P]) in LDS; a reset env's history was zeroed (go2.py:238)
   float* hist_g = B.obs_history + (size_t)e * H * Pp;
-  for (int i = lane; i < H * Pp; i += 64) s.hist[16 + i] = reset ? 0.f : hist_g[i];  // reset zeroes it (go2.py:238)
+  for (int i = lane; i < H * Pp; i += 64) s.hist[16 + i] = reset ? 0.f : hist_g[i];
   __syncthreads();
   const float co = Pm->clip_obs;
   float* obs = B.obs + (size_t)e * Pm->num_obs;
   float* cr = B.critic ? B.critic + (size_t)e * Pm->num_critic : nullptr;
-  const bool go2 = Pm->task_kind == LGX_TASK_GO2;
   for (int i = lane; i < H * Pp; i += 64) {
     float v = clipf(s.hist[16 + i], -co, co);
     obs[i] = v;
@@ -1204,12 +1207,13 @@ __global__ __launch_bounds__(64) void env_step_kernel(const lgx_model* __restric
       if (cr) cr[NO + Pm->num_priv + lane] = v;
     }
     for (int i = lane; i < Pm->num_scan; i += 64) {
-      float v = clipf(root[2] - 0.3f - s.heights[i], -1.0f, 1.0f);
+      float v = clipf(s.root[2] - 0.3f - s.heights[i], -1.0f, 1.0f);
       B.scan[(size_t)e * Pm->num_scan + i] = v;
       if (cr) cr[NO + Pm->num_priv + 3 + i] = clipf(v, -co, co);
     }
   }
   // history update go2.py:570-574
+  const long long ep = s.ep;
   for (int i = lane; i < H * Pp; i += 64) {
     float v = (ep <= 1) ? s.cur[i % Pp] : (i < (H - 1) * Pp ? s.hist[16 + i + Pp] : s.cur[i - (H - 1) * Pp]);
     hist_g[i] = v;
@@ -1222,21 +1226,19 @@ __global__ __launch_bounds__(64) void env_step_kernel(const lgx_model* __restric
     B.dof_state[((size_t)e * D + lane) * 2] = s.th[lane];
     B.dof_state[((size_t)e * D + lane) * 2 + 1] = s.thd[lane];
   }
-  if (lane < 6) B.last_root_vel[e * 6 + lane] = root[7 + lane];
+  if (lane < 6) B.last_root_vel[e * 6 + lane] = s.root[7 + lane];
   if (lane < 3) {
     B.last_base_lin_vel[e * 3 + lane] = x.blv[lane];
     if (B.base_lin_vel) B.base_lin_vel[e * 3 + lane] = x.blv[lane];
     if (B.base_ang_vel) B.base_ang_vel[e * 3 + lane] = x.bav[lane];
     if (B.projected_gravity) B.projected_gravity[e * 3 + lane] = x.pg[lane];
   }
-  if (lane < 13) root_g[lane] = root[lane];
-  if (lane < 4) B.commands[e * 4 + lane] = cmd[lane];
-  if (go2 && lane < Pm->num_feet) {
-    if (!reset) {
-      B.last_contacts[e * Pm->num_feet + lane] = lc[lane];
-      B.last_contact_heights[e * Pm->num_feet + lane] = lch[lane];
-    }
-    if (B.feet_air_time && !reset) B.feet_air_time[e * Pm->num_feet + lane] = fat[lane];
+  if (lane < 13) root_g[lane] = s.root[lane];
+  if (lane < 4) B.commands[e * 4 + lane] = s.cmd[lane];
+  if (go2 && lane < Pm->num_feet && !reset) {
+    B.last_contacts[e * Pm->num_feet + lane] = (uint8_t)s.lc[lane];
+    B.last_contact_heights[e * Pm->num_feet + lane] = s.lch[lane];
+    if (B.feet_air_time) B.feet_air_time[e * Pm->num_feet + lane] = s.fat[lane];
   }
   if (lane == 0) B.episode_length[e] = ep;
   if (B.rpy_phase && lane < 8) {
@@ -1256,18 +1258,17 @@ __global__ __launch_bounds__(64) void reset_kernel(const lgx_task_params* __rest
   if (!mask[e]) return;
   const int D = Pm->num_dof;
   fill_uniforms(s, seed, (uint32_t)(Pm->env_id_offset + e), call, 1, lane);
-  float root[13], cmd[4], th[LGX_MAX_DOF], thd[LGX_MAX_DOF];
-  for (int i = 0; i < 13; ++i) root[i] = B.root_states[(size_t)e * 13 + i];
-  for (int i = 0; i < 4; ++i) cmd[i] = B.commands[e * 4 + i];
-  int64_t ep = B.episode_length[e];
-  reset_env(Pm, B, e, lane, s.U, root, th, thd, cmd, ep, false, true);
-  if (lane < 13) B.root_states[(size_t)e * 13 + lane] = root[lane];
+  if (lane < 13) s.root[lane] = B.root_states[(size_t)e * 13 + lane];
+  if (lane < 4) s.cmd[lane] = B.commands[e * 4 + lane];
+  __syncthreads();
+  reset_env(Pm, B, s, e, lane, false, true);
+  if (lane < 13) B.root_states[(size_t)e * 13 + lane] = s.root[lane];
   if (lane < D) {
-    B.dof_state[((size_t)e * D + lane) * 2] = th[lane];
-    B.dof_state[((size_t)e * D + lane) * 2 + 1] = thd[lane];
+    B.dof_state[((size_t)e * D + lane) * 2] = s.th[lane];
+    B.dof_state[((size_t)e * D + lane) * 2 + 1] = s.thd[lane];
   }
-  if (lane < 4) B.commands[e * 4 + lane] = cmd[lane];
-  if (lane == 0) { B.episode_length[e] = ep; B.reset[e] = 1; }
+  if (lane < 4) B.commands[e * 4 + lane] = s.cmd[lane];
+  if (lane == 0) { B.episode_length[e] = s.ep; B.reset[e] = 1; }
 }
 
 }  // namespace lgx
