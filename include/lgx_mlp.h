@@ -1,0 +1,61 @@
+/* lgx_mlp.h — C ABI of liblgx_mlp.so: the learner's fused MLP layer GEMMs on MI355X.
+ *
+ * Replaces the nn.Linear + nn.ELU chains of the rsl_rl networks
+ * (reference rsl_rl/rsl_rl/modules/actor_critic.py:64-87 actor/critic MLPs,
+ * support_networks.py:22-33 scan encoder, :60-70 MlpEstimator, :100-112 privileged
+ * encoder) in forward (rollout ppo.py:129-153 and update ppo.py:186-201) and backward
+ * (loss.backward(), ppo.py:262 / :207).
+ *
+ * One entry point computes, for row-major fp32 operands,
+ *     C[m, n] = epilogue( sum_k A(m, k) * B(k, n) )
+ * with A(m,k) = A[m*lda + k] (a_kcontig = 1) or A[k*lda + m] (a_kcontig = 0), and the
+ * same for B(k,n) = B[n*ldb + k] (b_kcontig = 1) or B[k*ldb + n] (b_kcontig = 0). So
+ *     forward   Y  = X W^T + b       a_kcontig = 1, b_kcontig = 1 (+ bias, ELU)
+ *     input grad dX = dY W (* ELU'(Y_prev))   a_kcontig = 1, b_kcontig = 0
+ *     weight grad dW = dY^T X, db = sum_rows dY    a_kcontig = 0, b_kcontig = 0, split-K
+ * Arithmetic: products in 3 x bf16 MFMA (a = a_hi + a_lo, a_hi*b_hi + a_hi*b_lo +
+ * a_lo*b_hi, fp32 accumulation): ~2^-16 relative per product, tighter than the TF32
+ * the reference trains with (legged_gym/scripts/train.py:39 set_float32_matmul_precision('high')).
+ * All work is stream-ordered on `stream` (hipStream_t); no host synchronisation.
+ * Return 0 on success, negative on invalid arguments / launch failure (lgx_mlp_last_error).
+ */
+#ifndef LGX_MLP_H
+#define LGX_MLP_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LGX_MLP_ABI_VERSION 1
+
+enum {
+  LGX_EPI_BIAS = 1,  /* + bias[n] */
+  LGX_EPI_ELU = 2,   /* then ELU(alpha = 1): v > 0 ? v : expm1(v) */
+  LGX_EPI_DELU = 4,  /* * ELU'(z) from the ELU output y = act[m*ld_act + n]: y > 0 ? 1 : y + 1 */
+  LGX_EPI_ACCUM = 8  /* C += result (else C = result) */
+};
+
+typedef struct lgx_gemm_args {
+  const float* A; int64_t lda; int32_t a_kcontig;
+  const float* B; int64_t ldb; int32_t b_kcontig;
+  float* C; int64_t ldc;
+  int32_t M, N, K;
+  int32_t epilogue;          /* LGX_EPI_* bits */
+  const float* bias;         /* [N] for LGX_EPI_BIAS */
+  const float* act; int64_t ld_act;  /* ELU outputs for LGX_EPI_DELU */
+  int32_t split_k;           /* >= 1; > 1 needs workspace (split_k * M * N floats) */
+  float* workspace;
+  float* colsum;             /* optional [M]: sum_k A(m,k) (the bias gradient); needs a_kcontig = 0 */
+  float* colsum_ws;          /* split_k * M floats when colsum != NULL */
+} lgx_gemm_args;
+
+int32_t lgx_mlp_abi_version(void);
+/* Suggested split-K factor for an M x N x K weight-gradient GEMM. */
+int32_t lgx_mlp_pick_split(int32_t M, int32_t N, int32_t K);
+int32_t lgx_gemm(const lgx_gemm_args* args, void* stream);
+const char* lgx_mlp_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,36 +1,56 @@
-"""Build liblgx.so (the HIP env-step library) in-tree for gfx950 with hipcc."""
+"""Build the HIP libraries in-tree for gfx950 with hipcc:
+  lib/liblgx.so      env step (csrc/lgx_env.hip, include/lgx.h)
+  lib/liblgx_mlp.so  learner MLP GEMMs (csrc/lgx_mlp.hip, include/lgx_mlp.h)"""
 import os
 import subprocess
 import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-SRC = [os.path.join(HERE, "csrc", "lgx_env.hip")]
-OUT = os.path.join(HERE, "lib", "liblgx.so")
+INC = os.path.join(os.path.dirname(HERE), "include")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
+LIBS = {
+    "liblgx.so": (["lgx_env.hip"], ["lgx_device.h"], ["lgx.h"]),
+    "liblgx_mlp.so": (["lgx_mlp.hip"], [], ["lgx_mlp.h"]),
+}
+OUT = os.path.join(HERE, "lib", "liblgx.so")
+OUT_MLP = os.path.join(HERE, "lib", "liblgx_mlp.so")
 
 
-def needs_build():
-    if not os.path.exists(OUT):
+def _paths(name):
+    srcs, hdrs, incs = LIBS[name]
+    src = [os.path.join(HERE, "csrc", s) for s in srcs]
+    deps = src + [os.path.join(HERE, "csrc", h) for h in hdrs] + [os.path.join(INC, h) for h in incs]
+    return src, deps, os.path.join(HERE, "lib", name)
+
+
+def needs_build(name="liblgx.so"):
+    src, deps, out = _paths(name)
+    if not os.path.exists(out):
         return True
-    t = os.path.getmtime(OUT)
-    deps = SRC + [os.path.join(HERE, "csrc", f) for f in os.listdir(os.path.join(HERE, "csrc"))]
-    deps.append(os.path.join(os.path.dirname(HERE), "include", "lgx.h"))
+    t = os.path.getmtime(out)
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force=False, verbose=False):
-    if not force and not needs_build():
-        return OUT
-    os.makedirs(os.path.dirname(OUT), exist_ok=True)
+def build_one(name, force=False, verbose=False):
+    src, _, out = _paths(name)
+    if not force and not needs_build(name):
+        return out
+    os.makedirs(os.path.dirname(out), exist_ok=True)
     cmd = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-ffp-contract=off", "-o", OUT + ".tmp"] + SRC
+           "-ffp-contract=off", "-o", out + ".tmp"] + src
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
-    os.replace(OUT + ".tmp", OUT)
+    os.replace(out + ".tmp", out)
+    return out
+
+
+def build(force=False, verbose=False):
+    for name in LIBS:
+        build_one(name, force=force, verbose=verbose)
     return OUT
 
 
 if __name__ == "__main__":
     build(force="--force" in sys.argv, verbose=True)
-    print(OUT)
+    print(OUT, OUT_MLP)

@@ -4,14 +4,27 @@ Same hyper-parameters, losses, schedules, optimizers and param groups:
   optimizer            Adam([actor, critic, privileged_encoder_, std, scan_encoder]) lr
   adaptation_optimizer Adam(adaptation_encoder_) lr
   estimator_optimizer  Adam(estimator) estimator_learning_rate
-MI355X-side changes that keep the math: no per-minibatch host syncs (loss sums stay on
-device, one transfer per update instead of 80 .item() calls), and — when
-torch.distributed is initialised — one flattened-gradient all-reduce (mean over ranks)
-per backward before the global-norm clip.
+
+MI355X execution of the same math (DESIGN.md "Learner"):
+  * gradients live in ONE flat fp32 buffer (`FlatGrads`): p.grad are views into it, so
+    zero_grad is one memset, grad clipping is one norm over a slice, and the multi-GPU
+    all-reduce is one RCCL call per minibatch over [main | estimator | kl] (mean over ranks);
+  * the adaptive-KL learning-rate schedule (ppo.py:230-246) runs on the device (fp64
+    master, same branches), so a minibatch needs no host round trip;
+  * on a HIP device the whole 5x4-minibatch update is captured once as a hipGraph and
+    replayed per iteration (world_size 1), or as per-minibatch graphs around the RCCL
+    all-reduce (world_size > 1). The first two updates run eagerly (warm-up), and any
+    optimizer/model state load drops the graphs.
+The estimator step is issued after the main backward instead of before it: the two
+losses share no parameters, so the result is identical (the ROA update uses the TRUE
+estimated obs, ppo.py:190).
+Reference quirk kept: clip_grad_norm_(actor_critic.parameters()) also sees the
+adaptation encoder's stale DAgger gradients (never zeroed by `optimizer`), and scales them.
 """
+import copy
+
 import torch
 import torch.distributed as dist
-import torch.nn as nn
 import torch.optim as optim
 
 from legged_gym_custom_amd.rsl_rl.modules import ActorCritic
@@ -40,6 +53,73 @@ def allreduce_grads(params):
         off += n
 
 
+class FlatGrads:
+    """p.grad of every parameter as a view into one contiguous fp32 buffer.
+
+    `segments` = [(name, params | int)]: a parameter list, or a number of plain scalar
+    slots (e.g. the KL riding along in the all-reduce). Backward accumulates in place
+    into a defined .grad, so the views stay bound as long as nothing sets .grad to None
+    (PPO never calls optimizer.zero_grad())."""
+
+    def __init__(self, segments):
+        sizes = [(name, (sum(p.numel() for p in ps) if not isinstance(ps, int) else ps)) for name, ps in segments]
+        dev = next(ps for _, ps in segments if not isinstance(ps, int))[0].device
+        self.buf = torch.zeros(sum(n for _, n in sizes), device=dev)
+        self.slices = {}
+        self._ptrs = []
+        off = 0
+        for (name, ps), (_, n) in zip(segments, sizes):
+            self.slices[name] = (off, off + n)
+            if not isinstance(ps, int):
+                o = off
+                for p in ps:
+                    p.grad = self.buf[o:o + p.numel()].view_as(p)
+                    self._ptrs.append((p, p.grad.data_ptr()))
+                    o += p.numel()
+            off += n
+
+    def segment(self, name):
+        a, b = self.slices[name]
+        return self.buf[a:b]
+
+    def span(self, first, last):
+        return self.buf[self.slices[first][0]:self.slices[last][1]]
+
+    def check(self):
+        """True while every p.grad is still the view installed at construction."""
+        return all(p.grad is not None and p.grad.data_ptr() == ptr for p, ptr in self._ptrs)
+
+
+def _clip_(segs, max_norm):
+    """clip_grad_norm_ over the concatenation of `segs` (torch/nn/utils/clip_grad.py):
+    coef = clamp(max_norm / (||g||_2 + 1e-6), max=1); g *= coef. No host sync."""
+    if len(segs) == 1:
+        total = torch.linalg.vector_norm(segs[0])
+    else:
+        total = torch.linalg.vector_norm(torch.stack([torch.linalg.vector_norm(s) for s in segs]))
+    coef = torch.clamp(max_norm / (total + 1e-6), max=1.0)
+    for s in segs:
+        s.mul_(coef)
+
+
+def export_adam_state(opt):
+    """Optimizer state_dict in the reference's format (plain torch Adam, float lr,
+    CPU fp32 `step`), whatever execution flags this build runs Adam with."""
+    sd = copy.deepcopy(opt.state_dict())
+    for g in sd["param_groups"]:
+        if isinstance(g.get("lr"), torch.Tensor):
+            g["lr"] = float(g["lr"])
+        g["capturable"] = False
+        g["fused"] = None
+    for st in sd["state"].values():
+        if "step" in st:
+            st["step"] = torch.tensor(float(st["step"]), dtype=torch.float32)
+        for k in ("exp_avg", "exp_avg_sq", "max_exp_avg_sq"):
+            if k in st:
+                st[k] = st[k].cpu()
+    return sd
+
+
 class PPO:
     actor_critic: ActorCritic
     estimator: MlpEstimator
@@ -47,7 +127,7 @@ class PPO:
     def __init__(self, actor_critic, estimator, num_learning_epochs=1, num_mini_batches=1, clip_param=0.2,
                  gamma=0.998, lam=0.95, value_loss_coef=1.0, entropy_coef=0.0, learning_rate=1e-3,
                  estimator_learning_rate=1e-3, max_grad_norm=1.0, use_clipped_value_loss=True, schedule="fixed",
-                 desired_kl=0.01, resume=False, device="cpu"):
+                 desired_kl=0.01, resume=False, device="cpu", use_graphs=None):
         self.device = device
         self.desired_kl = desired_kl
         self.schedule = schedule
@@ -61,15 +141,29 @@ class PPO:
         self.storage = None
         self.estimator = estimator.to(self.device)
         ac = self.actor_critic
-        self.optimizer = optim.Adam([
-            {"params": ac.actor.parameters()},
-            {"params": ac.critic.parameters()},
-            {"params": ac.privileged_encoder_.parameters()},
-            {"params": ac.std},
-            {"params": ac.scan_encoder.parameters()},
-        ], lr=self.learning_rate)
-        self.adaptation_optimizer = optim.Adam(ac.adaptation_encoder_.parameters(), lr=self.learning_rate)
-        self.estimator_optimizer = optim.Adam(self.estimator.parameters(), lr=self.estimator_learning_rate)
+        self.on_gpu = str(device).startswith("cuda")
+        self.use_graphs = self.on_gpu if use_graphs is None else (use_graphs and self.on_gpu)
+
+        main_groups = [list(ac.actor.parameters()), list(ac.critic.parameters()),
+                       list(ac.privileged_encoder_.parameters()), [ac.std], list(ac.scan_encoder.parameters())]
+        self._main_params = [p for g in main_groups for p in g]
+        self._adapt_params = list(ac.adaptation_encoder_.parameters())
+        self._est_params = list(self.estimator.parameters())
+        # [main | estimator | kl] is the contiguous all-reduce span; adaptation after it
+        self.grads = FlatGrads([("main", self._main_params), ("estimator", self._est_params), ("kl", 1),
+                                ("adaptation", self._adapt_params)])
+
+        # learning rate: fp64 master on the device, fp32 copy read by the fused Adam kernel
+        self._lr64 = torch.tensor(float(learning_rate), dtype=torch.float64, device=device)
+        if self.on_gpu:
+            kw = dict(fused=True, capturable=True)
+            self._lr32 = torch.tensor(float(learning_rate), dtype=torch.float32, device=device)
+            lr = self._lr32
+        else:
+            kw, self._lr32, lr = {}, None, float(learning_rate)
+        self.optimizer = optim.Adam([{"params": g} for g in main_groups], lr=lr, **kw)
+        self.adaptation_optimizer = optim.Adam(self._adapt_params, lr=learning_rate, **kw)
+        self.estimator_optimizer = optim.Adam(self._est_params, lr=estimator_learning_rate, **kw)
         self.transition = RolloutStorage.Transition()
         self.clip_param = clip_param
         self.num_learning_epochs = num_learning_epochs
@@ -81,11 +175,23 @@ class PPO:
         self.max_grad_norm = max_grad_norm
         self.use_clipped_value_loss = use_clipped_value_loss
         self.total_updates = 0.0
+        # update-step device state (static addresses: captured by the graphs)
+        self._reg_coef = torch.zeros((), device=device)
+        self._losses = torch.zeros(4, device=device)   # value, surrogate, regularisation, estimator
+        self._sums = torch.zeros(4, device=device)
+        self._perm = None
+        self._graphs = None
+        self._eager_updates = 0
+        self.graph_mode = None  # "whole" | "phased" once captured
+        self.phased_graphs = None  # None: phased iff world_size > 1 (tests force it on one GPU)
 
+    # ------------------------------------------------------------------ storage / rollout
     def init_storage(self, num_envs, num_transitions_per_env, total_obs_shape, privileged_obs_shape, critic_obs_shape,
                      estimated_obs_shape, scan_obs_shape, action_shape):
         self.storage = RolloutStorage(num_envs, num_transitions_per_env, total_obs_shape, privileged_obs_shape,
                                       critic_obs_shape, estimated_obs_shape, scan_obs_shape, action_shape, self.device)
+        self._perm = torch.zeros(num_envs * num_transitions_per_env, dtype=torch.long, device=self.device)
+        self._graphs = None
 
     def test_mode(self):
         self.actor_critic.test()
@@ -128,66 +234,171 @@ class PPO:
         stage = min(max((self.total_updates - self.start_step) / self.duration, 0.0), 1.0)
         return self.start_val + stage * (self.end_val - self.start_val)
 
-    def update(self):
-        """ppo.py:182-293 (5 epochs x 4 minibatches)."""
-        sums = torch.zeros(4, device=self.device)  # value, surrogate, regularisation, estimator
+    # ------------------------------------------------------------------ one minibatch
+    def _minibatch_grads(self, idx):
+        """Phase A of one minibatch (ppo.py:186-265 minus the optimizer steps): both
+        backwards into the flat gradient buffer, the local KL into its slot, losses."""
         ac = self.actor_critic
+        g = self.grads
+        s = self.storage
+        (obs_b, priv_b, critic_b, est_b, scan_b, actions_b, target_values_b, adv_b, returns_b, old_logp_b,
+         old_mu_b, old_sigma_b) = s.gather(idx)
+        # the sample drawn by act() in the reference's update is unused: build the distribution only
+        ac.update_distribution(obs_b, priv_b, est_b, scan_b, adaptation_mode=False)  # TRUE est obs (Q12)
+        logp_b = ac.get_actions_log_prob(actions_b)
+        value_b = ac.evaluate(critic_b)
+        mu_b, sigma_b, entropy_b = ac.action_mean, ac.action_std, ac.entropy
+        priv_latent = ac.privileged_encoder(priv_b)
+        with torch.no_grad():
+            adapt_latent = ac.adaptation_encoder(obs_b)
+        regularization_loss = (priv_latent - adapt_latent).norm(p=2, dim=1).mean()
+        pred = self.estimator(obs_b)
+        estimator_loss = (pred - est_b).norm(p=2, dim=1).pow(2).mean()
+        if self.desired_kl is not None and self.schedule == "adaptive":
+            with torch.no_grad():
+                kl = torch.sum(torch.log(sigma_b / old_sigma_b + 1.0e-5) +
+                               (torch.square(old_sigma_b) + torch.square(old_mu_b - mu_b)) /
+                               (2.0 * torch.square(sigma_b)) - 0.5, axis=-1)
+                g.segment("kl").copy_(kl.mean().reshape(1))
+        ratio = torch.exp(logp_b - torch.squeeze(old_logp_b))
+        surrogate = -torch.squeeze(adv_b) * ratio
+        surrogate_clipped = -torch.squeeze(adv_b) * torch.clamp(ratio, 1.0 - self.clip_param, 1.0 + self.clip_param)
+        surrogate_loss = torch.max(surrogate, surrogate_clipped).mean()
+        if self.use_clipped_value_loss:
+            value_clipped = target_values_b + (value_b - target_values_b).clamp(-self.clip_param, self.clip_param)
+            value_loss = torch.max((value_b - returns_b).pow(2), (value_clipped - returns_b).pow(2)).mean()
+        else:
+            value_loss = (returns_b - value_b).pow(2).mean()
+        loss = surrogate_loss + self.value_loss_coef * value_loss - self.entropy_coef * entropy_b.mean() + \
+            self._reg_coef * regularization_loss
+        # zero_grad of `optimizer` and `estimator_optimizer` (adaptation grads stay)
+        g.span("main", "estimator").zero_()
+        estimator_loss.backward()
+        loss.backward()
+        with torch.no_grad():
+            self._losses.copy_(torch.stack([value_loss, surrogate_loss, regularization_loss, estimator_loss]))
+        ac.distribution = None
+
+    def _minibatch_step(self):
+        """Phase B: (ranks averaged) clip + estimator step, KL schedule, clip + main step."""
+        g = self.grads
+        with torch.no_grad():
+            _clip_([g.segment("estimator")], self.max_grad_norm)
+        self.estimator_optimizer.step()
+        if self.desired_kl is not None and self.schedule == "adaptive":
+            with torch.no_grad():
+                kl_mean = g.segment("kl")[0].double()
+                lr = self._lr64
+                up = torch.clamp(lr * 1.5, max=1e-2)
+                down = torch.clamp(lr / 1.5, min=1e-5)
+                lr_new = torch.where(kl_mean > self.desired_kl * 2.0, down,
+                                     torch.where((kl_mean < self.desired_kl / 2.0) & (kl_mean > 0.0), up, lr))
+                self._lr64.copy_(lr_new)
+                if self._lr32 is not None:
+                    self._lr32.copy_(lr_new)
+            if self._lr32 is None:  # host Adam (CPU): the schedule value goes to the param groups
+                for grp in self.optimizer.param_groups:
+                    grp["lr"] = float(self._lr64)
+        with torch.no_grad():
+            _clip_([g.segment("main"), g.segment("adaptation")], self.max_grad_norm)
+        self.optimizer.step()
+        with torch.no_grad():
+            self._sums.add_(self._losses)
+
+    def _allreduce_minibatch(self):
+        if _distributed():
+            span = self.grads.span("main", "kl")
+            dist.all_reduce(span)
+            span.div_(dist.get_world_size())
+            # the stale adaptation grads are identical on every rank (averaged at DAgger time)
+
+    def _minibatches(self):
+        mb = self._perm.numel() // self.num_mini_batches
+        return [self._perm[i * mb:(i + 1) * mb] for i in range(self.num_mini_batches)]
+
+    def _update_body_eager(self):
+        slices = self._minibatches()
+        for _ in range(self.num_learning_epochs):
+            for idx in slices:
+                self._minibatch_grads(idx)
+                self._allreduce_minibatch()
+                self._minibatch_step()
+
+    # ------------------------------------------------------------------ graphs
+    def _capture(self):
+        torch.cuda.synchronize(self.device)
+        slices = self._minibatches()
+        pool = torch.cuda.graph_pool_handle()
+        phased = _distributed() if self.phased_graphs is None else self.phased_graphs
+        if not phased:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=pool):
+                for _ in range(self.num_learning_epochs):
+                    for idx in slices:
+                        self._minibatch_grads(idx)
+                        self._minibatch_step()
+            self._graphs = {"whole": g}
+            self.graph_mode = "whole"
+        else:
+            ga = []
+            for idx in slices:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=pool):
+                    self._minibatch_grads(idx)
+                ga.append(g)
+            gb = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gb, pool=pool):
+                self._minibatch_step()
+            self._graphs = {"A": ga, "B": gb}
+            self.graph_mode = "phased"
+
+    def invalidate_graphs(self):
+        self._graphs = None
+        self._eager_updates = 0
+        self.graph_mode = None
+
+    def _run_update(self):
+        if not self.use_graphs:
+            self._update_body_eager()
+            return
+        if self._graphs is None and self._eager_updates < 2:
+            # warm-up on a side stream (lazy optimizer state, autograd + BLAS workspaces)
+            cur = torch.cuda.current_stream(self.device)
+            side = torch.cuda.Stream(self.device)
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                self._update_body_eager()
+            cur.wait_stream(side)
+            self._eager_updates += 1
+            return
+        if self._graphs is None:
+            # capture records, it does not run: the real update is the replay below
+            snap = [p.detach().clone() for p in self._main_params + self._est_params]
+            self._capture()
+            for p, v in zip(self._main_params + self._est_params, snap):
+                assert torch.equal(p.detach(), v), "graph capture must not execute the update"
+        if self.graph_mode == "whole":
+            self._graphs["whole"].replay()
+        else:
+            for _ in range(self.num_learning_epochs):
+                for ga in self._graphs["A"]:
+                    ga.replay()
+                    self._allreduce_minibatch()
+                    self._graphs["B"].replay()
+
+    # ------------------------------------------------------------------ update
+    def update(self):
+        """ppo.py:182-293 (num_learning_epochs x num_mini_batches minibatches)."""
         regularization_coef = self.reg_coef()
-        generator = self.storage.mini_batch_generator(self.num_mini_batches, self.num_learning_epochs)
-        for (obs_b, priv_b, critic_b, est_b, scan_b, actions_b, target_values_b, adv_b, returns_b, old_logp_b,
-             old_mu_b, old_sigma_b, _, _) in generator:
-            ac.act(obs_b, priv_b, est_b, scan_b, adaptation_mode=False)  # TRUE estimated obs here (Q12)
-            logp_b = ac.get_actions_log_prob(actions_b)
-            value_b = ac.evaluate(critic_b)
-            mu_b, sigma_b, entropy_b = ac.action_mean, ac.action_std, ac.entropy
-            priv_latent = ac.privileged_encoder(priv_b)
-            with torch.inference_mode():
-                adapt_latent = ac.adaptation_encoder(obs_b)
-            regularization_loss = (priv_latent - adapt_latent.detach()).norm(p=2, dim=1).mean()
-            # estimator (own optimizer, own clip)
-            pred = self.estimator(obs_b)
-            estimator_loss = (pred - est_b).norm(p=2, dim=1).pow(2).mean()
-            self.estimator_optimizer.zero_grad()
-            estimator_loss.backward()
-            allreduce_grads(list(self.estimator.parameters()))
-            nn.utils.clip_grad_norm_(self.estimator.parameters(), self.max_grad_norm)
-            self.estimator_optimizer.step()
-            if self.desired_kl is not None and self.schedule == "adaptive":
-                with torch.inference_mode():
-                    kl = torch.sum(torch.log(sigma_b / old_sigma_b + 1.0e-5) +
-                                   (torch.square(old_sigma_b) + torch.square(old_mu_b - mu_b)) /
-                                   (2.0 * torch.square(sigma_b)) - 0.5, axis=-1)
-                    kl_mean = torch.mean(kl)
-                    if _distributed():
-                        dist.all_reduce(kl_mean)
-                        kl_mean /= dist.get_world_size()
-                    kl_mean = kl_mean.item()  # the schedule needs the value on the host
-                    if kl_mean > self.desired_kl * 2.0:
-                        self.learning_rate = max(1e-5, self.learning_rate / 1.5)
-                    elif self.desired_kl / 2.0 > kl_mean > 0.0:
-                        self.learning_rate = min(1e-2, self.learning_rate * 1.5)
-                    for g in self.optimizer.param_groups:
-                        g["lr"] = self.learning_rate
-            ratio = torch.exp(logp_b - torch.squeeze(old_logp_b))
-            surrogate = -torch.squeeze(adv_b) * ratio
-            surrogate_clipped = -torch.squeeze(adv_b) * torch.clamp(ratio, 1.0 - self.clip_param, 1.0 + self.clip_param)
-            surrogate_loss = torch.max(surrogate, surrogate_clipped).mean()
-            if self.use_clipped_value_loss:
-                value_clipped = target_values_b + (value_b - target_values_b).clamp(-self.clip_param, self.clip_param)
-                value_loss = torch.max((value_b - returns_b).pow(2), (value_clipped - returns_b).pow(2)).mean()
-            else:
-                value_loss = (returns_b - value_b).pow(2).mean()
-            loss = surrogate_loss + self.value_loss_coef * value_loss - self.entropy_coef * entropy_b.mean() + \
-                regularization_coef * regularization_loss
-            self.optimizer.zero_grad()
-            loss.backward()
-            allreduce_grads(list(ac.parameters()))
-            nn.utils.clip_grad_norm_(ac.parameters(), self.max_grad_norm)
-            self.optimizer.step()
-            sums += torch.stack([value_loss.detach(), surrogate_loss.detach(), regularization_loss.detach(),
-                                 estimator_loss.detach()])
+        self._reg_coef.fill_(regularization_coef)
+        self._sums.zero_()
+        # one permutation shared by all epochs (rollout_storage.py:142, Appendix B Q24)
+        n = self._perm.numel()
+        self._perm.copy_(torch.randperm(n, device=self.device))
+        self._run_update()
         num_updates = self.num_learning_epochs * self.num_mini_batches
-        mv, ms, mr, me = (sums / num_updates).tolist()
+        mv, ms, mr, me, self.learning_rate = torch.cat([(self._sums / num_updates).double(),
+                                                        self._lr64.reshape(1)]).tolist()
         self.storage.clear()
         self.increase_update_count()
         self.enforce_max_std(1.0)
@@ -197,27 +408,65 @@ class PPO:
         self.total_updates += 1
 
     def enforce_max_std(self, max_action_std=1.0):
-        cur = self.actor_critic.std.detach()
-        self.actor_critic.std.data = torch.min(cur, torch.tensor(max_action_std, device=cur.device, dtype=cur.dtype))
+        """ppo.py:299-303 (std = min(std, max)); in place so captured graphs keep the address."""
+        with torch.no_grad():
+            self.actor_critic.std.clamp_(max=max_action_std)
 
     def update_dagger(self):
         """ppo.py:309-349: adaptation-encoder-only imitation of the privileged latent."""
         total = torch.zeros((), device=self.device)
         ac = self.actor_critic
+        g = self.grads
+        adapt = g.segment("adaptation")
         generator = self.storage.mini_batch_generator(self.num_mini_batches, self.num_learning_epochs)
         for obs_b, priv_b, critic_b, est_b, scan_b, actions_b, *_ in generator:
-            with torch.inference_mode():
-                ac.act(obs_b, priv_b, est_b, scan_b, adaptation_mode=True)
+            with torch.no_grad():
                 priv_latent = ac.privileged_encoder(priv_b)
             adapt_latent = ac.adaptation_encoder(obs_b)
-            adaptation_loss = (priv_latent.detach() - adapt_latent).norm(p=2, dim=1).mean()
-            self.adaptation_optimizer.zero_grad()
+            adaptation_loss = (priv_latent - adapt_latent).norm(p=2, dim=1).mean()
+            adapt.zero_()
             adaptation_loss.backward()
-            allreduce_grads(list(ac.adaptation_encoder_.parameters()))
-            nn.utils.clip_grad_norm_(ac.adaptation_encoder_.parameters(), self.max_grad_norm)
+            if _distributed():
+                dist.all_reduce(adapt)
+                adapt.div_(dist.get_world_size())
+            with torch.no_grad():
+                _clip_([adapt], self.max_grad_norm)
             self.adaptation_optimizer.step()
             total += adaptation_loss.detach()
         mean_adaptation_loss = (total / (self.num_learning_epochs * self.num_mini_batches)).item()
         self.storage.clear()
         self.increase_update_count()
         return mean_adaptation_loss
+
+    # ------------------------------------------------------------------ checkpoints
+    def optimizer_state_dicts(self):
+        """{'optimizer_state_dict', 'estimator_optimizer_state_dict',
+        'adaptation_optimizer_state_dict'} in the reference's (plain Adam) format."""
+        return {"optimizer_state_dict": export_adam_state(self.optimizer),
+                "estimator_optimizer_state_dict": export_adam_state(self.estimator_optimizer),
+                "adaptation_optimizer_state_dict": export_adam_state(self.adaptation_optimizer)}
+
+    def load_optimizer_state(self, name, state_dict):
+        """Load a (reference-format or own) Adam state into `name`, then restore this
+        build's execution flags and device-side lr; drops captured graphs."""
+        opt = getattr(self, name)
+        flags = [(grp.get("fused"), grp.get("capturable"), grp["lr"]) for grp in opt.param_groups]
+        opt.load_state_dict(state_dict)
+        for grp, (fused, capt, lr_obj) in zip(opt.param_groups, flags):
+            loaded_lr = float(grp["lr"])
+            grp["fused"], grp["capturable"] = fused, capt
+            if isinstance(lr_obj, torch.Tensor):
+                lr_obj.fill_(loaded_lr)
+                grp["lr"] = lr_obj
+            else:
+                grp["lr"] = loaded_lr
+            if name == "optimizer":
+                self._lr64.fill_(loaded_lr)
+                self.learning_rate = loaded_lr
+        for st in opt.state.values():
+            if "step" in st and self.on_gpu:
+                st["step"] = st["step"].to(device=self.device, dtype=torch.float32)
+        self.invalidate_graphs()
+
+    def after_model_load(self):
+        self.invalidate_graphs()

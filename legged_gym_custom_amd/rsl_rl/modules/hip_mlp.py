@@ -1,0 +1,193 @@
+"""HIP MLP: the rsl_rl networks' Linear/ELU chains on liblgx_mlp.so (include/lgx_mlp.h).
+
+`HipMLP` is an nn.Sequential with the reference's exact children ([Linear, act]*, Linear —
+rsl_rl/modules/actor_critic.py:64-87, support_networks.py:22-33,60-70,100-112), so
+state_dict keys (`actor.0.weight`, ...) and TorchScript-exported layouts are unchanged.
+On a HIP device its forward is ONE autograd node for the whole chain:
+  forward   per layer  Y = ELU(X W^T + b)          bias + ELU fused in the GEMM epilogue
+  backward  per layer  dW, db = dY^T X, sum dY      split-K GEMM, bias grad in the same pass
+                       dX = (dY W) * ELU'(X)        ELU' of the previous layer fused
+so only each layer's output is kept (ELU'(z) = y > 0 ? 1 : y + 1 from the output y).
+On the CPU (the host-side baseline learner) it is the plain nn.Sequential. On a HIP
+device a missing liblgx_mlp.so raises: there is no silent torch fallback.
+"""
+import ctypes as C
+import os
+
+import torch
+import torch.nn as nn
+
+_LIB_PATH = os.environ.get("LGX_MLP_LIB") or os.path.join(
+    os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))), "lib", "liblgx_mlp.so")
+_lib = None
+ABI_VERSION = 1
+EPI_BIAS, EPI_ELU, EPI_DELU, EPI_ACCUM = 1, 2, 4, 8
+EXPORTED = ["lgx_mlp_abi_version", "lgx_mlp_pick_split", "lgx_gemm", "lgx_mlp_last_error"]
+
+
+class GemmArgs(C.Structure):
+    """Mirror of lgx_gemm_args (include/lgx_mlp.h)."""
+    _fields_ = [("A", C.c_void_p), ("lda", C.c_int64), ("a_kcontig", C.c_int32),
+                ("B", C.c_void_p), ("ldb", C.c_int64), ("b_kcontig", C.c_int32),
+                ("C", C.c_void_p), ("ldc", C.c_int64),
+                ("M", C.c_int32), ("N", C.c_int32), ("K", C.c_int32), ("epilogue", C.c_int32),
+                ("bias", C.c_void_p), ("act", C.c_void_p), ("ld_act", C.c_int64),
+                ("split_k", C.c_int32), ("workspace", C.c_void_p), ("colsum", C.c_void_p),
+                ("colsum_ws", C.c_void_p)]
+
+
+class MlpLibError(RuntimeError):
+    pass
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(_LIB_PATH):
+        raise MlpLibError(f"liblgx_mlp.so not built ({_LIB_PATH}); run `python -m legged_gym_custom_amd.build_native`")
+    L = C.CDLL(_LIB_PATH)
+    L.lgx_mlp_abi_version.restype = C.c_int32
+    L.lgx_mlp_pick_split.argtypes = [C.c_int32, C.c_int32, C.c_int32]
+    L.lgx_mlp_pick_split.restype = C.c_int32
+    L.lgx_gemm.argtypes = [C.c_void_p, C.c_void_p]
+    L.lgx_gemm.restype = C.c_int32
+    L.lgx_mlp_last_error.restype = C.c_char_p
+    if L.lgx_mlp_abi_version() != ABI_VERSION:
+        raise MlpLibError("liblgx_mlp ABI version mismatch; rebuild")
+    _lib = L
+    return L
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def _run(args):
+    L = lib()
+    rc = L.lgx_gemm(C.byref(args), C.c_void_p(torch.cuda.current_stream().cuda_stream))
+    if rc != 0:
+        raise MlpLibError("lgx_gemm: " + L.lgx_mlp_last_error().decode())
+
+
+def _rowmajor(t):
+    return t if t.stride(-1) == 1 else t.contiguous()
+
+
+def linear_forward(x, W, b, elu, out=None):
+    """Y[M,N] = act(X[M,K] W[N,K]^T + b)."""
+    x = _rowmajor(x)
+    M, K = x.shape
+    N = W.shape[0]
+    y = out if out is not None else torch.empty(M, N, device=x.device, dtype=torch.float32)
+    _run(GemmArgs(A=_ptr(x), lda=x.stride(0), a_kcontig=1, B=_ptr(W), ldb=W.stride(0), b_kcontig=1,
+                  C=_ptr(y), ldc=y.stride(0), M=M, N=N, K=K, epilogue=EPI_BIAS | (EPI_ELU if elu else 0),
+                  bias=_ptr(b), split_k=1))
+    return y
+
+
+def linear_input_grad(g, W, y_prev=None, Wt=None):
+    """dX[M,K] = (dY[M,N] W[N,K]) * ELU'(y_prev) (when the layer input is an ELU output).
+    W is read through its transpose (Wt[K,N], contiguous) so both operands stream k-contiguous."""
+    g = _rowmajor(g)
+    M, N = g.shape
+    K = W.shape[1]
+    Wt = W.t().contiguous() if Wt is None else Wt
+    dx = torch.empty(M, K, device=g.device, dtype=torch.float32)
+    _run(GemmArgs(A=_ptr(g), lda=g.stride(0), a_kcontig=1, B=_ptr(Wt), ldb=Wt.stride(0), b_kcontig=1,
+                  C=_ptr(dx), ldc=dx.stride(0), M=M, N=K, K=N, epilogue=EPI_DELU if y_prev is not None else 0,
+                  act=_ptr(y_prev), ld_act=0 if y_prev is None else y_prev.stride(0), split_k=1))
+    return dx
+
+
+def linear_weight_grad(g, x):
+    """dW[N,K] = dY[M,N]^T X[M,K], db[N] = sum_m dY[m,:] (split-K, deterministic)."""
+    g = _rowmajor(g)
+    x = _rowmajor(x)
+    rows, N = g.shape
+    K = x.shape[1]
+    split = max(2, int(lib().lgx_mlp_pick_split(N, K, rows)))
+    dev = g.device
+    dW = torch.empty(N, K, device=dev, dtype=torch.float32)
+    db = torch.empty(N, device=dev, dtype=torch.float32)
+    ws = torch.empty(split * N * K + split * N, device=dev, dtype=torch.float32)
+    _run(GemmArgs(A=_ptr(g), lda=g.stride(0), a_kcontig=0, B=_ptr(x), ldb=x.stride(0), b_kcontig=0,
+                  C=_ptr(dW), ldc=dW.stride(0), M=N, N=K, K=rows, epilogue=0, split_k=split,
+                  workspace=_ptr(ws), colsum=_ptr(db), colsum_ws=ws.data_ptr() + 4 * split * N * K))
+    return dW, db
+
+
+class _MLPFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, elu_flags, *wb):
+        n = len(elu_flags)
+        outs = []
+        h = x
+        for i in range(n):
+            h = linear_forward(h, wb[2 * i], wb[2 * i + 1], elu_flags[i])
+            outs.append(h)
+        ctx.elu_flags = elu_flags
+        ctx.save_for_backward(x, *wb, *outs)
+        return h
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        flags = ctx.elu_flags
+        n = len(flags)
+        saved = ctx.saved_tensors
+        x, wb, outs = saved[0], saved[1:1 + 2 * n], saved[1 + 2 * n:]
+        g = grad_out
+        if flags[-1]:  # a chain ending in an activation (not built by _mlp): its ELU' on the incoming grad
+            y = outs[-1]
+            g = g * torch.where(y > 0, torch.ones_like(y), y + 1.0)
+        grads = [None] * (2 * n)
+        dx = None
+        for i in reversed(range(n)):
+            inp = x if i == 0 else outs[i - 1]
+            grads[2 * i], grads[2 * i + 1] = linear_weight_grad(g, inp)
+            if i > 0:
+                g = linear_input_grad(g, wb[2 * i], outs[i - 1] if flags[i - 1] else None)
+            elif ctx.needs_input_grad[0]:
+                dx = linear_input_grad(g, wb[0], None)
+        return (dx, None, *grads)
+
+
+def mlp_forward(x, weights, biases, elu_flags):
+    """Whole chain on the HIP device (autograd-aware)."""
+    wb = [t for pair in zip(weights, biases) for t in pair]
+    needs_graph = torch.is_grad_enabled() and (x.requires_grad or any(t.requires_grad for t in wb))
+    if not needs_graph:
+        h = x
+        for W, b, e in zip(weights, biases, elu_flags):
+            h = linear_forward(h, W, b, e)
+        return h
+    return _MLPFunction.apply(x, tuple(elu_flags), *wb)
+
+
+class HipMLP(nn.Sequential):
+    """nn.Sequential of [Linear, ELU]* Linear that runs as fused HIP GEMMs on the GPU."""
+
+    def _chain(self):
+        layers, flags = [], []
+        mods = list(self)
+        i = 0
+        while i < len(mods):
+            m = mods[i]
+            if not isinstance(m, nn.Linear) or m.bias is None:
+                return None
+            act = mods[i + 1] if i + 1 < len(mods) and not isinstance(mods[i + 1], nn.Linear) else None
+            if act is not None and not (isinstance(act, nn.ELU) and act.alpha == 1.0):
+                return None
+            layers.append(m)
+            flags.append(act is not None)
+            i += 2 if act is not None else 1
+        return layers, flags
+
+    def forward(self, x):
+        if x.device.type != "cuda":
+            return super().forward(x)
+        chain = self._chain()
+        if chain is None:  # an activation the fused epilogues do not cover (only ELU is built)
+            return super().forward(x)
+        layers, flags = chain
+        return mlp_forward(x, [m.weight for m in layers], [m.bias for m in layers], flags)

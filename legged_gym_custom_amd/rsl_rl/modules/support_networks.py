@@ -3,6 +3,8 @@ names (scan_encoder, estimator, priv_encoder, fc_encoder, conv_layers, fc_final)
 kept so state_dict keys match reference checkpoints and TorchScript exports."""
 import torch.nn as nn
 
+from .hip_mlp import HipMLP
+
 
 def get_activation(act_name):
     table = {"elu": nn.ELU, "selu": nn.SELU, "relu": nn.ReLU, "crelu": nn.ReLU, "lrelu": nn.LeakyReLU,
@@ -14,14 +16,15 @@ def get_activation(act_name):
 
 
 def _mlp(in_dim, hidden, out_dim, activation):
-    """[Linear, act] per hidden layer, last Linear -> out_dim (same layout as the reference)."""
+    """[Linear, act] per hidden layer, last Linear -> out_dim (same layout as the reference);
+    a HipMLP, i.e. fused HIP GEMMs on the GPU."""
     layers = [nn.Linear(in_dim, hidden[0]), activation]
     for i in range(len(hidden)):
         if i == len(hidden) - 1:
             layers.append(nn.Linear(hidden[i], out_dim))
         else:
             layers += [nn.Linear(hidden[i], hidden[i + 1]), activation]
-    return nn.Sequential(*layers)
+    return HipMLP(*layers)
 
 
 class ScanEncoder(nn.Module):

@@ -217,23 +217,25 @@ class OnPolicyRunner:
         print(s)
 
     def save(self, path, infos=None):
+        opt = self.alg.optimizer_state_dicts()
         torch.save({"model_state_dict": self.alg.actor_critic.state_dict(),
-                    "optimizer_state_dict": self.alg.optimizer.state_dict(),
+                    "optimizer_state_dict": opt["optimizer_state_dict"],
                     "iter": self.current_learning_iteration, "infos": infos,
                     "estimator_state_dict": self.alg.estimator.state_dict(),
-                    "estimator_optimizer_state_dict": self.alg.estimator_optimizer.state_dict(),
-                    "adaptation_optimizer_state_dict": self.alg.adaptation_optimizer.state_dict()}, path)
+                    "estimator_optimizer_state_dict": opt["estimator_optimizer_state_dict"],
+                    "adaptation_optimizer_state_dict": opt["adaptation_optimizer_state_dict"]}, path)
 
     def load(self, path, load_optimizer=True):
         loaded = torch.load(path, map_location=self.device, weights_only=True)
         self.alg.actor_critic.load_state_dict(loaded["model_state_dict"])
         if load_optimizer:
-            self.alg.optimizer.load_state_dict(loaded["optimizer_state_dict"])
+            self.alg.load_optimizer_state("optimizer", loaded["optimizer_state_dict"])
         if "estimator_state_dict" in loaded:
             self.alg.estimator.load_state_dict(loaded["estimator_state_dict"])
             if load_optimizer and "estimator_optimizer_state_dict" in loaded:
-                self.alg.estimator_optimizer.load_state_dict(loaded["estimator_optimizer_state_dict"])
-                self.alg.adaptation_optimizer.load_state_dict(loaded["adaptation_optimizer_state_dict"])
+                self.alg.load_optimizer_state("estimator_optimizer", loaded["estimator_optimizer_state_dict"])
+                self.alg.load_optimizer_state("adaptation_optimizer", loaded["adaptation_optimizer_state_dict"])
+        self.alg.after_model_load()
         self.current_learning_iteration = loaded["iter"]
         return loaded["infos"]
 

@@ -87,9 +87,10 @@ class RolloutStorage:
             delta = self.rewards[step] + not_terminal * gamma * next_values - self.values[step]
             advantage = delta + not_terminal * gamma * lam * advantage
             self.returns[step] = advantage + self.values[step]
-        self.advantages = self.returns - self.values
+        # in place: the captured update graph reads this buffer's address
+        torch.sub(self.returns, self.values, out=self.advantages)
         mean, std = self._global_mean(self.advantages)
-        self.advantages = (self.advantages - mean) / (std + 1e-8)
+        self.advantages.sub_(mean).div_(std + 1e-8)
 
     def _global_mean(self, a):
         """(mean, unbiased std) of `a` over every rank's shard."""
@@ -111,15 +112,23 @@ class RolloutStorage:
         trajectory_lengths = done_indices[1:] - done_indices[:-1]
         return trajectory_lengths.float().mean(), self.rewards.mean()
 
+    def _flat(self):
+        return [t.flatten(0, 1) for t in (self.observations, self.privileged_observations, self.critic_observations,
+                                          self.true_estimated_observations, self.scan_observations, self.actions,
+                                          self.values, self.advantages, self.returns, self.actions_log_prob,
+                                          self.mu, self.sigma)]
+
+    def gather(self, idx):
+        """The minibatch rows `idx` of every flattened [T*N, .] buffer (same tuple order
+        as mini_batch_generator's first 12 fields)."""
+        return tuple(t[idx] for t in self._flat())
+
     def mini_batch_generator(self, num_mini_batches, num_epochs=8):
         batch_size = self.num_envs * self.num_transitions_per_env
         mini_batch_size = batch_size // num_mini_batches
         # one permutation shared by all epochs (rollout_storage.py:142, Appendix B Q24)
         indices = torch.randperm(num_mini_batches * mini_batch_size, requires_grad=False, device=self.device)
-        flat = [t.flatten(0, 1) for t in (self.observations, self.privileged_observations, self.critic_observations,
-                                          self.true_estimated_observations, self.scan_observations, self.actions,
-                                          self.values, self.advantages, self.returns, self.actions_log_prob,
-                                          self.mu, self.sigma)]
+        flat = self._flat()
         for _ in range(num_epochs):
             for i in range(num_mini_batches):
                 idx = indices[i * mini_batch_size:(i + 1) * mini_batch_size]

@@ -1,0 +1,45 @@
+"""hipGraph-captured PPO update == the same update run eagerly (MI355X)."""
+import copy
+
+import pytest
+import torch
+
+from test_ppo_update import _fill, _make
+
+pytestmark = pytest.mark.gpu
+
+
+def _to_gpu(alg_cpu, use_graphs, phased=None):
+    from legged_gym_custom_amd.rsl_rl.algorithms import PPO
+    ac = copy.deepcopy(alg_cpu.actor_critic)
+    est = copy.deepcopy(alg_cpu.estimator)
+    alg = PPO(ac, est, num_learning_epochs=alg_cpu.num_learning_epochs, num_mini_batches=alg_cpu.num_mini_batches,
+              learning_rate=alg_cpu.learning_rate, schedule=alg_cpu.schedule, desired_kl=alg_cpu.desired_kl,
+              max_grad_norm=alg_cpu.max_grad_norm, device="cuda:0", use_graphs=use_graphs)
+    alg.phased_graphs = phased
+    s = alg_cpu.storage
+    alg.init_storage(s.num_envs, s.num_transitions_per_env, list(s.obs_shape), list(s.privileged_obs_shape),
+                     list(s.critic_obs_shape), list(s.estimated_obs_shape), [s.scan_observations.shape[-1]],
+                     [s.actions.shape[-1]])
+    return alg
+
+
+@pytest.mark.parametrize("phased", [False, True])
+def test_graph_update_matches_eager(phased):
+    base = _make("adaptive")
+    eager = _to_gpu(base, use_graphs=False)
+    graph = _to_gpu(base, use_graphs=True, phased=phased)
+    for it in range(5):
+        for alg in (eager, graph):
+            _fill(alg, 10 + it)
+        torch.manual_seed(100 + it)
+        le = eager.update()
+        torch.manual_seed(100 + it)
+        lg = graph.update()
+        torch.testing.assert_close(torch.tensor(lg), torch.tensor(le), rtol=1e-4, atol=1e-6)
+        assert graph.learning_rate == pytest.approx(eager.learning_rate, rel=1e-9)
+    assert graph.graph_mode == ("phased" if phased else "whole")
+    for a, b in zip(list(graph.actor_critic.parameters()) + list(graph.estimator.parameters()),
+                    list(eager.actor_critic.parameters()) + list(eager.estimator.parameters())):
+        torch.testing.assert_close(a.detach(), b.detach(), rtol=1e-4, atol=1e-6)
+    assert graph.grads.check()

@@ -1,0 +1,82 @@
+"""liblgx_mlp.so GEMMs (3 x bf16 MFMA split, fp32 accumulate) vs fp64 references.
+
+Bound per output: |C - C64| <= 3e-5 * sum_k |A(m,k) B(k,n)| + 1e-6 — the split's
+~2^-16 relative product error plus fp32 accumulation; TF32 (what the reference trains
+with, train.py:39) would need ~5e-4 * sum|ab|."""
+import pytest
+import torch
+
+from legged_gym_custom_amd.rsl_rl.modules import hip_mlp as H
+
+pytestmark = pytest.mark.gpu
+dev = "cuda:0"
+
+
+def _bound(A, B):
+    return 3e-5 * (A.abs().double() @ B.abs().double()) + 1e-6
+
+
+@pytest.mark.parametrize("M,N,K", [(24576, 512, 627), (1000, 13, 37), (4096, 12, 128), (77, 300, 736), (3, 1, 5)])
+def test_forward_bias_elu(M, N, K):
+    g = torch.Generator(device=dev).manual_seed(M + N + K)
+    x = torch.randn(M, K, device=dev, generator=g)
+    W = torch.randn(N, K, device=dev, generator=g) / K ** 0.5
+    b = torch.randn(N, device=dev, generator=g)
+    for elu in (False, True):
+        y = H.linear_forward(x, W, b, elu)
+        z = x.double() @ W.double().t() + b.double()
+        ref = torch.nn.functional.elu(z) if elu else z
+        err = (y.double() - ref).abs()
+        assert (err <= _bound(x, W.t())).all(), float(err.max())
+
+
+@pytest.mark.parametrize("M,N,K", [(24576, 627, 512), (500, 29, 64), (4096, 128, 12)])
+def test_input_grad_with_elu_derivative(M, N, K):
+    # dX[M,N] = dY[M,K] W[K,N] * ELU'(y_prev)
+    g = torch.Generator(device=dev).manual_seed(7 * M + N)
+    dy = torch.randn(M, K, device=dev, generator=g)
+    W = torch.randn(K, N, device=dev, generator=g) / N ** 0.5
+    y_prev = torch.nn.functional.elu(torch.randn(M, N, device=dev, generator=g) * 2)
+    dx = H.linear_input_grad(dy, W, y_prev)
+    d = torch.where(y_prev > 0, torch.ones_like(y_prev), y_prev + 1).double()
+    ref = (dy.double() @ W.double()) * d
+    err = (dx.double() - ref).abs()
+    assert (err <= _bound(dy, W) * d + 1e-6).all(), float(err.max())
+    dx2 = H.linear_input_grad(dy, W, None)
+    assert ((dx2.double() - dy.double() @ W.double()).abs() <= _bound(dy, W)).all()
+
+
+@pytest.mark.parametrize("rows,N,K", [(24576, 512, 627), (24576, 12, 128), (1000, 20, 29), (300, 64, 132)])
+def test_weight_and_bias_grad(rows, N, K):
+    g = torch.Generator(device=dev).manual_seed(rows + 3 * N)
+    dy = torch.randn(rows, N, device=dev, generator=g)
+    x = torch.randn(rows, K, device=dev, generator=g)
+    dW, db = H.linear_weight_grad(dy, x)
+    ref = dy.double().t() @ x.double()
+    err = (dW.double() - ref).abs()
+    assert (err <= _bound(dy.t(), x)).all(), float(err.max())
+    # the bias gradient is summed in fp32 from the unsplit values: fp32 summation bound
+    assert ((db.double() - dy.double().sum(0)).abs() <= 1e-6 * dy.double().abs().sum(0) + 1e-6).all()
+    # deterministic (fixed split-K reduction order)
+    dW2, db2 = H.linear_weight_grad(dy, x)
+    assert torch.equal(dW, dW2) and torch.equal(db, db2)
+
+
+def test_mlp_autograd_matches_fp64():
+    from legged_gym_custom_amd.rsl_rl.modules.support_networks import _mlp
+    torch.manual_seed(0)
+    net = _mlp(627, [512, 256, 128], 12, torch.nn.ELU()).to(dev)
+    ref = _mlp(627, [512, 256, 128], 12, torch.nn.ELU()).double()
+    ref.load_state_dict({k: v.double().cpu() for k, v in net.state_dict().items()})
+    x = torch.randn(3000, 627, device=dev, requires_grad=True)
+    xr = x.detach().double().cpu().requires_grad_(True)
+    y = net(x)
+    yr = torch.nn.Sequential.forward(ref, xr)
+    torch.testing.assert_close(y.double().cpu(), yr, rtol=1e-4, atol=1e-4)
+    w = torch.randn_like(y)
+    (y * w).sum().backward()
+    (yr * w.double().cpu()).sum().backward()
+    torch.testing.assert_close(x.grad.double().cpu(), xr.grad, rtol=1e-3, atol=1e-5)
+    for (n, p), (_, pr) in zip(net.named_parameters(), ref.named_parameters()):
+        scale = pr.grad.abs().max().item()
+        torch.testing.assert_close(p.grad.double().cpu(), pr.grad, rtol=1e-3, atol=1e-4 * scale, msg=n)

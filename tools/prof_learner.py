@@ -6,6 +6,7 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import torch  # noqa: E402
+torch.set_float32_matmul_precision(os.environ.get("PREC", "high"))
 from legged_gym_custom_amd.envs import task_registry  # noqa: E402
 from legged_gym_custom_amd.utils.helpers import get_args  # noqa: E402
 
