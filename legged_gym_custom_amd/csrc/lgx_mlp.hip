@@ -1,29 +1,34 @@
 // lgx_mlp.hip — fused MLP-layer GEMMs for the rsl_rl learner on gfx950 (include/lgx_mlp.h).
 //
-// Block: 256 threads = 4 waves, output tile 128 x 64, K step 32. Each wave owns a 64 x 32
-// sub-tile = 4 x 2 MFMA tiles of v_mfma_f32_16x16x32_bf16. fp32 operands are split on
-// the way into LDS, x = hi + lo (hi = bf16(x), lo = bf16(x - hi)), and every product is
-// lo*hi + hi*lo + hi*hi accumulated in fp32 (3 x bf16 MFMA, ~2^-16 relative per product).
+// Block: 256 threads = 4 waves; output tile 128 x BN (BN = 128: waves 2 x 2 of 64 x 64;
+// BN = 64: waves 2 x 2 of 64 x 32); K step 32. Products run on v_mfma_f32_16x16x32_bf16:
+// fp32 operands are split on the way into LDS, x = hi + lo (hi = bf16(x), lo = bf16(x - hi)),
+// and every product is lo*hi + hi*lo + hi*hi accumulated in fp32 (~2^-16 relative).
 //
-// Staging goes through registers (the split needs them anyway), so both global layouts
-// land in the same LDS image: [row = m or n][k], k contiguous, 80-B row pitch
-// (conflict-free ds_read_b128 fragment reads: row r of a 16-lane group hits banks
-// 20r mod 64 .. +3). K-contiguous operands: 4 lanes cover one row's 32 k (128 B, float4
-// loads when aligned); MN-contiguous operands: consecutive lanes take consecutive rows,
-// 8 k each (coalesced 256-B rows per load instruction). Double-buffered LDS, one
-// barrier per K step, next tile's global loads in flight during the MFMAs.
-//
-// Epilogues fuse what the torch graph runs as separate kernels: bias + ELU (forward),
-// ELU'(y) of the previous layer (input gradient), split-K partials + the bias gradient
-// (column sums of dY) in the weight-gradient pass; a small deterministic reduce adds
-// the split-K partials (fixed order, no atomics).
+// Operand staging ("stager" modes) goes through registers — the split needs them anyway —
+// so every global layout lands in the same LDS image [row = m or n][k] (k contiguous,
+// 80-B row pitch: conflict-free ds_read_b128 fragment reads):
+//   KS/KV  k-contiguous rows, 8 consecutive k per lane (KV: two float4 loads)
+//   MS     m/n-contiguous, one row per lane, 8 k (coalesced 4-B lanes)
+//   MV     m/n-contiguous, float4 along m/n: a lane loads a 4-row x (ROWS/32)-k block
+// Pipeline: double-buffered LDS; two register sets, so a K step's global loads are
+// issued two steps before they are staged; one barrier per step.
+// Grid: 1-D, XCD-aware — each XCD gets a contiguous run of logical tiles (n fastest),
+// so blocks sharing an A row-block run together on one XCD's L2.
+// Epilogue through an fp32 LDS image of the tile, then row-contiguous float4 traffic:
+//   forward   + bias, ELU                    input grad  * ELU'(y_prev) (y_prev prefetched)
+//   weight grad split-K partials to a workspace + the bias gradient (column sums of dY,
+//   taken from the unsplit fp32 values), reduced in fixed order by splitk_reduce.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 #include "../../include/lgx_mlp.h"
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 namespace lgxm {
@@ -31,6 +36,7 @@ namespace lgxm {
 constexpr int BM = 128, BKS = 32, NT = 256;
 constexpr int PITCH = BKS + 8;           // bf16 per LDS row (80 B)
 constexpr int A_ELEMS = BM * PITCH;      // one A image (hi or lo)
+enum Mode { KS = 0, KV = 1, MS = 2, MV = 3 };
 
 struct Params {
   const float* A; int64_t lda;
@@ -44,68 +50,142 @@ struct Params {
   int tiles_m, tiles_n, tiles;           // logical tile grid (per split) and total incl. splits
   float* ws;
   float* colsum_ws;
+  int c_vec, act_vec, ws_vec;            // row-aligned float4 access allowed for C / act / ws
 };
 
-// 8 consecutive-k values of one tile row; GUARD = tile crosses an M/N/K edge.
-template <bool KCONTIG, bool VEC, bool GUARD>
-__device__ __forceinline__ void load8(const float* __restrict__ p, int64_t ld, int row, int rows, int k, int kend,
-                                      float v[8]) {
-  if (KCONTIG) {
-    const float* q = p + (int64_t)row * ld + k;
-    if (!GUARD && VEC) {
-      const float4 x0 = *reinterpret_cast<const float4*>(q);
-      const float4 x1 = *reinterpret_cast<const float4*>(q + 4);
-      v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w;
-      v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
-    } else if (!GUARD) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = q[j];
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = (row < rows && k + j < kend) ? q[j] : 0.f;
-    }
-  } else {
-    const float* q = p + (int64_t)k * ld + row;
-    if (!GUARD) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = q[(int64_t)j * ld];
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = (row < rows && k + j < kend) ? q[(int64_t)j * ld] : 0.f;
-    }
-  }
-}
-
-__device__ __forceinline__ void split_store(__bf16* hi, __bf16* lo, int off, const float v[8]) {
-  bf16x8 h, l;
+__device__ __forceinline__ void split8(const float* v, bf16x8& h, bf16x8& l) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const __bf16 b = (__bf16)v[j];
     h[j] = b;
     l[j] = (__bf16)(v[j] - (float)b);
   }
-  *reinterpret_cast<bf16x8*>(hi + off) = h;
-  *reinterpret_cast<bf16x8*>(lo + off) = l;
 }
 
-// task -> (row, kgroup) of a tile with ROWS rows and 4 k-groups of 8
-template <bool KCONTIG, int ROWS>
-__device__ __forceinline__ void task_rc(int task, int& r, int& g) {
-  if (KCONTIG) { r = task >> 2; g = task & 3; }
-  else { r = task % ROWS; g = task / ROWS; }
-}
+// Staging of one operand tile [ROWS][BKS] — R = ROWS/8 floats per thread.
+template <int MODE, int ROWS>
+struct Stager {
+  static constexpr int R = ROWS / 8;
+  static constexpr int T = ROWS / 64;          // 8-k tasks per thread (KS/KV/MS)
+  static constexpr int KG = ROWS / 32;         // k per float4 row (MV)
+  static constexpr int RG = ROWS / 4;          // 4-row groups (MV)
 
-// Block tile BM x BN_ (BN_ = 64: waves 2x2 of 64x32; BN_ = 128: waves 2x2 of 64x64).
-template <bool AK, bool BKC, bool VA, bool VB, bool COLSUM, int BN_>
+  // GUARD: the tile crosses the M/N edge or the K end of this split.
+  template <bool GUARD>
+  __device__ __forceinline__ static void load(const float* __restrict__ p, int64_t ld, int row0, int rows, int k0,
+                                              int kend, int tid, float (&v)[R]) {
+    if (MODE == KS || MODE == KV) {
+#pragma unroll
+      for (int t = 0; t < T; ++t) {
+        const int idx = tid + t * NT, r = idx >> 2, g = idx & 3;
+        const int row = row0 + r, k = k0 + g * 8;
+        const float* q = p + (int64_t)row * ld + k;
+        float* o = v + t * 8;
+        if (!GUARD && MODE == KV) {
+          const float4 x0 = *reinterpret_cast<const float4*>(q);
+          const float4 x1 = *reinterpret_cast<const float4*>(q + 4);
+          o[0] = x0.x; o[1] = x0.y; o[2] = x0.z; o[3] = x0.w;
+          o[4] = x1.x; o[5] = x1.y; o[6] = x1.z; o[7] = x1.w;
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] = (!GUARD || (row < rows && k + j < kend)) ? q[j] : 0.f;
+        }
+      }
+    } else if (MODE == MS) {
+#pragma unroll
+      for (int t = 0; t < T; ++t) {
+        const int idx = tid + t * NT, r = idx % ROWS, g = idx / ROWS;
+        const int row = row0 + r, k = k0 + g * 8;
+        const float* q = p + (int64_t)k * ld + row;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          v[t * 8 + j] = (!GUARD || (row < rows && k + j < kend)) ? q[(int64_t)j * ld] : 0.f;
+      }
+    } else {  // MV
+      const int rg = tid % RG, kq = tid / RG;
+      const int row = row0 + rg * 4, k = k0 + kq * KG;
+#pragma unroll
+      for (int kk = 0; kk < KG; ++kk) {
+        const float* q = p + (int64_t)(k + kk) * ld + row;
+        if (!GUARD) {
+          const float4 x = *reinterpret_cast<const float4*>(q);
+          v[kk * 4 + 0] = x.x; v[kk * 4 + 1] = x.y; v[kk * 4 + 2] = x.z; v[kk * 4 + 3] = x.w;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[kk * 4 + e] = (row + e < rows && k + kk < kend) ? q[e] : 0.f;
+        }
+      }
+    }
+  }
+
+  __device__ __forceinline__ static void store(__bf16* hi, __bf16* lo, int tid, const float (&v)[R]) {
+    if (MODE != MV) {
+#pragma unroll
+      for (int t = 0; t < T; ++t) {
+        const int idx = tid + t * NT;
+        int r, g;
+        if (MODE == MS) { r = idx % ROWS; g = idx / ROWS; }
+        else { r = idx >> 2; g = idx & 3; }
+        bf16x8 h, l;
+        split8(v + t * 8, h, l);
+        *reinterpret_cast<bf16x8*>(hi + r * PITCH + g * 8) = h;
+        *reinterpret_cast<bf16x8*>(lo + r * PITCH + g * 8) = l;
+      }
+    } else {
+      const int rg = tid % RG, kq = tid / RG;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int off = (rg * 4 + e) * PITCH + kq * KG;
+        if (KG == 4) {
+          bf16x4 h, l;
+#pragma unroll
+          for (int kk = 0; kk < 4; ++kk) {
+            const float x = v[kk * 4 + e];
+            const __bf16 b = (__bf16)x;
+            h[kk] = b;
+            l[kk] = (__bf16)(x - (float)b);
+          }
+          *reinterpret_cast<bf16x4*>(hi + off) = h;
+          *reinterpret_cast<bf16x4*>(lo + off) = l;
+        } else {
+          bf16x2 h, l;
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk) {
+            const float x = v[kk * 4 + e];
+            const __bf16 b = (__bf16)x;
+            h[kk] = b;
+            l[kk] = (__bf16)(x - (float)b);
+          }
+          *reinterpret_cast<bf16x2*>(hi + off) = h;
+          *reinterpret_cast<bf16x2*>(lo + off) = l;
+        }
+      }
+    }
+  }
+
+  // Row sums of the A tile (bias gradient): this thread's contribution per owned row.
+  // MS: one row (tid % ROWS), slot tid / ROWS; MV: rows 4*rg + e, slot kq.
+  __device__ __forceinline__ static void colsum(const float (&v)[R], float (&cs)[4]) {
+    if (MODE == MS) {
+#pragma unroll
+      for (int j = 0; j < R; ++j) cs[0] += v[j];
+    } else if (MODE == MV) {
+#pragma unroll
+      for (int kk = 0; kk < KG; ++kk)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) cs[e] += v[kk * 4 + e];
+    }
+  }
+};
+
+template <int AM, int BMODE, bool COLSUM, int BN_>
 __global__ __launch_bounds__(NT, 2) void gemm_kernel(Params p) {
+  using SA = Stager<AM, BM>;
+  using SB = Stager<BMODE, BN_>;
   constexpr int NJ = BN_ / 32;             // 16-wide MFMA column tiles per wave
-  constexpr int BT = BN_ * 32 / 8 / NT;    // B staging tasks per thread
   constexpr int B_ELEMS = BN_ * PITCH;
   constexpr int STAGE = 2 * A_ELEMS + 2 * B_ELEMS;
   extern __shared__ __align__(16) __bf16 lds[];
-  // XCD-aware logical tile: hardware spreads consecutive block ids over the 8 XCDs, so
-  // give each XCD a contiguous run of logical tiles (n fastest, then m, then split):
-  // blocks sharing an A row-block run together on one XCD and hit its L2.
   const int per_xcd = (p.tiles + 7) >> 3;
   const int L = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
   if (L >= p.tiles) return;
@@ -120,55 +200,22 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(Params p) {
   const int wm = (wave & 1) * 64, wn = (wave >> 1) * (BN_ / 2);
   const bool mn_in = (m0 + BM <= p.M) && (n0 + BN_ <= p.N);
 
-  float va[2][8], vb[BT][8];
-  float csum = 0.f;
-  auto gload = [&](int k0) {
+  float va0[SA::R], vb0[SB::R], va1[SA::R], vb1[SB::R];
+  float csum[4] = {0.f, 0.f, 0.f, 0.f};
+  auto gload = [&](float (&va)[SA::R], float (&vb)[SB::R], int k0) {
     if (mn_in && k0 + BKS <= kend) {
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        int r, g;
-        task_rc<AK, BM>(tid + t * NT, r, g);
-        load8<AK, VA, false>(p.A, p.lda, m0 + r, p.M, k0 + g * 8, kend, va[t]);
-      }
-#pragma unroll
-      for (int t = 0; t < BT; ++t) {
-        int r, g;
-        task_rc<BKC, BN_>(tid + t * NT, r, g);
-        load8<BKC, VB, false>(p.B, p.ldb, n0 + r, p.N, k0 + g * 8, kend, vb[t]);
-      }
+      SA::template load<false>(p.A, p.lda, m0, p.M, k0, kend, tid, va);
+      SB::template load<false>(p.B, p.ldb, n0, p.N, k0, kend, tid, vb);
     } else {
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        int r, g;
-        task_rc<AK, BM>(tid + t * NT, r, g);
-        load8<AK, VA, true>(p.A, p.lda, m0 + r, p.M, k0 + g * 8, kend, va[t]);
-      }
-#pragma unroll
-      for (int t = 0; t < BT; ++t) {
-        int r, g;
-        task_rc<BKC, BN_>(tid + t * NT, r, g);
-        load8<BKC, VB, true>(p.B, p.ldb, n0 + r, p.N, k0 + g * 8, kend, vb[t]);
-      }
+      SA::template load<true>(p.A, p.lda, m0, p.M, k0, kend, tid, va);
+      SB::template load<true>(p.B, p.ldb, n0, p.N, k0, kend, tid, vb);
     }
   };
-  auto sstore = [&](int buf) {
+  auto sstore = [&](const float (&va)[SA::R], const float (&vb)[SB::R], int buf) {
     __bf16* base = lds + buf * STAGE;
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      int r, g;
-      task_rc<AK, BM>(tid + t * NT, r, g);
-      split_store(base, base + A_ELEMS, r * PITCH + g * 8, va[t]);
-      if (COLSUM) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) csum += va[t][j];
-      }
-    }
-#pragma unroll
-    for (int t = 0; t < BT; ++t) {
-      int r, g;
-      task_rc<BKC, BN_>(tid + t * NT, r, g);
-      split_store(base + 2 * A_ELEMS, base + 2 * A_ELEMS + B_ELEMS, r * PITCH + g * 8, vb[t]);
-    }
+    SA::store(base, base + A_ELEMS, tid, va);
+    SB::store(base + 2 * A_ELEMS, base + 2 * A_ELEMS + B_ELEMS, tid, vb);
+    if (COLSUM) SA::colsum(va, csum);
   };
 
   f32x4 acc[4][NJ];
@@ -177,15 +224,8 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(Params p) {
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if (nsteps > 0) {
-    gload(kbeg);
-    sstore(0);
-  }
-  __syncthreads();
   const int fr = lane & 15, fk = (lane >> 4) * 8;
-  for (int s = 0; s < nsteps; ++s) {
-    const int buf = s & 1;
-    if (s + 1 < nsteps) gload(kbeg + (s + 1) * BKS);
+  auto compute = [&](int buf) {
     const __bf16* base = lds + buf * STAGE;
     const __bf16* ahi = base;
     const __bf16* alo = base + A_ELEMS;
@@ -210,53 +250,129 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(Params p) {
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh[j], acc[i][j], 0, 0, 0);
       }
     }
-    if (s + 1 < nsteps) sstore(buf ^ 1);
+  };
+  // step s: MFMAs on LDS[s&1]; stage step s+1 (registers loaded two steps ago) into
+  // LDS[(s+1)&1]; refill those registers with step s+3; one barrier.
+  auto step = [&](int s, float (&va)[SA::R], float (&vb)[SB::R]) {
+    compute(s & 1);
+    if (s + 1 < nsteps) sstore(va, vb, (s + 1) & 1);
+    if (s + 3 < nsteps) gload(va, vb, kbeg + (s + 3) * BKS);
+    __syncthreads();
+  };
+
+  if (nsteps > 0) {
+    gload(va0, vb0, kbeg);
+    sstore(va0, vb0, 0);
+    if (nsteps > 1) gload(va1, vb1, kbeg + BKS);
+    if (nsteps > 2) gload(va0, vb0, kbeg + 2 * BKS);
+  }
+  __syncthreads();
+  for (int s = 0; s < nsteps; s += 2) {
+    step(s, va1, vb1);
+    if (s + 1 < nsteps) step(s + 1, va0, vb0);
+  }
+
+  float* cs = reinterpret_cast<float*>(lds);
+  // bias gradient partial: this block's A rows summed over its K range (n-tile 0 only)
+  if (COLSUM) {
+    if (tn == 0) {
+      constexpr int SLOTS = AM == MV ? NT / (BM / 4) : NT / BM;
+      if (AM == MV) {
+        const int rg = tid % (BM / 4), kq = tid / (BM / 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) cs[kq * BM + rg * 4 + e] = csum[e];
+      } else {
+        cs[(tid / BM) * BM + tid % BM] = csum[0];
+      }
+      __syncthreads();
+      if (tid < BM) {
+        float v = 0.f;
+#pragma unroll
+        for (int sl = 0; sl < SLOTS; ++sl) v += cs[sl * BM + tid];
+        if (m0 + tid < p.M) p.colsum_ws[(int64_t)z * p.M + m0 + tid] = v;
+      }
+    }
     __syncthreads();
   }
 
-  // bias gradient partial: this block's A rows summed over its K range (n-tile 0 only)
-  if (COLSUM && tn == 0) {
-    float* red = reinterpret_cast<float*>(lds);
-    red[tid] = csum;
-    __syncthreads();
-    if (tid < BM) {
-      const float v = red[tid] + red[tid + BM];
-      if (m0 + tid < p.M) p.colsum_ws[(int64_t)z * p.M + m0 + tid] = v;
+  // epilogue through LDS: MFMA C/D map (col = lane & 15, row = (lane >> 4) * 4 + r) into a
+  // [BM][BN_ + 4] fp32 image, then row-contiguous float4 reads/writes of C (and act).
+  constexpr int CP = BN_ + 4;
+  constexpr int CH = BN_ / 4;              // float4 chunks per row
+  constexpr int IT = BM * CH / NT;         // chunks per thread
+  const bool part = p.split > 1;
+  const bool delu = !part && (p.epi & LGX_EPI_DELU);
+  // ELU outputs of the previous layer: issue every load before the tile is even staged
+  float4 yv[IT];
+  if (delu) {
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int idx = tid + it * NT;
+      const int m = m0 + idx / CH, n = n0 + (idx % CH) * 4;
+      const float* ap = p.act + (int64_t)m * p.ld_act + n;
+      if (m < p.M && n + 4 <= p.N && p.act_vec) {
+        yv[it] = *reinterpret_cast<const float4*>(ap);
+      } else {
+        float y[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) y[e] = (m < p.M && n + e < p.N) ? ap[e] : 0.f;
+        yv[it] = make_float4(y[0], y[1], y[2], y[3]);
+      }
     }
   }
-
-  // epilogue: C/D map of 16x16 MFMA tiles: col = lane & 15, row = (lane >> 4) * 4 + r
   const int ec = lane & 15, er = (lane >> 4) * 4;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int n = n0 + wn + j * 16 + ec;
-      if (n >= p.N) continue;
-      float bn = 0.f;
-      if (p.split == 1 && (p.epi & LGX_EPI_BIAS)) bn = p.bias[n];
+    for (int j = 0; j < NJ; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wm + i * 16 + er + r;
-        if (m >= p.M) continue;
-        float v = acc[i][j][r];
-        if (p.split > 1) {
-          p.ws[((int64_t)z * p.M + m) * p.N + n] = v;
-          continue;
-        }
-        v += bn;
-        if (p.epi & LGX_EPI_ELU) v = v > 0.f ? v : expm1f(v);
-        if (p.epi & LGX_EPI_DELU) {
-          const float y = p.act[(int64_t)m * p.ld_act + n];
-          v *= y > 0.f ? 1.f : y + 1.f;
-        }
-        float* c = p.C + (int64_t)m * p.ldc + n;
-        *c = (p.epi & LGX_EPI_ACCUM) ? *c + v : v;
+      for (int r = 0; r < 4; ++r) cs[(wm + i * 16 + er + r) * CP + wn + j * 16 + ec] = acc[i][j][r];
+  __syncthreads();
+  float* dst = part ? p.ws + (int64_t)z * p.M * p.N : p.C;
+  const int64_t ldd = part ? p.N : p.ldc;
+  const bool dvec = part ? p.ws_vec : p.c_vec;
+  const bool accum = !part && (p.epi & LGX_EPI_ACCUM);
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int idx = tid + it * NT;
+    const int row = idx / CH, c = (idx % CH) * 4;
+    const int m = m0 + row, n = n0 + c;
+    if (m >= p.M || n >= p.N) continue;
+    const float4 t = *reinterpret_cast<const float4*>(cs + row * CP + c);
+    float v[4] = {t.x, t.y, t.z, t.w};
+    const bool full = n + 4 <= p.N;
+    if (!part) {
+      if (p.epi & LGX_EPI_BIAS) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] += (full || n + e < p.N) ? p.bias[n + e] : 0.f;
+      }
+      if (p.epi & LGX_EPI_ELU) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : expm1f(v[e]);
+      }
+      if (delu) {
+        const float y[4] = {yv[it].x, yv[it].y, yv[it].z, yv[it].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] *= y[e] > 0.f ? 1.f : y[e] + 1.f;
       }
     }
+    float* d = dst + (int64_t)m * ldd + n;
+    if (full && dvec) {
+      float4 o = make_float4(v[0], v[1], v[2], v[3]);
+      if (accum) {
+        const float4 q = *reinterpret_cast<const float4*>(d);
+        o.x += q.x; o.y += q.y; o.z += q.z; o.w += q.w;
+      }
+      *reinterpret_cast<float4*>(d) = o;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (n + e < p.N) d[e] = accum ? d[e] + v[e] : v[e];
+    }
+  }
 }
 
-// C (=|+=) epilogue(sum_z ws[z]) and colsum[m] = sum_z colsum_ws[z][m], fixed z order.
+// C (=|+=) epilogue(sum_z ws[z]) and colsum[m] (=|+=) sum_z colsum_ws[z][m], fixed z order.
 __global__ void splitk_reduce(Params p, float* colsum) {
   const int64_t mn = (int64_t)p.M * p.N;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -280,27 +396,30 @@ __global__ void splitk_reduce(Params p, float* colsum) {
   }
 }
 
-template <bool AK, bool BKC, bool VA, bool VB, bool CS>
+// dynamic LDS: two K-step stages of hi/lo A and B images, or the fp32 C image (reused)
+constexpr size_t lds_bytes(int bn) {
+  const size_t stages = 2 * (2 * A_ELEMS + 2 * bn * PITCH) * sizeof(__bf16);
+  const size_t cimg = (size_t)BM * (bn + 4) * sizeof(float);
+  return stages > cimg ? stages : cimg;
+}
+
+template <int AM, int BMODE, bool CS>
 void launch(Params p, int bn, hipStream_t s) {
   p.tiles_m = (p.M + BM - 1) / BM;
   p.tiles_n = (p.N + bn - 1) / bn;
   p.tiles = p.tiles_m * p.tiles_n * p.split;
   const int grid = (p.tiles + 7) / 8 * 8;
   if (bn == 128) {
-    const size_t lds = 2 * (2 * A_ELEMS + 2 * 128 * PITCH) * sizeof(__bf16);
-    hipLaunchKernelGGL((gemm_kernel<AK, BKC, VA, VB, CS, 128>), dim3(grid), dim3(NT), lds, s, p);
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_kernel<AM, BMODE, CS, 128>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes(128));
+      attr = true;
+    }
+    hipLaunchKernelGGL((gemm_kernel<AM, BMODE, CS, 128>), dim3(grid), dim3(NT), lds_bytes(128), s, p);
   } else {
-    const size_t lds = 2 * (2 * A_ELEMS + 2 * 64 * PITCH) * sizeof(__bf16);
-    hipLaunchKernelGGL((gemm_kernel<AK, BKC, VA, VB, CS, 64>), dim3(grid), dim3(NT), lds, s, p);
+    hipLaunchKernelGGL((gemm_kernel<AM, BMODE, CS, 64>), dim3(grid), dim3(NT), lds_bytes(64), s, p);
   }
-}
-
-static bool g_attr_set = false;
-
-template <bool AK, bool BKC, bool VA, bool VB, bool CS>
-void allow_big_lds() {
-  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_kernel<AK, BKC, VA, VB, CS, 128>),
-                      hipFuncAttributeMaxDynamicSharedMemorySize, 2 * (2 * A_ELEMS + 2 * 128 * PITCH) * 2);
 }
 
 }  // namespace lgxm
@@ -314,6 +433,16 @@ static int fail(const char* msg) {
 
 static bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
+static int tile_n(int N) {
+  static int forced = -1;
+  if (forced < 0) {
+    const char* e = getenv("LGX_MLP_BN");  // dev knob: force 64 or 128
+    forced = e ? atoi(e) : 0;
+  }
+  if (forced == 64 || forced == 128) return forced;
+  return N >= 128 ? 128 : 64;
+}
+
 extern "C" {
 
 int32_t lgx_mlp_abi_version(void) { return LGX_MLP_ABI_VERSION; }
@@ -321,13 +450,16 @@ int32_t lgx_mlp_abi_version(void) { return LGX_MLP_ABI_VERSION; }
 const char* lgx_mlp_last_error(void) { return g_err; }
 
 int32_t lgx_mlp_pick_split(int32_t M, int32_t N, int32_t K) {
-  const int bn = N >= 128 ? 128 : 64;
+  const int bn = tile_n(N);
   const int tiles = ((M + lgxm::BM - 1) / lgxm::BM) * ((N + bn - 1) / bn);
-  int s = (1024 + tiles - 1) / tiles;           // ~4 blocks per CU over 256 CUs
+  int s = (768 + tiles - 1) / tiles;            // ~3 blocks per CU over 256 CUs
   const int kmax = (K + 255) / 256;             // keep >= 256 rows of K per split
   if (s > kmax) s = kmax;
+  if (s > 48) s = 48;
+  // cap the partial-sum workspace at ~8 M floats (32 MB)
+  const int64_t mn = (int64_t)M * N;
+  while (s > 2 && (int64_t)s * mn > (8 << 20)) --s;
   if (s < 1) s = 1;
-  if (s > 64) s = 64;
   return s;
 }
 
@@ -344,17 +476,7 @@ int32_t lgx_gemm(const lgx_gemm_args* a, void* stream) {
   const bool cs = a->colsum != nullptr;
   if (cs && (a->a_kcontig || !a->colsum_ws)) return fail("lgx_gemm: colsum needs a_kcontig = 0 and colsum_ws");
   if (cs && split == 1) return fail("lgx_gemm: colsum requires split_k > 1");
-  if (!g_attr_set) {
-    allow_big_lds<true, true, true, true, false>();
-    allow_big_lds<true, true, true, false, false>();
-    allow_big_lds<true, true, false, true, false>();
-    allow_big_lds<true, true, false, false, false>();
-    allow_big_lds<true, false, true, false, false>();
-    allow_big_lds<true, false, false, false, false>();
-    allow_big_lds<false, false, false, false, true>();
-    allow_big_lds<false, false, false, false, false>();
-    g_attr_set = true;
-  }
+  if (a->a_kcontig != a->b_kcontig) return fail("lgx_gemm: mixed operand layouts are not built");
   Params p;
   p.A = a->A; p.lda = a->lda; p.B = a->B; p.ldb = a->ldb; p.C = a->C; p.ldc = a->ldc;
   p.M = a->M; p.N = a->N; p.K = a->K; p.epi = a->epilogue; p.bias = a->bias; p.act = a->act;
@@ -363,23 +485,29 @@ int32_t lgx_gemm(const lgx_gemm_args* a, void* stream) {
   if (p.kchunk == 0) p.kchunk = BKS;
   p.ws = a->workspace;
   p.colsum_ws = a->colsum_ws;
+  p.c_vec = (a->ldc % 4 == 0) && aligned16(a->C);
+  p.act_vec = a->act && (a->ld_act % 4 == 0) && aligned16(a->act);
+  p.ws_vec = (a->N % 4 == 0) && (!a->workspace || aligned16(a->workspace));
   hipStream_t s = static_cast<hipStream_t>(stream);
-  const int bn = a->N >= 128 ? 128 : 64;
-  const bool va = a->a_kcontig && (a->lda % 4 == 0) && aligned16(a->A);
-  const bool vb = a->b_kcontig && (a->ldb % 4 == 0) && aligned16(a->B);
-  if (a->a_kcontig && a->b_kcontig) {
-    if (va && vb) launch<true, true, true, true, false>(p, bn, s);
-    else if (va) launch<true, true, true, false, false>(p, bn, s);
-    else if (vb) launch<true, true, false, true, false>(p, bn, s);
-    else launch<true, true, false, false, false>(p, bn, s);
-  } else if (a->a_kcontig && !a->b_kcontig) {
-    if (va) launch<true, false, true, false, false>(p, bn, s);
-    else launch<true, false, false, false, false>(p, bn, s);
-  } else if (!a->a_kcontig && !a->b_kcontig) {
-    if (cs) launch<false, false, false, false, true>(p, bn, s);
-    else launch<false, false, false, false, false>(p, bn, s);
+  const int bn = tile_n(a->N);
+  // float4 staging needs 16-B aligned rows (k-contiguous) or columns (m/n-contiguous)
+  const bool va = (a->lda % 4 == 0) && aligned16(a->A);
+  const bool vb = (a->ldb % 4 == 0) && aligned16(a->B);
+  if (a->a_kcontig) {
+    if (va && vb) launch<KV, KV, false>(p, bn, s);
+    else if (va) launch<KV, KS, false>(p, bn, s);
+    else if (vb) launch<KS, KV, false>(p, bn, s);
+    else launch<KS, KS, false>(p, bn, s);
+  } else if (cs) {
+    if (va && vb) launch<MV, MV, true>(p, bn, s);
+    else if (va) launch<MV, MS, true>(p, bn, s);
+    else if (vb) launch<MS, MV, true>(p, bn, s);
+    else launch<MS, MS, true>(p, bn, s);
   } else {
-    return fail("lgx_gemm: a_kcontig = 0 with b_kcontig = 1 is not built");
+    if (va && vb) launch<MV, MV, false>(p, bn, s);
+    else if (va) launch<MV, MS, false>(p, bn, s);
+    else if (vb) launch<MS, MV, false>(p, bn, s);
+    else launch<MS, MS, false>(p, bn, s);
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(hipGetErrorString(e));

@@ -100,21 +100,30 @@ def linear_input_grad(g, W, y_prev=None, Wt=None):
     return dx
 
 
-def linear_weight_grad(g, x):
-    """dW[N,K] = dY[M,N]^T X[M,K], db[N] = sum_m dY[m,:] (split-K, deterministic)."""
+def linear_weight_grad(g, x, dW=None, db=None, accumulate=False):
+    """dW[N,K] (+)= dY[M,N]^T X[M,K], db[N] (+)= sum_m dY[m,:] (split-K, deterministic order)."""
     g = _rowmajor(g)
     x = _rowmajor(x)
     rows, N = g.shape
     K = x.shape[1]
     split = max(2, int(lib().lgx_mlp_pick_split(N, K, rows)))
     dev = g.device
-    dW = torch.empty(N, K, device=dev, dtype=torch.float32)
-    db = torch.empty(N, device=dev, dtype=torch.float32)
+    dW = torch.empty(N, K, device=dev, dtype=torch.float32) if dW is None else dW
+    db = torch.empty(N, device=dev, dtype=torch.float32) if db is None else db
     ws = torch.empty(split * N * K + split * N, device=dev, dtype=torch.float32)
     _run(GemmArgs(A=_ptr(g), lda=g.stride(0), a_kcontig=0, B=_ptr(x), ldb=x.stride(0), b_kcontig=0,
-                  C=_ptr(dW), ldc=dW.stride(0), M=N, N=K, K=rows, epilogue=0, split_k=split,
-                  workspace=_ptr(ws), colsum=_ptr(db), colsum_ws=ws.data_ptr() + 4 * split * N * K))
+                  C=_ptr(dW), ldc=dW.stride(0), M=N, N=K, K=rows, epilogue=EPI_ACCUM if accumulate else 0,
+                  split_k=split, workspace=_ptr(ws), colsum=_ptr(db),
+                  colsum_ws=ws.data_ptr() + 4 * split * N * K))
     return dW, db
+
+
+def _grad_of(p):
+    """The parameter's .grad buffer (created zeroed if absent): the weight-gradient pass
+    accumulates into it directly, so autograd has no AccumulateGrad add to run."""
+    if p.grad is None:
+        p.grad = torch.zeros_like(p)
+    return p.grad
 
 
 class _MLPFunction(torch.autograd.Function):
@@ -127,6 +136,7 @@ class _MLPFunction(torch.autograd.Function):
             h = linear_forward(h, wb[2 * i], wb[2 * i + 1], elu_flags[i])
             outs.append(h)
         ctx.elu_flags = elu_flags
+        ctx.params = wb  # the leaf Parameters (their .grad is written in backward)
         ctx.save_for_backward(x, *wb, *outs)
         return h
 
@@ -140,11 +150,13 @@ class _MLPFunction(torch.autograd.Function):
         if flags[-1]:  # a chain ending in an activation (not built by _mlp): its ELU' on the incoming grad
             y = outs[-1]
             g = g * torch.where(y > 0, torch.ones_like(y), y + 1.0)
-        grads = [None] * (2 * n)
+        grads = [None] * (2 * n)  # W/b grads go straight into p.grad (see _grad_of)
         dx = None
         for i in reversed(range(n)):
             inp = x if i == 0 else outs[i - 1]
-            grads[2 * i], grads[2 * i + 1] = linear_weight_grad(g, inp)
+            if ctx.needs_input_grad[2 + 2 * i] or ctx.needs_input_grad[3 + 2 * i]:
+                linear_weight_grad(g, inp, _grad_of(ctx.params[2 * i]), _grad_of(ctx.params[2 * i + 1]),
+                                   accumulate=True)
             if i > 0:
                 g = linear_input_grad(g, wb[2 * i], outs[i - 1] if flags[i - 1] else None)
             elif ctx.needs_input_grad[0]:

@@ -46,7 +46,8 @@ def test_input_grad_with_elu_derivative(M, N, K):
     assert ((dx2.double() - dy.double() @ W.double()).abs() <= _bound(dy, W)).all()
 
 
-@pytest.mark.parametrize("rows,N,K", [(24576, 512, 627), (24576, 12, 128), (1000, 20, 29), (300, 64, 132)])
+@pytest.mark.parametrize("rows,N,K", [(24576, 512, 627), (24576, 12, 128), (1000, 20, 29), (300, 64, 132),
+                                       (24576, 1, 128), (1000, 13, 29), (500, 3, 64), (777, 736, 512)])
 def test_weight_and_bias_grad(rows, N, K):
     g = torch.Generator(device=dev).manual_seed(rows + 3 * N)
     dy = torch.randn(rows, N, device=dev, generator=g)
