@@ -70,49 +70,48 @@ struct Stager {
   static constexpr int KG = ROWS / 32;         // k per float4 row (MV)
   static constexpr int RG = ROWS / 4;          // 4-row groups (MV)
 
-  // GUARD: the tile crosses the M/N edge or the K end of this split.
-  template <bool GUARD>
+  // Rows past the M/N edge are clamped to a valid row (their products only reach outputs
+  // that are never stored), so loads stay vectorised at the edges; KGUARD (the last,
+  // partial K step of a split) zero-fills k >= kend, which does reach valid outputs.
+  template <bool KGUARD>
   __device__ __forceinline__ static void load(const float* __restrict__ p, int64_t ld, int row0, int rows, int k0,
                                               int kend, int tid, float (&v)[R]) {
     if (MODE == KS || MODE == KV) {
 #pragma unroll
       for (int t = 0; t < T; ++t) {
         const int idx = tid + t * NT, r = idx >> 2, g = idx & 3;
-        const int row = row0 + r, k = k0 + g * 8;
+        const int row = min(row0 + r, rows - 1), k = k0 + g * 8;
         const float* q = p + (int64_t)row * ld + k;
         float* o = v + t * 8;
-        if (!GUARD && MODE == KV) {
+        if (!KGUARD && MODE == KV) {
           const float4 x0 = *reinterpret_cast<const float4*>(q);
           const float4 x1 = *reinterpret_cast<const float4*>(q + 4);
           o[0] = x0.x; o[1] = x0.y; o[2] = x0.z; o[3] = x0.w;
           o[4] = x1.x; o[5] = x1.y; o[6] = x1.z; o[7] = x1.w;
         } else {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) o[j] = (!GUARD || (row < rows && k + j < kend)) ? q[j] : 0.f;
+          for (int j = 0; j < 8; ++j) o[j] = (!KGUARD || k + j < kend) ? q[j] : 0.f;
         }
       }
     } else if (MODE == MS) {
 #pragma unroll
       for (int t = 0; t < T; ++t) {
         const int idx = tid + t * NT, r = idx % ROWS, g = idx / ROWS;
-        const int row = row0 + r, k = k0 + g * 8;
+        const int row = min(row0 + r, rows - 1), k = k0 + g * 8;
         const float* q = p + (int64_t)k * ld + row;
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-          v[t * 8 + j] = (!GUARD || (row < rows && k + j < kend)) ? q[(int64_t)j * ld] : 0.f;
+        for (int j = 0; j < 8; ++j) v[t * 8 + j] = (!KGUARD || k + j < kend) ? q[(int64_t)j * ld] : 0.f;
       }
-    } else {  // MV
+    } else {  // MV: rows % 4 == 0 (host), so a 4-row group is all valid or all past the edge
       const int rg = tid % RG, kq = tid / RG;
-      const int row = row0 + rg * 4, k = k0 + kq * KG;
+      const int row = min(row0 + rg * 4, rows - 4), k = k0 + kq * KG;
 #pragma unroll
       for (int kk = 0; kk < KG; ++kk) {
-        const float* q = p + (int64_t)(k + kk) * ld + row;
-        if (!GUARD) {
-          const float4 x = *reinterpret_cast<const float4*>(q);
+        if (!KGUARD || k + kk < kend) {
+          const float4 x = *reinterpret_cast<const float4*>(p + (int64_t)(k + kk) * ld + row);
           v[kk * 4 + 0] = x.x; v[kk * 4 + 1] = x.y; v[kk * 4 + 2] = x.z; v[kk * 4 + 3] = x.w;
         } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[kk * 4 + e] = (row + e < rows && k + kk < kend) ? q[e] : 0.f;
+          v[kk * 4 + 0] = v[kk * 4 + 1] = v[kk * 4 + 2] = v[kk * 4 + 3] = 0.f;
         }
       }
     }
@@ -198,12 +197,11 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(Params p) {
   const int kend = min(p.K, kbeg + p.kchunk);
   const int nsteps = kend > kbeg ? (kend - kbeg + BKS - 1) / BKS : 0;
   const int wm = (wave & 1) * 64, wn = (wave >> 1) * (BN_ / 2);
-  const bool mn_in = (m0 + BM <= p.M) && (n0 + BN_ <= p.N);
 
   float va0[SA::R], vb0[SB::R], va1[SA::R], vb1[SB::R];
   float csum[4] = {0.f, 0.f, 0.f, 0.f};
   auto gload = [&](float (&va)[SA::R], float (&vb)[SB::R], int k0) {
-    if (mn_in && k0 + BKS <= kend) {
+    if (k0 + BKS <= kend) {
       SA::template load<false>(p.A, p.lda, m0, p.M, k0, kend, tid, va);
       SB::template load<false>(p.B, p.ldb, n0, p.N, k0, kend, tid, vb);
     } else {
@@ -490,9 +488,9 @@ int32_t lgx_gemm(const lgx_gemm_args* a, void* stream) {
   p.ws_vec = (a->N % 4 == 0) && (!a->workspace || aligned16(a->workspace));
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int bn = tile_n(a->N);
-  // float4 staging needs 16-B aligned rows (k-contiguous) or columns (m/n-contiguous)
-  const bool va = (a->lda % 4 == 0) && aligned16(a->A);
-  const bool vb = (a->ldb % 4 == 0) && aligned16(a->B);
+  // float4 staging needs 16-B aligned rows (k-contiguous) or 4-aligned columns (m/n-contiguous)
+  const bool va = (a->lda % 4 == 0) && aligned16(a->A) && (a->a_kcontig || a->M % 4 == 0);
+  const bool vb = (a->ldb % 4 == 0) && aligned16(a->B) && (a->b_kcontig || a->N % 4 == 0);
   if (a->a_kcontig) {
     if (va && vb) launch<KV, KV, false>(p, bn, s);
     else if (va) launch<KV, KS, false>(p, bn, s);
