@@ -74,6 +74,22 @@ def _rowmajor(t):
     return t if t.stride(-1) == 1 else t.contiguous()
 
 
+def gemm_raw(A, lda, a_kcontig, B, ldb, b_kcontig, C, ldc, M, N, K, epilogue=0, bias=None, act=None, ld_act=0):
+    """One lgx_gemm on raw device addresses (ints) — for strided sub-views such as the
+    conv1d windows of the adaptation encoder. k-contiguous operands only (split_k 1)."""
+    _run(GemmArgs(A=A, lda=lda, a_kcontig=a_kcontig, B=B, ldb=ldb, b_kcontig=b_kcontig, C=C, ldc=ldc,
+                  M=M, N=N, K=K, epilogue=epilogue, bias=bias, act=act, ld_act=ld_act, split_k=1))
+
+
+def weight_grad_raw(G, ldg, X, ldx, rows, N, K, dW, db):
+    """dW[N,K] += sum_r G[r*ldg + n] X[r*ldx + k]; db[N] += sum_r G[r*ldg + n] (raw addresses)."""
+    split = max(2, int(lib().lgx_mlp_pick_split(N, K, rows)))
+    ws = torch.empty(split * N * K + split * N, device=dW.device, dtype=torch.float32)
+    _run(GemmArgs(A=G, lda=ldg, a_kcontig=0, B=X, ldb=ldx, b_kcontig=0, C=dW.data_ptr(), ldc=dW.stride(0),
+                  M=N, N=K, K=rows, epilogue=EPI_ACCUM, split_k=split, workspace=ws.data_ptr(),
+                  colsum=db.data_ptr(), colsum_ws=ws.data_ptr() + 4 * split * N * K))
+
+
 def linear_forward(x, W, b, elu, out=None):
     """Y[M,N] = act(X[M,K] W[N,K]^T + b)."""
     x = _rowmajor(x)
@@ -203,3 +219,112 @@ class HipMLP(nn.Sequential):
             return super().forward(x)
         layers, flags = chain
         return mlp_forward(x, [m.weight for m in layers], [m.bias for m in layers], flags)
+
+
+# ---------------------------------------------------------------------------------------
+# Adaptation encoder (support_networks.py:116-175): Linear(P->30)+ELU per history step,
+# Conv1d(30->20, k4, s2)+ELU, Conv1d(20->10, k2, s1)+ELU, Flatten, Linear(30->out)+ELU.
+# Kept channels-last ([B, time, ch]) so every conv1d output position t reads ONE
+# contiguous window (k x ch floats at row offset t*stride*ch): a conv is L_out GEMMs on
+# strided row views. Weights are re-laid to the window order (tap-major) per call.
+# ---------------------------------------------------------------------------------------
+def _conv_w(w):
+    """Conv1d weight [out, in, k] -> [out, k*in] (tap-major, matches the window layout)."""
+    return w.permute(0, 2, 1).reshape(w.shape[0], -1).contiguous()
+
+
+def _final_w(w, c3, l2):
+    """fc_final weight indexed by torch's flatten (c*L + t) -> our (t*C + c) order."""
+    return w.reshape(w.shape[0], c3, l2).permute(0, 2, 1).reshape(w.shape[0], -1).contiguous()
+
+
+def _conv_dims(mod, H):
+    c1 = mod.fc_encoder[0].out_features
+    conv1, conv2 = mod.conv_layers[0], mod.conv_layers[2]
+    k1, s1 = conv1.kernel_size[0], conv1.stride[0]
+    k2, s2 = conv2.kernel_size[0], conv2.stride[0]
+    L1 = (H - k1) // s1 + 1
+    L2 = (L1 - k2) // s2 + 1
+    return c1, conv1.out_channels, conv2.out_channels, k1, s1, k2, s2, L1, L2
+
+
+class _AdaptationFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h, dims, fc_w, fc_b, c1_w, c1_b, c2_w, c2_b, f_w, f_b):
+        C1, C2, C3, k1, s1, k2, s2, L1, L2 = dims
+        Bn, H, P = h.shape
+        dev = h.device
+        x = _rowmajor(h.reshape(Bn * H, P))
+        y0 = linear_forward(x, fc_w, fc_b, True)                         # [B, H, C1]
+        W1 = _conv_w(c1_w)
+        y1 = torch.empty(Bn, L1, C2, device=dev)
+        for t in range(L1):
+            gemm_raw(y0.data_ptr() + 4 * t * s1 * C1, H * C1, 1, W1.data_ptr(), W1.stride(0), 1,
+                     y1.data_ptr() + 4 * t * C2, L1 * C2, Bn, C2, k1 * C1, EPI_BIAS | EPI_ELU, c1_b.data_ptr())
+        W2 = _conv_w(c2_w)
+        y2 = torch.empty(Bn, L2, C3, device=dev)
+        for t in range(L2):
+            gemm_raw(y1.data_ptr() + 4 * t * s2 * C2, L1 * C2, 1, W2.data_ptr(), W2.stride(0), 1,
+                     y2.data_ptr() + 4 * t * C3, L2 * C3, Bn, C3, k2 * C2, EPI_BIAS | EPI_ELU, c2_b.data_ptr())
+        Wf = _final_w(f_w, C3, L2)
+        out = linear_forward(y2.reshape(Bn, L2 * C3), Wf, f_b, True)
+        ctx.dims = dims
+        ctx.params = (fc_w, fc_b, c1_w, c1_b, c2_w, c2_b, f_w, f_b)
+        ctx.save_for_backward(x, y0, y1, y2, out, W1, W2, Wf)
+        return out
+
+    @staticmethod
+    def backward(ctx, g_out):
+        C1, C2, C3, k1, s1, k2, s2, L1, L2 = ctx.dims
+        x, y0, y1, y2, out, W1, W2, Wf = ctx.saved_tensors
+        fc_w, fc_b, c1_w, c1_b, c2_w, c2_b, f_w, f_b = ctx.params
+        Bn = out.shape[0]
+        H = y0.shape[0] // Bn
+        dev = out.device
+        # fc_final (its output ELU first)
+        gz = g_out * torch.where(out > 0, torch.ones_like(out), out + 1.0)
+        dWf = torch.zeros_like(Wf)
+        linear_weight_grad(gz, y2.reshape(Bn, L2 * C3), dWf, _grad_of(f_b), accumulate=True)
+        _grad_of(f_w).add_(dWf.reshape(-1, L2, C3).permute(0, 2, 1).reshape(f_w.shape[0], -1))
+        g2 = linear_input_grad(gz, Wf, y2.reshape(Bn, L2 * C3))          # [B, L2, C3], pre-activation
+        # conv2: per output position t, window t*s2 .. t*s2+k2-1 of y1
+        dW2 = torch.zeros_like(W2)
+        g1 = torch.zeros(Bn, L1, C2, device=dev)
+        W2t = W2.t().contiguous()
+        for t in range(L2):
+            gp = g2.data_ptr() + 4 * t * C3
+            weight_grad_raw(gp, L2 * C3, y1.data_ptr() + 4 * t * s2 * C2, L1 * C2, Bn, C3, k2 * C2, dW2,
+                            _grad_of(c2_b))
+            gemm_raw(gp, L2 * C3, 1, W2t.data_ptr(), W2t.stride(0), 1, g1.data_ptr() + 4 * t * s2 * C2, L1 * C2,
+                     Bn, k2 * C2, C3, EPI_DELU | EPI_ACCUM, act=y1.data_ptr() + 4 * t * s2 * C2, ld_act=L1 * C2)
+        _grad_of(c2_w).add_(dW2.reshape(C3, k2, C2).permute(0, 2, 1))
+        # conv1
+        dW1 = torch.zeros_like(W1)
+        g0 = torch.zeros(Bn, H, C1, device=dev)
+        W1t = W1.t().contiguous()
+        for t in range(L1):
+            gp = g1.data_ptr() + 4 * t * C2
+            weight_grad_raw(gp, L1 * C2, y0.data_ptr() + 4 * t * s1 * C1, H * C1, Bn, C2, k1 * C1, dW1,
+                            _grad_of(c1_b))
+            gemm_raw(gp, L1 * C2, 1, W1t.data_ptr(), W1t.stride(0), 1, g0.data_ptr() + 4 * t * s1 * C1, H * C1,
+                     Bn, k1 * C1, C2, EPI_DELU | EPI_ACCUM, act=y0.data_ptr() + 4 * t * s1 * C1, ld_act=H * C1)
+        _grad_of(c1_w).add_(dW1.reshape(C2, k1, C1).permute(0, 2, 1))
+        # fc_encoder over all B*H steps
+        g0 = g0.reshape(Bn * H, C1)
+        linear_weight_grad(g0, x, _grad_of(fc_w), _grad_of(fc_b), accumulate=True)
+        dh = None
+        if ctx.needs_input_grad[0]:
+            dh = linear_input_grad(g0, fc_w, None).reshape(Bn, H, -1)
+        return (dh, None) + (None,) * 8
+
+
+def adaptation_forward(mod, hist):
+    """AdaptationEncoder.forward on the HIP GEMMs; hist [B, H, P]."""
+    H = hist.shape[1]
+    dims = _conv_dims(mod, H)
+    if dims[8] * dims[2] != mod.fc_final[0].in_features:
+        raise ValueError(f"adaptation encoder: flatten size {dims[8] * dims[2]} != fc_final input "
+                         f"{mod.fc_final[0].in_features} (the reference assumes history 10, Q17)")
+    ps = (mod.fc_encoder[0].weight, mod.fc_encoder[0].bias, mod.conv_layers[0].weight, mod.conv_layers[0].bias,
+          mod.conv_layers[2].weight, mod.conv_layers[2].bias, mod.fc_final[0].weight, mod.fc_final[0].bias)
+    return _AdaptationFn.apply(hist, dims, *ps)

@@ -87,6 +87,9 @@ class AdaptationEncoder(nn.Module):
         self.fc_final = nn.Sequential(nn.Linear(3 * ch, output_dim), self.activation)
 
     def forward(self, unflattened_obs_history):
+        if unflattened_obs_history.device.type == "cuda" and isinstance(self.activation, nn.ELU):
+            from .hip_mlp import adaptation_forward  # channels-last conv1d as HIP GEMMs
+            return adaptation_forward(self, unflattened_obs_history)
         x = self.fc_encoder(unflattened_obs_history)
         x = self.conv_layers(x.permute(0, 2, 1))
         return self.fc_final(x)

@@ -81,3 +81,24 @@ def test_mlp_autograd_matches_fp64():
     for (n, p), (_, pr) in zip(net.named_parameters(), ref.named_parameters()):
         scale = pr.grad.abs().max().item()
         torch.testing.assert_close(p.grad.double().cpu(), pr.grad, rtol=1e-3, atol=1e-4 * scale, msg=n)
+
+
+def test_adaptation_encoder_matches_torch_fp64():
+    """Channels-last conv1d-as-GEMM adaptation encoder vs the module's own torch path (fp64)."""
+    from legged_gym_custom_amd.rsl_rl.modules.support_networks import AdaptationEncoder
+    torch.manual_seed(0)
+    enc = AdaptationEncoder(num_proprio=52, history_buffer_length=10, output_dim=20).to(dev)
+    ref = AdaptationEncoder(num_proprio=52, history_buffer_length=10, output_dim=20).double()
+    ref.load_state_dict({k: v.double().cpu() for k, v in enc.state_dict().items()})
+    h = torch.randn(2000, 10, 52, device=dev, requires_grad=True)
+    hr = h.detach().double().cpu().requires_grad_(True)
+    y = enc(h)
+    yr = ref(hr)  # CPU -> torch conv1d path
+    torch.testing.assert_close(y.double().cpu(), yr, rtol=1e-4, atol=1e-4)
+    w = torch.randn_like(y)
+    (y * w).sum().backward()
+    (yr * w.double().cpu()).sum().backward()
+    torch.testing.assert_close(h.grad.double().cpu(), hr.grad, rtol=1e-3, atol=1e-5)
+    for (n, p), (_, pr) in zip(enc.named_parameters(), ref.named_parameters()):
+        scale = pr.grad.abs().max().item()
+        torch.testing.assert_close(p.grad.double().cpu(), pr.grad, rtol=1e-3, atol=1e-4 * scale, msg=n)
