@@ -50,6 +50,8 @@ typedef struct lgx_gemm_args {
 } lgx_gemm_args;
 
 int32_t lgx_mlp_abi_version(void);
+/* sizeof(lgx_gemm_args) as compiled (binding layout check; no device needed). */
+int32_t lgx_mlp_sizeof_gemm_args(void);
 /* Suggested split-K factor for an M x N x K weight-gradient GEMM. */
 int32_t lgx_mlp_pick_split(int32_t M, int32_t N, int32_t K);
 int32_t lgx_gemm(const lgx_gemm_args* args, void* stream);

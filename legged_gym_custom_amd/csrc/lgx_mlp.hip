@@ -445,6 +445,8 @@ extern "C" {
 
 int32_t lgx_mlp_abi_version(void) { return LGX_MLP_ABI_VERSION; }
 
+int32_t lgx_mlp_sizeof_gemm_args(void) { return (int32_t)sizeof(lgx_gemm_args); }
+
 const char* lgx_mlp_last_error(void) { return g_err; }
 
 int32_t lgx_mlp_pick_split(int32_t M, int32_t N, int32_t K) {

@@ -393,8 +393,7 @@ class PPO:
         self._reg_coef.fill_(regularization_coef)
         self._sums.zero_()
         # one permutation shared by all epochs (rollout_storage.py:142, Appendix B Q24)
-        n = self._perm.numel()
-        self._perm.copy_(torch.randperm(n, device=self.device))
+        self._perm.copy_(self._next_perm(self._perm.numel()))
         self._run_update()
         num_updates = self.num_learning_epochs * self.num_mini_batches
         mv, ms, mr, me, self.learning_rate = torch.cat([(self._sums / num_updates).double(),
@@ -403,6 +402,10 @@ class PPO:
         self.increase_update_count()
         self.enforce_max_std(1.0)
         return mv, ms, mr, regularization_coef, me
+
+    def _next_perm(self, n):
+        """The epoch-shared minibatch permutation (rollout_storage.py:142)."""
+        return torch.randperm(n, device=self.device)
 
     def increase_update_count(self):
         self.total_updates += 1
@@ -413,26 +416,29 @@ class PPO:
             self.actor_critic.std.clamp_(max=max_action_std)
 
     def update_dagger(self):
-        """ppo.py:309-349: adaptation-encoder-only imitation of the privileged latent."""
+        """ppo.py:309-349: adaptation-encoder-only imitation of the privileged latent
+        (same epoch-shared permutation and minibatch slices as update())."""
         total = torch.zeros((), device=self.device)
         ac = self.actor_critic
-        g = self.grads
-        adapt = g.segment("adaptation")
-        generator = self.storage.mini_batch_generator(self.num_mini_batches, self.num_learning_epochs)
-        for obs_b, priv_b, critic_b, est_b, scan_b, actions_b, *_ in generator:
-            with torch.no_grad():
-                priv_latent = ac.privileged_encoder(priv_b)
-            adapt_latent = ac.adaptation_encoder(obs_b)
-            adaptation_loss = (priv_latent - adapt_latent).norm(p=2, dim=1).mean()
-            adapt.zero_()
-            adaptation_loss.backward()
-            if _distributed():
-                dist.all_reduce(adapt)
-                adapt.div_(dist.get_world_size())
-            with torch.no_grad():
-                _clip_([adapt], self.max_grad_norm)
-            self.adaptation_optimizer.step()
-            total += adaptation_loss.detach()
+        adapt = self.grads.segment("adaptation")
+        self._perm.copy_(self._next_perm(self._perm.numel()))
+        slices = self._minibatches()
+        for _ in range(self.num_learning_epochs):
+            for idx in slices:
+                obs_b, priv_b = self.storage.gather_fields(idx, ("observations", "privileged_observations"))
+                with torch.no_grad():
+                    priv_latent = ac.privileged_encoder(priv_b)
+                adapt_latent = ac.adaptation_encoder(obs_b)
+                adaptation_loss = (priv_latent - adapt_latent).norm(p=2, dim=1).mean()
+                adapt.zero_()
+                adaptation_loss.backward()
+                if _distributed():
+                    dist.all_reduce(adapt)
+                    adapt.div_(dist.get_world_size())
+                with torch.no_grad():
+                    _clip_([adapt], self.max_grad_norm)
+                self.adaptation_optimizer.step()
+                total += adaptation_loss.detach()
         mean_adaptation_loss = (total / (self.num_learning_epochs * self.num_mini_batches)).item()
         self.storage.clear()
         self.increase_update_count()

@@ -22,7 +22,8 @@ _LIB_PATH = os.environ.get("LGX_MLP_LIB") or os.path.join(
 _lib = None
 ABI_VERSION = 1
 EPI_BIAS, EPI_ELU, EPI_DELU, EPI_ACCUM = 1, 2, 4, 8
-EXPORTED = ["lgx_mlp_abi_version", "lgx_mlp_pick_split", "lgx_gemm", "lgx_mlp_last_error"]
+EXPORTED = ["lgx_mlp_abi_version", "lgx_mlp_sizeof_gemm_args", "lgx_mlp_pick_split", "lgx_gemm",
+            "lgx_mlp_last_error"]
 
 
 class GemmArgs(C.Structure):
@@ -55,6 +56,10 @@ def lib():
     L.lgx_mlp_last_error.restype = C.c_char_p
     if L.lgx_mlp_abi_version() != ABI_VERSION:
         raise MlpLibError("liblgx_mlp ABI version mismatch; rebuild")
+    L.lgx_mlp_sizeof_gemm_args.restype = C.c_int32
+    if L.lgx_mlp_sizeof_gemm_args() != C.sizeof(GemmArgs):
+        raise MlpLibError(f"lgx_gemm_args layout mismatch: C {L.lgx_mlp_sizeof_gemm_args()} vs ctypes "
+                          f"{C.sizeof(GemmArgs)}")
     _lib = L
     return L
 

@@ -123,6 +123,10 @@ class RolloutStorage:
         as mini_batch_generator's first 12 fields)."""
         return tuple(t[idx] for t in self._flat())
 
+    def gather_fields(self, idx, names):
+        """Minibatch rows `idx` of the named [T, N, .] buffers only."""
+        return tuple(getattr(self, n).flatten(0, 1)[idx] for n in names)
+
     def mini_batch_generator(self, num_mini_batches, num_epochs=8):
         batch_size = self.num_envs * self.num_transitions_per_env
         mini_batch_size = batch_size // num_mini_batches

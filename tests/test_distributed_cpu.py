@@ -1,0 +1,133 @@
+"""Env-sharded multi-process learner on CPU with gloo, world_size 2.
+
+Each rank holds its own envs' rollout. The only exchanges are the advantage moments
+(one all-reduce of {sum a, sum a^2, n}) and, per minibatch, one all-reduce of the flat
+[main | estimator | kl] gradient buffer. With equal per-rank minibatches the result must
+equal ONE process learning on the union of the shards with the union minibatches
+(means of means = mean of the union), and every rank must end with identical weights."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from test_ppo_update import N, T, _make
+
+WORLD = 2
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rollout(seed, n_envs):
+    """Synthetic [T, n_envs, .] rollout fields + last values (seeded)."""
+    g = torch.Generator().manual_seed(seed)
+    alg = _make("adaptive")
+    s = alg.storage
+    shapes = {name: (T, n_envs) + tuple(getattr(s, name).shape[2:]) for name in
+              ("observations", "privileged_observations", "critic_observations", "true_estimated_observations",
+               "scan_observations", "actions", "rewards", "values", "mu", "sigma", "actions_log_prob", "dones")}
+    d = {k: torch.randn(v, generator=g) for k, v in shapes.items()}
+    d["sigma"] = d["sigma"].abs() + 0.5
+    d["actions_log_prob"] = -d["actions_log_prob"].abs() * 5
+    d["dones"] = (torch.rand(shapes["dones"], generator=g) < 0.2).byte()
+    return d, torch.randn(n_envs, 1, generator=g)
+
+
+def _load(alg, d, last_values):
+    s = alg.storage
+    for k, v in d.items():
+        getattr(s, k).copy_(v)
+    s.step = T
+    s.compute_returns(last_values, alg.gamma, alg.lam)
+
+
+def _flat_params(alg):
+    return torch.cat([p.detach().reshape(-1) for p in list(alg.actor_critic.parameters()) +
+                      list(alg.estimator.parameters())])
+
+
+def _worker(rank, port, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        torch.manual_seed(0)
+        alg = _make("adaptive", seed=0)  # identical init on every rank
+        alg._next_perm = lambda n: torch.arange(n)
+        d, lv = _rollout(100 + rank, N)
+        _load(alg, d, lv)
+        adv = alg.storage.advantages.clone()
+        alg.update_dagger()
+        _load(alg, d, lv)
+        alg.update()
+        out[rank] = {"adv": adv, "params": _flat_params(alg), "lr": alg.learning_rate,
+                     "adapt_grads": alg.grads.segment("adaptation").clone()}
+    finally:
+        dist.destroy_process_group()
+
+
+def _union_perm(n_local, mb):
+    """Union-storage rows of minibatch i = rank 0's rows i*mb.. then rank 1's (flat row
+    t*N + n of a shard -> t*2N + rank*N + n of the union)."""
+    blocks = []
+    for i in range(n_local * T // mb):
+        for r in range(WORLD):
+            f = torch.arange(i * mb, (i + 1) * mb)
+            t, n = f // n_local, f % n_local
+            blocks.append(t * (WORLD * n_local) + r * n_local + n)
+    return torch.cat(blocks)
+
+
+@pytest.fixture(scope="module")
+def sharded():
+    out = mp.Manager().dict()
+    mp.spawn(_worker, args=(_port(), out), nprocs=WORLD, join=True)
+    return dict(out)
+
+
+@pytest.fixture(scope="module")
+def union():
+    import test_ppo_update as tpu
+    shards = [_rollout(100 + r, N) for r in range(WORLD)]
+    saved = tpu.N
+    tpu.N = WORLD * N
+    try:
+        alg = _make("adaptive", seed=0)
+    finally:
+        tpu.N = saved
+    d = {k: torch.cat([s[0][k] for s in shards], dim=1) for k in shards[0][0]}
+    lv = torch.cat([s[1] for s in shards], dim=0)
+    mb = N * T // alg.num_mini_batches
+    perm = _union_perm(N, mb)
+    alg._next_perm = lambda n: perm
+    _load(alg, d, lv)
+    adv = alg.storage.advantages.clone()
+    alg.update_dagger()
+    _load(alg, d, lv)
+    alg.update()
+    return {"adv": adv, "params": _flat_params(alg), "lr": alg.learning_rate,
+            "adapt_grads": alg.grads.segment("adaptation").clone()}
+
+
+def test_advantages_normalised_with_global_moments(sharded, union):
+    for r in range(WORLD):
+        torch.testing.assert_close(sharded[r]["adv"], union["adv"][:, r * N:(r + 1) * N], rtol=1e-5, atol=1e-6)
+
+
+def test_ranks_end_identical(sharded):
+    assert torch.equal(sharded[0]["params"], sharded[1]["params"])
+    assert sharded[0]["lr"] == sharded[1]["lr"]
+
+
+def test_sharded_update_equals_union_update(sharded, union):
+    torch.testing.assert_close(sharded[0]["params"], union["params"], rtol=1e-4, atol=2e-6)
+    assert sharded[0]["lr"] == pytest.approx(union["lr"], rel=1e-12)
+    torch.testing.assert_close(sharded[0]["adapt_grads"], union["adapt_grads"], rtol=1e-3, atol=1e-7)

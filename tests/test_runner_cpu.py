@@ -1,0 +1,52 @@
+"""OnPolicyRunner host logic on the CPU (oracle env, torch-CPU learner): the learn loop
+(DAgger at it % 20 == 0, then PPO), and checkpoints in the reference's format
+(on_policy_runner.py:283-297) that load back into a fresh runner."""
+import os
+
+import torch
+
+from legged_gym_custom_amd import model as mdl, params as prm
+from legged_gym_custom_amd.envs import task_registry_configs
+from legged_gym_custom_amd.rsl_rl.runners import OnPolicyRunner
+from legged_gym_custom_amd.utils.helpers import class_to_dict
+
+
+def _runner(log_dir, n=16, steps=4):
+    import cpu_env
+    cfg, tcfg = task_registry_configs("go2")
+    cfg.env.num_envs = n
+    m = mdl.load_model(cfg.asset.file, cfg.asset.foot_name)
+    P = prm.build_task_params(cfg, m, n)
+    env = cpu_env.OracleVecEnv(cfg, m, P, mdl.to_struct(m))
+    tcfg.runner.num_steps_per_env = steps
+    torch.manual_seed(1)
+    return OnPolicyRunner(env, class_to_dict(tcfg), log_dir, device="cpu")
+
+
+def test_learn_saves_reference_format_checkpoints(tmp_path):
+    r = _runner(str(tmp_path))
+    r.learn(2, init_at_random_ep_len=True)
+    assert r.current_learning_iteration == 2
+    files = sorted(os.listdir(tmp_path))
+    assert "model_0.pt" in files and "model_2.pt" in files
+    ck = torch.load(os.path.join(tmp_path, "model_2.pt"), weights_only=True)
+    for k in ("model_state_dict", "optimizer_state_dict", "iter", "infos"):
+        assert k in ck
+    assert ck["iter"] == 2
+    assert "actor.0.weight" in ck["model_state_dict"] and ck["model_state_dict"]["actor.0.weight"].shape == (512, 627)
+    assert "adaptation_encoder_.conv_layers.0.weight" in ck["model_state_dict"]
+    groups = ck["optimizer_state_dict"]["param_groups"]
+    assert len(groups) == 5 and all(isinstance(g["lr"], float) for g in groups)
+    # a fresh runner resumes from it
+    r2 = _runner(None)
+    r2.load(os.path.join(tmp_path, "model_2.pt"))
+    assert r2.current_learning_iteration == 2
+    for (k, a), (_, b) in zip(r.alg.actor_critic.state_dict().items(), r2.alg.actor_critic.state_dict().items()):
+        assert torch.equal(a, b), k
+    s1 = r.alg.optimizer.state_dict()["state"]
+    s2 = r2.alg.optimizer.state_dict()["state"]
+    for i in s1:
+        assert torch.equal(s1[i]["exp_avg"], s2[i]["exp_avg"])
+    assert r2.alg.grads.check()
+    r2.learn(1)  # and keeps learning
+    assert all(torch.isfinite(p).all() for p in r2.alg.actor_critic.parameters())
