@@ -42,6 +42,20 @@ def env_bytes_per_env_step(P, num_bodies, ks):
     return rd + wr
 
 
+def committed_traffic(num_envs):
+    """Env-step kernel HBM bytes per launch from the newest committed PMC profile
+    (profiles/<round>_env_traffic.json, made by tools/profile_round.sh: FETCH_SIZE x2 +
+    WRITE_SIZE, separate --pmc passes), when it was measured on this workload size."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_env_traffic.json")))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1]))
+    if "traffic_bytes_per_launch" not in d or f"{num_envs} envs" not in d.get("workload", ""):
+        return None, None
+    return d["traffic_bytes_per_launch"], os.path.relpath(files[-1], ROOT)
+
+
 def cpu_baseline(num_envs=256, iters=1, steps_per_env=24):
     """Oracle env step (single-threaded C) + torch-CPU rsl_rl learner, same runner."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -143,6 +157,7 @@ def main():
     bpe = env_bytes_per_env_step(env.task_params, env.num_bodies, ks)
     launch_bytes = bpe * env.num_envs
     achieved = launch_bytes / (kern_avg_ms * 1e-3) / 1e9
+    traffic, traffic_src = committed_traffic(args.num_envs)
 
     if rank == 0:
         out = {
@@ -159,7 +174,8 @@ def main():
                            "env_steps_per_s": round(env.num_envs / (kern_avg_ms * 1e-3), 1)},
             "roofline": {"bound": "hbm", "kernel": "lgx::env_step_kernel<true>", "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "bytes_per_env_step": bpe, "bytes_per_launch": launch_bytes, "traffic": None},
+                         "bytes_per_env_step": bpe, "bytes_per_launch": launch_bytes,
+                         "traffic": None if traffic is None else round(traffic), "traffic_source": traffic_src},
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline()
