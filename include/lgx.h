@@ -272,6 +272,10 @@ int lgx_bind(lgx_env* env, const lgx_buffers* buffers);
 int lgx_step(lgx_env* env, uint64_t seed, uint64_t step_counter, void* hip_stream);
 /* post-physics only: the caller has written the physics state (root/dof/contact/
  * rigid-body) and torques; otherwise identical to the tail of lgx_step. */
+/* lgx_step with the step counter read from device memory at kernel time (the caller
+ * increments it on the same stream): the whole rollout can be captured as one hipGraph
+ * and replayed (on_policy_runner.py:147-170 loop). Same semantics as lgx_step. */
+int lgx_step_dev(lgx_env* env, uint64_t seed, const uint64_t* d_step_counter, void* hip_stream);
 int lgx_post_physics(lgx_env* env, uint64_t seed, uint64_t step_counter, void* hip_stream);
 /* physics substeps only (decimation × {PD torque, dynamics, contacts}). */
 int lgx_physics(lgx_env* env, void* hip_stream);

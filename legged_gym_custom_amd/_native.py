@@ -27,6 +27,7 @@ def lib():
     L.lgx_create.restype = C.c_int
     L.lgx_bind.argtypes = [vp, vp]
     L.lgx_step.argtypes = [vp, u64, u64, vp]
+    L.lgx_step_dev.argtypes = [vp, u64, vp, vp]
     L.lgx_post_physics.argtypes = [vp, u64, u64, vp]
     L.lgx_physics.argtypes = [vp, vp]
     L.lgx_reset_envs.argtypes = [vp, vp, u64, u64, vp]
@@ -42,7 +43,7 @@ def lib():
 
 
 EXPORTED = ["lgx_abi_version", "lgx_sizeof_model", "lgx_sizeof_task_params", "lgx_sizeof_buffers", "lgx_create",
-            "lgx_bind", "lgx_step", "lgx_post_physics", "lgx_physics", "lgx_reset_envs", "lgx_last_error",
+            "lgx_bind", "lgx_step", "lgx_step_dev", "lgx_post_physics", "lgx_physics", "lgx_reset_envs", "lgx_last_error",
             "lgx_destroy"]
 
 
@@ -81,6 +82,11 @@ class NativeEnv:
 
     def step(self, seed, step_counter, stream):
         self._check(self._L.lgx_step(self.handle, seed, step_counter, C.c_void_p(stream)), "lgx_step")
+
+    def step_dev(self, seed, step_counter_tensor, stream):
+        """lgx_step_dev: the step counter lives in a device uint64/int64 scalar tensor."""
+        self._check(self._L.lgx_step_dev(self.handle, seed, C.c_void_p(step_counter_tensor.data_ptr()),
+                                         C.c_void_p(stream)), "lgx_step_dev")
 
     def post_physics(self, seed, step_counter, stream):
         self._check(self._L.lgx_post_physics(self.handle, seed, step_counter, C.c_void_p(stream)), "lgx_post_physics")

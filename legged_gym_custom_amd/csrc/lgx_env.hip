@@ -925,8 +925,11 @@ LGX_DEV void get_heights(const lgx_task_params* Pm, const lgx_buffers& B, Sh& s,
 template <bool PHYSICS>
 __global__ __launch_bounds__(64, LGX_WAVES_PER_EU) void env_step_kernel(const lgx_model* __restrict__ M,
                                                       const lgx_task_params* __restrict__ Pm, lgx_buffers B,
-                                                      uint64_t seed, uint64_t step) {
+                                                      uint64_t seed, uint64_t step_arg,
+                                                      const uint64_t* __restrict__ step_dev) {
   __shared__ Sh s;
+  // graph-replayable form: the step counter is read from device memory (lgx_step_dev)
+  const uint64_t step = step_dev ? *step_dev : step_arg;
   const int e = blockIdx.x;
   const int lane = threadIdx.x;
   const int D = Pm->num_dof, A = Pm->num_actions, NB = Pm->num_bodies;
@@ -1358,7 +1361,8 @@ int lgx_bind(lgx_env* env, const lgx_buffers* b) {
   return 0;
 }
 
-static int launch_step(lgx_env* env, uint64_t seed, uint64_t step, void* stream, bool physics) {
+static int launch_step(lgx_env* env, uint64_t seed, uint64_t step, const uint64_t* step_dev, void* stream,
+                       bool physics) {
   if (!env) return -2;
   if (!env->bound) return fail(env, "lgx_step before lgx_bind");
   hipStream_t st = (hipStream_t)stream;
@@ -1368,20 +1372,25 @@ static int launch_step(lgx_env* env, uint64_t seed, uint64_t step, void* stream,
     HIP_OK(hipMemsetAsync(env->buffers.episode_stats, 0, sizeof(float) * (KS + 1), st));
   if (physics)
     hipLaunchKernelGGL(lgx::env_step_kernel<true>, dim3(N), dim3(64), 0, st, env->d_model, env->d_params, env->buffers,
-                       seed, step);
+                       seed, step, step_dev);
   else
     hipLaunchKernelGGL(lgx::env_step_kernel<false>, dim3(N), dim3(64), 0, st, env->d_model, env->d_params,
-                       env->buffers, seed, step);
+                       env->buffers, seed, step, step_dev);
   HIP_OK(hipGetLastError());
   return 0;
 }
 
 int lgx_step(lgx_env* env, uint64_t seed, uint64_t step_counter, void* hip_stream) {
-  return launch_step(env, seed, step_counter, hip_stream, true);
+  return launch_step(env, seed, step_counter, nullptr, hip_stream, true);
+}
+
+int lgx_step_dev(lgx_env* env, uint64_t seed, const uint64_t* d_step_counter, void* hip_stream) {
+  if (!d_step_counter) return fail(env, "lgx_step_dev: null step counter");
+  return launch_step(env, seed, 0, d_step_counter, hip_stream, true);
 }
 
 int lgx_post_physics(lgx_env* env, uint64_t seed, uint64_t step_counter, void* hip_stream) {
-  return launch_step(env, seed, step_counter, hip_stream, false);
+  return launch_step(env, seed, step_counter, nullptr, hip_stream, false);
 }
 
 int lgx_physics(lgx_env* env, void* hip_stream) {

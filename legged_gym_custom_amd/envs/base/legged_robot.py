@@ -49,8 +49,11 @@ class LeggedRobot(BaseTask):
     def step(self, actions):
         """legged_robot.py:67-100 as one kernel launch; returns the reference's 8-tuple."""
         self.actions_in.copy_(actions, non_blocking=True)
-        self.common_step_counter += 1
-        self._native.step(self.seed, self.common_step_counter, torch.cuda.current_stream(self.device).cuda_stream)
+        # the counter the kernel reads lives on the device (lgx_step_dev), so a captured
+        # rollout replays with the right step numbers; the host mirror follows
+        self._csc += 1
+        self._step_dev.add_(1)
+        self._native.step_dev(self.seed, self._step_dev, torch.cuda.current_stream(self.device).cuda_stream)
         self._update_extras()
         return (self.obs_buf, self.privileged_obs_buf, self.critic_obs_buf, self.estimated_obs_buf, self.scan_obs_buf,
                 self.rew_buf, self.reset_buf, self.extras)
@@ -72,11 +75,27 @@ class LeggedRobot(BaseTask):
         st = self.episode_stats
         cnt = st[-1]
         means = st[:-1] / torch.clamp(cnt, min=1.0) / self.max_episode_length_s
-        self._episode_means = torch.where(cnt > 0, means, self._episode_means)
-        self.extras["episode"] = {"rew_" + k: self._episode_means[i] for i, k in enumerate(self._episode_keys)}
+        # in place on static buffers: a captured rollout keeps the stale-value chain
+        self._episode_means.copy_(torch.where(cnt > 0, means, self._episode_means))
+        if "episode" not in self.extras:
+            self.extras["episode"] = {"rew_" + k: self._episode_means[i] for i, k in enumerate(self._episode_keys)}
         if self.cfg.env.send_timeouts:
-            self._extras_time_outs = torch.where(self.reset_buf.any(), self.time_out_buf, self._extras_time_outs)
+            self._extras_time_outs.copy_(torch.where(self.reset_buf.any(), self.time_out_buf, self._extras_time_outs))
             self.extras["time_outs"] = self._extras_time_outs
+
+    @property
+    def common_step_counter(self):
+        return self._csc
+
+    @common_step_counter.setter
+    def common_step_counter(self, value):
+        self._csc = int(value)
+        if hasattr(self, "_step_dev"):
+            self._step_dev.fill_(self._csc)
+
+    def advance_step_counter(self, k):
+        """Host mirror after a replayed capture that already advanced the device counter k times."""
+        self._csc += int(k)
 
     # ------------------------------------------------------------------ setup
     def create_sim(self):
@@ -178,6 +197,7 @@ class LeggedRobot(BaseTask):
         self.contact_forces = self._contact3
         self.rigid_body_states = z(n * nb, 13)
         self.rigid_body_states_view = self.rigid_body_states.view(n, nb, 13)
+        self._step_dev = torch.zeros(1, dtype=torch.int64, device=self.device)
         self.common_step_counter = 0
         self._reset_calls = 0
         self.extras = {}

@@ -361,8 +361,10 @@ class PPO:
         if not self.use_graphs:
             self._update_body_eager()
             return
-        if self._graphs is None and self._eager_updates < 2:
-            # warm-up on a side stream (lazy optimizer state, autograd + BLAS workspaces)
+        if self._graphs is None:
+            # the first update runs eagerly on a side stream (lazy optimizer state, autograd
+            # and GEMM workspaces), then the graph is captured right away — capture only
+            # records, so the next update is already a replay
             cur = torch.cuda.current_stream(self.device)
             side = torch.cuda.Stream(self.device)
             side.wait_stream(cur)
@@ -370,13 +372,11 @@ class PPO:
                 self._update_body_eager()
             cur.wait_stream(side)
             self._eager_updates += 1
-            return
-        if self._graphs is None:
-            # capture records, it does not run: the real update is the replay below
             snap = [p.detach().clone() for p in self._main_params + self._est_params]
             self._capture()
             for p, v in zip(self._main_params + self._est_params, snap):
                 assert torch.equal(p.detach(), v), "graph capture must not execute the update"
+            return
         if self.graph_mode == "whole":
             self._graphs["whole"].replay()
         else:

@@ -83,8 +83,13 @@ class ActorCritic(nn.Module):
         self.distribution = Normal(mean, mean * 0.0 + self.std)
 
     def act(self, obs_buf, privileged_obs_buf, estimated_obs_buf, scan_obs_buf, adaptation_mode=False):
+        """actor_critic.py:205-207: a ~ N(mean, std). Drawn as mean + std * eps with
+        eps = randn_like(mean) (the same law as Normal.sample(); torch.normal(loc, scale)
+        checks scale >= 0 on the host, which a captured hipGraph rollout cannot do)."""
         self.update_distribution(obs_buf, privileged_obs_buf, estimated_obs_buf, scan_obs_buf, adaptation_mode)
-        return self.distribution.sample()
+        d = self.distribution
+        with torch.no_grad():
+            return d.loc + d.scale * torch.randn_like(d.loc)
 
     def act_inference(self, obs_buf, privileged_obs_buf, estimated_obs_buf, scan_obs_buf, adaptation_mode=False):
         return self._actor_mean(obs_buf, privileged_obs_buf, estimated_obs_buf, scan_obs_buf, adaptation_mode)

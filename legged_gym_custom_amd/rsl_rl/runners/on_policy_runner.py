@@ -13,7 +13,6 @@ Multi-GPU: one process per GPU; rank 0 logs and saves; PPO all-reduces gradients
 import os
 import statistics
 import time
-from collections import deque
 
 import torch
 import torch.distributed as dist
@@ -96,7 +95,89 @@ class OnPolicyRunner:
         self.tot_time = 0
         self.current_learning_iteration = 0
         self.last_perf = {}
+        self.use_graphs = str(device).startswith("cuda")
+        self._graphs = {}
+        self._eager_rollouts = 0
+        self._stats = None
+        self._obs = None
         _ = self.env.reset()
+
+    # ------------------------------------------------------------------ rollout
+    def _track_episodes(self, rewards, dones, infos):
+        """Device-side form of on_policy_runner.py:160-170 (no host sync, graph-capturable):
+        rewbuffer/lenbuffer are 100-slot rings with the deque's keep-the-last-100 rule,
+        and ep_infos are kept as per-step sums of infos['episode']."""
+        st = self._stats
+        st["cur_rew"] += rewards
+        st["cur_len"] += 1
+        d = dones > 0
+        k = d.sum()
+        rank = torch.cumsum(d.long(), 0) - 1
+        keep = d & (rank >= k - 100)
+        pos = torch.where(keep, (st["ptr"] + rank) % 100, torch.full_like(rank, 100))  # slot 100 = discard
+        st["rew_ring"].scatter_(0, pos, st["cur_rew"])
+        st["len_ring"].scatter_(0, pos, st["cur_len"])
+        st["ptr"].copy_((st["ptr"] + k) % 100)
+        st["n"].copy_(torch.clamp(st["n"] + k, max=100))
+        st["cur_rew"].masked_fill_(d, 0.0)
+        st["cur_len"].masked_fill_(d, 0.0)
+        if "episode" in infos:
+            ep = infos["episode"]
+            if st["ep_keys"] is None:
+                st["ep_keys"] = list(ep.keys())
+                with torch.inference_mode(False):  # a normal tensor: a later capture updates it in place
+                    st["ep_sum"] = torch.zeros(len(st["ep_keys"]), device=self.device)
+            st["ep_sum"] += torch.stack([ep[key].reshape(()).to(self.device).float() for key in st["ep_keys"]])
+            st["ep_cnt"] += 1
+
+    def _rollout_step(self, adaptation_mode, track):
+        """One env step of the rollout loop (on_policy_runner.py:147-170)."""
+        o = self._obs
+        actions = self.alg.act(o[0], o[1], o[2], o[3], o[4], adaptation_mode=adaptation_mode)
+        obs, priv, critic, est, scan, rewards, dones, infos = self.env.step(actions)
+        new = (obs.to(self.device), priv.to(self.device), critic.to(self.device), est.to(self.device),
+               scan.to(self.device))
+        for dst, src in zip(o, new):  # the env hands back its own static buffers; keep them
+            if dst.data_ptr() != src.data_ptr():
+                dst.copy_(src)
+        rewards, dones = rewards.to(self.device), dones.to(self.device)
+        self.alg.process_env_step(rewards, dones, infos)
+        if track:
+            self._track_episodes(rewards, dones, infos)
+
+    def _graphable(self, adaptation_mode):
+        return (self.use_graphs and not adaptation_mode and self.device.startswith("cuda")
+                and hasattr(self.env, "advance_step_counter"))
+
+    def _rollout(self, adaptation_mode, track):
+        key = ("rollout", track)
+        if self._graphable(adaptation_mode) and key in self._graphs:
+            self._graphs[key].replay()
+            self.alg.storage.step = self.num_steps_per_env
+            self.env.advance_step_counter(self.num_steps_per_env)
+            return
+        for _ in range(self.num_steps_per_env):
+            self._rollout_step(adaptation_mode, track)
+        if not adaptation_mode:
+            self._eager_rollouts += 1
+
+    def _capture_rollout(self, track):
+        """Record the 24-step rollout once (after one eager rollout has warmed every
+        kernel and the storage is empty). Capture does not execute anything."""
+        key = ("rollout", track)
+        if key in self._graphs or not self._graphable(False) or self._eager_rollouts < 1:
+            return
+        torch.cuda.synchronize(self.device)
+        csc, st0 = self.env.common_step_counter, self.alg.storage.step
+        g = torch.cuda.CUDAGraph()
+        # no_grad, not inference_mode: capture registers the CUDA generator's graph-safe
+        # state, which must stay a normal tensor for the update graph's capture
+        with torch.inference_mode(False), torch.no_grad(), torch.cuda.graph(g):
+            for _ in range(self.num_steps_per_env):
+                self._rollout_step(False, track)
+        self.env.common_step_counter = csc  # host mirror (capture advanced it, the device did not)
+        self.alg.storage.step = st0
+        self._graphs[key] = g
 
     def learn(self, num_learning_iterations, init_at_random_ep_len=False):
         mean_value_loss = mean_surrogate_loss = mean_regularization_loss = 0.0
@@ -107,42 +188,29 @@ class OnPolicyRunner:
             self.env.episode_length_buf = torch.randint_like(self.env.episode_length_buf,
                                                              high=int(self.env.max_episode_length))
         env = self.env
-        obs = env.get_observations().to(self.device)
-        privileged_obs = env.get_privileged_observations().to(self.device)
-        critic_obs = env.get_critic_observations().to(self.device)
-        true_estimated_obs = env.get_estimated_observations().to(self.device)
-        scan_obs = env.get_scan_observations().to(self.device)
+        self._obs = [env.get_observations().to(self.device), env.get_privileged_observations().to(self.device),
+                     env.get_critic_observations().to(self.device), env.get_estimated_observations().to(self.device),
+                     env.get_scan_observations().to(self.device)]
         self.alg.actor_critic.train()
-        ep_infos = []
-        rewbuffer, lenbuffer = deque(maxlen=100), deque(maxlen=100)
-        cur_reward_sum = torch.zeros(env.num_envs, dtype=torch.float, device=self.device)
-        cur_episode_length = torch.zeros(env.num_envs, dtype=torch.float, device=self.device)
+        track = self.log_dir is not None
+        if track and self._stats is None:
+            z = lambda *sh: torch.zeros(*sh, device=self.device)  # noqa: E731
+            self._stats = {"cur_rew": z(env.num_envs), "cur_len": z(env.num_envs), "rew_ring": z(101),
+                           "len_ring": z(101), "ptr": torch.zeros((), dtype=torch.long, device=self.device),
+                           "n": torch.zeros((), dtype=torch.long, device=self.device), "ep_keys": None,
+                           "ep_sum": None, "ep_cnt": z(())}
         tot_iter = self.current_learning_iteration + num_learning_iterations
         for it in range(self.current_learning_iteration, tot_iter):
             start = time.time()
             use_adaptation_mode = it % self.dagger_update_freq == 0
             with torch.inference_mode():
-                for _ in range(self.num_steps_per_env):
-                    actions = self.alg.act(obs, privileged_obs, critic_obs, true_estimated_obs, scan_obs,
-                                           adaptation_mode=use_adaptation_mode)
-                    obs, privileged_obs, critic_obs, true_estimated_obs, scan_obs, rewards, dones, infos = env.step(actions)
-                    self.alg.process_env_step(rewards, dones, infos)
-                    if self.log_dir is not None:
-                        if "episode" in infos:
-                            ep_infos.append(infos["episode"])
-                        cur_reward_sum += rewards
-                        cur_episode_length += 1
-                        new_ids = (dones > 0).nonzero(as_tuple=False)
-                        rewbuffer.extend(cur_reward_sum[new_ids][:, 0].cpu().numpy().tolist())
-                        lenbuffer.extend(cur_episode_length[new_ids][:, 0].cpu().numpy().tolist())
-                        cur_reward_sum[new_ids] = 0
-                        cur_episode_length[new_ids] = 0
+                self._rollout(use_adaptation_mode, track)
                 if self.device.startswith("cuda"):
                     torch.cuda.synchronize(self.device)
                 stop = time.time()
                 collection_time = stop - start
                 start = stop
-                self.alg.compute_returns(critic_obs)
+                self.alg.compute_returns(self._obs[2])
             if use_adaptation_mode:
                 mean_adaptation_loss = self.alg.update_dagger()
             else:
@@ -154,31 +222,45 @@ class OnPolicyRunner:
             learn_time = stop - start
             self.last_perf = {"collection_time": collection_time, "learn_time": learn_time,
                               "fps": self.num_steps_per_env * env.num_envs / (collection_time + learn_time)}
+            self._capture_rollout(track)
             if self.log_dir is not None:
+                rewbuffer, lenbuffer, ep_means = self._host_stats()
                 self.log(locals())
                 if it % self.save_interval == 0:
                     self.save(os.path.join(self.log_dir, "model_{}.pt".format(it)))
-            ep_infos.clear()
         self.current_learning_iteration += num_learning_iterations
         if self.log_dir is not None:
             self.save(os.path.join(self.log_dir, "model_{}.pt".format(self.current_learning_iteration)))
+
+    def _host_stats(self):
+        """One transfer per iteration: the rings (last <=100 completed episodes, oldest
+        first as a deque would iterate) and the mean of each infos['episode'] key over the
+        steps since the last log (then reset)."""
+        with torch.inference_mode():  # the accumulators are touched inside the rollout's inference mode
+            return self._host_stats_impl()
+
+    def _host_stats_impl(self):
+        st = self._stats
+        n, ptr = int(st["n"]), int(st["ptr"])
+        idx = [(ptr - n + i) % 100 for i in range(n)]
+        rew = st["rew_ring"][idx].tolist() if n else []
+        ln = st["len_ring"][idx].tolist() if n else []
+        ep = {}
+        cnt = float(st["ep_cnt"])
+        if st["ep_keys"] is not None and cnt > 0:
+            ep = dict(zip(st["ep_keys"], (st["ep_sum"] / cnt).tolist()))
+            st["ep_sum"].zero_()
+            st["ep_cnt"].zero_()
+        return rew, ln, ep
 
     def log(self, locs, width=80, pad=35):
         self.tot_timesteps += self.num_steps_per_env * self.env.num_envs
         self.tot_time += locs["collection_time"] + locs["learn_time"]
         iteration_time = locs["collection_time"] + locs["learn_time"]
         ep_string = ""
-        if locs["ep_infos"]:
-            for key in locs["ep_infos"][0]:
-                vals = []
-                for ep_info in locs["ep_infos"]:
-                    v = ep_info[key]
-                    if not isinstance(v, torch.Tensor):
-                        v = torch.Tensor([v])
-                    vals.append(v.reshape(-1).to(self.device))
-                value = torch.mean(torch.cat(vals))
-                self.writer.add_scalar("Episode/" + key, value, locs["it"])
-                ep_string += f"""{f'Mean episode {key}:':>{pad}} {value:.4f}\n"""
+        for key, value in locs["ep_means"].items():
+            self.writer.add_scalar("Episode/" + key, value, locs["it"])
+            ep_string += f"""{f'Mean episode {key}:':>{pad}} {value:.4f}\n"""
         mean_std = self.alg.actor_critic.std.mean()
         fps = int(self.num_steps_per_env * self.env.num_envs / (locs["collection_time"] + locs["learn_time"]))
         w = self.writer
@@ -226,6 +308,8 @@ class OnPolicyRunner:
                     "adaptation_optimizer_state_dict": opt["adaptation_optimizer_state_dict"]}, path)
 
     def load(self, path, load_optimizer=True):
+        self._graphs = {}
+        self._eager_rollouts = 0
         loaded = torch.load(path, map_location=self.device, weights_only=True)
         self.alg.actor_critic.load_state_dict(loaded["model_state_dict"])
         if load_optimizer:

@@ -1,0 +1,61 @@
+"""The hipGraph-replayed rollout (24 env steps: act + lgx_step_dev + storage + episode
+logging) produces exactly what the eager loop does (deterministic policy, std = 0)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup(use_graphs):
+    from legged_gym_custom_amd.envs import task_registry
+    from legged_gym_custom_amd.utils.helpers import get_args
+    # no --seed: make_alg_runner writes args.seed into the shared train cfg, which the next
+    # make_env would pick up (the reference's cfg mutation) and the two envs would differ
+    a = get_args(["--task=go2", "--headless", "--num_envs=256", "--sim_device=cuda:0", "--rl_device=cuda:0"])
+    env, _ = task_registry.make_env("go2", a)
+    _, tcfg = task_registry.get_cfgs("go2")
+    tcfg.runner.num_steps_per_env = 6
+    torch.manual_seed(3)
+    runner, _ = task_registry.make_alg_runner(env, args=a, train_cfg=tcfg, log_root=None)
+    runner.use_graphs = use_graphs
+    with torch.no_grad():
+        runner.alg.actor_critic.std.zero_()
+    runner.log_dir = "unused"  # turn on the device-side episode tracking (no writer is made here)
+    return env, runner
+
+
+def _run(env, runner, iters):
+    import torch as T
+    z = lambda *sh: T.zeros(*sh, device="cuda:0")  # noqa: E731
+    runner._stats = {"cur_rew": z(env.num_envs), "cur_len": z(env.num_envs), "rew_ring": z(101), "len_ring": z(101),
+                     "ptr": T.zeros((), dtype=T.long, device="cuda:0"), "n": T.zeros((), dtype=T.long, device="cuda:0"),
+                     "ep_keys": None, "ep_sum": None, "ep_cnt": z(())}
+    runner._obs = [env.get_observations(), env.get_privileged_observations(), env.get_critic_observations(),
+                   env.get_estimated_observations(), env.get_scan_observations()]
+    snaps = []
+    csc0 = env.common_step_counter
+    for _ in range(iters):
+        with T.inference_mode():
+            runner._rollout(False, True)
+        s = runner.alg.storage
+        snaps.append({"obs": s.observations.clone(), "rew": s.rewards.clone(), "dones": s.dones.clone(),
+                      "root": env.root_states.clone(), "csc": env.common_step_counter - csc0,
+                      "ring": runner._stats["rew_ring"][:100].clone(),  # slot 100 = discard (arbitrary)
+                      "n": int(runner._stats["n"])})
+        s.clear()
+        runner._capture_rollout(True)  # as learn() does after each iteration (no-op when eager)
+    return snaps
+
+
+def test_graph_rollout_equals_eager():
+    env_a, run_a = _setup(False)
+    eager = _run(env_a, run_a, 5)
+    env_b, run_b = _setup(True)
+    graph = _run(env_b, run_b, 5)
+    assert ("rollout", True) in run_b._graphs  # iterations 3.. replayed a capture
+    for i, (a, b) in enumerate(zip(eager, graph)):
+        assert a["csc"] == b["csc"] == 6 * (i + 1)
+        for k in ("obs", "rew", "dones", "root", "ring"):
+            torch.testing.assert_close(b[k], a[k], rtol=0, atol=0, msg=f"iteration {i} {k}")
+        assert a["n"] == b["n"]
+    assert int(env_b._step_dev) == env_b.common_step_counter

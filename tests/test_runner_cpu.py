@@ -50,3 +50,37 @@ def test_learn_saves_reference_format_checkpoints(tmp_path):
     assert r2.alg.grads.check()
     r2.learn(1)  # and keeps learning
     assert all(torch.isfinite(p).all() for p in r2.alg.actor_critic.parameters())
+
+
+def test_device_episode_logging_matches_reference_deques():
+    """_track_episodes (graph-capturable) == the reference's deque bookkeeping
+    (on_policy_runner.py:160-170) over many steps, incl. >100 dones in one step."""
+    from collections import deque
+    r = OnPolicyRunner.__new__(OnPolicyRunner)
+    r.device = "cpu"
+    n = 300
+    z = lambda *sh: torch.zeros(*sh)  # noqa: E731
+    r._stats = {"cur_rew": z(n), "cur_len": z(n), "rew_ring": z(101), "len_ring": z(101),
+                "ptr": torch.zeros((), dtype=torch.long), "n": torch.zeros((), dtype=torch.long), "ep_keys": None,
+                "ep_sum": None, "ep_cnt": z(())}
+    rewbuffer, lenbuffer = deque(maxlen=100), deque(maxlen=100)
+    cur_r, cur_l = torch.zeros(n), torch.zeros(n)
+    g = torch.Generator().manual_seed(0)
+    ep_vals = []
+    for step in range(60):
+        rewards = torch.randn(n, generator=g)
+        p = 0.5 if step == 7 else 0.05
+        dones = torch.rand(n, generator=g) < p
+        info = {"episode": {"rew_a": torch.tensor(float(step)), "rew_b": torch.tensor(2.0 * step)}}
+        r._track_episodes(rewards, dones, info)
+        ep_vals.append([float(step), 2.0 * step])
+        cur_r += rewards
+        cur_l += 1
+        ids = dones.nonzero(as_tuple=False)
+        rewbuffer.extend(cur_r[ids][:, 0].tolist())
+        lenbuffer.extend(cur_l[ids][:, 0].tolist())
+        cur_r[ids] = 0
+        cur_l[ids] = 0
+    rew, ln, ep = r._host_stats()
+    assert rew == list(rewbuffer) and ln == list(lenbuffer)
+    assert ep["rew_a"] == sum(v[0] for v in ep_vals) / 60 and ep["rew_b"] == sum(v[1] for v in ep_vals) / 60
