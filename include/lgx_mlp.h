@@ -57,6 +57,17 @@ int32_t lgx_mlp_pick_split(int32_t M, int32_t N, int32_t K);
 int32_t lgx_gemm(const lgx_gemm_args* args, void* stream);
 const char* lgx_mlp_last_error(void);
 
+/* One Adam step over a contiguous parameter segment (fp32), replacing torch.optim.Adam's
+ * step (rsl_rl ppo.py:58-66 optimizers; the arithmetic of torch's fused Adam):
+ *   t = *step (already incremented by the caller), g' = g * (grad_scale ? *grad_scale : 1)
+ *   m = b1 m + (1-b1) g';  v = b2 v + (1-b2) g'^2
+ *   p -= (lr / (1-b1^t)) * m / (sqrt(v) / sqrt(1-b2^t) + eps)
+ * lr is read from lr_dev when non-NULL (device-side KL schedule), else lr. grad_scale is
+ * the clip_grad_norm_ coefficient (device scalar). Stream-ordered; graph-capturable. */
+int32_t lgx_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                      const float* lr_dev, float lr, float beta1, float beta2, float eps, const float* step,
+                      const float* grad_scale, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -394,6 +394,45 @@ __global__ void splitk_reduce(Params p, float* colsum) {
   }
 }
 
+__device__ __forceinline__ void adam1(float& p, float g, float& m, float& v, float b1, float b2, float eps,
+                                      float step_size, float bc2s) {
+  m = b1 * m + (1.f - b1) * g;
+  v = b2 * v + (1.f - b2) * g * g;
+  p -= step_size * m / (sqrtf(v) / bc2s + eps);
+}
+
+// Adam over a flat fp32 segment: float4 lanes, grid-stride.
+__global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                            float* __restrict__ v, int64_t n, const float* __restrict__ lr_dev, float lr, float b1,
+                            float b2, float eps, const float* __restrict__ step, const float* __restrict__ gscale) {
+  const float t = *step;
+  const float lr_ = lr_dev ? *lr_dev : lr;
+  const float bc1 = 1.f - powf(b1, t), bc2 = 1.f - powf(b2, t);
+  const float step_size = lr_ / bc1, bc2s = sqrtf(bc2);
+  const float sc = gscale ? *gscale : 1.f;
+  const int64_t n4 = n / 4;
+  const bool vec = ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(m) |
+                     reinterpret_cast<uintptr_t>(v)) & 15) == 0;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (vec) {
+    for (int64_t i = i0; i < n4; i += stride) {
+      float4 P = reinterpret_cast<float4*>(p)[i], G = reinterpret_cast<const float4*>(g)[i];
+      float4 M = reinterpret_cast<float4*>(m)[i], V = reinterpret_cast<float4*>(v)[i];
+      adam1(P.x, G.x * sc, M.x, V.x, b1, b2, eps, step_size, bc2s);
+      adam1(P.y, G.y * sc, M.y, V.y, b1, b2, eps, step_size, bc2s);
+      adam1(P.z, G.z * sc, M.z, V.z, b1, b2, eps, step_size, bc2s);
+      adam1(P.w, G.w * sc, M.w, V.w, b1, b2, eps, step_size, bc2s);
+      reinterpret_cast<float4*>(p)[i] = P;
+      reinterpret_cast<float4*>(m)[i] = M;
+      reinterpret_cast<float4*>(v)[i] = V;
+    }
+    for (int64_t i = n4 * 4 + i0; i < n; i += stride) adam1(p[i], g[i] * sc, m[i], v[i], b1, b2, eps, step_size, bc2s);
+  } else {
+    for (int64_t i = i0; i < n; i += stride) adam1(p[i], g[i] * sc, m[i], v[i], b1, b2, eps, step_size, bc2s);
+  }
+}
+
 // dynamic LDS: two K-step stages of hi/lo A and B images, or the fp32 C image (reused)
 constexpr size_t lds_bytes(int bn) {
   const size_t stages = 2 * (2 * A_ELEMS + 2 * bn * PITCH) * sizeof(__bf16);
@@ -448,6 +487,21 @@ int32_t lgx_mlp_abi_version(void) { return LGX_MLP_ABI_VERSION; }
 int32_t lgx_mlp_sizeof_gemm_args(void) { return (int32_t)sizeof(lgx_gemm_args); }
 
 const char* lgx_mlp_last_error(void) { return g_err; }
+
+int32_t lgx_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                      const float* lr_dev, float lr, float beta1, float beta2, float eps, const float* step,
+                      const float* grad_scale, void* stream) {
+  if (n < 0) return fail("lgx_adam_step: negative size");
+  if (n == 0) return 0;
+  if (!param || !grad || !exp_avg || !exp_avg_sq || !step) return fail("lgx_adam_step: null pointer");
+  const int64_t work = (n + 3) / 4;
+  int blocks = (int)((work + 255) / 256);
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(lgxm::adam_kernel, dim3(blocks), dim3(256), 0, static_cast<hipStream_t>(stream), param, grad,
+                     exp_avg, exp_avg_sq, n, lr_dev, lr, beta1, beta2, eps, step, grad_scale);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : fail(hipGetErrorString(e));
+}
 
 int32_t lgx_mlp_pick_split(int32_t M, int32_t N, int32_t K) {
   const int bn = tile_n(N);

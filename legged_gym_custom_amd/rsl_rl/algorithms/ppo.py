@@ -11,6 +11,10 @@ MI355X execution of the same math (DESIGN.md "Learner"):
     all-reduce is one RCCL call per minibatch over [main | estimator | kl] (mean over ranks);
   * the adaptive-KL learning-rate schedule (ppo.py:230-246) runs on the device (fp64
     master, same branches), so a minibatch needs no host round trip;
+  * on the GPU, parameters and Adam moments are views into flat buffers with the same
+    layout, and each optimizer step is one lgx_adam_step launch over its segment with the
+    clip_grad_norm_ coefficient folded in (torch's Adam objects remain the containers:
+    param groups, state_dict and load_state_dict in the reference's format);
   * on a HIP device the whole 5x4-minibatch update is captured once as a hipGraph and
     replayed per iteration (world_size 1), or as per-minibatch graphs around the RCCL
     all-reduce (world_size > 1). The first two updates run eagerly (warm-up), and any
@@ -27,7 +31,7 @@ import torch
 import torch.distributed as dist
 import torch.optim as optim
 
-from legged_gym_custom_amd.rsl_rl.modules import ActorCritic
+from legged_gym_custom_amd.rsl_rl.modules import ActorCritic, hip_mlp
 from legged_gym_custom_amd.rsl_rl.modules.support_networks import MlpEstimator
 from legged_gym_custom_amd.rsl_rl.storage import RolloutStorage
 
@@ -62,6 +66,7 @@ class FlatGrads:
     (PPO never calls optimizer.zero_grad())."""
 
     def __init__(self, segments):
+        self._segments = segments
         sizes = [(name, (sum(p.numel() for p in ps) if not isinstance(ps, int) else ps)) for name, ps in segments]
         dev = next(ps for _, ps in segments if not isinstance(ps, int))[0].device
         self.buf = torch.zeros(sum(n for _, n in sizes), device=dev)
@@ -89,17 +94,38 @@ class FlatGrads:
         """True while every p.grad is still the view installed at construction."""
         return all(p.grad is not None and p.grad.data_ptr() == ptr for p, ptr in self._ptrs)
 
+    def rebind(self):
+        """Re-install the views (e.g. after copy.deepcopy, which copies p.grad and the
+        buffer separately); the buffer keeps its values."""
+        off = 0
+        self._ptrs = []
+        for name, ps in self._segments:
+            a, b = self.slices[name]
+            if not isinstance(ps, int):
+                o = a
+                for p in ps:
+                    p.grad = self.buf[o:o + p.numel()].view_as(p)
+                    self._ptrs.append((p, p.grad.data_ptr()))
+                    o += p.numel()
+            off = b
 
-def _clip_(segs, max_norm):
-    """clip_grad_norm_ over the concatenation of `segs` (torch/nn/utils/clip_grad.py):
-    coef = clamp(max_norm / (||g||_2 + 1e-6), max=1); g *= coef. No host sync."""
+
+def _clip_coef(segs, max_norm):
+    """clip_grad_norm_'s coefficient over the concatenation of `segs`
+    (torch/nn/utils/clip_grad.py): clamp(max_norm / (||g||_2 + 1e-6), max=1). No host sync."""
     if len(segs) == 1:
         total = torch.linalg.vector_norm(segs[0])
     else:
         total = torch.linalg.vector_norm(torch.stack([torch.linalg.vector_norm(s) for s in segs]))
-    coef = torch.clamp(max_norm / (total + 1e-6), max=1.0)
+    return torch.clamp(max_norm / (total + 1e-6), max=1.0)
+
+
+def _clip_(segs, max_norm):
+    """clip_grad_norm_ in place: g *= coef."""
+    coef = _clip_coef(segs, max_norm)
     for s in segs:
         s.mul_(coef)
+    return coef
 
 
 def export_adam_state(opt):
@@ -153,17 +179,17 @@ class PPO:
         self.grads = FlatGrads([("main", self._main_params), ("estimator", self._est_params), ("kl", 1),
                                 ("adaptation", self._adapt_params)])
 
-        # learning rate: fp64 master on the device, fp32 copy read by the fused Adam kernel
+        # learning rate: fp64 master on the device (KL schedule), fp32 copy read by the Adam kernel
         self._lr64 = torch.tensor(float(learning_rate), dtype=torch.float64, device=device)
+        self._lr32 = torch.tensor(float(learning_rate), dtype=torch.float32, device=device) if self.on_gpu else None
+        self._adapt_lr = float(learning_rate)  # adaptation_optimizer keeps its construction lr (ppo.py:65)
+        self.optimizer = optim.Adam([{"params": g} for g in main_groups], lr=learning_rate)
+        self.adaptation_optimizer = optim.Adam(self._adapt_params, lr=learning_rate)
+        self.estimator_optimizer = optim.Adam(self._est_params, lr=estimator_learning_rate)
+        self._segment_of = {"optimizer": "main", "estimator_optimizer": "estimator",
+                            "adaptation_optimizer": "adaptation"}
         if self.on_gpu:
-            kw = dict(fused=True, capturable=True)
-            self._lr32 = torch.tensor(float(learning_rate), dtype=torch.float32, device=device)
-            lr = self._lr32
-        else:
-            kw, self._lr32, lr = {}, None, float(learning_rate)
-        self.optimizer = optim.Adam([{"params": g} for g in main_groups], lr=lr, **kw)
-        self.adaptation_optimizer = optim.Adam(self._adapt_params, lr=learning_rate, **kw)
-        self.estimator_optimizer = optim.Adam(self._est_params, lr=estimator_learning_rate, **kw)
+            self._flatten_params_and_moments()
         self.transition = RolloutStorage.Transition()
         self.clip_param = clip_param
         self.num_learning_epochs = num_learning_epochs
@@ -184,6 +210,48 @@ class PPO:
         self._eager_updates = 0
         self.graph_mode = None  # "whole" | "phased" once captured
         self.phased_graphs = None  # None: phased iff world_size > 1 (tests force it on one GPU)
+
+    # ------------------------------------------------------------------ flat Adam (HIP)
+    def _flatten_params_and_moments(self):
+        """Parameters, Adam exp_avg and exp_avg_sq as views into flat buffers with the
+        gradient buffer's layout, so one lgx_adam_step per optimizer updates a whole
+        segment. The torch Adam objects stay the containers (param groups, state_dict)."""
+        g = self.grads
+        self.params_buf = torch.zeros_like(g.buf)
+        self.exp_avg = torch.zeros_like(g.buf)
+        self.exp_avg_sq = torch.zeros_like(g.buf)
+        for p in self._main_params + self._est_params + self._adapt_params:
+            off = (p.grad.data_ptr() - g.buf.data_ptr()) // 4
+            n = p.numel()
+            self.params_buf[off:off + n].copy_(p.data.reshape(-1))
+            p.data = self.params_buf[off:off + n].view_as(p)
+        self._opt_step = {name: torch.zeros((), device=self.device) for name in self._segment_of}
+        for name in self._segment_of:
+            self._bind_adam_state(name)
+
+    def _range_of(self, p):
+        off = (p.data_ptr() - self.params_buf.data_ptr()) // 4
+        return off, off + p.numel()
+
+    def _bind_adam_state(self, name):
+        opt = getattr(self, name)
+        step = self._opt_step[name]
+        for grp in opt.param_groups:
+            for p in grp["params"]:
+                a, b = self._range_of(p)
+                opt.state[p] = {"step": step, "exp_avg": self.exp_avg[a:b].view_as(p),
+                                "exp_avg_sq": self.exp_avg_sq[a:b].view_as(p)}
+
+    def _adam(self, name, lr, grad_scale=None):
+        """torch Adam(fused) arithmetic over this optimizer's whole flat segment."""
+        opt = getattr(self, name)
+        b1, b2 = opt.param_groups[0]["betas"]
+        eps = opt.param_groups[0]["eps"]
+        a, b = self.grads.slices[self._segment_of[name]]
+        step = self._opt_step[name]
+        step.add_(1)
+        hip_mlp.adam_step(self.params_buf[a:b], self.grads.buf[a:b], self.exp_avg[a:b], self.exp_avg_sq[a:b], step,
+                          lr, b1, b2, eps, grad_scale)
 
     # ------------------------------------------------------------------ storage / rollout
     def init_storage(self, num_envs, num_transitions_per_env, total_obs_shape, privileged_obs_shape, critic_obs_shape,
@@ -283,8 +351,12 @@ class PPO:
         """Phase B: (ranks averaged) clip + estimator step, KL schedule, clip + main step."""
         g = self.grads
         with torch.no_grad():
-            _clip_([g.segment("estimator")], self.max_grad_norm)
-        self.estimator_optimizer.step()
+            if self.on_gpu:  # clip coefficient folded into the Adam kernel
+                self._adam("estimator_optimizer", self.estimator_learning_rate,
+                           _clip_coef([g.segment("estimator")], self.max_grad_norm))
+            else:
+                _clip_([g.segment("estimator")], self.max_grad_norm)
+                self.estimator_optimizer.step()
         if self.desired_kl is not None and self.schedule == "adaptive":
             with torch.no_grad():
                 kl_mean = g.segment("kl")[0].double()
@@ -300,9 +372,13 @@ class PPO:
                 for grp in self.optimizer.param_groups:
                     grp["lr"] = float(self._lr64)
         with torch.no_grad():
-            _clip_([g.segment("main"), g.segment("adaptation")], self.max_grad_norm)
-        self.optimizer.step()
-        with torch.no_grad():
+            if self.on_gpu:
+                coef = _clip_coef([g.segment("main"), g.segment("adaptation")], self.max_grad_norm)
+                g.segment("adaptation").mul_(coef)  # the stale DAgger grads are scaled in place (quirk)
+                self._adam("optimizer", self._lr32, coef)
+            else:
+                _clip_([g.segment("main"), g.segment("adaptation")], self.max_grad_norm)
+                self.optimizer.step()
             self._sums.add_(self._losses)
 
     def _allreduce_minibatch(self):
@@ -389,6 +465,9 @@ class PPO:
     # ------------------------------------------------------------------ update
     def update(self):
         """ppo.py:182-293 (num_learning_epochs x num_mini_batches minibatches)."""
+        if not self.grads.check():
+            self.grads.rebind()
+            self.invalidate_graphs()
         regularization_coef = self.reg_coef()
         self._reg_coef.fill_(regularization_coef)
         self._sums.zero_()
@@ -398,6 +477,8 @@ class PPO:
         num_updates = self.num_learning_epochs * self.num_mini_batches
         mv, ms, mr, me, self.learning_rate = torch.cat([(self._sums / num_updates).double(),
                                                         self._lr64.reshape(1)]).tolist()
+        for grp in self.optimizer.param_groups:  # the containers show the scheduled lr
+            grp["lr"] = self.learning_rate
         self.storage.clear()
         self.increase_update_count()
         self.enforce_max_std(1.0)
@@ -418,6 +499,9 @@ class PPO:
     def update_dagger(self):
         """ppo.py:309-349: adaptation-encoder-only imitation of the privileged latent
         (same epoch-shared permutation and minibatch slices as update())."""
+        if not self.grads.check():
+            self.grads.rebind()
+            self.invalidate_graphs()
         total = torch.zeros((), device=self.device)
         ac = self.actor_critic
         adapt = self.grads.segment("adaptation")
@@ -437,7 +521,10 @@ class PPO:
                     adapt.div_(dist.get_world_size())
                 with torch.no_grad():
                     _clip_([adapt], self.max_grad_norm)
-                self.adaptation_optimizer.step()
+                    if self.on_gpu:
+                        self._adam("adaptation_optimizer", self._adapt_lr)
+                if not self.on_gpu:
+                    self.adaptation_optimizer.step()
                 total += adaptation_loss.detach()
         mean_adaptation_loss = (total / (self.num_learning_epochs * self.num_mini_batches)).item()
         self.storage.clear()
@@ -453,25 +540,34 @@ class PPO:
                 "adaptation_optimizer_state_dict": export_adam_state(self.adaptation_optimizer)}
 
     def load_optimizer_state(self, name, state_dict):
-        """Load a (reference-format or own) Adam state into `name`, then restore this
-        build's execution flags and device-side lr; drops captured graphs."""
+        """Load a (reference-format) Adam state into `name`; on the GPU the moments are
+        copied into the flat buffers and the state re-bound to views. Drops graphs."""
         opt = getattr(self, name)
-        flags = [(grp.get("fused"), grp.get("capturable"), grp["lr"]) for grp in opt.param_groups]
         opt.load_state_dict(state_dict)
-        for grp, (fused, capt, lr_obj) in zip(opt.param_groups, flags):
-            loaded_lr = float(grp["lr"])
-            grp["fused"], grp["capturable"] = fused, capt
-            if isinstance(lr_obj, torch.Tensor):
-                lr_obj.fill_(loaded_lr)
-                grp["lr"] = lr_obj
-            else:
-                grp["lr"] = loaded_lr
-            if name == "optimizer":
-                self._lr64.fill_(loaded_lr)
-                self.learning_rate = loaded_lr
-        for st in opt.state.values():
-            if "step" in st and self.on_gpu:
-                st["step"] = st["step"].to(device=self.device, dtype=torch.float32)
+        for grp in opt.param_groups:
+            grp["lr"] = float(grp["lr"])
+            grp["fused"], grp["capturable"] = None, False
+        if name == "optimizer":
+            lr = float(opt.param_groups[0]["lr"])
+            self._lr64.fill_(lr)
+            if self._lr32 is not None:
+                self._lr32.fill_(lr)
+            self.learning_rate = lr
+        elif name == "adaptation_optimizer":
+            self._adapt_lr = float(opt.param_groups[0]["lr"])
+        if self.on_gpu:
+            step = None
+            with torch.no_grad():
+                for grp in opt.param_groups:
+                    for p in grp["params"]:
+                        st = opt.state.get(p, {})
+                        a, b = self._range_of(p)
+                        if "exp_avg" in st:
+                            self.exp_avg[a:b].copy_(st["exp_avg"].reshape(-1))
+                            self.exp_avg_sq[a:b].copy_(st["exp_avg_sq"].reshape(-1))
+                            step = float(st["step"])
+            self._opt_step[name].fill_(step or 0.0)
+            self._bind_adam_state(name)
         self.invalidate_graphs()
 
     def after_model_load(self):

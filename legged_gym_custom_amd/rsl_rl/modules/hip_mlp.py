@@ -23,7 +23,7 @@ _lib = None
 ABI_VERSION = 1
 EPI_BIAS, EPI_ELU, EPI_DELU, EPI_ACCUM = 1, 2, 4, 8
 EXPORTED = ["lgx_mlp_abi_version", "lgx_mlp_sizeof_gemm_args", "lgx_mlp_pick_split", "lgx_gemm",
-            "lgx_mlp_last_error"]
+            "lgx_mlp_last_error", "lgx_adam_step"]
 
 
 class GemmArgs(C.Structure):
@@ -54,6 +54,9 @@ def lib():
     L.lgx_gemm.argtypes = [C.c_void_p, C.c_void_p]
     L.lgx_gemm.restype = C.c_int32
     L.lgx_mlp_last_error.restype = C.c_char_p
+    vp, f32 = C.c_void_p, C.c_float
+    L.lgx_adam_step.argtypes = [vp, vp, vp, vp, C.c_int64, vp, f32, f32, f32, f32, vp, vp, vp]
+    L.lgx_adam_step.restype = C.c_int32
     if L.lgx_mlp_abi_version() != ABI_VERSION:
         raise MlpLibError("liblgx_mlp ABI version mismatch; rebuild")
     L.lgx_mlp_sizeof_gemm_args.restype = C.c_int32
@@ -77,6 +80,18 @@ def _run(args):
 
 def _rowmajor(t):
     return t if t.stride(-1) == 1 else t.contiguous()
+
+
+def adam_step(p, g, m, v, step, lr, beta1, beta2, eps, grad_scale=None):
+    """lgx_adam_step over flat fp32 segments (views); lr: float or 0-dim device tensor."""
+    lr_dev = lr.data_ptr() if isinstance(lr, torch.Tensor) else None
+    lr_f = 0.0 if isinstance(lr, torch.Tensor) else float(lr)
+    L = lib()
+    rc = L.lgx_adam_step(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p.numel(), lr_dev, lr_f, beta1, beta2,
+                         eps, step.data_ptr(), None if grad_scale is None else grad_scale.data_ptr(),
+                         C.c_void_p(torch.cuda.current_stream().cuda_stream))
+    if rc != 0:
+        raise MlpLibError("lgx_adam_step: " + L.lgx_mlp_last_error().decode())
 
 
 def gemm_raw(A, lda, a_kcontig, B, ldb, b_kcontig, C, ldc, M, N, K, epilogue=0, bias=None, act=None, ld_act=0):
