@@ -44,6 +44,8 @@ struct Scratch {  // per-env post-physics scalars (go2.py:357-367, 279-328)
   float jump;
 };
 
+constexpr int AMAX = 41;  // rows of the explicit-A PGS (A overlays the post-physics staging)
+
 struct Sh {
   // --- post-physics per-env scalars (written by lane 0, read by all lanes)
   Scratch x;
@@ -71,11 +73,17 @@ struct Sh {
   int nrows, nlim, ncon;
   float cf[LGX_MAX_BODIES][3];
   float rbz[LGX_MAX_BODIES];
-  // --- post-physics
-  float U[NSLOT];
-  float cur[LGX_MAX_PROPRIO];
-  float hist[MAXHIST];
-  float heights[LGX_MAX_HEIGHT_POINTS];
+  // --- post-physics staging; during the substeps the same LDS holds the Delassus
+  //     matrix A = J M⁻¹ Jᵀ of the active constraint rows (PGS, nrows <= AMAX)
+  union {
+    struct {
+      float U[NSLOT];
+      float cur[LGX_MAX_PROPRIO];
+      float hist[MAXHIST];
+      float heights[LGX_MAX_HEIGHT_POINTS];
+    };
+    float A[AMAX * AMAX];
+  };
 };
 
 // ============================================================== physics helpers
@@ -475,39 +483,111 @@ LGX_DEV void substep(Sh& s, const lgx_model* M, const lgx_task_params* Pm, const
 #if defined(LGX_DBG_STAGE) && LGX_DBG_STAGE == 4
   return;
 #endif
-  // ---- projected Gauss-Seidel, generalized velocity spread over lanes 0..17
-  float uc = lane < NU ? s.us[lane] : 0.f;
-  const float mu = s.mu;
-  for (int it = 0; it < Pm->solver_iterations; ++it) {
-    for (int r = 0; r < nrows; ++r) {
-      const int kind = s.rkind[r];
-      if (kind == 0) {
-        float w = row_sums_32(lane < NU ? s.J[r][lane] * uc : 0.f);
-        float lo = s.lam[r];
-        float ln = fmaxf(0.f, lo + (s.tgt[r] - w) / s.Arr[r]);
-        float d = ln - lo;
-        if (lane < NU) uc += s.MJ[r][lane] * d;
-        if (lane == 0) s.lam[r] = ln;
-      } else {
-        float w1 = row_sums_32(lane < NU ? s.J[r][lane] * uc : 0.f);
-        float w2 = row_sums_32(lane < NU ? s.J[r + 1][lane] * uc : 0.f);
-        float o1 = s.lam[r], o2 = s.lam[r + 1];
-        float l1 = o1 - w1 / s.Arr[r];
-        float l2 = o2 - w2 / s.Arr[r + 1];
-        float lim = mu * s.lam[r - 1];
-        float n = sqrtf(l1 * l1 + l2 * l2);
-        if (n > lim) {
-          float sc = n > 0.f ? lim / n : 0.f;
-          l1 *= sc; l2 *= sc;
-        }
-        if (lane < NU) uc += s.MJ[r][lane] * (l1 - o1) + s.MJ[r + 1][lane] * (l2 - o2);
-        if (lane == 0) { s.lam[r] = l1; s.lam[r + 1] = l2; }
-        ++r;
+  if (nrows <= AMAX) {
+    // ---- projected Gauss-Seidel on A (oracle_physics.c step 4): lane r keeps the row
+    //      velocity w_r = J_r u and lambda_r; a row update is one readlane + scalar
+    //      projection + one FMA per lane with row r of A (no cross-lane reductions)
+    float w = 0.f, lam = 0.f;
+    if (lane < nrows) {
+      float mj[NU];
+#pragma unroll
+      for (int q = 0; q < NU; ++q) mj[q] = s.MJ[lane][q];
+      float a = 0.f;
+#pragma unroll
+      for (int q = 0; q < NU; ++q) a += s.J[lane][q] * s.us[q];
+      w = a;
+#pragma unroll 1
+      for (int r = 0; r < nrows; ++r) {  // column `lane` of A (A is symmetric: row r, entry lane)
+        const float* jr = s.J[r];
+        float v = 0.f;
+#pragma unroll
+        for (int q = 0; q < NU; ++q) v += jr[q] * mj[q];
+        s.A[r * nrows + lane] = v;
       }
     }
+    __syncthreads();
+    const float mu = s.mu;
+    auto rd = [](float v, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); };
+    const bool row_lane = lane < nrows;
+    // per-row constants live in their row's lane (readlane, no LDS round trip in the sweep)
+    const float tg = row_lane ? s.tgt[lane] : 0.f;
+    const float ia = row_lane ? 1.0f / s.Arr[lane] : 0.f;
+    const uint64_t pairs = __ballot(row_lane && s.rkind[lane] == 1);  // first row of each tangent pair
+    for (int it = 0; it < Pm->solver_iterations; ++it) {
+      for (int r = 0; r < nrows;) {
+        const bool pair = (pairs >> r) & 1ull;
+        const float a0 = row_lane ? s.A[r * nrows + lane] : 0.f;
+        const float a1 = (pair && row_lane) ? s.A[(r + 1) * nrows + lane] : 0.f;
+        if (!pair) {
+          const float wr = rd(w, r), lo = rd(lam, r);
+          const float ln = fmaxf(0.f, lo + (rd(tg, r) - wr) * rd(ia, r));
+          const float d = ln - lo;
+          if (lane == r) lam = ln;
+          w += a0 * d;
+          r += 1;
+        } else {
+          const float w1 = rd(w, r), w2 = rd(w, r + 1);
+          const float o1 = rd(lam, r), o2 = rd(lam, r + 1);
+          float l1 = o1 - w1 * rd(ia, r);
+          float l2 = o2 - w2 * rd(ia, r + 1);
+          const float lim = mu * rd(lam, r - 1);
+          const float n = sqrtf(l1 * l1 + l2 * l2);
+          if (n > lim) {
+            const float sc = n > 0.f ? lim / n : 0.f;
+            l1 *= sc; l2 *= sc;
+          }
+          if (lane == r) lam = l1;
+          if (lane == r + 1) lam = l2;
+          w += a0 * (l1 - o1) + a1 * (l2 - o2);
+          r += 2;
+        }
+      }
+    }
+    if (row_lane) s.lam[lane] = lam;
+    __syncthreads();
+    // u+ = u* + M⁻¹ Jᵀ lambda
+    if (lane < NU) {
+      float uc = s.us[lane];
+#pragma unroll 1
+      for (int r = 0; r < nrows; ++r) uc += s.MJ[r][lane] * s.lam[r];
+      s.up[lane] = uc;
+    }
+    __syncthreads();
+  } else {
+    // ---- wide systems: PGS in velocity space, generalized velocity over lanes 0..17
+    float uc = lane < NU ? s.us[lane] : 0.f;
+    const float mu = s.mu;
+    for (int it = 0; it < Pm->solver_iterations; ++it) {
+      for (int r = 0; r < nrows; ++r) {
+        const int kind = s.rkind[r];
+        if (kind == 0) {
+          float w = row_sums_32(lane < NU ? s.J[r][lane] * uc : 0.f);
+          float lo = s.lam[r];
+          float ln = fmaxf(0.f, lo + (s.tgt[r] - w) / s.Arr[r]);
+          float d = ln - lo;
+          if (lane < NU) uc += s.MJ[r][lane] * d;
+          if (lane == 0) s.lam[r] = ln;
+        } else {
+          float w1 = row_sums_32(lane < NU ? s.J[r][lane] * uc : 0.f);
+          float w2 = row_sums_32(lane < NU ? s.J[r + 1][lane] * uc : 0.f);
+          float o1 = s.lam[r], o2 = s.lam[r + 1];
+          float l1 = o1 - w1 / s.Arr[r];
+          float l2 = o2 - w2 / s.Arr[r + 1];
+          float lim = mu * s.lam[r - 1];
+          float n = sqrtf(l1 * l1 + l2 * l2);
+          if (n > lim) {
+            float sc = n > 0.f ? lim / n : 0.f;
+            l1 *= sc; l2 *= sc;
+          }
+          if (lane < NU) uc += s.MJ[r][lane] * (l1 - o1) + s.MJ[r + 1][lane] * (l2 - o2);
+          if (lane == 0) { s.lam[r] = l1; s.lam[r + 1] = l2; }
+          ++r;
+        }
+      }
+    }
+    if (lane < NU) s.up[lane] = uc;
+    __syncthreads();
   }
-  if (lane < NU) s.up[lane] = uc;
-  __syncthreads();
   // ---- contact forces of the last substep, per reported body (world frame)
   if (last && lane < LGX_MAX_BODIES) {
     float f[3] = {0.f, 0.f, 0.f};

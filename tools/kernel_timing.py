@@ -61,3 +61,7 @@ for it in (0, 1, 4):
     print(f"solver_iterations={it}: {timeit(run(variant(solver_iterations=it))):.1f} us")
 print(f"decimation=1: {timeit(run(variant(decimation=1))):.1f} us")
 print(f"post-physics only: {timeit(run(base, post=True)):.1f} us")
+cf = env.contact_forces.reshape(N, -1, 3).norm(dim=-1)
+nb = (cf > 1e-6).sum(dim=1).float()
+print("bodies in contact per env: mean %.2f p50 %.0f p90 %.0f max %.0f" % (
+    nb.mean().item(), nb.median().item(), torch.quantile(nb, 0.9).item(), nb.max().item()))
