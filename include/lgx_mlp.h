@@ -68,6 +68,35 @@ int32_t lgx_adam_step(float* param, const float* grad, float* exp_avg, float* ex
                       const float* lr_dev, float lr, float beta1, float beta2, float eps, const float* step,
                       const float* grad_scale, void* stream);
 
+/* PPO loss head (rsl_rl ppo.py:196-262 with the Gaussian policy of actor_critic.py:
+ * Normal(mu, std) log_prob / entropy), forward and backward in one kernel each.
+ * Row i of B (A actions):
+ *   logp_i  = sum_j -(a-mu)^2/(2 std_j^2) - log std_j - log sqrt(2 pi)
+ *   r_i     = exp(logp_i - old_logp_i)
+ *   surr    = mean_i max(-adv_i r_i, -adv_i clamp(r_i, 1-clip, 1+clip))
+ *   vloss   = mean_i max((v-R)^2, (tv + clamp(v-tv, -clip, clip) - R)^2)   (clipped_value)
+ *             mean_i (R - v)^2                                              (otherwise)
+ *   entropy = sum_j 0.5 + 0.5 log(2 pi) + log std_j      (= mean_i of the row entropy)
+ *   kl      = mean_i sum_j log(std_j/old_sigma + 1e-5) + (old_sigma^2 + (old_mu-mu)^2)/(2 std_j^2) - 0.5
+ * out[4] = {surr, vloss, entropy, kl}. Backward takes g[3] = d(loss)/d{surr, vloss,
+ * entropy} and writes dmu [B,A], dvalue [B], dstd [A] with torch's gradient rules (max
+ * splits ties evenly, clamp passes on [lo, hi]). Row sums are reduced deterministically
+ * (per-block partials, fixed-order sum by the last block). ws: >= 16 * ceil(B/256) floats;
+ * counter: one zero-initialised uint32 (left at zero). */
+typedef struct lgx_ppo_head_args {
+  const float* mu; const float* value; const float* std; const float* actions;
+  const float* old_logp; const float* adv; const float* target_values; const float* returns;
+  const float* old_mu; const float* old_sigma;
+  int32_t B, A; float clip; int32_t clipped_value;
+  float* out;
+  const float* g;
+  float* dmu; float* dvalue; float* dstd;
+  float* ws; uint32_t* counter;
+} lgx_ppo_head_args;
+
+int32_t lgx_ppo_head_forward(const lgx_ppo_head_args* args, void* stream);
+int32_t lgx_ppo_head_backward(const lgx_ppo_head_args* args, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -433,6 +433,157 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, 
   }
 }
 
+// ---------------------------------------------------------------- PPO loss head
+constexpr int HT = 256;     // rows per block
+constexpr int HMAXA = 16;   // max actions
+
+// block-wide sum of NV values per thread into red[NV] (thread 0 holds the result)
+template <int NV>
+__device__ void block_sum(float (&v)[NV], float* red) {
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    float x = v[k];
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_down(x, o, 64);
+    v[k] = x;
+  }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane == 0)
+#pragma unroll
+    for (int k = 0; k < NV; ++k) red[wv * NV + k] = v[k];
+  __syncthreads();
+  if (threadIdx.x == 0)
+#pragma unroll
+    for (int k = 0; k < NV; ++k) v[k] = red[k] + red[NV + k] + red[2 * NV + k] + red[3 * NV + k];
+}
+
+// last block to finish sums the per-block partials in block order (deterministic)
+__device__ bool last_block(uint32_t* counter) {
+  __shared__ bool last;
+  __threadfence();
+  if (threadIdx.x == 0) last = atomicAdd(counter, 1u) == gridDim.x - 1;
+  __syncthreads();
+  return last;
+}
+
+struct HeadRow {
+  float logp, ratio;
+};
+
+__device__ __forceinline__ HeadRow head_row(const lgx_ppo_head_args& p, int i, const float* stdv, const float* lstd) {
+  const float l2pi = 0.9189385332046727f;  // log(sqrt(2 pi))
+  float lp = 0.f;
+  for (int j = 0; j < p.A; ++j) {
+    const float d = p.actions[(int64_t)i * p.A + j] - p.mu[(int64_t)i * p.A + j];
+    lp += -(d * d) / (2.f * stdv[j] * stdv[j]) - lstd[j] - l2pi;
+  }
+  HeadRow r;
+  r.logp = lp;
+  r.ratio = expf(lp - p.old_logp[i]);
+  return r;
+}
+
+__global__ void ppo_head_fwd(lgx_ppo_head_args p) {
+  __shared__ float red[4 * 4];
+  __shared__ float stdv[HMAXA], lstd[HMAXA];
+  if (threadIdx.x < p.A) { stdv[threadIdx.x] = p.std[threadIdx.x]; lstd[threadIdx.x] = logf(p.std[threadIdx.x]); }
+  __syncthreads();
+  const int i = blockIdx.x * HT + threadIdx.x;
+  float v[3] = {0.f, 0.f, 0.f};
+  if (i < p.B) {
+    const HeadRow h = head_row(p, i, stdv, lstd);
+    const float a = p.adv[i];
+    const float s1 = -a * h.ratio, s2 = -a * fminf(fmaxf(h.ratio, 1.f - p.clip), 1.f + p.clip);
+    v[0] = fmaxf(s1, s2);
+    const float val = p.value[i], R = p.returns[i];
+    if (p.clipped_value) {
+      const float tv = p.target_values[i];
+      const float vc = tv + fminf(fmaxf(val - tv, -p.clip), p.clip);
+      v[1] = fmaxf((val - R) * (val - R), (vc - R) * (vc - R));
+    } else {
+      v[1] = (R - val) * (R - val);
+    }
+    float kl = 0.f;
+    for (int j = 0; j < p.A; ++j) {
+      const float os = p.old_sigma[(int64_t)i * p.A + j], om = p.old_mu[(int64_t)i * p.A + j];
+      const float dm = om - p.mu[(int64_t)i * p.A + j];
+      kl += logf(stdv[j] / os + 1.0e-5f) + (os * os + dm * dm) / (2.f * (stdv[j] * stdv[j])) - 0.5f;
+    }
+    v[2] = kl;
+  }
+  block_sum<3>(v, red);
+  if (threadIdx.x == 0)
+    for (int k = 0; k < 3; ++k) p.ws[blockIdx.x * 3 + k] = v[k];
+  if (last_block(p.counter) && threadIdx.x == 0) {
+    float t[3] = {0.f, 0.f, 0.f};
+    for (int b = 0; b < (int)gridDim.x; ++b)
+      for (int k = 0; k < 3; ++k) t[k] += p.ws[b * 3 + k];
+    float ent = 0.f;
+    for (int j = 0; j < p.A; ++j) ent += 0.5f + 0.9189385332046727f + lstd[j];
+    p.out[0] = t[0] / p.B;
+    p.out[1] = t[1] / p.B;
+    p.out[2] = ent;
+    p.out[3] = t[2] / p.B;
+    *p.counter = 0u;
+  }
+}
+
+__global__ void ppo_head_bwd(lgx_ppo_head_args p) {
+  __shared__ float red[4 * HMAXA];
+  __shared__ float stdv[HMAXA], lstd[HMAXA];
+  if (threadIdx.x < p.A) { stdv[threadIdx.x] = p.std[threadIdx.x]; lstd[threadIdx.x] = logf(p.std[threadIdx.x]); }
+  __syncthreads();
+  const float gs = p.g[0] / p.B, gv = p.g[1] / p.B, ge = p.g[2];
+  const int i = blockIdx.x * HT + threadIdx.x;
+  float ds[HMAXA];
+#pragma unroll
+  for (int j = 0; j < HMAXA; ++j) ds[j] = 0.f;
+  if (i < p.B) {
+    const HeadRow h = head_row(p, i, stdv, lstd);
+    const float a = p.adv[i];
+    const float lo = 1.f - p.clip, hi = 1.f + p.clip;
+    const float s1 = -a * h.ratio, s2 = -a * fminf(fmaxf(h.ratio, lo), hi);
+    // torch.max(s1, s2): ties split evenly; clamp passes on [lo, hi]
+    const float w1 = s1 > s2 ? 1.f : (s1 == s2 ? 0.5f : 0.f);
+    const float w2 = 1.f - w1;
+    const float in = (h.ratio >= lo && h.ratio <= hi) ? 1.f : 0.f;
+    const float dratio = gs * (w1 * -a + w2 * -a * in);
+    const float dlogp = dratio * h.ratio;
+#pragma unroll
+    for (int j = 0; j < HMAXA; ++j) {
+      if (j < p.A) {
+        const float d = p.actions[(int64_t)i * p.A + j] - p.mu[(int64_t)i * p.A + j];
+        const float var = stdv[j] * stdv[j];
+        p.dmu[(int64_t)i * p.A + j] = dlogp * d / var;
+        ds[j] = dlogp * (d * d / (var * stdv[j]) - 1.f / stdv[j]);
+      }
+    }
+    const float val = p.value[i], R = p.returns[i];
+    float dv;
+    if (p.clipped_value) {
+      const float tv = p.target_values[i];
+      const float vc = tv + fminf(fmaxf(val - tv, -p.clip), p.clip);
+      const float l1 = (val - R) * (val - R), l2 = (vc - R) * (vc - R);
+      const float u1 = l1 > l2 ? 1.f : (l1 == l2 ? 0.5f : 0.f);
+      const float inv = (val - tv >= -p.clip && val - tv <= p.clip) ? 1.f : 0.f;
+      dv = gv * (u1 * 2.f * (val - R) + (1.f - u1) * 2.f * (vc - R) * inv);
+    } else {
+      dv = gv * 2.f * (val - R);
+    }
+    p.dvalue[i] = dv;
+  }
+  block_sum<HMAXA>(ds, red);
+  if (threadIdx.x == 0)
+    for (int j = 0; j < p.A; ++j) p.ws[blockIdx.x * HMAXA + j] = ds[j];
+  if (last_block(p.counter) && threadIdx.x == 0) {
+    for (int j = 0; j < p.A; ++j) {
+      float t = 0.f;
+      for (int b = 0; b < (int)gridDim.x; ++b) t += p.ws[b * HMAXA + j];
+      p.dstd[j] = t + ge / stdv[j];  // entropy: d(sum_j log std_j)/d std_j
+    }
+    *p.counter = 0u;
+  }
+}
+
 // dynamic LDS: two K-step stages of hi/lo A and B images, or the fp32 C image (reused)
 constexpr size_t lds_bytes(int bn) {
   const size_t stages = 2 * (2 * A_ELEMS + 2 * bn * PITCH) * sizeof(__bf16);
@@ -499,6 +650,34 @@ int32_t lgx_adam_step(float* param, const float* grad, float* exp_avg, float* ex
   if (blocks > 2048) blocks = 2048;
   hipLaunchKernelGGL(lgxm::adam_kernel, dim3(blocks), dim3(256), 0, static_cast<hipStream_t>(stream), param, grad,
                      exp_avg, exp_avg_sq, n, lr_dev, lr, beta1, beta2, eps, step, grad_scale);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : fail(hipGetErrorString(e));
+}
+
+static int head_check(const lgx_ppo_head_args* a) {
+  if (!a) return fail("lgx_ppo_head: null args");
+  if (a->A < 1 || a->A > lgxm::HMAXA) return fail("lgx_ppo_head: 1 <= A <= 16");
+  if (a->B < 1) return fail("lgx_ppo_head: B >= 1");
+  if (!a->mu || !a->value || !a->std || !a->actions || !a->old_logp || !a->adv || !a->returns || !a->ws || !a->counter)
+    return fail("lgx_ppo_head: null pointer");
+  if (a->clipped_value && !a->target_values) return fail("lgx_ppo_head: clipped_value needs target_values");
+  return 0;
+}
+
+int32_t lgx_ppo_head_forward(const lgx_ppo_head_args* a, void* stream) {
+  if (head_check(a)) return -1;
+  if (!a->out || !a->old_mu || !a->old_sigma) return fail("lgx_ppo_head_forward: null out/old_mu/old_sigma");
+  hipLaunchKernelGGL(lgxm::ppo_head_fwd, dim3((a->B + lgxm::HT - 1) / lgxm::HT), dim3(lgxm::HT), 0,
+                     static_cast<hipStream_t>(stream), *a);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : fail(hipGetErrorString(e));
+}
+
+int32_t lgx_ppo_head_backward(const lgx_ppo_head_args* a, void* stream) {
+  if (head_check(a)) return -1;
+  if (!a->g || !a->dmu || !a->dvalue || !a->dstd) return fail("lgx_ppo_head_backward: null g/dmu/dvalue/dstd");
+  hipLaunchKernelGGL(lgxm::ppo_head_bwd, dim3((a->B + lgxm::HT - 1) / lgxm::HT), dim3(lgxm::HT), 0,
+                     static_cast<hipStream_t>(stream), *a);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : fail(hipGetErrorString(e));
 }

@@ -311,6 +311,43 @@ class PPO:
         s = self.storage
         (obs_b, priv_b, critic_b, est_b, scan_b, actions_b, target_values_b, adv_b, returns_b, old_logp_b,
          old_mu_b, old_sigma_b) = s.gather(idx)
+        if self.on_gpu:
+            # fused loss head: Normal log-prob/entropy, ratio, clipped surrogate, clipped value
+            # loss and KL in one HIP kernel each way (hip_mlp.ppo_head). The privileged latent
+            # is computed once and feeds both the actor and the ROA regulariser (the
+            # reference evaluates the same encoder on the same input twice, ppo.py:190,204)
+            priv_latent = ac.privileged_encoder(priv_b)
+            scan_latent = ac.scan_encoder(scan_b)
+            mu_b = ac.actor(torch.cat((obs_b, priv_latent, scan_latent, est_b), dim=-1))  # TRUE est obs (Q12)
+            value_b = ac.evaluate(critic_b)
+            surrogate_loss, value_loss, entropy_mean, kl_mean = hip_mlp.ppo_head(
+                mu_b, value_b, ac.std, actions_b, old_logp_b, adv_b, target_values_b, returns_b, old_mu_b, old_sigma_b,
+                self.clip_param, self.use_clipped_value_loss)
+            with torch.no_grad():
+                adapt_latent = ac.adaptation_encoder(obs_b)
+            regularization_loss = (priv_latent - adapt_latent).norm(p=2, dim=1).mean()
+            pred = self.estimator(obs_b)
+            estimator_loss = (pred - est_b).norm(p=2, dim=1).pow(2).mean()
+            if self.desired_kl is not None and self.schedule == "adaptive":
+                g.segment("kl").copy_(kl_mean.reshape(1))
+        else:
+            (surrogate_loss, value_loss, entropy_mean, regularization_loss,
+             estimator_loss) = self._losses_torch(obs_b, priv_b, critic_b, est_b, scan_b, actions_b, target_values_b,
+                                                  adv_b, returns_b, old_logp_b, old_mu_b, old_sigma_b)
+        loss = surrogate_loss + self.value_loss_coef * value_loss - self.entropy_coef * entropy_mean + \
+            self._reg_coef * regularization_loss
+        # zero_grad of `optimizer` and `estimator_optimizer` (adaptation grads stay)
+        g.span("main", "estimator").zero_()
+        estimator_loss.backward()
+        loss.backward()
+        with torch.no_grad():
+            self._losses.copy_(torch.stack([value_loss, surrogate_loss, regularization_loss, estimator_loss]))
+        ac.distribution = None
+
+    def _losses_torch(self, obs_b, priv_b, critic_b, est_b, scan_b, actions_b, target_values_b, adv_b, returns_b,
+                      old_logp_b, old_mu_b, old_sigma_b):
+        """The reference's loss terms in torch ops (CPU learner): ppo.py:186-260."""
+        ac = self.actor_critic
         # the sample drawn by act() in the reference's update is unused: build the distribution only
         ac.update_distribution(obs_b, priv_b, est_b, scan_b, adaptation_mode=False)  # TRUE est obs (Q12)
         logp_b = ac.get_actions_log_prob(actions_b)
@@ -327,7 +364,7 @@ class PPO:
                 kl = torch.sum(torch.log(sigma_b / old_sigma_b + 1.0e-5) +
                                (torch.square(old_sigma_b) + torch.square(old_mu_b - mu_b)) /
                                (2.0 * torch.square(sigma_b)) - 0.5, axis=-1)
-                g.segment("kl").copy_(kl.mean().reshape(1))
+                self.grads.segment("kl").copy_(kl.mean().reshape(1))
         ratio = torch.exp(logp_b - torch.squeeze(old_logp_b))
         surrogate = -torch.squeeze(adv_b) * ratio
         surrogate_clipped = -torch.squeeze(adv_b) * torch.clamp(ratio, 1.0 - self.clip_param, 1.0 + self.clip_param)
@@ -337,15 +374,7 @@ class PPO:
             value_loss = torch.max((value_b - returns_b).pow(2), (value_clipped - returns_b).pow(2)).mean()
         else:
             value_loss = (returns_b - value_b).pow(2).mean()
-        loss = surrogate_loss + self.value_loss_coef * value_loss - self.entropy_coef * entropy_b.mean() + \
-            self._reg_coef * regularization_loss
-        # zero_grad of `optimizer` and `estimator_optimizer` (adaptation grads stay)
-        g.span("main", "estimator").zero_()
-        estimator_loss.backward()
-        loss.backward()
-        with torch.no_grad():
-            self._losses.copy_(torch.stack([value_loss, surrogate_loss, regularization_loss, estimator_loss]))
-        ac.distribution = None
+        return surrogate_loss, value_loss, entropy_b.mean(), regularization_loss, estimator_loss
 
     def _minibatch_step(self):
         """Phase B: (ranks averaged) clip + estimator step, KL schedule, clip + main step."""

@@ -23,7 +23,7 @@ _lib = None
 ABI_VERSION = 1
 EPI_BIAS, EPI_ELU, EPI_DELU, EPI_ACCUM = 1, 2, 4, 8
 EXPORTED = ["lgx_mlp_abi_version", "lgx_mlp_sizeof_gemm_args", "lgx_mlp_pick_split", "lgx_gemm",
-            "lgx_mlp_last_error", "lgx_adam_step"]
+            "lgx_mlp_last_error", "lgx_adam_step", "lgx_ppo_head_forward", "lgx_ppo_head_backward"]
 
 
 class GemmArgs(C.Structure):
@@ -35,6 +35,15 @@ class GemmArgs(C.Structure):
                 ("bias", C.c_void_p), ("act", C.c_void_p), ("ld_act", C.c_int64),
                 ("split_k", C.c_int32), ("workspace", C.c_void_p), ("colsum", C.c_void_p),
                 ("colsum_ws", C.c_void_p)]
+
+
+class HeadArgs(C.Structure):
+    """Mirror of lgx_ppo_head_args (include/lgx_mlp.h)."""
+    _fields_ = [(n, C.c_void_p) for n in ("mu", "value", "std", "actions", "old_logp", "adv", "target_values",
+                                          "returns", "old_mu", "old_sigma")] + \
+               [("B", C.c_int32), ("A", C.c_int32), ("clip", C.c_float), ("clipped_value", C.c_int32),
+                ("out", C.c_void_p), ("g", C.c_void_p), ("dmu", C.c_void_p), ("dvalue", C.c_void_p),
+                ("dstd", C.c_void_p), ("ws", C.c_void_p), ("counter", C.c_void_p)]
 
 
 class MlpLibError(RuntimeError):
@@ -55,6 +64,10 @@ def lib():
     L.lgx_gemm.restype = C.c_int32
     L.lgx_mlp_last_error.restype = C.c_char_p
     vp, f32 = C.c_void_p, C.c_float
+    L.lgx_ppo_head_forward.argtypes = [vp, vp]
+    L.lgx_ppo_head_forward.restype = C.c_int32
+    L.lgx_ppo_head_backward.argtypes = [vp, vp]
+    L.lgx_ppo_head_backward.restype = C.c_int32
     L.lgx_adam_step.argtypes = [vp, vp, vp, vp, C.c_int64, vp, f32, f32, f32, f32, vp, vp, vp]
     L.lgx_adam_step.restype = C.c_int32
     if L.lgx_mlp_abi_version() != ABI_VERSION:
@@ -348,3 +361,72 @@ def adaptation_forward(mod, hist):
     ps = (mod.fc_encoder[0].weight, mod.fc_encoder[0].bias, mod.conv_layers[0].weight, mod.conv_layers[0].bias,
           mod.conv_layers[2].weight, mod.conv_layers[2].bias, mod.fc_final[0].weight, mod.fc_final[0].bias)
     return _AdaptationFn.apply(hist, dims, *ps)
+
+
+# ---------------------------------------------------------------------------------------
+# PPO loss head (ppo.py:196-262 over actor_critic.py's Normal(mu, std)): surrogate, clipped
+# value loss, entropy and KL as one forward and one backward kernel (lgx_ppo_head_*).
+# ---------------------------------------------------------------------------------------
+_head_counter = {}
+
+
+def _counter(dev):
+    c = _head_counter.get(dev)
+    if c is None:
+        c = _head_counter[dev] = torch.zeros(1, dtype=torch.int32, device=dev)
+    return c
+
+
+class _PPOHeadFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, mu, value, std, actions, old_logp, adv, target_values, returns, old_mu, old_sigma, clip,
+                clipped_value):
+        B, A = mu.shape
+        dev = mu.device
+        ts = [_rowmajor(t.reshape(B, -1)) for t in (mu, value, actions, old_logp, adv, target_values, returns, old_mu,
+                                                     old_sigma)]
+        mu_, value_, actions_, old_logp_, adv_, tv_, ret_, old_mu_, old_sigma_ = ts
+        std_ = std.contiguous()
+        out = torch.empty(4, device=dev)
+        ws = torch.empty(16 * ((B + 255) // 256), device=dev)
+        a = HeadArgs(mu=mu_.data_ptr(), value=value_.data_ptr(), std=std_.data_ptr(), actions=actions_.data_ptr(),
+                     old_logp=old_logp_.data_ptr(), adv=adv_.data_ptr(), target_values=tv_.data_ptr(),
+                     returns=ret_.data_ptr(), old_mu=old_mu_.data_ptr(), old_sigma=old_sigma_.data_ptr(), B=B, A=A,
+                     clip=float(clip), clipped_value=int(bool(clipped_value)), out=out.data_ptr(), ws=ws.data_ptr(),
+                     counter=_counter(dev).data_ptr())
+        L = lib()
+        if L.lgx_ppo_head_forward(C.byref(a), C.c_void_p(torch.cuda.current_stream().cuda_stream)) != 0:
+            raise MlpLibError("lgx_ppo_head_forward: " + L.lgx_mlp_last_error().decode())
+        ctx.save_for_backward(mu_, value_, std_, actions_, old_logp_, adv_, tv_, ret_)
+        ctx.clip, ctx.clipped = float(clip), int(bool(clipped_value))
+        ctx.value_shape = value.shape
+        ctx.mark_non_differentiable(out)
+        return out[0], out[1], out[2], out[3]
+
+    @staticmethod
+    def backward(ctx, g_surr, g_value, g_ent, g_kl):
+        mu, value, std, actions, old_logp, adv, tv, ret = ctx.saved_tensors
+        B, A = mu.shape
+        dev = mu.device
+        z = torch.zeros((), device=dev)
+        g = torch.stack([g_surr if g_surr is not None else z, g_value if g_value is not None else z,
+                         g_ent if g_ent is not None else z]).float().contiguous()
+        dmu = torch.empty_like(mu)
+        dvalue = torch.empty(B, device=dev)
+        dstd = torch.empty_like(std)
+        ws = torch.empty(16 * ((B + 255) // 256), device=dev)
+        a = HeadArgs(mu=mu.data_ptr(), value=value.data_ptr(), std=std.data_ptr(), actions=actions.data_ptr(),
+                     old_logp=old_logp.data_ptr(), adv=adv.data_ptr(), target_values=tv.data_ptr(),
+                     returns=ret.data_ptr(), B=B, A=A, clip=ctx.clip, clipped_value=ctx.clipped, g=g.data_ptr(),
+                     dmu=dmu.data_ptr(), dvalue=dvalue.data_ptr(), dstd=dstd.data_ptr(), ws=ws.data_ptr(),
+                     counter=_counter(dev).data_ptr())
+        L = lib()
+        if L.lgx_ppo_head_backward(C.byref(a), C.c_void_p(torch.cuda.current_stream().cuda_stream)) != 0:
+            raise MlpLibError("lgx_ppo_head_backward: " + L.lgx_mlp_last_error().decode())
+        return (dmu, dvalue.view(ctx.value_shape), dstd) + (None,) * 9
+
+
+def ppo_head(mu, value, std, actions, old_logp, adv, target_values, returns, old_mu, old_sigma, clip, clipped_value):
+    """(surrogate_loss, value_loss, entropy_mean, kl_mean) on the HIP device; kl carries no grad."""
+    return _PPOHeadFn.apply(mu, value, std, actions, old_logp, adv, target_values, returns, old_mu, old_sigma, clip,
+                            clipped_value)

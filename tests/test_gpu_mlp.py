@@ -102,3 +102,50 @@ def test_adaptation_encoder_matches_torch_fp64():
     for (n, p), (_, pr) in zip(enc.named_parameters(), ref.named_parameters()):
         scale = pr.grad.abs().max().item()
         torch.testing.assert_close(p.grad.double().cpu(), pr.grad, rtol=1e-3, atol=1e-4 * scale, msg=n)
+
+
+@pytest.mark.parametrize("clipped", [True, False])
+def test_ppo_head_matches_torch_autograd(clipped):
+    """lgx_ppo_head_{forward,backward} vs the reference's loss code (ppo.py:196-262 over
+    torch.distributions.Normal) differentiated by torch autograd in fp64."""
+    from torch.distributions import Normal
+    g = torch.Generator(device=dev).manual_seed(11)
+    B, A, clip = 3000, 12, 0.2
+    r = lambda *s: torch.randn(*s, device=dev, generator=g)  # noqa: E731
+    mu, value, std = r(B, A), r(B, 1), torch.rand(A, device=dev, generator=g) + 0.3
+    actions, old_mu = mu + 0.3 * r(B, A), mu + 0.1 * r(B, A)
+    old_sigma = std + 0.05 * torch.rand(B, A, device=dev, generator=g)
+    adv, tv, ret = r(B, 1), value + 0.3 * r(B, 1), r(B, 1)
+    adv[:50] = 0.0  # surrogate ties (s1 == s2): torch.max splits the gradient
+    lp_ref = Normal(mu.double(), std.double()).log_prob(actions.double()).sum(-1)
+    old_logp = (lp_ref + 0.15 * r(B).double()).float().reshape(B, 1)
+    old_logp[50:60, 0] = lp_ref[50:60].float()  # ratio exactly 1 (inside the clip range)
+
+    def reference(mu, value, std):
+        d = Normal(mu, mu * 0.0 + std)
+        logp = d.log_prob(actions.double()).sum(-1)
+        ratio = torch.exp(logp - old_logp.double().squeeze())
+        a = adv.double().squeeze()
+        surr = torch.max(-a * ratio, -a * torch.clamp(ratio, 1 - clip, 1 + clip)).mean()
+        if clipped:
+            vc = tv.double() + (value - tv.double()).clamp(-clip, clip)
+            vl = torch.max((value - ret.double()).pow(2), (vc - ret.double()).pow(2)).mean()
+        else:
+            vl = (ret.double() - value).pow(2).mean()
+        ent = d.entropy().sum(-1).mean()
+        sig = d.stddev
+        kl = torch.sum(torch.log(sig / old_sigma.double() + 1e-5) + (old_sigma.double() ** 2 + (old_mu.double() - mu) ** 2)
+                       / (2.0 * sig ** 2) - 0.5, -1).mean()
+        return surr, vl, ent, kl
+
+    m64, v64, s64 = (t.double().requires_grad_(True) for t in (mu, value, std))
+    rs, rv, re, rk = reference(m64, v64, s64)
+    (rs + 0.7 * rv - 0.01 * re).backward()
+    m32, v32, s32 = (t.clone().requires_grad_(True) for t in (mu, value, std))
+    hs, hv, he, hk = H.ppo_head(m32, v32, s32, actions, old_logp, adv, tv, ret, old_mu, old_sigma, clip, clipped)
+    (hs + 0.7 * hv - 0.01 * he).backward()
+    for got, want in ((hs, rs), (hv, rv), (he, re), (hk, rk)):
+        torch.testing.assert_close(got.double(), want.detach(), rtol=2e-5, atol=1e-6)
+    torch.testing.assert_close(m32.grad.double(), m64.grad, rtol=1e-4, atol=1e-8)
+    torch.testing.assert_close(v32.grad.double(), v64.grad, rtol=1e-4, atol=1e-8)
+    torch.testing.assert_close(s32.grad.double(), s64.grad, rtol=1e-4, atol=1e-7)
