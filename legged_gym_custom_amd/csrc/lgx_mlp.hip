@@ -370,27 +370,70 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(Params p) {
   }
 }
 
-// C (=|+=) epilogue(sum_z ws[z]) and colsum[m] (=|+=) sum_z colsum_ws[z][m], fixed z order.
+// C (=|+=) epilogue(sum_z ws[z]) and colsum[m] (=|+=) sum_z colsum_ws[z][m]. Each thread owns
+// 4 consecutive outputs (float4 when N % 4 == 0) and walks the splits with 4 independent
+// accumulators (z mod 4) combined in a fixed order: deterministic, memory-level parallel.
+__device__ __forceinline__ float sum_splits(const float* ws, int64_t stride, int split, int64_t i) {
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  int z = 0;
+  for (; z + 4 <= split; z += 4) {
+    a0 += ws[(z + 0) * stride + i]; a1 += ws[(z + 1) * stride + i];
+    a2 += ws[(z + 2) * stride + i]; a3 += ws[(z + 3) * stride + i];
+  }
+  for (; z < split; ++z) a0 += ws[z * stride + i];
+  return (a0 + a1) + (a2 + a3);
+}
+
 __global__ void splitk_reduce(Params p, float* colsum) {
   const int64_t mn = (int64_t)p.M * p.N;
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < mn) {
-    float v = 0.f;
-    for (int z = 0; z < p.split; ++z) v += p.ws[z * mn + i];
-    const int m = (int)(i / p.N), n = (int)(i % p.N);
-    if (p.epi & LGX_EPI_BIAS) v += p.bias[n];
-    if (p.epi & LGX_EPI_ELU) v = v > 0.f ? v : expm1f(v);
-    if (p.epi & LGX_EPI_DELU) {
-      const float y = p.act[(int64_t)m * p.ld_act + n];
-      v *= y > 0.f ? 1.f : y + 1.f;
+  const int64_t q = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (q < mn) {
+    const bool vec = (p.N % 4 == 0) && p.c_vec && p.ws_vec;
+    float v[4];
+    if (vec) {
+      float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a, c = a, d = a;
+      int z = 0;
+      for (; z + 4 <= p.split; z += 4) {
+        const float4 x0 = *reinterpret_cast<const float4*>(p.ws + (z + 0) * mn + q);
+        const float4 x1 = *reinterpret_cast<const float4*>(p.ws + (z + 1) * mn + q);
+        const float4 x2 = *reinterpret_cast<const float4*>(p.ws + (z + 2) * mn + q);
+        const float4 x3 = *reinterpret_cast<const float4*>(p.ws + (z + 3) * mn + q);
+        a.x += x0.x; a.y += x0.y; a.z += x0.z; a.w += x0.w;
+        b.x += x1.x; b.y += x1.y; b.z += x1.z; b.w += x1.w;
+        c.x += x2.x; c.y += x2.y; c.z += x2.z; c.w += x2.w;
+        d.x += x3.x; d.y += x3.y; d.z += x3.z; d.w += x3.w;
+      }
+      for (; z < p.split; ++z) {
+        const float4 x = *reinterpret_cast<const float4*>(p.ws + z * mn + q);
+        a.x += x.x; a.y += x.y; a.z += x.z; a.w += x.w;
+      }
+      v[0] = (a.x + b.x) + (c.x + d.x); v[1] = (a.y + b.y) + (c.y + d.y);
+      v[2] = (a.z + b.z) + (c.z + d.z); v[3] = (a.w + b.w) + (c.w + d.w);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = q + e < mn ? sum_splits(p.ws, mn, p.split, q + e) : 0.f;
     }
-    float* c = p.C + (int64_t)m * p.ldc + n;
-    *c = (p.epi & LGX_EPI_ACCUM) ? *c + v : v;
-  } else if (colsum != nullptr && i < mn + p.M) {
-    const int m = (int)(i - mn);
-    float v = 0.f;
-    for (int z = 0; z < p.split; ++z) v += p.colsum_ws[(int64_t)z * p.M + m];
-    colsum[m] = (p.epi & LGX_EPI_ACCUM) ? colsum[m] + v : v;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int64_t i = q + e;
+      if (i >= mn) break;
+      const int m = (int)(i / p.N), n = (int)(i % p.N);
+      float x = v[e];
+      if (p.epi & LGX_EPI_BIAS) x += p.bias[n];
+      if (p.epi & LGX_EPI_ELU) x = x > 0.f ? x : expm1f(x);
+      if (p.epi & LGX_EPI_DELU) {
+        const float y = p.act[(int64_t)m * p.ld_act + n];
+        x *= y > 0.f ? 1.f : y + 1.f;
+      }
+      float* c = p.C + (int64_t)m * p.ldc + n;
+      *c = (p.epi & LGX_EPI_ACCUM) ? *c + x : x;
+    }
+  }
+  // bias gradient: one thread per row of A beyond the M*N range
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x - (mn + 3) / 4;
+  if (colsum != nullptr && t >= 0 && t < p.M) {
+    const float x = sum_splits(p.colsum_ws, p.M, p.split, t);
+    colsum[t] = (p.epi & LGX_EPI_ACCUM) ? colsum[t] + x : x;
   }
 }
 
@@ -513,17 +556,19 @@ __global__ void ppo_head_fwd(lgx_ppo_head_args p) {
   block_sum<3>(v, red);
   if (threadIdx.x == 0)
     for (int k = 0; k < 3; ++k) p.ws[blockIdx.x * 3 + k] = v[k];
-  if (last_block(p.counter) && threadIdx.x == 0) {
-    float t[3] = {0.f, 0.f, 0.f};
-    for (int b = 0; b < (int)gridDim.x; ++b)
-      for (int k = 0; k < 3; ++k) t[k] += p.ws[b * 3 + k];
-    float ent = 0.f;
-    for (int j = 0; j < p.A; ++j) ent += 0.5f + 0.9189385332046727f + lstd[j];
-    p.out[0] = t[0] / p.B;
-    p.out[1] = t[1] / p.B;
-    p.out[2] = ent;
-    p.out[3] = t[2] / p.B;
-    *p.counter = 0u;
+  if (last_block(p.counter)) {
+    // threads k < 3 each sum one quantity over the blocks, in block order
+    if (threadIdx.x < 3) {
+      float t = 0.f;
+      for (int b = 0; b < (int)gridDim.x; ++b) t += p.ws[b * 3 + threadIdx.x];
+      p.out[threadIdx.x == 2 ? 3 : threadIdx.x] = t / p.B;
+    }
+    if (threadIdx.x == 3) {
+      float ent = 0.f;
+      for (int j = 0; j < p.A; ++j) ent += 0.5f + 0.9189385332046727f + lstd[j];
+      p.out[2] = ent;
+    }
+    if (threadIdx.x == 0) *p.counter = 0u;
   }
 }
 
@@ -574,13 +619,14 @@ __global__ void ppo_head_bwd(lgx_ppo_head_args p) {
   block_sum<HMAXA>(ds, red);
   if (threadIdx.x == 0)
     for (int j = 0; j < p.A; ++j) p.ws[blockIdx.x * HMAXA + j] = ds[j];
-  if (last_block(p.counter) && threadIdx.x == 0) {
-    for (int j = 0; j < p.A; ++j) {
+  if (last_block(p.counter)) {
+    const int j = threadIdx.x;
+    if (j < p.A) {  // one action column per thread, blocks in order
       float t = 0.f;
       for (int b = 0; b < (int)gridDim.x; ++b) t += p.ws[b * HMAXA + j];
       p.dstd[j] = t + ge / stdv[j];  // entropy: d(sum_j log std_j)/d std_j
     }
-    *p.counter = 0u;
+    if (j == 0) *p.counter = 0u;
   }
 }
 
@@ -709,7 +755,7 @@ int32_t lgx_gemm(const lgx_gemm_args* a, void* stream) {
   const bool cs = a->colsum != nullptr;
   if (cs && (a->a_kcontig || !a->colsum_ws)) return fail("lgx_gemm: colsum needs a_kcontig = 0 and colsum_ws");
   if (cs && split == 1) return fail("lgx_gemm: colsum requires split_k > 1");
-  if (a->a_kcontig != a->b_kcontig) return fail("lgx_gemm: mixed operand layouts are not built");
+  if (!a->a_kcontig && a->b_kcontig) return fail("lgx_gemm: a_kcontig = 0 with b_kcontig = 1 is not built");
   Params p;
   p.A = a->A; p.lda = a->lda; p.B = a->B; p.ldb = a->ldb; p.C = a->C; p.ldc = a->ldc;
   p.M = a->M; p.N = a->N; p.K = a->K; p.epi = a->epilogue; p.bias = a->bias; p.act = a->act;
@@ -726,7 +772,12 @@ int32_t lgx_gemm(const lgx_gemm_args* a, void* stream) {
   // float4 staging needs 16-B aligned rows (k-contiguous) or 4-aligned columns (m/n-contiguous)
   const bool va = (a->lda % 4 == 0) && aligned16(a->A) && (a->a_kcontig || a->M % 4 == 0);
   const bool vb = (a->ldb % 4 == 0) && aligned16(a->B) && (a->b_kcontig || a->N % 4 == 0);
-  if (a->a_kcontig) {
+  if (a->a_kcontig && !a->b_kcontig) {  // input gradient with W read in place (n-contiguous)
+    if (va && vb) launch<KV, MV, false>(p, bn, s);
+    else if (va) launch<KV, MS, false>(p, bn, s);
+    else if (vb) launch<KS, MV, false>(p, bn, s);
+    else launch<KS, MS, false>(p, bn, s);
+  } else if (a->a_kcontig) {
     if (va && vb) launch<KV, KV, false>(p, bn, s);
     else if (va) launch<KV, KS, false>(p, bn, s);
     else if (vb) launch<KS, KV, false>(p, bn, s);
@@ -745,7 +796,7 @@ int32_t lgx_gemm(const lgx_gemm_args* a, void* stream) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(hipGetErrorString(e));
   if (split > 1) {
-    const int64_t n = (int64_t)a->M * a->N + (cs ? a->M : 0);
+    const int64_t n = ((int64_t)a->M * a->N + 3) / 4 + (cs ? a->M : 0);  // float4 outputs + bias rows
     hipLaunchKernelGGL(splitk_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, p, a->colsum);
     e = hipGetLastError();
     if (e != hipSuccess) return fail(hipGetErrorString(e));

@@ -137,12 +137,17 @@ def linear_forward(x, W, b, elu, out=None):
 
 def linear_input_grad(g, W, y_prev=None, Wt=None):
     """dX[M,K] = (dY[M,N] W[N,K]) * ELU'(y_prev) (when the layer input is an ELU output).
-    W is read through its transpose (Wt[K,N], contiguous) so both operands stream k-contiguous."""
+    W is read in place: B(k=n_out, n=k_in) = W[n_out, k_in] is n-contiguous (float4 staging
+    along n when aligned); pass Wt ([K,N] contiguous) to stream it k-contiguous instead."""
     g = _rowmajor(g)
     M, N = g.shape
     K = W.shape[1]
-    Wt = W.t().contiguous() if Wt is None else Wt
     dx = torch.empty(M, K, device=g.device, dtype=torch.float32)
+    if Wt is None:
+        _run(GemmArgs(A=_ptr(g), lda=g.stride(0), a_kcontig=1, B=_ptr(W), ldb=W.stride(0), b_kcontig=0,
+                      C=_ptr(dx), ldc=dx.stride(0), M=M, N=K, K=N, epilogue=EPI_DELU if y_prev is not None else 0,
+                      act=_ptr(y_prev), ld_act=0 if y_prev is None else y_prev.stride(0), split_k=1))
+        return dx
     _run(GemmArgs(A=_ptr(g), lda=g.stride(0), a_kcontig=1, B=_ptr(Wt), ldb=Wt.stride(0), b_kcontig=1,
                   C=_ptr(dx), ldc=dx.stride(0), M=M, N=K, K=N, epilogue=EPI_DELU if y_prev is not None else 0,
                   act=_ptr(y_prev), ld_act=0 if y_prev is None else y_prev.stride(0), split_k=1))
