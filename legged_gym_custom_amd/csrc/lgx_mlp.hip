@@ -674,7 +674,7 @@ static int tile_n(int N) {
     forced = e ? atoi(e) : 0;
   }
   if (forced == 64 || forced == 128) return forced;
-  return N >= 128 ? 128 : 64;
+  return N > 128 ? 128 : 64;
 }
 
 extern "C" {
