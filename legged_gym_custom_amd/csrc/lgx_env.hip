@@ -44,7 +44,12 @@ struct Scratch {  // per-env post-physics scalars (go2.py:357-367, 279-328)
   float jump;
 };
 
-constexpr int AMAX = 41;  // rows of the explicit-A PGS (A overlays the post-physics staging)
+// LDS arena time-shared by phase (dynamics temporaries -> constraint rows -> post-physics
+// staging): J [n][NU], M⁻¹Jᵀ [n][NU] and, for n <= AMAX rows, A = J M⁻¹ Jᵀ [n][n]
+constexpr int ARENA = 2200;
+constexpr int AMAX = 32;
+static_assert(2 * MAXR * NU <= ARENA, "arena must hold J and M^-1 J^T at MAXR rows");
+static_assert(2 * AMAX * NU + AMAX * AMAX <= ARENA, "arena must hold J, M^-1 J^T and A at AMAX rows");
 
 struct Sh {
   // --- post-physics per-env scalars (written by lane 0, read by all lanes)
@@ -61,28 +66,30 @@ struct Sh {
   // --- kinematics per dynamic link
   float R[NL][9], P[NL][3], Ax[NL][3], W[NL][3], V[NL][3], Al[NL][3], Ao[NL][3], C[NL][3], I[NL][6], m[NL];
   // --- dynamics
-  float red[NL][16];  // per-link partials about p0: m, h(3), Ip(6), F(3), N(3)
-  float tot[16];
-  float Fw[NL][3], Nw[NL][3];  // per-link COM wrench (bias)
-  float Dl[4][6];
-  float Bc[NJ][6], Dinv[4][6], X[NJ][6], S[4][21], L[21], hj[NJ], hb[6], us[NU], up[NU];
-  // --- constraints
-  float J[MAXR][NU], MJ[MAXR][NU], Arr[MAXR], tgt[MAXR], lam[MAXR];
+  float Bc[NJ][6], Dinv[4][6], X[NJ][6], L[21], hj[NJ], hb[6], us[NU], up[NU];
+  // --- constraints (J, M⁻¹Jᵀ and A live in the arena below)
+  float Arr[MAXR], tgt[MAXR], lam[MAXR];
   int rkind[MAXR];
   int cbody[MAXC];
   int nrows, nlim, ncon;
   float cf[LGX_MAX_BODIES][3];
   float rbz[LGX_MAX_BODIES];
-  // --- post-physics staging; during the substeps the same LDS holds the Delassus
-  //     matrix A = J M⁻¹ Jᵀ of the active constraint rows (PGS, nrows <= AMAX)
+  // --- one arena, three phases (never live at the same time)
   union {
-    struct {
+    struct {  // post-physics staging
       float U[NSLOT];
       float cur[LGX_MAX_PROPRIO];
       float hist[MAXHIST];
       float heights[LGX_MAX_HEIGHT_POINTS];
     };
-    float A[AMAX * AMAX];
+    struct {  // dynamics() temporaries
+      float red[NL][16];  // per-link partials about p0: m, h(3), Ip(6), F(3), N(3)
+      float tot[16];
+      float Fw[NL][3], Nw[NL][3];  // per-link COM wrench (bias)
+      float Dl[4][6];
+      float S[4][21];
+    };
+    float arena[ARENA];  // constraint rows: J, M⁻¹Jᵀ, A (see ARENA)
   };
 };
 
@@ -432,11 +439,14 @@ LGX_DEV void substep(Sh& s, const lgx_model* M, const lgx_task_params* Pm, const
     else tv = d / dt;
     return tv;
   };
+  float* const J = s.arena;                 // [nrows][NU]
+  float* const MJ = s.arena + nrows * NU;   // [nrows][NU]
+  float* const Am = s.arena + 2 * nrows * NU;  // [nrows][nrows] (A path)
   if (lim_lo || lim_hi) {
     int r = __popcll(lmask & below);
 #pragma unroll
-    for (int q = 0; q < NU; ++q) s.J[r][q] = 0.f;
-    s.J[r][6 + lane] = lim_lo ? 1.f : -1.f;
+    for (int q = 0; q < NU; ++q) J[(r) * NU + q] = 0.f;
+    J[(r) * NU + 6 + lane] = lim_lo ? 1.f : -1.f;
     float d = lim_lo ? (M->joint_lower[lane + 1] - s.th[lane]) : (s.th[lane] - M->joint_upper[lane + 1]);
     s.tgt[r] = target(d);
     s.rkind[r] = 0;
@@ -452,13 +462,13 @@ LGX_DEV void substep(Sh& s, const lgx_model* M, const lgx_task_params* Pm, const
       const int r = r0 + t;
       const f3 d = dirs[t];
       f3 ang = cross(xc - p0, d);
-      s.J[r][0] = d.x; s.J[r][1] = d.y; s.J[r][2] = d.z;
-      s.J[r][3] = ang.x; s.J[r][4] = ang.y; s.J[r][5] = ang.z;
+      J[(r) * NU + 0] = d.x; J[(r) * NU + 1] = d.y; J[(r) * NU + 2] = d.z;
+      J[(r) * NU + 3] = ang.x; J[(r) * NU + 4] = ang.y; J[(r) * NU + 5] = ang.z;
 #pragma unroll 4
-      for (int q = 0; q < NJ; ++q) s.J[r][6 + q] = 0.f;
+      for (int q = 0; q < NJ; ++q) J[(r) * NU + 6 + q] = 0.f;
       for (int i = 0; i <= pos; ++i) {
         const int ki = 1 + 3 * leg + i;
-        s.J[r][6 + 3 * leg + i] = dot(ld3(s.Ax[ki]), cross(xc - ld3(s.P[ki]), d));
+        J[(r) * NU + 6 + 3 * leg + i] = dot(ld3(s.Ax[ki]), cross(xc - ld3(s.P[ki]), d));
       }
       s.rkind[r] = t;
       s.tgt[r] = t == 0 ? target(depth) : 0.f;
@@ -472,10 +482,10 @@ LGX_DEV void substep(Sh& s, const lgx_model* M, const lgx_task_params* Pm, const
 #endif
   // ---- per-row M⁻¹Jᵀ column and diagonal of A = J M⁻¹ Jᵀ (one lane per row)
   if (lane < nrows) {
-    mass_solve(s, s.J[lane], s.MJ[lane]);
+    mass_solve(s, J + lane * NU, MJ + lane * NU);
     float a = 0.f;
 #pragma unroll 1
-    for (int q = 0; q < NU; ++q) a += s.J[lane][q] * s.MJ[lane][q];
+    for (int q = 0; q < NU; ++q) a += J[(lane) * NU + q] * MJ[(lane) * NU + q];
     s.Arr[lane] = a;
     s.lam[lane] = 0.f;
   }
@@ -491,18 +501,18 @@ LGX_DEV void substep(Sh& s, const lgx_model* M, const lgx_task_params* Pm, const
     if (lane < nrows) {
       float mj[NU];
 #pragma unroll
-      for (int q = 0; q < NU; ++q) mj[q] = s.MJ[lane][q];
+      for (int q = 0; q < NU; ++q) mj[q] = MJ[(lane) * NU + q];
       float a = 0.f;
 #pragma unroll
-      for (int q = 0; q < NU; ++q) a += s.J[lane][q] * s.us[q];
+      for (int q = 0; q < NU; ++q) a += J[(lane) * NU + q] * s.us[q];
       w = a;
 #pragma unroll 1
       for (int r = 0; r < nrows; ++r) {  // column `lane` of A (A is symmetric: row r, entry lane)
-        const float* jr = s.J[r];
+        const float* jr = J + r * NU;
         float v = 0.f;
 #pragma unroll
         for (int q = 0; q < NU; ++q) v += jr[q] * mj[q];
-        s.A[r * nrows + lane] = v;
+        Am[r * nrows + lane] = v;
       }
     }
     __syncthreads();
@@ -516,8 +526,8 @@ LGX_DEV void substep(Sh& s, const lgx_model* M, const lgx_task_params* Pm, const
     for (int it = 0; it < Pm->solver_iterations; ++it) {
       for (int r = 0; r < nrows;) {
         const bool pair = (pairs >> r) & 1ull;
-        const float a0 = row_lane ? s.A[r * nrows + lane] : 0.f;
-        const float a1 = (pair && row_lane) ? s.A[(r + 1) * nrows + lane] : 0.f;
+        const float a0 = row_lane ? Am[r * nrows + lane] : 0.f;
+        const float a1 = (pair && row_lane) ? Am[(r + 1) * nrows + lane] : 0.f;
         if (!pair) {
           const float wr = rd(w, r), lo = rd(lam, r);
           const float ln = fmaxf(0.f, lo + (rd(tg, r) - wr) * rd(ia, r));
@@ -549,7 +559,7 @@ LGX_DEV void substep(Sh& s, const lgx_model* M, const lgx_task_params* Pm, const
     if (lane < NU) {
       float uc = s.us[lane];
 #pragma unroll 1
-      for (int r = 0; r < nrows; ++r) uc += s.MJ[r][lane] * s.lam[r];
+      for (int r = 0; r < nrows; ++r) uc += MJ[(r) * NU + lane] * s.lam[r];
       s.up[lane] = uc;
     }
     __syncthreads();
@@ -561,15 +571,15 @@ LGX_DEV void substep(Sh& s, const lgx_model* M, const lgx_task_params* Pm, const
       for (int r = 0; r < nrows; ++r) {
         const int kind = s.rkind[r];
         if (kind == 0) {
-          float w = row_sums_32(lane < NU ? s.J[r][lane] * uc : 0.f);
+          float w = row_sums_32(lane < NU ? J[(r) * NU + lane] * uc : 0.f);
           float lo = s.lam[r];
           float ln = fmaxf(0.f, lo + (s.tgt[r] - w) / s.Arr[r]);
           float d = ln - lo;
-          if (lane < NU) uc += s.MJ[r][lane] * d;
+          if (lane < NU) uc += MJ[(r) * NU + lane] * d;
           if (lane == 0) s.lam[r] = ln;
         } else {
-          float w1 = row_sums_32(lane < NU ? s.J[r][lane] * uc : 0.f);
-          float w2 = row_sums_32(lane < NU ? s.J[r + 1][lane] * uc : 0.f);
+          float w1 = row_sums_32(lane < NU ? J[(r) * NU + lane] * uc : 0.f);
+          float w2 = row_sums_32(lane < NU ? J[(r + 1) * NU + lane] * uc : 0.f);
           float o1 = s.lam[r], o2 = s.lam[r + 1];
           float l1 = o1 - w1 / s.Arr[r];
           float l2 = o2 - w2 / s.Arr[r + 1];
@@ -579,7 +589,7 @@ LGX_DEV void substep(Sh& s, const lgx_model* M, const lgx_task_params* Pm, const
             float sc = n > 0.f ? lim / n : 0.f;
             l1 *= sc; l2 *= sc;
           }
-          if (lane < NU) uc += s.MJ[r][lane] * (l1 - o1) + s.MJ[r + 1][lane] * (l2 - o2);
+          if (lane < NU) uc += MJ[(r) * NU + lane] * (l1 - o1) + MJ[(r + 1) * NU + lane] * (l2 - o2);
           if (lane == 0) { s.lam[r] = l1; s.lam[r + 1] = l2; }
           ++r;
         }
