@@ -323,8 +323,9 @@ class PPO:
             surrogate_loss, value_loss, entropy_mean, kl_mean = hip_mlp.ppo_head(
                 mu_b, value_b, ac.std, actions_b, old_logp_b, adv_b, target_values_b, returns_b, old_mu_b, old_sigma_b,
                 self.clip_param, self.use_clipped_value_loss)
-            with torch.no_grad():
-                adapt_latent = ac.adaptation_encoder(obs_b)
+            # sg(z_adapt): the adaptation encoder only trains in DAgger iterations, so over a
+            # PPO update its latents are fixed — computed once per update (_adapt_all)
+            adapt_latent = self._adapt_all[idx]
             regularization_loss = (priv_latent - adapt_latent).norm(p=2, dim=1).mean()
             pred = self.estimator(obs_b)
             estimator_loss = (pred - est_b).norm(p=2, dim=1).pow(2).mean()
@@ -421,7 +422,15 @@ class PPO:
         mb = self._perm.numel() // self.num_mini_batches
         return [self._perm[i * mb:(i + 1) * mb] for i in range(self.num_mini_batches)]
 
+    def _precompute(self):
+        """Per-update constants read by every minibatch: sg(adaptation_encoder(obs)) for all
+        T*N samples (its weights change only in update_dagger)."""
+        if self.on_gpu:
+            with torch.no_grad():
+                self._adapt_all = self.actor_critic.adaptation_encoder(self.storage.observations.flatten(0, 1))
+
     def _update_body_eager(self):
+        self._precompute()
         slices = self._minibatches()
         for _ in range(self.num_learning_epochs):
             for idx in slices:
@@ -438,6 +447,7 @@ class PPO:
         if not phased:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, pool=pool):
+                self._precompute()
                 for _ in range(self.num_learning_epochs):
                     for idx in slices:
                         self._minibatch_grads(idx)
@@ -445,6 +455,9 @@ class PPO:
             self._graphs = {"whole": g}
             self.graph_mode = "whole"
         else:
+            gp = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gp, pool=pool):
+                self._precompute()
             ga = []
             for idx in slices:
                 g = torch.cuda.CUDAGraph()
@@ -454,7 +467,7 @@ class PPO:
             gb = torch.cuda.CUDAGraph()
             with torch.cuda.graph(gb, pool=pool):
                 self._minibatch_step()
-            self._graphs = {"A": ga, "B": gb}
+            self._graphs = {"P": gp, "A": ga, "B": gb}
             self.graph_mode = "phased"
 
     def invalidate_graphs(self):
@@ -485,6 +498,7 @@ class PPO:
         if self.graph_mode == "whole":
             self._graphs["whole"].replay()
         else:
+            self._graphs["P"].replay()
             for _ in range(self.num_learning_epochs):
                 for ga in self._graphs["A"]:
                     ga.replay()
