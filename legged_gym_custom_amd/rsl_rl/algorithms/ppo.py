@@ -305,12 +305,18 @@ class PPO:
     # ------------------------------------------------------------------ one minibatch
     def _minibatch_grads(self, idx):
         """Phase A of one minibatch (ppo.py:186-265 minus the optimizer steps): both
-        backwards into the flat gradient buffer, the local KL into its slot, losses."""
+        backwards into the flat gradient buffer, the local KL into its slot, losses.
+        `idx` is the minibatch's slice of the permutation (GPU: a slice of the storage
+        permuted once per update)."""
         ac = self.actor_critic
         g = self.grads
         s = self.storage
-        (obs_b, priv_b, critic_b, est_b, scan_b, actions_b, target_values_b, adv_b, returns_b, old_logp_b,
-         old_mu_b, old_sigma_b) = s.gather(idx)
+        if self.on_gpu:
+            (obs_b, priv_b, critic_b, est_b, scan_b, actions_b, target_values_b, adv_b, returns_b, old_logp_b,
+             old_mu_b, old_sigma_b) = [t[idx] for t in self._shuf]
+        else:
+            (obs_b, priv_b, critic_b, est_b, scan_b, actions_b, target_values_b, adv_b, returns_b, old_logp_b,
+             old_mu_b, old_sigma_b) = s.gather(idx)
         if self.on_gpu:
             # fused loss head: Normal log-prob/entropy, ratio, clipped surrogate, clipped value
             # loss and KL in one HIP kernel each way (hip_mlp.ppo_head). The privileged latent
@@ -325,7 +331,7 @@ class PPO:
                 self.clip_param, self.use_clipped_value_loss)
             # sg(z_adapt): the adaptation encoder only trains in DAgger iterations, so over a
             # PPO update its latents are fixed — computed once per update (_adapt_all)
-            adapt_latent = self._adapt_all[idx]
+            adapt_latent = self._adapt_all[idx]  # (shuffled order, like the rows)
             regularization_loss = (priv_latent - adapt_latent).norm(p=2, dim=1).mean()
             pred = self.estimator(obs_b)
             estimator_loss = (pred - est_b).norm(p=2, dim=1).pow(2).mean()
@@ -418,16 +424,26 @@ class PPO:
             span.div_(dist.get_world_size())
             # the stale adaptation grads are identical on every rank (averaged at DAgger time)
 
-    def _minibatches(self):
+    def _perm_slices(self):
         mb = self._perm.numel() // self.num_mini_batches
         return [self._perm[i * mb:(i + 1) * mb] for i in range(self.num_mini_batches)]
 
+    def _minibatches(self):
+        mb = self._perm.numel() // self.num_mini_batches
+        if self.on_gpu:  # slices of the once-permuted storage (_precompute)
+            return [slice(i * mb, (i + 1) * mb) for i in range(self.num_mini_batches)]
+        return [self._perm[i * mb:(i + 1) * mb] for i in range(self.num_mini_batches)]
+
     def _precompute(self):
-        """Per-update constants read by every minibatch: sg(adaptation_encoder(obs)) for all
-        T*N samples (its weights change only in update_dagger)."""
+        """Per-update constants read by every minibatch (GPU): the storage rows permuted
+        once (the permutation is shared by all epochs, rollout_storage.py:142, so minibatch
+        i is the same rows every epoch — a contiguous slice here instead of 12 gathers per
+        minibatch), and sg(adaptation_encoder(obs)) for all samples (its weights change only
+        in update_dagger)."""
         if self.on_gpu:
             with torch.no_grad():
-                self._adapt_all = self.actor_critic.adaptation_encoder(self.storage.observations.flatten(0, 1))
+                self._shuf = [t.index_select(0, self._perm) for t in self.storage._flat()]
+                self._adapt_all = self.actor_critic.adaptation_encoder(self._shuf[0])
 
     def _update_body_eager(self):
         self._precompute()
@@ -549,7 +565,7 @@ class PPO:
         ac = self.actor_critic
         adapt = self.grads.segment("adaptation")
         self._perm.copy_(self._next_perm(self._perm.numel()))
-        slices = self._minibatches()
+        slices = self._perm_slices()
         for _ in range(self.num_learning_epochs):
             for idx in slices:
                 obs_b, priv_b = self.storage.gather_fields(idx, ("observations", "privileged_observations"))
