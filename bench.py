@@ -172,7 +172,7 @@ def main():
             "learn_s": round(runner.last_perf.get("learn_time", 0.0), 4),
             "env_kernel": {"avg_us": round(kern_avg_ms * 1e3, 2), "min_us": round(kern_ms[0] * 1e3, 2),
                            "env_steps_per_s": round(env.num_envs / (kern_avg_ms * 1e-3), 1)},
-            "roofline": {"bound": "hbm", "kernel": "lgx::env_step_kernel<true>", "achieved": round(achieved, 1),
+            "roofline": {"bound": "hbm", "kernel": "lgx::env_step_kernel<true, false>", "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "bytes_per_env_step": bpe, "bytes_per_launch": launch_bytes,
                          "traffic": None if traffic is None else round(traffic), "traffic_source": traffic_src},

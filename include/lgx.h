@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define LGX_ABI_VERSION 1
+#define LGX_ABI_VERSION 2
 
 #define LGX_MAX_DOF 12
 #define LGX_MAX_LINKS 16          /* dynamic links: base + 12 leg links (+spare) */
@@ -252,7 +252,11 @@ typedef struct lgx_buffers {
   int64_t* terrain_levels;     /* [N] */
   const int64_t* terrain_types;/* [N] */
   const float* terrain_origins;/* [rows,cols,3] */
-  const int16_t* height_samples; /* [hf_rows, hf_cols] */
+  const int16_t* height_samples; /* [hf_rows, hf_cols] terrain.heightsamples (scan, legged_robot.py:997-1032) */
+  /* [hf_rows, hf_cols] collision mesh, one word per vertex: bits 0-15 int16 height,
+     bits 16-17 dx+1, bits 18-19 dy+1 (slope-threshold wall shift, terrain_utils.py:401-446;
+     zero shifts for mesh_type heightfield). Required unless mesh_type is plane. */
+  const uint32_t* terrain_mesh;
   /* device-side reductions for extras['episode'] (go2.py:246-249): [K+1] sums + count */
   float* episode_stats;
 } lgx_buffers;

@@ -5,7 +5,7 @@ sizeof against the values the native library (and the oracle) report.
 """
 import ctypes as C
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 MAX_DOF = 12
 MAX_LINKS = 16
 MAX_BODIES = 24
@@ -121,7 +121,7 @@ class Buffers(C.Structure):
         "obs", "priv", "critic", "est", "scan", "rew", "reset", "time_out",
         "base_lin_vel", "base_ang_vel", "projected_gravity", "rpy_phase", "measured_heights",
         "friction", "mass_params", "kp_kd", "env_origins", "terrain_levels", "terrain_types",
-        "terrain_origins", "height_samples", "episode_stats",
+        "terrain_origins", "height_samples", "terrain_mesh", "episode_stats",
     ]]
 
 

@@ -2,16 +2,28 @@
 from legged_gym_custom_amd import LEGGED_GYM_ROOT_DIR, LEGGED_GYM_ENVS_DIR  # noqa: F401
 from legged_gym_custom_amd.envs.base.legged_robot import LeggedRobot  # noqa: F401
 from legged_gym_custom_amd.envs.base.legged_robot_config import LeggedRobotCfg, LeggedRobotCfgPPO  # noqa: F401
+from legged_gym_custom_amd.envs.anymal_c.mixed_terrains.anymal_c_rough_config import AnymalCRoughCfg, AnymalCRoughCfgPPO
+from legged_gym_custom_amd.envs.anymal_c.flat.anymal_c_flat_config import AnymalCFlatCfg, AnymalCFlatCfgPPO
 from legged_gym_custom_amd.envs.go2.go2 import Go2Robot
 from legged_gym_custom_amd.envs.go2.go2_config import Go2Cfg, Go2CfgPPO
+from legged_gym_custom_amd.envs.go2.go2_parkour_config import Go2ParkourCfg, Go2ParkourCfgPPO
+from legged_gym_custom_amd.envs.go2.go2_parkour_finetune_config import Go2FinetuneCfg, Go2FinetuneCfgPPO
 from legged_gym_custom_amd.utils.task_registry import task_registry
 
 task_registry.register("go2", Go2Robot, Go2Cfg(), Go2CfgPPO())
+task_registry.register("go2_parkour", Go2Robot, Go2ParkourCfg(), Go2ParkourCfgPPO())
+task_registry.register("go2_parkour_finetune", Go2Robot, Go2FinetuneCfg(), Go2FinetuneCfgPPO())
 
-_CONFIGS = {"go2": (Go2Cfg, Go2CfgPPO)}
+_CONFIGS = {
+    "go2": (Go2Cfg, Go2CfgPPO),
+    "go2_parkour": (Go2ParkourCfg, Go2ParkourCfgPPO),
+    "go2_parkour_finetune": (Go2FinetuneCfg, Go2FinetuneCfgPPO),
+    "anymal_c_rough": (AnymalCRoughCfg, AnymalCRoughCfgPPO),
+    "anymal_c_flat": (AnymalCFlatCfg, AnymalCFlatCfgPPO),
+}
 
 
 def task_registry_configs(name):
-    """Fresh (env_cfg, train_cfg) instances for a registered task name (tests/tools)."""
+    """Fresh (env_cfg, train_cfg) instances for a task name (tests/tools)."""
     e, t = _CONFIGS[name]
     return e(), t()

@@ -16,7 +16,9 @@ from legged_gym_custom_amd import LEGGED_GYM_ROOT_DIR, _abi, _native
 from legged_gym_custom_amd import model as mdl
 from legged_gym_custom_amd import params as prm
 from legged_gym_custom_amd.envs.base.base_task import BaseTask
+from legged_gym_custom_amd.utils import terrain_utils
 from legged_gym_custom_amd.utils.helpers import class_to_dict
+from legged_gym_custom_amd.utils.terrain import Terrain
 
 
 class LeggedRobot(BaseTask):
@@ -77,8 +79,13 @@ class LeggedRobot(BaseTask):
         means = st[:-1] / torch.clamp(cnt, min=1.0) / self.max_episode_length_s
         # in place on static buffers: a captured rollout keeps the stale-value chain
         self._episode_means.copy_(torch.where(cnt > 0, means, self._episode_means))
+        if self.cfg.terrain.curriculum:  # go2.py:252-253 (mean level, refreshed when envs reset)
+            self._terrain_level_mean.copy_(torch.where(cnt > 0, self.terrain_levels.float().mean(),
+                                                       self._terrain_level_mean))
         if "episode" not in self.extras:
             self.extras["episode"] = {"rew_" + k: self._episode_means[i] for i, k in enumerate(self._episode_keys)}
+            if self.cfg.terrain.curriculum:
+                self.extras["episode"]["terrain_level"] = self._terrain_level_mean
         if self.cfg.env.send_timeouts:
             self._extras_time_outs.copy_(torch.where(self.reset_buf.any(), self.time_out_buf, self._extras_time_outs))
             self.extras["time_outs"] = self._extras_time_outs
@@ -99,14 +106,39 @@ class LeggedRobot(BaseTask):
 
     # ------------------------------------------------------------------ setup
     def create_sim(self):
+        """legged_robot.py:278-293: terrain (heightfield / trimesh) or plane, then envs."""
         self.up_axis_idx = 2
         mesh_type = self.cfg.terrain.mesh_type
         if mesh_type in ("heightfield", "trimesh"):
-            raise NotImplementedError(
-                "heightfield/trimesh terrain is the next §8 row (SURVEY.md §8f #1); plane is supported")
-        elif mesh_type not in ("plane", None, "none"):
+            self.terrain = Terrain(self.cfg.terrain, self.num_envs)
+        if mesh_type == "plane":
+            self._create_ground_plane()
+        elif mesh_type == "heightfield":
+            self._create_heightfield()
+        elif mesh_type == "trimesh":
+            self._create_trimesh()
+        elif mesh_type is not None:
             raise ValueError("Terrain mesh type not recognised. Allowed types are [None, plane, heightfield, trimesh]")
         self._create_envs()
+
+    def _create_ground_plane(self):
+        """legged_robot.py:757-765: the kernel's contact against z = 0 (no buffers)."""
+        self._terrain_mesh = None
+
+    def _upload_terrain(self, slope_threshold):
+        t = self.terrain
+        self.height_samples = torch.tensor(t.heightsamples).view(t.tot_rows, t.tot_cols).to(self.device)
+        mesh = terrain_utils.pack_mesh(t.heightsamples, t.cfg.horizontal_scale, t.cfg.vertical_scale, slope_threshold)
+        self._terrain_mesh = torch.from_numpy(mesh.view(np.int32)).to(self.device)
+
+    def _create_heightfield(self):
+        """legged_robot.py:768-786: heightfield collision (no wall correction) + samples."""
+        self._upload_terrain(None)
+
+    def _create_trimesh(self):
+        """legged_robot.py:788-802: the slope-corrected triangle mesh + samples. The kernel
+        collides against it through the packed per-vertex words (no index buffer)."""
+        self._upload_terrain(self.cfg.terrain.slope_treshold)
 
     def _create_envs(self):
         """legged_robot.py:805-894: model, body/dof names, index tables, domain randomisation."""
@@ -154,15 +186,27 @@ class LeggedRobot(BaseTask):
         self.torque_limits = torch.tensor([l["effort"] for l in links], dtype=torch.float, device=self.device)
 
     def _get_env_origins(self):
-        """legged_robot.py:897-930 (plane: a grid with env_spacing)."""
-        self.custom_origins = False
+        """legged_robot.py:897-930. Rough terrain: origins from the terrain tiles
+        (level = random up to max_init_terrain_level, type = global env index / (N / cols));
+        plane: a grid with env_spacing. Both use the GLOBAL env index, and the level draw is
+        made for all envs and sliced, so shards reproduce the single-GPU layout."""
+        total, sl = self.num_envs_total, slice(self.env_id_offset, self.env_id_offset + self.num_envs)
         self.env_origins = torch.zeros(self.num_envs, 3, device=self.device)
-        # the grid is laid out over the GLOBAL env index so shards tile one field
-        total = self.num_envs_total
+        if self.cfg.terrain.mesh_type in ("heightfield", "trimesh"):
+            self.custom_origins = True
+            t = self.cfg.terrain
+            max_init_level = t.max_init_terrain_level if t.curriculum else t.num_rows - 1
+            self.max_terrain_level = t.num_rows
+            self.terrain_levels = torch.randint(0, max_init_level + 1, (total,), device=self.device)[sl].contiguous()
+            self.terrain_types = torch.div(torch.arange(total, device=self.device), (total / t.num_cols),
+                                           rounding_mode="floor").to(torch.long)[sl].contiguous()
+            self.terrain_origins = torch.from_numpy(self.terrain.env_origins).to(self.device).to(torch.float)
+            self.env_origins[:] = self.terrain_origins[self.terrain_levels, self.terrain_types]
+            return
+        self.custom_origins = False
         num_cols = np.floor(np.sqrt(total))
         num_rows = np.ceil(total / num_cols)
         xx, yy = torch.meshgrid(torch.arange(num_rows), torch.arange(num_cols), indexing="ij")
-        sl = slice(self.env_id_offset, self.env_id_offset + self.num_envs)
         spacing = self.cfg.env.env_spacing
         self.env_origins[:, 0] = spacing * xx.flatten()[sl].to(self.device)
         self.env_origins[:, 1] = spacing * yy.flatten()[sl].to(self.device)
@@ -258,8 +302,10 @@ class LeggedRobot(BaseTask):
         self.d_gains = torch.tensor(d_gains, device=dev)
         # ---- native env
         model_struct = mdl.to_struct(self.model_dict)
+        terrain = getattr(self, "terrain", None)
         self.task_params = prm.build_task_params(self.cfg, self.model_dict, n, self.num_envs_total, self.env_id_offset,
-                                                 sim_dt=self.sim_params.dt, go2=self.TASK_KIND == _abi.TASK_GO2)
+                                                 sim_dt=self.sim_params.dt, go2=self.TASK_KIND == _abi.TASK_GO2,
+                                                 terrain_shape=(terrain.tot_rows, terrain.tot_cols) if terrain else None)
         names, _, _, term = prm.reward_terms(self.cfg, self.dt)
         self._episode_keys = names + (["termination"] if term is not None else [])
         ks = len(self._episode_keys)
@@ -267,6 +313,7 @@ class LeggedRobot(BaseTask):
         self.episode_sums = {k: self.episode_sums_buf[:, i] for i, k in enumerate(self._episode_keys)}
         self.episode_stats = z(ks + 1)
         self._episode_means = z(ks)
+        self._terrain_level_mean = z(())
         self._extras_time_outs = z(n, dtype=torch.bool)
         self._native = _native.NativeEnv(model_struct, self.task_params, self.sim_device_id)
         self._bind()
@@ -289,6 +336,9 @@ class LeggedRobot(BaseTask):
             "measured_heights": self.measured_heights, "friction": self._friction,
             "mass_params": self.privileged_mass_params, "kp_kd": self.kp_kd_multipliers,
             "env_origins": self.env_origins, "episode_stats": self.episode_stats,
+            "terrain_levels": getattr(self, "terrain_levels", None), "terrain_types": getattr(self, "terrain_types", None),
+            "terrain_origins": getattr(self, "terrain_origins", None), "height_samples": self.height_samples,
+            "terrain_mesh": self._terrain_mesh,
         })
 
     def _prepare_reward_function(self):

@@ -75,7 +75,8 @@ def soft_dof_limits(lower, upper, soft):
     return np.stack([m - (F32(0.5) * r) * F32(soft), m + (F32(0.5) * r) * F32(soft)], 1).astype(F32)
 
 
-def build_task_params(cfg, model, num_envs, num_envs_total=None, env_id_offset=0, sim_dt=None, go2=True):
+def build_task_params(cfg, model, num_envs, num_envs_total=None, env_id_offset=0, sim_dt=None, go2=True,
+                      terrain_shape=None):
     P = _abi.TaskParams()
     P.abi_version = _abi.ABI_VERSION
     P.task_kind = _abi.TASK_GO2 if go2 else _abi.TASK_LEGGED
@@ -212,6 +213,8 @@ def build_task_params(cfg, model, num_envs, num_envs_total=None, env_id_offset=0
     P.promote_threshold, P.demote_threshold = t.promote_threshold, t.demote_threshold
     P.num_terrain_rows, P.num_terrain_cols = t.num_rows, t.num_cols
     P.max_terrain_level = t.num_rows
+    if terrain_shape is not None:  # Terrain.tot_rows, tot_cols (terrain.py:29-31)
+        P.hf_rows, P.hf_cols = int(terrain_shape[0]), int(terrain_shape[1])
     # physics
     P.gravity[:] = cfg.sim.gravity
     P.ground_friction = t.static_friction

@@ -67,6 +67,7 @@ class OracleEnv:
             "measured_heights": f(N, P.num_height_points),
             "friction": f(N), "mass_params": f(N, 4), "kp_kd": f(2, N, D), "env_origins": f(N, 3),
             "terrain_levels": None, "terrain_types": None, "terrain_origins": None, "height_samples": None,
+            "terrain_mesh": None,
             "episode_stats": f(num_reward_slots + 1),
         }
         self.a["kp_kd"][:] = 1.0
@@ -79,6 +80,17 @@ class OracleEnv:
 
     def post_physics(self, seed, step):
         lib().oracle_post_physics(C.byref(self.P), C.byref(self.B), seed, step)
+
+    def set_terrain(self, height_samples, mesh_words, levels=None, types=None, origins=None):
+        """Bind a terrain: int16 samples + packed uint32 mesh words [rows, cols]; the
+        curriculum tables when given (int64 levels/types [N], float32 origins [R, C, 3])."""
+        self.a["height_samples"] = np.ascontiguousarray(height_samples, dtype=np.int16)
+        self.a["terrain_mesh"] = np.ascontiguousarray(mesh_words, dtype=np.uint32)
+        if levels is not None:
+            self.a["terrain_levels"] = np.ascontiguousarray(levels, dtype=np.int64)
+            self.a["terrain_types"] = np.ascontiguousarray(types, dtype=np.int64)
+            self.a["terrain_origins"] = np.ascontiguousarray(origins, dtype=np.float32)
+        self.rebind()
 
     def reset_envs(self, mask, seed, call, after_init=1):
         m = np.ascontiguousarray(mask.astype(np.uint8))

@@ -218,24 +218,119 @@ static void mass_matrix_and_bias(const kin_t* K, const double* g, double* Mm, do
   }
 }
 
-static double ground_height(const lgx_task_params* P, const lgx_buffers* B, double x, double y) {
-  if (P->mesh_type == LGX_MESH_PLANE || B->height_samples == NULL) return 0.0;
-  /* heightfield: bilinear interpolation of height_samples (DESIGN.md "terrain contact") */
-  double fx = (x + P->border_size) / P->horizontal_scale, fy = (y + P->border_size) / P->horizontal_scale;
-  int ix = (int)floor(fx), iy = (int)floor(fy);
-  if (ix < 0) ix = 0;
-  if (iy < 0) iy = 0;
-  if (ix > P->hf_rows - 2) ix = P->hf_rows - 2;
-  if (iy > P->hf_cols - 2) iy = P->hf_cols - 2;
-  double tx = fx - ix, ty = fy - iy;
-  if (tx < 0) tx = 0;
-  if (tx > 1) tx = 1;
-  if (ty < 0) ty = 0;
-  if (ty > 1) ty = 1;
-  const int16_t* hs = B->height_samples;
-  double h00 = hs[ix * P->hf_cols + iy], h10 = hs[(ix + 1) * P->hf_cols + iy];
-  double h01 = hs[ix * P->hf_cols + iy + 1], h11 = hs[(ix + 1) * P->hf_cols + iy + 1];
-  return P->vertical_scale * ((1 - tx) * (1 - ty) * h00 + tx * (1 - ty) * h10 + (1 - tx) * ty * h01 + tx * ty * h11);
+/* ---- terrain contact, restating legged_gym_custom_amd/csrc/lgx_env.hip terrain_contact
+   in double (same mesh, same cell range, same inside/outside rule). The collision surface
+   is the reference's trimesh (terrain_utils.py:382-465) rebuilt from B->terrain_mesh. */
+static void mesh_vertex(const lgx_task_params* P, const lgx_buffers* B, int i, int j, int ci, int cj, double v[3]) {
+  uint32_t w = B->terrain_mesh[(size_t)i * P->hf_cols + j];
+  double h = (double)(int16_t)(w & 0xffffu);
+  int dx = (int)((w >> 16) & 3u) - 1, dy = (int)((w >> 18) & 3u) - 1;
+  v[0] = (double)(i - ci + dx) * P->horizontal_scale;
+  v[1] = (double)(j - cj + dy) * P->horizontal_scale;
+  v[2] = h * P->vertical_scale;
+}
+
+static void sub3(const double* a, const double* b, double* o) { o[0] = a[0] - b[0]; o[1] = a[1] - b[1]; o[2] = a[2] - b[2]; }
+static void axpy3(const double* a, const double* d, double t, double* o) {
+  o[0] = a[0] + t * d[0]; o[1] = a[1] + t * d[1]; o[2] = a[2] + t * d[2];
+}
+
+static void closest_on_triangle(const double* p, const double* a, const double* b, const double* c, double* q) {
+  double ab[3], ac[3], ap[3], bp[3], cp[3], bc[3];
+  sub3(b, a, ab); sub3(c, a, ac); sub3(p, a, ap);
+  double d1 = dot(ab, ap), d2 = dot(ac, ap);
+  if (d1 <= 0 && d2 <= 0) { memcpy(q, a, 3 * sizeof(double)); return; }
+  sub3(p, b, bp);
+  double d3 = dot(ab, bp), d4 = dot(ac, bp);
+  if (d3 >= 0 && d4 <= d3) { memcpy(q, b, 3 * sizeof(double)); return; }
+  double vc = d1 * d4 - d3 * d2;
+  if (vc <= 0 && d1 >= 0 && d3 <= 0) { axpy3(a, ab, d1 / fmax(d1 - d3, 1e-300), q); return; }
+  sub3(p, c, cp);
+  double d5 = dot(ab, cp), d6 = dot(ac, cp);
+  if (d6 >= 0 && d5 <= d6) { memcpy(q, c, 3 * sizeof(double)); return; }
+  double vb = d5 * d2 - d1 * d6;
+  if (vb <= 0 && d2 >= 0 && d6 <= 0) { axpy3(a, ac, d2 / fmax(d2 - d6, 1e-300), q); return; }
+  double va = d3 * d6 - d5 * d4;
+  if (va <= 0 && d4 - d3 >= 0 && d5 - d6 >= 0) {
+    sub3(c, b, bc);
+    axpy3(b, bc, (d4 - d3) / fmax((d4 - d3) + (d5 - d6), 1e-300), q);
+    return;
+  }
+  double inv = 1.0 / fmax(va + vb + vc, 1e-300);
+  for (int k = 0; k < 3; ++k) q[k] = a[k] + ab[k] * (vb * inv) + ac[k] * (vc * inv);
+}
+
+static int height_in_triangle(const double* p, const double* a, const double* b, const double* c, double* z) {
+  double e1x = b[0] - a[0], e1y = b[1] - a[1], e2x = c[0] - a[0], e2y = c[1] - a[1];
+  double det = e1x * e2y - e1y * e2x;
+  if (fabs(det) < 1e-10) return 0;
+  double px = p[0] - a[0], py = p[1] - a[1];
+  double u = (px * e2y - py * e2x) / det, v = (e1x * py - e1y * px) / det;
+  if (u < -1e-6 || v < -1e-6 || u + v > 1.0 + 1e-6) return 0;
+  *z = a[2] + u * (b[2] - a[2]) + v * (c[2] - a[2]);
+  return 1;
+}
+
+/* depth (> 0 overlapping) and unit normal (terrain -> sphere) of a sphere at x */
+static double terrain_contact(const lgx_task_params* P, const lgx_buffers* B, const double* x, double r, double* n) {
+  double hs = P->horizontal_scale, vs = P->vertical_scale;
+  (void)vs;
+  double gx = x[0] + P->border_size, gy = x[1] + P->border_size;
+  int ci = (int)floor(gx / hs), cj = (int)floor(gy / hs);
+  double p[3] = {gx - ci * hs, gy - cj * hs, x[2]};
+  int i0 = ci + (int)ceil((p[0] - r) / hs) - 2, i1 = ci + (int)floor((p[0] + r) / hs) + 1;
+  int j0 = cj + (int)ceil((p[1] - r) / hs) - 2, j1 = cj + (int)floor((p[1] + r) / hs) + 1;
+  if (i0 < 0) i0 = 0;
+  if (j0 < 0) j0 = 0;
+  if (i1 > P->hf_rows - 2) i1 = P->hf_rows - 2;
+  if (j1 > P->hf_cols - 2) j1 = P->hf_cols - 2;
+  double best = 1e300, zs = -1e300, q[3] = {0, 0, 0}, fn[3] = {0, 0, 1};
+  for (int i = i0; i <= i1; ++i)
+    for (int j = j0; j <= j1; ++j) {
+      double v00[3], v01[3], v10[3], v11[3];
+      mesh_vertex(P, B, i, j, ci, cj, v00);
+      mesh_vertex(P, B, i, j + 1, ci, cj, v01);
+      mesh_vertex(P, B, i + 1, j, ci, cj, v10);
+      mesh_vertex(P, B, i + 1, j + 1, ci, cj, v11);
+      for (int t = 0; t < 2; ++t) {
+        const double* a = v00;
+        const double* b = t == 0 ? v11 : v10;
+        const double* c = t == 0 ? v01 : v11;
+        double cp[3], d[3], z;
+        closest_on_triangle(p, a, b, c, cp);
+        sub3(p, cp, d);
+        double d2 = dot(d, d);
+        if (d2 < best) {
+          double ab[3], ac[3];
+          best = d2;
+          memcpy(q, cp, sizeof(q));
+          sub3(b, a, ab); sub3(c, a, ac);
+          cross(ab, ac, fn);
+        }
+        if (height_in_triangle(p, a, b, c, &z) && z > zs) zs = z;
+      }
+    }
+  if (best >= 1e300) { n[0] = 0; n[1] = 0; n[2] = 1; return -1e300; }
+  double dist = sqrt(best);
+  int below = p[2] < zs;
+  if (dist > 1e-6) {
+    double s = (below ? -1.0 : 1.0) / dist;
+    for (int k = 0; k < 3; ++k) n[k] = (p[k] - q[k]) * s;
+  } else {
+    double l = sqrt(dot(fn, fn));
+    for (int k = 0; k < 3; ++k) n[k] = fn[k] / (l > 0 ? l : 1);
+  }
+  return below ? r + dist : r - dist;
+}
+
+/* tangents of a contact normal; (0,0,1) -> (1,0,0), (0,1,0) (kernel contact_tangents) */
+static void contact_tangents(const double* n, double* t1, double* t2) {
+  double a[3] = {n[2], 0.0, -n[0]};
+  double l2 = a[0] * a[0] + a[2] * a[2];
+  if (l2 < 1e-8) { a[0] = 0; a[1] = n[2]; a[2] = -n[1]; l2 = a[1] * a[1] + a[2] * a[2]; }
+  double l = sqrt(l2);
+  for (int k = 0; k < 3; ++k) t1[k] = a[k] / l;
+  cross(n, t1, t2);
 }
 
 typedef struct {
@@ -328,6 +423,7 @@ void oracle_physics_substep(const lgx_model* M, const lgx_task_params* P, lgx_bu
     }
   }
   int nc = 0, cbody[LGX_MAX_CONTACTS];
+  double cnrm[LGX_MAX_CONTACTS][3];
   double mu_env = B->friction ? B->friction[e] : 1.0;
   double mu = 0.5 * (mu_env + P->ground_friction);
   for (int c = 0; c < M->num_candidates && nc < LGX_MAX_CONTACTS; ++c) {
@@ -336,13 +432,19 @@ void oracle_physics_substep(const lgx_model* M, const lgx_task_params* P, lgx_bu
     matvec(K.R[k], s, xc);
     for (int i = 0; i < 3; ++i) xc[i] += K.p[k][i];
     double r = M->cand_radius[c];
-    double hg = ground_height(P, B, xc[0], xc[1]);
-    double d = r + hg - xc[2];
+    double nrm[3] = {0, 0, 1}, d;
+    int terrain = P->mesh_type != LGX_MESH_PLANE && B->terrain_mesh != NULL;
+    d = terrain ? terrain_contact(P, B, xc, r, nrm) : r - xc[2];
     if (d <= -P->contact_margin) continue;
-    double x[3] = {xc[0], xc[1], xc[2] - r};
+    double x[3] = {xc[0] - r * nrm[0], xc[1] - r * nrm[1], xc[2] - r * nrm[2]};
     double Jv[3][NU], Jw[3][NU];
     point_jac(&K, k, x, Jv, Jw);
-    const double dirs[3][3] = {{0, 0, 1}, {1, 0, 0}, {0, 1, 0}};
+    double dirs[3][3] = {{0, 0, 1}, {1, 0, 0}, {0, 1, 0}};
+    if (terrain) {
+      memcpy(dirs[0], nrm, sizeof(nrm));
+      contact_tangents(nrm, dirs[1], dirs[2]);
+    }
+    memcpy(cnrm[nc], dirs[0], sizeof(nrm));
     for (int t = 0; t < 3; ++t) {
       for (int j = 0; j < NU; ++j) rows[nr].J[j] = dirs[t][0] * Jv[0][j] + dirs[t][1] * Jv[1][j] + dirs[t][2] * Jv[2][j];
       rows[nr].target = t == 0 ? d : 0.0;
@@ -421,8 +523,11 @@ void oracle_physics_substep(const lgx_model* M, const lgx_task_params* P, lgx_bu
   for (int r = 0; r < nr; ++r) {
     if (rows[r].contact < 0) continue;
     int bidx = cbody[rows[r].contact];
-    int axis = rows[r].kind == 0 ? 2 : (rows[r].kind == 1 ? 0 : 1);
-    cf[bidx * 3 + axis] += (float)(lam[r] / dt);
+    double fr[3], t1[3], t2[3];
+    contact_tangents(cnrm[rows[r].contact], t1, t2);
+    const double* dir = rows[r].kind == 0 ? cnrm[rows[r].contact] : (rows[r].kind == 1 ? t1 : t2);
+    for (int k = 0; k < 3; ++k) fr[k] = dir[k];
+    for (int k = 0; k < 3; ++k) cf[bidx * 3 + k] += (float)(fr[k] * lam[r] / dt);
   }
   /* integrate */
   double vn[3] = {up[0], up[1], up[2]}, wn[3] = {up[3], up[4], up[5]};

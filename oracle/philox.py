@@ -24,6 +24,7 @@ MASK32 = np.uint64(0xFFFFFFFF)
 # ---- slot layout: must match lgx_rng.h / lgx_oracle.c --------------------------
 SLOT_CMD = 0          # block 0: cmd x, cmd y, cmd yaw/heading, zero-mask   (step callback)
 SLOT_PUSH = 4         # block 1: push vx, push vy, terrain level, (unused)
+SLOT_TERR = 6         # block 1, 3rd: solved-terrain random level (legged_robot.py:571-573)
 SLOT_DOF = 8          # blocks 2-4: 12 dof reset draws
 SLOT_ROOT_XY = 20     # block 5: root x, root y
 SLOT_ROOT_VEL = 24    # blocks 6-7: 6 root velocity draws

@@ -22,10 +22,28 @@ def step(d, t, key):
     return d[f"steps.{t}.{key}"]
 
 
-def go2_setup(num_envs, task="go2"):
+def terrain_for(env_cfg, np_seed=1):
+    """The task's Terrain (legged_gym_custom_amd.utils.terrain, pinned bit-exact to the
+    reference in test_terrain.py) and its packed collision mesh, or (None, None)."""
+    t = env_cfg.terrain
+    if t.mesh_type not in ("heightfield", "trimesh"):
+        return None, None
+    from legged_gym_custom_amd.utils.terrain import Terrain
+    from legged_gym_custom_amd.utils import terrain_utils
+    np.random.seed(np_seed)
+    ter = Terrain(t, env_cfg.env.num_envs)
+    mesh = terrain_utils.pack_mesh(ter.heightsamples, t.horizontal_scale, t.vertical_scale,
+                                   t.slope_treshold if t.mesh_type == "trimesh" else None)
+    return ter, mesh
+
+
+def go2_setup(num_envs, task="go2", terrain=None):
     from legged_gym_custom_amd.envs import task_registry_configs
     from legged_gym_custom_amd import model as mdl, params as prm
     env_cfg, _ = task_registry_configs(task)
     m = mdl.load_model(env_cfg.asset.file, env_cfg.asset.foot_name)
-    P = prm.build_task_params(env_cfg, m, num_envs, go2=True)
+    shape = (terrain.tot_rows, terrain.tot_cols) if terrain is not None else None
+    if env_cfg.terrain.mesh_type not in ("heightfield", "trimesh"):
+        env_cfg.terrain.curriculum = False  # LeggedRobot._parse_cfg (legged_robot.py:950-951)
+    P = prm.build_task_params(env_cfg, m, num_envs, go2=True, terrain_shape=shape)
     return env_cfg, m, P

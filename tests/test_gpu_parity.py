@@ -14,11 +14,11 @@ import golden_util as G
 pytestmark = pytest.mark.gpu
 
 
-def _twin(n, task="go2"):
+def _twin(n, task="go2", terrain=None, ter=None):
     from native_util import Twin
     from legged_gym_custom_amd import model as mdl
-    cfg, m, P = G.go2_setup(n, task)
-    return cfg, m, P, Twin(P, mdl.to_struct(m), P.num_reward_terms + P.has_termination_reward)
+    cfg, m, P = G.go2_setup(n, task, terrain=ter)
+    return cfg, m, P, Twin(P, mdl.to_struct(m), P.num_reward_terms + P.has_termination_reward, terrain=terrain)
 
 
 def _close(got, want, atol=1e-5, rtol=1e-5):
@@ -28,10 +28,19 @@ def _close(got, want, atol=1e-5, rtol=1e-5):
     return np.allclose(got, want, atol=atol, rtol=rtol)
 
 
-def test_post_physics_matches_reference_golden():
-    d = G.load("go2_flat_n64.npz")
+@pytest.mark.parametrize("name,task", [("go2_flat_n64.npz", "go2"), ("go2_parkour_n64.npz", "go2_parkour")])
+def test_post_physics_matches_reference_golden(name, task):
+    d = G.load(name)
     N = int(d["num_envs"])
-    cfg, m, P, tw = _twin(N)
+    terrain = "terrain_levels" in d
+    ter = tw_terrain = None
+    if terrain:
+        from legged_gym_custom_amd.envs import task_registry_configs
+        env_cfg = task_registry_configs(task)[0]
+        env_cfg.env.num_envs = N
+        ter, mesh = G.terrain_for(env_cfg, int(d["np_seed"]))
+        tw_terrain = (ter.heightsamples, mesh, d["terrain_levels"], d["terrain_types"], d["terrain_origins"])
+    cfg, m, P, tw = _twin(N, task, tw_terrain, ter)
     a, t = tw.a, tw.t
     a["friction"][:] = d["friction"]
     a["mass_params"][:] = d["mass_params"]
@@ -44,6 +53,9 @@ def test_post_physics_matches_reference_golden():
     assert _close(tw.gpu("root_states"), d["reset0_state.root_states"])
     assert _close(tw.gpu("dof_state").reshape(-1, 2), d["reset0_state.dof_state"])
     assert _close(tw.gpu("commands"), d["reset0_state.commands"])
+    if terrain:
+        assert np.array_equal(tw.gpu("terrain_levels"), d["reset0_state.terrain_levels"])
+        assert _close(tw.gpu("env_origins"), d["reset0_state.env_origins"])
     K = P.num_reward_terms
     for step in range(G.num_steps(d)):
         S = lambda k: G.step(d, step, k)  # noqa: E731
@@ -60,6 +72,11 @@ def test_post_physics_matches_reference_golden():
         t["torques"].copy_(tw.torch.from_numpy(S("out.torques")))
         tw.native.post_physics(int(d["seed"]), int(S("csc_in")) + 1, tw.stream())
         tw.sync()
+        if terrain:
+            assert _close(tw.gpu("measured_heights"), S("out.measured_heights")), f"step {step}: heights"
+            assert _close(tw.gpu("rpy_phase")[:, 7:8], S("out.jump_flags")), f"step {step}: jump flags"
+            assert np.array_equal(tw.gpu("terrain_levels"), S("out.state_out.terrain_levels")), f"step {step}: levels"
+            assert _close(tw.gpu("env_origins"), S("out.state_out.env_origins")), f"step {step}: origins"
         checks = [("rew", "rew", "out.rew_buf"), ("reset", "reset", "out.reset_buf"),
                   ("time_out", "time_out", "out.time_out_buf"), ("priv", "priv", "out.privileged_obs_buf"),
                   ("est", "est", "out.estimated_obs_buf"), ("scan", "scan", "out.scan_obs_buf"),

@@ -8,6 +8,12 @@ all 15 Go2 reward terms + only_positive clip, reset_idx with its RNG draws, obse
 noise, history refill (ep <= 1) and shift, priv/est/scan/critic, last_* copies,
 extras['episode'] means. Tolerance: atol=rtol=1e-5 (fp32; transcendental libm and
 reduction-order differences vs torch CPU are ~1 ulp).
+
+go2_parkour_n64.npz adds the C4 terrain path on the full 12 x 20
+gap-course field: the height scan (_get_heights legged_robot.py:997-1032, truncating
+index math, min of 3 samples), scan obs, jump flags (go2.py:487-494), the fell-into-
+hole termination (go2.py:202-204), custom-origin resets (xy jitter) and the terrain
+curriculum with its random level for solved courses (legged_robot.py:543-574).
 """
 import numpy as np
 import pytest
@@ -45,12 +51,24 @@ def test_params_match_reference(fixture):
     assert np.allclose([P.reward_scales[i] for i in range(P.num_reward_terms)], d["reward_scales"], rtol=1e-7)
 
 
-def test_oracle_replays_reference_steps(fixture):
+def replay(name, task):
+    """Replay a golden fixture through the C oracle: setup-time inputs injected, then per
+    step the reference's post-simulate state in, every output compared."""
     import driver
     from legged_gym_custom_amd import model as mdl
-    d = fixture
+    d = G.load(name)
     N = int(d["num_envs"])
-    cfg, m, P = G.go2_setup(N)
+    terrain = "terrain_levels" in d
+    env_cfg = None
+    ter = mesh = None
+    if terrain:
+        from legged_gym_custom_amd.envs import task_registry_configs
+        env_cfg = task_registry_configs(task)[0]
+        env_cfg.env.num_envs = N
+        ter, mesh = G.terrain_for(env_cfg, int(d["np_seed"]))
+        import hashlib
+        assert hashlib.sha1(ter.heightsamples.tobytes()).hexdigest() == str(d["height_samples_sha1"])
+    cfg, m, P = G.go2_setup(N, task, terrain=ter)
     K = P.num_reward_terms
     o = driver.OracleEnv(P, mdl.to_struct(m), K + P.has_termination_reward)
     a = o.a
@@ -58,11 +76,16 @@ def test_oracle_replays_reference_steps(fixture):
     a["mass_params"][:] = d["mass_params"]
     a["kp_kd"][:] = d["kp_kd_multipliers"]
     a["env_origins"][:] = d["env_origins"]
-    # BaseTask.reset(): reset_idx(all) outside a step (RNG stream 1, call 0)
-    o.reset_envs(np.ones(N, bool), seed=int(d["seed"]), call=0, after_init=0)
+    if terrain:
+        o.set_terrain(ter.heightsamples, mesh, d["terrain_levels"], d["terrain_types"], d["terrain_origins"])
+    # BaseTask.reset(): reset_idx(all) outside a step (RNG stream 1, call 0), after init
+    o.reset_envs(np.ones(N, bool), seed=int(d["seed"]), call=0, after_init=1)
     assert _close(a["root_states"], d["reset0_state.root_states"])
     assert _close(a["dof_state"].reshape(-1, 2), d["reset0_state.dof_state"])
     assert _close(a["commands"], d["reset0_state.commands"])
+    if terrain:
+        assert np.array_equal(a["terrain_levels"], d["reset0_state.terrain_levels"])
+        assert _close(a["env_origins"], d["reset0_state.env_origins"])
     worst = {}
     for t in range(G.num_steps(d)):
         S = lambda k: G.step(d, t, k)  # noqa: E731
@@ -101,14 +124,24 @@ def test_oracle_replays_reference_steps(fixture):
         for k in ["last_actions", "last_dof_vel", "last_root_vel", "last_base_lin_vel", "last_torques",
                   "last_contact_heights"]:
             checks.append((k, a[k], S("out.state_out." + k)))
+        if terrain:
+            checks += [("measured_heights", a["measured_heights"], S("out.measured_heights")),
+                       ("jump_flags", a["rpy_phase"][:, 7:8], S("out.jump_flags")),
+                       ("env_origins", a["env_origins"], S("out.state_out.env_origins"))]
+            assert np.array_equal(a["terrain_levels"], S("out.state_out.terrain_levels")), f"step {t}: terrain_levels"
         if f"steps.{t}.out.obs_buf" in d:
             checks += [("obs", a["obs"], S("out.obs_buf")), ("critic", a["critic"], S("out.critic_obs_buf"))]
-        for name, got, want in checks:
-            assert _close(got, want), f"step {t}: {name} max err {np.abs(np.asarray(got, float) - np.asarray(want, float)).max()}"
+        for nm, got, want in checks:
+            assert _close(got, want), f"step {t}: {nm} max err {np.abs(np.asarray(got, float) - np.asarray(want, float)).max()}"
             if got.dtype == np.float32:
-                worst[name] = max(worst.get(name, 0.0), float(np.abs(got.astype(np.float64) - want).max()))
+                worst[nm] = max(worst.get(nm, 0.0), float(np.abs(got.astype(np.float64) - want).max()))
         cnt = a["episode_stats"][-1]
         if cnt > 0 and f"steps.{t}.out.extras_episode" in d:
             assert np.allclose(a["episode_stats"][:K] / cnt / 20.0, S("out.extras_episode"), atol=1e-6, rtol=1e-4)
     assert _close(a["obs_history"], d["final_obs_history"])
     print("worst abs errors:", {k: f"{v:.2e}" for k, v in worst.items()})
+
+
+@pytest.mark.parametrize("name,task", [("go2_flat_n64.npz", "go2"), ("go2_parkour_n64.npz", "go2_parkour")])
+def test_oracle_replays_reference_steps(name, task):
+    replay(name, task)

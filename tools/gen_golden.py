@@ -123,7 +123,7 @@ class RNGRouter:
 
     def take(self, n_rows, n_cols):
         name, env_ids, cur = self.ctx
-        base = {"cmd": philox.SLOT_CMD, "rcmd": philox.SLOT_RCMD, "push": philox.SLOT_PUSH,
+        base = {"cmd": philox.SLOT_CMD, "rcmd": philox.SLOT_RCMD, "push": philox.SLOT_PUSH, "terr": philox.SLOT_TERR,
                 "dof": philox.SLOT_DOF, "root_xy": philox.SLOT_ROOT_XY, "root_vel": philox.SLOT_ROOT_VEL,
                 "noise": philox.SLOT_NOISE}[name]
         idx = env_ids if env_ids is not None else torch.arange(self.env.num_envs)
@@ -158,8 +158,20 @@ def install_rng(router):
             return real_rand_like(t, **kw)
         return router.take(t.shape[0], t.shape[1])
 
+    real_randint_like = torch.randint_like
+
+    def randint_like(t, *args, **kw):
+        # torch.randint_like(t, high) in _update_terrain_curriculum (legged_robot.py:572):
+        # floor(u * high) of the Philox uniform, as the kernel draws it
+        if router.ctx is None:
+            return real_randint_like(t, *args, **kw)
+        high = args[-1]
+        u = router.take(t.shape[0], 1)[:, 0]
+        return (u * float(high)).to(torch.long)
+
     torch.rand = rand
     torch.rand_like = rand_like
+    torch.randint_like = randint_like
 
 
 def make_harness_class():
@@ -233,6 +245,11 @@ def make_harness_class():
                 r.ctx = ("root_vel", env_ids, 0)
                 super()._reset_root_states(env_ids)
             r.ctx = None
+
+        def _update_terrain_curriculum(self, env_ids):
+            self._router.ctx = ("terr", env_ids, 0)
+            super()._update_terrain_curriculum(env_ids)
+            self._router.ctx = None
 
         def _push_robots(self):
             self._router.ctx = ("push", None, 0)
@@ -310,6 +327,24 @@ def scripted_physics(env, rng, t):
     rb[:, env.feet_indices, 2] = torch.from_numpy(rng.uniform(-0.01, 0.12, (n, 4))).float()
 
 
+def scripted_physics_course(env, rng, t):
+    """Like scripted_physics, but robots spread along their terrain tile (parkour: x from
+    the tile start), z set above the local ground, and a few fallen into gaps (z < -1)."""
+    scripted_physics(env, rng, t)
+    n = env.num_envs
+    root = env.root_states
+    tl = env.cfg.terrain
+    root[:, 0] = env.env_origins[:, 0] + torch.from_numpy(rng.uniform(0.5, tl.terrain_length - 0.5, n)).float()
+    root[:, 1] = env.env_origins[:, 1] + torch.from_numpy(rng.uniform(-0.45, 0.45, n) * tl.terrain_width).float()
+    hs = env.height_samples
+    ix = ((root[:, 0] + tl.border_size) / tl.horizontal_scale).long().clamp(0, hs.shape[0] - 1)
+    iy = ((root[:, 1] + tl.border_size) / tl.horizontal_scale).long().clamp(0, hs.shape[1] - 1)
+    ground = hs[ix, iy].float() * tl.vertical_scale
+    root[:, 2] = ground + torch.from_numpy(rng.uniform(0.2, 0.45, n)).float()
+    fell = torch.from_numpy(rng.uniform(size=n) < 0.06)
+    root[fell, 2] = torch.from_numpy(rng.uniform(-1.8, -1.05, int(fell.sum()))).float()
+
+
 STATE_KEYS = ["root_states", "dof_state", "contact_forces", "commands", "last_actions", "last_dof_vel",
               "last_root_vel", "last_base_lin_vel", "last_torques", "obs_history_buf", "episode_length_buf",
               "last_contacts", "last_contact_heights", "feet_air_time"]
@@ -326,8 +361,10 @@ def snapshot(env, keys):
     return out
 
 
-def run_fixture(task, n, steps, seed, path, ep_init=None, csc0=0, overrides=None):
+def run_fixture(task, n, steps, seed, path, ep_init=None, csc0=0, overrides=None, physics=None, terrain=False):
     env, cfg = build_env(task, n, seed, overrides)
+    physics = physics or scripted_physics
+    state_keys = STATE_KEYS + (["terrain_levels", "env_origins"] if terrain else [])
     rng = np.random.default_rng(seed + 100)
     rec = {"num_envs": n, "seed": seed, "task": task, "torch_version": torch.__version__}
     # static per-env setup-time params (inputs to the oracle/kernel)
@@ -343,14 +380,21 @@ def run_fixture(task, n, steps, seed, path, ep_init=None, csc0=0, overrides=None
     rec["noise_scale_vec"] = env.noise_scale_vec.numpy().astype(np.float32)
     rec["reward_names"] = np.array(list(env.reward_scales.keys()))
     rec["reward_scales"] = np.array([env.reward_scales[k] for k in env.reward_scales], dtype=np.float64)
+    if terrain:
+        import hashlib
+        rec["terrain_levels"] = env.terrain_levels.numpy().copy()
+        rec["terrain_types"] = env.terrain_types.numpy().copy()
+        rec["terrain_origins"] = env.terrain_origins.numpy().astype(np.float32)
+        rec["height_samples_sha1"] = np.array(hashlib.sha1(env.height_samples.numpy().tobytes()).hexdigest())
+        rec["np_seed"] = np.array(seed)
 
     # ---- BaseTask.reset(): external reset_idx(all) then step(zeros) ------------
     env.external_reset(torch.arange(n))
-    rec["reset0_state"] = {k: getattr(env, k).detach().clone().numpy() for k in STATE_KEYS}
+    rec["reset0_state"] = {k: getattr(env, k).detach().clone().numpy() for k in state_keys}
 
     def one_step(actions):
         env.actions = torch.clip(actions, -cfg.normalization.clip_actions, cfg.normalization.clip_actions)
-        scripted_physics(env, rng, None)
+        physics(env, rng, None)
         pre = {k: getattr(env, k).detach().clone().numpy() for k in ["root_states", "dof_state", "contact_forces", "rigid_body_states"]}
         env.torques = env._compute_torques(env.actions).view(env.torques.shape)
         env.post_physics_step()
@@ -383,7 +427,10 @@ def run_fixture(task, n, steps, seed, path, ep_init=None, csc0=0, overrides=None
         if t < 3:
             o["obs_buf"] = env.obs_buf.numpy().copy()
             o["critic_obs_buf"] = env.critic_obs_buf.numpy().copy()
-        o["state_out"] = {k: getattr(env, k).detach().clone().numpy() for k in STATE_KEYS if k != "obs_history_buf"}
+        o["state_out"] = {k: getattr(env, k).detach().clone().numpy() for k in state_keys if k != "obs_history_buf"}
+        if terrain:
+            o["measured_heights"] = env.measured_heights.numpy().copy()
+            o["jump_flags"] = env.jump_flags.numpy().copy()
         o["episode_sums"] = np.stack([env.episode_sums[k].numpy() for k in env.reward_scales]).astype(np.float32)
         o["extras_time_outs"] = env.extras["time_outs"].numpy().copy() if "time_outs" in env.extras else None
         if "episode" in env.extras:
@@ -419,4 +466,11 @@ def flatten(d, prefix=""):
 
 if __name__ == "__main__":
     os.makedirs(os.path.join(REPO, "tests", "golden"), exist_ok=True)
-    run_fixture("go2", 64, 30, 1, os.path.join(REPO, "tests", "golden", "go2_flat_n64.npz"), csc0=390)
+    which = sys.argv[1:] or ["go2", "go2_parkour"]
+    if "go2" in which:
+        run_fixture("go2", 64, 30, 1, os.path.join(REPO, "tests", "golden", "go2_flat_n64.npz"), csc0=390)
+    if "go2_parkour" in which:
+        # C4 task on its full terrain (12 x 20 gap courses); robots spread along the
+        # courses so the scan, jump flags, hole termination and curriculum all fire
+        run_fixture("go2_parkour", 64, 24, 1, os.path.join(REPO, "tests", "golden", "go2_parkour_n64.npz"),
+                    csc0=390, physics=scripted_physics_course, terrain=True)

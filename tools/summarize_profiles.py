@@ -26,7 +26,7 @@ def pmc(name):
     return vals
 
 
-res = {"kernel": "lgx::env_step_kernel<true>", "workload": "go2 flat, 4096 envs, actions N(0,1) clipped"}
+res = {"kernel": "lgx::env_step_kernel<true, false>", "workload": "go2 flat, 4096 envs, actions N(0,1) clipped"}
 fetch = pmc("fetch").get("FETCH_SIZE", [])
 write = pmc("write").get("WRITE_SIZE", [])
 if fetch and write:
