@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define LGX_ABI_VERSION 2
+#define LGX_ABI_VERSION 3
 
 #define LGX_MAX_DOF 12
 #define LGX_MAX_LINKS 16          /* dynamic links: base + 12 leg links (+spare) */
@@ -204,6 +204,15 @@ typedef struct lgx_task_params {
   float ground_friction;                  /* terrain static/dynamic friction (plane 1.0) */
   int32_t solver_iterations;              /* projected Gauss-Seidel sweeps per substep */
   float baumgarte, slop, max_depenetration_vel, contact_margin, limit_margin;
+  /* ANYmal series-elastic actuator network (anymal.py:56-81, replaces _compute_torques):
+     per joint and substep a 2-layer LSTM(2 -> 8 -> 8), gates i f g o, then Linear(8 -> 1);
+     input (a*action_scale + q0 - q, qd) * in_scale, torque = out_scale * linear. Weights
+     row-major as in the archive (legged_gym_custom_amd/actuator.py). 0 = PD control. */
+  int32_t actuator_net;
+  float sea_in_scale[2], sea_out_scale, sea_lin_b;
+  float sea_w_ih0[32 * 2], sea_w_hh0[32 * 8], sea_b_ih0[32], sea_b_hh0[32];
+  float sea_w_ih1[32 * 8], sea_w_hh1[32 * 8], sea_b_ih1[32], sea_b_hh1[32];
+  float sea_lin_w[8];
 } lgx_task_params;
 
 /* Every per-env buffer the step reads/writes. NULL = not present. */
@@ -257,6 +266,9 @@ typedef struct lgx_buffers {
      bits 16-17 dx+1, bits 18-19 dy+1 (slope-threshold wall shift, terrain_utils.py:401-446;
      zero shifts for mesh_type heightfield). Required unless mesh_type is plane. */
   const uint32_t* terrain_mesh;
+  /* actuator network state (anymal.py:62-69): [2 layers, N*D, 8], zeroed on reset */
+  float* sea_hidden;
+  float* sea_cell;
   /* device-side reductions for extras['episode'] (go2.py:246-249): [K+1] sums + count */
   float* episode_stats;
 } lgx_buffers;

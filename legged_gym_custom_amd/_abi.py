@@ -5,7 +5,7 @@ sizeof against the values the native library (and the oracle) report.
 """
 import ctypes as C
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 MAX_DOF = 12
 MAX_LINKS = 16
 MAX_BODIES = 24
@@ -105,6 +105,10 @@ class TaskParams(C.Structure):
         ("gravity", f32 * 3), ("ground_friction", f32), ("solver_iterations", i32),
         ("baumgarte", f32), ("slop", f32), ("max_depenetration_vel", f32), ("contact_margin", f32),
         ("limit_margin", f32),
+        ("actuator_net", i32), ("sea_in_scale", f32 * 2), ("sea_out_scale", f32), ("sea_lin_b", f32),
+        ("sea_w_ih0", f32 * 64), ("sea_w_hh0", f32 * 256), ("sea_b_ih0", f32 * 32), ("sea_b_hh0", f32 * 32),
+        ("sea_w_ih1", f32 * 256), ("sea_w_hh1", f32 * 256), ("sea_b_ih1", f32 * 32), ("sea_b_hh1", f32 * 32),
+        ("sea_lin_w", f32 * 8),
     ]
 
 
@@ -121,7 +125,7 @@ class Buffers(C.Structure):
         "obs", "priv", "critic", "est", "scan", "rew", "reset", "time_out",
         "base_lin_vel", "base_ang_vel", "projected_gravity", "rpy_phase", "measured_heights",
         "friction", "mass_params", "kp_kd", "env_origins", "terrain_levels", "terrain_types",
-        "terrain_origins", "height_samples", "terrain_mesh", "episode_stats",
+        "terrain_origins", "height_samples", "terrain_mesh", "sea_hidden", "sea_cell", "episode_stats",
     ]]
 
 

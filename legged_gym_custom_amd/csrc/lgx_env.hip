@@ -29,8 +29,12 @@ constexpr int NJ = 12;
 constexpr int NU = 18;
 constexpr int MAXC = LGX_MAX_CONTACTS;
 constexpr int MAXR = NJ + 3 * MAXC;
-constexpr int NBLK = 22;  // Philox blocks per env per step (oracle/philox.py NUM_BLOCKS)
-constexpr int NSLOT = NBLK * 4;
+// Philox blocks per env per step: 9 fixed blocks (commands, push/terrain, dof, root, reset
+// commands) + one per 4 observation-noise draws (oracle/philox.py num_blocks): Go2 22,
+// ANYmal (235 proprio) 68
+constexpr int NBLK_MAX = 9 + (LGX_MAX_PROPRIO + 3) / 4;
+constexpr int NSLOT = NBLK_MAX * 4;
+LGX_DEV int rng_blocks(const lgx_task_params* Pm) { return 9 + (Pm->num_proprio + 3) / 4; }
 constexpr int MAXHIST = 1216;
 
 enum Slot { S_CMD = 0, S_PUSH = 4, S_TERR = 6, S_DOF = 8, S_ROOT_XY = 20, S_ROOT_VEL = 24, S_RCMD = 32, S_NOISE = 36 };
@@ -48,6 +52,8 @@ struct Scratch {  // per-env post-physics scalars (go2.py:357-367, 279-328)
 // staging): J [n][NU], M⁻¹Jᵀ [n][NU] and, for n <= AMAX rows, A = J M⁻¹ Jᵀ [n][n]
 constexpr int ARENA = 2200;
 constexpr int AMAX = 32;
+static_assert(NSLOT + LGX_MAX_PROPRIO + MAXHIST + LGX_MAX_HEIGHT_POINTS <= ARENA,
+              "post-physics staging must fit the arena");
 static_assert(2 * MAXR * NU <= ARENA, "arena must hold J and M^-1 J^T at MAXR rows");
 static_assert(2 * AMAX * NU + AMAX * AMAX <= ARENA, "arena must hold J, M^-1 J^T and A at AMAX rows");
 
@@ -467,15 +473,78 @@ LGX_DEV void contact_tangents(f3 n, f3& t1, f3& t2) {
   t2 = cross(n, t1);
 }
 
+// ---- ANYmal series-elastic actuator net (anymal.py:71-81)
+// One joint per lane: 2-layer LSTM(2 -> 8 -> 8) step + Linear(8 -> 1), torch.nn.LSTM gate
+// order i f g o, state [2, N*D, 8] in HBM (read and written once per substep). The
+// weights are wave-uniform (task params), so they stream through scalar loads; one
+// hidden unit's four gates are formed at a time to keep the live set small.
+LGX_DEV float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+template <int NIN>
+LGX_DEV void sea_lstm_layer(const float* __restrict__ w_ih, const float* __restrict__ w_hh,
+                            const float* __restrict__ b_ih, const float* __restrict__ b_hh, const float* x, float* h,
+                            float* c) {
+  float hn[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    float g4[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int g = q * 8 + u;
+      float a = 0.0f, b = 0.0f;
+#pragma unroll
+      for (int k = 0; k < NIN; ++k) a += w_ih[g * NIN + k] * x[k];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) b += w_hh[g * 8 + k] * h[k];
+      g4[q] = (a + b_ih[g]) + (b + b_hh[g]);
+    }
+    const float ig = sigmoidf_(g4[0]), fg = sigmoidf_(g4[1]), gg = tanhf(g4[2]), og = sigmoidf_(g4[3]);
+    c[u] = fg * c[u] + ig * gg;
+    hn[u] = og * tanhf(c[u]);
+  }
+#pragma unroll
+  for (int u = 0; u < 8; ++u) h[u] = hn[u];
+}
+
+LGX_DEV float sea_torque(const lgx_task_params* Pm, const lgx_buffers& B, int e, int j, float in0, float in1) {
+  const size_t NT = (size_t)Pm->num_envs * Pm->num_dof, r = (size_t)e * Pm->num_dof + j;
+  float4* hp0 = reinterpret_cast<float4*>(B.sea_hidden + r * 8);
+  float4* cp0 = reinterpret_cast<float4*>(B.sea_cell + r * 8);
+  float4* hp1 = reinterpret_cast<float4*>(B.sea_hidden + (NT + r) * 8);
+  float4* cp1 = reinterpret_cast<float4*>(B.sea_cell + (NT + r) * 8);
+  float h0[8], c0[8], h1[8], c1[8];
+  auto ld8 = [](const float4* p, float* v) {
+    const float4 a = p[0], b = p[1];
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  };
+  auto st8 = [](float4* p, const float* v) {
+    p[0] = make_float4(v[0], v[1], v[2], v[3]);
+    p[1] = make_float4(v[4], v[5], v[6], v[7]);
+  };
+  ld8(hp0, h0); ld8(cp0, c0); ld8(hp1, h1); ld8(cp1, c1);
+  const float x[2] = {in0 * Pm->sea_in_scale[0], in1 * Pm->sea_in_scale[1]};
+  sea_lstm_layer<2>(Pm->sea_w_ih0, Pm->sea_w_hh0, Pm->sea_b_ih0, Pm->sea_b_hh0, x, h0, c0);
+  sea_lstm_layer<8>(Pm->sea_w_ih1, Pm->sea_w_hh1, Pm->sea_b_ih1, Pm->sea_b_hh1, h0, h1, c1);
+  st8(hp0, h0); st8(cp0, c0); st8(hp1, h1); st8(cp1, c1);
+  float y = 0.0f;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) y += Pm->sea_lin_w[k] * h1[k];
+  return Pm->sea_out_scale * (y + Pm->sea_lin_b);
+}
+
 // one physics substep (legged_robot.py:80-85 loop body)
-template <bool TERRAIN>
+template <bool TERRAIN, bool ACTNET>
 LGX_DEV void substep(Sh& s, const lgx_model* M, const lgx_task_params* Pm, const lgx_buffers& B, int lane,
                      bool last) {
   const float dt = Pm->sim_dt;
   // ---- PD torques: LeggedRobot._compute_torques legged_robot.py:440-478
   {
 #pragma clang fp contract(off)
-    if (lane < NJ) {
+    if (ACTNET && lane < NJ) {
+      const int j = lane;
+      s.tau[j] = sea_torque(Pm, B, blockIdx.x, j, (s.act[j] * Pm->action_scale + Pm->default_dof_pos[j]) - s.th[j],
+                            s.thd[j]);
+    } else if (lane < NJ) {
       const int j = lane;
       float as = s.act[j] * Pm->action_scale;
       float t;
@@ -896,6 +965,13 @@ LGX_DEV void reset_env(const lgx_task_params* Pm, const lgx_buffers& B, Sh& s, i
     if (lane < 3) B.last_base_lin_vel[e * 3 + lane] = 0.f;
     for (int i = lane; i < H; i += 64) B.obs_history[(size_t)e * H + i] = 0.f;
   }
+  if (Pm->actuator_net && lane < 2 * D) {  // Anymal.reset_idx anymal.py:56-60: zero h, c
+    const size_t NT = (size_t)Pm->num_envs * D;
+    const int l = lane / D, j = lane % D;
+    float4* hp = reinterpret_cast<float4*>(B.sea_hidden + (l * NT + (size_t)e * D + j) * 8);
+    float4* cp = reinterpret_cast<float4*>(B.sea_cell + (l * NT + (size_t)e * D + j) * 8);
+    hp[0] = hp[1] = cp[0] = cp[1] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
   if (Pm->task_kind == LGX_TASK_GO2 && lane < Pm->num_feet) {
     if (B.feet_air_time) B.feet_air_time[e * Pm->num_feet + lane] = 0.f;
     B.last_contacts[e * Pm->num_feet + lane] = 0;
@@ -911,13 +987,13 @@ LGX_DEV void reset_env(const lgx_task_params* Pm, const lgx_buffers& B, Sh& s, i
   __syncthreads();
 }
 
-LGX_DEV void fill_uniforms(Sh& s, uint64_t seed, uint32_t gid, uint64_t step, uint32_t stream, int lane) {
-  if (lane < NBLK) {
+LGX_DEV void fill_uniforms(Sh& s, uint64_t seed, uint32_t gid, uint64_t step, uint32_t stream, int lane, int nblk) {
+  for (int b = lane; b < nblk; b += 64) {
     uint32_t o[4];
-    philox4x32_10(gid, (uint32_t)step, (uint32_t)lane | (stream << 16), (uint32_t)(step >> 32), (uint32_t)seed,
+    philox4x32_10(gid, (uint32_t)step, (uint32_t)b | (stream << 16), (uint32_t)(step >> 32), (uint32_t)seed,
                   (uint32_t)(seed >> 32), o);
-    s.U[4 * lane + 0] = u01(o[0]); s.U[4 * lane + 1] = u01(o[1]);
-    s.U[4 * lane + 2] = u01(o[2]); s.U[4 * lane + 3] = u01(o[3]);
+    s.U[4 * b + 0] = u01(o[0]); s.U[4 * b + 1] = u01(o[1]);
+    s.U[4 * b + 2] = u01(o[2]); s.U[4 * b + 3] = u01(o[3]);
   }
   __syncthreads();
 }
@@ -1138,7 +1214,7 @@ LGX_DEV void get_heights(const lgx_task_params* Pm, const lgx_buffers& B, Sh& s,
 #ifndef LGX_WAVES_PER_EU
 #define LGX_WAVES_PER_EU 1
 #endif
-template <bool PHYSICS, bool TERRAIN>
+template <bool PHYSICS, bool TERRAIN, bool ACTNET>
 __global__ __launch_bounds__(64, LGX_WAVES_PER_EU) void env_step_kernel(const lgx_model* __restrict__ M,
                                                       const lgx_task_params* __restrict__ Pm, lgx_buffers B,
                                                       uint64_t seed, uint64_t step_arg,
@@ -1187,7 +1263,7 @@ __global__ __launch_bounds__(64, LGX_WAVES_PER_EU) void env_step_kernel(const lg
       st3(s.vo, vo);
     }
     __syncthreads();
-    for (int sub = 0; sub < Pm->decimation; ++sub) substep<TERRAIN>(s, M, Pm, B, lane, sub == Pm->decimation - 1);
+    for (int sub = 0; sub < Pm->decimation; ++sub) substep<TERRAIN, ACTNET>(s, M, Pm, B, lane, sub == Pm->decimation - 1);
     // final kinematics for the rigid-body state tensor
     kinematics(s, M, lane);
     float root[13];
@@ -1257,7 +1333,7 @@ __global__ __launch_bounds__(64, LGX_WAVES_PER_EU) void env_step_kernel(const lg
   // ================================================================ post-physics
   // Go2Robot.post_physics_step go2.py:345-387 / LeggedRobot legged_robot.py:103-138.
   // Per-env scalars: lane 0, into LDS. Vectors: lane-parallel from LDS.
-  fill_uniforms(s, seed, gid, step, 0, lane);
+  fill_uniforms(s, seed, gid, step, 0, lane, rng_blocks(Pm));
   const bool go2 = Pm->task_kind == LGX_TASK_GO2;
   if (lane == 0) {
     Scratch& x = s.x;
@@ -1476,7 +1552,7 @@ __global__ __launch_bounds__(64) void reset_kernel(const lgx_task_params* __rest
   const int lane = threadIdx.x;
   if (!mask[e]) return;
   const int D = Pm->num_dof;
-  fill_uniforms(s, seed, (uint32_t)(Pm->env_id_offset + e), call, 1, lane);
+  fill_uniforms(s, seed, (uint32_t)(Pm->env_id_offset + e), call, 1, lane, rng_blocks(Pm));
   if (lane < 13) s.root[lane] = B.root_states[(size_t)e * 13 + lane];
   if (lane < 4) s.cmd[lane] = B.commands[e * 4 + lane];
   __syncthreads();
@@ -1579,6 +1655,11 @@ int lgx_bind(lgx_env* env, const lgx_buffers* b) {
       return fail(env, "lgx_bind: heightfield/trimesh terrain needs height_samples and terrain_mesh");
     if (env->params.hf_rows < 2 || env->params.hf_cols < 2) return fail(env, "lgx_bind: terrain smaller than 2x2");
   }
+  if (env->params.actuator_net && (!b->sea_hidden || !b->sea_cell))
+    return fail(env, "lgx_bind: the actuator network needs sea_hidden/sea_cell [2, N*D, 8]");
+  if (env->params.actuator_net &&
+      ((reinterpret_cast<uintptr_t>(b->sea_hidden) | reinterpret_cast<uintptr_t>(b->sea_cell)) & 15))
+    return fail(env, "lgx_bind: sea_hidden/sea_cell must be 16-byte aligned");
   if (env->params.curriculum && (!b->terrain_levels || !b->terrain_types || !b->terrain_origins))
     return fail(env, "lgx_bind: terrain curriculum needs terrain_levels/terrain_types/terrain_origins");
   env->buffers = *b;
@@ -1595,9 +1676,11 @@ static int launch_step(lgx_env* env, uint64_t seed, uint64_t step, const uint64_
   const int KS = env->params.num_reward_terms + (env->params.has_termination_reward ? 1 : 0);
   if (env->buffers.episode_stats)
     HIP_OK(hipMemsetAsync(env->buffers.episode_stats, 0, sizeof(float) * (KS + 1), st));
-  const bool terrain = env->params.mesh_type != LGX_MESH_PLANE;
-  auto kern = physics ? (terrain ? lgx::env_step_kernel<true, true> : lgx::env_step_kernel<true, false>)
-                      : lgx::env_step_kernel<false, false>;
+  // compiled variants: the plane/PD path (the benchmark) carries no terrain or LSTM code
+  const bool terrain = env->params.mesh_type != LGX_MESH_PLANE, actnet = env->params.actuator_net != 0;
+  auto kern = !physics ? lgx::env_step_kernel<false, false, false>
+              : actnet ? (terrain ? lgx::env_step_kernel<true, true, true> : lgx::env_step_kernel<true, false, true>)
+                       : (terrain ? lgx::env_step_kernel<true, true, false> : lgx::env_step_kernel<true, false, false>);
   hipLaunchKernelGGL(kern, dim3(N), dim3(64), 0, st, env->d_model, env->d_params, env->buffers, seed, step,
                      step_dev);
   HIP_OK(hipGetLastError());

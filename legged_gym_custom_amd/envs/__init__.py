@@ -2,6 +2,7 @@
 from legged_gym_custom_amd import LEGGED_GYM_ROOT_DIR, LEGGED_GYM_ENVS_DIR  # noqa: F401
 from legged_gym_custom_amd.envs.base.legged_robot import LeggedRobot  # noqa: F401
 from legged_gym_custom_amd.envs.base.legged_robot_config import LeggedRobotCfg, LeggedRobotCfgPPO  # noqa: F401
+from legged_gym_custom_amd.envs.anymal_c.anymal import Anymal
 from legged_gym_custom_amd.envs.anymal_c.mixed_terrains.anymal_c_rough_config import AnymalCRoughCfg, AnymalCRoughCfgPPO
 from legged_gym_custom_amd.envs.anymal_c.flat.anymal_c_flat_config import AnymalCFlatCfg, AnymalCFlatCfgPPO
 from legged_gym_custom_amd.envs.go2.go2 import Go2Robot
@@ -10,6 +11,8 @@ from legged_gym_custom_amd.envs.go2.go2_parkour_config import Go2ParkourCfg, Go2
 from legged_gym_custom_amd.envs.go2.go2_parkour_finetune_config import Go2FinetuneCfg, Go2FinetuneCfgPPO
 from legged_gym_custom_amd.utils.task_registry import task_registry
 
+task_registry.register("anymal_c_rough", Anymal, AnymalCRoughCfg(), AnymalCRoughCfgPPO())
+task_registry.register("anymal_c_flat", Anymal, AnymalCFlatCfg(), AnymalCFlatCfgPPO())
 task_registry.register("go2", Go2Robot, Go2Cfg(), Go2CfgPPO())
 task_registry.register("go2_parkour", Go2Robot, Go2ParkourCfg(), Go2ParkourCfgPPO())
 task_registry.register("go2_parkour_finetune", Go2Robot, Go2FinetuneCfg(), Go2FinetuneCfgPPO())

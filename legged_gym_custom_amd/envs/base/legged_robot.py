@@ -196,6 +196,11 @@ class LeggedRobot(BaseTask):
             self.custom_origins = True
             t = self.cfg.terrain
             max_init_level = t.max_init_terrain_level if t.curriculum else t.num_rows - 1
+            if max_init_level >= t.num_rows:
+                # the reference indexes terrain_origins out of bounds here (a device fault);
+                # refuse the configuration up front instead
+                raise ValueError(f"terrain.max_init_terrain_level ({max_init_level}) must be < terrain.num_rows "
+                                 f"({t.num_rows})")
             self.max_terrain_level = t.num_rows
             self.terrain_levels = torch.randint(0, max_init_level + 1, (total,), device=self.device)[sl].contiguous()
             self.terrain_types = torch.div(torch.arange(total, device=self.device), (total / t.num_cols),
@@ -306,6 +311,7 @@ class LeggedRobot(BaseTask):
         self.task_params = prm.build_task_params(self.cfg, self.model_dict, n, self.num_envs_total, self.env_id_offset,
                                                  sim_dt=self.sim_params.dt, go2=self.TASK_KIND == _abi.TASK_GO2,
                                                  terrain_shape=(terrain.tot_rows, terrain.tot_cols) if terrain else None)
+        self._sea_buffers = self._setup_actuator(self.task_params)
         names, _, _, term = prm.reward_terms(self.cfg, self.dt)
         self._episode_keys = names + (["termination"] if term is not None else [])
         ks = len(self._episode_keys)
@@ -338,8 +344,13 @@ class LeggedRobot(BaseTask):
             "env_origins": self.env_origins, "episode_stats": self.episode_stats,
             "terrain_levels": getattr(self, "terrain_levels", None), "terrain_types": getattr(self, "terrain_types", None),
             "terrain_origins": getattr(self, "terrain_origins", None), "height_samples": self.height_samples,
-            "terrain_mesh": self._terrain_mesh,
+            "terrain_mesh": self._terrain_mesh, **self._sea_buffers,
         })
+
+    def _setup_actuator(self, P):
+        """PD control (legged_robot.py:440-478) lives in the kernel; subclasses with an
+        actuator network fill P.sea_* and return its state buffers (anymal.py)."""
+        return {}
 
     def _prepare_reward_function(self):
         """legged_robot.py:730-754: nonzero scales x dt, alphabetical; the terms run in

@@ -68,6 +68,8 @@ class OracleEnv:
             "friction": f(N), "mass_params": f(N, 4), "kp_kd": f(2, N, D), "env_origins": f(N, 3),
             "terrain_levels": None, "terrain_types": None, "terrain_origins": None, "height_samples": None,
             "terrain_mesh": None,
+            "sea_hidden": f(2, N * D, 8) if P.actuator_net else None,
+            "sea_cell": f(2, N * D, 8) if P.actuator_net else None,
             "episode_stats": f(num_reward_slots + 1),
         }
         self.a["kp_kd"][:] = 1.0

@@ -115,9 +115,54 @@ static float norm3(const float* v) { return sqrtf(v[0] * v[0] + v[1] * v[1] + v[
 static float norm2(float a, float b) { return sqrtf(a * a + b * b); }
 
 /* --------------------------------------------------------- actuator (pinned) */
+/* ANYmal SEA actuator network, Anymal._compute_torques anymal.py:71-81: one step of the
+   2-layer LSTM (torch.nn.LSTM cell: gates = W_ih x + b_ih + W_hh h + b_hh, order i f g o;
+   c' = f c + i g; h' = o tanh(c')) then Linear, per joint; state [2, N*D, 8] in place. */
+static float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+static void lstm_layer(const float* w_ih, int nin, const float* w_hh, const float* b_ih, const float* b_hh,
+                       const float* x, float* h, float* c) {
+  float gates[32], hn[8];
+  for (int g = 0; g < 32; ++g) {
+    float a = 0.0f, b = 0.0f;
+    for (int k = 0; k < nin; ++k) a += w_ih[g * nin + k] * x[k];
+    for (int k = 0; k < 8; ++k) b += w_hh[g * 8 + k] * h[k];
+    gates[g] = (a + b_ih[g]) + (b + b_hh[g]);
+  }
+  for (int u = 0; u < 8; ++u) {
+    float i = sigm(gates[u]), f = sigm(gates[8 + u]), gg = tanhf(gates[16 + u]), o = sigm(gates[24 + u]);
+    c[u] = f * c[u] + i * gg;
+    hn[u] = o * tanhf(c[u]);
+  }
+  for (int u = 0; u < 8; ++u) h[u] = hn[u];
+}
+
+static float sea_torque(const lgx_task_params* P, const lgx_buffers* B, int e, int j, float in0, float in1) {
+  const size_t NT = (size_t)P->num_envs * P->num_dof, r = (size_t)e * P->num_dof + j;
+  float* h0 = B->sea_hidden + r * 8;
+  float* c0 = B->sea_cell + r * 8;
+  float* h1 = B->sea_hidden + (NT + r) * 8;
+  float* c1 = B->sea_cell + (NT + r) * 8;
+  float x[2] = {in0 * P->sea_in_scale[0], in1 * P->sea_in_scale[1]};
+  lstm_layer(P->sea_w_ih0, 2, P->sea_w_hh0, P->sea_b_ih0, P->sea_b_hh0, x, h0, c0);
+  lstm_layer(P->sea_w_ih1, 8, P->sea_w_hh1, P->sea_b_ih1, P->sea_b_hh1, h0, h1, c1);
+  float y = 0.0f;
+  for (int k = 0; k < 8; ++k) y += P->sea_lin_w[k] * h1[k];
+  return P->sea_out_scale * (y + P->sea_lin_b);
+}
+
 /* LeggedRobot._compute_torques, legged_robot.py:440-478 (P control, kp/kd mult.) */
 void oracle_compute_torques(const lgx_task_params* P, const lgx_buffers* B, int e) {
   const int D = P->num_dof, N = P->num_envs;
+  if (P->actuator_net) {
+    for (int j = 0; j < D; ++j) {
+      float a = B->actions[e * P->num_actions + j];
+      float q = B->dof_state[(e * D + j) * 2 + 0];
+      float qd = B->dof_state[(e * D + j) * 2 + 1];
+      B->torques[e * D + j] = sea_torque(P, B, e, j, (a * P->action_scale + P->default_dof_pos[j]) - q, qd);
+    }
+    return;
+  }
   for (int j = 0; j < D; ++j) {
     float a = B->actions[e * P->num_actions + j];
     float q = B->dof_state[(e * D + j) * 2 + 0];
@@ -270,6 +315,14 @@ static void reset_env(const lgx_task_params* P, lgx_buffers* B, int e, uint64_t 
   for (int i = 0; i < P->history_len * P->num_proprio; ++i) B->obs_history[(size_t)e * P->history_len * P->num_proprio + i] = 0.0f;
   B->episode_length[e] = 0;
   B->reset[e] = 1;
+  if (P->actuator_net && B->sea_hidden) { /* Anymal.reset_idx anymal.py:56-60 */
+    const size_t NT = (size_t)P->num_envs * D;
+    for (int l = 0; l < 2; ++l)
+      for (int k = 0; k < D * 8; ++k) {
+        B->sea_hidden[(l * NT + (size_t)e * D) * 8 + k] = 0.0f;
+        B->sea_cell[(l * NT + (size_t)e * D) * 8 + k] = 0.0f;
+      }
+  }
   if (P->task_kind == LGX_TASK_GO2) {
     for (int f = 0; f < P->num_feet; ++f) {
       if (B->feet_air_time) B->feet_air_time[e * P->num_feet + f] = 0.0f;

@@ -30,8 +30,13 @@ SLOT_ROOT_XY = 20     # block 5: root x, root y
 SLOT_ROOT_VEL = 24    # blocks 6-7: 6 root velocity draws
 SLOT_RCMD = 32        # block 8: cmd resample inside reset_idx
 SLOT_NOISE = 36       # blocks 9-21: 52 observation-noise draws
-NUM_BLOCKS = 22
+NUM_BLOCKS = 22       # Go2 (52 noise draws); see num_blocks
 NUM_SLOTS = NUM_BLOCKS * 4
+
+
+def num_blocks(num_proprio):
+    """Blocks per env per step: 9 fixed + one per 4 noise draws (ANYmal 235 -> 68)."""
+    return SLOT_NOISE // 4 + (num_proprio + 3) // 4
 
 STREAM_STEP = 0       # draws inside env.step()
 STREAM_RESET = 1      # draws inside an external reset_idx() call (BaseTask.reset)

@@ -37,7 +37,10 @@ def terrain_for(env_cfg, np_seed=1):
     return ter, mesh
 
 
-def go2_setup(num_envs, task="go2", terrain=None):
+def go2_setup(num_envs, task="go2", terrain=None, sea_seed=None):
+    """(env_cfg, model, task params) for a task; `sea_seed` installs the synthetic SEA
+    actuator net (legged_gym_custom_amd.actuator.random_sea_weights) the ANYmal fixtures
+    were recorded with."""
     from legged_gym_custom_amd.envs import task_registry_configs
     from legged_gym_custom_amd import model as mdl, params as prm
     env_cfg, _ = task_registry_configs(task)
@@ -45,5 +48,26 @@ def go2_setup(num_envs, task="go2", terrain=None):
     shape = (terrain.tot_rows, terrain.tot_cols) if terrain is not None else None
     if env_cfg.terrain.mesh_type not in ("heightfield", "trimesh"):
         env_cfg.terrain.curriculum = False  # LeggedRobot._parse_cfg (legged_robot.py:950-951)
-    P = prm.build_task_params(env_cfg, m, num_envs, go2=True, terrain_shape=shape)
+    P = prm.build_task_params(env_cfg, m, num_envs, go2=task.startswith("go2"), terrain_shape=shape)
+    if sea_seed is not None:
+        from legged_gym_custom_amd import actuator as act
+        act.fill_task_params(P, act.random_sea_weights(int(sea_seed)))
     return env_cfg, m, P
+
+
+def fixture_setup(d, task):
+    """Everything a replay needs from a fixture: (env_cfg, model, params, terrain tuple
+    for OracleEnv.set_terrain / Twin, sea flag)."""
+    import hashlib
+    N = int(d["num_envs"])
+    ter = tw = None
+    if "terrain_levels" in d:
+        from legged_gym_custom_amd.envs import task_registry_configs
+        env_cfg = task_registry_configs(task)[0]
+        env_cfg.env.num_envs = N
+        ter, mesh = terrain_for(env_cfg, int(d["np_seed"]))
+        assert hashlib.sha1(ter.heightsamples.tobytes()).hexdigest() == str(d["height_samples_sha1"])
+        tw = (ter.heightsamples, mesh, d["terrain_levels"], d["terrain_types"], d["terrain_origins"])
+    sea = int(d["sea_seed"]) if "sea_seed" in d else None
+    cfg, m, P = go2_setup(N, task, terrain=ter, sea_seed=sea)
+    return cfg, m, P, tw, sea is not None

@@ -150,3 +150,50 @@ def test_go2_parkour_env_builds_and_stands():
     assert (_weight_ratio(env, standing).median() - 1.0).abs() < 0.1
     # the scan sees the first gap ahead for no-one yet (5 m away): all zero heights here
     assert env.measured_heights.abs().max() < 1e-6
+
+
+def test_anymal_rough_env_with_actuator_net(tmp_path):
+    """anymal_c_rough end to end on the GPU: rough curriculum trimesh, 187-point scan in
+    the 235-dim proprio (history 5 -> obs 1410), SEA actuator net loaded from a
+    TorchScript archive (synthetic weights, written here) and run in the kernel; reset
+    envs leave the step with zero LSTM state (anymal.py:56-60)."""
+    import torch
+    from legged_gym_custom_amd import actuator as act
+    from legged_gym_custom_amd.envs import task_registry_configs
+    from legged_gym_custom_amd.envs.anymal_c.anymal import Anymal
+    from legged_gym_custom_amd.utils.helpers import SimParams, class_to_dict, set_seed
+    path = str(tmp_path / "sea.pt")
+    act.save_sea_archive(act.random_sea_weights(1, scale=0.3), path)
+    cfg = task_registry_configs("anymal_c_rough")[0]
+    cfg.env.num_envs = 1024
+    cfg.terrain.num_rows, cfg.terrain.num_cols = 6, 6   # max_init_terrain_level 5 < num_rows
+    cfg.control.actuator_net_file = path
+    set_seed(1)
+    env = Anymal(cfg, SimParams(class_to_dict(cfg.sim)), 1, "cuda:0", True)
+    env.reset()
+    assert env.obs_buf.shape == (1024, 1410)
+    z = torch.zeros(env.num_envs, 12, device="cuda")
+    resets = 0
+    for _ in range(30):
+        env.step(z)
+        resets += int(env.reset_buf.sum())
+    torch.cuda.synchronize()
+    assert torch.isfinite(env.obs_buf).all() and torch.isfinite(env.sea_hidden_state).all()
+    assert env.sea_hidden_state.abs().sum() > 0
+    r = env.reset_buf.nonzero().flatten()
+    if len(r):
+        assert env.sea_hidden_state_per_env[:, r].abs().max() == 0
+        assert env.sea_cell_state_per_env[:, r].abs().max() == 0
+    heights = env.obs_buf[:, -187:]
+    assert heights.abs().max() > 0  # the scan sees the terrain
+
+
+def test_anymal_missing_actuator_archive_fails_loudly(tmp_path):
+    from legged_gym_custom_amd.envs import task_registry_configs
+    from legged_gym_custom_amd.envs.anymal_c.anymal import Anymal
+    from legged_gym_custom_amd.utils.helpers import SimParams, class_to_dict
+    cfg = task_registry_configs("anymal_c_flat")[0]
+    cfg.env.num_envs = 8
+    cfg.control.actuator_net_file = str(tmp_path / "missing.pt")
+    with pytest.raises(FileNotFoundError):
+        Anymal(cfg, SimParams(class_to_dict(cfg.sim)), 1, "cuda:0", True)

@@ -58,32 +58,23 @@ def replay(name, task):
     from legged_gym_custom_amd import model as mdl
     d = G.load(name)
     N = int(d["num_envs"])
-    terrain = "terrain_levels" in d
-    env_cfg = None
-    ter = mesh = None
-    if terrain:
-        from legged_gym_custom_amd.envs import task_registry_configs
-        env_cfg = task_registry_configs(task)[0]
-        env_cfg.env.num_envs = N
-        ter, mesh = G.terrain_for(env_cfg, int(d["np_seed"]))
-        import hashlib
-        assert hashlib.sha1(ter.heightsamples.tobytes()).hexdigest() == str(d["height_samples_sha1"])
-    cfg, m, P = G.go2_setup(N, task, terrain=ter)
-    K = P.num_reward_terms
+    cfg, m, P, terrain, sea = G.fixture_setup(d, task)
+    K, NB, PP = P.num_reward_terms, P.num_bodies, P.num_proprio
+    go2 = task.startswith("go2")
     o = driver.OracleEnv(P, mdl.to_struct(m), K + P.has_termination_reward)
     a = o.a
     a["friction"][:] = d["friction"]
     a["mass_params"][:] = d["mass_params"]
     a["kp_kd"][:] = d["kp_kd_multipliers"]
     a["env_origins"][:] = d["env_origins"]
-    if terrain:
-        o.set_terrain(ter.heightsamples, mesh, d["terrain_levels"], d["terrain_types"], d["terrain_origins"])
+    if terrain is not None:
+        o.set_terrain(*terrain)
     # BaseTask.reset(): reset_idx(all) outside a step (RNG stream 1, call 0), after init
     o.reset_envs(np.ones(N, bool), seed=int(d["seed"]), call=0, after_init=1)
     assert _close(a["root_states"], d["reset0_state.root_states"])
     assert _close(a["dof_state"].reshape(-1, 2), d["reset0_state.dof_state"])
     assert _close(a["commands"], d["reset0_state.commands"])
-    if terrain:
+    if terrain is not None:
         assert np.array_equal(a["terrain_levels"], d["reset0_state.terrain_levels"])
         assert _close(a["env_origins"], d["reset0_state.env_origins"])
     worst = {}
@@ -96,7 +87,7 @@ def replay(name, task):
         o.clip_actions()
         a["root_states"][:] = S("physics.root_states")
         a["dof_state"][:] = S("physics.dof_state").reshape(N, 12, 2)
-        a["contact_forces"][:] = S("physics.contact_forces").reshape(N, 19, 3)
+        a["contact_forces"][:] = S("physics.contact_forces").reshape(N, NB, 3)
         rb = a["rigid_body_states"]
         rb[:] = 0
         rb[:, list(P.feet_idx[:4]), 0:3] = S("physics.feet_pos")
@@ -108,26 +99,26 @@ def replay(name, task):
             ("rew", a["rew"], S("out.rew_buf")),
             ("reset", a["reset"], S("out.reset_buf")),
             ("time_out", a["time_out"], S("out.time_out_buf")),
-            ("obs_cur", a["obs"][:, -52:], S("out.obs_cur")),
-            ("priv", a["priv"], S("out.privileged_obs_buf")),
-            ("est", a["est"], S("out.estimated_obs_buf")),
-            ("scan", a["scan"], S("out.scan_obs_buf")),
+            ("obs_cur", a["obs"][:, -PP:], S("out.obs_cur")),
             ("episode_sums", a["episode_sums"][:, :K].T, S("out.episode_sums")),
-            ("roll", a["rpy_phase"][:, 0], S("out.roll")),
-            ("pitch", a["rpy_phase"][:, 1], S("out.pitch")),
             ("episode_length", a["episode_length"], S("out.state_out.episode_length_buf")),
-            ("last_contacts", a["last_contacts"], S("out.state_out.last_contacts")),
             ("root_states", a["root_states"], S("out.state_out.root_states")),
             ("dof_state", a["dof_state"].reshape(-1, 2), S("out.state_out.dof_state")),
             ("commands", a["commands"], S("out.state_out.commands")),
         ]
-        for k in ["last_actions", "last_dof_vel", "last_root_vel", "last_base_lin_vel", "last_torques",
-                  "last_contact_heights"]:
+        if go2:
+            checks += [("priv", a["priv"], S("out.privileged_obs_buf")), ("est", a["est"], S("out.estimated_obs_buf")),
+                       ("scan", a["scan"], S("out.scan_obs_buf")), ("roll", a["rpy_phase"][:, 0], S("out.roll")),
+                       ("pitch", a["rpy_phase"][:, 1], S("out.pitch")),
+                       ("last_contacts", a["last_contacts"], S("out.state_out.last_contacts")),
+                       ("last_contact_heights", a["last_contact_heights"], S("out.state_out.last_contact_heights"))]
+        for k in ["last_actions", "last_dof_vel", "last_root_vel", "last_base_lin_vel", "last_torques"]:
             checks.append((k, a[k], S("out.state_out." + k)))
-        if terrain:
+        if terrain is not None:
             checks += [("measured_heights", a["measured_heights"], S("out.measured_heights")),
-                       ("jump_flags", a["rpy_phase"][:, 7:8], S("out.jump_flags")),
                        ("env_origins", a["env_origins"], S("out.state_out.env_origins"))]
+            if f"steps.{t}.out.jump_flags" in d:
+                checks.append(("jump_flags", a["rpy_phase"][:, 7:8], S("out.jump_flags")))
             assert np.array_equal(a["terrain_levels"], S("out.state_out.terrain_levels")), f"step {t}: terrain_levels"
         if f"steps.{t}.out.obs_buf" in d:
             checks += [("obs", a["obs"], S("out.obs_buf")), ("critic", a["critic"], S("out.critic_obs_buf"))]
@@ -139,9 +130,12 @@ def replay(name, task):
         if cnt > 0 and f"steps.{t}.out.extras_episode" in d:
             assert np.allclose(a["episode_stats"][:K] / cnt / 20.0, S("out.extras_episode"), atol=1e-6, rtol=1e-4)
     assert _close(a["obs_history"], d["final_obs_history"])
+    if sea:
+        assert _close(a["sea_hidden"], d["final_sea_hidden"]) and _close(a["sea_cell"], d["final_sea_cell"])
     print("worst abs errors:", {k: f"{v:.2e}" for k, v in worst.items()})
 
 
-@pytest.mark.parametrize("name,task", [("go2_flat_n64.npz", "go2"), ("go2_parkour_n64.npz", "go2_parkour")])
+@pytest.mark.parametrize("name,task", [("go2_flat_n64.npz", "go2"), ("go2_parkour_n64.npz", "go2_parkour"),
+                                       ("anymal_c_rough_n64.npz", "anymal_c_rough")])
 def test_oracle_replays_reference_steps(name, task):
     replay(name, task)

@@ -153,3 +153,45 @@ def test_packed_mesh_rebuilds_the_reference_trimesh(gold):
         np.testing.assert_array_equal(h, hf)
         np.testing.assert_allclose(v, gold[key], atol=2e-6, rtol=0)
         assert (np.abs(dx) <= 1).all() and (np.abs(dy) <= 1).all()
+
+
+def test_torchscript_reader_round_trip(tmp_path):
+    """actuator.read_torchscript_tensors (no deserialisation) returns exactly the
+    tensors torch.jit.save wrote, for the SEA net architecture (anymal.py:24)."""
+    from legged_gym_custom_amd import actuator as act
+    w = act.random_sea_weights(7)
+    p = str(tmp_path / "net.pt")
+    act.save_sea_archive(w, p)
+    r = act.load_sea_lstm(p)
+    for k in act.SEA_KEYS:
+        np.testing.assert_array_equal(r[k], w[k])
+
+
+def test_sea_lstm_restatement_matches_torch_lstm_cell():
+    """SeaLSTM == x*in_scale -> 2-layer nn.LSTM step -> Linear -> *out_scale, checked
+    against an explicit gate-by-gate fp64 evaluation (gate order i f g o)."""
+    import torch
+    from legged_gym_custom_amd import actuator as act
+    w = act.random_sea_weights(4)
+    net = act.SeaLSTM(w).double()
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(50, 1, 2, generator=g, dtype=torch.float64)
+    h = torch.randn(2, 50, 8, generator=g, dtype=torch.float64)
+    c = torch.randn(2, 50, 8, generator=g, dtype=torch.float64)
+    with torch.no_grad():
+        tau, (h1, c1) = net(x, (h, c))
+    W = {k: torch.from_numpy(v).double() for k, v in w.items()}
+    inp = x[:, 0, :] * W["in_scale"].reshape(2)
+    hs, cs = [], []
+    for layer in range(2):
+        gates = inp @ W[f"lstm.weight_ih_l{layer}"].T + W[f"lstm.bias_ih_l{layer}"] + \
+            h[layer] @ W[f"lstm.weight_hh_l{layer}"].T + W[f"lstm.bias_hh_l{layer}"]
+        i, f, gg, o = gates.split(8, dim=1)
+        cn = torch.sigmoid(f) * c[layer] + torch.sigmoid(i) * torch.tanh(gg)
+        hn = torch.sigmoid(o) * torch.tanh(cn)
+        hs.append(hn); cs.append(cn)
+        inp = hn
+    want = W["out_scale"] * (inp @ W["linear.weight"].T + W["linear.bias"])[:, 0]
+    torch.testing.assert_close(tau, want)
+    torch.testing.assert_close(h1, torch.stack(hs))
+    torch.testing.assert_close(c1, torch.stack(cs))
