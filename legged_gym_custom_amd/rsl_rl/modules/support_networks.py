@@ -93,3 +93,12 @@ class AdaptationEncoder(nn.Module):
         x = self.fc_encoder(unflattened_obs_history)
         x = self.conv_layers(x.permute(0, 2, 1))
         return self.fc_final(x)
+
+
+class AdaptationEncoderTS(AdaptationEncoder):
+    """The adaptation encoder's plain forward only (TorchScript export, helpers.py:196-200)."""
+
+    def forward(self, unflattened_obs_history):
+        x = self.fc_encoder(unflattened_obs_history)
+        x = self.conv_layers(x.permute(0, 2, 1))
+        return self.fc_final(x)

@@ -9,6 +9,7 @@ import argparse
 import copy
 import os
 import random
+from collections import OrderedDict
 
 import numpy as np
 import torch
@@ -163,11 +164,43 @@ def get_args(argv=None):
     return args
 
 
+def _scriptable(module):
+    """CPU copy of `module` that torch.jit.script accepts and that computes the reference
+    module's forward: HipMLP -> nn.Sequential of the same children (same state_dict keys),
+    the adaptation encoder -> its plain Linear/Conv1d forward (support_networks.py:160-175)."""
+    from legged_gym_custom_amd.rsl_rl.modules.hip_mlp import HipMLP
+    from legged_gym_custom_amd.rsl_rl.modules.support_networks import AdaptationEncoder, AdaptationEncoderTS
+
+    m = copy.deepcopy(module).to("cpu")
+
+    def plain(seq):  # _modules keeps repeated (shared) activation instances and their indices
+        return torch.nn.Sequential(OrderedDict((k, convert(c)) for k, c in seq._modules.items()))
+
+    def convert(mod):
+        for name, child in list(mod._modules.items()):
+            if isinstance(child, HipMLP):
+                setattr(mod, name, plain(child))
+            elif child is not None:
+                convert(child)
+        return mod
+
+    if isinstance(m, HipMLP):
+        m = plain(m)
+    convert(m)
+    if isinstance(m, AdaptationEncoder):
+        m.__class__ = AdaptationEncoderTS
+    return m.eval()
+
+
 def export_policy_as_jit(actor_critic, estimator, path):
-    """helpers.py:180-214: policy.pt, adaptation_module.pt, estimator.pt, scan_encoder.pt."""
+    """helpers.py:180-214: TorchScript policy.pt (the actor MLP), adaptation_module.pt
+    (obs history [B, H, P] -> latent), estimator.pt (obs -> estimated obs) and
+    scan_encoder.pt (scan -> latent), the files deploy_base.py:32-35 loads and calls as
+    policy(cat(obs, adaptation(hist), scan_encoder(scan), estimator(obs)))."""
+    if hasattr(actor_critic, "memory_a"):
+        raise NotImplementedError("recurrent policies are not exported (PolicyExporterLSTM, helpers.py:217)")
     os.makedirs(path, exist_ok=True)
     for fname, module in (("policy.pt", actor_critic.actor), ("adaptation_module.pt", actor_critic.adaptation_encoder_),
                           ("estimator.pt", estimator), ("scan_encoder.pt", actor_critic.scan_encoder)):
-        m = copy.deepcopy(module).to("cpu")
-        torch.jit.script(m).save(os.path.join(path, fname))
+        torch.jit.script(_scriptable(module)).save(os.path.join(path, fname))
         print(f"Exported {fname} to: {path}")
