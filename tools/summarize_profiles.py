@@ -15,6 +15,10 @@ os.makedirs(out, exist_ok=True)
 stats = glob.glob(os.path.join(src, "trace", "*", "*_kernel_stats.csv"))
 if stats:
     shutil.copy(stats[0], os.path.join(out, f"{tag}_bench_kernel_stats.csv"))
+for sub, name in (("parkour", "parkour_n8192"), ("anymal", "anymal_rough_n4096")):
+    st = glob.glob(os.path.join(src, sub, "*", "*_kernel_stats.csv"))
+    if st:
+        shutil.copy(st[0], os.path.join(out, f"{tag}_env_{name}_kernel_stats.csv"))
 
 
 def pmc(name):
