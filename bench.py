@@ -93,6 +93,7 @@ def main():
     ap.add_argument("--num_envs", type=int, default=4096)
     ap.add_argument("--no_cpu_baseline", action="store_true")
     ap.add_argument("--kernel_iters", type=int, default=50)
+    ap.add_argument("--task", default="go2", help="go2 (the BASELINE metric) | go2_parkour (C4, informative)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -110,10 +111,10 @@ def main():
     from legged_gym_custom_amd import _abi
     from legged_gym_custom_amd.envs import task_registry
     from legged_gym_custom_amd.utils.helpers import get_args
-    a = get_args(["--task=go2", "--headless", f"--num_envs={args.num_envs}", f"--sim_device={dev}",
+    a = get_args([f"--task={args.task}", "--headless", f"--num_envs={args.num_envs}", f"--sim_device={dev}",
                   f"--rl_device={dev}", "--seed=1"])
-    env, env_cfg = task_registry.make_env("go2", a)
-    _, train_cfg = task_registry.get_cfgs("go2")
+    env, env_cfg = task_registry.make_env(args.task, a)
+    _, train_cfg = task_registry.get_cfgs(args.task)
     runner, _ = task_registry.make_alg_runner(env, args=a, train_cfg=train_cfg, log_root=None)
 
     def barrier():
@@ -157,22 +158,26 @@ def main():
     bpe = env_bytes_per_env_step(env.task_params, env.num_bodies, ks)
     launch_bytes = bpe * env.num_envs
     achieved = launch_bytes / (kern_avg_ms * 1e-3) / 1e9
-    traffic, traffic_src = committed_traffic(args.num_envs)
+    traffic, traffic_src = committed_traffic(args.num_envs) if args.task == "go2" else (None, None)
 
     if rank == 0:
+        terrain = env.cfg.terrain.mesh_type in ("heightfield", "trimesh")
+        kname = f"lgx::env_step_kernel<true, {'true' if terrain else 'false'}, false>"
+        data = ("synthetic (Go2 flat terrain, random-init ActorCritic/estimator, seed 1)" if args.task == "go2" else
+                f"synthetic ({args.task}: generated terrain, random-init ActorCritic/estimator, seed 1)")
         out = {
-            "metric": METRIC, "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world,
+            "metric": METRIC if args.task == "go2" else f"env-steps/sec, {args.task} {args.num_envs} envs per GPU", "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic (Go2 flat terrain, random-init ActorCritic/estimator, seed 1)",
-            "config": {"workload": "go2 flat terrain, rsl_rl PPO/ROA iteration (24 env steps + 5x4 minibatch update)",
+            "data": data,
+            "config": {"workload": f"{args.task}, rsl_rl PPO/ROA iteration (24 env steps + 5x4 minibatch update)",
                        "num_envs_per_gpu": args.num_envs, "num_steps_per_env": steps_per_iter,
                        "global_envs": args.num_envs * world, "parallelism": f"env-sharded dp{world}"},
             "collection_s": round(runner.last_perf.get("collection_time", 0.0), 4),
             "learn_s": round(runner.last_perf.get("learn_time", 0.0), 4),
             "env_kernel": {"avg_us": round(kern_avg_ms * 1e3, 2), "min_us": round(kern_ms[0] * 1e3, 2),
                            "env_steps_per_s": round(env.num_envs / (kern_avg_ms * 1e-3), 1)},
-            "roofline": {"bound": "hbm", "kernel": "lgx::env_step_kernel<true, false>", "achieved": round(achieved, 1),
+            "roofline": {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "bytes_per_env_step": bpe, "bytes_per_launch": launch_bytes,
                          "traffic": None if traffic is None else round(traffic), "traffic_source": traffic_src},

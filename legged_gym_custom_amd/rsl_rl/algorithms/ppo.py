@@ -268,19 +268,19 @@ class PPO:
         self.actor_critic.train()
 
     def act(self, obs, privileged_obs, critic_obs, true_estimated_obs, scan_obs, adaptation_mode=False):
-        """ppo.py:129-153: the rollout actor sees the ESTIMATOR's output (Q12)."""
+        """ppo.py:129-153: the rollout actor sees the ESTIMATOR's output (Q12). The
+        observations are stored at act time (RolloutStorage.record_observations): the env
+        overwrites its buffers in place during the step that follows."""
         estimated_obs = self.estimator(obs)
         t = self.transition
+        (t.observations, t.privileged_observations, t.critic_observations, t.true_estimated_observations,
+         t.scan_observations) = self.storage.record_observations(obs, privileged_obs, critic_obs, true_estimated_obs,
+                                                                 scan_obs)
         t.actions = self.actor_critic.act(obs, privileged_obs, estimated_obs, scan_obs, adaptation_mode).detach()
         t.values = self.actor_critic.evaluate(critic_obs).detach()
         t.actions_log_prob = self.actor_critic.get_actions_log_prob(t.actions).detach()
         t.action_mean = self.actor_critic.action_mean.detach()
         t.action_sigma = self.actor_critic.action_std.detach()
-        t.observations = obs
-        t.privileged_observations = privileged_obs
-        t.critic_observations = critic_obs
-        t.true_estimated_observations = true_estimated_obs
-        t.scan_observations = scan_obs
         return t.actions
 
     def process_env_step(self, rewards, dones, infos):

@@ -58,19 +58,47 @@ class RolloutStorage:
         self.saved_hidden_states_c = None
         self.step = 0
 
+    def observation_slots(self):
+        """This step's [obs, priv, critic, true est, scan] rows of the storage."""
+        s = self.step
+        return [self.observations[s], self.privileged_observations[s], self.critic_observations[s],
+                self.true_estimated_observations[s], self.scan_observations[s]]
+
+    def record_observations(self, obs, privileged_obs, critic_obs, true_estimated_obs, scan_obs):
+        """Copy the observations an action is taken on into this step's rows, at act time.
+        The env here writes its observation buffers in place, so by add_transitions time
+        (after env.step) they already hold the next observations; the reference keeps the
+        pre-step tensors because its env rebinds new ones (legged_robot.py:93-98)."""
+        if self.step >= self.num_transitions_per_env:
+            raise AssertionError("Rollout buffer overflow")
+        dst = self.observation_slots()
+        src = [obs, privileged_obs, critic_obs, true_estimated_obs, scan_obs]
+        if str(self.device).startswith("cuda"):
+            torch._foreach_copy_(dst, src)
+        else:
+            for d, x in zip(dst, src):
+                d.copy_(x)
+        return dst
+
     def add_transitions(self, transition):
+        """rollout_storage.py:87-105. Observation fields that already alias this step's rows
+        (record_observations) are not copied again."""
         if self.step >= self.num_transitions_per_env:
             raise AssertionError("Rollout buffer overflow")
         s = self.step
-        dst = [self.observations[s], self.privileged_observations[s], self.critic_observations[s],
-               self.true_estimated_observations[s], self.scan_observations[s], self.actions[s], self.rewards[s],
-               self.dones[s], self.values[s], self.actions_log_prob[s], self.mu[s], self.sigma[s]]
-        src = [transition.observations, transition.privileged_observations, transition.critic_observations,
-               transition.true_estimated_observations, transition.scan_observations, transition.actions,
-               transition.rewards.view(-1, 1), transition.dones.view(-1, 1).to(self.dones.dtype), transition.values,
-               transition.actions_log_prob.view(-1, 1), transition.action_mean, transition.action_sigma]
-        if self.device != "cpu" and str(self.device).startswith("cuda"):
-            torch._foreach_copy_(dst, src)  # one multi-tensor launch instead of 12 copies
+        dst = [self.actions[s], self.rewards[s], self.dones[s], self.values[s], self.actions_log_prob[s], self.mu[s],
+               self.sigma[s]]
+        src = [transition.actions, transition.rewards.view(-1, 1), transition.dones.view(-1, 1).to(self.dones.dtype),
+               transition.values, transition.actions_log_prob.view(-1, 1), transition.action_mean,
+               transition.action_sigma]
+        obs_src = [transition.observations, transition.privileged_observations, transition.critic_observations,
+                   transition.true_estimated_observations, transition.scan_observations]
+        for d, x in zip(self.observation_slots(), obs_src):
+            if x is not None and d.data_ptr() != x.data_ptr():
+                dst.append(d)
+                src.append(x)
+        if str(self.device).startswith("cuda"):
+            torch._foreach_copy_(dst, src)  # one multi-tensor call instead of 12 copies
         else:
             for d, x in zip(dst, src):
                 d.copy_(x)

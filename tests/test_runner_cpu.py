@@ -84,3 +84,41 @@ def test_device_episode_logging_matches_reference_deques():
     rew, ln, ep = r._host_stats()
     assert rew == list(rewbuffer) and ln == list(lenbuffer)
     assert ep["rew_a"] == sum(v[0] for v in ep_vals) / 60 and ep["rew_b"] == sum(v[1] for v in ep_vals) / 60
+
+
+def test_storage_holds_the_observations_the_policy_acted_on():
+    """Each stored transition pairs an action with the observations it was taken on
+    (ppo.py:129-153 + rollout_storage.py:87-105). The env writes its buffers in place, so
+    the storage must snapshot them at act time, not after env.step; and the stored log-prob
+    must equal the policy's log-prob of the stored action at the stored observations."""
+    r = _runner(None, steps=4)
+    seen = []
+    act = r.alg.act
+
+    def spy(obs, priv, critic, est, scan, **kw):
+        seen.append([x.clone() for x in (obs, priv, critic, est, scan)])
+        return act(obs, priv, critic, est, scan, **kw)
+
+    r.alg.act = spy
+    checked = []
+
+    def check(*a, **k):
+        s = r.alg.storage
+        for t in range(4):
+            for got, want in zip((s.observations[t], s.privileged_observations[t], s.critic_observations[t],
+                                  s.true_estimated_observations[t], s.scan_observations[t]), seen[t]):
+                assert torch.equal(got, want), t
+            ac = r.alg.actor_critic
+            with torch.no_grad():
+                est = r.alg.estimator(s.observations[t])
+                # iteration 0 is a DAgger iteration: the rollout acts in adaptation mode
+                ac.update_distribution(s.observations[t], s.privileged_observations[t], est, s.scan_observations[t],
+                                       adaptation_mode=True)
+                lp = ac.get_actions_log_prob(s.actions[t])
+            torch.testing.assert_close(lp, s.actions_log_prob[t].view(-1), rtol=1e-5, atol=1e-5)
+        checked.append(True)
+        return (0.0,) * 8
+
+    r.alg.update_dagger = check
+    r.learn(1, init_at_random_ep_len=True)
+    assert checked
