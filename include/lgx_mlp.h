@@ -97,6 +97,38 @@ typedef struct lgx_ppo_head_args {
 int32_t lgx_ppo_head_forward(const lgx_ppo_head_args* args, void* stream);
 int32_t lgx_ppo_head_backward(const lgx_ppo_head_args* args, void* stream);
 
+/* ---- rollout bookkeeping (ppo.py:129-171, rollout_storage.py:87-105), one launch each */
+
+/* Up to LGX_COPY_MAX device-to-device copies in one launch (the storage writes of one
+ * rollout step). Each entry: nbytes from src to dst; 16-byte aligned entries whose size
+ * is a multiple of 16 take the vector path. */
+#define LGX_COPY_MAX 16
+typedef struct lgx_copy_desc {
+  const void* src; void* dst; int64_t nbytes;
+} lgx_copy_desc;
+int32_t lgx_copy_batch(const lgx_copy_desc* descs, int32_t n, void* stream);
+
+/* PPO.act action head (actor_critic.py:205-226 + ppo.py:141-146) for a diagonal Gaussian:
+ *   a = mean + std * eps,  logp_i = sum_j -(a-mean)^2/(2 std_j^2) - log std_j - log sqrt(2 pi)
+ * (torch.distributions.Normal.log_prob op order), written straight into the storage rows:
+ * actions [B,A], mu [B,A] (= mean), sigma [B,A] (= std broadcast), logp [B]. */
+typedef struct lgx_act_head_args {
+  const float* mean; const float* std; const float* eps;
+  float* actions; float* mu; float* sigma; float* logp;
+  int32_t B, A;
+} lgx_act_head_args;
+int32_t lgx_act_head(const lgx_act_head_args* args, void* stream);
+
+/* PPO.process_env_step (ppo.py:156-171) into the storage rows of this step:
+ *   rewards_out[i] = rewards[i] + gamma * (values[i] * time_outs[i])   (time_outs may be NULL)
+ *   dones_out[i] = dones[i] (uint8), values_out[i] = values[i]. */
+typedef struct lgx_transition_args {
+  const float* rewards; const uint8_t* dones; const uint8_t* time_outs; const float* values;
+  float* rewards_out; uint8_t* dones_out; float* values_out;
+  float gamma; int32_t B;
+} lgx_transition_args;
+int32_t lgx_store_transition(const lgx_transition_args* args, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -20,6 +20,7 @@
 //   weight grad split-K partials to a workspace + the bias gradient (column sums of dY,
 //   taken from the unsplit fp32 values), reduced in fixed order by splitk_reduce.
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -677,6 +678,63 @@ static int tile_n(int N) {
   return N > 128 ? 128 : 64;
 }
 
+// ================================================================ rollout bookkeeping
+namespace lgxm {
+
+struct CopyBatch {
+  lgx_copy_desc d[LGX_COPY_MAX];
+  int32_t n;
+};
+
+// blockIdx.y = entry; blocks stride over the entry's 16-byte chunks
+__global__ __launch_bounds__(256) void copy_batch_kernel(CopyBatch cb) {
+  const lgx_copy_desc& d = cb.d[blockIdx.y];
+  const bool vec = ((reinterpret_cast<uintptr_t>(d.src) | reinterpret_cast<uintptr_t>(d.dst) | (uintptr_t)d.nbytes) &
+                    15) == 0;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  if (vec) {
+    const int64_t n16 = d.nbytes >> 4;
+    const float4* __restrict__ s = reinterpret_cast<const float4*>(d.src);
+    float4* __restrict__ t = reinterpret_cast<float4*>(d.dst);
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) t[i] = s[i];
+  } else {
+    const uint8_t* __restrict__ s = reinterpret_cast<const uint8_t*>(d.src);
+    uint8_t* __restrict__ t = reinterpret_cast<uint8_t*>(d.dst);
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < d.nbytes; i += stride) t[i] = s[i];
+  }
+}
+
+__global__ __launch_bounds__(256) void act_head_kernel(lgx_act_head_args p) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= p.B) return;
+  const float c = 0.91893853320467274178f;  // log(sqrt(2 pi))
+  float lp = 0.0f;
+  for (int j = 0; j < p.A; ++j) {
+    const size_t k = (size_t)i * p.A + j;
+    const float m = p.mean[k], sd = p.std[j];
+    const float a = m + sd * p.eps[k];
+    const float d = a - m;
+    lp += -(d * d) / (2.0f * (sd * sd)) - logf(sd) - c;
+    p.actions[k] = a;
+    p.mu[k] = m;
+    p.sigma[k] = sd;
+  }
+  p.logp[i] = lp;
+}
+
+__global__ __launch_bounds__(256) void transition_kernel(lgx_transition_args p) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= p.B) return;
+  const float v = p.values[i];
+  float r = p.rewards[i];
+  if (p.time_outs) r = r + p.gamma * (v * (float)p.time_outs[i]);
+  p.rewards_out[i] = r;
+  p.dones_out[i] = p.dones[i] ? 1 : 0;
+  p.values_out[i] = v;
+}
+
+}  // namespace lgxm
+
 extern "C" {
 
 int32_t lgx_mlp_abi_version(void) { return LGX_MLP_ABI_VERSION; }
@@ -802,6 +860,48 @@ int32_t lgx_gemm(const lgx_gemm_args* a, void* stream) {
     if (e != hipSuccess) return fail(hipGetErrorString(e));
   }
   return 0;
+}
+
+int32_t lgx_copy_batch(const lgx_copy_desc* descs, int32_t n, void* stream) {
+  if (n < 0 || n > LGX_COPY_MAX || (n > 0 && !descs)) return fail("lgx_copy_batch: 0 <= n <= LGX_COPY_MAX");
+  if (n == 0) return 0;
+  lgxm::CopyBatch cb;
+  int64_t most = 0;
+  for (int i = 0; i < n; ++i) {
+    if (descs[i].nbytes < 0 || (descs[i].nbytes > 0 && (!descs[i].src || !descs[i].dst)))
+      return fail("lgx_copy_batch: bad entry");
+    cb.d[i] = descs[i];
+    most = descs[i].nbytes > most ? descs[i].nbytes : most;
+  }
+  cb.n = n;
+  if (most == 0) return 0;
+  // enough blocks per entry to stream the largest at full rate (16 B per thread per pass)
+  const int64_t chunks = (most + 15) / 16;
+  const unsigned bx = (unsigned)std::min<int64_t>((chunks + 255) / 256, 1024);
+  hipLaunchKernelGGL(lgxm::copy_batch_kernel, dim3(bx, (unsigned)n), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     cb);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : fail(hipGetErrorString(e));
+}
+
+int32_t lgx_act_head(const lgx_act_head_args* a, void* stream) {
+  if (!a || !a->mean || !a->std || !a->eps || !a->actions || !a->mu || !a->sigma || !a->logp || a->B < 0 || a->A <= 0)
+    return fail("lgx_act_head: bad arguments");
+  if (a->B == 0) return 0;
+  hipLaunchKernelGGL(lgxm::act_head_kernel, dim3((a->B + 255) / 256), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     *a);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : fail(hipGetErrorString(e));
+}
+
+int32_t lgx_store_transition(const lgx_transition_args* a, void* stream) {
+  if (!a || !a->rewards || !a->dones || !a->values || !a->rewards_out || !a->dones_out || !a->values_out || a->B < 0)
+    return fail("lgx_store_transition: bad arguments");
+  if (a->B == 0) return 0;
+  hipLaunchKernelGGL(lgxm::transition_kernel, dim3((a->B + 255) / 256), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), *a);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : fail(hipGetErrorString(e));
 }
 
 }  // extern "C"

@@ -276,16 +276,46 @@ class PPO:
         (t.observations, t.privileged_observations, t.critic_observations, t.true_estimated_observations,
          t.scan_observations) = self.storage.record_observations(obs, privileged_obs, critic_obs, true_estimated_obs,
                                                                  scan_obs)
-        t.actions = self.actor_critic.act(obs, privileged_obs, estimated_obs, scan_obs, adaptation_mode).detach()
-        t.values = self.actor_critic.evaluate(critic_obs).detach()
-        t.actions_log_prob = self.actor_critic.get_actions_log_prob(t.actions).detach()
-        t.action_mean = self.actor_critic.action_mean.detach()
-        t.action_sigma = self.actor_critic.action_std.detach()
+        ac = self.actor_critic
+        if self._gpu_rollout():
+            # one HIP kernel samples a = mu + std * eps and writes actions, mu, sigma and the
+            # Normal log-prob straight into this step's storage rows (lgx_act_head)
+            s, k = self.storage, self.storage.step
+            with torch.no_grad():
+                mean = ac._actor_mean(obs, privileged_obs, estimated_obs, scan_obs, adaptation_mode)
+                eps = torch.randn_like(mean)
+                hip_mlp.act_head(mean, ac.std.detach(), eps, s.actions[k], s.mu[k], s.sigma[k], s.actions_log_prob[k])
+                t.values = ac.evaluate(critic_obs)
+            t.actions, t.action_mean, t.action_sigma = s.actions[k], s.mu[k], s.sigma[k]
+            t.actions_log_prob = s.actions_log_prob[k].view(-1)
+            return t.actions
+        t.actions = ac.act(obs, privileged_obs, estimated_obs, scan_obs, adaptation_mode).detach()
+        t.values = ac.evaluate(critic_obs).detach()
+        t.actions_log_prob = ac.get_actions_log_prob(t.actions).detach()
+        t.action_mean = ac.action_mean.detach()
+        t.action_sigma = ac.action_std.detach()
         return t.actions
+
+    def _gpu_rollout(self):
+        return str(self.device).startswith("cuda")
 
     def process_env_step(self, rewards, dones, infos):
         """ppo.py:156-171: time-out bootstrap r += γ V(s) on timed-out envs."""
         t = self.transition
+        if self._gpu_rollout():
+            # bootstrap + rewards/dones/values rows in one HIP kernel (lgx_store_transition)
+            s, k = self.storage, self.storage.step
+            if k >= s.num_transitions_per_env:
+                raise AssertionError("Rollout buffer overflow")
+            to = infos.get("time_outs")
+            b = lambda x: x.view(torch.uint8) if x.dtype == torch.bool else x.to(torch.uint8)  # noqa: E731
+            hip_mlp.store_transition(rewards.contiguous(), b(dones), None if to is None else b(to),
+                                     t.values.reshape(-1), s.rewards[k].view(-1), s.dones[k].view(-1),
+                                     s.values[k].view(-1), self.gamma)
+            s.step += 1
+            t.clear()
+            self.actor_critic.reset(dones)
+            return
         t.rewards = rewards.clone()
         t.dones = dones
         if "time_outs" in infos:

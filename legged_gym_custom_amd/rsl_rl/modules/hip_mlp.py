@@ -23,7 +23,9 @@ _lib = None
 ABI_VERSION = 1
 EPI_BIAS, EPI_ELU, EPI_DELU, EPI_ACCUM = 1, 2, 4, 8
 EXPORTED = ["lgx_mlp_abi_version", "lgx_mlp_sizeof_gemm_args", "lgx_mlp_pick_split", "lgx_gemm",
-            "lgx_mlp_last_error", "lgx_adam_step", "lgx_ppo_head_forward", "lgx_ppo_head_backward"]
+            "lgx_mlp_last_error", "lgx_adam_step", "lgx_ppo_head_forward", "lgx_ppo_head_backward",
+            "lgx_copy_batch", "lgx_act_head", "lgx_store_transition"]
+COPY_MAX = 16
 
 
 class GemmArgs(C.Structure):
@@ -44,6 +46,23 @@ class HeadArgs(C.Structure):
                [("B", C.c_int32), ("A", C.c_int32), ("clip", C.c_float), ("clipped_value", C.c_int32),
                 ("out", C.c_void_p), ("g", C.c_void_p), ("dmu", C.c_void_p), ("dvalue", C.c_void_p),
                 ("dstd", C.c_void_p), ("ws", C.c_void_p), ("counter", C.c_void_p)]
+
+
+class CopyDesc(C.Structure):
+    """Mirror of lgx_copy_desc."""
+    _fields_ = [("src", C.c_void_p), ("dst", C.c_void_p), ("nbytes", C.c_int64)]
+
+
+class ActHeadArgs(C.Structure):
+    """Mirror of lgx_act_head_args."""
+    _fields_ = [(n, C.c_void_p) for n in ("mean", "std", "eps", "actions", "mu", "sigma", "logp")] + \
+               [("B", C.c_int32), ("A", C.c_int32)]
+
+
+class TransitionArgs(C.Structure):
+    """Mirror of lgx_transition_args."""
+    _fields_ = [(n, C.c_void_p) for n in ("rewards", "dones", "time_outs", "values", "rewards_out", "dones_out",
+                                          "values_out")] + [("gamma", C.c_float), ("B", C.c_int32)]
 
 
 class MlpLibError(RuntimeError):
@@ -70,6 +89,12 @@ def lib():
     L.lgx_ppo_head_backward.restype = C.c_int32
     L.lgx_adam_step.argtypes = [vp, vp, vp, vp, C.c_int64, vp, f32, f32, f32, f32, vp, vp, vp]
     L.lgx_adam_step.restype = C.c_int32
+    L.lgx_copy_batch.argtypes = [vp, C.c_int32, vp]
+    L.lgx_copy_batch.restype = C.c_int32
+    L.lgx_act_head.argtypes = [vp, vp]
+    L.lgx_act_head.restype = C.c_int32
+    L.lgx_store_transition.argtypes = [vp, vp]
+    L.lgx_store_transition.restype = C.c_int32
     if L.lgx_mlp_abi_version() != ABI_VERSION:
         raise MlpLibError("liblgx_mlp ABI version mismatch; rebuild")
     L.lgx_mlp_sizeof_gemm_args.restype = C.c_int32
@@ -93,6 +118,45 @@ def _run(args):
 
 def _rowmajor(t):
     return t if t.stride(-1) == 1 else t.contiguous()
+
+
+def _stream():
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _check(rc, what):
+    if rc != 0:
+        raise MlpLibError(f"{what}: " + lib().lgx_mlp_last_error().decode())
+
+
+def copy_batch(dsts, srcs):
+    """dst.copy_(src) for each pair (same dtype, contiguous, on the HIP device) in one launch."""
+    descs = (CopyDesc * COPY_MAX)()
+    n = 0
+    for d, x in zip(dsts, srcs):
+        if not (d.is_contiguous() and x.is_contiguous()) or d.dtype != x.dtype or d.numel() != x.numel():
+            raise MlpLibError("copy_batch: contiguous tensors of equal dtype and size only")
+        if n == COPY_MAX:
+            _check(lib().lgx_copy_batch(descs, n, _stream()), "lgx_copy_batch")
+            n = 0
+        descs[n].src, descs[n].dst, descs[n].nbytes = x.data_ptr(), d.data_ptr(), x.numel() * x.element_size()
+        n += 1
+    _check(lib().lgx_copy_batch(descs, n, _stream()), "lgx_copy_batch")
+
+
+def act_head(mean, std, eps, actions, mu, sigma, logp):
+    """a = mean + std * eps and the Normal log-prob row sums, written into storage rows."""
+    B, A = mean.shape
+    args = ActHeadArgs(mean.data_ptr(), std.data_ptr(), eps.data_ptr(), actions.data_ptr(), mu.data_ptr(),
+                       sigma.data_ptr(), logp.data_ptr(), B, A)
+    _check(lib().lgx_act_head(C.byref(args), _stream()), "lgx_act_head")
+
+
+def store_transition(rewards, dones, time_outs, values, rewards_out, dones_out, values_out, gamma):
+    args = TransitionArgs(rewards.data_ptr(), dones.data_ptr(), None if time_outs is None else time_outs.data_ptr(),
+                          values.data_ptr(), rewards_out.data_ptr(), dones_out.data_ptr(), values_out.data_ptr(),
+                          float(gamma), rewards.shape[0])
+    _check(lib().lgx_store_transition(C.byref(args), _stream()), "lgx_store_transition")
 
 
 def adam_step(p, g, m, v, step, lr, beta1, beta2, eps, grad_scale=None):

@@ -149,3 +149,44 @@ def test_ppo_head_matches_torch_autograd(clipped):
     torch.testing.assert_close(m32.grad.double(), m64.grad, rtol=1e-4, atol=1e-8)
     torch.testing.assert_close(v32.grad.double(), v64.grad, rtol=1e-4, atol=1e-8)
     torch.testing.assert_close(s32.grad.double(), s64.grad, rtol=1e-4, atol=1e-7)
+
+
+def test_rollout_bookkeeping_kernels_match_torch():
+    """lgx_copy_batch / lgx_act_head / lgx_store_transition (the rollout step's storage
+    writes, ppo.py:129-171) against the torch ops they replace."""
+    import torch
+    from legged_gym_custom_amd.rsl_rl.modules import hip_mlp
+    g = torch.Generator(device="cuda").manual_seed(0)
+    B, A = 1000, 12
+    # batched copies, incl. an unaligned byte-sized entry
+    srcs = [torch.randn(B, n, device="cuda", generator=g) for n in (572, 29, 736, 3, 132)]
+    srcs.append(torch.randint(0, 255, (37,), device="cuda", dtype=torch.uint8, generator=g))
+    dsts = [torch.empty_like(x) for x in srcs]
+    hip_mlp.copy_batch(dsts, srcs)
+    for d, x in zip(dsts, srcs):
+        assert torch.equal(d, x)
+    # action head == Normal(mean, std) sample with the same eps + log_prob
+    mean = torch.randn(B, A, device="cuda", generator=g)
+    std = torch.rand(A, device="cuda", generator=g) + 0.2
+    eps = torch.randn(B, A, device="cuda", generator=g)
+    act, mu, sig, lp = (torch.empty(B, A, device="cuda"), torch.empty(B, A, device="cuda"),
+                        torch.empty(B, A, device="cuda"), torch.empty(B, 1, device="cuda"))
+    hip_mlp.act_head(mean, std, eps, act, mu, sig, lp)
+    want_a = mean + std * eps
+    dist = torch.distributions.Normal(mean, mean * 0.0 + std)
+    torch.testing.assert_close(act, want_a, rtol=0, atol=0)
+    torch.testing.assert_close(mu, mean, rtol=0, atol=0)
+    torch.testing.assert_close(sig, std.expand(B, A), rtol=0, atol=0)
+    torch.testing.assert_close(lp.view(-1), dist.log_prob(want_a).sum(-1), rtol=1e-6, atol=1e-5)
+    # transition: r + gamma * V * time_out
+    r = torch.randn(B, device="cuda", generator=g)
+    v = torch.randn(B, 1, device="cuda", generator=g)
+    done = torch.rand(B, device="cuda", generator=g) < 0.2
+    to = done & (torch.rand(B, device="cuda", generator=g) < 0.5)
+    ro, do_, vo = torch.empty(B, 1, device="cuda"), torch.empty(B, 1, device="cuda", dtype=torch.uint8), \
+        torch.empty(B, 1, device="cuda")
+    hip_mlp.store_transition(r, done.view(torch.uint8), to.view(torch.uint8), v.view(-1), ro.view(-1), do_.view(-1),
+                             vo.view(-1), 0.99)
+    want_r = r + 0.99 * torch.squeeze(v * to.unsqueeze(1).float(), 1)
+    torch.testing.assert_close(ro.view(-1), want_r, rtol=0, atol=0)
+    assert torch.equal(do_.view(-1).bool(), done) and torch.equal(vo, v)
