@@ -6,11 +6,14 @@
 // and every product is lo*hi + hi*lo + hi*hi accumulated in fp32 (~2^-16 relative).
 //
 // Operand staging ("stager" modes) goes through registers — the split needs them anyway —
-// so every global layout lands in the same LDS image [row = m or n][k] (k contiguous,
-// 80-B row pitch: conflict-free ds_read_b128 fragment reads):
-//   KS/KV  k-contiguous rows, 8 consecutive k per lane (KV: two float4 loads)
-//   MS     m/n-contiguous, one row per lane, 8 k (coalesced 4-B lanes)
-//   MV     m/n-contiguous, float4 along m/n: a lane loads a 4-row x (ROWS/32)-k block
+// so every global layout lands in the same LDS image [row = m or n][k] (k contiguous):
+//   KV  k-contiguous rows, 8 consecutive k per lane (two float4 loads)
+//   MV  m/n-contiguous, float4 along m/n: a lane loads a 4-row x (ROWS/32)-k block
+// Vector loads need only 4-B alignment (global_load_dwordx4 on gfx950), so odd leading
+// dimensions (the actor's 627-wide input) stay vectorised. The LDS image has 64-B rows
+// (32 bf16) with rows and 16-B chunks swizzled (lds_off) so that the fragment reads
+// (ds_read_b128), the KV stores (ds_write_b128) and the MV stores (ds_write_b64/_b32) are
+// all conflict-free under the gfx950 bank rules (MI355X_MICROARCH.md §LDS).
 // Pipeline: double-buffered LDS; two register sets, so a K step's global loads are
 // issued two steps before they are staged; one barrier per step.
 // Grid: 1-D, XCD-aware — each XCD gets a contiguous run of logical tiles (n fastest),
@@ -35,9 +38,19 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 namespace lgxm {
 
 constexpr int BM = 128, BKS = 32, NT = 256;
-constexpr int PITCH = BKS + 8;           // bf16 per LDS row (80 B)
+constexpr int PITCH = BKS;               // bf16 per LDS row (64 B, swizzled: lds_off)
 constexpr int A_ELEMS = BM * PITCH;      // one A image (hi or lo)
-enum Mode { KS = 0, KV = 1, MS = 2, MV = 3 };
+enum Mode { KV = 1, MV = 3, MVE = 4 };  // MVE: MV for a row count that is not a multiple of 4
+
+typedef float f32x4u __attribute__((ext_vector_type(4), aligned(4)));  // 4-B aligned float4
+
+// bf16 offset of 16-B chunk c (0..3) of row r in an LDS image: adjacent rows swap when
+// bit 2 of r is set (rows 4 apart land on opposite bank halves: MV stores), and the chunk
+// index is XORed with bits 1 and 3 of the physical row (ds_read_b128 lane groups).
+__device__ __forceinline__ int lds_off(int r, int c) {
+  const int pr = r ^ ((r >> 2) & 1);
+  return pr * PITCH + 8 * (c ^ (((pr >> 1) & 1) | (((pr >> 3) & 1) << 1)));
+}
 
 struct Params {
   const float* A; int64_t lda;
@@ -51,7 +64,7 @@ struct Params {
   int tiles_m, tiles_n, tiles;           // logical tile grid (per split) and total incl. splits
   float* ws;
   float* colsum_ws;
-  int c_vec, act_vec, ws_vec;            // row-aligned float4 access allowed for C / act / ws
+  int ws_vec;                            // N % 4 == 0 (float4 runs of the flat workspace)
 };
 
 __device__ __forceinline__ void split8(const float* v, bf16x8& h, bf16x8& l) {
@@ -67,9 +80,12 @@ __device__ __forceinline__ void split8(const float* v, bf16x8& h, bf16x8& l) {
 template <int MODE, int ROWS>
 struct Stager {
   static constexpr int R = ROWS / 8;
-  static constexpr int T = ROWS / 64;          // 8-k tasks per thread (KS/KV/MS)
-  static constexpr int KG = ROWS / 32;         // k per float4 row (MV)
-  static constexpr int RG = ROWS / 4;          // 4-row groups (MV)
+  static constexpr int T = ROWS / 64;          // 8-k tasks per thread (KV)
+  static constexpr int KG = ROWS / 32;         // k per thread (MV)
+  static constexpr int NKQ = BKS / KG;         // k groups per step (MV): 8 or 16
+  // MV thread map: kq = tid % NKQ (k group), rg = tid / NKQ (4-row group): a wave's load
+  // instruction covers NKQ source rows (k) x 64 B or more, and each store's NKQ lanes fill
+  // one 64-B LDS row
 
   // Rows past the M/N edge are clamped to a valid row (their products only reach outputs
   // that are never stored), so loads stay vectorised at the edges; KGUARD (the last,
@@ -77,65 +93,68 @@ struct Stager {
   template <bool KGUARD>
   __device__ __forceinline__ static void load(const float* __restrict__ p, int64_t ld, int row0, int rows, int k0,
                                               int kend, int tid, float (&v)[R]) {
-    if (MODE == KS || MODE == KV) {
+    if (MODE == KV) {
 #pragma unroll
       for (int t = 0; t < T; ++t) {
         const int idx = tid + t * NT, r = idx >> 2, g = idx & 3;
         const int row = min(row0 + r, rows - 1), k = k0 + g * 8;
         const float* q = p + (int64_t)row * ld + k;
         float* o = v + t * 8;
-        if (!KGUARD && MODE == KV) {
-          const float4 x0 = *reinterpret_cast<const float4*>(q);
-          const float4 x1 = *reinterpret_cast<const float4*>(q + 4);
+        if (!KGUARD) {
+          const f32x4u x0 = *reinterpret_cast<const f32x4u*>(q);
+          const f32x4u x1 = *reinterpret_cast<const f32x4u*>(q + 4);
           o[0] = x0.x; o[1] = x0.y; o[2] = x0.z; o[3] = x0.w;
           o[4] = x1.x; o[5] = x1.y; o[6] = x1.z; o[7] = x1.w;
         } else {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) o[j] = (!KGUARD || k + j < kend) ? q[j] : 0.f;
+          for (int j = 0; j < 8; ++j) o[j] = k + j < kend ? q[j] : 0.f;
         }
       }
-    } else if (MODE == MS) {
+    } else {  // MV / MVE
+      const int kq = tid % NKQ, rg = tid / NKQ;
+      const int k = k0 + kq * KG;
+      if (MODE == MV || row0 + ROWS <= rows) {
+        // MV: rows % 4 == 0 (host), so a 4-row group is all valid or all past the edge;
+        // MVE: an interior tile (a block-uniform branch)
+        const int row = min(row0 + rg * 4, rows - 4);
 #pragma unroll
-      for (int t = 0; t < T; ++t) {
-        const int idx = tid + t * NT, r = idx % ROWS, g = idx / ROWS;
-        const int row = min(row0 + r, rows - 1), k = k0 + g * 8;
-        const float* q = p + (int64_t)k * ld + row;
+        for (int kk = 0; kk < KG; ++kk) {
+          if (!KGUARD || k + kk < kend) {
+            const f32x4u x = *reinterpret_cast<const f32x4u*>(p + (int64_t)(k + kk) * ld + row);
+            v[kk * 4 + 0] = x.x; v[kk * 4 + 1] = x.y; v[kk * 4 + 2] = x.z; v[kk * 4 + 3] = x.w;
+          } else {
+            v[kk * 4 + 0] = v[kk * 4 + 1] = v[kk * 4 + 2] = v[kk * 4 + 3] = 0.f;
+          }
+        }
+      } else {  // MVE edge tile: per-row loads, clamped
+        const int row = row0 + rg * 4;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[t * 8 + j] = (!KGUARD || k + j < kend) ? q[(int64_t)j * ld] : 0.f;
-      }
-    } else {  // MV: rows % 4 == 0 (host), so a 4-row group is all valid or all past the edge
-      const int rg = tid % RG, kq = tid / RG;
-      const int row = min(row0 + rg * 4, rows - 4), k = k0 + kq * KG;
+        for (int kk = 0; kk < KG; ++kk) {
+          const float* q = p + (int64_t)(k + kk) * ld;
 #pragma unroll
-      for (int kk = 0; kk < KG; ++kk) {
-        if (!KGUARD || k + kk < kend) {
-          const float4 x = *reinterpret_cast<const float4*>(p + (int64_t)(k + kk) * ld + row);
-          v[kk * 4 + 0] = x.x; v[kk * 4 + 1] = x.y; v[kk * 4 + 2] = x.z; v[kk * 4 + 3] = x.w;
-        } else {
-          v[kk * 4 + 0] = v[kk * 4 + 1] = v[kk * 4 + 2] = v[kk * 4 + 3] = 0.f;
+          for (int e = 0; e < 4; ++e) v[kk * 4 + e] = (!KGUARD || k + kk < kend) ? q[min(row + e, rows - 1)] : 0.f;
         }
       }
     }
   }
 
   __device__ __forceinline__ static void store(__bf16* hi, __bf16* lo, int tid, const float (&v)[R]) {
-    if (MODE != MV) {
+    if (MODE == KV) {
 #pragma unroll
       for (int t = 0; t < T; ++t) {
-        const int idx = tid + t * NT;
-        int r, g;
-        if (MODE == MS) { r = idx % ROWS; g = idx / ROWS; }
-        else { r = idx >> 2; g = idx & 3; }
+        const int idx = tid + t * NT, r = idx >> 2, g = idx & 3;
         bf16x8 h, l;
         split8(v + t * 8, h, l);
-        *reinterpret_cast<bf16x8*>(hi + r * PITCH + g * 8) = h;
-        *reinterpret_cast<bf16x8*>(lo + r * PITCH + g * 8) = l;
+        const int off = lds_off(r, g);
+        *reinterpret_cast<bf16x8*>(hi + off) = h;
+        *reinterpret_cast<bf16x8*>(lo + off) = l;
       }
     } else {
-      const int rg = tid % RG, kq = tid / RG;
+      const int kq = tid % NKQ, rg = tid / NKQ;
+      const int kb = kq * KG;  // first k of this thread inside the step
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int off = (rg * 4 + e) * PITCH + kq * KG;
+        const int off = lds_off(rg * 4 + e, kb >> 3) + (kb & 7);
         if (KG == 4) {
           bf16x4 h, l;
 #pragma unroll
@@ -163,18 +182,12 @@ struct Stager {
     }
   }
 
-  // Row sums of the A tile (bias gradient): this thread's contribution per owned row.
-  // MS: one row (tid % ROWS), slot tid / ROWS; MV: rows 4*rg + e, slot kq.
+  // Row sums of the A tile (bias gradient), MV/MVE only: rows 4*rg + e, slot kq.
   __device__ __forceinline__ static void colsum(const float (&v)[R], float (&cs)[4]) {
-    if (MODE == MS) {
 #pragma unroll
-      for (int j = 0; j < R; ++j) cs[0] += v[j];
-    } else if (MODE == MV) {
+    for (int kk = 0; kk < KG; ++kk)
 #pragma unroll
-      for (int kk = 0; kk < KG; ++kk)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) cs[e] += v[kk * 4 + e];
-    }
+      for (int e = 0; e < 4; ++e) cs[e] += v[kk * 4 + e];
   }
 };
 
@@ -214,7 +227,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(Params p) {
     __bf16* base = lds + buf * STAGE;
     SA::store(base, base + A_ELEMS, tid, va);
     SB::store(base + 2 * A_ELEMS, base + 2 * A_ELEMS + B_ELEMS, tid, vb);
-    if (COLSUM) SA::colsum(va, csum);
+    if constexpr (COLSUM) SA::colsum(va, csum);
   };
 
   f32x4 acc[4][NJ];
@@ -223,7 +236,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(Params p) {
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int fr = lane & 15, fk = (lane >> 4) * 8;
+  const int fr = lane & 15, fc = lane >> 4;
   auto compute = [&](int buf) {
     const __bf16* base = lds + buf * STAGE;
     const __bf16* ahi = base;
@@ -233,13 +246,13 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(Params p) {
     bf16x8 bh[NJ], bl[NJ];
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
-      const int off = (wn + j * 16 + fr) * PITCH + fk;
+      const int off = lds_off(wn + j * 16 + fr, fc);
       bh[j] = *reinterpret_cast<const bf16x8*>(bhi + off);
       bl[j] = *reinterpret_cast<const bf16x8*>(blo + off);
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int off = (wm + i * 16 + fr) * PITCH + fk;
+      const int off = lds_off(wm + i * 16 + fr, fc);
       const bf16x8 ah = *reinterpret_cast<const bf16x8*>(ahi + off);
       const bf16x8 al = *reinterpret_cast<const bf16x8*>(alo + off);
 #pragma unroll
@@ -273,16 +286,13 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(Params p) {
 
   float* cs = reinterpret_cast<float*>(lds);
   // bias gradient partial: this block's A rows summed over its K range (n-tile 0 only)
-  if (COLSUM) {
+  if constexpr (COLSUM) {
     if (tn == 0) {
-      constexpr int SLOTS = AM == MV ? NT / (BM / 4) : NT / BM;
-      if (AM == MV) {
-        const int rg = tid % (BM / 4), kq = tid / (BM / 4);
+      static_assert(AM == MV || AM == MVE, "colsum needs the m-contiguous A stager");
+      constexpr int SLOTS = SA::NKQ;
+      const int kq = tid % SLOTS, rg = tid / SLOTS;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) cs[kq * BM + rg * 4 + e] = csum[e];
-      } else {
-        cs[(tid / BM) * BM + tid % BM] = csum[0];
-      }
+      for (int e = 0; e < 4; ++e) cs[kq * BM + rg * 4 + e] = csum[e];
       __syncthreads();
       if (tid < BM) {
         float v = 0.f;
@@ -309,8 +319,9 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(Params p) {
       const int idx = tid + it * NT;
       const int m = m0 + idx / CH, n = n0 + (idx % CH) * 4;
       const float* ap = p.act + (int64_t)m * p.ld_act + n;
-      if (m < p.M && n + 4 <= p.N && p.act_vec) {
-        yv[it] = *reinterpret_cast<const float4*>(ap);
+      if (m < p.M && n + 4 <= p.N) {
+        const f32x4u y = *reinterpret_cast<const f32x4u*>(ap);
+        yv[it] = make_float4(y.x, y.y, y.z, y.w);
       } else {
         float y[4];
 #pragma unroll
@@ -329,7 +340,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(Params p) {
   __syncthreads();
   float* dst = part ? p.ws + (int64_t)z * p.M * p.N : p.C;
   const int64_t ldd = part ? p.N : p.ldc;
-  const bool dvec = part ? p.ws_vec : p.c_vec;
+
   const bool accum = !part && (p.epi & LGX_EPI_ACCUM);
 #pragma unroll
   for (int it = 0; it < IT; ++it) {
@@ -356,13 +367,10 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(Params p) {
       }
     }
     float* d = dst + (int64_t)m * ldd + n;
-    if (full && dvec) {
-      float4 o = make_float4(v[0], v[1], v[2], v[3]);
-      if (accum) {
-        const float4 q = *reinterpret_cast<const float4*>(d);
-        o.x += q.x; o.y += q.y; o.z += q.z; o.w += q.w;
-      }
-      *reinterpret_cast<float4*>(d) = o;
+    if (full) {
+      f32x4u o = {v[0], v[1], v[2], v[3]};
+      if (accum) o += *reinterpret_cast<const f32x4u*>(d);
+      *reinterpret_cast<f32x4u*>(d) = o;
     } else {
 #pragma unroll
       for (int e = 0; e < 4; ++e)
@@ -389,7 +397,7 @@ __global__ void splitk_reduce(Params p, float* colsum) {
   const int64_t mn = (int64_t)p.M * p.N;
   const int64_t q = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
   if (q < mn) {
-    const bool vec = (p.N % 4 == 0) && p.c_vec && p.ws_vec;
+    const bool vec = p.ws_vec;
     float v[4];
     if (vec) {
       float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a, c = a, d = a;
@@ -666,7 +674,6 @@ static int fail(const char* msg) {
   return -1;
 }
 
-static bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 static int tile_n(int N) {
   static int forced = -1;
@@ -822,34 +829,23 @@ int32_t lgx_gemm(const lgx_gemm_args* a, void* stream) {
   if (p.kchunk == 0) p.kchunk = BKS;
   p.ws = a->workspace;
   p.colsum_ws = a->colsum_ws;
-  p.c_vec = (a->ldc % 4 == 0) && aligned16(a->C);
-  p.act_vec = a->act && (a->ld_act % 4 == 0) && aligned16(a->act);
-  p.ws_vec = (a->N % 4 == 0) && (!a->workspace || aligned16(a->workspace));
+  p.ws_vec = a->N % 4 == 0;  // a float4 of the flat workspace stays inside one row
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int bn = tile_n(a->N);
-  // float4 staging needs 16-B aligned rows (k-contiguous) or 4-aligned columns (m/n-contiguous)
-  const bool va = (a->lda % 4 == 0) && aligned16(a->A) && (a->a_kcontig || a->M % 4 == 0);
-  const bool vb = (a->ldb % 4 == 0) && aligned16(a->B) && (a->b_kcontig || a->N % 4 == 0);
-  if (a->a_kcontig && !a->b_kcontig) {  // input gradient with W read in place (n-contiguous)
-    if (va && vb) launch<KV, MV, false>(p, bn, s);
-    else if (va) launch<KV, MS, false>(p, bn, s);
-    else if (vb) launch<KS, MV, false>(p, bn, s);
-    else launch<KS, MS, false>(p, bn, s);
+  const bool ma = a->M % 4 == 0, nb = a->N % 4 == 0;  // m/n-contiguous stagers: whole 4-row groups
+  if (a->a_kcontig && !a->b_kcontig) {  // input gradient, W read in place
+    if (nb) launch<KV, MV, false>(p, bn, s);
+    else launch<KV, MVE, false>(p, bn, s);
   } else if (a->a_kcontig) {
-    if (va && vb) launch<KV, KV, false>(p, bn, s);
-    else if (va) launch<KV, KS, false>(p, bn, s);
-    else if (vb) launch<KS, KV, false>(p, bn, s);
-    else launch<KS, KS, false>(p, bn, s);
+    launch<KV, KV, false>(p, bn, s);
   } else if (cs) {
-    if (va && vb) launch<MV, MV, true>(p, bn, s);
-    else if (va) launch<MV, MS, true>(p, bn, s);
-    else if (vb) launch<MS, MV, true>(p, bn, s);
-    else launch<MS, MS, true>(p, bn, s);
+    if (ma && nb) launch<MV, MV, true>(p, bn, s);
+    else if (ma) launch<MV, MVE, true>(p, bn, s);
+    else if (nb) launch<MVE, MV, true>(p, bn, s);
+    else launch<MVE, MVE, true>(p, bn, s);
   } else {
-    if (va && vb) launch<MV, MV, false>(p, bn, s);
-    else if (va) launch<MV, MS, false>(p, bn, s);
-    else if (vb) launch<MS, MV, false>(p, bn, s);
-    else launch<MS, MS, false>(p, bn, s);
+    if (ma && nb) launch<MV, MV, false>(p, bn, s);
+    else launch<MVE, MVE, false>(p, bn, s);
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(hipGetErrorString(e));

@@ -354,7 +354,7 @@ class PPO:
             # reference evaluates the same encoder on the same input twice, ppo.py:190,204)
             priv_latent = ac.privileged_encoder(priv_b)
             scan_latent = ac.scan_encoder(scan_b)
-            mu_b = ac.actor(torch.cat((obs_b, priv_latent, scan_latent, est_b), dim=-1))  # TRUE est obs (Q12)
+            mu_b = ac.actor_forward(obs_b, priv_latent, scan_latent, est_b)  # TRUE est obs (Q12)
             value_b = ac.evaluate(critic_b)
             surrogate_loss, value_loss, entropy_mean, kl_mean = hip_mlp.ppo_head(
                 mu_b, value_b, ac.std, actions_b, old_logp_b, adv_b, target_values_b, returns_b, old_mu_b, old_sigma_b,

@@ -76,7 +76,14 @@ class ActorCritic(nn.Module):
     def _actor_mean(self, obs_buf, privileged_obs_buf, estimated_obs_buf, scan_obs_buf, adaptation_mode):
         latent = self.get_latent(obs_buf, privileged_obs_buf, adaptation_mode)
         scan_latent = self.scan_encoder(scan_obs_buf)
-        return self.actor(torch.cat((obs_buf, latent, scan_latent, estimated_obs_buf), dim=-1))
+        return self.actor_forward(obs_buf, latent, scan_latent, estimated_obs_buf)
+
+    def actor_forward(self, obs_buf, latent, scan_latent, estimated_obs_buf):
+        """actor(cat(obs, latent, scan latent, est)) (actor_critic.py:79); on the HIP device
+        the input gradient covers only the latent columns (obs/est carry none)."""
+        parts = (obs_buf, latent, scan_latent, estimated_obs_buf)
+        fp = getattr(self.actor, "forward_parts", None)
+        return fp(parts) if fp is not None else self.actor(torch.cat(parts, dim=-1))
 
     def update_distribution(self, obs_buf, privileged_obs_buf, estimated_obs_buf, scan_obs_buf, adaptation_mode=False):
         mean = self._actor_mean(obs_buf, privileged_obs_buf, estimated_obs_buf, scan_obs_buf, adaptation_mode)

@@ -245,8 +245,16 @@ def _grad_of(p):
 
 
 class _MLPFunction(torch.autograd.Function):
+    """The whole chain as one autograd node. The chain input is the concatenation of
+    `nparts` tensors (the actor's [obs | latent | scan latent | est], actor_critic.py:79):
+    the concatenation is built here, and the first layer's input gradient is computed only
+    for the column span of the parts that need one (the actor's 55 latent columns, not
+    its 627 — obs and est carry no gradient)."""
+
     @staticmethod
-    def forward(ctx, x, elu_flags, *wb):
+    def forward(ctx, nparts, elu_flags, *args):
+        parts, wb = args[:nparts], args[nparts:]
+        x = parts[0] if nparts == 1 else torch.cat(parts, dim=-1)
         n = len(elu_flags)
         outs = []
         h = x
@@ -254,6 +262,8 @@ class _MLPFunction(torch.autograd.Function):
             h = linear_forward(h, wb[2 * i], wb[2 * i + 1], elu_flags[i])
             outs.append(h)
         ctx.elu_flags = elu_flags
+        ctx.nparts = nparts
+        ctx.widths = [t.shape[-1] for t in parts]
         ctx.params = wb  # the leaf Parameters (their .grad is written in backward)
         ctx.save_for_backward(x, *wb, *outs)
         return h
@@ -262,36 +272,50 @@ class _MLPFunction(torch.autograd.Function):
     def backward(ctx, grad_out):
         flags = ctx.elu_flags
         n = len(flags)
+        np_ = ctx.nparts
         saved = ctx.saved_tensors
         x, wb, outs = saved[0], saved[1:1 + 2 * n], saved[1 + 2 * n:]
         g = grad_out
         if flags[-1]:  # a chain ending in an activation (not built by _mlp): its ELU' on the incoming grad
             y = outs[-1]
             g = g * torch.where(y > 0, torch.ones_like(y), y + 1.0)
-        grads = [None] * (2 * n)  # W/b grads go straight into p.grad (see _grad_of)
-        dx = None
+        need = [ctx.needs_input_grad[2 + i] for i in range(np_)]
+        part_grads = [None] * np_
         for i in reversed(range(n)):
             inp = x if i == 0 else outs[i - 1]
-            if ctx.needs_input_grad[2 + 2 * i] or ctx.needs_input_grad[3 + 2 * i]:
+            if ctx.needs_input_grad[2 + np_ + 2 * i] or ctx.needs_input_grad[3 + np_ + 2 * i]:
                 linear_weight_grad(g, inp, _grad_of(ctx.params[2 * i]), _grad_of(ctx.params[2 * i + 1]),
                                    accumulate=True)
             if i > 0:
                 g = linear_input_grad(g, wb[2 * i], outs[i - 1] if flags[i - 1] else None)
-            elif ctx.needs_input_grad[0]:
-                dx = linear_input_grad(g, wb[0], None)
-        return (dx, None, *grads)
+            elif any(need):
+                # dX for the columns [lo, hi) spanning the parts that need a gradient: W read in place
+                offs = [0]
+                for w in ctx.widths:
+                    offs.append(offs[-1] + w)
+                first = need.index(True)
+                last = np_ - 1 - need[::-1].index(True)
+                lo, hi = offs[first], offs[last + 1]
+                dx = linear_input_grad(g, wb[0][:, lo:hi], None)
+                for k in range(first, last + 1):
+                    if need[k]:
+                        part_grads[k] = dx[:, offs[k] - lo:offs[k + 1] - lo]
+        return (None, None, *part_grads) + (None,) * (2 * n)
 
 
 def mlp_forward(x, weights, biases, elu_flags):
-    """Whole chain on the HIP device (autograd-aware)."""
+    """Whole chain on the HIP device (autograd-aware). `x` is a tensor, or a tuple of
+    tensors whose concatenation along the last dim is the chain input."""
+    parts = tuple(x) if isinstance(x, (tuple, list)) else (x,)
     wb = [t for pair in zip(weights, biases) for t in pair]
-    needs_graph = torch.is_grad_enabled() and (x.requires_grad or any(t.requires_grad for t in wb))
+    needs_graph = torch.is_grad_enabled() and (any(t.requires_grad for t in parts) or
+                                               any(t.requires_grad for t in wb))
     if not needs_graph:
-        h = x
+        h = parts[0] if len(parts) == 1 else torch.cat(parts, dim=-1)
         for W, b, e in zip(weights, biases, elu_flags):
             h = linear_forward(h, W, b, e)
         return h
-    return _MLPFunction.apply(x, tuple(elu_flags), *wb)
+    return _MLPFunction.apply(len(parts), tuple(elu_flags), *parts, *wb)
 
 
 class HipMLP(nn.Sequential):
@@ -321,6 +345,16 @@ class HipMLP(nn.Sequential):
             return super().forward(x)
         layers, flags = chain
         return mlp_forward(x, [m.weight for m in layers], [m.bias for m in layers], flags)
+
+    def forward_parts(self, parts):
+        """forward(torch.cat(parts, -1)); on the HIP device the concatenation happens inside
+        the chain's autograd node, and the input gradient is only formed for the parts that
+        require one."""
+        chain = self._chain() if parts[0].device.type == "cuda" else None
+        if chain is None:
+            return self.forward(torch.cat(parts, dim=-1))
+        layers, flags = chain
+        return mlp_forward(tuple(parts), [m.weight for m in layers], [m.bias for m in layers], flags)
 
 
 # ---------------------------------------------------------------------------------------

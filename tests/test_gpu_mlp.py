@@ -190,3 +190,30 @@ def test_rollout_bookkeeping_kernels_match_torch():
     want_r = r + 0.99 * torch.squeeze(v * to.unsqueeze(1).float(), 1)
     torch.testing.assert_close(ro.view(-1), want_r, rtol=0, atol=0)
     assert torch.equal(do_.view(-1).bool(), done) and torch.equal(vo, v)
+
+
+def test_forward_parts_grads_only_where_needed():
+    """actor(cat(obs, latent, scan, est)) as one node: the input gradient is formed for the
+    latent parts only, and equals the fp64 gradient of the concatenated input there."""
+    from legged_gym_custom_amd.rsl_rl.modules.support_networks import _mlp
+    torch.manual_seed(1)
+    net = _mlp(627, [512, 256, 128], 12, torch.nn.ELU()).to(dev)
+    ref = _mlp(627, [512, 256, 128], 12, torch.nn.ELU()).double()
+    ref.load_state_dict({k: v.double().cpu() for k, v in net.state_dict().items()})
+    M = 2000
+    obs = torch.randn(M, 572, device=dev)
+    lat = torch.randn(M, 20, device=dev, requires_grad=True)
+    scan = torch.randn(M, 32, device=dev, requires_grad=True)
+    est = torch.randn(M, 3, device=dev)
+    y = net.forward_parts((obs, lat, scan, est))
+    xr = torch.cat((obs, lat, scan, est), -1).detach().double().cpu().requires_grad_(True)
+    yr = torch.nn.Sequential.forward(ref, xr)
+    torch.testing.assert_close(y.double().cpu(), yr, rtol=1e-4, atol=1e-4)
+    w = torch.randn_like(y)
+    (y * w).sum().backward()
+    (yr * w.double().cpu()).sum().backward()
+    torch.testing.assert_close(lat.grad.double().cpu(), xr.grad[:, 572:592], rtol=1e-3, atol=1e-5)
+    torch.testing.assert_close(scan.grad.double().cpu(), xr.grad[:, 592:624], rtol=1e-3, atol=1e-5)
+    # parameter gradients sum ~M products each: cancellation needs an absolute slack
+    for p, pr in zip(net.parameters(), ref.parameters()):
+        torch.testing.assert_close(p.grad.double().cpu(), pr.grad, rtol=1e-3, atol=2e-3)
