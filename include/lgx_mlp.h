@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define LGX_MLP_ABI_VERSION 1
+#define LGX_MLP_ABI_VERSION 2
 
 enum {
   LGX_EPI_BIAS = 1,  /* + bias[n] */
@@ -47,6 +47,8 @@ typedef struct lgx_gemm_args {
   float* workspace;
   float* colsum;             /* optional [M]: sum_k A(m,k) (the bias gradient); needs a_kcontig = 0 */
   float* colsum_ws;          /* split_k * M floats when colsum != NULL */
+  int32_t defer_reduce;      /* split_k > 1: leave the partials in workspace/colsum_ws; the
+                                caller reduces them later with lgx_splitk_reduce_batch */
 } lgx_gemm_args;
 
 int32_t lgx_mlp_abi_version(void);
@@ -55,6 +57,20 @@ int32_t lgx_mlp_sizeof_gemm_args(void);
 /* Suggested split-K factor for an M x N x K weight-gradient GEMM. */
 int32_t lgx_mlp_pick_split(int32_t M, int32_t N, int32_t K);
 int32_t lgx_gemm(const lgx_gemm_args* args, void* stream);
+
+/* Deferred split-K reductions of several weight-gradient GEMMs in ONE launch (a whole
+ * backward pass's dW/db, rsl_rl ppo.py:262 loss.backward()): for each entry
+ *   C[m*ldc + n] (+)= sum_{z in order} ws[(z*M + m)*N + n]
+ *   colsum[m]    (+)= sum_{z in order} colsum_ws[z*M + m]          (colsum != NULL)
+ * (+= when epilogue has LGX_EPI_ACCUM). Fixed summation order: the result equals the
+ * immediate reduction of lgx_gemm bit for bit. Entries must not overlap in C / colsum. */
+#define LGX_SPLITK_MAX 24
+typedef struct lgx_splitk_desc {
+  const float* ws; const float* colsum_ws;
+  float* C; int64_t ldc; float* colsum;
+  int32_t M, N, split, epilogue;
+} lgx_splitk_desc;
+int32_t lgx_splitk_reduce_batch(const lgx_splitk_desc* descs, int32_t n, void* stream);
 const char* lgx_mlp_last_error(void);
 
 /* One Adam step over a contiguous parameter segment (fp32), replacing torch.optim.Adam's

@@ -393,57 +393,80 @@ __device__ __forceinline__ float sum_splits(const float* ws, int64_t stride, int
   return (a0 + a1) + (a2 + a3);
 }
 
-__global__ void splitk_reduce(Params p, float* colsum) {
-  const int64_t mn = (int64_t)p.M * p.N;
-  const int64_t q = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
-  if (q < mn) {
-    const bool vec = p.ws_vec;
+// One split-K reduction: item t < ceil(M*N/4) sums 4 consecutive outputs (float4 when
+// N % 4 == 0) and applies the epilogue; items past that sum one bias-gradient row each.
+__device__ __forceinline__ void splitk_item(const float* __restrict__ ws, const float* __restrict__ colsum_ws,
+                                            float* C, int64_t ldc, float* colsum, int M, int N, int split, int epi,
+                                            const float* bias, const float* act, int64_t ld_act, int64_t t) {
+  const int64_t mn = (int64_t)M * N;
+  const int64_t nq = (mn + 3) / 4;
+  if (t < nq) {
+    const int64_t q = t * 4;
     float v[4];
-    if (vec) {
+    if (N % 4 == 0) {
       float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a, c = a, d = a;
       int z = 0;
-      for (; z + 4 <= p.split; z += 4) {
-        const float4 x0 = *reinterpret_cast<const float4*>(p.ws + (z + 0) * mn + q);
-        const float4 x1 = *reinterpret_cast<const float4*>(p.ws + (z + 1) * mn + q);
-        const float4 x2 = *reinterpret_cast<const float4*>(p.ws + (z + 2) * mn + q);
-        const float4 x3 = *reinterpret_cast<const float4*>(p.ws + (z + 3) * mn + q);
+      for (; z + 4 <= split; z += 4) {
+        const float4 x0 = *reinterpret_cast<const float4*>(ws + (z + 0) * mn + q);
+        const float4 x1 = *reinterpret_cast<const float4*>(ws + (z + 1) * mn + q);
+        const float4 x2 = *reinterpret_cast<const float4*>(ws + (z + 2) * mn + q);
+        const float4 x3 = *reinterpret_cast<const float4*>(ws + (z + 3) * mn + q);
         a.x += x0.x; a.y += x0.y; a.z += x0.z; a.w += x0.w;
         b.x += x1.x; b.y += x1.y; b.z += x1.z; b.w += x1.w;
         c.x += x2.x; c.y += x2.y; c.z += x2.z; c.w += x2.w;
         d.x += x3.x; d.y += x3.y; d.z += x3.z; d.w += x3.w;
       }
-      for (; z < p.split; ++z) {
-        const float4 x = *reinterpret_cast<const float4*>(p.ws + z * mn + q);
+      for (; z < split; ++z) {
+        const float4 x = *reinterpret_cast<const float4*>(ws + z * mn + q);
         a.x += x.x; a.y += x.y; a.z += x.z; a.w += x.w;
       }
       v[0] = (a.x + b.x) + (c.x + d.x); v[1] = (a.y + b.y) + (c.y + d.y);
       v[2] = (a.z + b.z) + (c.z + d.z); v[3] = (a.w + b.w) + (c.w + d.w);
     } else {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = q + e < mn ? sum_splits(p.ws, mn, p.split, q + e) : 0.f;
+      for (int e = 0; e < 4; ++e) v[e] = q + e < mn ? sum_splits(ws, mn, split, q + e) : 0.f;
     }
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int64_t i = q + e;
       if (i >= mn) break;
-      const int m = (int)(i / p.N), n = (int)(i % p.N);
+      const int m = (int)(i / N), n = (int)(i % N);
       float x = v[e];
-      if (p.epi & LGX_EPI_BIAS) x += p.bias[n];
-      if (p.epi & LGX_EPI_ELU) x = x > 0.f ? x : expm1f(x);
-      if (p.epi & LGX_EPI_DELU) {
-        const float y = p.act[(int64_t)m * p.ld_act + n];
+      if (epi & LGX_EPI_BIAS) x += bias[n];
+      if (epi & LGX_EPI_ELU) x = x > 0.f ? x : expm1f(x);
+      if (epi & LGX_EPI_DELU) {
+        const float y = act[(int64_t)m * ld_act + n];
         x *= y > 0.f ? 1.f : y + 1.f;
       }
-      float* c = p.C + (int64_t)m * p.ldc + n;
-      *c = (p.epi & LGX_EPI_ACCUM) ? *c + x : x;
+      float* c = C + (int64_t)m * ldc + n;
+      *c = (epi & LGX_EPI_ACCUM) ? *c + x : x;
     }
+    return;
   }
-  // bias gradient: one thread per row of A beyond the M*N range
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x - (mn + 3) / 4;
-  if (colsum != nullptr && t >= 0 && t < p.M) {
-    const float x = sum_splits(p.colsum_ws, p.M, p.split, t);
-    colsum[t] = (p.epi & LGX_EPI_ACCUM) ? colsum[t] + x : x;
+  const int64_t r = t - nq;  // bias gradient: one row of A
+  if (colsum != nullptr && r < M) {
+    const float x = sum_splits(colsum_ws, M, split, r);
+    colsum[r] = (epi & LGX_EPI_ACCUM) ? colsum[r] + x : x;
   }
+}
+
+__global__ void splitk_reduce(Params p, float* colsum) {
+  splitk_item(p.ws, p.colsum_ws, p.C, p.ldc, colsum, p.M, p.N, p.split, p.epi, p.bias, p.act, p.ld_act,
+              (int64_t)blockIdx.x * blockDim.x + threadIdx.x);
+}
+
+struct SplitkBatch {
+  lgx_splitk_desc d[LGX_SPLITK_MAX];
+};
+
+// blockIdx.y = entry; blocks stride over the entry's items
+__global__ __launch_bounds__(256) void splitk_reduce_batch(SplitkBatch b) {
+  const lgx_splitk_desc& d = b.d[blockIdx.y];
+  const int64_t items = ((int64_t)d.M * d.N + 3) / 4 + (d.colsum ? d.M : 0);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < items; t += stride)
+    splitk_item(d.ws, d.colsum_ws, d.C, d.ldc, d.colsum, d.M, d.N, d.split, d.epilogue & LGX_EPI_ACCUM, nullptr,
+                nullptr, 0, t);
 }
 
 __device__ __forceinline__ void adam1(float& p, float g, float& m, float& v, float b1, float b2, float eps,
@@ -849,13 +872,36 @@ int32_t lgx_gemm(const lgx_gemm_args* a, void* stream) {
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(hipGetErrorString(e));
-  if (split > 1) {
+  if (split > 1 && !a->defer_reduce) {
     const int64_t n = ((int64_t)a->M * a->N + 3) / 4 + (cs ? a->M : 0);  // float4 outputs + bias rows
     hipLaunchKernelGGL(splitk_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, p, a->colsum);
     e = hipGetLastError();
     if (e != hipSuccess) return fail(hipGetErrorString(e));
   }
   return 0;
+}
+
+int32_t lgx_splitk_reduce_batch(const lgx_splitk_desc* descs, int32_t n, void* stream) {
+  if (n < 0 || n > LGX_SPLITK_MAX || (n > 0 && !descs)) return fail("lgx_splitk_reduce_batch: 0 <= n <= LGX_SPLITK_MAX");
+  if (n == 0) return 0;
+  lgxm::SplitkBatch b;
+  int64_t most = 0;
+  for (int i = 0; i < n; ++i) {
+    const lgx_splitk_desc& d = descs[i];
+    if (d.M < 0 || d.N < 0 || d.split < 1 || !d.ws || !d.C || (d.colsum && !d.colsum_ws))
+      return fail("lgx_splitk_reduce_batch: bad entry");
+    if (d.N % 4 == 0 && (reinterpret_cast<uintptr_t>(d.ws) & 15) != 0)
+      return fail("lgx_splitk_reduce_batch: workspace must be 16-B aligned");
+    b.d[i] = d;
+    const int64_t items = ((int64_t)d.M * d.N + 3) / 4 + (d.colsum ? d.M : 0);
+    most = items > most ? items : most;
+  }
+  if (most == 0) return 0;
+  const unsigned bx = (unsigned)std::min<int64_t>((most + 255) / 256, 2048);
+  hipLaunchKernelGGL(lgxm::splitk_reduce_batch, dim3(bx, (unsigned)n), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     b);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : fail(hipGetErrorString(e));
 }
 
 int32_t lgx_copy_batch(const lgx_copy_desc* descs, int32_t n, void* stream) {

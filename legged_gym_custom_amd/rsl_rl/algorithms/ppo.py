@@ -375,8 +375,13 @@ class PPO:
             self._reg_coef * regularization_loss
         # zero_grad of `optimizer` and `estimator_optimizer` (adaptation grads stay)
         g.span("main", "estimator").zero_()
-        estimator_loss.backward()
-        loss.backward()
+        if self.on_gpu:  # every weight-gradient reduction of both backwards in one launch
+            with hip_mlp.deferred_splitk():
+                estimator_loss.backward()
+                loss.backward()
+        else:
+            estimator_loss.backward()
+            loss.backward()
         with torch.no_grad():
             self._losses.copy_(torch.stack([value_loss, surrogate_loss, regularization_loss, estimator_loss]))
         ac.distribution = None

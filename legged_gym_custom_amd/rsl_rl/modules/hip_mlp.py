@@ -20,12 +20,13 @@ import torch.nn as nn
 _LIB_PATH = os.environ.get("LGX_MLP_LIB") or os.path.join(
     os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))), "lib", "liblgx_mlp.so")
 _lib = None
-ABI_VERSION = 1
+ABI_VERSION = 2
 EPI_BIAS, EPI_ELU, EPI_DELU, EPI_ACCUM = 1, 2, 4, 8
 EXPORTED = ["lgx_mlp_abi_version", "lgx_mlp_sizeof_gemm_args", "lgx_mlp_pick_split", "lgx_gemm",
             "lgx_mlp_last_error", "lgx_adam_step", "lgx_ppo_head_forward", "lgx_ppo_head_backward",
-            "lgx_copy_batch", "lgx_act_head", "lgx_store_transition"]
+            "lgx_copy_batch", "lgx_act_head", "lgx_store_transition", "lgx_splitk_reduce_batch"]
 COPY_MAX = 16
+SPLITK_MAX = 24
 
 
 class GemmArgs(C.Structure):
@@ -36,7 +37,14 @@ class GemmArgs(C.Structure):
                 ("M", C.c_int32), ("N", C.c_int32), ("K", C.c_int32), ("epilogue", C.c_int32),
                 ("bias", C.c_void_p), ("act", C.c_void_p), ("ld_act", C.c_int64),
                 ("split_k", C.c_int32), ("workspace", C.c_void_p), ("colsum", C.c_void_p),
-                ("colsum_ws", C.c_void_p)]
+                ("colsum_ws", C.c_void_p), ("defer_reduce", C.c_int32)]
+
+
+class SplitkDesc(C.Structure):
+    """Mirror of lgx_splitk_desc."""
+    _fields_ = [("ws", C.c_void_p), ("colsum_ws", C.c_void_p), ("C", C.c_void_p), ("ldc", C.c_int64),
+                ("colsum", C.c_void_p), ("M", C.c_int32), ("N", C.c_int32), ("split", C.c_int32),
+                ("epilogue", C.c_int32)]
 
 
 class HeadArgs(C.Structure):
@@ -95,6 +103,8 @@ def lib():
     L.lgx_act_head.restype = C.c_int32
     L.lgx_store_transition.argtypes = [vp, vp]
     L.lgx_store_transition.restype = C.c_int32
+    L.lgx_splitk_reduce_batch.argtypes = [vp, C.c_int32, vp]
+    L.lgx_splitk_reduce_batch.restype = C.c_int32
     if L.lgx_mlp_abi_version() != ABI_VERSION:
         raise MlpLibError("liblgx_mlp ABI version mismatch; rebuild")
     L.lgx_mlp_sizeof_gemm_args.restype = C.c_int32
@@ -187,6 +197,94 @@ def weight_grad_raw(G, ldg, X, ldx, rows, N, K, dW, db):
                   colsum=db.data_ptr(), colsum_ws=ws.data_ptr() + 4 * split * N * K))
 
 
+# ---------------------------------------------------------------------------------------
+# Deferred split-K reductions: inside `deferred_splitk()`, every weight-gradient GEMM
+# leaves its split partials in its workspace, and the reductions of the whole backward
+# pass run as ONE lgx_splitk_reduce_batch launch at exit (same fixed summation order as
+# the immediate reduction, so the gradients are bit-identical).
+# ---------------------------------------------------------------------------------------
+_pending = None  # list of (SplitkDesc fields, workspace tensor, (lo, hi) byte ranges) while deferring
+
+
+class deferred_splitk:
+    def __enter__(self):
+        global _pending
+        if _pending is not None:
+            raise RuntimeError("deferred_splitk does not nest")
+        _pending = []
+        return self
+
+    def __exit__(self, *exc):
+        global _pending
+        try:
+            if exc[0] is None:
+                _flush()
+        finally:
+            _pending = None
+        return False
+
+
+def _flush():
+    global _pending
+    items, _pending[:] = list(_pending), []
+    for i in range(0, len(items), SPLITK_MAX):
+        chunk = items[i:i + SPLITK_MAX]
+        descs = (SplitkDesc * SPLITK_MAX)()
+        for k, (d, _ws, _rng) in enumerate(chunk):
+            descs[k] = d
+        _check(lib().lgx_splitk_reduce_batch(descs, len(chunk), _stream()), "lgx_splitk_reduce_batch")
+
+
+class _immediate:
+    """Settle pending reductions and reduce immediately inside (code that reads its
+    weight gradients right away, e.g. the adaptation encoder's re-laid conv weights)."""
+
+    def __enter__(self):
+        global _pending
+        self._saved = _pending
+        if _pending is not None:
+            _flush()
+        _pending = None
+
+    def __exit__(self, *exc):
+        global _pending
+        _pending = self._saved
+        return False
+
+
+def _overlaps(ranges):
+    return any(lo < h and l2 < hi for (lo, hi) in ranges for (_, _, rs) in _pending for (l2, h) in rs)
+
+
+def linear_weight_grad(g, x, dW=None, db=None, accumulate=False):
+    """dW[N,K] (+)= dY[M,N]^T X[M,K], db[N] (+)= sum_m dY[m,:] (split-K, deterministic order;
+    the reduction is deferred inside `deferred_splitk()`)."""
+    g = _rowmajor(g)
+    x = _rowmajor(x)
+    rows, N = g.shape
+    K = x.shape[1]
+    split = max(2, int(lib().lgx_mlp_pick_split(N, K, rows)))
+    dev = g.device
+    dW = torch.empty(N, K, device=dev, dtype=torch.float32) if dW is None else dW
+    db = torch.empty(N, device=dev, dtype=torch.float32) if db is None else db
+    ws = torch.empty(split * N * K + split * N, device=dev, dtype=torch.float32)
+    defer = _pending is not None
+    if defer:  # an output an earlier deferred reduction still owes: settle those first
+        rng = [(dW.data_ptr(), dW.data_ptr() + 4 * (dW.stride(0) * (N - 1) + K)), (db.data_ptr(), db.data_ptr() + 4 * N)]
+        if _overlaps(rng):
+            _flush()
+    epi = EPI_ACCUM if accumulate else 0
+    _run(GemmArgs(A=_ptr(g), lda=g.stride(0), a_kcontig=0, B=_ptr(x), ldb=x.stride(0), b_kcontig=0,
+                  C=_ptr(dW), ldc=dW.stride(0), M=N, N=K, K=rows, epilogue=epi,
+                  split_k=split, workspace=_ptr(ws), colsum=_ptr(db),
+                  colsum_ws=ws.data_ptr() + 4 * split * N * K, defer_reduce=int(defer)))
+    if defer:
+        d = SplitkDesc(ws=ws.data_ptr(), colsum_ws=ws.data_ptr() + 4 * split * N * K, C=dW.data_ptr(),
+                       ldc=dW.stride(0), colsum=db.data_ptr(), M=N, N=K, split=split, epilogue=epi)
+        _pending.append((d, ws, rng))
+    return dW, db
+
+
 def linear_forward(x, W, b, elu, out=None):
     """Y[M,N] = act(X[M,K] W[N,K]^T + b)."""
     x = _rowmajor(x)
@@ -216,24 +314,6 @@ def linear_input_grad(g, W, y_prev=None, Wt=None):
                   C=_ptr(dx), ldc=dx.stride(0), M=M, N=K, K=N, epilogue=EPI_DELU if y_prev is not None else 0,
                   act=_ptr(y_prev), ld_act=0 if y_prev is None else y_prev.stride(0), split_k=1))
     return dx
-
-
-def linear_weight_grad(g, x, dW=None, db=None, accumulate=False):
-    """dW[N,K] (+)= dY[M,N]^T X[M,K], db[N] (+)= sum_m dY[m,:] (split-K, deterministic order)."""
-    g = _rowmajor(g)
-    x = _rowmajor(x)
-    rows, N = g.shape
-    K = x.shape[1]
-    split = max(2, int(lib().lgx_mlp_pick_split(N, K, rows)))
-    dev = g.device
-    dW = torch.empty(N, K, device=dev, dtype=torch.float32) if dW is None else dW
-    db = torch.empty(N, device=dev, dtype=torch.float32) if db is None else db
-    ws = torch.empty(split * N * K + split * N, device=dev, dtype=torch.float32)
-    _run(GemmArgs(A=_ptr(g), lda=g.stride(0), a_kcontig=0, B=_ptr(x), ldb=x.stride(0), b_kcontig=0,
-                  C=_ptr(dW), ldc=dW.stride(0), M=N, N=K, K=rows, epilogue=EPI_ACCUM if accumulate else 0,
-                  split_k=split, workspace=_ptr(ws), colsum=_ptr(db),
-                  colsum_ws=ws.data_ptr() + 4 * split * N * K))
-    return dW, db
 
 
 def _grad_of(p):
@@ -411,6 +491,11 @@ class _AdaptationFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g_out):
+        with _immediate():
+            return _AdaptationFn._backward(ctx, g_out)
+
+    @staticmethod
+    def _backward(ctx, g_out):
         C1, C2, C3, k1, s1, k2, s2, L1, L2 = ctx.dims
         x, y0, y1, y2, out, W1, W2, Wf = ctx.saved_tensors
         fc_w, fc_b, c1_w, c1_b, c2_w, c2_b, f_w, f_b = ctx.params

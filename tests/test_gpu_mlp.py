@@ -217,3 +217,27 @@ def test_forward_parts_grads_only_where_needed():
     # parameter gradients sum ~M products each: cancellation needs an absolute slack
     for p, pr in zip(net.parameters(), ref.parameters()):
         torch.testing.assert_close(p.grad.double().cpu(), pr.grad, rtol=1e-3, atol=2e-3)
+
+
+def test_deferred_splitk_matches_immediate_bitwise():
+    """One lgx_splitk_reduce_batch over several weight-gradient GEMMs == each GEMM's own
+    reduction, bit for bit (same fixed order), incl. accumulation and a shared output."""
+    g = torch.Generator(device=dev).manual_seed(5)
+    shapes = [(24576, 512, 627), (24576, 12, 128), (1000, 20, 29), (777, 3, 64)]
+    data = [(torch.randn(r, n, device=dev, generator=g), torch.randn(r, k, device=dev, generator=g))
+            for r, n, k in shapes]
+    ref = []
+    for dy, x in data:
+        dW = torch.randn(dy.shape[1], x.shape[1], device=dev, generator=g)
+        db = torch.randn(dy.shape[1], device=dev, generator=g)
+        ref.append((dW.clone(), db.clone()))
+    out = [(a.clone(), b.clone()) for a, b in ref]
+    for (dy, x), (dW, db) in zip(data, ref):
+        H.linear_weight_grad(dy, x, dW, db, accumulate=True)
+        H.linear_weight_grad(dy, x, dW, db, accumulate=True)  # twice: accumulation order
+    with H.deferred_splitk():
+        for (dy, x), (dW, db) in zip(data, out):
+            H.linear_weight_grad(dy, x, dW, db, accumulate=True)
+            H.linear_weight_grad(dy, x, dW, db, accumulate=True)  # overlaps: settles the first
+    for (a, b), (c, d) in zip(ref, out):
+        assert torch.equal(a, c) and torch.equal(b, d)
