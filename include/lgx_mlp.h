@@ -108,10 +108,57 @@ typedef struct lgx_ppo_head_args {
   const float* g;
   float* dmu; float* dvalue; float* dstd;
   float* ws; uint32_t* counter;
+  float* kl_dst;             /* optional: forward also writes the KL mean here (the KL slot
+                                of the flat gradient buffer that rides the all-reduce) */
 } lgx_ppo_head_args;
 
 int32_t lgx_ppo_head_forward(const lgx_ppo_head_args* args, void* stream);
 int32_t lgx_ppo_head_backward(const lgx_ppo_head_args* args, void* stream);
+
+/* ROA regulariser and estimator loss (rsl_rl ppo.py:204-206 and :190-192):
+ *   reg = mean_i || p_i - a_i ||_2          (p = privileged latent, a = sg(adaptation latent), [B, L])
+ *   est = mean_i || e_i - t_i ||_2^2        (e = estimator output, t = true estimated obs, [B, E])
+ * Forward writes out[0] = reg, out[1] = est (deterministic: per-block partials summed in
+ * block order by the last block). Backward takes g[0], g[1] (device scalars: d loss/d reg,
+ * d loss/d est) and writes dp = g0 (p - a) / (B ||p - a||) (0 where the norm is 0, as
+ * torch's norm backward) and de = g1 * 2 (e - t) / B. ws >= 2 * ceil(B/256) floats; counter
+ * one zero-initialised uint32. */
+typedef struct lgx_aux_loss_args {
+  const float* p; const float* a; int32_t L;
+  const float* e; const float* t; int32_t E;
+  int32_t B;
+  float* out; const float* g; float* dp; float* de;
+  float* ws; uint32_t* counter;
+} lgx_aux_loss_args;
+int32_t lgx_aux_loss_forward(const lgx_aux_loss_args* args, void* stream);
+int32_t lgx_aux_loss_backward(const lgx_aux_loss_args* args, void* stream);
+
+/* The optimizer tail of one PPO minibatch (rsl_rl ppo.py:264-291) in two launches, over
+ * the flat gradient/parameter/moment buffers (one layout):
+ *   coef_e = min(max_norm / (||g[est]|| + 1e-6), 1)            clip_grad_norm_(estimator)
+ *   Adam(est segment, est_lr, coef_e)                           estimator_optimizer.step()
+ *   adaptive KL schedule in fp64 on lr64 (kl = g[kl_index]; skipped when kl_index < 0):
+ *     kl > 2 d: lr = max(lr / 1.5, 1e-5);  d/2 > kl > 0: lr = min(lr * 1.5, 1e-2)
+ *   coef_m = min(max_norm / (||g[main] ++ g[adapt]|| + 1e-6), 1)  clip_grad_norm_(actor_critic)
+ *   g[adapt] *= coef_m (the stale DAgger gradients, a reference quirk)
+ *   Adam(main segment, (float) lr, coef_m)                      optimizer.step()
+ *   sums[i] += *loss_ptrs[i] (i < nloss)                        loss bookkeeping
+ * Adam arithmetic as lgx_adam_step; step_main / step_est are incremented here. Norms are
+ * block partials summed in block order (deterministic). ws >= 2 * 512 floats + 8; counter:
+ * one zero-initialised uint32 (left at zero). */
+#define LGX_TAIL_MAX_LOSSES 8
+typedef struct lgx_ppo_tail_args {
+  float* grads; float* params; float* exp_avg; float* exp_avg_sq;
+  int64_t main_lo, main_hi, est_lo, est_hi, adapt_lo, adapt_hi, kl_index;
+  float max_norm;
+  float b1_main, b2_main, eps_main, b1_est, b2_est, eps_est, est_lr;
+  double desired_kl;
+  double* lr64; float* lr32;
+  float* step_main; float* step_est;
+  const float* loss_ptrs[LGX_TAIL_MAX_LOSSES]; float* sums; int32_t nloss;
+  float* ws; uint32_t* counter;
+} lgx_ppo_tail_args;
+int32_t lgx_ppo_tail(const lgx_ppo_tail_args* args, void* stream);
 
 /* ---- rollout bookkeeping (ppo.py:129-171, rollout_storage.py:87-105), one launch each */
 

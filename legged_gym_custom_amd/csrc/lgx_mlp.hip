@@ -594,6 +594,7 @@ __global__ void ppo_head_fwd(lgx_ppo_head_args p) {
       float t = 0.f;
       for (int b = 0; b < (int)gridDim.x; ++b) t += p.ws[b * 3 + threadIdx.x];
       p.out[threadIdx.x == 2 ? 3 : threadIdx.x] = t / p.B;
+      if (threadIdx.x == 2 && p.kl_dst) *p.kl_dst = t / p.B;
     }
     if (threadIdx.x == 3) {
       float ent = 0.f;
@@ -660,6 +661,116 @@ __global__ void ppo_head_bwd(lgx_ppo_head_args p) {
     }
     if (j == 0) *p.counter = 0u;
   }
+}
+
+// ---------------------------------------------------------------- ROA + estimator losses
+__global__ void aux_loss_fwd(lgx_aux_loss_args p) {
+  __shared__ float red[4 * 2];
+  const int i = blockIdx.x * HT + threadIdx.x;
+  float v[2] = {0.f, 0.f};
+  if (i < p.B) {
+    float s = 0.f;
+    for (int j = 0; j < p.L; ++j) {
+      const float d = p.p[(int64_t)i * p.L + j] - p.a[(int64_t)i * p.L + j];
+      s += d * d;
+    }
+    v[0] = sqrtf(s);
+    float q = 0.f;
+    for (int j = 0; j < p.E; ++j) {
+      const float d = p.e[(int64_t)i * p.E + j] - p.t[(int64_t)i * p.E + j];
+      q += d * d;
+    }
+    const float nq = sqrtf(q);  // torch: norm(dim=1).pow(2)
+    v[1] = nq * nq;
+  }
+  block_sum<2>(v, red);
+  if (threadIdx.x == 0) { p.ws[blockIdx.x * 2] = v[0]; p.ws[blockIdx.x * 2 + 1] = v[1]; }
+  if (last_block(p.counter)) {
+    if (threadIdx.x < 2) {
+      float t = 0.f;
+      for (int b = 0; b < (int)gridDim.x; ++b) t += p.ws[b * 2 + threadIdx.x];
+      p.out[threadIdx.x] = t / p.B;
+    }
+    if (threadIdx.x == 0) *p.counter = 0u;
+  }
+}
+
+__global__ void aux_loss_bwd(lgx_aux_loss_args p) {
+  const int i = blockIdx.x * HT + threadIdx.x;
+  if (i >= p.B) return;
+  const float gr = p.g[0] / p.B, ge = p.g[1] / p.B;
+  float s = 0.f;
+  for (int j = 0; j < p.L; ++j) {
+    const float d = p.p[(int64_t)i * p.L + j] - p.a[(int64_t)i * p.L + j];
+    s += d * d;
+  }
+  const float n = sqrtf(s);
+  const float k = n > 0.f ? gr / n : 0.f;
+  for (int j = 0; j < p.L; ++j)
+    p.dp[(int64_t)i * p.L + j] = k * (p.p[(int64_t)i * p.L + j] - p.a[(int64_t)i * p.L + j]);
+  for (int j = 0; j < p.E; ++j)
+    p.de[(int64_t)i * p.E + j] = ge * 2.f * (p.e[(int64_t)i * p.E + j] - p.t[(int64_t)i * p.E + j]);
+}
+
+// ---------------------------------------------------------------- PPO minibatch optimizer tail
+constexpr int TAIL_BLOCKS = 512;
+
+__device__ __forceinline__ float sumsq_range(const float* __restrict__ g, int64_t lo, int64_t hi, int64_t i0,
+                                             int64_t stride) {
+  float s = 0.f;
+  for (int64_t i = lo + i0; i < hi; i += stride) s += g[i] * g[i];
+  return s;
+}
+
+// grid TAIL_BLOCKS: squared norms (estimator; main + adaptation) -> the last block turns
+// them into clip coefficients, runs the KL schedule, bumps the Adam steps and the loss sums
+__global__ __launch_bounds__(256) void tail_norms(lgx_ppo_tail_args p) {
+  __shared__ float red[4 * 2];
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  float v[2];
+  v[0] = sumsq_range(p.grads, p.est_lo, p.est_hi, i0, stride);
+  v[1] = sumsq_range(p.grads, p.main_lo, p.main_hi, i0, stride) + sumsq_range(p.grads, p.adapt_lo, p.adapt_hi, i0, stride);
+  block_sum<2>(v, red);
+  if (threadIdx.x == 0) { p.ws[blockIdx.x * 2] = v[0]; p.ws[blockIdx.x * 2 + 1] = v[1]; }
+  if (last_block(p.counter)) {
+    if (threadIdx.x == 0) {
+      float se = 0.f, sm = 0.f;
+      for (int b = 0; b < (int)gridDim.x; ++b) { se += p.ws[b * 2]; sm += p.ws[b * 2 + 1]; }
+      float* sc = p.ws + 2 * TAIL_BLOCKS;  // [coef_e, coef_m]
+      sc[0] = fminf(p.max_norm / (sqrtf(se) + 1e-6f), 1.f);
+      sc[1] = fminf(p.max_norm / (sqrtf(sm) + 1e-6f), 1.f);
+      if (p.kl_index >= 0) {
+        const double kl = (double)p.grads[p.kl_index];
+        double lr = *p.lr64;
+        if (kl > p.desired_kl * 2.0) lr = fmax(lr / 1.5, 1e-5);
+        else if (kl < p.desired_kl / 2.0 && kl > 0.0) lr = fmin(lr * 1.5, 1e-2);
+        *p.lr64 = lr;
+        *p.lr32 = (float)lr;
+      }
+      *p.step_main += 1.f;
+      *p.step_est += 1.f;
+      for (int k = 0; k < p.nloss; ++k) p.sums[k] += *p.loss_ptrs[k];
+      *p.counter = 0u;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void tail_adam(lgx_ppo_tail_args p) {
+  const float* sc = p.ws + 2 * TAIL_BLOCKS;
+  const float ce = sc[0], cm = sc[1];
+  const float tm = *p.step_main, te = *p.step_est;
+  const float lrm = *p.lr32;
+  const float bcm1 = 1.f - powf(p.b1_main, tm), bcm2 = 1.f - powf(p.b2_main, tm);
+  const float bce1 = 1.f - powf(p.b1_est, te), bce2 = 1.f - powf(p.b2_est, te);
+  const float ssm = lrm / bcm1, sqm = sqrtf(bcm2), sse = p.est_lr / bce1, sqe = sqrtf(bce2);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (int64_t i = p.main_lo + i0; i < p.main_hi; i += stride)
+    adam1(p.params[i], p.grads[i] * cm, p.exp_avg[i], p.exp_avg_sq[i], p.b1_main, p.b2_main, p.eps_main, ssm, sqm);
+  for (int64_t i = p.est_lo + i0; i < p.est_hi; i += stride)
+    adam1(p.params[i], p.grads[i] * ce, p.exp_avg[i], p.exp_avg_sq[i], p.b1_est, p.b2_est, p.eps_est, sse, sqe);
+  for (int64_t i = p.adapt_lo + i0; i < p.adapt_hi; i += stride) p.grads[i] *= cm;
 }
 
 // dynamic LDS: two K-step stages of hi/lo A and B images, or the fp32 C image (reused)
@@ -812,6 +923,40 @@ int32_t lgx_ppo_head_backward(const lgx_ppo_head_args* a, void* stream) {
   if (!a->g || !a->dmu || !a->dvalue || !a->dstd) return fail("lgx_ppo_head_backward: null g/dmu/dvalue/dstd");
   hipLaunchKernelGGL(lgxm::ppo_head_bwd, dim3((a->B + lgxm::HT - 1) / lgxm::HT), dim3(lgxm::HT), 0,
                      static_cast<hipStream_t>(stream), *a);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : fail(hipGetErrorString(e));
+}
+
+int32_t lgx_aux_loss_forward(const lgx_aux_loss_args* a, void* stream) {
+  if (!a || a->B < 1 || a->L < 1 || a->E < 1 || !a->p || !a->a || !a->e || !a->t || !a->out || !a->ws || !a->counter)
+    return fail("lgx_aux_loss_forward: bad arguments");
+  hipLaunchKernelGGL(lgxm::aux_loss_fwd, dim3((a->B + lgxm::HT - 1) / lgxm::HT), dim3(lgxm::HT), 0,
+                     static_cast<hipStream_t>(stream), *a);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : fail(hipGetErrorString(e));
+}
+
+int32_t lgx_aux_loss_backward(const lgx_aux_loss_args* a, void* stream) {
+  if (!a || a->B < 1 || a->L < 1 || a->E < 1 || !a->p || !a->a || !a->e || !a->t || !a->g || !a->dp || !a->de)
+    return fail("lgx_aux_loss_backward: bad arguments");
+  hipLaunchKernelGGL(lgxm::aux_loss_bwd, dim3((a->B + lgxm::HT - 1) / lgxm::HT), dim3(lgxm::HT), 0,
+                     static_cast<hipStream_t>(stream), *a);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : fail(hipGetErrorString(e));
+}
+
+int32_t lgx_ppo_tail(const lgx_ppo_tail_args* a, void* stream) {
+  if (!a || !a->grads || !a->params || !a->exp_avg || !a->exp_avg_sq || !a->lr32 || !a->lr64 || !a->step_main ||
+      !a->step_est || !a->ws || !a->counter)
+    return fail("lgx_ppo_tail: null pointer");
+  if (a->main_lo > a->main_hi || a->est_lo > a->est_hi || a->adapt_lo > a->adapt_hi || a->nloss < 0 ||
+      a->nloss > LGX_TAIL_MAX_LOSSES || (a->nloss > 0 && !a->sums))
+    return fail("lgx_ppo_tail: bad ranges");
+  for (int k = 0; k < a->nloss; ++k)
+    if (!a->loss_ptrs[k]) return fail("lgx_ppo_tail: null loss pointer");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(lgxm::tail_norms, dim3(lgxm::TAIL_BLOCKS), dim3(256), 0, s, *a);
+  hipLaunchKernelGGL(lgxm::tail_adam, dim3(1024), dim3(256), 0, s, *a);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : fail(hipGetErrorString(e));
 }

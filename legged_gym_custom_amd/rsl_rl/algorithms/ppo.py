@@ -205,6 +205,14 @@ class PPO:
         self._reg_coef = torch.zeros((), device=device)
         self._losses = torch.zeros(4, device=device)   # value, surrogate, regularisation, estimator
         self._sums = torch.zeros(4, device=device)
+        if self.on_gpu:  # fixed-address loss outputs and tail scratch (read by the captured tail)
+            self._head_out = torch.zeros(4, device=device)   # surrogate, value, entropy, kl
+            self._aux_out = torch.zeros(2, device=device)    # regularisation, estimator
+            self._tail_ws = torch.zeros(2 * 512 + 8, device=device)
+            self._tail_counter = torch.zeros(1, dtype=torch.int32, device=device)
+            self._g_one = torch.ones((), device=device)
+            self._g_value = torch.full((), float(value_loss_coef), device=device)
+            self._g_ent = torch.full((), -float(entropy_coef), device=device)
         self._perm = None
         self._graphs = None
         self._eager_updates = 0
@@ -349,39 +357,45 @@ class PPO:
              old_mu_b, old_sigma_b) = s.gather(idx)
         if self.on_gpu:
             # fused loss head: Normal log-prob/entropy, ratio, clipped surrogate, clipped value
-            # loss and KL in one HIP kernel each way (hip_mlp.ppo_head). The privileged latent
-            # is computed once and feeds both the actor and the ROA regulariser (the
-            # reference evaluates the same encoder on the same input twice, ppo.py:190,204)
+            # loss and KL in one HIP kernel each way (hip_mlp.ppo_head); the KL goes straight
+            # into its slot of the flat gradient buffer (it rides the all-reduce). The
+            # privileged latent is computed once and feeds both the actor and the ROA
+            # regulariser (the reference evaluates the same encoder on the same input twice,
+            # ppo.py:190,204)
+            adaptive = self.desired_kl is not None and self.schedule == "adaptive"
             priv_latent = ac.privileged_encoder(priv_b)
             scan_latent = ac.scan_encoder(scan_b)
             mu_b = ac.actor_forward(obs_b, priv_latent, scan_latent, est_b)  # TRUE est obs (Q12)
             value_b = ac.evaluate(critic_b)
-            surrogate_loss, value_loss, entropy_mean, kl_mean = hip_mlp.ppo_head(
+            surrogate_loss, value_loss, entropy_mean, _kl = hip_mlp.ppo_head(
                 mu_b, value_b, ac.std, actions_b, old_logp_b, adv_b, target_values_b, returns_b, old_mu_b, old_sigma_b,
-                self.clip_param, self.use_clipped_value_loss)
+                self.clip_param, self.use_clipped_value_loss, kl_dst=g.segment("kl") if adaptive else None,
+                out=self._head_out)
             # sg(z_adapt): the adaptation encoder only trains in DAgger iterations, so over a
             # PPO update its latents are fixed — computed once per update (_adapt_all)
             adapt_latent = self._adapt_all[idx]  # (shuffled order, like the rows)
-            regularization_loss = (priv_latent - adapt_latent).norm(p=2, dim=1).mean()
             pred = self.estimator(obs_b)
-            estimator_loss = (pred - est_b).norm(p=2, dim=1).pow(2).mean()
-            if self.desired_kl is not None and self.schedule == "adaptive":
-                g.segment("kl").copy_(kl_mean.reshape(1))
-        else:
-            (surrogate_loss, value_loss, entropy_mean, regularization_loss,
-             estimator_loss) = self._losses_torch(obs_b, priv_b, critic_b, est_b, scan_b, actions_b, target_values_b,
-                                                  adv_b, returns_b, old_logp_b, old_mu_b, old_sigma_b)
+            regularization_loss, estimator_loss = hip_mlp.aux_losses(priv_latent, adapt_latent, pred, est_b,
+                                                                     out=self._aux_out)
+            # zero_grad of `optimizer` and `estimator_optimizer` (adaptation grads stay), then
+            # both backwards (ppo.py:207, :262) as one pass seeded with the loss coefficients
+            # (loss = surr + c_v vloss - c_e entropy + c_reg reg; the estimator loss on its own
+            # parameters), every weight-gradient reduction in one launch
+            g.span("main", "estimator").zero_()
+            with hip_mlp.deferred_splitk():
+                torch.autograd.backward([surrogate_loss, value_loss, entropy_mean, regularization_loss, estimator_loss],
+                                        [self._g_one, self._g_value, self._g_ent, self._reg_coef, self._g_one])
+            ac.distribution = None
+            return
+        (surrogate_loss, value_loss, entropy_mean, regularization_loss,
+         estimator_loss) = self._losses_torch(obs_b, priv_b, critic_b, est_b, scan_b, actions_b, target_values_b,
+                                              adv_b, returns_b, old_logp_b, old_mu_b, old_sigma_b)
         loss = surrogate_loss + self.value_loss_coef * value_loss - self.entropy_coef * entropy_mean + \
             self._reg_coef * regularization_loss
         # zero_grad of `optimizer` and `estimator_optimizer` (adaptation grads stay)
         g.span("main", "estimator").zero_()
-        if self.on_gpu:  # every weight-gradient reduction of both backwards in one launch
-            with hip_mlp.deferred_splitk():
-                estimator_loss.backward()
-                loss.backward()
-        else:
-            estimator_loss.backward()
-            loss.backward()
+        estimator_loss.backward()
+        loss.backward()
         with torch.no_grad():
             self._losses.copy_(torch.stack([value_loss, surrogate_loss, regularization_loss, estimator_loss]))
         ac.distribution = None
@@ -419,15 +433,24 @@ class PPO:
         return surrogate_loss, value_loss, entropy_b.mean(), regularization_loss, estimator_loss
 
     def _minibatch_step(self):
-        """Phase B: (ranks averaged) clip + estimator step, KL schedule, clip + main step."""
+        """Phase B: (ranks averaged) clip + estimator step, KL schedule, clip + main step.
+        GPU: one lgx_ppo_tail (two launches) for all of it."""
         g = self.grads
+        if self.on_gpu:
+            adaptive = self.desired_kl is not None and self.schedule == "adaptive"
+            o, eo = self.optimizer.param_groups[0], self.estimator_optimizer.param_groups[0]
+            hip_mlp.ppo_tail(g.buf, self.params_buf, self.exp_avg, self.exp_avg_sq, g.slices["main"],
+                             g.slices["estimator"], g.slices["adaptation"],
+                             g.slices["kl"][0] if adaptive else -1, self.max_grad_norm, o["betas"], o["eps"],
+                             eo["betas"], eo["eps"], self.estimator_learning_rate,
+                             self.desired_kl if adaptive else 0.0, self._lr64, self._lr32,
+                             self._opt_step["optimizer"], self._opt_step["estimator_optimizer"],
+                             [self._head_out[1], self._head_out[0], self._aux_out[0], self._aux_out[1]], self._sums,
+                             self._tail_ws, self._tail_counter)
+            return
         with torch.no_grad():
-            if self.on_gpu:  # clip coefficient folded into the Adam kernel
-                self._adam("estimator_optimizer", self.estimator_learning_rate,
-                           _clip_coef([g.segment("estimator")], self.max_grad_norm))
-            else:
-                _clip_([g.segment("estimator")], self.max_grad_norm)
-                self.estimator_optimizer.step()
+            _clip_([g.segment("estimator")], self.max_grad_norm)
+            self.estimator_optimizer.step()
         if self.desired_kl is not None and self.schedule == "adaptive":
             with torch.no_grad():
                 kl_mean = g.segment("kl")[0].double()
@@ -437,19 +460,11 @@ class PPO:
                 lr_new = torch.where(kl_mean > self.desired_kl * 2.0, down,
                                      torch.where((kl_mean < self.desired_kl / 2.0) & (kl_mean > 0.0), up, lr))
                 self._lr64.copy_(lr_new)
-                if self._lr32 is not None:
-                    self._lr32.copy_(lr_new)
-            if self._lr32 is None:  # host Adam (CPU): the schedule value goes to the param groups
-                for grp in self.optimizer.param_groups:
-                    grp["lr"] = float(self._lr64)
+            for grp in self.optimizer.param_groups:  # host Adam (CPU): the schedule value goes to the param groups
+                grp["lr"] = float(self._lr64)
         with torch.no_grad():
-            if self.on_gpu:
-                coef = _clip_coef([g.segment("main"), g.segment("adaptation")], self.max_grad_norm)
-                g.segment("adaptation").mul_(coef)  # the stale DAgger grads are scaled in place (quirk)
-                self._adam("optimizer", self._lr32, coef)
-            else:
-                _clip_([g.segment("main"), g.segment("adaptation")], self.max_grad_norm)
-                self.optimizer.step()
+            _clip_([g.segment("main"), g.segment("adaptation")], self.max_grad_norm)
+            self.optimizer.step()
             self._sums.add_(self._losses)
 
     def _allreduce_minibatch(self):

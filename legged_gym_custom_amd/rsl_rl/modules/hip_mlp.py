@@ -24,7 +24,9 @@ ABI_VERSION = 2
 EPI_BIAS, EPI_ELU, EPI_DELU, EPI_ACCUM = 1, 2, 4, 8
 EXPORTED = ["lgx_mlp_abi_version", "lgx_mlp_sizeof_gemm_args", "lgx_mlp_pick_split", "lgx_gemm",
             "lgx_mlp_last_error", "lgx_adam_step", "lgx_ppo_head_forward", "lgx_ppo_head_backward",
-            "lgx_copy_batch", "lgx_act_head", "lgx_store_transition", "lgx_splitk_reduce_batch"]
+            "lgx_copy_batch", "lgx_act_head", "lgx_store_transition", "lgx_splitk_reduce_batch",
+            "lgx_aux_loss_forward", "lgx_aux_loss_backward", "lgx_ppo_tail"]
+TAIL_MAX_LOSSES = 8
 COPY_MAX = 16
 SPLITK_MAX = 24
 
@@ -53,7 +55,26 @@ class HeadArgs(C.Structure):
                                           "returns", "old_mu", "old_sigma")] + \
                [("B", C.c_int32), ("A", C.c_int32), ("clip", C.c_float), ("clipped_value", C.c_int32),
                 ("out", C.c_void_p), ("g", C.c_void_p), ("dmu", C.c_void_p), ("dvalue", C.c_void_p),
-                ("dstd", C.c_void_p), ("ws", C.c_void_p), ("counter", C.c_void_p)]
+                ("dstd", C.c_void_p), ("ws", C.c_void_p), ("counter", C.c_void_p), ("kl_dst", C.c_void_p)]
+
+
+class AuxArgs(C.Structure):
+    """Mirror of lgx_aux_loss_args."""
+    _fields_ = [("p", C.c_void_p), ("a", C.c_void_p), ("L", C.c_int32), ("e", C.c_void_p), ("t", C.c_void_p),
+                ("E", C.c_int32), ("B", C.c_int32), ("out", C.c_void_p), ("g", C.c_void_p), ("dp", C.c_void_p),
+                ("de", C.c_void_p), ("ws", C.c_void_p), ("counter", C.c_void_p)]
+
+
+class TailArgs(C.Structure):
+    """Mirror of lgx_ppo_tail_args."""
+    _fields_ = [(n, C.c_void_p) for n in ("grads", "params", "exp_avg", "exp_avg_sq")] + \
+               [(n, C.c_int64) for n in ("main_lo", "main_hi", "est_lo", "est_hi", "adapt_lo", "adapt_hi",
+                                         "kl_index")] + \
+               [(n, C.c_float) for n in ("max_norm", "b1_main", "b2_main", "eps_main", "b1_est", "b2_est", "eps_est",
+                                         "est_lr")] + \
+               [("desired_kl", C.c_double), ("lr64", C.c_void_p), ("lr32", C.c_void_p), ("step_main", C.c_void_p),
+                ("step_est", C.c_void_p), ("loss_ptrs", C.c_void_p * TAIL_MAX_LOSSES), ("sums", C.c_void_p),
+                ("nloss", C.c_int32), ("ws", C.c_void_p), ("counter", C.c_void_p)]
 
 
 class CopyDesc(C.Structure):
@@ -103,6 +124,9 @@ def lib():
     L.lgx_act_head.restype = C.c_int32
     L.lgx_store_transition.argtypes = [vp, vp]
     L.lgx_store_transition.restype = C.c_int32
+    for fn in ("lgx_aux_loss_forward", "lgx_aux_loss_backward", "lgx_ppo_tail"):
+        getattr(L, fn).argtypes = [vp, vp]
+        getattr(L, fn).restype = C.c_int32
     L.lgx_splitk_reduce_batch.argtypes = [vp, C.c_int32, vp]
     L.lgx_splitk_reduce_batch.restype = C.c_int32
     if L.lgx_mlp_abi_version() != ABI_VERSION:
@@ -558,30 +582,30 @@ def adaptation_forward(mod, hist):
 _head_counter = {}
 
 
-def _counter(dev):
-    c = _head_counter.get(dev)
+def _counter(dev, kind="head"):
+    c = _head_counter.get((dev, kind))
     if c is None:
-        c = _head_counter[dev] = torch.zeros(1, dtype=torch.int32, device=dev)
+        c = _head_counter[(dev, kind)] = torch.zeros(1, dtype=torch.int32, device=dev)
     return c
 
 
 class _PPOHeadFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, mu, value, std, actions, old_logp, adv, target_values, returns, old_mu, old_sigma, clip,
-                clipped_value):
+                clipped_value, kl_dst, out):
         B, A = mu.shape
         dev = mu.device
         ts = [_rowmajor(t.reshape(B, -1)) for t in (mu, value, actions, old_logp, adv, target_values, returns, old_mu,
                                                      old_sigma)]
         mu_, value_, actions_, old_logp_, adv_, tv_, ret_, old_mu_, old_sigma_ = ts
         std_ = std.contiguous()
-        out = torch.empty(4, device=dev)
+        out = torch.empty(4, device=dev) if out is None else out
         ws = torch.empty(16 * ((B + 255) // 256), device=dev)
         a = HeadArgs(mu=mu_.data_ptr(), value=value_.data_ptr(), std=std_.data_ptr(), actions=actions_.data_ptr(),
                      old_logp=old_logp_.data_ptr(), adv=adv_.data_ptr(), target_values=tv_.data_ptr(),
                      returns=ret_.data_ptr(), old_mu=old_mu_.data_ptr(), old_sigma=old_sigma_.data_ptr(), B=B, A=A,
                      clip=float(clip), clipped_value=int(bool(clipped_value)), out=out.data_ptr(), ws=ws.data_ptr(),
-                     counter=_counter(dev).data_ptr())
+                     counter=_counter(dev).data_ptr(), kl_dst=None if kl_dst is None else kl_dst.data_ptr())
         L = lib()
         if L.lgx_ppo_head_forward(C.byref(a), C.c_void_p(torch.cuda.current_stream().cuda_stream)) != 0:
             raise MlpLibError("lgx_ppo_head_forward: " + L.lgx_mlp_last_error().decode())
@@ -611,10 +635,71 @@ class _PPOHeadFn(torch.autograd.Function):
         L = lib()
         if L.lgx_ppo_head_backward(C.byref(a), C.c_void_p(torch.cuda.current_stream().cuda_stream)) != 0:
             raise MlpLibError("lgx_ppo_head_backward: " + L.lgx_mlp_last_error().decode())
-        return (dmu, dvalue.view(ctx.value_shape), dstd) + (None,) * 9
+        return (dmu, dvalue.view(ctx.value_shape), dstd) + (None,) * 11
 
 
-def ppo_head(mu, value, std, actions, old_logp, adv, target_values, returns, old_mu, old_sigma, clip, clipped_value):
-    """(surrogate_loss, value_loss, entropy_mean, kl_mean) on the HIP device; kl carries no grad."""
+def ppo_head(mu, value, std, actions, old_logp, adv, target_values, returns, old_mu, old_sigma, clip, clipped_value,
+             kl_dst=None, out=None):
+    """(surrogate_loss, value_loss, entropy_mean, kl_mean) on the HIP device; kl carries no grad
+    (and is also written to `kl_dst`, a 1-element device tensor, when given). `out`: an
+    optional persistent [4] buffer the four values are written to (fixed addresses)."""
     return _PPOHeadFn.apply(mu, value, std, actions, old_logp, adv, target_values, returns, old_mu, old_sigma, clip,
-                            clipped_value)
+                            clipped_value, kl_dst, out)
+
+
+# ---------------------------------------------------------------------------------------
+# ROA regulariser ||z_priv - sg(z_adapt)|| and estimator loss ||e - t||^2 (ppo.py:190-206)
+# as one forward and one backward kernel (lgx_aux_loss_*).
+# ---------------------------------------------------------------------------------------
+class _AuxLossFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, p, a, e, t, out):
+        p, a, e, t = (_rowmajor(x) for x in (p, a, e, t))
+        B, L = p.shape
+        E = e.shape[1]
+        dev = p.device
+        out = torch.empty(2, device=dev) if out is None else out
+        ws = torch.empty(2 * ((B + 255) // 256), device=dev)
+        args = AuxArgs(p=p.data_ptr(), a=a.data_ptr(), L=L, e=e.data_ptr(), t=t.data_ptr(), E=E, B=B,
+                       out=out.data_ptr(), ws=ws.data_ptr(), counter=_counter(dev, "aux").data_ptr())
+        _check(lib().lgx_aux_loss_forward(C.byref(args), _stream()), "lgx_aux_loss_forward")
+        ctx.save_for_backward(p, a, e, t)
+        return out[0], out[1]
+
+    @staticmethod
+    def backward(ctx, g_reg, g_est):
+        p, a, e, t = ctx.saved_tensors
+        B, L = p.shape
+        dev = p.device
+        z = torch.zeros((), device=dev)
+        g = torch.stack([g_reg if g_reg is not None else z, g_est if g_est is not None else z]).float().contiguous()
+        dp = torch.empty_like(p)
+        de = torch.empty_like(e)
+        args = AuxArgs(p=p.data_ptr(), a=a.data_ptr(), L=L, e=e.data_ptr(), t=t.data_ptr(), E=e.shape[1], B=B,
+                       g=g.data_ptr(), dp=dp.data_ptr(), de=de.data_ptr())
+        _check(lib().lgx_aux_loss_backward(C.byref(args), _stream()), "lgx_aux_loss_backward")
+        return dp, None, de, None, None
+
+
+def aux_losses(priv_latent, adapt_latent, pred, true_est, out=None):
+    """(mean ||priv_latent - adapt_latent||_2, mean ||pred - true_est||_2^2); gradients flow
+    to priv_latent and pred only (adapt_latent and true_est are constants). `out`: optional
+    persistent [2] buffer for the two values."""
+    return _AuxLossFn.apply(priv_latent, adapt_latent.detach(), pred, true_est.detach(), out)
+
+
+def ppo_tail(grads, params, exp_avg, exp_avg_sq, main, est, adapt, kl_index, max_norm, betas_main, eps_main,
+             betas_est, eps_est, est_lr, desired_kl, lr64, lr32, step_main, step_est, loss_ptrs, sums, ws, counter):
+    """lgx_ppo_tail: clip + Adam of both optimizers, the KL schedule and the loss sums
+    (one minibatch's optimizer tail, two launches). main/est/adapt: (lo, hi) element ranges."""
+    a = TailArgs(grads=grads.data_ptr(), params=params.data_ptr(), exp_avg=exp_avg.data_ptr(),
+                 exp_avg_sq=exp_avg_sq.data_ptr(), main_lo=main[0], main_hi=main[1], est_lo=est[0], est_hi=est[1],
+                 adapt_lo=adapt[0], adapt_hi=adapt[1], kl_index=kl_index, max_norm=max_norm,
+                 b1_main=betas_main[0], b2_main=betas_main[1], eps_main=eps_main, b1_est=betas_est[0],
+                 b2_est=betas_est[1], eps_est=eps_est, est_lr=est_lr, desired_kl=desired_kl,
+                 lr64=lr64.data_ptr(), lr32=lr32.data_ptr(), step_main=step_main.data_ptr(),
+                 step_est=step_est.data_ptr(), sums=sums.data_ptr(), nloss=len(loss_ptrs), ws=ws.data_ptr(),
+                 counter=counter.data_ptr())
+    for k, t in enumerate(loss_ptrs):
+        a.loss_ptrs[k] = t.data_ptr()
+    _check(lib().lgx_ppo_tail(C.byref(a), _stream()), "lgx_ppo_tail")
