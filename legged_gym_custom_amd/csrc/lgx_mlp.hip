@@ -531,13 +531,29 @@ __device__ void block_sum(float (&v)[NV], float* red) {
     for (int k = 0; k < NV; ++k) v[k] = red[k] + red[NV + k] + red[2 * NV + k] + red[3 * NV + k];
 }
 
-// last block to finish sums the per-block partials in block order (deterministic)
+// The last block to finish reduces the per-block partials (agent-scope release by every
+// writer before the counter; acquire by the last block before it reads them).
 __device__ bool last_block(uint32_t* counter) {
   __shared__ bool last;
   __threadfence();
   if (threadIdx.x == 0) last = atomicAdd(counter, 1u) == gridDim.x - 1;
   __syncthreads();
+  if (last) __threadfence();
   return last;
+}
+
+// Sum of the NV-wide partial rows ws[b * stride + k] over b < nblk, by the whole block: a
+// fixed assignment (thread t takes rows t, t + 256, ...) and the fixed block_sum tree, so
+// the result is deterministic for a given grid. Thread 0 holds the totals.
+template <int NV>
+__device__ void final_sum(const float* ws, int stride, int nblk, float (&v)[NV], float* red) {
+#pragma unroll
+  for (int k = 0; k < NV; ++k) v[k] = 0.f;
+  for (int b = threadIdx.x; b < nblk; b += blockDim.x)
+#pragma unroll
+    for (int k = 0; k < NV; ++k) v[k] += ws[b * stride + k];
+  __syncthreads();  // red is reused
+  block_sum<NV>(v, red);
 }
 
 struct HeadRow {
@@ -589,19 +605,18 @@ __global__ void ppo_head_fwd(lgx_ppo_head_args p) {
   if (threadIdx.x == 0)
     for (int k = 0; k < 3; ++k) p.ws[blockIdx.x * 3 + k] = v[k];
   if (last_block(p.counter)) {
-    // threads k < 3 each sum one quantity over the blocks, in block order
-    if (threadIdx.x < 3) {
-      float t = 0.f;
-      for (int b = 0; b < (int)gridDim.x; ++b) t += p.ws[b * 3 + threadIdx.x];
-      p.out[threadIdx.x == 2 ? 3 : threadIdx.x] = t / p.B;
-      if (threadIdx.x == 2 && p.kl_dst) *p.kl_dst = t / p.B;
-    }
-    if (threadIdx.x == 3) {
+    float t[3];
+    final_sum<3>(p.ws, 3, gridDim.x, t, red);
+    if (threadIdx.x == 0) {
+      p.out[0] = t[0] / p.B;
+      p.out[1] = t[1] / p.B;
+      p.out[3] = t[2] / p.B;
+      if (p.kl_dst) *p.kl_dst = t[2] / p.B;
       float ent = 0.f;
       for (int j = 0; j < p.A; ++j) ent += 0.5f + 0.9189385332046727f + lstd[j];
       p.out[2] = ent;
+      *p.counter = 0u;
     }
-    if (threadIdx.x == 0) *p.counter = 0u;
   }
 }
 
@@ -653,13 +668,12 @@ __global__ void ppo_head_bwd(lgx_ppo_head_args p) {
   if (threadIdx.x == 0)
     for (int j = 0; j < p.A; ++j) p.ws[blockIdx.x * HMAXA + j] = ds[j];
   if (last_block(p.counter)) {
-    const int j = threadIdx.x;
-    if (j < p.A) {  // one action column per thread, blocks in order
-      float t = 0.f;
-      for (int b = 0; b < (int)gridDim.x; ++b) t += p.ws[b * HMAXA + j];
-      p.dstd[j] = t + ge / stdv[j];  // entropy: d(sum_j log std_j)/d std_j
+    float t[HMAXA];
+    final_sum<HMAXA>(p.ws, HMAXA, gridDim.x, t, red);
+    if (threadIdx.x == 0) {
+      for (int j = 0; j < p.A; ++j) p.dstd[j] = t[j] + ge / stdv[j];  // entropy: d(sum_j log std_j)/d std_j
+      *p.counter = 0u;
     }
-    if (j == 0) *p.counter = 0u;
   }
 }
 
@@ -686,12 +700,13 @@ __global__ void aux_loss_fwd(lgx_aux_loss_args p) {
   block_sum<2>(v, red);
   if (threadIdx.x == 0) { p.ws[blockIdx.x * 2] = v[0]; p.ws[blockIdx.x * 2 + 1] = v[1]; }
   if (last_block(p.counter)) {
-    if (threadIdx.x < 2) {
-      float t = 0.f;
-      for (int b = 0; b < (int)gridDim.x; ++b) t += p.ws[b * 2 + threadIdx.x];
-      p.out[threadIdx.x] = t / p.B;
+    float t[2];
+    final_sum<2>(p.ws, 2, gridDim.x, t, red);
+    if (threadIdx.x == 0) {
+      p.out[0] = t[0] / p.B;
+      p.out[1] = t[1] / p.B;
+      *p.counter = 0u;
     }
-    if (threadIdx.x == 0) *p.counter = 0u;
   }
 }
 
@@ -734,9 +749,10 @@ __global__ __launch_bounds__(256) void tail_norms(lgx_ppo_tail_args p) {
   block_sum<2>(v, red);
   if (threadIdx.x == 0) { p.ws[blockIdx.x * 2] = v[0]; p.ws[blockIdx.x * 2 + 1] = v[1]; }
   if (last_block(p.counter)) {
+    float t[2];
+    final_sum<2>(p.ws, 2, gridDim.x, t, red);
     if (threadIdx.x == 0) {
-      float se = 0.f, sm = 0.f;
-      for (int b = 0; b < (int)gridDim.x; ++b) { se += p.ws[b * 2]; sm += p.ws[b * 2 + 1]; }
+      const float se = t[0], sm = t[1];
       float* sc = p.ws + 2 * TAIL_BLOCKS;  // [coef_e, coef_m]
       sc[0] = fminf(p.max_norm / (sqrtf(se) + 1e-6f), 1.f);
       sc[1] = fminf(p.max_norm / (sqrtf(sm) + 1e-6f), 1.f);
