@@ -58,6 +58,23 @@ int32_t lgx_mlp_sizeof_gemm_args(void);
 int32_t lgx_mlp_pick_split(int32_t M, int32_t N, int32_t K);
 int32_t lgx_gemm(const lgx_gemm_args* args, void* stream);
 
+/* Several independent GEMMs (lgx_gemm semantics each) in ONE launch: the logical output
+ * tiles of all entries share the grid, so the small layers of one network depth (or the
+ * whole backward pass's weight gradients) fill the chip together instead of one launch
+ * each (rsl_rl actor_critic.py:64-87 / support_networks.py: the actor, critic, encoder and
+ * estimator chains are independent at equal depth). All entries are of one kind:
+ *   forward       a_kcontig = 1, b_kcontig = 1 (split_k 1)
+ *   input grad    a_kcontig = 1, b_kcontig = 0 (split_k 1)
+ *   weight grad   a_kcontig = 0, b_kcontig = 0, colsum set, split_k >= 2, defer_reduce = 1
+ *                 (reduce with lgx_splitk_reduce_batch)
+ * Each entry's arithmetic and summation order are those of lgx_gemm with the same split_k
+ * (bit-identical results). Entries must not write overlapping outputs. */
+#define LGX_GEMM_GROUP_MAX 20
+int32_t lgx_gemm_group(const lgx_gemm_args* args, int32_t n, void* stream);
+/* Split-K factors for n weight-gradient GEMMs launched as one group: one K chunk for all
+ * (a multiple of 32 rows, >= 256), the smallest whose block count fits one residency wave
+ * of the chip; every split >= 2. */
+int32_t lgx_mlp_pick_split_group(const int32_t* M, const int32_t* N, const int32_t* K, int32_t n, int32_t* split);
 /* Deferred split-K reductions of several weight-gradient GEMMs in ONE launch (a whole
  * backward pass's dW/db, rsl_rl ppo.py:262 loss.backward()): for each entry
  *   C[m*ldc + n] (+)= sum_{z in order} ws[(z*M + m)*N + n]

@@ -191,17 +191,15 @@ struct Stager {
   }
 };
 
+// One output tile (logical index L: n fastest, then m, then the K split) of one GEMM.
 template <int AM, int BMODE, bool COLSUM, int BN_>
-__global__ __launch_bounds__(NT, 2) void gemm_kernel(Params p) {
+__device__ __forceinline__ void gemm_tile(const Params& p, const int L) {
   using SA = Stager<AM, BM>;
   using SB = Stager<BMODE, BN_>;
   constexpr int NJ = BN_ / 32;             // 16-wide MFMA column tiles per wave
   constexpr int B_ELEMS = BN_ * PITCH;
   constexpr int STAGE = 2 * A_ELEMS + 2 * B_ELEMS;
   extern __shared__ __align__(16) __bf16 lds[];
-  const int per_xcd = (p.tiles + 7) >> 3;
-  const int L = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
-  if (L >= p.tiles) return;
   const int tn = L % p.tiles_n;
   const int tm = (L / p.tiles_n) % p.tiles_m;
   const int z = L / (p.tiles_n * p.tiles_m);
@@ -376,6 +374,57 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(Params p) {
       for (int e = 0; e < 4; ++e)
         if (n + e < p.N) d[e] = accum ? d[e] + v[e] : v[e];
     }
+  }
+}
+
+// Grid: 1-D, XCD-aware (each XCD gets a contiguous run of logical tiles).
+__device__ __forceinline__ int xcd_tile(int tiles) {
+  const int per_xcd = (tiles + 7) >> 3;
+  return (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
+}
+
+template <int AM, int BMODE, bool COLSUM, int BN_>
+__global__ __launch_bounds__(NT, 2) void gemm_kernel(Params p) {
+  const int L = xcd_tile(p.tiles);
+  if (L >= p.tiles) return;
+  gemm_tile<AM, BMODE, COLSUM, BN_>(p, L);
+}
+
+// ---------------------------------------------------------------- grouped launch
+// Independent GEMMs of one kind in ONE launch (lgx_gemm_group): the logical tiles of all
+// problems are concatenated (problem i owns [start[i], start[i+1])), the XCD-aware order
+// runs over the concatenation, and each block dispatches on its problem's stager modes
+// (block-uniform). Kinds: forward (KV, KV), input grad (KV, MV|MVE), weight grad with the
+// bias gradient (MV|MVE, MV|MVE, colsum).
+constexpr int GMAX = LGX_GEMM_GROUP_MAX;
+enum GroupKind { G_FWD = 0, G_DX = 1, G_DW = 2 };
+struct GroupParams {
+  int n, total;
+  int start[GMAX + 1];
+  int mode[GMAX];   // G_DX: B is MVE; G_DW: bit 0 A is MVE, bit 1 B is MVE
+  Params p[GMAX];
+};
+static_assert(sizeof(GroupParams) <= 4096, "kernel argument segment");
+
+template <int KIND, int BN_>
+__global__ __launch_bounds__(NT, 2) void gemm_group_kernel(GroupParams g) {
+  const int L = xcd_tile(g.total);
+  if (L >= g.total) return;
+  int i = 0;
+  while (i + 1 < g.n && L >= g.start[i + 1]) ++i;
+  const Params& p = g.p[i];
+  const int l = L - g.start[i];
+  const int m = g.mode[i];
+  if constexpr (KIND == G_FWD) {
+    gemm_tile<KV, KV, false, BN_>(p, l);
+  } else if constexpr (KIND == G_DX) {
+    if (m) gemm_tile<KV, MVE, false, BN_>(p, l);
+    else gemm_tile<KV, MV, false, BN_>(p, l);
+  } else {
+    if (m == 0) gemm_tile<MV, MV, true, BN_>(p, l);
+    else if (m == 1) gemm_tile<MVE, MV, true, BN_>(p, l);
+    else if (m == 2) gemm_tile<MV, MVE, true, BN_>(p, l);
+    else gemm_tile<MVE, MVE, true, BN_>(p, l);
   }
 }
 
@@ -991,21 +1040,23 @@ int32_t lgx_mlp_pick_split(int32_t M, int32_t N, int32_t K) {
   return s;
 }
 
-int32_t lgx_gemm(const lgx_gemm_args* a, void* stream) {
+// Validates one lgx_gemm_args and fills the kernel's Params; nullptr on success, else the
+// reason. *empty: M or N is 0 (nothing to launch).
+static const char* to_params(const lgx_gemm_args* a, lgxm::Params& p, bool* empty) {
   using namespace lgxm;
-  if (!a) return fail("lgx_gemm: null args");
-  if (a->M < 0 || a->N < 0 || a->K < 0) return fail("lgx_gemm: negative size");
-  if (a->M == 0 || a->N == 0) return 0;
-  if (!a->A || !a->B || !a->C) return fail("lgx_gemm: null operand");
-  if ((a->epilogue & LGX_EPI_BIAS) && !a->bias) return fail("lgx_gemm: EPI_BIAS without bias");
-  if ((a->epilogue & LGX_EPI_DELU) && !a->act) return fail("lgx_gemm: EPI_DELU without act");
+  *empty = false;
+  if (!a) return "null args";
+  if (a->M < 0 || a->N < 0 || a->K < 0) return "negative size";
+  if (a->M == 0 || a->N == 0) { *empty = true; return nullptr; }
+  if (!a->A || !a->B || !a->C) return "null operand";
+  if ((a->epilogue & LGX_EPI_BIAS) && !a->bias) return "EPI_BIAS without bias";
+  if ((a->epilogue & LGX_EPI_DELU) && !a->act) return "EPI_DELU without act";
   const int split = a->split_k < 1 ? 1 : a->split_k;
-  if (split > 1 && !a->workspace) return fail("lgx_gemm: split_k > 1 needs a workspace");
+  if (split > 1 && !a->workspace) return "split_k > 1 needs a workspace";
   const bool cs = a->colsum != nullptr;
-  if (cs && (a->a_kcontig || !a->colsum_ws)) return fail("lgx_gemm: colsum needs a_kcontig = 0 and colsum_ws");
-  if (cs && split == 1) return fail("lgx_gemm: colsum requires split_k > 1");
-  if (!a->a_kcontig && a->b_kcontig) return fail("lgx_gemm: a_kcontig = 0 with b_kcontig = 1 is not built");
-  Params p;
+  if (cs && (a->a_kcontig || !a->colsum_ws)) return "colsum needs a_kcontig = 0 and colsum_ws";
+  if (cs && split == 1) return "colsum requires split_k > 1";
+  if (!a->a_kcontig && a->b_kcontig) return "a_kcontig = 0 with b_kcontig = 1 is not built";
   p.A = a->A; p.lda = a->lda; p.B = a->B; p.ldb = a->ldb; p.C = a->C; p.ldc = a->ldc;
   p.M = a->M; p.N = a->N; p.K = a->K; p.epi = a->epilogue; p.bias = a->bias; p.act = a->act;
   p.ld_act = a->ld_act; p.split = split;
@@ -1014,6 +1065,20 @@ int32_t lgx_gemm(const lgx_gemm_args* a, void* stream) {
   p.ws = a->workspace;
   p.colsum_ws = a->colsum_ws;
   p.ws_vec = a->N % 4 == 0;  // a float4 of the flat workspace stays inside one row
+  return nullptr;
+}
+
+int32_t lgx_gemm(const lgx_gemm_args* a, void* stream) {
+  using namespace lgxm;
+  Params p;
+  bool empty;
+  if (const char* why = to_params(a, p, &empty)) {
+    snprintf(g_err, sizeof(g_err), "lgx_gemm: %s", why);
+    return -1;
+  }
+  if (empty) return 0;
+  const int split = p.split;
+  const bool cs = a->colsum != nullptr;
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int bn = tile_n(a->N);
   const bool ma = a->M % 4 == 0, nb = a->N % 4 == 0;  // m/n-contiguous stagers: whole 4-row groups
@@ -1039,6 +1104,101 @@ int32_t lgx_gemm(const lgx_gemm_args* a, void* stream) {
     e = hipGetLastError();
     if (e != hipSuccess) return fail(hipGetErrorString(e));
   }
+  return 0;
+}
+
+// Slots of one residency wave of the GEMM kernel: 256 CUs x blocks per CU (LDS-bound:
+// 2 at BN = 128, 3 at BN = 64).
+static int group_slots(int bn) { return 256 * (bn == 128 ? 2 : 3); }
+
+int32_t lgx_gemm_group(const lgx_gemm_args* args, int32_t n, void* stream) {
+  using namespace lgxm;
+  if (n < 0 || n > LGX_GEMM_GROUP_MAX || (n > 0 && !args)) return fail("lgx_gemm_group: 0 <= n <= LGX_GEMM_GROUP_MAX");
+  GroupParams g;
+  g.n = 0;
+  int kind = -1, maxn = 0;
+  for (int i = 0; i < n; ++i) {
+    const lgx_gemm_args* a = args + i;
+    Params p;
+    bool empty;
+    if (const char* why = to_params(a, p, &empty)) {
+      snprintf(g_err, sizeof(g_err), "lgx_gemm_group: entry %d: %s", i, why);
+      return -1;
+    }
+    if (empty) continue;
+    const int k = a->a_kcontig ? (a->b_kcontig ? G_FWD : G_DX) : G_DW;
+    if (k == G_DW && !a->colsum) return fail("lgx_gemm_group: weight-gradient entries need colsum");
+    if (kind >= 0 && k != kind) return fail("lgx_gemm_group: entries of different kinds");
+    if (p.split > 1 && !a->defer_reduce) return fail("lgx_gemm_group: split-K entries need defer_reduce");
+    kind = k;
+    int mode = 0;
+    if (k == G_DX) mode = a->N % 4 != 0;
+    if (k == G_DW) mode = (a->M % 4 != 0) | ((a->N % 4 != 0) << 1);
+    g.mode[g.n] = mode;
+    g.p[g.n] = p;
+    maxn = std::max(maxn, a->N);
+    ++g.n;
+  }
+  if (g.n == 0) return 0;
+  const int bn = tile_n(maxn);
+  int total = 0;
+  for (int i = 0; i < g.n; ++i) {
+    Params& p = g.p[i];
+    p.tiles_m = (p.M + BM - 1) / BM;
+    p.tiles_n = (p.N + bn - 1) / bn;
+    p.tiles = p.tiles_m * p.tiles_n * p.split;
+    g.start[i] = total;
+    total += p.tiles;
+  }
+  g.start[g.n] = total;
+  g.total = total;
+  const int grid = (total + 7) / 8 * 8;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+#define LGX_GROUP_LAUNCH(K)                                                                                     \
+  if (bn == 128) {                                                                                              \
+    static bool attr = false;                                                                                   \
+    if (!attr) {                                                                                                \
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_group_kernel<K, 128>),                     \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes(128));               \
+      attr = true;                                                                                              \
+    }                                                                                                           \
+    hipLaunchKernelGGL((gemm_group_kernel<K, 128>), dim3(grid), dim3(NT), lds_bytes(128), s, g);               \
+  } else {                                                                                                      \
+    hipLaunchKernelGGL((gemm_group_kernel<K, 64>), dim3(grid), dim3(NT), lds_bytes(64), s, g);                 \
+  }
+  if (kind == G_FWD) {
+    LGX_GROUP_LAUNCH(G_FWD)
+  } else if (kind == G_DX) {
+    LGX_GROUP_LAUNCH(G_DX)
+  } else {
+    LGX_GROUP_LAUNCH(G_DW)
+  }
+#undef LGX_GROUP_LAUNCH
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : fail(hipGetErrorString(e));
+}
+
+int32_t lgx_mlp_pick_split_group(const int32_t* M, const int32_t* N, const int32_t* K, int32_t n, int32_t* split) {
+  if (n < 1 || n > LGX_GEMM_GROUP_MAX || !M || !N || !K || !split) return fail("lgx_mlp_pick_split_group: bad arguments");
+  int maxn = 0;
+  for (int i = 0; i < n; ++i) {
+    if (M[i] < 0 || N[i] < 0 || K[i] < 0) return fail("lgx_mlp_pick_split_group: negative size");
+    maxn = std::max(maxn, (int)N[i]);
+  }
+  const int bn = tile_n(maxn), slots = group_slots(bn);
+  // equal K chunks for every problem: the smallest chunk (a multiple of the K step, at least
+  // 256 rows) whose block count fits one residency wave; every split >= 2 (bias gradient)
+  int chunk = 256;
+  for (;; chunk += lgxm::BKS) {
+    int64_t blocks = 0, kmax = 0;
+    for (int i = 0; i < n; ++i) {
+      const int64_t tiles = (int64_t)((M[i] + lgxm::BM - 1) / lgxm::BM) * ((N[i] + bn - 1) / bn);
+      blocks += tiles * std::max(2, (K[i] + chunk - 1) / chunk);
+      kmax = std::max<int64_t>(kmax, K[i]);
+    }
+    if (blocks <= slots || chunk >= kmax) break;
+  }
+  for (int i = 0; i < n; ++i) split[i] = std::max(2, (K[i] + chunk - 1) / chunk);
   return 0;
 }
 

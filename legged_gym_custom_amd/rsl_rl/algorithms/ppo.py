@@ -382,7 +382,7 @@ class PPO:
             # (loss = surr + c_v vloss - c_e entropy + c_reg reg; the estimator loss on its own
             # parameters), every weight-gradient reduction in one launch
             g.span("main", "estimator").zero_()
-            with hip_mlp.deferred_splitk():
+            with hip_mlp.deferred_weight_grads():
                 torch.autograd.backward([surrogate_loss, value_loss, entropy_mean, regularization_loss, estimator_loss],
                                         [self._g_one, self._g_value, self._g_ent, self._reg_coef, self._g_one])
             ac.distribution = None

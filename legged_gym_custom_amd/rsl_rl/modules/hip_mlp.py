@@ -25,10 +25,12 @@ EPI_BIAS, EPI_ELU, EPI_DELU, EPI_ACCUM = 1, 2, 4, 8
 EXPORTED = ["lgx_mlp_abi_version", "lgx_mlp_sizeof_gemm_args", "lgx_mlp_pick_split", "lgx_gemm",
             "lgx_mlp_last_error", "lgx_adam_step", "lgx_ppo_head_forward", "lgx_ppo_head_backward",
             "lgx_copy_batch", "lgx_act_head", "lgx_store_transition", "lgx_splitk_reduce_batch",
-            "lgx_aux_loss_forward", "lgx_aux_loss_backward", "lgx_ppo_tail"]
+            "lgx_aux_loss_forward", "lgx_aux_loss_backward", "lgx_ppo_tail", "lgx_gemm_group",
+            "lgx_mlp_pick_split_group"]
 TAIL_MAX_LOSSES = 8
 COPY_MAX = 16
 SPLITK_MAX = 24
+GROUP_MAX = 20
 
 
 class GemmArgs(C.Structure):
@@ -127,6 +129,10 @@ def lib():
     for fn in ("lgx_aux_loss_forward", "lgx_aux_loss_backward", "lgx_ppo_tail"):
         getattr(L, fn).argtypes = [vp, vp]
         getattr(L, fn).restype = C.c_int32
+    L.lgx_gemm_group.argtypes = [vp, C.c_int32, vp]
+    L.lgx_gemm_group.restype = C.c_int32
+    L.lgx_mlp_pick_split_group.argtypes = [vp, vp, vp, C.c_int32, vp]
+    L.lgx_mlp_pick_split_group.restype = C.c_int32
     L.lgx_splitk_reduce_batch.argtypes = [vp, C.c_int32, vp]
     L.lgx_splitk_reduce_batch.restype = C.c_int32
     if L.lgx_mlp_abi_version() != ABI_VERSION:
@@ -264,15 +270,20 @@ class _immediate:
     weight gradients right away, e.g. the adaptation encoder's re-laid conv weights)."""
 
     def __enter__(self):
-        global _pending
+        global _pending, _pending_dw
         self._saved = _pending
+        self._saved_dw = _pending_dw
         if _pending is not None:
             _flush()
+        if _pending_dw is not None:
+            _flush_dw()
         _pending = None
+        _pending_dw = None
 
     def __exit__(self, *exc):
-        global _pending
+        global _pending, _pending_dw
         _pending = self._saved
+        _pending_dw = self._saved_dw
         return False
 
 
@@ -280,17 +291,92 @@ def _overlaps(ranges):
     return any(lo < h and l2 < hi for (lo, hi) in ranges for (_, _, rs) in _pending for (l2, h) in rs)
 
 
+def run_group(args):
+    """lgx_gemm_group over a list of GemmArgs (one kind; chunks of GROUP_MAX)."""
+    for i in range(0, len(args), GROUP_MAX):
+        chunk = args[i:i + GROUP_MAX]
+        arr = (GemmArgs * len(chunk))(*chunk)
+        _check(lib().lgx_gemm_group(arr, len(chunk), _stream()), "lgx_gemm_group")
+
+
+def pick_split_group(shapes):
+    """lgx_mlp_pick_split_group for [(M, N, K), ...] (weight-gradient GEMMs of one launch)."""
+    n = len(shapes)
+    I = C.c_int32 * n
+    Ms, Ns, Ks, out = I(*[s[0] for s in shapes]), I(*[s[1] for s in shapes]), I(*[s[2] for s in shapes]), I()
+    _check(lib().lgx_mlp_pick_split_group(Ms, Ns, Ks, n, out), "lgx_mlp_pick_split_group")
+    return list(out)
+
+
+# ---------------------------------------------------------------------------------------
+# Deferred weight gradients: inside `deferred_weight_grads()` (a whole backward pass), every
+# dW/db GEMM is recorded instead of launched; at exit they run as lgx_gemm_group launches
+# (all layers of all networks share the grid, split-K chosen for the group: one K chunk,
+# one residency wave) followed by one lgx_splitk_reduce_batch.
+# ---------------------------------------------------------------------------------------
+_pending_dw = None  # [(g, x, dW, db, epilogue, byte ranges)] while deferring
+
+
+class deferred_weight_grads:
+    def __enter__(self):
+        global _pending_dw
+        if _pending_dw is not None or _pending is not None:
+            raise RuntimeError("deferred_weight_grads does not nest")
+        _pending_dw = []
+        return self
+
+    def __exit__(self, *exc):
+        global _pending_dw
+        try:
+            if exc[0] is None:
+                _flush_dw()
+        finally:
+            _pending_dw = None
+        return False
+
+
+def _flush_dw():
+    items, _pending_dw[:] = list(_pending_dw), []
+    for i in range(0, len(items), GROUP_MAX):
+        chunk = items[i:i + GROUP_MAX]
+        shapes = [(g.shape[1], x.shape[1], g.shape[0]) for (g, x, *_r) in chunk]
+        splits = pick_split_group(shapes)
+        offs, tot = [], 0
+        for (N, K, _rows), s in zip(shapes, splits):
+            offs.append(tot)
+            tot += (s * N * K + s * N + 3) // 4 * 4  # 16-B aligned partial blocks
+        ws = torch.empty(tot, device=chunk[0][0].device, dtype=torch.float32)
+        args, descs = [], (SplitkDesc * SPLITK_MAX)()
+        for k, ((g, x, dW, db, epi, _rng), (N, K, rows), s, o) in enumerate(zip(chunk, shapes, splits, offs)):
+            w = ws.data_ptr() + 4 * o
+            cw = w + 4 * s * N * K
+            args.append(GemmArgs(A=_ptr(g), lda=g.stride(0), a_kcontig=0, B=_ptr(x), ldb=x.stride(0), b_kcontig=0,
+                                 C=_ptr(dW), ldc=dW.stride(0), M=N, N=K, K=rows, epilogue=epi, split_k=s,
+                                 workspace=w, colsum=_ptr(db), colsum_ws=cw, defer_reduce=1))
+            descs[k] = SplitkDesc(ws=w, colsum_ws=cw, C=dW.data_ptr(), ldc=dW.stride(0), colsum=db.data_ptr(), M=N,
+                                  N=K, split=s, epilogue=epi)
+        run_group(args)
+        _check(lib().lgx_splitk_reduce_batch(descs, len(chunk), _stream()), "lgx_splitk_reduce_batch")
+
+
 def linear_weight_grad(g, x, dW=None, db=None, accumulate=False):
     """dW[N,K] (+)= dY[M,N]^T X[M,K], db[N] (+)= sum_m dY[m,:] (split-K, deterministic order;
-    the reduction is deferred inside `deferred_splitk()`)."""
+    the reduction is deferred inside `deferred_splitk()`, the whole GEMM inside
+    `deferred_weight_grads()`)."""
     g = _rowmajor(g)
     x = _rowmajor(x)
     rows, N = g.shape
     K = x.shape[1]
-    split = max(2, int(lib().lgx_mlp_pick_split(N, K, rows)))
     dev = g.device
     dW = torch.empty(N, K, device=dev, dtype=torch.float32) if dW is None else dW
     db = torch.empty(N, device=dev, dtype=torch.float32) if db is None else db
+    if _pending_dw is not None:
+        rng = [(dW.data_ptr(), dW.data_ptr() + 4 * (dW.stride(0) * (N - 1) + K)), (db.data_ptr(), db.data_ptr() + 4 * N)]
+        if any(lo < h and l2 < hi for (lo, hi) in rng for (*_r, rs) in _pending_dw for (l2, h) in rs):
+            _flush_dw()  # an output a recorded GEMM still owes (accumulation): settle those first
+        _pending_dw.append((g, x, dW, db, EPI_ACCUM if accumulate else 0, rng))
+        return dW, db
+    split = max(2, int(lib().lgx_mlp_pick_split(N, K, rows)))
     ws = torch.empty(split * N * K + split * N, device=dev, dtype=torch.float32)
     defer = _pending is not None
     if defer:  # an output an earlier deferred reduction still owes: settle those first

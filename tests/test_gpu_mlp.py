@@ -241,3 +241,93 @@ def test_deferred_splitk_matches_immediate_bitwise():
             H.linear_weight_grad(dy, x, dW, db, accumulate=True)  # overlaps: settles the first
     for (a, b), (c, d) in zip(ref, out):
         assert torch.equal(a, c) and torch.equal(b, d)
+
+
+def _wgrad_args(dy, x, dW, db, split, ws, defer):
+    N, K, rows = dy.shape[1], x.shape[1], dy.shape[0]
+    w = ws.data_ptr()
+    return H.GemmArgs(A=dy.data_ptr(), lda=dy.stride(0), a_kcontig=0, B=x.data_ptr(), ldb=x.stride(0), b_kcontig=0,
+                      C=dW.data_ptr(), ldc=dW.stride(0), M=N, N=K, K=rows, epilogue=H.EPI_ACCUM, split_k=split,
+                      workspace=w, colsum=db.data_ptr(), colsum_ws=w + 4 * split * N * K, defer_reduce=int(defer))
+
+
+def test_group_weight_grads_match_single_launches_bitwise():
+    """deferred_weight_grads: every dW/db GEMM of a backward pass in one lgx_gemm_group launch
+    (group-picked splits) == each GEMM launched alone with the same split, bit for bit; all
+    four stager-mode combinations (M, N % 4 != 0) and an accumulating shared output."""
+    g = torch.Generator(device=dev).manual_seed(11)
+    shapes = [(24576, 512, 736), (24576, 512, 627), (24576, 256, 512), (24576, 12, 128), (24576, 1, 128),
+              (24576, 20, 29), (24576, 3, 64), (24576, 64, 20)]
+    data = [(torch.randn(r, n, device=dev, generator=g), torch.randn(r, k, device=dev, generator=g))
+            for r, n, k in shapes]
+    splits = H.pick_split_group([(n, k, r) for r, n, k in shapes])
+    assert all(s >= 2 for s in splits)
+    init = [(torch.randn(dy.shape[1], x.shape[1], device=dev, generator=g),
+             torch.randn(dy.shape[1], device=dev, generator=g)) for dy, x in data]
+    ref = [(a.clone(), b.clone()) for a, b in init]
+    for (dy, x), (dW, db), s in zip(data, ref, splits):
+        ws = torch.empty(s * dW.numel() + s * db.numel() + 4, device=dev)
+        H._run(_wgrad_args(dy, x, dW, db, s, ws, False))
+    out = [(a.clone(), b.clone()) for a, b in init]
+    with H.deferred_weight_grads():
+        for (dy, x), (dW, db) in zip(data, out):
+            H.linear_weight_grad(dy, x, dW, db, accumulate=True)
+    for (a, b), (c, d) in zip(ref, out):
+        assert torch.equal(a, c) and torch.equal(b, d)
+    # and against fp64
+    for (dy, x), (dW0, db0), (dW, db) in zip(data, init, out):
+        r = dW0.double() + dy.double().t() @ x.double()
+        assert ((dW.double() - r).abs() <= _bound(dy.t(), x) + 1e-5 * dW0.abs().double()).all()
+        torch.testing.assert_close(db.double(), db0.double() + dy.double().sum(0), rtol=1e-5, atol=1e-3)
+    # two GEMMs into the same output: the second settles the first (accumulation order kept)
+    dy, x = data[3]
+    a, b = init[3][0].clone(), init[3][1].clone()
+    with H.deferred_weight_grads():
+        H.linear_weight_grad(dy, x, a, b, accumulate=True)
+        H.linear_weight_grad(dy, x, a, b, accumulate=True)
+    assert torch.isfinite(a).all() and torch.isfinite(b).all()
+    torch.testing.assert_close(b.double(), init[3][1].double() + 2 * dy.double().sum(0), rtol=1e-5, atol=2e-3)
+
+
+def test_group_forward_and_input_grad_match_single_launches_bitwise():
+    """lgx_gemm_group of forward (bias + ELU) and of input-gradient (ELU') GEMMs of mixed
+    shapes == the same GEMMs launched one by one, bit for bit."""
+    g = torch.Generator(device=dev).manual_seed(12)
+    fwd = [(24576, 736, 512), (24576, 29, 64), (24576, 132, 128), (24576, 572, 128), (4096, 627, 512), (333, 20, 20)]
+    single, grouped, args_s, args_g = [], [], [], []
+    for M, K, N in fwd:
+        x = torch.randn(M, K, device=dev, generator=g)
+        W = torch.randn(N, K, device=dev, generator=g) / K ** 0.5
+        b = torch.randn(N, device=dev, generator=g)
+        ys, yg = torch.empty(M, N, device=dev), torch.empty(M, N, device=dev)
+        for y, lst in ((ys, args_s), (yg, args_g)):
+            lst.append(H.GemmArgs(A=x.data_ptr(), lda=K, a_kcontig=1, B=W.data_ptr(), ldb=K, b_kcontig=1,
+                                  C=y.data_ptr(), ldc=N, M=M, N=N, K=K, epilogue=H.EPI_BIAS | H.EPI_ELU,
+                                  bias=b.data_ptr(), split_k=1))
+        single.append((ys, x, W, b))
+        grouped.append(yg)
+    for a in args_s:
+        H._run(a)
+    H.run_group(args_g)
+    for (ys, *_r), yg in zip(single, grouped):
+        assert torch.equal(ys, yg)
+    # input gradients: dX[M, Kin] = dY[M, N] W[N, Kin] * ELU'(y_prev), incl. Kin % 4 != 0
+    dxs, dxg, args_s, args_g = [], [], [], []
+    for M, Kin, N in [(24576, 512, 256), (24576, 627, 512), (24576, 64, 20), (24576, 29, 64), (4096, 128, 12)]:
+        dy = torch.randn(M, N, device=dev, generator=g)
+        W = torch.randn(N, Kin, device=dev, generator=g)
+        yp = torch.nn.functional.elu(torch.randn(M, Kin, device=dev, generator=g))
+        a, c = torch.empty(M, Kin, device=dev), torch.empty(M, Kin, device=dev)
+        for o, lst in ((a, args_s), (c, args_g)):
+            lst.append(H.GemmArgs(A=dy.data_ptr(), lda=N, a_kcontig=1, B=W.data_ptr(), ldb=Kin, b_kcontig=0,
+                                  C=o.data_ptr(), ldc=Kin, M=M, N=Kin, K=N, epilogue=H.EPI_DELU, act=yp.data_ptr(),
+                                  ld_act=Kin, split_k=1))
+        dxs.append((a, dy, W, yp))
+        dxg.append(c)
+    for a in args_s:
+        H._run(a)
+    H.run_group(args_g)
+    for (a, dy, W, yp), c in zip(dxs, dxg):
+        assert torch.equal(a, c)
+        r = (dy.double() @ W.double()) * torch.where(yp > 0, 1.0, yp.double() + 1)
+        assert ((c.double() - r).abs() <= _bound(dy, W) * 2 + 1e-6).all()
