@@ -279,24 +279,34 @@ class PPO:
         """ppo.py:129-153: the rollout actor sees the ESTIMATOR's output (Q12). The
         observations are stored at act time (RolloutStorage.record_observations): the env
         overwrites its buffers in place during the step that follows."""
-        estimated_obs = self.estimator(obs)
         t = self.transition
-        (t.observations, t.privileged_observations, t.critic_observations, t.true_estimated_observations,
-         t.scan_observations) = self.storage.record_observations(obs, privileged_obs, critic_obs, true_estimated_obs,
-                                                                 scan_obs)
         ac = self.actor_critic
         if self._gpu_rollout():
-            # one HIP kernel samples a = mu + std * eps and writes actions, mu, sigma and the
-            # Normal log-prob straight into this step's storage rows (lgx_act_head)
+            (t.observations, t.privileged_observations, t.critic_observations, t.true_estimated_observations,
+             t.scan_observations) = self.storage.record_observations(obs, privileged_obs, critic_obs,
+                                                                     true_estimated_obs, scan_obs)
+            # the estimator, privileged/scan encoders and critic read only observations: one
+            # grouped launch per depth (hip_mlp.forward_group), then the actor; one HIP kernel
+            # samples a = mu + std * eps and writes actions, mu, sigma and the Normal
+            # log-prob straight into this step's storage rows (lgx_act_head)
             s, k = self.storage, self.storage.step
             with torch.no_grad():
-                mean = ac._actor_mean(obs, privileged_obs, estimated_obs, scan_obs, adaptation_mode)
+                items = [self.estimator.group_item(obs), ac.scan_encoder.group_item(scan_obs), (ac.critic, critic_obs)]
+                if not adaptation_mode:
+                    items.append(ac.privileged_encoder_.group_item(privileged_obs))
+                outs = hip_mlp.forward_group(items)
+                estimated_obs, scan_latent, t.values = outs[:3]
+                latent = ac.adaptation_encoder(obs) if adaptation_mode else outs[3]
+                mean = ac.actor_forward(obs, latent, scan_latent, estimated_obs)
                 eps = torch.randn_like(mean)
                 hip_mlp.act_head(mean, ac.std.detach(), eps, s.actions[k], s.mu[k], s.sigma[k], s.actions_log_prob[k])
-                t.values = ac.evaluate(critic_obs)
             t.actions, t.action_mean, t.action_sigma = s.actions[k], s.mu[k], s.sigma[k]
             t.actions_log_prob = s.actions_log_prob[k].view(-1)
             return t.actions
+        estimated_obs = self.estimator(obs)
+        (t.observations, t.privileged_observations, t.critic_observations, t.true_estimated_observations,
+         t.scan_observations) = self.storage.record_observations(obs, privileged_obs, critic_obs, true_estimated_obs,
+                                                                 scan_obs)
         t.actions = ac.act(obs, privileged_obs, estimated_obs, scan_obs, adaptation_mode).detach()
         t.values = ac.evaluate(critic_obs).detach()
         t.actions_log_prob = ac.get_actions_log_prob(t.actions).detach()
@@ -363,10 +373,12 @@ class PPO:
             # regulariser (the reference evaluates the same encoder on the same input twice,
             # ppo.py:190,204)
             adaptive = self.desired_kl is not None and self.schedule == "adaptive"
-            priv_latent = ac.privileged_encoder(priv_b)
-            scan_latent = ac.scan_encoder(scan_b)
+            # the privileged/scan encoders, critic and estimator read only the minibatch: one
+            # autograd node, one grouped launch per depth each way (hip_mlp.forward_group)
+            priv_latent, scan_latent, value_b, pred = hip_mlp.forward_group(
+                [ac.privileged_encoder_.group_item(priv_b), ac.scan_encoder.group_item(scan_b), (ac.critic, critic_b),
+                 self.estimator.group_item(obs_b)])
             mu_b = ac.actor_forward(obs_b, priv_latent, scan_latent, est_b)  # TRUE est obs (Q12)
-            value_b = ac.evaluate(critic_b)
             surrogate_loss, value_loss, entropy_mean, _kl = hip_mlp.ppo_head(
                 mu_b, value_b, ac.std, actions_b, old_logp_b, adv_b, target_values_b, returns_b, old_mu_b, old_sigma_b,
                 self.clip_param, self.use_clipped_value_loss, kl_dst=g.segment("kl") if adaptive else None,
@@ -374,7 +386,6 @@ class PPO:
             # sg(z_adapt): the adaptation encoder only trains in DAgger iterations, so over a
             # PPO update its latents are fixed — computed once per update (_adapt_all)
             adapt_latent = self._adapt_all[idx]  # (shuffled order, like the rows)
-            pred = self.estimator(obs_b)
             regularization_loss, estimator_loss = hip_mlp.aux_losses(priv_latent, adapt_latent, pred, est_b,
                                                                      out=self._aux_out)
             # zero_grad of `optimizer` and `estimator_optimizer` (adaptation grads stay), then

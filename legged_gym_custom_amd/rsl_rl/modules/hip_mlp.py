@@ -548,6 +548,151 @@ class HipMLP(nn.Sequential):
 
 
 # ---------------------------------------------------------------------------------------
+# Independent chains at equal depth in one launch per depth (lgx_gemm_group): the update's
+# privileged/scan encoders, critic and estimator (ppo.py:186-206) and the rollout's
+# (ppo.py:129-153) read only data, so layer d of every chain shares one grid. Backward
+# aligns the chains at their outputs (step t = each chain's layer n - 1 - t): one grouped
+# input-gradient launch per step; weight gradients as in _MLPFunction (deferred inside
+# deferred_weight_grads()). Forward / input-gradient results equal the per-chain launches
+# bit for bit.
+# ---------------------------------------------------------------------------------------
+def _fwd_args(h, W, b, elu, y):
+    M, K = h.shape
+    N = W.shape[0]
+    return GemmArgs(A=_ptr(h), lda=h.stride(0), a_kcontig=1, B=_ptr(W), ldb=W.stride(0), b_kcontig=1, C=_ptr(y),
+                    ldc=y.stride(0), M=M, N=N, K=K, epilogue=EPI_BIAS | (EPI_ELU if elu else 0), bias=_ptr(b),
+                    split_k=1)
+
+
+def _dx_args(g, W, y_prev, dx):
+    M, N = g.shape
+    K = W.shape[1]
+    return GemmArgs(A=_ptr(g), lda=g.stride(0), a_kcontig=1, B=_ptr(W), ldb=W.stride(0), b_kcontig=0, C=_ptr(dx),
+                    ldc=dx.stride(0), M=M, N=K, K=N, epilogue=EPI_DELU if y_prev is not None else 0,
+                    act=_ptr(y_prev), ld_act=0 if y_prev is None else y_prev.stride(0), split_k=1)
+
+
+def _group_forward(xs, chains):
+    """Layer d of every chain in one launch; returns each chain's list of layer outputs."""
+    outs = [[] for _ in chains]
+    hs = [_rowmajor(x) for x in xs]
+    for d in range(max(len(c[2]) for c in chains)):
+        args = []
+        for c, (Ws, bs, flags) in enumerate(chains):
+            if d < len(flags):
+                y = torch.empty(hs[c].shape[0], Ws[d].shape[0], device=hs[c].device, dtype=torch.float32)
+                args.append(_fwd_args(hs[c], Ws[d], bs[d], flags[d], y))
+                outs[c].append(y)
+                hs[c] = y
+        run_group(args)
+    return outs
+
+
+class _GroupFn(torch.autograd.Function):
+    """Several independent chains as one autograd node. meta: per chain (nparts, flags)."""
+
+    @staticmethod
+    def forward(ctx, meta, *flat):
+        xs, chains, params, widths = [], [], [], []
+        i = 0
+        for nparts, flags in meta:
+            parts = flat[i:i + nparts]
+            i += nparts
+            n = len(flags)
+            wb = flat[i:i + 2 * n]
+            i += 2 * n
+            xs.append(parts[0] if nparts == 1 else torch.cat(parts, dim=-1))
+            chains.append((wb[0::2], wb[1::2], flags))
+            params.append(wb)
+            widths.append([t.shape[-1] for t in parts])
+        outs = _group_forward(xs, chains)
+        ctx.meta, ctx.params, ctx.widths = meta, params, widths
+        saved = []
+        for x, wb, o in zip(xs, params, outs):
+            saved += [x, *wb, *o]
+        ctx.save_for_backward(*saved)
+        return tuple(o[-1] for o in outs)
+
+    @staticmethod
+    def backward(ctx, *grad_outs):
+        saved = ctx.saved_tensors
+        meta = ctx.meta
+        st, k, pos, gi = [], 0, 0, 0  # per chain: x, wb, outs, grad, first needs_input_grad index
+        for (nparts, flags), g in zip(meta, grad_outs):
+            n = len(flags)
+            x, wb, outs = saved[k], saved[k + 1:k + 1 + 2 * n], saved[k + 1 + 2 * n:k + 1 + 3 * n]
+            k += 1 + 3 * n
+            if g is not None and flags[-1]:
+                y = outs[-1]
+                g = g * torch.where(y > 0, torch.ones_like(y), y + 1.0)
+            st.append([x, wb, outs, g, pos])
+            pos += nparts + 2 * n
+        part_grads = [[None] * nparts for nparts, _f in meta]
+        for t in range(max(len(f) for _n, f in meta)):
+            args, news = [], []
+            for c, ((nparts, flags), item) in enumerate(zip(meta, st)):
+                x, wb, outs, g, p0 = item
+                n = len(flags)
+                i = n - 1 - t
+                if g is None or i < 0:
+                    continue
+                inp = x if i == 0 else outs[i - 1]
+                if ctx.needs_input_grad[1 + p0 + nparts + 2 * i] or ctx.needs_input_grad[2 + p0 + nparts + 2 * i]:
+                    linear_weight_grad(g, inp, _grad_of(ctx.params[c][2 * i]), _grad_of(ctx.params[c][2 * i + 1]),
+                                       accumulate=True)
+                if i > 0:
+                    dx = torch.empty(g.shape[0], wb[2 * i].shape[1], device=g.device, dtype=torch.float32)
+                    args.append(_dx_args(g, wb[2 * i], outs[i - 1] if flags[i - 1] else None, dx))
+                    news.append((c, dx))
+                    continue
+                need = [ctx.needs_input_grad[1 + p0 + j] for j in range(nparts)]
+                if any(need):  # columns [lo, hi) spanning the parts that need a gradient
+                    offs = [0]
+                    for w in ctx.widths[c]:
+                        offs.append(offs[-1] + w)
+                    first = need.index(True)
+                    last = nparts - 1 - need[::-1].index(True)
+                    lo, hi = offs[first], offs[last + 1]
+                    dx = torch.empty(g.shape[0], hi - lo, device=g.device, dtype=torch.float32)
+                    args.append(_dx_args(g, wb[0][:, lo:hi], None, dx))
+                    for j in range(first, last + 1):
+                        if need[j]:
+                            part_grads[c][j] = dx[:, offs[j] - lo:offs[j + 1] - lo]
+                item[3] = None
+            if args:
+                run_group(args)
+            for c, dx in news:
+                st[c][3] = dx
+        res = [None]
+        for (nparts, flags), pg in zip(meta, part_grads):
+            res += pg + [None] * (2 * len(flags))
+        return tuple(res)
+
+
+def forward_group(items):
+    """Outputs of independent chains [(HipMLP, x or tuple of parts), ...], one launch per
+    depth on the HIP device (autograd-aware); elsewhere each module's own forward."""
+    resolved = []
+    for mod, x in items:
+        parts = tuple(x) if isinstance(x, (tuple, list)) else (x,)
+        chain = mod._chain() if isinstance(mod, HipMLP) and parts[0].device.type == "cuda" else None
+        if chain is None:
+            return [m.forward_parts(tuple(v)) if isinstance(v, (tuple, list)) else m(v) for m, v in items]
+        resolved.append((parts, chain))
+    wbs = [[t for pair in zip([m.weight for m in layers], [m.bias for m in layers]) for t in pair]
+           for _p, (layers, _f) in resolved]
+    needs_graph = torch.is_grad_enabled() and any(
+        t.requires_grad for (parts, _c), wb in zip(resolved, wbs) for t in (*parts, *wb))
+    if not needs_graph:
+        xs = [p[0] if len(p) == 1 else torch.cat(p, dim=-1) for p, _c in resolved]
+        chains = [([m.weight for m in layers], [m.bias for m in layers], flags) for _p, (layers, flags) in resolved]
+        return [o[-1] for o in _group_forward(xs, chains)]
+    meta = tuple((len(parts), tuple(flags)) for parts, (_l, flags) in resolved)
+    flat = [t for (parts, _c), wb in zip(resolved, wbs) for t in (*parts, *wb)]
+    return list(_GroupFn.apply(meta, *flat))
+
+
+# ---------------------------------------------------------------------------------------
 # Adaptation encoder (support_networks.py:116-175): Linear(P->30)+ELU per history step,
 # Conv1d(30->20, k4, s2)+ELU, Conv1d(20->10, k2, s1)+ELU, Flatten, Linear(30->out)+ELU.
 # Kept channels-last ([B, time, ch]) so every conv1d output position t reads ONE

@@ -37,6 +37,10 @@ class ScanEncoder(nn.Module):
     def forward(self, scan_obs):
         return self.scan_encoder(scan_obs)
 
+    def group_item(self, scan_obs):
+        """(chain, input) of forward() for hip_mlp.forward_group."""
+        return self.scan_encoder, scan_obs
+
 
 class MlpEstimator(nn.Module):
     def __init__(self, num_proprio, history_buffer_length, output_dim, hidden_dims=[128, 64], activation="elu",
@@ -54,6 +58,10 @@ class MlpEstimator(nn.Module):
             return self.estimator(obs_with_history)
         return self.estimator(obs_with_history[:, -self.num_proprio:])
 
+    def group_item(self, obs_with_history):
+        """(chain, input) of forward() for hip_mlp.forward_group."""
+        return self.estimator, obs_with_history if self.use_history else obs_with_history[:, -self.num_proprio:]
+
 
 class PrivilegedEncoder(nn.Module):
     def __init__(self, num_privileged_obs, output_dim=20, hidden_dims=[64, 20], activation="elu"):
@@ -66,6 +74,10 @@ class PrivilegedEncoder(nn.Module):
 
     def forward(self, privileged_obs):
         return self.priv_encoder(privileged_obs)
+
+    def group_item(self, privileged_obs):
+        """(chain, input) of forward() for hip_mlp.forward_group."""
+        return self.priv_encoder, privileged_obs
 
 
 class AdaptationEncoder(nn.Module):

@@ -331,3 +331,41 @@ def test_group_forward_and_input_grad_match_single_launches_bitwise():
         assert torch.equal(a, c)
         r = (dy.double() @ W.double()) * torch.where(yp > 0, 1.0, yp.double() + 1)
         assert ((c.double() - r).abs() <= _bound(dy, W) * 2 + 1e-6).all()
+
+
+def test_forward_group_matches_separate_chains_bitwise():
+    """hip_mlp.forward_group (one launch per depth, one autograd node) == the chains run one
+    by one: outputs, input gradients (incl. a parts input) and parameter gradients, bitwise."""
+    from legged_gym_custom_amd.rsl_rl.modules.support_networks import _mlp
+    torch.manual_seed(3)
+    act = torch.nn.ELU()
+    nets = [_mlp(29, [64, 20], 20, act), _mlp(132, [128, 64], 32, act), _mlp(736, [512, 256, 128], 1, act),
+            _mlp(572, [128, 64], 3, act)]
+    nets = [n.to(dev) for n in nets]
+    B = 3000
+    g = torch.Generator(device=dev).manual_seed(4)
+    xs = [torch.randn(B, d, device=dev, generator=g) for d in (29, 132, 736)]
+    parts = (torch.randn(B, 520, device=dev, generator=g), torch.randn(B, 52, device=dev, generator=g,
+                                                                         requires_grad=True))
+    seeds = [torch.randn(B, o, device=dev, generator=g) for o in (20, 32, 1, 3)]
+
+    def run(grouped):
+        for n in nets:
+            n.zero_grad(set_to_none=True)
+        parts[1].grad = None
+        items = [(nets[0], xs[0]), (nets[1], xs[1]), (nets[2], xs[2]), (nets[3], parts)]
+        with H.deferred_weight_grads():
+            outs = H.forward_group(items) if grouped else [n.forward_parts(x) if isinstance(x, tuple) else n(x)
+                                                           for n, x in items]
+            torch.autograd.backward(outs, seeds)
+        return [o.detach().clone() for o in outs], [p.grad.clone() for n in nets for p in n.parameters()], \
+            parts[1].grad.clone()
+
+    o1, g1, d1 = run(False)
+    o2, g2, d2 = run(True)
+    assert all(torch.equal(a, b) for a, b in zip(o1, o2))
+    assert all(torch.equal(a, b) for a, b in zip(g1, g2))
+    assert torch.equal(d1, d2)
+    with torch.no_grad():
+        o3 = H.forward_group([(nets[0], xs[0]), (nets[1], xs[1]), (nets[2], xs[2]), (nets[3], parts)])
+    assert all(torch.equal(a, b) for a, b in zip(o1, o3))
