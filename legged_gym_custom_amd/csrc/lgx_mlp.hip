@@ -391,16 +391,17 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(Params p) {
 }
 
 // ---------------------------------------------------------------- grouped launch
-// Independent GEMMs of one kind in ONE launch (lgx_gemm_group): the logical tiles of all
-// problems are concatenated (problem i owns [start[i], start[i+1])), the XCD-aware order
-// runs over the concatenation, and each block dispatches on its problem's stager modes
-// (block-uniform). Kinds: forward (KV, KV), input grad (KV, MV|MVE), weight grad with the
-// bias gradient (MV|MVE, MV|MVE, colsum).
+// Independent GEMMs of one kind in ONE launch (lgx_gemm_group). Every problem's logical
+// tiles are spread evenly over the 8 XCDs (XCD x runs a contiguous 1/8 of each problem,
+// problems in the host's order — longest K chunk first), so the per-XCD work stays
+// balanced when the problems' tile costs differ; each block dispatches on its problem's
+// stager modes (block-uniform). Kinds: forward (KV, KV), input grad (KV, MV|MVE), weight
+// grad with the bias gradient (MV|MVE, MV|MVE, colsum).
 constexpr int GMAX = LGX_GEMM_GROUP_MAX;
 enum GroupKind { G_FWD = 0, G_DX = 1, G_DW = 2 };
 struct GroupParams {
-  int n, total;
-  int start[GMAX + 1];
+  int n, per_xcd;    // per_xcd: sum over problems of ceil(tiles_i / 8)
+  int start[GMAX + 1];  // prefix sums of ceil(tiles_i / 8)
   int mode[GMAX];   // G_DX: B is MVE; G_DW: bit 0 A is MVE, bit 1 B is MVE
   Params p[GMAX];
 };
@@ -408,12 +409,13 @@ static_assert(sizeof(GroupParams) <= 4096, "kernel argument segment");
 
 template <int KIND, int BN_>
 __global__ __launch_bounds__(NT, 2) void gemm_group_kernel(GroupParams g) {
-  const int L = xcd_tile(g.total);
-  if (L >= g.total) return;
+  const int x = blockIdx.x & 7, j = blockIdx.x >> 3;
+  if (j >= g.per_xcd) return;
   int i = 0;
-  while (i + 1 < g.n && L >= g.start[i + 1]) ++i;
+  while (i + 1 < g.n && j >= g.start[i + 1]) ++i;
   const Params& p = g.p[i];
-  const int l = L - g.start[i];
+  const int l = x * (g.start[i + 1] - g.start[i]) + (j - g.start[i]);
+  if (l >= p.tiles) return;
   const int m = g.mode[i];
   if constexpr (KIND == G_FWD) {
     gemm_tile<KV, KV, false, BN_>(p, l);
@@ -580,12 +582,17 @@ __device__ void block_sum(float (&v)[NV], float* red) {
     for (int k = 0; k < NV; ++k) v[k] = red[k] + red[NV + k] + red[2 * NV + k] + red[3 * NV + k];
 }
 
-// The last block to finish reduces the per-block partials (agent-scope release by every
-// writer before the counter; acquire by the last block before it reads them).
+// The last block to finish reduces the per-block partials. Thread 0 wrote this block's
+// partials: it alone releases them (agent scope) before the counter — an agent-scope fence
+// by every thread of every block costs microseconds per block — and the last block's
+// threads acquire before they read the other blocks' partials.
 __device__ bool last_block(uint32_t* counter) {
   __shared__ bool last;
-  __threadfence();
-  if (threadIdx.x == 0) last = atomicAdd(counter, 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    last = atomicAdd(counter, 1u) == gridDim.x - 1;
+  }
   __syncthreads();
   if (last) __threadfence();
   return last;
@@ -1140,6 +1147,12 @@ int32_t lgx_gemm_group(const lgx_gemm_args* args, int32_t n, void* stream) {
     ++g.n;
   }
   if (g.n == 0) return 0;
+  // longest K chunk first: every XCD starts its costliest tiles first
+  for (int i = 1; i < g.n; ++i)
+    for (int k = i; k > 0 && g.p[k].kchunk > g.p[k - 1].kchunk; --k) {
+      std::swap(g.p[k], g.p[k - 1]);
+      std::swap(g.mode[k], g.mode[k - 1]);
+    }
   const int bn = tile_n(maxn);
   int total = 0;
   for (int i = 0; i < g.n; ++i) {
@@ -1148,11 +1161,11 @@ int32_t lgx_gemm_group(const lgx_gemm_args* args, int32_t n, void* stream) {
     p.tiles_n = (p.N + bn - 1) / bn;
     p.tiles = p.tiles_m * p.tiles_n * p.split;
     g.start[i] = total;
-    total += p.tiles;
+    total += (p.tiles + 7) / 8;
   }
   g.start[g.n] = total;
-  g.total = total;
-  const int grid = (total + 7) / 8 * 8;
+  g.per_xcd = total;
+  const int grid = 8 * total;
   hipStream_t s = static_cast<hipStream_t>(stream);
 #define LGX_GROUP_LAUNCH(K)                                                                                     \
   if (bn == 128) {                                                                                              \
