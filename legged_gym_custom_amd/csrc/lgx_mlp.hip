@@ -138,48 +138,52 @@ struct Stager {
     }
   }
 
-  __device__ __forceinline__ static void store(__bf16* hi, __bf16* lo, int tid, const float (&v)[R]) {
+  // The staging store in PARTS independent pieces (KV: one 8-k task; MV: one of the 4 rows
+  // of the thread's 4-row group), so they can be spread between the MFMAs of a K step.
+  static constexpr int PARTS = MODE == KV ? T : 4;
+  __device__ __forceinline__ static void store_part(__bf16* hi, __bf16* lo, int tid, const float (&v)[R], int q) {
     if (MODE == KV) {
-#pragma unroll
-      for (int t = 0; t < T; ++t) {
-        const int idx = tid + t * NT, r = idx >> 2, g = idx & 3;
-        bf16x8 h, l;
-        split8(v + t * 8, h, l);
-        const int off = lds_off(r, g);
-        *reinterpret_cast<bf16x8*>(hi + off) = h;
-        *reinterpret_cast<bf16x8*>(lo + off) = l;
-      }
+      const int t = q;
+      const int idx = tid + t * NT, r = idx >> 2, g = idx & 3;
+      bf16x8 h, l;
+      split8(v + t * 8, h, l);
+      const int off = lds_off(r, g);
+      *reinterpret_cast<bf16x8*>(hi + off) = h;
+      *reinterpret_cast<bf16x8*>(lo + off) = l;
     } else {
       const int kq = tid % NKQ, rg = tid / NKQ;
       const int kb = kq * KG;  // first k of this thread inside the step
+      const int e = q;
+      const int off = lds_off(rg * 4 + e, kb >> 3) + (kb & 7);
+      if (KG == 4) {
+        bf16x4 h, l;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int off = lds_off(rg * 4 + e, kb >> 3) + (kb & 7);
-        if (KG == 4) {
-          bf16x4 h, l;
-#pragma unroll
-          for (int kk = 0; kk < 4; ++kk) {
-            const float x = v[kk * 4 + e];
-            const __bf16 b = (__bf16)x;
-            h[kk] = b;
-            l[kk] = (__bf16)(x - (float)b);
-          }
-          *reinterpret_cast<bf16x4*>(hi + off) = h;
-          *reinterpret_cast<bf16x4*>(lo + off) = l;
-        } else {
-          bf16x2 h, l;
-#pragma unroll
-          for (int kk = 0; kk < 2; ++kk) {
-            const float x = v[kk * 4 + e];
-            const __bf16 b = (__bf16)x;
-            h[kk] = b;
-            l[kk] = (__bf16)(x - (float)b);
-          }
-          *reinterpret_cast<bf16x2*>(hi + off) = h;
-          *reinterpret_cast<bf16x2*>(lo + off) = l;
+        for (int kk = 0; kk < 4; ++kk) {
+          const float x = v[kk * 4 + e];
+          const __bf16 b = (__bf16)x;
+          h[kk] = b;
+          l[kk] = (__bf16)(x - (float)b);
         }
+        *reinterpret_cast<bf16x4*>(hi + off) = h;
+        *reinterpret_cast<bf16x4*>(lo + off) = l;
+      } else {
+        bf16x2 h, l;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          const float x = v[kk * 4 + e];
+          const __bf16 b = (__bf16)x;
+          h[kk] = b;
+          l[kk] = (__bf16)(x - (float)b);
+        }
+        *reinterpret_cast<bf16x2*>(hi + off) = h;
+        *reinterpret_cast<bf16x2*>(lo + off) = l;
       }
     }
+  }
+
+  __device__ __forceinline__ static void store(__bf16* hi, __bf16* lo, int tid, const float (&v)[R]) {
+#pragma unroll
+    for (int q = 0; q < PARTS; ++q) store_part(hi, lo, tid, v, q);
   }
 
   // Row sums of the A tile (bias gradient), MV/MVE only: rows 4*rg + e, slot kq.
@@ -235,7 +239,10 @@ __device__ __forceinline__ void gemm_tile(const Params& p, const int L) {
     for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int fr = lane & 15, fc = lane >> 4;
-  auto compute = [&](int buf) {
+  // MFMAs of one K step on LDS[buf]; when `st`, the next step's registers (va, vb) are then
+  // split and stored into LDS[nbuf]. (Spreading those stores between the MFMA groups, with
+  // or without sched_group_barrier / s_setprio, measured the same: tools/gemm_variants.py.)
+  auto compute = [&](int buf, bool st, int nbuf, const float (&va)[SA::R], const float (&vb)[SB::R]) {
     const __bf16* base = lds + buf * STAGE;
     const __bf16* ahi = base;
     const __bf16* alo = base + A_ELEMS;
@@ -260,12 +267,12 @@ __device__ __forceinline__ void gemm_tile(const Params& p, const int L) {
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh[j], acc[i][j], 0, 0, 0);
       }
     }
+    if (st) sstore(va, vb, nbuf);
   };
-  // step s: MFMAs on LDS[s&1]; stage step s+1 (registers loaded two steps ago) into
+  // step s: MFMAs on LDS[s&1] with step s+1 (registers loaded two steps ago) staged into
   // LDS[(s+1)&1]; refill those registers with step s+3; one barrier.
   auto step = [&](int s, float (&va)[SA::R], float (&vb)[SB::R]) {
-    compute(s & 1);
-    if (s + 1 < nsteps) sstore(va, vb, (s + 1) & 1);
+    compute(s & 1, s + 1 < nsteps, (s + 1) & 1, va, vb);
     if (s + 3 < nsteps) gload(va, vb, kbeg + (s + 3) * BKS);
     __syncthreads();
   };

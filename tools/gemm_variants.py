@@ -1,0 +1,39 @@
+"""Time the learner's dominant GEMM launches for the liblgx_mlp.so named by LGX_MLP_LIB
+(dev tool for comparing kernel variants): critic layer-0 forward, an input-gradient
+launch, and the whole-backward weight-gradient group (the go2 update's 17 dW GEMMs)."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+from legged_gym_custom_amd.rsl_rl.modules import hip_mlp as H  # noqa: E402
+from bench_mlp import t  # noqa: E402
+
+B = 24576
+torch.manual_seed(0)
+X = torch.randn(B, 736, device="cuda")
+W = torch.randn(512, 736, device="cuda") * 0.05
+b = torch.randn(512, device="cuda")
+g1 = torch.randn(B, 256, device="cuda")
+W1 = torch.randn(256, 512, device="cuda") * 0.05
+Y0 = torch.nn.functional.elu(torch.randn(B, 512, device="cuda"))
+# (in, out) of every layer of the go2 update: actor, critic, privileged/scan encoders, estimator
+layers = [(627, 512), (512, 256), (256, 128), (128, 12), (736, 512), (512, 256), (256, 128), (128, 1),
+          (29, 64), (64, 20), (20, 20), (132, 128), (128, 64), (64, 32), (572, 128), (128, 64), (64, 3)]
+data = [(torch.randn(B, o, device="cuda"), torch.randn(B, i, device="cuda"), torch.zeros(o, i, device="cuda"),
+         torch.zeros(o, device="cuda")) for i, o in layers]
+
+
+def dw_group():
+    with H.deferred_weight_grads():
+        for dy, x, dW, db in data:
+            H.linear_weight_grad(dy, x, dW, db, accumulate=True)
+
+
+r = {"fwd736x512": t(lambda: H.linear_forward(X, W, b, True)),
+     "dx256to512": t(lambda: H.linear_input_grad(g1, W1, Y0)),
+     "dWgroup": t(dw_group, it=5)}
+fl = {"fwd736x512": 2 * B * 736 * 512, "dx256to512": 2 * B * 256 * 512,
+      "dWgroup": sum(2 * B * i * o for i, o in layers)}
+print(os.path.basename(os.environ.get("LGX_MLP_LIB", "default")), " ".join(
+    f"{k} {v:.1f}us ({fl[k] / v / 1e6:.0f}TF)" for k, v in r.items()), flush=True)
