@@ -30,6 +30,10 @@
 
 #include "../../include/lgx_mlp.h"
 
+#ifndef LGX_ELU_EXACT
+#define LGX_ELU_EXACT 0
+#endif
+
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
@@ -195,6 +199,26 @@ struct Stager {
   }
 };
 
+// ELU(alpha = 1): v > 0 ? v : expm1(v), branch-free. expm1 on v <= 0: a degree-8 Taylor
+// polynomial for v > -0.5 (truncation < 1.2e-8 relative), exp(v) - 1 below (v_exp_f32;
+// within ~3 ulp of expm1f at the switch, < 1 ulp past v = -1). LGX_ELU_EXACT: ocml expm1f.
+__device__ __forceinline__ float elu(float v) {
+#if LGX_ELU_EXACT
+  return v > 0.f ? v : expm1f(v);
+#else
+  float q = fmaf(v, 1.f / 40320.f, 1.f / 5040.f);
+  q = fmaf(v, q, 1.f / 720.f);
+  q = fmaf(v, q, 1.f / 120.f);
+  q = fmaf(v, q, 1.f / 24.f);
+  q = fmaf(v, q, 1.f / 6.f);
+  q = fmaf(v, q, 0.5f);
+  q = fmaf(v, q, 1.f);
+  const float small = v * q;
+  const float big = __expf(v) - 1.f;
+  return v > 0.f ? v : (v > -0.5f ? small : big);
+#endif
+}
+
 // One output tile (logical index L: n fastest, then m, then the K split) of one GEMM.
 template <int AM, int BMODE, bool COLSUM, int BN_>
 __device__ __forceinline__ void gemm_tile(const Params& p, const int L) {
@@ -358,12 +382,17 @@ __device__ __forceinline__ void gemm_tile(const Params& p, const int L) {
     const bool full = n + 4 <= p.N;
     if (!part) {
       if (p.epi & LGX_EPI_BIAS) {
+        if (full) {
+          const f32x4u bb = *reinterpret_cast<const f32x4u*>(p.bias + n);
+          v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
+        } else {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] += (full || n + e < p.N) ? p.bias[n + e] : 0.f;
+          for (int e = 0; e < 4; ++e) v[e] += n + e < p.N ? p.bias[n + e] : 0.f;
+        }
       }
       if (p.epi & LGX_EPI_ELU) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : expm1f(v[e]);
+        for (int e = 0; e < 4; ++e) v[e] = elu(v[e]);
       }
       if (delu) {
         const float y[4] = {yv[it].x, yv[it].y, yv[it].z, yv[it].w};

@@ -7,7 +7,7 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 from legged_gym_custom_amd.rsl_rl.modules import hip_mlp as H  # noqa: E402
-from bench_mlp import t  # noqa: E402
+from bench_mlp_t import t  # noqa: E402
 
 B = 24576
 torch.manual_seed(0)
@@ -30,10 +30,22 @@ def dw_group():
             H.linear_weight_grad(dy, x, dW, db, accumulate=True)
 
 
+Xs = torch.randn(B, 128, device="cuda")
+Ws = torch.randn(64, 128, device="cuda") * 0.3
+bs = torch.randn(64, device="cuda")
+Xr = X[:4096].contiguous()
+# ELU epilogue accuracy: x @ I + b over a sweep of pre-activations in [-20, 5]
+z = torch.linspace(-20, 5, 4096 * 64, device="cuda").view(4096, 64)
+eye = torch.eye(64, device="cuda")
+yz = H.linear_forward(z, eye, torch.zeros(64, device="cuda"), True)
+ref = torch.nn.functional.elu(z.double())
+ulp = ((yz.double() - ref).abs() / (ref.abs() * 2.0 ** -23 + 1e-30)).max().item()
 r = {"fwd736x512": t(lambda: H.linear_forward(X, W, b, True)),
+     "fwd128x64": t(lambda: H.linear_forward(Xs, Ws, bs, True)),
+     "fwd4096r": t(lambda: H.linear_forward(Xr, W, b, True)),
      "dx256to512": t(lambda: H.linear_input_grad(g1, W1, Y0)),
      "dWgroup": t(dw_group, it=5)}
-fl = {"fwd736x512": 2 * B * 736 * 512, "dx256to512": 2 * B * 256 * 512,
+fl = {"fwd736x512": 2 * B * 736 * 512, "fwd128x64": 2 * B * 128 * 64, "fwd4096r": 2 * 4096 * 736 * 512, "dx256to512": 2 * B * 256 * 512,
       "dWgroup": sum(2 * B * i * o for i, o in layers)}
-print(os.path.basename(os.environ.get("LGX_MLP_LIB", "default")), " ".join(
+print(os.path.basename(os.environ.get("LGX_MLP_LIB", "default")), f"elu max {ulp:.1f} ulp", " ".join(
     f"{k} {v:.1f}us ({fl[k] / v / 1e6:.0f}TF)" for k, v in r.items()), flush=True)
