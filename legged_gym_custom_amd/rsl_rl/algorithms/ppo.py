@@ -291,13 +291,14 @@ class PPO:
             # log-prob straight into this step's storage rows (lgx_act_head)
             s, k = self.storage, self.storage.step
             with torch.no_grad():
-                items = [self.estimator.group_item(obs), ac.scan_encoder.group_item(scan_obs), (ac.critic, critic_obs)]
+                items = [self.estimator.group_item(obs), ac.scan_encoder.group_item(scan_obs)]
                 if not adaptation_mode:
                     items.append(ac.privileged_encoder_.group_item(privileged_obs))
                 outs = hip_mlp.forward_group(items)
-                estimated_obs, scan_latent, t.values = outs[:3]
-                latent = ac.adaptation_encoder(obs) if adaptation_mode else outs[3]
-                mean = ac.actor_forward(obs, latent, scan_latent, estimated_obs)
+                estimated_obs, scan_latent = outs[:2]
+                latent = ac.adaptation_encoder(obs) if adaptation_mode else outs[2]
+                mean, t.values = hip_mlp.forward_group([(ac.actor, (obs, latent, scan_latent, estimated_obs)),
+                                                        (ac.critic, critic_obs)])
                 eps = torch.randn_like(mean)
                 hip_mlp.act_head(mean, ac.std.detach(), eps, s.actions[k], s.mu[k], s.sigma[k], s.actions_log_prob[k])
             t.actions, t.action_mean, t.action_sigma = s.actions[k], s.mu[k], s.sigma[k]
@@ -373,12 +374,14 @@ class PPO:
             # regulariser (the reference evaluates the same encoder on the same input twice,
             # ppo.py:190,204)
             adaptive = self.desired_kl is not None and self.schedule == "adaptive"
-            # the privileged/scan encoders, critic and estimator read only the minibatch: one
-            # autograd node, one grouped launch per depth each way (hip_mlp.forward_group)
-            priv_latent, scan_latent, value_b, pred = hip_mlp.forward_group(
-                [ac.privileged_encoder_.group_item(priv_b), ac.scan_encoder.group_item(scan_b), (ac.critic, critic_b),
+            # the privileged/scan encoders and the estimator read only the minibatch, then the
+            # actor (on their latents) and the critic: two autograd nodes, one grouped launch
+            # per depth each way (hip_mlp.forward_group)
+            priv_latent, scan_latent, pred = hip_mlp.forward_group(
+                [ac.privileged_encoder_.group_item(priv_b), ac.scan_encoder.group_item(scan_b),
                  self.estimator.group_item(obs_b)])
-            mu_b = ac.actor_forward(obs_b, priv_latent, scan_latent, est_b)  # TRUE est obs (Q12)
+            mu_b, value_b = hip_mlp.forward_group([(ac.actor, (obs_b, priv_latent, scan_latent, est_b)),  # TRUE est (Q12)
+                                                   (ac.critic, critic_b)])
             surrogate_loss, value_loss, entropy_mean, _kl = hip_mlp.ppo_head(
                 mu_b, value_b, ac.std, actions_b, old_logp_b, adv_b, target_values_b, returns_b, old_mu_b, old_sigma_b,
                 self.clip_param, self.use_clipped_value_loss, kl_dst=g.segment("kl") if adaptive else None,
