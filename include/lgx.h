@@ -298,6 +298,13 @@ int lgx_physics(lgx_env* env, void* hip_stream);
 /* reset_idx for the envs with env_mask[i] != 0 (device pointer, uint8 [N]);
  * reset_call numbers external reset calls for the RNG stream. */
 int lgx_reset_envs(lgx_env* env, const uint8_t* env_mask, uint64_t seed, uint64_t reset_call, void* hip_stream);
+/* extras['episode'] / extras['time_outs'] of the step just run (go2.py:246-263, the
+ * send_timeouts flag of legged_robot.py), one launch, no host synchronisation:
+ *   cnt = episode_stats[K]; if cnt > 0: means[k] = episode_stats[k] / cnt / max_episode_length_s
+ *                                      *level_mean = mean(terrain_levels)   (level_mean != NULL)
+ *   if time_outs != NULL and any(reset): time_outs[i] = time_out[i]
+ * Outputs keep their previous values otherwise (the reference's stale-when-no-reset values). */
+int lgx_episode_extras(lgx_env* env, float* means, float* level_mean, uint8_t* time_outs, void* hip_stream);
 const char* lgx_last_error(const lgx_env* env);
 void lgx_destroy(lgx_env* env);
 

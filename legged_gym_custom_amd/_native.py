@@ -31,6 +31,7 @@ def lib():
     L.lgx_post_physics.argtypes = [vp, u64, u64, vp]
     L.lgx_physics.argtypes = [vp, vp]
     L.lgx_reset_envs.argtypes = [vp, vp, u64, u64, vp]
+    L.lgx_episode_extras.argtypes = [vp, vp, vp, vp, vp]
     L.lgx_last_error.argtypes = [vp]
     L.lgx_last_error.restype = C.c_char_p
     L.lgx_destroy.argtypes = [vp]
@@ -44,7 +45,7 @@ def lib():
 
 EXPORTED = ["lgx_abi_version", "lgx_sizeof_model", "lgx_sizeof_task_params", "lgx_sizeof_buffers", "lgx_create",
             "lgx_bind", "lgx_step", "lgx_step_dev", "lgx_post_physics", "lgx_physics", "lgx_reset_envs", "lgx_last_error",
-            "lgx_destroy"]
+            "lgx_destroy", "lgx_episode_extras"]
 
 
 class NativeEnv:
@@ -95,6 +96,12 @@ class NativeEnv:
         self._keep["_mask"] = mask
         self._check(self._L.lgx_reset_envs(self.handle, C.c_void_p(mask.data_ptr()), seed, call, C.c_void_p(stream)),
                     "lgx_reset_envs")
+
+    def episode_extras(self, means, level_mean, time_outs, stream):
+        """lgx_episode_extras into the given device tensors (level_mean / time_outs: None = skip)."""
+        p = lambda t: None if t is None else C.c_void_p(t.data_ptr())  # noqa: E731
+        self._check(self._L.lgx_episode_extras(self.handle, p(means), p(level_mean), p(time_outs),
+                                               C.c_void_p(stream)), "lgx_episode_extras")
 
     def __del__(self):
         try:

@@ -1719,6 +1719,64 @@ int lgx_reset_envs(lgx_env* env, const uint8_t* env_mask, uint64_t seed, uint64_
   return 0;
 }
 
+namespace lgx {
+// extras['episode'] / extras['time_outs'] (go2.py:246-263, Appendix B Q5 stale values):
+// one block; thread k < K forms the episode mean of reward term k, the block reduces
+// any(reset) and the mean terrain level, then time_outs is refreshed when any env reset.
+__global__ __launch_bounds__(1024) void extras_kernel(const float* __restrict__ stats, int K, float inv_T, int N,
+                                                      const uint8_t* __restrict__ reset,
+                                                      const uint8_t* __restrict__ time_out,
+                                                      const int64_t* __restrict__ levels, float* __restrict__ means,
+                                                      float* __restrict__ level_mean, uint8_t* __restrict__ time_outs) {
+  __shared__ int any_s;
+  __shared__ double lsum[16];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (tid == 0) any_s = 0;
+  __syncthreads();
+  const float cnt = stats[K];
+  if (tid < K && cnt > 0.f) means[tid] = stats[tid] / cnt * inv_T;
+  int any = 0;
+  double ls = 0.0;
+  for (int i = tid; i < N; i += blockDim.x) {
+    if (reset) any |= reset[i];
+    if (levels) ls += (double)levels[i];
+  }
+  if (reset && __any(any)) {
+    if (lane == 0) atomicOr(&any_s, 1);
+  }
+  if (levels) {
+    for (int o = 32; o > 0; o >>= 1) ls += __shfl_down(ls, o, 64);
+    if (lane == 0) lsum[wv] = ls;
+  }
+  __syncthreads();
+  if (levels && tid == 0 && cnt > 0.f) {
+    double t = 0.0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += lsum[w];
+    *level_mean = (float)(t / N);
+  }
+  if (time_outs && any_s)
+    for (int i = tid; i < N; i += blockDim.x) time_outs[i] = time_out[i];
+}
+}  // namespace lgx
+
+int lgx_episode_extras(lgx_env* env, float* means, float* level_mean, uint8_t* time_outs, void* hip_stream) {
+  if (!env) return -2;
+  if (!env->bound) return fail(env, "lgx_episode_extras before lgx_bind");
+  const lgx_buffers& b = env->buffers;
+  if (!b.episode_stats || !means) return fail(env, "lgx_episode_extras: episode_stats and means are required");
+  if (level_mean && !b.terrain_levels) return fail(env, "lgx_episode_extras: level_mean needs terrain_levels");
+  if (time_outs && (!b.reset || !b.time_out)) return fail(env, "lgx_episode_extras: time_outs needs reset/time_out");
+  const int KS = env->params.num_reward_terms + (env->params.has_termination_reward ? 1 : 0);
+  if (KS > 1024) return fail(env, "lgx_episode_extras: too many reward terms");
+  hipStream_t st = (hipStream_t)hip_stream;
+  // torch divides a tensor by a Python scalar as a multiply by the fp32 reciprocal
+  hipLaunchKernelGGL(lgx::extras_kernel, dim3(1), dim3(1024), 0, st, b.episode_stats, KS,
+                     1.0f / env->params.max_episode_length_s, env->params.num_envs, time_outs ? b.reset : nullptr,
+                     b.time_out, level_mean ? b.terrain_levels : nullptr, means, level_mean, time_outs);
+  HIP_OK(hipGetLastError());
+  return 0;
+}
+
 const char* lgx_last_error(const lgx_env* env) { return env ? env->err.c_str() : "null env"; }
 
 void lgx_destroy(lgx_env* env) {

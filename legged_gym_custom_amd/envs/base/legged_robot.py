@@ -73,7 +73,23 @@ class LeggedRobot(BaseTask):
 
     def _update_extras(self):
         """extras['episode'] / ['time_outs'] with the reference's stale-when-no-reset
-        semantics (go2.py:246-263, Appendix B Q5), computed on device (no host sync)."""
+        semantics (go2.py:246-263, Appendix B Q5): one lgx_episode_extras launch (no host
+        sync); _update_extras_torch states the same in torch ops (tests compare them)."""
+        cur, to = self.cfg.terrain.curriculum, self.cfg.env.send_timeouts
+        self._native.episode_extras(self._episode_means, self._terrain_level_mean if cur else None,
+                                    self._extras_time_outs if to else None,
+                                    torch.cuda.current_stream(self.device).cuda_stream)
+        self._publish_extras()
+
+    def _publish_extras(self):
+        if "episode" not in self.extras:
+            self.extras["episode"] = {"rew_" + k: self._episode_means[i] for i, k in enumerate(self._episode_keys)}
+            if self.cfg.terrain.curriculum:
+                self.extras["episode"]["terrain_level"] = self._terrain_level_mean
+        if self.cfg.env.send_timeouts:
+            self.extras["time_outs"] = self._extras_time_outs
+
+    def _update_extras_torch(self):
         st = self.episode_stats
         cnt = st[-1]
         means = st[:-1] / torch.clamp(cnt, min=1.0) / self.max_episode_length_s
@@ -82,13 +98,9 @@ class LeggedRobot(BaseTask):
         if self.cfg.terrain.curriculum:  # go2.py:252-253 (mean level, refreshed when envs reset)
             self._terrain_level_mean.copy_(torch.where(cnt > 0, self.terrain_levels.float().mean(),
                                                        self._terrain_level_mean))
-        if "episode" not in self.extras:
-            self.extras["episode"] = {"rew_" + k: self._episode_means[i] for i, k in enumerate(self._episode_keys)}
-            if self.cfg.terrain.curriculum:
-                self.extras["episode"]["terrain_level"] = self._terrain_level_mean
         if self.cfg.env.send_timeouts:
             self._extras_time_outs.copy_(torch.where(self.reset_buf.any(), self.time_out_buf, self._extras_time_outs))
-            self.extras["time_outs"] = self._extras_time_outs
+        self._publish_extras()
 
     @property
     def common_step_counter(self):
