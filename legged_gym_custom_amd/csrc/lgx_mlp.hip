@@ -42,6 +42,10 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 namespace lgxm {
 
 constexpr int BM = 128, BKS = 32, NT = 256;
+#ifndef LGX_PF
+#define LGX_PF 2
+#endif
+constexpr int PF = LGX_PF;               // global-load register sets (prefetch depth in K steps)
 constexpr int PITCH = BKS;               // bf16 per LDS row (64 B, swizzled: lds_off)
 constexpr int A_ELEMS = BM * PITCH;      // one A image (hi or lo)
 enum Mode { KV = 1, MV = 3, MVE = 4 };  // MVE: MV for a row count that is not a multiple of 4
@@ -238,7 +242,7 @@ __device__ __forceinline__ void gemm_tile(const Params& p, const int L) {
   const int nsteps = kend > kbeg ? (kend - kbeg + BKS - 1) / BKS : 0;
   const int wm = (wave & 1) * 64, wn = (wave >> 1) * (BN_ / 2);
 
-  float va0[SA::R], vb0[SB::R], va1[SA::R], vb1[SB::R];
+  float va[PF][SA::R], vb[PF][SB::R];  // PF register sets: loads run PF steps ahead
   float csum[4] = {0.f, 0.f, 0.f, 0.f};
   auto gload = [&](float (&va)[SA::R], float (&vb)[SB::R], int k0) {
     if (k0 + BKS <= kend) {
@@ -295,22 +299,26 @@ __device__ __forceinline__ void gemm_tile(const Params& p, const int L) {
   };
   // step s: MFMAs on LDS[s&1] with step s+1 (registers loaded two steps ago) staged into
   // LDS[(s+1)&1]; refill those registers with step s+3; one barrier.
-  auto step = [&](int s, float (&va)[SA::R], float (&vb)[SB::R]) {
-    compute(s & 1, s + 1 < nsteps, (s + 1) & 1, va, vb);
-    if (s + 3 < nsteps) gload(va, vb, kbeg + (s + 3) * BKS);
+  auto step = [&](int s, float (&ra)[SA::R], float (&rb)[SB::R]) {
+    compute(s & 1, s + 1 < nsteps, (s + 1) & 1, ra, rb);
+    if (s + 1 + PF < nsteps) gload(ra, rb, kbeg + (s + 1 + PF) * BKS);
     __syncthreads();
   };
 
   if (nsteps > 0) {
-    gload(va0, vb0, kbeg);
-    sstore(va0, vb0, 0);
-    if (nsteps > 1) gload(va1, vb1, kbeg + BKS);
-    if (nsteps > 2) gload(va0, vb0, kbeg + 2 * BKS);
+    gload(va[0], vb[0], kbeg);
+    sstore(va[0], vb[0], 0);
+#pragma unroll
+    for (int j = 1; j <= PF; ++j)
+      if (j < nsteps) gload(va[j % PF], vb[j % PF], kbeg + j * BKS);
   }
   __syncthreads();
-  for (int s = 0; s < nsteps; s += 2) {
-    step(s, va1, vb1);
-    if (s + 1 < nsteps) step(s + 1, va0, vb0);
+  // step s stages register set (s + 1) % PF (step s + 1, loaded PF steps earlier) and refills
+  // it with step s + 1 + PF
+  for (int s = 0; s < nsteps; s += PF) {
+#pragma unroll
+    for (int j = 0; j < PF; ++j)
+      if (s + j < nsteps) step(s + j, va[(j + 1) % PF], vb[(j + 1) % PF]);
   }
 
   float* cs = reinterpret_cast<float*>(lds);

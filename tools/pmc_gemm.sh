@@ -4,9 +4,9 @@ R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/pmc_gemm2; rm -rf $O; mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
 i=0
 for C in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU" \
-         "SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_MISC SQ_INSTS_VMEM_RD SQ_INSTS_SALU" \
+         "SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_MISC SQ_INSTS_VMEM_RD SQ_INSTS_SALU" "TA_TA_BUSY_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum" \
          "TCP_TCR_TCP_STALL_CYCLES_sum TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum GRBM_GUI_ACTIVE"; do
   i=$((i+1))
-  timeout -s KILL 90 rocprofv3 --pmc $C --output-format csv -d $O/p$i -- python3 $R/tools/prof_gemm.py > $O/p$i.log 2>&1 || exit 1
+  timeout -s KILL 90 rocprofv3 --pmc $C --output-format csv -d $O/p$i -- python3 $R/tools/${PROG:-prof_gemm.py} > $O/p$i.log 2>&1 || exit 1
 done
 cd $R && python3 tools/pmc_summary.py $O
