@@ -56,7 +56,7 @@ def committed_traffic(num_envs):
     return d["traffic_bytes_per_launch"], os.path.relpath(files[-1], ROOT)
 
 
-def cpu_baseline(num_envs=256, iters=1, steps_per_env=24):
+def cpu_baseline(num_envs=1024, iters=3, steps_per_env=24):
     """Oracle env step (single-threaded C) + torch-CPU rsl_rl learner, same runner."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import cpu_env
