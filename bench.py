@@ -99,10 +99,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # LGX_DIST_BACKEND=gloo: rehearsal of the N>1 path with several ranks on one GPU
+    # (correctness only; RCCL needs one GPU per rank)
+    backend = os.environ.get("LGX_DIST_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(1, torch.cuda.device_count())
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        else:
+            dist.init_process_group(backend)
     dev = f"cuda:{local}"
     # the reference's own training precision (legged_gym/scripts/train.py:39): fp32
     # storage, hipBLASLt's reduced-precision fp32 GEMM path allowed
