@@ -9,7 +9,7 @@ for f in sorted(glob.glob(sys.argv[1] + "/p*/*/*_counter_collection.csv")):
     for r in csv.DictReader(open(f)):
         agg[r["Kernel_Name"].split("(")[0][-48:]][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, d in agg.items():
-    if "lgx" not in k:
+    if "lgx" not in k and "env_step" not in k:
         continue
     print(k)
     for c, v in sorted(d.items()):
