@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define LGX_MLP_ABI_VERSION 2
+#define LGX_MLP_ABI_VERSION 3
 
 enum {
   LGX_EPI_BIAS = 1,  /* + bias[n] */
@@ -127,6 +127,7 @@ typedef struct lgx_ppo_head_args {
   float* ws; uint32_t* counter;
   float* kl_dst;             /* optional: forward also writes the KL mean here (the KL slot
                                 of the flat gradient buffer that rides the all-reduce) */
+  int32_t accumulate_dstd;   /* backward: dstd += (the parameter's .grad) instead of = */
 } lgx_ppo_head_args;
 
 int32_t lgx_ppo_head_forward(const lgx_ppo_head_args* args, void* stream);

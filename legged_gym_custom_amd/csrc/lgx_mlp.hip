@@ -604,7 +604,9 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, 
 }
 
 // ---------------------------------------------------------------- PPO loss head
-constexpr int HT = 256;     // rows per block
+constexpr int HT = 256;     // threads per block (rows per block and grid-stride pass)
+// one row per thread (grid-stride loops, so any grid is correct; fewer blocks measured slower)
+static unsigned head_grid(int B) { return (unsigned)((B + HT - 1) / HT); }
 constexpr int HMAXA = 16;   // max actions
 
 // block-wide sum of NV values per thread into red[NV] (thread 0 holds the result)
@@ -678,20 +680,19 @@ __global__ void ppo_head_fwd(lgx_ppo_head_args p) {
   __shared__ float stdv[HMAXA], lstd[HMAXA];
   if (threadIdx.x < p.A) { stdv[threadIdx.x] = p.std[threadIdx.x]; lstd[threadIdx.x] = logf(p.std[threadIdx.x]); }
   __syncthreads();
-  const int i = blockIdx.x * HT + threadIdx.x;
   float v[3] = {0.f, 0.f, 0.f};
-  if (i < p.B) {
+  for (int i = blockIdx.x * HT + threadIdx.x; i < p.B; i += gridDim.x * HT) {
     const HeadRow h = head_row(p, i, stdv, lstd);
     const float a = p.adv[i];
     const float s1 = -a * h.ratio, s2 = -a * fminf(fmaxf(h.ratio, 1.f - p.clip), 1.f + p.clip);
-    v[0] = fmaxf(s1, s2);
+    v[0] += fmaxf(s1, s2);
     const float val = p.value[i], R = p.returns[i];
     if (p.clipped_value) {
       const float tv = p.target_values[i];
       const float vc = tv + fminf(fmaxf(val - tv, -p.clip), p.clip);
-      v[1] = fmaxf((val - R) * (val - R), (vc - R) * (vc - R));
+      v[1] += fmaxf((val - R) * (val - R), (vc - R) * (vc - R));
     } else {
-      v[1] = (R - val) * (R - val);
+      v[1] += (R - val) * (R - val);
     }
     float kl = 0.f;
     for (int j = 0; j < p.A; ++j) {
@@ -699,7 +700,7 @@ __global__ void ppo_head_fwd(lgx_ppo_head_args p) {
       const float dm = om - p.mu[(int64_t)i * p.A + j];
       kl += logf(stdv[j] / os + 1.0e-5f) + (os * os + dm * dm) / (2.f * (stdv[j] * stdv[j])) - 0.5f;
     }
-    v[2] = kl;
+    v[2] += kl;
   }
   block_sum<3>(v, red);
   if (threadIdx.x == 0)
@@ -726,11 +727,10 @@ __global__ void ppo_head_bwd(lgx_ppo_head_args p) {
   if (threadIdx.x < p.A) { stdv[threadIdx.x] = p.std[threadIdx.x]; lstd[threadIdx.x] = logf(p.std[threadIdx.x]); }
   __syncthreads();
   const float gs = p.g[0] / p.B, gv = p.g[1] / p.B, ge = p.g[2];
-  const int i = blockIdx.x * HT + threadIdx.x;
   float ds[HMAXA];
 #pragma unroll
   for (int j = 0; j < HMAXA; ++j) ds[j] = 0.f;
-  if (i < p.B) {
+  for (int i = blockIdx.x * HT + threadIdx.x; i < p.B; i += gridDim.x * HT) {
     const HeadRow h = head_row(p, i, stdv, lstd);
     const float a = p.adv[i];
     const float lo = 1.f - p.clip, hi = 1.f + p.clip;
@@ -747,7 +747,7 @@ __global__ void ppo_head_bwd(lgx_ppo_head_args p) {
         const float d = p.actions[(int64_t)i * p.A + j] - p.mu[(int64_t)i * p.A + j];
         const float var = stdv[j] * stdv[j];
         p.dmu[(int64_t)i * p.A + j] = dlogp * d / var;
-        ds[j] = dlogp * (d * d / (var * stdv[j]) - 1.f / stdv[j]);
+        ds[j] += dlogp * (d * d / (var * stdv[j]) - 1.f / stdv[j]);
       }
     }
     const float val = p.value[i], R = p.returns[i];
@@ -771,7 +771,10 @@ __global__ void ppo_head_bwd(lgx_ppo_head_args p) {
     float t[HMAXA];
     final_sum<HMAXA>(p.ws, HMAXA, gridDim.x, t, red);
     if (threadIdx.x == 0) {
-      for (int j = 0; j < p.A; ++j) p.dstd[j] = t[j] + ge / stdv[j];  // entropy: d(sum_j log std_j)/d std_j
+      for (int j = 0; j < p.A; ++j) {  // entropy: d(sum_j log std_j)/d std_j
+        const float d = t[j] + ge / stdv[j];
+        p.dstd[j] = p.accumulate_dstd ? p.dstd[j] + d : d;
+      }
       *p.counter = 0u;
     }
   }
@@ -780,22 +783,21 @@ __global__ void ppo_head_bwd(lgx_ppo_head_args p) {
 // ---------------------------------------------------------------- ROA + estimator losses
 __global__ void aux_loss_fwd(lgx_aux_loss_args p) {
   __shared__ float red[4 * 2];
-  const int i = blockIdx.x * HT + threadIdx.x;
   float v[2] = {0.f, 0.f};
-  if (i < p.B) {
+  for (int i = blockIdx.x * HT + threadIdx.x; i < p.B; i += gridDim.x * HT) {
     float s = 0.f;
     for (int j = 0; j < p.L; ++j) {
       const float d = p.p[(int64_t)i * p.L + j] - p.a[(int64_t)i * p.L + j];
       s += d * d;
     }
-    v[0] = sqrtf(s);
+    v[0] += sqrtf(s);
     float q = 0.f;
     for (int j = 0; j < p.E; ++j) {
       const float d = p.e[(int64_t)i * p.E + j] - p.t[(int64_t)i * p.E + j];
       q += d * d;
     }
     const float nq = sqrtf(q);  // torch: norm(dim=1).pow(2)
-    v[1] = nq * nq;
+    v[1] += nq * nq;
   }
   block_sum<2>(v, red);
   if (threadIdx.x == 0) { p.ws[blockIdx.x * 2] = v[0]; p.ws[blockIdx.x * 2 + 1] = v[1]; }
@@ -1028,7 +1030,7 @@ static int head_check(const lgx_ppo_head_args* a) {
 int32_t lgx_ppo_head_forward(const lgx_ppo_head_args* a, void* stream) {
   if (head_check(a)) return -1;
   if (!a->out || !a->old_mu || !a->old_sigma) return fail("lgx_ppo_head_forward: null out/old_mu/old_sigma");
-  hipLaunchKernelGGL(lgxm::ppo_head_fwd, dim3((a->B + lgxm::HT - 1) / lgxm::HT), dim3(lgxm::HT), 0,
+  hipLaunchKernelGGL(lgxm::ppo_head_fwd, dim3(lgxm::head_grid(a->B)), dim3(lgxm::HT), 0,
                      static_cast<hipStream_t>(stream), *a);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : fail(hipGetErrorString(e));
@@ -1037,7 +1039,7 @@ int32_t lgx_ppo_head_forward(const lgx_ppo_head_args* a, void* stream) {
 int32_t lgx_ppo_head_backward(const lgx_ppo_head_args* a, void* stream) {
   if (head_check(a)) return -1;
   if (!a->g || !a->dmu || !a->dvalue || !a->dstd) return fail("lgx_ppo_head_backward: null g/dmu/dvalue/dstd");
-  hipLaunchKernelGGL(lgxm::ppo_head_bwd, dim3((a->B + lgxm::HT - 1) / lgxm::HT), dim3(lgxm::HT), 0,
+  hipLaunchKernelGGL(lgxm::ppo_head_bwd, dim3(lgxm::head_grid(a->B)), dim3(lgxm::HT), 0,
                      static_cast<hipStream_t>(stream), *a);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : fail(hipGetErrorString(e));
@@ -1046,7 +1048,7 @@ int32_t lgx_ppo_head_backward(const lgx_ppo_head_args* a, void* stream) {
 int32_t lgx_aux_loss_forward(const lgx_aux_loss_args* a, void* stream) {
   if (!a || a->B < 1 || a->L < 1 || a->E < 1 || !a->p || !a->a || !a->e || !a->t || !a->out || !a->ws || !a->counter)
     return fail("lgx_aux_loss_forward: bad arguments");
-  hipLaunchKernelGGL(lgxm::aux_loss_fwd, dim3((a->B + lgxm::HT - 1) / lgxm::HT), dim3(lgxm::HT), 0,
+  hipLaunchKernelGGL(lgxm::aux_loss_fwd, dim3(lgxm::head_grid(a->B)), dim3(lgxm::HT), 0,
                      static_cast<hipStream_t>(stream), *a);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : fail(hipGetErrorString(e));

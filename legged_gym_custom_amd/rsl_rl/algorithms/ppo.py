@@ -210,9 +210,10 @@ class PPO:
             self._aux_out = torch.zeros(2, device=device)    # regularisation, estimator
             self._tail_ws = torch.zeros(2 * 512 + 8, device=device)
             self._tail_counter = torch.zeros(1, dtype=torch.int32, device=device)
-            self._g_one = torch.ones((), device=device)
-            self._g_value = torch.full((), float(value_loss_coef), device=device)
-            self._g_ent = torch.full((), -float(entropy_coef), device=device)
+            # the backward seeds d loss / d {surrogate, value, entropy, regularisation, estimator}
+            # back to back in one buffer: the loss-head backward kernels read them in place
+            self._seeds = torch.tensor([1.0, float(value_loss_coef), -float(entropy_coef), 0.0, 1.0], device=device)
+            self._g_one, self._g_value, self._g_ent, self._reg_coef, self._g_est = self._seeds.unbind()
         self._perm = None
         self._graphs = None
         self._eager_updates = 0
@@ -398,7 +399,7 @@ class PPO:
             g.span("main", "estimator").zero_()
             with hip_mlp.deferred_weight_grads():
                 torch.autograd.backward([surrogate_loss, value_loss, entropy_mean, regularization_loss, estimator_loss],
-                                        [self._g_one, self._g_value, self._g_ent, self._reg_coef, self._g_one])
+                                        [self._g_one, self._g_value, self._g_ent, self._reg_coef, self._g_est])
             ac.distribution = None
             return
         (surrogate_loss, value_loss, entropy_mean, regularization_loss,

@@ -20,7 +20,7 @@ import torch.nn as nn
 _LIB_PATH = os.environ.get("LGX_MLP_LIB") or os.path.join(
     os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))), "lib", "liblgx_mlp.so")
 _lib = None
-ABI_VERSION = 2
+ABI_VERSION = 3
 EPI_BIAS, EPI_ELU, EPI_DELU, EPI_ACCUM = 1, 2, 4, 8
 EXPORTED = ["lgx_mlp_abi_version", "lgx_mlp_sizeof_gemm_args", "lgx_mlp_pick_split", "lgx_gemm",
             "lgx_mlp_last_error", "lgx_adam_step", "lgx_ppo_head_forward", "lgx_ppo_head_backward",
@@ -57,7 +57,8 @@ class HeadArgs(C.Structure):
                                           "returns", "old_mu", "old_sigma")] + \
                [("B", C.c_int32), ("A", C.c_int32), ("clip", C.c_float), ("clipped_value", C.c_int32),
                 ("out", C.c_void_p), ("g", C.c_void_p), ("dmu", C.c_void_p), ("dvalue", C.c_void_p),
-                ("dstd", C.c_void_p), ("ws", C.c_void_p), ("counter", C.c_void_p), ("kl_dst", C.c_void_p)]
+                ("dstd", C.c_void_p), ("ws", C.c_void_p), ("counter", C.c_void_p), ("kl_dst", C.c_void_p),
+                ("accumulate_dstd", C.c_int32)]
 
 
 class AuxArgs(C.Structure):
@@ -820,6 +821,17 @@ def _counter(dev, kind="head"):
     return c
 
 
+def _seed_vector(gs, dev):
+    """The incoming output gradients as one contiguous fp32 vector: read in place when they
+    already sit back to back in one buffer (the PPO update's seeds), else stacked."""
+    if all(t is not None and t.dtype == torch.float32 and t.numel() == 1 for t in gs):
+        p0 = gs[0].data_ptr()
+        if all(t.data_ptr() == p0 + 4 * k for k, t in enumerate(gs)):
+            return gs[0].as_strided((len(gs),), (1,))
+    z = torch.zeros((), device=dev)
+    return torch.stack([t if t is not None else z for t in gs]).float().contiguous()
+
+
 class _PPOHeadFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, mu, value, std, actions, old_logp, adv, target_values, returns, old_mu, old_sigma, clip,
@@ -841,6 +853,8 @@ class _PPOHeadFn(torch.autograd.Function):
         if L.lgx_ppo_head_forward(C.byref(a), C.c_void_p(torch.cuda.current_stream().cuda_stream)) != 0:
             raise MlpLibError("lgx_ppo_head_forward: " + L.lgx_mlp_last_error().decode())
         ctx.save_for_backward(mu_, value_, std_, actions_, old_logp_, adv_, tv_, ret_)
+        ctx.std_param = std  # its .grad (a view into the flat gradients) takes dstd in place
+        ctx.set_materialize_grads(False)  # the KL output carries no gradient: no zero fill
         ctx.clip, ctx.clipped = float(clip), int(bool(clipped_value))
         ctx.value_shape = value.shape
         ctx.mark_non_differentiable(out)
@@ -851,22 +865,23 @@ class _PPOHeadFn(torch.autograd.Function):
         mu, value, std, actions, old_logp, adv, tv, ret = ctx.saved_tensors
         B, A = mu.shape
         dev = mu.device
-        z = torch.zeros((), device=dev)
-        g = torch.stack([g_surr if g_surr is not None else z, g_value if g_value is not None else z,
-                         g_ent if g_ent is not None else z]).float().contiguous()
+        g = _seed_vector((g_surr, g_value, g_ent), dev)
         dmu = torch.empty_like(mu)
         dvalue = torch.empty(B, device=dev)
-        dstd = torch.empty_like(std)
+        sp = ctx.std_param
+        direct = sp.requires_grad and sp.is_leaf and sp.grad is not None and sp.grad.is_contiguous() and \
+            not sp._backward_hooks
+        dstd = sp.grad if direct else torch.empty_like(std)
         ws = torch.empty(16 * ((B + 255) // 256), device=dev)
         a = HeadArgs(mu=mu.data_ptr(), value=value.data_ptr(), std=std.data_ptr(), actions=actions.data_ptr(),
                      old_logp=old_logp.data_ptr(), adv=adv.data_ptr(), target_values=tv.data_ptr(),
                      returns=ret.data_ptr(), B=B, A=A, clip=ctx.clip, clipped_value=ctx.clipped, g=g.data_ptr(),
                      dmu=dmu.data_ptr(), dvalue=dvalue.data_ptr(), dstd=dstd.data_ptr(), ws=ws.data_ptr(),
-                     counter=_counter(dev).data_ptr())
+                     counter=_counter(dev).data_ptr(), accumulate_dstd=int(direct))
         L = lib()
         if L.lgx_ppo_head_backward(C.byref(a), C.c_void_p(torch.cuda.current_stream().cuda_stream)) != 0:
             raise MlpLibError("lgx_ppo_head_backward: " + L.lgx_mlp_last_error().decode())
-        return (dmu, dvalue.view(ctx.value_shape), dstd) + (None,) * 11
+        return (dmu, dvalue.view(ctx.value_shape), None if direct else dstd) + (None,) * 11
 
 
 def ppo_head(mu, value, std, actions, old_logp, adv, target_values, returns, old_mu, old_sigma, clip, clipped_value,
@@ -902,8 +917,7 @@ class _AuxLossFn(torch.autograd.Function):
         p, a, e, t = ctx.saved_tensors
         B, L = p.shape
         dev = p.device
-        z = torch.zeros((), device=dev)
-        g = torch.stack([g_reg if g_reg is not None else z, g_est if g_est is not None else z]).float().contiguous()
+        g = _seed_vector((g_reg, g_est), dev)
         dp = torch.empty_like(p)
         de = torch.empty_like(e)
         args = AuxArgs(p=p.data_ptr(), a=a.data_ptr(), L=L, e=e.data_ptr(), t=t.data_ptr(), E=e.shape[1], B=B,
