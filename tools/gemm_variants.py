@@ -24,6 +24,16 @@ data = [(torch.randn(B, o, device="cuda"), torch.randn(B, i, device="cuda"), tor
          torch.zeros(o, device="cuda")) for i, o in layers]
 
 
+Xa = torch.randn(B, 627, device="cuda")
+Wa = torch.randn(512, 627, device="cuda") * 0.05
+ya, yc = torch.empty(B, 512, device="cuda"), torch.empty(B, 512, device="cuda")
+fwd_args = [H._fwd_args(Xa, Wa, b, True, ya), H._fwd_args(X, W, b, True, yc)]
+g2 = torch.randn(B, 256, device="cuda")
+W2 = torch.randn(256, 512, device="cuda") * 0.05
+dxa, dxc = torch.empty(B, 512, device="cuda"), torch.empty(B, 512, device="cuda")
+dx_args = [H._dx_args(g1, W1, Y0, dxa), H._dx_args(g2, W2, Y0, dxc)]
+
+
 def dw_group():
     with H.deferred_weight_grads():
         for dy, x, dW, db in data:
@@ -44,8 +54,11 @@ r = {"fwd736x512": t(lambda: H.linear_forward(X, W, b, True)),
      "fwd128x64": t(lambda: H.linear_forward(Xs, Ws, bs, True)),
      "fwd4096r": t(lambda: H.linear_forward(Xr, W, b, True)),
      "dx256to512": t(lambda: H.linear_input_grad(g1, W1, Y0)),
+     "fwdgroup": t(lambda: H.run_group(fwd_args)),
+     "dxgroup": t(lambda: H.run_group(dx_args)),
      "dWgroup": t(dw_group, it=5)}
 fl = {"fwd736x512": 2 * B * 736 * 512, "fwd128x64": 2 * B * 128 * 64, "fwd4096r": 2 * 4096 * 736 * 512, "dx256to512": 2 * B * 256 * 512,
+      "fwdgroup": 2 * B * 512 * (627 + 736), "dxgroup": 2 * 2 * B * 256 * 512,
       "dWgroup": sum(2 * B * i * o for i, o in layers)}
-print(os.path.basename(os.environ.get("LGX_MLP_LIB", "default")), f"elu max {ulp:.1f} ulp", " ".join(
+print(os.path.basename(os.environ.get("LGX_MLP_LIB", "default")), "BN", os.environ.get("LGX_GROUP_BN", "auto"), f"elu max {ulp:.1f} ulp", " ".join(
     f"{k} {v:.1f}us ({fl[k] / v / 1e6:.0f}TF)" for k, v in r.items()), flush=True)
