@@ -210,6 +210,25 @@ typedef struct lgx_transition_args {
 } lgx_transition_args;
 int32_t lgx_store_transition(const lgx_transition_args* args, void* stream);
 
+/* RolloutStorage.compute_returns (rollout_storage.py:110-124) over [T, N] rows, one thread
+ * per env walking the steps backwards in torch's operation order:
+ *   nt = 1 - dones[t];  delta = (rewards[t] + (nt*gamma) * V[t+1]) - V[t]   (V[T] = last_values)
+ *   A = delta + ((nt*gamma)*lam) * A;  returns[t] = A + V[t];  advantages[t] = returns[t] - V[t]
+ * and moments[0..1] = (sum, sum of squares) of the advantages in fp64 (per-block partials
+ * summed in block order by the last block: deterministic). ws >= 2 * ceil(N / 256) doubles;
+ * counter: one zero-initialised uint32 (left at zero). */
+typedef struct lgx_gae_args {
+  const float* rewards; const uint8_t* dones; const float* values; const float* last_values;
+  float* returns; float* advantages;
+  int32_t T, N; float gamma, lam;
+  double* moments; double* ws; uint32_t* counter;
+} lgx_gae_args;
+int32_t lgx_gae(const lgx_gae_args* args, void* stream);
+/* advantages = (advantages - mean) / (std + 1e-8) with mean = moments[0] / count and the
+ * unbiased std sqrt((moments[1] - count mean^2) / (count - 1)) (fp64, then fp32 like torch's
+ * mean()/std() scalars); count = the number of advantages over all ranks. */
+int32_t lgx_normalize_advantages(float* advantages, int64_t n, const double* moments, double count, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

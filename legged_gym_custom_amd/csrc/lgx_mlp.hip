@@ -992,6 +992,62 @@ __global__ __launch_bounds__(256) void transition_kernel(lgx_transition_args p) 
   p.values_out[i] = v;
 }
 
+// GAE (lgx_gae): one thread per env, the T steps backwards in torch's operation order;
+// fp64 block partials of the advantages' sum and sum of squares, summed by the last block.
+__global__ __launch_bounds__(256) void gae_kernel(lgx_gae_args p) {
+  __shared__ double red[2 * 4];
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  double s1 = 0.0, s2 = 0.0;
+  if (n < p.N) {
+    const int64_t N = p.N;
+    const float g = p.gamma, lam = p.lam;
+    float adv = 0.f;
+    for (int t = p.T - 1; t >= 0; --t) {
+      const int64_t i = (int64_t)t * N + n;
+      const float v = p.values[i];
+      const float next = t == p.T - 1 ? p.last_values[n] : p.values[i + N];
+      const float nt = 1.0f - (float)p.dones[i];
+      const float delta = (p.rewards[i] + (nt * g) * next) - v;
+      adv = delta + ((nt * g) * lam) * adv;
+      const float ret = adv + v;
+      const float a = ret - v;
+      p.returns[i] = ret;
+      p.advantages[i] = a;
+      s1 += (double)a;
+      s2 += (double)a * (double)a;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    s1 += __shfl_down(s1, o, 64);
+    s2 += __shfl_down(s2, o, 64);
+  }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane == 0) { red[wv] = s1; red[4 + wv] = s2; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    p.ws[2 * blockIdx.x] = ((red[0] + red[1]) + red[2]) + red[3];
+    p.ws[2 * blockIdx.x + 1] = ((red[4] + red[5]) + red[6]) + red[7];
+    __threadfence();
+    if (atomicAdd(p.counter, 1u) == gridDim.x - 1) {  // last block: partials in block order
+      __threadfence();
+      double t1 = 0.0, t2 = 0.0;
+      for (int b = 0; b < (int)gridDim.x; ++b) { t1 += p.ws[2 * b]; t2 += p.ws[2 * b + 1]; }
+      p.moments[0] = t1;
+      p.moments[1] = t2;
+      *p.counter = 0u;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void adv_norm_kernel(float* __restrict__ a, int64_t n, const double* __restrict__ m,
+                                                       double count) {
+  const double mean = m[0] / count;
+  const double var = (m[1] - count * mean * mean) / (count - 1.0);
+  const float mf = (float)mean, den = (float)sqrt(var > 0.0 ? var : 0.0) + 1e-8f;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) a[i] = (a[i] - mf) / den;
+}
+
 }  // namespace lgxm
 
 extern "C" {
@@ -1075,6 +1131,25 @@ int32_t lgx_ppo_tail(const lgx_ppo_tail_args* a, void* stream) {
   hipStream_t s = static_cast<hipStream_t>(stream);
   hipLaunchKernelGGL(lgxm::tail_norms, dim3(lgxm::TAIL_BLOCKS), dim3(256), 0, s, *a);
   hipLaunchKernelGGL(lgxm::tail_adam, dim3(1024), dim3(256), 0, s, *a);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : fail(hipGetErrorString(e));
+}
+
+int32_t lgx_gae(const lgx_gae_args* a, void* stream) {
+  if (!a || a->T < 1 || a->N < 1 || !a->rewards || !a->dones || !a->values || !a->last_values || !a->returns ||
+      !a->advantages || !a->moments || !a->ws || !a->counter)
+    return fail("lgx_gae: bad arguments");
+  hipLaunchKernelGGL(lgxm::gae_kernel, dim3((a->N + 255) / 256), dim3(256), 0, static_cast<hipStream_t>(stream), *a);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : fail(hipGetErrorString(e));
+}
+
+int32_t lgx_normalize_advantages(float* adv, int64_t n, const double* moments, double count, void* stream) {
+  if (n < 0 || (n > 0 && (!adv || !moments)) || !(count >= 2.0)) return fail("lgx_normalize_advantages: bad arguments");
+  if (n == 0) return 0;
+  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 1024);
+  hipLaunchKernelGGL(lgxm::adv_norm_kernel, dim3(blocks), dim3(256), 0, static_cast<hipStream_t>(stream), adv, n,
+                     moments, count);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : fail(hipGetErrorString(e));
 }

@@ -26,7 +26,7 @@ EXPORTED = ["lgx_mlp_abi_version", "lgx_mlp_sizeof_gemm_args", "lgx_mlp_pick_spl
             "lgx_mlp_last_error", "lgx_adam_step", "lgx_ppo_head_forward", "lgx_ppo_head_backward",
             "lgx_copy_batch", "lgx_act_head", "lgx_store_transition", "lgx_splitk_reduce_batch",
             "lgx_aux_loss_forward", "lgx_aux_loss_backward", "lgx_ppo_tail", "lgx_gemm_group",
-            "lgx_mlp_pick_split_group"]
+            "lgx_mlp_pick_split_group", "lgx_gae", "lgx_normalize_advantages"]
 TAIL_MAX_LOSSES = 8
 COPY_MAX = 16
 SPLITK_MAX = 24
@@ -97,6 +97,13 @@ class TransitionArgs(C.Structure):
                                           "values_out")] + [("gamma", C.c_float), ("B", C.c_int32)]
 
 
+class GaeArgs(C.Structure):
+    """Mirror of lgx_gae_args."""
+    _fields_ = [(n, C.c_void_p) for n in ("rewards", "dones", "values", "last_values", "returns", "advantages")] + \
+               [("T", C.c_int32), ("N", C.c_int32), ("gamma", C.c_float), ("lam", C.c_float)] + \
+               [(n, C.c_void_p) for n in ("moments", "ws", "counter")]
+
+
 class MlpLibError(RuntimeError):
     pass
 
@@ -134,6 +141,10 @@ def lib():
     L.lgx_gemm_group.restype = C.c_int32
     L.lgx_mlp_pick_split_group.argtypes = [vp, vp, vp, C.c_int32, vp]
     L.lgx_mlp_pick_split_group.restype = C.c_int32
+    L.lgx_gae.argtypes = [vp, vp]
+    L.lgx_gae.restype = C.c_int32
+    L.lgx_normalize_advantages.argtypes = [vp, C.c_int64, vp, C.c_double, vp]
+    L.lgx_normalize_advantages.restype = C.c_int32
     L.lgx_splitk_reduce_batch.argtypes = [vp, C.c_int32, vp]
     L.lgx_splitk_reduce_batch.restype = C.c_int32
     if L.lgx_mlp_abi_version() != ABI_VERSION:
@@ -198,6 +209,23 @@ def store_transition(rewards, dones, time_outs, values, rewards_out, dones_out, 
                           values.data_ptr(), rewards_out.data_ptr(), dones_out.data_ptr(), values_out.data_ptr(),
                           float(gamma), rewards.shape[0])
     _check(lib().lgx_store_transition(C.byref(args), _stream()), "lgx_store_transition")
+
+
+def gae(rewards, dones, values, last_values, returns, advantages, gamma, lam, moments, ws, counter):
+    """lgx_gae over [T, N, 1] storage buffers: returns, raw advantages, fp64 moments[0:2]."""
+    T, N = rewards.shape[0], rewards.shape[1]
+    for t in (rewards, dones, values, last_values, returns, advantages):
+        if not t.is_contiguous():
+            raise MlpLibError("gae: contiguous buffers only")
+    args = GaeArgs(rewards.data_ptr(), dones.data_ptr(), values.data_ptr(), last_values.data_ptr(), returns.data_ptr(),
+                   advantages.data_ptr(), T, N, float(gamma), float(lam), moments.data_ptr(), ws.data_ptr(),
+                   counter.data_ptr())
+    _check(lib().lgx_gae(C.byref(args), _stream()), "lgx_gae")
+
+
+def normalize_advantages(advantages, moments, count):
+    _check(lib().lgx_normalize_advantages(advantages.data_ptr(), advantages.numel(), moments.data_ptr(), float(count),
+                                          _stream()), "lgx_normalize_advantages")
 
 
 def adam_step(p, g, m, v, step, lr, beta1, beta2, eps, grad_scale=None):

@@ -109,6 +109,9 @@ class RolloutStorage:
         self.step = 0
 
     def compute_returns(self, last_values, gamma, lam):
+        if str(self.device).startswith("cuda"):
+            self._compute_returns_hip(last_values, gamma, lam)
+            return
         advantage = 0
         for step in reversed(range(self.num_transitions_per_env)):
             next_values = last_values if step == self.num_transitions_per_env - 1 else self.values[step + 1]
@@ -120,6 +123,23 @@ class RolloutStorage:
         torch.sub(self.returns, self.values, out=self.advantages)
         mean, std = self._global_mean(self.advantages)
         self.advantages.sub_(mean).div_(std + 1e-8)
+
+    def _compute_returns_hip(self, last_values, gamma, lam):
+        """The same scan and normalisation as two HIP launches (lgx_gae, lgx_normalize_advantages)
+        instead of ~150 small kernels; the moments are all-reduced across ranks in between."""
+        from legged_gym_custom_amd.rsl_rl.modules import hip_mlp
+        if getattr(self, "_gae_ws", None) is None:
+            self._gae_moments = torch.zeros(2, dtype=torch.float64, device=self.device)
+            self._gae_ws = torch.empty(2 * ((self.num_envs + 255) // 256), dtype=torch.float64, device=self.device)
+            self._gae_counter = torch.zeros(1, dtype=torch.int32, device=self.device)
+        m = self._gae_moments
+        hip_mlp.gae(self.rewards, self.dones, self.values, last_values.reshape(-1).contiguous(), self.returns,
+                    self.advantages, gamma, lam, m, self._gae_ws, self._gae_counter)
+        count = float(self.advantages.numel())
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            dist.all_reduce(m)
+            count *= dist.get_world_size()
+        hip_mlp.normalize_advantages(self.advantages, m, count)
 
     def _global_mean(self, a):
         """(mean, unbiased std) of `a` over every rank's shard."""

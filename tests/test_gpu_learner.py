@@ -74,3 +74,32 @@ def test_gpu_update_tracks_cpu_torch_update():
     st = gpu.optimizer.state_dict()["state"]
     assert float(st[0]["step"]) == 3 * gpu.num_learning_epochs * gpu.num_mini_batches
     assert gpu.grads.check()
+
+
+def test_gae_kernel_matches_torch_statement():
+    """RolloutStorage.compute_returns on the GPU (lgx_gae + lgx_normalize_advantages) == the
+    reference's loop (rollout_storage.py:110-124) in torch ops: returns bitwise (same fp32
+    operation order), normalised advantages to fp32 rounding (fp64 moments vs torch's)."""
+    from legged_gym_custom_amd.rsl_rl.storage import RolloutStorage
+    T, N, gamma, lam = 24, 1000, 0.99, 0.95
+    dev = "cuda:0"
+    s = RolloutStorage(N, T, [5], [2], [3], [1], [1], [2], device=dev)
+    g = torch.Generator(device=dev).manual_seed(0)
+    s.rewards.copy_(torch.randn(T, N, 1, device=dev, generator=g))
+    s.values.copy_(torch.randn(T, N, 1, device=dev, generator=g) * 3)
+    s.dones.copy_((torch.rand(T, N, 1, device=dev, generator=g) < 0.05).byte())
+    last = torch.randn(N, 1, device=dev, generator=g)
+    for _ in range(2):  # the counter/workspace are reused
+        s.compute_returns(last, gamma, lam)
+    ret = torch.zeros_like(s.returns)
+    adv = 0
+    for step in reversed(range(T)):
+        next_values = last if step == T - 1 else s.values[step + 1]
+        not_terminal = 1.0 - s.dones[step].float()
+        delta = s.rewards[step] + not_terminal * gamma * next_values - s.values[step]
+        adv = delta + not_terminal * gamma * lam * adv
+        ret[step] = adv + s.values[step]
+    a = ret - s.values
+    a = (a - a.mean()) / (a.std() + 1e-8)
+    assert torch.equal(ret, s.returns)
+    torch.testing.assert_close(s.advantages, a, rtol=1e-5, atol=1e-6)
