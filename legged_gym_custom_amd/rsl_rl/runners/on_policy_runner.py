@@ -200,26 +200,34 @@ class OnPolicyRunner:
                            "n": torch.zeros((), dtype=torch.long, device=self.device), "ep_keys": None,
                            "ep_sum": None, "ep_cnt": z(())}
         tot_iter = self.current_learning_iteration + num_learning_iterations
+        on_gpu = self.device.startswith("cuda")
         for it in range(self.current_learning_iteration, tot_iter):
             start = time.time()
             use_adaptation_mode = it % self.dagger_update_freq == 0
+            if on_gpu:  # split collection/learning by device events: no host sync in between
+                evs = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+                evs[0].record()
             with torch.inference_mode():
                 self._rollout(use_adaptation_mode, track)
-                if self.device.startswith("cuda"):
-                    torch.cuda.synchronize(self.device)
-                stop = time.time()
-                collection_time = stop - start
-                start = stop
+                if on_gpu:
+                    evs[1].record()
+                mid = time.time()
                 self.alg.compute_returns(self._obs[2])
             if use_adaptation_mode:
                 mean_adaptation_loss = self.alg.update_dagger()
             else:
                 mean_value_loss, mean_surrogate_loss, mean_regularization_loss, reg_coef, mean_estimator_loss = \
                     self.alg.update()
-            if self.device.startswith("cuda"):
+            if on_gpu:
+                evs[2].record()
                 torch.cuda.synchronize(self.device)
             stop = time.time()
-            learn_time = stop - start
+            if on_gpu:  # wall time of the iteration, split at the rollout's end on the device
+                host_lead = max(0.0, stop - start - evs[0].elapsed_time(evs[2]) * 1e-3)
+                collection_time = evs[0].elapsed_time(evs[1]) * 1e-3 + host_lead
+                learn_time = stop - start - collection_time
+            else:
+                collection_time, learn_time = mid - start, stop - mid
             self.last_perf = {"collection_time": collection_time, "learn_time": learn_time,
                               "fps": self.num_steps_per_env * env.num_envs / (collection_time + learn_time)}
             self._capture_rollout(track)
