@@ -937,6 +937,21 @@ static int tile_n(int N) {
   return N > 128 ? 128 : 64;
 }
 
+// Forward / input-gradient launches over few rows (the rollout's 4096-env batches): 64-wide
+// tiles double the block count of a launch that would otherwise leave most CUs idle
+// (4096 x 736 -> 512 forward: 33 -> 23 us, tools/gemm_variants.py); weight gradients and
+// the update's 24,576-row launches keep tile_n.
+static int tile_n_for(int M, int N, bool rows_are_batch) {
+  static int forced = -1;
+  if (forced < 0) {
+    const char* e = getenv("LGX_MLP_BN");
+    forced = e ? atoi(e) : 0;
+  }
+  if (forced == 64 || forced == 128) return forced;
+  if (rows_are_batch && M <= 8192) return 64;
+  return tile_n(N);
+}
+
 // ================================================================ rollout bookkeeping
 namespace lgxm {
 
@@ -1208,7 +1223,7 @@ int32_t lgx_gemm(const lgx_gemm_args* a, void* stream) {
   const int split = p.split;
   const bool cs = a->colsum != nullptr;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  const int bn = tile_n(a->N);
+  const int bn = tile_n_for(a->M, a->N, a->a_kcontig != 0);
   const bool ma = a->M % 4 == 0, nb = a->N % 4 == 0;  // m/n-contiguous stagers: whole 4-row groups
   if (a->a_kcontig && !a->b_kcontig) {  // input gradient, W read in place
     if (nb) launch<KV, MV, false>(p, bn, s);
@@ -1244,7 +1259,7 @@ int32_t lgx_gemm_group(const lgx_gemm_args* args, int32_t n, void* stream) {
   if (n < 0 || n > LGX_GEMM_GROUP_MAX || (n > 0 && !args)) return fail("lgx_gemm_group: 0 <= n <= LGX_GEMM_GROUP_MAX");
   GroupParams g;
   g.n = 0;
-  int kind = -1, maxn = 0;
+  int kind = -1, maxn = 0, maxm = 0;
   for (int i = 0; i < n; ++i) {
     const lgx_gemm_args* a = args + i;
     Params p;
@@ -1265,6 +1280,7 @@ int32_t lgx_gemm_group(const lgx_gemm_args* args, int32_t n, void* stream) {
     g.mode[g.n] = mode;
     g.p[g.n] = p;
     maxn = std::max(maxn, a->N);
+    maxm = std::max(maxm, a->M);
     ++g.n;
   }
   if (g.n == 0) return 0;
@@ -1274,7 +1290,7 @@ int32_t lgx_gemm_group(const lgx_gemm_args* args, int32_t n, void* stream) {
       std::swap(g.p[k], g.p[k - 1]);
       std::swap(g.mode[k], g.mode[k - 1]);
     }
-  const int bn = tile_n(maxn);
+  const int bn = tile_n_for(maxm, maxn, kind != G_DW);
   int total = 0;
   for (int i = 0; i < g.n; ++i) {
     Params& p = g.p[i];
