@@ -188,6 +188,10 @@ typedef struct lgx_copy_desc {
   const void* src; void* dst; int64_t nbytes;
 } lgx_copy_desc;
 int32_t lgx_copy_batch(const lgx_copy_desc* descs, int32_t n, void* stream);
+/* Row gather of up to LGX_COPY_MAX row-major buffers in one launch (the storage permuted once
+ * per update, rollout_storage.py:134-181): dst row r = src row idx[r] (r < rows), row_bytes
+ * each (16-B vector path when row_bytes and both bases are 16-B aligned). */
+int32_t lgx_gather_rows(const lgx_copy_desc* descs, int32_t n, const int64_t* idx, int64_t rows, void* stream);
 
 /* PPO.act action head (actor_critic.py:205-226 + ppo.py:141-146) for a diagonal Gaussian:
  *   a = mean + std * eps,  logp_i = sum_j -(a-mean)^2/(2 std_j^2) - log std_j - log sqrt(2 pi)

@@ -978,6 +978,32 @@ __global__ __launch_bounds__(256) void copy_batch_kernel(CopyBatch cb) {
   }
 }
 
+// blockIdx.y = entry (nbytes = bytes per row); threads stride over (row, chunk) pairs
+__global__ __launch_bounds__(256) void gather_rows_kernel(CopyBatch cb, const int64_t* __restrict__ idx, int64_t rows) {
+  const lgx_copy_desc& d = cb.d[blockIdx.y];
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool vec = ((reinterpret_cast<uintptr_t>(d.src) | reinterpret_cast<uintptr_t>(d.dst) | (uintptr_t)d.nbytes) &
+                    15) == 0;
+  if (vec) {
+    const int64_t per = d.nbytes >> 4;
+    const float4* __restrict__ s = reinterpret_cast<const float4*>(d.src);
+    float4* __restrict__ t = reinterpret_cast<float4*>(d.dst);
+    for (int64_t i = i0; i < rows * per; i += stride) {
+      const int64_t r = i / per, c = i - r * per;
+      t[i] = s[idx[r] * per + c];
+    }
+  } else {
+    const int64_t per = d.nbytes >> 2;  // 4-B elements (host checks)
+    const float* __restrict__ s = reinterpret_cast<const float*>(d.src);
+    float* __restrict__ t = reinterpret_cast<float*>(d.dst);
+    for (int64_t i = i0; i < rows * per; i += stride) {
+      const int64_t r = i / per, c = i - r * per;
+      t[i] = s[idx[r] * per + c];
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void act_head_kernel(lgx_act_head_args p) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= p.B) return;
@@ -1393,6 +1419,27 @@ int32_t lgx_copy_batch(const lgx_copy_desc* descs, int32_t n, void* stream) {
   const unsigned bx = (unsigned)std::min<int64_t>((chunks + 255) / 256, 1024);
   hipLaunchKernelGGL(lgxm::copy_batch_kernel, dim3(bx, (unsigned)n), dim3(256), 0, static_cast<hipStream_t>(stream),
                      cb);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : fail(hipGetErrorString(e));
+}
+
+int32_t lgx_gather_rows(const lgx_copy_desc* descs, int32_t n, const int64_t* idx, int64_t rows, void* stream) {
+  if (n < 0 || n > LGX_COPY_MAX || (n > 0 && !descs) || rows < 0 || (rows > 0 && !idx))
+    return fail("lgx_gather_rows: bad arguments");
+  if (n == 0 || rows == 0) return 0;
+  lgxm::CopyBatch cb;
+  int64_t most = 0;
+  for (int i = 0; i < n; ++i) {
+    if (descs[i].nbytes < 0 || descs[i].nbytes % 4 != 0 || (descs[i].nbytes > 0 && (!descs[i].src || !descs[i].dst)))
+      return fail("lgx_gather_rows: bad entry (row bytes must be a multiple of 4)");
+    cb.d[i] = descs[i];
+    most = descs[i].nbytes > most ? descs[i].nbytes : most;
+  }
+  cb.n = n;
+  const int64_t work = rows * ((most + 15) / 16);
+  const unsigned bx = (unsigned)std::min<int64_t>((work + 255) / 256, 2048);
+  hipLaunchKernelGGL(lgxm::gather_rows_kernel, dim3(bx, (unsigned)n), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     cb, idx, rows);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : fail(hipGetErrorString(e));
 }

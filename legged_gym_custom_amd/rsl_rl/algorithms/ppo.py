@@ -507,7 +507,7 @@ class PPO:
         in update_dagger)."""
         if self.on_gpu:
             with torch.no_grad():
-                self._shuf = [t.index_select(0, self._perm) for t in self.storage._flat()]
+                self._shuf = hip_mlp.gather_rows(self.storage._flat(), self._perm)  # one launch
                 self._adapt_all = self.actor_critic.adaptation_encoder(self._shuf[0])
 
     def _update_body_eager(self):

@@ -26,7 +26,8 @@ EXPORTED = ["lgx_mlp_abi_version", "lgx_mlp_sizeof_gemm_args", "lgx_mlp_pick_spl
             "lgx_mlp_last_error", "lgx_adam_step", "lgx_ppo_head_forward", "lgx_ppo_head_backward",
             "lgx_copy_batch", "lgx_act_head", "lgx_store_transition", "lgx_splitk_reduce_batch",
             "lgx_aux_loss_forward", "lgx_aux_loss_backward", "lgx_ppo_tail", "lgx_gemm_group",
-            "lgx_mlp_pick_split_group", "lgx_gae", "lgx_normalize_advantages"]
+            "lgx_mlp_pick_split_group", "lgx_gae", "lgx_normalize_advantages",
+            "lgx_gather_rows"]
 TAIL_MAX_LOSSES = 8
 COPY_MAX = 16
 SPLITK_MAX = 24
@@ -141,6 +142,8 @@ def lib():
     L.lgx_gemm_group.restype = C.c_int32
     L.lgx_mlp_pick_split_group.argtypes = [vp, vp, vp, C.c_int32, vp]
     L.lgx_mlp_pick_split_group.restype = C.c_int32
+    L.lgx_gather_rows.argtypes = [vp, C.c_int32, vp, C.c_int64, vp]
+    L.lgx_gather_rows.restype = C.c_int32
     L.lgx_gae.argtypes = [vp, vp]
     L.lgx_gae.restype = C.c_int32
     L.lgx_normalize_advantages.argtypes = [vp, C.c_int64, vp, C.c_double, vp]
@@ -194,6 +197,24 @@ def copy_batch(dsts, srcs):
         descs[n].src, descs[n].dst, descs[n].nbytes = x.data_ptr(), d.data_ptr(), x.numel() * x.element_size()
         n += 1
     _check(lib().lgx_copy_batch(descs, n, _stream()), "lgx_copy_batch")
+
+
+def gather_rows(srcs, idx):
+    """[t.index_select(0, idx) for t in srcs] (contiguous fp32/4-B tensors) in one launch."""
+    if idx.dtype != torch.int64:
+        raise MlpLibError("gather_rows: int64 indices only")
+    idx = idx.contiguous()
+    outs = [torch.empty((idx.numel(),) + tuple(t.shape[1:]), device=t.device, dtype=t.dtype) for t in srcs]
+    for i in range(0, len(srcs), COPY_MAX):
+        chunk = list(zip(srcs[i:i + COPY_MAX], outs[i:i + COPY_MAX]))
+        descs = (CopyDesc * COPY_MAX)()
+        for k, (x, o) in enumerate(chunk):
+            if not x.is_contiguous() or x.element_size() != 4:
+                raise MlpLibError("gather_rows: contiguous 4-byte tensors only")
+            descs[k].src, descs[k].dst = x.data_ptr(), o.data_ptr()
+            descs[k].nbytes = (x.numel() // max(1, x.shape[0])) * 4
+        _check(lib().lgx_gather_rows(descs, len(chunk), idx.data_ptr(), idx.numel(), _stream()), "lgx_gather_rows")
+    return outs
 
 
 def act_head(mean, std, eps, actions, mu, sigma, logp):

@@ -369,3 +369,14 @@ def test_forward_group_matches_separate_chains_bitwise():
     with torch.no_grad():
         o3 = H.forward_group([(nets[0], xs[0]), (nets[1], xs[1]), (nets[2], xs[2]), (nets[3], parts)])
     assert all(torch.equal(a, b) for a, b in zip(o1, o3))
+
+
+def test_gather_rows_matches_index_select():
+    """lgx_gather_rows (one launch over the storage's buffers) == index_select, bitwise, for
+    16-B (vector) and 4-B row widths."""
+    g = torch.Generator(device=dev).manual_seed(21)
+    rows = 5000
+    srcs = [torch.randn(rows, w, device=dev, generator=g) for w in (572, 29, 736, 3, 132, 12, 1)]
+    idx = torch.randperm(rows, device=dev, generator=g)[:3000]
+    for a, b in zip(H.gather_rows(srcs, idx), [t.index_select(0, idx) for t in srcs]):
+        assert torch.equal(a, b)
