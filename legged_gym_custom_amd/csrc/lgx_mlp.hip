@@ -108,7 +108,7 @@ struct Stager {
         const int row = min(row0 + r, rows - 1), k = k0 + g * 8;
         const float* q = p + (int64_t)row * ld + k;
         float* o = v + t * 8;
-        if (!KGUARD) {
+        if (!KGUARD || k + 8 <= kend) {  // whole 8-k chunk inside the K range: vector loads
           const f32x4u x0 = *reinterpret_cast<const f32x4u*>(q);
           const f32x4u x1 = *reinterpret_cast<const f32x4u*>(q + 4);
           o[0] = x0.x; o[1] = x0.y; o[2] = x0.z; o[3] = x0.w;
