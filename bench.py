@@ -42,6 +42,52 @@ def env_bytes_per_env_step(P, num_bodies, ks):
     return rd + wr
 
 
+MFMA_BF16_PEAK_TFLOPS = 2500.0  # dense bf16 (MI355X_MICROARCH.md); 3xbf16 = 3 MFMA products per fp32 MAC
+
+
+def learner_gemm_roofline(dev, rows=24576, reps=10):
+    """The update's weight-gradient group (every dW/db of one go2 minibatch backward, one
+    lgx_gemm_group launch + its split-K reduction) timed with HIP events on its stream:
+    MFMA rate = 3 bf16 products x 2 x rows x sum(in x out) / time."""
+    from legged_gym_custom_amd.rsl_rl.modules import hip_mlp as H
+    layers = [(627, 512), (512, 256), (256, 128), (128, 12), (736, 512), (512, 256), (256, 128), (128, 1),
+              (29, 64), (64, 20), (20, 20), (132, 128), (128, 64), (64, 32), (572, 128), (128, 64), (64, 3)]
+    g = torch.Generator(device=dev).manual_seed(7)
+    data = [(torch.randn(rows, o, device=dev, generator=g), torch.randn(rows, i, device=dev, generator=g),
+             torch.zeros(o, i, device=dev), torch.zeros(o, device=dev)) for i, o in layers]
+
+    def once():
+        with H.deferred_weight_grads():
+            for dy, x, dW, db in data:
+                H.linear_weight_grad(dy, x, dW, db, accumulate=True)
+    side = torch.cuda.Stream(dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(side):
+        for _ in range(3):
+            once()
+    torch.cuda.current_stream(dev).wait_stream(side)
+    graph = torch.cuda.CUDAGraph()  # replayed: device time only, no host launch gaps
+    with torch.cuda.graph(graph):
+        for _ in range(reps):
+            once()
+    graph.replay()
+    stream = torch.cuda.current_stream(dev)
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize(dev)
+    s.record(stream)
+    graph.replay()
+    e.record(stream)
+    torch.cuda.synchronize(dev)
+    t = s.elapsed_time(e) / reps * 1e-3
+    flop = 2.0 * rows * sum(i * o for i, o in layers)
+    achieved = 3 * flop / t / 1e12
+    return {"bound": "mfma", "kernel": "lgxm::gemm_group_kernel<2, 128> + splitk_reduce_batch",
+            "workload": f"all 17 weight gradients of one go2 minibatch ({rows} rows)", "achieved": round(achieved, 1),
+            "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4),
+            "us_per_launch": round(t * 1e6, 1), "fp32_equivalent_tflops": round(flop / t / 1e12, 1),
+            "note": "3xbf16 split: 3 bf16 MFMA products per fp32 multiply-add"}
+
+
 def committed_traffic(num_envs):
     """Env-step kernel HBM bytes per launch from the newest committed PMC profile
     (profiles/<round>_env_traffic.json, made by tools/profile_round.sh: FETCH_SIZE x2 +
@@ -190,6 +236,8 @@ def main():
                          "bytes_per_env_step": bpe, "bytes_per_launch": launch_bytes,
                          "traffic": None if traffic is None else round(traffic), "traffic_source": traffic_src},
         }
+        if args.task == "go2":
+            out["roofline_learner"] = learner_gemm_roofline(dev)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline()
         print(json.dumps(out))
