@@ -88,6 +88,15 @@ typedef struct lgx_splitk_desc {
   int32_t M, N, split, epilogue;
 } lgx_splitk_desc;
 int32_t lgx_splitk_reduce_batch(const lgx_splitk_desc* descs, int32_t n, void* stream);
+/* Up to LGX_TRANSPOSE_MAX matrix transposes in one launch: dst[c * rows + r] = src[r * ld + c]
+ * (r < rows, c < cols; dst contiguous [cols, rows]). The backward pass transposes the layer
+ * weights it needs once, so input-gradient GEMMs read W^T k-contiguous (lgx_gemm with
+ * b_kcontig = 1) instead of W n-contiguous. */
+#define LGX_TRANSPOSE_MAX 24
+typedef struct lgx_transpose_desc {
+  const float* src; int64_t ld; int32_t rows, cols; float* dst;
+} lgx_transpose_desc;
+int32_t lgx_transpose_batch(const lgx_transpose_desc* descs, int32_t n, void* stream);
 const char* lgx_mlp_last_error(void);
 
 /* One Adam step over a contiguous parameter segment (fp32), replacing torch.optim.Adam's

@@ -571,6 +571,33 @@ __device__ __forceinline__ void adam1(float& p, float g, float& m, float& v, flo
   p -= step_size * m / (sqrtf(v) / bc2s + eps);
 }
 
+struct TransposeBatch {
+  lgx_transpose_desc d[LGX_TRANSPOSE_MAX];
+};
+
+// blockIdx.z = entry; 32 x 32 tiles through LDS (padded rows), blocks stride over the tiles
+__global__ __launch_bounds__(256) void transpose_batch_kernel(TransposeBatch b) {
+  __shared__ float tile[32][33];
+  const lgx_transpose_desc& d = b.d[blockIdx.z];
+  const int tiles_c = (d.cols + 31) / 32, tiles = ((d.rows + 31) / 32) * tiles_c;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int t = blockIdx.x; t < tiles; t += gridDim.x) {
+    const int r0 = (t / tiles_c) * 32, c0 = (t % tiles_c) * 32;
+#pragma unroll
+    for (int k = 0; k < 32; k += 8) {
+      const int r = r0 + ty + k, c = c0 + tx;
+      tile[ty + k][tx] = (r < d.rows && c < d.cols) ? d.src[(int64_t)r * d.ld + c] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 32; k += 8) {
+      const int c = c0 + ty + k, r = r0 + tx;
+      if (c < d.cols && r < d.rows) d.dst[(int64_t)c * d.rows + r] = tile[tx][ty + k];
+    }
+    __syncthreads();
+  }
+}
+
 // Adam over a flat fp32 segment: float4 lanes, grid-stride.
 __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                             float* __restrict__ v, int64_t n, const float* __restrict__ lr_dev, float lr, float b1,
@@ -1397,6 +1424,25 @@ int32_t lgx_splitk_reduce_batch(const lgx_splitk_desc* descs, int32_t n, void* s
   const unsigned bx = (unsigned)std::min<int64_t>((most + 255) / 256, 2048);
   hipLaunchKernelGGL(lgxm::splitk_reduce_batch, dim3(bx, (unsigned)n), dim3(256), 0, static_cast<hipStream_t>(stream),
                      b);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : fail(hipGetErrorString(e));
+}
+
+int32_t lgx_transpose_batch(const lgx_transpose_desc* descs, int32_t n, void* stream) {
+  if (n < 0 || n > LGX_TRANSPOSE_MAX || (n > 0 && !descs)) return fail("lgx_transpose_batch: 0 <= n <= LGX_TRANSPOSE_MAX");
+  if (n == 0) return 0;
+  lgxm::TransposeBatch b;
+  int most = 0;
+  for (int i = 0; i < n; ++i) {
+    const lgx_transpose_desc& d = descs[i];
+    if (d.rows < 0 || d.cols < 0 || d.ld < d.cols || ((int64_t)d.rows * d.cols > 0 && (!d.src || !d.dst)))
+      return fail("lgx_transpose_batch: bad entry");
+    b.d[i] = d;
+    most = std::max(most, ((d.rows + 31) / 32) * ((d.cols + 31) / 32));
+  }
+  if (most == 0) return 0;
+  hipLaunchKernelGGL(lgxm::transpose_batch_kernel, dim3((unsigned)std::min(most, 256), 1, (unsigned)n), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), b);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : fail(hipGetErrorString(e));
 }

@@ -27,11 +27,12 @@ EXPORTED = ["lgx_mlp_abi_version", "lgx_mlp_sizeof_gemm_args", "lgx_mlp_pick_spl
             "lgx_copy_batch", "lgx_act_head", "lgx_store_transition", "lgx_splitk_reduce_batch",
             "lgx_aux_loss_forward", "lgx_aux_loss_backward", "lgx_ppo_tail", "lgx_gemm_group",
             "lgx_mlp_pick_split_group", "lgx_gae", "lgx_normalize_advantages",
-            "lgx_gather_rows"]
+            "lgx_gather_rows", "lgx_transpose_batch"]
 TAIL_MAX_LOSSES = 8
 COPY_MAX = 16
 SPLITK_MAX = 24
 GROUP_MAX = 20
+TRANSPOSE_MAX = 24
 
 
 class GemmArgs(C.Structure):
@@ -98,6 +99,12 @@ class TransitionArgs(C.Structure):
                                           "values_out")] + [("gamma", C.c_float), ("B", C.c_int32)]
 
 
+class TransposeDesc(C.Structure):
+    """Mirror of lgx_transpose_desc."""
+    _fields_ = [("src", C.c_void_p), ("ld", C.c_int64), ("rows", C.c_int32), ("cols", C.c_int32),
+                ("dst", C.c_void_p)]
+
+
 class GaeArgs(C.Structure):
     """Mirror of lgx_gae_args."""
     _fields_ = [(n, C.c_void_p) for n in ("rewards", "dones", "values", "last_values", "returns", "advantages")] + \
@@ -142,6 +149,8 @@ def lib():
     L.lgx_gemm_group.restype = C.c_int32
     L.lgx_mlp_pick_split_group.argtypes = [vp, vp, vp, C.c_int32, vp]
     L.lgx_mlp_pick_split_group.restype = C.c_int32
+    L.lgx_transpose_batch.argtypes = [vp, C.c_int32, vp]
+    L.lgx_transpose_batch.restype = C.c_int32
     L.lgx_gather_rows.argtypes = [vp, C.c_int32, vp, C.c_int64, vp]
     L.lgx_gather_rows.restype = C.c_int32
     L.lgx_gae.argtypes = [vp, vp]
@@ -622,6 +631,31 @@ def _dx_args(g, W, y_prev, dx):
                     act=_ptr(y_prev), ld_act=0 if y_prev is None else y_prev.stride(0), split_k=1)
 
 
+def transpose_batch(mats):
+    """[m.t().contiguous() for m in mats] (2-D fp32 views with unit column stride) in one launch."""
+    outs = []
+    for i in range(0, len(mats), TRANSPOSE_MAX):
+        chunk = mats[i:i + TRANSPOSE_MAX]
+        descs = (TransposeDesc * TRANSPOSE_MAX)()
+        for k, m in enumerate(chunk):
+            if m.dim() != 2 or m.stride(1) != 1 or m.dtype != torch.float32:
+                raise MlpLibError("transpose_batch: 2-D fp32 with unit column stride only")
+            o = torch.empty(m.shape[1], m.shape[0], device=m.device, dtype=torch.float32)
+            descs[k] = TransposeDesc(m.data_ptr(), m.stride(0), m.shape[0], m.shape[1], o.data_ptr())
+            outs.append(o)
+        _check(lib().lgx_transpose_batch(descs, len(chunk), _stream()), "lgx_transpose_batch")
+    return outs
+
+
+def _dxt_args(g, Wt, y_prev, dx):
+    """Input gradient dX = (dY W) * ELU'(y_prev) with W^T ([K_in, N_out] contiguous) streamed
+    k-contiguous."""
+    M, N = g.shape
+    return GemmArgs(A=_ptr(g), lda=g.stride(0), a_kcontig=1, B=_ptr(Wt), ldb=Wt.stride(0), b_kcontig=1, C=_ptr(dx),
+                    ldc=dx.stride(0), M=M, N=Wt.shape[0], K=N, epilogue=EPI_DELU if y_prev is not None else 0,
+                    act=_ptr(y_prev), ld_act=0 if y_prev is None else y_prev.stride(0), split_k=1)
+
+
 def _group_forward(xs, chains):
     """Layer d of every chain in one launch; returns each chain's list of layer outputs."""
     outs = [[] for _ in chains]
@@ -678,6 +712,25 @@ class _GroupFn(torch.autograd.Function):
             st.append([x, wb, outs, g, pos])
             pos += nparts + 2 * n
         part_grads = [[None] * nparts for nparts, _f in meta]
+        # the weights (or layer-0 column spans) whose input gradient this pass forms, transposed
+        # in one launch so the input-gradient GEMMs stream W^T k-contiguous
+        need_t, spans = [], {}
+        for c, ((nparts, flags), item) in enumerate(zip(meta, st)):
+            if item[3] is None:
+                continue
+            wb = item[1]
+            for i in range(1, len(flags)):
+                spans[(c, i)] = len(need_t)
+                need_t.append(wb[2 * i])
+            need = [ctx.needs_input_grad[1 + item[4] + j] for j in range(nparts)]
+            if any(need):
+                offs = [0]
+                for w in ctx.widths[c]:
+                    offs.append(offs[-1] + w)
+                first, last = need.index(True), nparts - 1 - need[::-1].index(True)
+                spans[(c, 0)] = len(need_t)
+                need_t.append(wb[0][:, offs[first]:offs[last + 1]])
+        wts = transpose_batch(need_t) if need_t else []
         for t in range(max(len(f) for _n, f in meta)):
             args, news = [], []
             for c, ((nparts, flags), item) in enumerate(zip(meta, st)):
@@ -692,7 +745,7 @@ class _GroupFn(torch.autograd.Function):
                                        accumulate=True)
                 if i > 0:
                     dx = torch.empty(g.shape[0], wb[2 * i].shape[1], device=g.device, dtype=torch.float32)
-                    args.append(_dx_args(g, wb[2 * i], outs[i - 1] if flags[i - 1] else None, dx))
+                    args.append(_dxt_args(g, wts[spans[(c, i)]], outs[i - 1] if flags[i - 1] else None, dx))
                     news.append((c, dx))
                     continue
                 need = [ctx.needs_input_grad[1 + p0 + j] for j in range(nparts)]
@@ -704,7 +757,7 @@ class _GroupFn(torch.autograd.Function):
                     last = nparts - 1 - need[::-1].index(True)
                     lo, hi = offs[first], offs[last + 1]
                     dx = torch.empty(g.shape[0], hi - lo, device=g.device, dtype=torch.float32)
-                    args.append(_dx_args(g, wb[0][:, lo:hi], None, dx))
+                    args.append(_dxt_args(g, wts[spans[(c, 0)]], None, dx))
                     for j in range(first, last + 1):
                         if need[j]:
                             part_grads[c][j] = dx[:, offs[j] - lo:offs[j + 1] - lo]

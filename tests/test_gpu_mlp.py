@@ -380,3 +380,11 @@ def test_gather_rows_matches_index_select():
     idx = torch.randperm(rows, device=dev, generator=g)[:3000]
     for a, b in zip(H.gather_rows(srcs, idx), [t.index_select(0, idx) for t in srcs]):
         assert torch.equal(a, b)
+
+
+def test_transpose_batch_matches_torch():
+    g = torch.Generator(device=dev).manual_seed(31)
+    W = torch.randn(512, 627, device=dev, generator=g)
+    mats = [W, W[:, 572:624], torch.randn(1, 128, device=dev, generator=g), torch.randn(33, 65, device=dev, generator=g)]
+    for a, m in zip(H.transpose_batch(mats), mats):
+        assert torch.equal(a, m.t().contiguous())

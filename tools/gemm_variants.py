@@ -32,6 +32,17 @@ g2 = torch.randn(B, 256, device="cuda")
 W2 = torch.randn(256, 512, device="cuda") * 0.05
 dxa, dxc = torch.empty(B, 512, device="cuda"), torch.empty(B, 512, device="cuda")
 dx_args = [H._dx_args(g1, W1, Y0, dxa), H._dx_args(g2, W2, Y0, dxc)]
+W1t, W2t = W1.t().contiguous(), W2.t().contiguous()
+
+
+def _dxt(g, Wt, y, dx):  # the same input gradient with W transposed (k-contiguous B)
+    M, N = g.shape
+    return H.GemmArgs(A=g.data_ptr(), lda=g.stride(0), a_kcontig=1, B=Wt.data_ptr(), ldb=Wt.stride(0), b_kcontig=1,
+                      C=dx.data_ptr(), ldc=dx.stride(0), M=M, N=Wt.shape[0], K=N, epilogue=H.EPI_DELU,
+                      act=y.data_ptr(), ld_act=y.stride(0), split_k=1)
+
+
+dxt_args = [_dxt(g1, W1t, Y0, dxa), _dxt(g2, W2t, Y0, dxc)]
 
 
 def dw_group():
@@ -56,9 +67,10 @@ r = {"fwd736x512": t(lambda: H.linear_forward(X, W, b, True)),
      "dx256to512": t(lambda: H.linear_input_grad(g1, W1, Y0)),
      "fwdgroup": t(lambda: H.run_group(fwd_args)),
      "dxgroup": t(lambda: H.run_group(dx_args)),
+     "dxgroupT": t(lambda: H.run_group(dxt_args)),
      "dWgroup": t(dw_group, it=5)}
 fl = {"fwd736x512": 2 * B * 736 * 512, "fwd128x64": 2 * B * 128 * 64, "fwd4096r": 2 * 4096 * 736 * 512, "dx256to512": 2 * B * 256 * 512,
-      "fwdgroup": 2 * B * 512 * (627 + 736), "dxgroup": 2 * 2 * B * 256 * 512,
+      "fwdgroup": 2 * B * 512 * (627 + 736), "dxgroup": 2 * 2 * B * 256 * 512, "dxgroupT": 2 * 2 * B * 256 * 512,
       "dWgroup": sum(2 * B * i * o for i, o in layers)}
 print(os.path.basename(os.environ.get("LGX_MLP_LIB", "default")), "BN", os.environ.get("LGX_GROUP_BN", "auto"), f"elu max {ulp:.1f} ulp", " ".join(
     f"{k} {v:.1f}us ({fl[k] / v / 1e6:.0f}TF)" for k, v in r.items()), flush=True)
