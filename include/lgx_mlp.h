@@ -159,6 +159,11 @@ typedef struct lgx_aux_loss_args {
 } lgx_aux_loss_args;
 int32_t lgx_aux_loss_forward(const lgx_aux_loss_args* args, void* stream);
 int32_t lgx_aux_loss_backward(const lgx_aux_loss_args* args, void* stream);
+/* Both loss heads of one minibatch in one launch each way (blockIdx.y selects the head):
+ * the same results as lgx_ppo_head_* and lgx_aux_loss_* on the same arguments. head->B must
+ * equal aux->B. */
+int32_t lgx_loss_heads_forward(const lgx_ppo_head_args* head, const lgx_aux_loss_args* aux, void* stream);
+int32_t lgx_loss_heads_backward(const lgx_ppo_head_args* head, const lgx_aux_loss_args* aux, void* stream);
 
 /* The optimizer tail of one PPO minibatch (rsl_rl ppo.py:264-291) in two launches, over
  * the flat gradient/parameter/moment buffers (one layout):

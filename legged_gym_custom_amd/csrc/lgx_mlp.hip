@@ -702,7 +702,7 @@ __device__ __forceinline__ HeadRow head_row(const lgx_ppo_head_args& p, int i, c
   return r;
 }
 
-__global__ void ppo_head_fwd(lgx_ppo_head_args p) {
+__device__ __forceinline__ void ppo_head_fwd_body(const lgx_ppo_head_args& p) {
   __shared__ float red[4 * 4];
   __shared__ float stdv[HMAXA], lstd[HMAXA];
   if (threadIdx.x < p.A) { stdv[threadIdx.x] = p.std[threadIdx.x]; lstd[threadIdx.x] = logf(p.std[threadIdx.x]); }
@@ -748,7 +748,7 @@ __global__ void ppo_head_fwd(lgx_ppo_head_args p) {
   }
 }
 
-__global__ void ppo_head_bwd(lgx_ppo_head_args p) {
+__device__ __forceinline__ void ppo_head_bwd_body(const lgx_ppo_head_args& p) {
   __shared__ float red[4 * HMAXA];
   __shared__ float stdv[HMAXA], lstd[HMAXA];
   if (threadIdx.x < p.A) { stdv[threadIdx.x] = p.std[threadIdx.x]; lstd[threadIdx.x] = logf(p.std[threadIdx.x]); }
@@ -808,7 +808,7 @@ __global__ void ppo_head_bwd(lgx_ppo_head_args p) {
 }
 
 // ---------------------------------------------------------------- ROA + estimator losses
-__global__ void aux_loss_fwd(lgx_aux_loss_args p) {
+__device__ __forceinline__ void aux_loss_fwd_body(const lgx_aux_loss_args& p) {
   __shared__ float red[4 * 2];
   float v[2] = {0.f, 0.f};
   for (int i = blockIdx.x * HT + threadIdx.x; i < p.B; i += gridDim.x * HT) {
@@ -839,7 +839,7 @@ __global__ void aux_loss_fwd(lgx_aux_loss_args p) {
   }
 }
 
-__global__ void aux_loss_bwd(lgx_aux_loss_args p) {
+__device__ __forceinline__ void aux_loss_bwd_body(const lgx_aux_loss_args& p) {
   const int i = blockIdx.x * HT + threadIdx.x;
   if (i >= p.B) return;
   const float gr = p.g[0] / p.B, ge = p.g[1] / p.B;
@@ -854,6 +854,21 @@ __global__ void aux_loss_bwd(lgx_aux_loss_args p) {
     p.dp[(int64_t)i * p.L + j] = k * (p.p[(int64_t)i * p.L + j] - p.a[(int64_t)i * p.L + j]);
   for (int j = 0; j < p.E; ++j)
     p.de[(int64_t)i * p.E + j] = ge * 2.f * (p.e[(int64_t)i * p.E + j] - p.t[(int64_t)i * p.E + j]);
+}
+
+__global__ void ppo_head_fwd(lgx_ppo_head_args p) { ppo_head_fwd_body(p); }
+__global__ void ppo_head_bwd(lgx_ppo_head_args p) { ppo_head_bwd_body(p); }
+__global__ void aux_loss_fwd(lgx_aux_loss_args p) { aux_loss_fwd_body(p); }
+__global__ void aux_loss_bwd(lgx_aux_loss_args p) { aux_loss_bwd_body(p); }
+// both heads in one launch: blockIdx.y = 0 the PPO head, 1 the ROA/estimator losses (each
+// y-slice is the single-head grid, with its own counter)
+__global__ void loss_heads_fwd(lgx_ppo_head_args h, lgx_aux_loss_args a) {
+  if (blockIdx.y == 0) ppo_head_fwd_body(h);
+  else aux_loss_fwd_body(a);
+}
+__global__ void loss_heads_bwd(lgx_ppo_head_args h, lgx_aux_loss_args a) {
+  if (blockIdx.y == 0) ppo_head_bwd_body(h);
+  else aux_loss_bwd_body(a);
 }
 
 // ---------------------------------------------------------------- PPO minibatch optimizer tail
@@ -1183,6 +1198,29 @@ int32_t lgx_aux_loss_backward(const lgx_aux_loss_args* a, void* stream) {
     return fail("lgx_aux_loss_backward: bad arguments");
   hipLaunchKernelGGL(lgxm::aux_loss_bwd, dim3((a->B + lgxm::HT - 1) / lgxm::HT), dim3(lgxm::HT), 0,
                      static_cast<hipStream_t>(stream), *a);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : fail(hipGetErrorString(e));
+}
+
+int32_t lgx_loss_heads_forward(const lgx_ppo_head_args* h, const lgx_aux_loss_args* a, void* stream) {
+  if (head_check(h)) return -1;
+  if (!h->out || !h->old_mu || !h->old_sigma) return fail("lgx_loss_heads_forward: null out/old_mu/old_sigma");
+  if (!a || a->B != h->B || a->L < 1 || a->E < 1 || !a->p || !a->a || !a->e || !a->t || !a->out || !a->ws ||
+      !a->counter)
+    return fail("lgx_loss_heads_forward: bad aux arguments");
+  hipLaunchKernelGGL(lgxm::loss_heads_fwd, dim3(lgxm::head_grid(h->B), 2), dim3(lgxm::HT), 0,
+                     static_cast<hipStream_t>(stream), *h, *a);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : fail(hipGetErrorString(e));
+}
+
+int32_t lgx_loss_heads_backward(const lgx_ppo_head_args* h, const lgx_aux_loss_args* a, void* stream) {
+  if (head_check(h)) return -1;
+  if (!h->g || !h->dmu || !h->dvalue || !h->dstd) return fail("lgx_loss_heads_backward: null g/dmu/dvalue/dstd");
+  if (!a || a->B != h->B || a->L < 1 || a->E < 1 || !a->p || !a->a || !a->e || !a->t || !a->g || !a->dp || !a->de)
+    return fail("lgx_loss_heads_backward: bad aux arguments");
+  hipLaunchKernelGGL(lgxm::loss_heads_bwd, dim3(lgxm::head_grid(h->B), 2), dim3(lgxm::HT), 0,
+                     static_cast<hipStream_t>(stream), *h, *a);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : fail(hipGetErrorString(e));
 }

@@ -383,15 +383,15 @@ class PPO:
                  self.estimator.group_item(obs_b)])
             mu_b, value_b = hip_mlp.forward_group([(ac.actor, (obs_b, priv_latent, scan_latent, est_b)),  # TRUE est (Q12)
                                                    (ac.critic, critic_b)])
-            surrogate_loss, value_loss, entropy_mean, _kl = hip_mlp.ppo_head(
-                mu_b, value_b, ac.std, actions_b, old_logp_b, adv_b, target_values_b, returns_b, old_mu_b, old_sigma_b,
-                self.clip_param, self.use_clipped_value_loss, kl_dst=g.segment("kl") if adaptive else None,
-                out=self._head_out)
             # sg(z_adapt): the adaptation encoder only trains in DAgger iterations, so over a
-            # PPO update its latents are fixed — computed once per update (_adapt_all)
+            # PPO update its latents are fixed — computed once per update (_adapt_all). Both
+            # loss heads (PPO terms; ROA regulariser + estimator loss) in one launch each way
             adapt_latent = self._adapt_all[idx]  # (shuffled order, like the rows)
-            regularization_loss, estimator_loss = hip_mlp.aux_losses(priv_latent, adapt_latent, pred, est_b,
-                                                                     out=self._aux_out)
+            (surrogate_loss, value_loss, entropy_mean, _kl, regularization_loss,
+             estimator_loss) = hip_mlp.loss_heads(
+                mu_b, value_b, ac.std, actions_b, old_logp_b, adv_b, target_values_b, returns_b, old_mu_b, old_sigma_b,
+                self.clip_param, self.use_clipped_value_loss, priv_latent, adapt_latent, pred, est_b,
+                kl_dst=g.segment("kl") if adaptive else None, out=self._head_out, out_aux=self._aux_out)
             # zero_grad of `optimizer` and `estimator_optimizer` (adaptation grads stay), then
             # both backwards (ppo.py:207, :262) as one pass seeded with the loss coefficients
             # (loss = surr + c_v vloss - c_e entropy + c_reg reg; the estimator loss on its own

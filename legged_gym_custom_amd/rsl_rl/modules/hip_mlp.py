@@ -27,7 +27,7 @@ EXPORTED = ["lgx_mlp_abi_version", "lgx_mlp_sizeof_gemm_args", "lgx_mlp_pick_spl
             "lgx_copy_batch", "lgx_act_head", "lgx_store_transition", "lgx_splitk_reduce_batch",
             "lgx_aux_loss_forward", "lgx_aux_loss_backward", "lgx_ppo_tail", "lgx_gemm_group",
             "lgx_mlp_pick_split_group", "lgx_gae", "lgx_normalize_advantages",
-            "lgx_gather_rows", "lgx_transpose_batch"]
+            "lgx_gather_rows", "lgx_transpose_batch", "lgx_loss_heads_forward", "lgx_loss_heads_backward"]
 TAIL_MAX_LOSSES = 8
 COPY_MAX = 16
 SPLITK_MAX = 24
@@ -142,6 +142,9 @@ def lib():
     L.lgx_act_head.restype = C.c_int32
     L.lgx_store_transition.argtypes = [vp, vp]
     L.lgx_store_transition.restype = C.c_int32
+    for fn in ("lgx_loss_heads_forward", "lgx_loss_heads_backward"):
+        getattr(L, fn).argtypes = [vp, vp, vp]
+        getattr(L, fn).restype = C.c_int32
     for fn in ("lgx_aux_loss_forward", "lgx_aux_loss_backward", "lgx_ppo_tail"):
         getattr(L, fn).argtypes = [vp, vp]
         getattr(L, fn).restype = C.c_int32
@@ -1033,6 +1036,76 @@ def aux_losses(priv_latent, adapt_latent, pred, true_est, out=None):
     to priv_latent and pred only (adapt_latent and true_est are constants). `out`: optional
     persistent [2] buffer for the two values."""
     return _AuxLossFn.apply(priv_latent, adapt_latent.detach(), pred, true_est.detach(), out)
+
+
+class _LossHeadsFn(torch.autograd.Function):
+    """_PPOHeadFn and _AuxLossFn as one autograd node: one launch each way
+    (lgx_loss_heads_forward / _backward), the same arguments and results."""
+
+    @staticmethod
+    def forward(ctx, mu, value, std, actions, old_logp, adv, target_values, returns, old_mu, old_sigma, p, a, e, t,
+                clip, clipped_value, kl_dst, out, out_aux):
+        B, A = mu.shape
+        dev = mu.device
+        ts = [_rowmajor(x.reshape(B, -1)) for x in (mu, value, actions, old_logp, adv, target_values, returns, old_mu,
+                                                     old_sigma)]
+        mu_, value_, actions_, old_logp_, adv_, tv_, ret_, old_mu_, old_sigma_ = ts
+        std_ = std.contiguous()
+        p_, a_, e_, t_ = (_rowmajor(x) for x in (p, a, e, t))
+        out = torch.empty(4, device=dev) if out is None else out
+        out_aux = torch.empty(2, device=dev) if out_aux is None else out_aux
+        ws = torch.empty(16 * ((B + 255) // 256), device=dev)
+        ws_aux = torch.empty(2 * ((B + 255) // 256), device=dev)
+        h = HeadArgs(mu=mu_.data_ptr(), value=value_.data_ptr(), std=std_.data_ptr(), actions=actions_.data_ptr(),
+                     old_logp=old_logp_.data_ptr(), adv=adv_.data_ptr(), target_values=tv_.data_ptr(),
+                     returns=ret_.data_ptr(), old_mu=old_mu_.data_ptr(), old_sigma=old_sigma_.data_ptr(), B=B, A=A,
+                     clip=float(clip), clipped_value=int(bool(clipped_value)), out=out.data_ptr(), ws=ws.data_ptr(),
+                     counter=_counter(dev).data_ptr(), kl_dst=None if kl_dst is None else kl_dst.data_ptr())
+        x = AuxArgs(p=p_.data_ptr(), a=a_.data_ptr(), L=p_.shape[1], e=e_.data_ptr(), t=t_.data_ptr(), E=e_.shape[1],
+                    B=B, out=out_aux.data_ptr(), ws=ws_aux.data_ptr(), counter=_counter(dev, "aux").data_ptr())
+        _check(lib().lgx_loss_heads_forward(C.byref(h), C.byref(x), _stream()), "lgx_loss_heads_forward")
+        ctx.save_for_backward(mu_, value_, std_, actions_, old_logp_, adv_, tv_, ret_, p_, a_, e_, t_)
+        ctx.std_param = std
+        ctx.set_materialize_grads(False)
+        ctx.clip, ctx.clipped = float(clip), int(bool(clipped_value))
+        ctx.value_shape = value.shape
+        ctx.mark_non_differentiable(out, out_aux)
+        return out[0], out[1], out[2], out[3], out_aux[0], out_aux[1]
+
+    @staticmethod
+    def backward(ctx, g_surr, g_value, g_ent, g_kl, g_reg, g_est):
+        mu, value, std, actions, old_logp, adv, tv, ret, p, a, e, t = ctx.saved_tensors
+        B, A = mu.shape
+        dev = mu.device
+        g = _seed_vector((g_surr, g_value, g_ent), dev)
+        g_aux = _seed_vector((g_reg, g_est), dev)
+        dmu = torch.empty_like(mu)
+        dvalue = torch.empty(B, device=dev)
+        sp = ctx.std_param
+        direct = sp.requires_grad and sp.is_leaf and sp.grad is not None and sp.grad.is_contiguous() and \
+            not sp._backward_hooks
+        dstd = sp.grad if direct else torch.empty_like(std)
+        dp, de = torch.empty_like(p), torch.empty_like(e)
+        ws = torch.empty(16 * ((B + 255) // 256), device=dev)
+        h = HeadArgs(mu=mu.data_ptr(), value=value.data_ptr(), std=std.data_ptr(), actions=actions.data_ptr(),
+                     old_logp=old_logp.data_ptr(), adv=adv.data_ptr(), target_values=tv.data_ptr(),
+                     returns=ret.data_ptr(), B=B, A=A, clip=ctx.clip, clipped_value=ctx.clipped, g=g.data_ptr(),
+                     dmu=dmu.data_ptr(), dvalue=dvalue.data_ptr(), dstd=dstd.data_ptr(), ws=ws.data_ptr(),
+                     counter=_counter(dev).data_ptr(), accumulate_dstd=int(direct))
+        x = AuxArgs(p=p.data_ptr(), a=a.data_ptr(), L=p.shape[1], e=e.data_ptr(), t=t.data_ptr(), E=e.shape[1], B=B,
+                    g=g_aux.data_ptr(), dp=dp.data_ptr(), de=de.data_ptr())
+        _check(lib().lgx_loss_heads_backward(C.byref(h), C.byref(x), _stream()), "lgx_loss_heads_backward")
+        return (dmu, dvalue.view(ctx.value_shape), None if direct else dstd) + (None,) * 7 + \
+            (dp, None, de, None) + (None,) * 5
+
+
+def loss_heads(mu, value, std, actions, old_logp, adv, target_values, returns, old_mu, old_sigma, clip, clipped_value,
+               priv_latent, adapt_latent, pred, true_est, kl_dst=None, out=None, out_aux=None):
+    """ppo_head(...) + aux_losses(...) in one launch each way: (surrogate_loss, value_loss,
+    entropy_mean, kl_mean, regularisation, estimator_loss)."""
+    return _LossHeadsFn.apply(mu, value, std, actions, old_logp, adv, target_values, returns, old_mu, old_sigma,
+                              priv_latent, adapt_latent.detach(), pred, true_est.detach(), clip, clipped_value, kl_dst,
+                              out, out_aux)
 
 
 def ppo_tail(grads, params, exp_avg, exp_avg_sq, main, est, adapt, kl_index, max_norm, betas_main, eps_main,

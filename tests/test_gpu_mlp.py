@@ -388,3 +388,33 @@ def test_transpose_batch_matches_torch():
     mats = [W, W[:, 572:624], torch.randn(1, 128, device=dev, generator=g), torch.randn(33, 65, device=dev, generator=g)]
     for a, m in zip(H.transpose_batch(mats), mats):
         assert torch.equal(a, m.t().contiguous())
+
+
+def test_fused_loss_heads_match_separate_heads_bitwise():
+    """hip_mlp.loss_heads (one launch each way) == ppo_head + aux_losses: the six losses and
+    the gradients of mu, value, std, the privileged latent and the estimator output."""
+    g = torch.Generator(device=dev).manual_seed(41)
+    B, A = 3000, 12
+    r = lambda *s: torch.randn(*s, device=dev, generator=g)  # noqa: E731
+    base = dict(actions=r(B, A), old_logp=r(B, 1), adv=r(B, 1), tv=r(B, 1), ret=r(B, 1), old_mu=r(B, A),
+                old_sigma=r(B, A).abs() + 0.5, a=r(B, 20), t=r(B, 3))
+    leaves = [r(B, A), r(B, 1), r(A).abs() + 0.5, r(B, 20), r(B, 3)]
+    seeds = torch.tensor([1.0, 1.3, -0.01, 0.05, 1.0], device=dev)
+
+    def run(fused):
+        mu, v, std, pl, pr = [x.clone().requires_grad_(True) for x in leaves]
+        b = base
+        if fused:
+            outs = H.loss_heads(mu, v, std, b["actions"], b["old_logp"], b["adv"], b["tv"], b["ret"], b["old_mu"],
+                                b["old_sigma"], 0.2, True, pl, b["a"], pr, b["t"])
+            losses = [outs[0], outs[1], outs[2], outs[4], outs[5]]
+        else:
+            s1, v1, e1, _k = H.ppo_head(mu, v, std, b["actions"], b["old_logp"], b["adv"], b["tv"], b["ret"],
+                                        b["old_mu"], b["old_sigma"], 0.2, True)
+            rg, es = H.aux_losses(pl, b["a"], pr, b["t"])
+            losses = [s1, v1, e1, rg, es]
+        torch.autograd.backward(losses, list(seeds.unbind()))
+        return [x.detach().clone() for x in losses] + [x.grad.clone() for x in (mu, v, std, pl, pr)]
+
+    for x, y in zip(run(True), run(False)):
+        assert torch.equal(x, y)
