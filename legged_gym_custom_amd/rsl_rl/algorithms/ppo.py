@@ -381,8 +381,11 @@ class PPO:
             priv_latent, scan_latent, pred = hip_mlp.forward_group(
                 [ac.privileged_encoder_.group_item(priv_b), ac.scan_encoder.group_item(scan_b),
                  self.estimator.group_item(obs_b)])
-            mu_b, value_b = hip_mlp.forward_group([(ac.actor, (obs_b, priv_latent, scan_latent, est_b)),  # TRUE est (Q12)
-                                                   (ac.critic, critic_b)])
+            ain = self._actor_in[idx]  # [obs | latents | est] rows: only the latents are copied in
+            nobs, nest = obs_b.shape[1], est_b.shape[1]
+            mu_b, value_b = hip_mlp.forward_group(
+                [(ac.actor, (ain[:, :nobs], priv_latent, scan_latent, ain[:, ain.shape[1] - nest:]), ain),  # TRUE est
+                 (ac.critic, critic_b)])
             # sg(z_adapt): the adaptation encoder only trains in DAgger iterations, so over a
             # PPO update its latents are fixed — computed once per update (_adapt_all). Both
             # loss heads (PPO terms; ROA regulariser + estimator loss) in one launch each way
@@ -508,6 +511,13 @@ class PPO:
         if self.on_gpu:
             with torch.no_grad():
                 self._shuf = hip_mlp.gather_rows(self.storage._flat(), self._perm)  # one launch
+                # the actor input [obs | priv latent | scan latent | est] per row: obs and est
+                # placed once per update, the latents per minibatch (no full concatenation)
+                obs, est = self._shuf[0], self._shuf[3]
+                self._actor_in = torch.empty(obs.shape[0], self.actor_critic.actor[0].in_features,
+                                             device=obs.device, dtype=obs.dtype)
+                self._actor_in[:, :obs.shape[1]].copy_(obs)
+                self._actor_in[:, self._actor_in.shape[1] - est.shape[1]:].copy_(est)
                 self._adapt_all = self.actor_critic.adaptation_encoder(self._shuf[0])
 
     def _update_body_eager(self):

@@ -675,25 +675,46 @@ def _group_forward(xs, chains):
     return outs
 
 
+def _concat(parts, buf=None):
+    """torch.cat(parts, -1); with `buf` (a [rows, sum of widths] buffer), only the parts not
+    already in place inside it are copied (the PPO update keeps the actor's obs and est
+    columns in one buffer, so only the two latents move)."""
+    if len(parts) == 1 and buf is None:
+        return parts[0]
+    if buf is None:
+        return torch.cat(parts, dim=-1)
+    off = 0
+    for t in parts:
+        w = t.shape[-1]
+        dst = buf[:, off:off + w]
+        if not (t.data_ptr() == dst.data_ptr() and t.stride() == dst.stride() and t.shape == dst.shape):
+            dst.copy_(t)
+        off += w
+    if off != buf.shape[-1]:
+        raise MlpLibError("concat buffer width does not match the parts")
+    return buf
+
+
 class _GroupFn(torch.autograd.Function):
-    """Several independent chains as one autograd node. meta: per chain (nparts, flags)."""
+    """Several independent chains as one autograd node. meta: per chain (nparts, flags,
+    concat buffer or None)."""
 
     @staticmethod
     def forward(ctx, meta, *flat):
         xs, chains, params, widths = [], [], [], []
         i = 0
-        for nparts, flags in meta:
+        for nparts, flags, buf in meta:
             parts = flat[i:i + nparts]
             i += nparts
             n = len(flags)
             wb = flat[i:i + 2 * n]
             i += 2 * n
-            xs.append(parts[0] if nparts == 1 else torch.cat(parts, dim=-1))
+            xs.append(_concat(parts, buf))
             chains.append((wb[0::2], wb[1::2], flags))
             params.append(wb)
             widths.append([t.shape[-1] for t in parts])
         outs = _group_forward(xs, chains)
-        ctx.meta, ctx.params, ctx.widths = meta, params, widths
+        ctx.meta, ctx.params, ctx.widths = tuple((m[0], m[1]) for m in meta), params, widths
         saved = []
         for x, wb, o in zip(xs, params, outs):
             saved += [x, *wb, *o]
@@ -776,24 +797,28 @@ class _GroupFn(torch.autograd.Function):
 
 
 def forward_group(items):
-    """Outputs of independent chains [(HipMLP, x or tuple of parts), ...], one launch per
-    depth on the HIP device (autograd-aware); elsewhere each module's own forward."""
-    resolved = []
-    for mod, x in items:
+    """Outputs of independent chains [(HipMLP, x or tuple of parts[, concat buffer]), ...],
+    one launch per depth on the HIP device (autograd-aware); elsewhere each module's own
+    forward."""
+    resolved, bufs = [], []
+    for item in items:
+        mod, x = item[0], item[1]
         parts = tuple(x) if isinstance(x, (tuple, list)) else (x,)
         chain = mod._chain() if isinstance(mod, HipMLP) and parts[0].device.type == "cuda" else None
         if chain is None:
-            return [m.forward_parts(tuple(v)) if isinstance(v, (tuple, list)) else m(v) for m, v in items]
+            return [it[0].forward_parts(tuple(it[1])) if isinstance(it[1], (tuple, list)) else it[0](it[1])
+                    for it in items]
         resolved.append((parts, chain))
+        bufs.append(item[2] if len(item) > 2 else None)
     wbs = [[t for pair in zip([m.weight for m in layers], [m.bias for m in layers]) for t in pair]
            for _p, (layers, _f) in resolved]
     needs_graph = torch.is_grad_enabled() and any(
         t.requires_grad for (parts, _c), wb in zip(resolved, wbs) for t in (*parts, *wb))
     if not needs_graph:
-        xs = [p[0] if len(p) == 1 else torch.cat(p, dim=-1) for p, _c in resolved]
+        xs = [_concat(p, b) for (p, _c), b in zip(resolved, bufs)]
         chains = [([m.weight for m in layers], [m.bias for m in layers], flags) for _p, (layers, flags) in resolved]
         return [o[-1] for o in _group_forward(xs, chains)]
-    meta = tuple((len(parts), tuple(flags)) for parts, (_l, flags) in resolved)
+    meta = tuple((len(parts), tuple(flags), b) for (parts, (_l, flags)), b in zip(resolved, bufs))
     flat = [t for (parts, _c), wb in zip(resolved, wbs) for t in (*parts, *wb)]
     return list(_GroupFn.apply(meta, *flat))
 
