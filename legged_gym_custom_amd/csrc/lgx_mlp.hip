@@ -895,23 +895,29 @@ __global__ __launch_bounds__(256) void tail_norms(lgx_ppo_tail_args p) {
   if (last_block(p.counter)) {
     float t[2];
     final_sum<2>(p.ws, 2, gridDim.x, t, red);
-    if (threadIdx.x == 0) {
+    // the scalar bookkeeping on separate threads (each one dependent memory round trip,
+    // not one thread's serial chain of loads behind possibly-aliasing stores)
+    const int tid = threadIdx.x;
+    if (tid == 0) {
       const float se = t[0], sm = t[1];
+      const double kl = p.kl_index >= 0 ? (double)p.grads[p.kl_index] : 0.0;
+      double lr = p.kl_index >= 0 ? *p.lr64 : 0.0;
       float* sc = p.ws + 2 * TAIL_BLOCKS;  // [coef_e, coef_m]
       sc[0] = fminf(p.max_norm / (sqrtf(se) + 1e-6f), 1.f);
       sc[1] = fminf(p.max_norm / (sqrtf(sm) + 1e-6f), 1.f);
       if (p.kl_index >= 0) {
-        const double kl = (double)p.grads[p.kl_index];
-        double lr = *p.lr64;
         if (kl > p.desired_kl * 2.0) lr = fmax(lr / 1.5, 1e-5);
         else if (kl < p.desired_kl / 2.0 && kl > 0.0) lr = fmin(lr * 1.5, 1e-2);
         *p.lr64 = lr;
         *p.lr32 = (float)lr;
       }
-      *p.step_main += 1.f;
-      *p.step_est += 1.f;
-      for (int k = 0; k < p.nloss; ++k) p.sums[k] += *p.loss_ptrs[k];
       *p.counter = 0u;
+    } else if (tid == 1) {
+      *p.step_main += 1.f;
+    } else if (tid == 2) {
+      *p.step_est += 1.f;
+    } else if (tid - 3 < p.nloss) {
+      p.sums[tid - 3] += *p.loss_ptrs[tid - 3];
     }
   }
 }
