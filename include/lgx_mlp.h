@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define LGX_MLP_ABI_VERSION 3
+#define LGX_MLP_ABI_VERSION 4
 
 enum {
   LGX_EPI_BIAS = 1,  /* + bias[n] */
@@ -156,6 +156,7 @@ typedef struct lgx_aux_loss_args {
   int32_t B;
   float* out; const float* g; float* dp; float* de;
   float* ws; uint32_t* counter;
+  int64_t ld_p;              /* row stride of p (0: L); p may be a column span of a wider buffer */
 } lgx_aux_loss_args;
 int32_t lgx_aux_loss_forward(const lgx_aux_loss_args* args, void* stream);
 int32_t lgx_aux_loss_backward(const lgx_aux_loss_args* args, void* stream);

@@ -808,15 +808,45 @@ __device__ __forceinline__ void ppo_head_bwd_body(const lgx_ppo_head_args& p) {
 }
 
 // ---------------------------------------------------------------- ROA + estimator losses
+// p rows i0 .. i0 + HT - 1, columns [j0, j0 + w) (w <= AUX_CW) staged into st[row][AUX_CW + 1]
+// with coalesced loads: p is usually a column span of the actor-input buffer (row stride
+// ld_p), where one row per thread would touch a separate cache line per lane and load.
+constexpr int AUX_CW = 16;
+__device__ __forceinline__ void aux_stage_p(const lgx_aux_loss_args& p, int64_t ldp, int i0, int j0, int w,
+                                            float* st) {
+  __syncthreads();
+  for (int k = threadIdx.x; k < HT * w; k += HT) {
+    const int r = k / w, j = k % w;
+    if (i0 + r < p.B) st[r * (AUX_CW + 1) + j] = p.p[(int64_t)(i0 + r) * ldp + j0 + j];
+  }
+  __syncthreads();
+}
+
+// sum_j (p[i, j] - a[i, j])^2 in column order for row i = i0 + threadIdx.x (block-uniform call)
+__device__ __forceinline__ float aux_row_sq(const lgx_aux_loss_args& p, int64_t ldp, int i0, float* st) {
+  const int i = i0 + threadIdx.x;
+  float s = 0.f;
+  for (int j0 = 0; j0 < p.L; j0 += AUX_CW) {
+    const int w = min(AUX_CW, p.L - j0);
+    aux_stage_p(p, ldp, i0, j0, w, st);
+    if (i < p.B)
+      for (int j = 0; j < w; ++j) {
+        const float d = st[threadIdx.x * (AUX_CW + 1) + j] - p.a[(int64_t)i * p.L + j0 + j];
+        s += d * d;
+      }
+  }
+  return s;
+}
+
 __device__ __forceinline__ void aux_loss_fwd_body(const lgx_aux_loss_args& p) {
   __shared__ float red[4 * 2];
+  __shared__ float st[HT * (AUX_CW + 1)];
   float v[2] = {0.f, 0.f};
-  for (int i = blockIdx.x * HT + threadIdx.x; i < p.B; i += gridDim.x * HT) {
-    float s = 0.f;
-    for (int j = 0; j < p.L; ++j) {
-      const float d = p.p[(int64_t)i * p.L + j] - p.a[(int64_t)i * p.L + j];
-      s += d * d;
-    }
+  const int64_t ldp = p.ld_p > 0 ? p.ld_p : p.L;
+  for (int i0 = blockIdx.x * HT; i0 < p.B; i0 += gridDim.x * HT) {
+    const float s = aux_row_sq(p, ldp, i0, st);
+    const int i = i0 + threadIdx.x;
+    if (i >= p.B) continue;
     v[0] += sqrtf(s);
     float q = 0.f;
     for (int j = 0; j < p.E; ++j) {
@@ -840,18 +870,20 @@ __device__ __forceinline__ void aux_loss_fwd_body(const lgx_aux_loss_args& p) {
 }
 
 __device__ __forceinline__ void aux_loss_bwd_body(const lgx_aux_loss_args& p) {
-  const int i = blockIdx.x * HT + threadIdx.x;
-  if (i >= p.B) return;
+  __shared__ float st[HT * (AUX_CW + 1)];
+  const int i0 = blockIdx.x * HT, i = i0 + threadIdx.x;
   const float gr = p.g[0] / p.B, ge = p.g[1] / p.B;
-  float s = 0.f;
-  for (int j = 0; j < p.L; ++j) {
-    const float d = p.p[(int64_t)i * p.L + j] - p.a[(int64_t)i * p.L + j];
-    s += d * d;
-  }
-  const float n = sqrtf(s);
+  const int64_t ldp = p.ld_p > 0 ? p.ld_p : p.L;
+  const float n = sqrtf(aux_row_sq(p, ldp, i0, st));
   const float k = n > 0.f ? gr / n : 0.f;
-  for (int j = 0; j < p.L; ++j)
-    p.dp[(int64_t)i * p.L + j] = k * (p.p[(int64_t)i * p.L + j] - p.a[(int64_t)i * p.L + j]);
+  for (int j0 = 0; j0 < p.L; j0 += AUX_CW) {
+    const int w = min(AUX_CW, p.L - j0);
+    aux_stage_p(p, ldp, i0, j0, w, st);
+    if (i < p.B)
+      for (int j = 0; j < w; ++j)
+        p.dp[(int64_t)i * p.L + j0 + j] = k * (st[threadIdx.x * (AUX_CW + 1) + j] - p.a[(int64_t)i * p.L + j0 + j]);
+  }
+  if (i >= p.B) return;
   for (int j = 0; j < p.E; ++j)
     p.de[(int64_t)i * p.E + j] = ge * 2.f * (p.e[(int64_t)i * p.E + j] - p.t[(int64_t)i * p.E + j]);
 }

@@ -378,11 +378,15 @@ class PPO:
             # the privileged/scan encoders and the estimator read only the minibatch, then the
             # actor (on their latents) and the critic: two autograd nodes, one grouped launch
             # per depth each way (hip_mlp.forward_group)
-            priv_latent, scan_latent, pred = hip_mlp.forward_group(
-                [ac.privileged_encoder_.group_item(priv_b), ac.scan_encoder.group_item(scan_b),
-                 self.estimator.group_item(obs_b)])
-            ain = self._actor_in[idx]  # [obs | latents | est] rows: only the latents are copied in
+            # the encoders' last layers write their latents straight into this minibatch's rows
+            # of the actor-input buffer [obs | priv latent | scan latent | est]
+            ain = self._actor_in[idx]
             nobs, nest = obs_b.shape[1], est_b.shape[1]
+            nlat = ain.shape[1] - nobs - nest - self._scan_latent_dim
+            priv_latent, scan_latent, pred = hip_mlp.forward_group(
+                [(*ac.privileged_encoder_.group_item(priv_b), None, ain[:, nobs:nobs + nlat]),
+                 (*ac.scan_encoder.group_item(scan_b), None, ain[:, nobs + nlat:ain.shape[1] - nest]),
+                 self.estimator.group_item(obs_b)])
             mu_b, value_b = hip_mlp.forward_group(
                 [(ac.actor, (ain[:, :nobs], priv_latent, scan_latent, ain[:, ain.shape[1] - nest:]), ain),  # TRUE est
                  (ac.critic, critic_b)])
@@ -518,6 +522,7 @@ class PPO:
                                              device=obs.device, dtype=obs.dtype)
                 self._actor_in[:, :obs.shape[1]].copy_(obs)
                 self._actor_in[:, self._actor_in.shape[1] - est.shape[1]:].copy_(est)
+                self._scan_latent_dim = self.actor_critic.scan_encoder.output_dim
                 self._adapt_all = self.actor_critic.adaptation_encoder(self._shuf[0])
 
     def _update_body_eager(self):

@@ -20,7 +20,7 @@ import torch.nn as nn
 _LIB_PATH = os.environ.get("LGX_MLP_LIB") or os.path.join(
     os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))), "lib", "liblgx_mlp.so")
 _lib = None
-ABI_VERSION = 3
+ABI_VERSION = 4
 EPI_BIAS, EPI_ELU, EPI_DELU, EPI_ACCUM = 1, 2, 4, 8
 EXPORTED = ["lgx_mlp_abi_version", "lgx_mlp_sizeof_gemm_args", "lgx_mlp_pick_split", "lgx_gemm",
             "lgx_mlp_last_error", "lgx_adam_step", "lgx_ppo_head_forward", "lgx_ppo_head_backward",
@@ -67,7 +67,7 @@ class AuxArgs(C.Structure):
     """Mirror of lgx_aux_loss_args."""
     _fields_ = [("p", C.c_void_p), ("a", C.c_void_p), ("L", C.c_int32), ("e", C.c_void_p), ("t", C.c_void_p),
                 ("E", C.c_int32), ("B", C.c_int32), ("out", C.c_void_p), ("g", C.c_void_p), ("dp", C.c_void_p),
-                ("de", C.c_void_p), ("ws", C.c_void_p), ("counter", C.c_void_p)]
+                ("de", C.c_void_p), ("ws", C.c_void_p), ("counter", C.c_void_p), ("ld_p", C.c_int64)]
 
 
 class TailArgs(C.Structure):
@@ -659,15 +659,21 @@ def _dxt_args(g, Wt, y_prev, dx):
                     act=_ptr(y_prev), ld_act=0 if y_prev is None else y_prev.stride(0), split_k=1)
 
 
-def _group_forward(xs, chains):
-    """Layer d of every chain in one launch; returns each chain's list of layer outputs."""
+def _group_forward(xs, chains, finals=None):
+    """Layer d of every chain in one launch; returns each chain's list of layer outputs.
+    finals[c] (optional): where chain c's last layer writes (a [rows, out] span with unit
+    column stride, e.g. the latent columns of the actor-input buffer)."""
     outs = [[] for _ in chains]
     hs = [_rowmajor(x) for x in xs]
     for d in range(max(len(c[2]) for c in chains)):
         args = []
         for c, (Ws, bs, flags) in enumerate(chains):
             if d < len(flags):
-                y = torch.empty(hs[c].shape[0], Ws[d].shape[0], device=hs[c].device, dtype=torch.float32)
+                y = finals[c] if finals is not None and finals[c] is not None and d == len(flags) - 1 else None
+                if y is not None and (y.shape != (hs[c].shape[0], Ws[d].shape[0]) or y.stride(1) != 1):
+                    raise MlpLibError("forward_group: output span shape does not match the chain")
+                if y is None:
+                    y = torch.empty(hs[c].shape[0], Ws[d].shape[0], device=hs[c].device, dtype=torch.float32)
                 args.append(_fwd_args(hs[c], Ws[d], bs[d], flags[d], y))
                 outs[c].append(y)
                 hs[c] = y
@@ -697,13 +703,13 @@ def _concat(parts, buf=None):
 
 class _GroupFn(torch.autograd.Function):
     """Several independent chains as one autograd node. meta: per chain (nparts, flags,
-    concat buffer or None)."""
+    concat buffer or None, output span or None)."""
 
     @staticmethod
     def forward(ctx, meta, *flat):
         xs, chains, params, widths = [], [], [], []
         i = 0
-        for nparts, flags, buf in meta:
+        for nparts, flags, buf, _out in meta:
             parts = flat[i:i + nparts]
             i += nparts
             n = len(flags)
@@ -713,7 +719,7 @@ class _GroupFn(torch.autograd.Function):
             chains.append((wb[0::2], wb[1::2], flags))
             params.append(wb)
             widths.append([t.shape[-1] for t in parts])
-        outs = _group_forward(xs, chains)
+        outs = _group_forward(xs, chains, [m[3] for m in meta])
         ctx.meta, ctx.params, ctx.widths = tuple((m[0], m[1]) for m in meta), params, widths
         saved = []
         for x, wb, o in zip(xs, params, outs):
@@ -797,10 +803,11 @@ class _GroupFn(torch.autograd.Function):
 
 
 def forward_group(items):
-    """Outputs of independent chains [(HipMLP, x or tuple of parts[, concat buffer]), ...],
-    one launch per depth on the HIP device (autograd-aware); elsewhere each module's own
-    forward."""
-    resolved, bufs = [], []
+    """Outputs of independent chains [(HipMLP, x or tuple of parts[, concat buffer[, output
+    span]]), ...], one launch per depth on the HIP device (autograd-aware); elsewhere each
+    module's own forward. An output span receives the chain's last layer in place (the update
+    writes the encoders' latents straight into the actor-input buffer)."""
+    resolved, bufs, finals = [], [], []
     for item in items:
         mod, x = item[0], item[1]
         parts = tuple(x) if isinstance(x, (tuple, list)) else (x,)
@@ -810,6 +817,7 @@ def forward_group(items):
                     for it in items]
         resolved.append((parts, chain))
         bufs.append(item[2] if len(item) > 2 else None)
+        finals.append(item[3] if len(item) > 3 else None)
     wbs = [[t for pair in zip([m.weight for m in layers], [m.bias for m in layers]) for t in pair]
            for _p, (layers, _f) in resolved]
     needs_graph = torch.is_grad_enabled() and any(
@@ -817,8 +825,8 @@ def forward_group(items):
     if not needs_graph:
         xs = [_concat(p, b) for (p, _c), b in zip(resolved, bufs)]
         chains = [([m.weight for m in layers], [m.bias for m in layers], flags) for _p, (layers, flags) in resolved]
-        return [o[-1] for o in _group_forward(xs, chains)]
-    meta = tuple((len(parts), tuple(flags), b) for (parts, (_l, flags)), b in zip(resolved, bufs))
+        return [o[-1] for o in _group_forward(xs, chains, finals)]
+    meta = tuple((len(parts), tuple(flags), b, f) for (parts, (_l, flags)), b, f in zip(resolved, bufs, finals))
     flat = [t for (parts, _c), wb in zip(resolved, wbs) for t in (*parts, *wb)]
     return list(_GroupFn.apply(meta, *flat))
 
@@ -1076,7 +1084,8 @@ class _LossHeadsFn(torch.autograd.Function):
                                                      old_sigma)]
         mu_, value_, actions_, old_logp_, adv_, tv_, ret_, old_mu_, old_sigma_ = ts
         std_ = std.contiguous()
-        p_, a_, e_, t_ = (_rowmajor(x) for x in (p, a, e, t))
+        p_ = _rowmajor(p)  # row stride passed (ld_p): p may be a column span of the actor-input buffer
+        a_, e_, t_ = (x.contiguous() for x in (a, e, t))
         out = torch.empty(4, device=dev) if out is None else out
         out_aux = torch.empty(2, device=dev) if out_aux is None else out_aux
         ws = torch.empty(16 * ((B + 255) // 256), device=dev)
@@ -1087,7 +1096,8 @@ class _LossHeadsFn(torch.autograd.Function):
                      clip=float(clip), clipped_value=int(bool(clipped_value)), out=out.data_ptr(), ws=ws.data_ptr(),
                      counter=_counter(dev).data_ptr(), kl_dst=None if kl_dst is None else kl_dst.data_ptr())
         x = AuxArgs(p=p_.data_ptr(), a=a_.data_ptr(), L=p_.shape[1], e=e_.data_ptr(), t=t_.data_ptr(), E=e_.shape[1],
-                    B=B, out=out_aux.data_ptr(), ws=ws_aux.data_ptr(), counter=_counter(dev, "aux").data_ptr())
+                    B=B, out=out_aux.data_ptr(), ws=ws_aux.data_ptr(), counter=_counter(dev, "aux").data_ptr(),
+                    ld_p=p_.stride(0))
         _check(lib().lgx_loss_heads_forward(C.byref(h), C.byref(x), _stream()), "lgx_loss_heads_forward")
         ctx.save_for_backward(mu_, value_, std_, actions_, old_logp_, adv_, tv_, ret_, p_, a_, e_, t_)
         ctx.std_param = std
@@ -1110,7 +1120,8 @@ class _LossHeadsFn(torch.autograd.Function):
         direct = sp.requires_grad and sp.is_leaf and sp.grad is not None and sp.grad.is_contiguous() and \
             not sp._backward_hooks
         dstd = sp.grad if direct else torch.empty_like(std)
-        dp, de = torch.empty_like(p), torch.empty_like(e)
+        dp = torch.empty(p.shape, device=dev, dtype=torch.float32)  # contiguous even when p is a span
+        de = torch.empty_like(e)
         ws = torch.empty(16 * ((B + 255) // 256), device=dev)
         h = HeadArgs(mu=mu.data_ptr(), value=value.data_ptr(), std=std.data_ptr(), actions=actions.data_ptr(),
                      old_logp=old_logp.data_ptr(), adv=adv.data_ptr(), target_values=tv.data_ptr(),
@@ -1118,7 +1129,7 @@ class _LossHeadsFn(torch.autograd.Function):
                      dmu=dmu.data_ptr(), dvalue=dvalue.data_ptr(), dstd=dstd.data_ptr(), ws=ws.data_ptr(),
                      counter=_counter(dev).data_ptr(), accumulate_dstd=int(direct))
         x = AuxArgs(p=p.data_ptr(), a=a.data_ptr(), L=p.shape[1], e=e.data_ptr(), t=t.data_ptr(), E=e.shape[1], B=B,
-                    g=g_aux.data_ptr(), dp=dp.data_ptr(), de=de.data_ptr())
+                    g=g_aux.data_ptr(), dp=dp.data_ptr(), de=de.data_ptr(), ld_p=p.stride(0))
         _check(lib().lgx_loss_heads_backward(C.byref(h), C.byref(x), _stream()), "lgx_loss_heads_backward")
         return (dmu, dvalue.view(ctx.value_shape), None if direct else dstd) + (None,) * 7 + \
             (dp, None, de, None) + (None,) * 5

@@ -371,6 +371,45 @@ def test_forward_group_matches_separate_chains_bitwise():
     assert all(torch.equal(a, b) for a, b in zip(o1, o3))
 
 
+def test_forward_group_output_spans_bitwise():
+    """Chains whose last layer writes into column spans of a shared buffer (the update's
+    latents inside the actor input) == the same chains writing their own outputs: outputs,
+    the actor's output and every gradient, bitwise; the spans hold the latents."""
+    from legged_gym_custom_amd.rsl_rl.modules.support_networks import _mlp
+    torch.manual_seed(5)
+    act = torch.nn.ELU()
+    enc = [_mlp(29, [64, 20], 20, act).to(dev), _mlp(132, [128, 64], 32, act).to(dev)]
+    actor = _mlp(90, [256, 128], 12, act).to(dev)
+    B = 2500
+    g = torch.Generator(device=dev).manual_seed(6)
+    xs = [torch.randn(B, 29, device=dev, generator=g), torch.randn(B, 132, device=dev, generator=g)]
+    obs, est = torch.randn(B, 35, device=dev, generator=g), torch.randn(B, 3, device=dev, generator=g)
+    seed, seed_l = torch.randn(B, 12, device=dev, generator=g), torch.randn(B, 20, device=dev, generator=g)
+
+    def run(spans):
+        for n in (*enc, actor):
+            n.zero_grad(set_to_none=True)
+        buf = torch.full((B, 90), float("nan"), device=dev)
+        buf[:, :35].copy_(obs)
+        buf[:, 87:].copy_(est)
+        with H.deferred_weight_grads():
+            if spans:
+                lat = H.forward_group([(enc[0], xs[0], None, buf[:, 35:55]), (enc[1], xs[1], None, buf[:, 55:87])])
+            else:
+                lat = H.forward_group([(enc[0], xs[0]), (enc[1], xs[1])])
+            (mu,) = H.forward_group([(actor, (buf[:, :35], lat[0], lat[1], buf[:, 87:]), buf)])
+            torch.autograd.backward([mu, lat[0]], [seed, seed_l])
+        if spans:
+            assert lat[0].data_ptr() == buf[:, 35:55].data_ptr()
+        return [mu.detach().clone(), lat[0].detach().clone(), buf.clone()], \
+            [p.grad.clone() for n in (*enc, actor) for p in n.parameters()]
+
+    o1, g1 = run(False)
+    o2, g2 = run(True)
+    assert all(torch.equal(a, b) for a, b in zip(o1, o2))
+    assert all(torch.equal(a, b) for a, b in zip(g1, g2))
+
+
 def test_gather_rows_matches_index_select():
     """lgx_gather_rows (one launch over the storage's buffers) == index_select, bitwise, for
     16-B (vector) and 4-B row widths."""
@@ -401,8 +440,13 @@ def test_fused_loss_heads_match_separate_heads_bitwise():
     leaves = [r(B, A), r(B, 1), r(A).abs() + 0.5, r(B, 20), r(B, 3)]
     seeds = torch.tensor([1.0, 1.3, -0.01, 0.05, 1.0], device=dev)
 
-    def run(fused):
+    def run(fused, span=False):
         mu, v, std, pl, pr = [x.clone().requires_grad_(True) for x in leaves]
+        if span:  # the privileged latent as a column span of a wider buffer (ld_p)
+            wide = torch.zeros(B, 50, device=dev)
+            wide[:, 10:30] = leaves[3]
+            wide.requires_grad_(True)
+            pl = wide[:, 10:30]
         b = base
         if fused:
             outs = H.loss_heads(mu, v, std, b["actions"], b["old_logp"], b["adv"], b["tv"], b["ret"], b["old_mu"],
@@ -414,7 +458,12 @@ def test_fused_loss_heads_match_separate_heads_bitwise():
             rg, es = H.aux_losses(pl, b["a"], pr, b["t"])
             losses = [s1, v1, e1, rg, es]
         torch.autograd.backward(losses, list(seeds.unbind()))
-        return [x.detach().clone() for x in losses] + [x.grad.clone() for x in (mu, v, std, pl, pr)]
+        dpl = wide.grad[:, 10:30] if span else pl.grad
+        return [x.detach().clone() for x in losses] + [x.grad.clone() for x in (mu, v, std)] + \
+            [dpl.clone(), pr.grad.clone()]
 
-    for x, y in zip(run(True), run(False)):
+    ref = run(False)
+    for x, y in zip(run(True), ref):
+        assert torch.equal(x, y)
+    for x, y in zip(run(True, span=True), ref):
         assert torch.equal(x, y)
