@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define LGX_ABI_VERSION 3
+#define LGX_ABI_VERSION 4
 
 #define LGX_MAX_DOF 12
 #define LGX_MAX_LINKS 16          /* dynamic links: base + 12 leg links (+spare) */
@@ -303,8 +303,12 @@ int lgx_reset_envs(lgx_env* env, const uint8_t* env_mask, uint64_t seed, uint64_
  *   cnt = episode_stats[K]; if cnt > 0: means[k] = episode_stats[k] / cnt / max_episode_length_s
  *                                      *level_mean = mean(terrain_levels)   (level_mean != NULL)
  *   if time_outs != NULL and any(reset): time_outs[i] = time_out[i]
- * Outputs keep their previous values otherwise (the reference's stale-when-no-reset values). */
-int lgx_episode_extras(lgx_env* env, float* means, float* level_mean, uint8_t* time_outs, void* hip_stream);
+ * Outputs keep their previous values otherwise (the reference's stale-when-no-reset values).
+ * The statistics are consumed: episode_stats is zeroed, so the next lgx_step / lgx_step_dev /
+ * lgx_reset_envs skips its clearing memset. step_dev (optional, device uint64): incremented
+ * after the step, so the rollout's device step counter needs no separate launch. */
+int lgx_episode_extras(lgx_env* env, float* means, float* level_mean, uint8_t* time_outs, uint64_t* step_dev,
+                       void* hip_stream);
 const char* lgx_last_error(const lgx_env* env);
 void lgx_destroy(lgx_env* env);
 

@@ -216,6 +216,7 @@ typedef struct lgx_act_head_args {
   const float* mean; const float* std; const float* eps;
   float* actions; float* mu; float* sigma; float* logp;
   int32_t B, A;
+  float* actions_copy;       /* optional second destination of the actions (the env's input buffer) */
 } lgx_act_head_args;
 int32_t lgx_act_head(const lgx_act_head_args* args, void* stream);
 

@@ -31,7 +31,7 @@ def lib():
     L.lgx_post_physics.argtypes = [vp, u64, u64, vp]
     L.lgx_physics.argtypes = [vp, vp]
     L.lgx_reset_envs.argtypes = [vp, vp, u64, u64, vp]
-    L.lgx_episode_extras.argtypes = [vp, vp, vp, vp, vp]
+    L.lgx_episode_extras.argtypes = [vp, vp, vp, vp, vp, vp]
     L.lgx_last_error.argtypes = [vp]
     L.lgx_last_error.restype = C.c_char_p
     L.lgx_destroy.argtypes = [vp]
@@ -97,10 +97,11 @@ class NativeEnv:
         self._check(self._L.lgx_reset_envs(self.handle, C.c_void_p(mask.data_ptr()), seed, call, C.c_void_p(stream)),
                     "lgx_reset_envs")
 
-    def episode_extras(self, means, level_mean, time_outs, stream):
-        """lgx_episode_extras into the given device tensors (level_mean / time_outs: None = skip)."""
+    def episode_extras(self, means, level_mean, time_outs, stream, step_dev=None):
+        """lgx_episode_extras into the given device tensors (level_mean / time_outs: None = skip);
+        consumes episode_stats and, with step_dev (a device int64 scalar), advances it by one."""
         p = lambda t: None if t is None else C.c_void_p(t.data_ptr())  # noqa: E731
-        self._check(self._L.lgx_episode_extras(self.handle, p(means), p(level_mean), p(time_outs),
+        self._check(self._L.lgx_episode_extras(self.handle, p(means), p(level_mean), p(time_outs), p(step_dev),
                                                C.c_void_p(stream)), "lgx_episode_extras")
 
     def __del__(self):

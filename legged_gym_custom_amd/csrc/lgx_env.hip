@@ -1581,6 +1581,7 @@ struct lgx_env {
   lgx_task_params* d_params = nullptr;
   int device = 0;
   bool bound = false;
+  bool stats_clean = false;  // episode_stats zeroed by lgx_episode_extras and not written since
   std::string err;
 };
 
@@ -1664,6 +1665,7 @@ int lgx_bind(lgx_env* env, const lgx_buffers* b) {
     return fail(env, "lgx_bind: terrain curriculum needs terrain_levels/terrain_types/terrain_origins");
   env->buffers = *b;
   env->bound = true;
+  env->stats_clean = false;
   return 0;
 }
 
@@ -1674,8 +1676,9 @@ static int launch_step(lgx_env* env, uint64_t seed, uint64_t step, const uint64_
   hipStream_t st = (hipStream_t)stream;
   const int N = env->params.num_envs;
   const int KS = env->params.num_reward_terms + (env->params.has_termination_reward ? 1 : 0);
-  if (env->buffers.episode_stats)
+  if (env->buffers.episode_stats && !env->stats_clean)
     HIP_OK(hipMemsetAsync(env->buffers.episode_stats, 0, sizeof(float) * (KS + 1), st));
+  env->stats_clean = false;
   // compiled variants: the plane/PD path (the benchmark) carries no terrain or LSTM code
   const bool terrain = env->params.mesh_type != LGX_MESH_PLANE, actnet = env->params.actuator_net != 0;
   auto kern = !physics ? lgx::env_step_kernel<false, false, false>
@@ -1711,8 +1714,9 @@ int lgx_reset_envs(lgx_env* env, const uint8_t* env_mask, uint64_t seed, uint64_
   if (!env_mask) return fail(env, "lgx_reset_envs: env_mask is NULL");
   hipStream_t st = (hipStream_t)hip_stream;
   const int KS = env->params.num_reward_terms + (env->params.has_termination_reward ? 1 : 0);
-  if (env->buffers.episode_stats)
+  if (env->buffers.episode_stats && !env->stats_clean)
     HIP_OK(hipMemsetAsync(env->buffers.episode_stats, 0, sizeof(float) * (KS + 1), st));
+  env->stats_clean = false;
   hipLaunchKernelGGL(lgx::reset_kernel, dim3(env->params.num_envs), dim3(64), 0, st, env->d_params, env->buffers,
                      env_mask, seed, reset_call);
   HIP_OK(hipGetLastError());
@@ -1723,7 +1727,10 @@ namespace lgx {
 // extras['episode'] / extras['time_outs'] (go2.py:246-263, Appendix B Q5 stale values):
 // one block; thread k < K forms the episode mean of reward term k, the block reduces
 // any(reset) and the mean terrain level, then time_outs is refreshed when any env reset.
-__global__ __launch_bounds__(1024) void extras_kernel(const float* __restrict__ stats, int K, float inv_T, int N,
+// The statistics are consumed (zeroed for the next step, which then needs no memset) and
+// the device step counter, if given, advances for the next lgx_step_dev.
+__global__ __launch_bounds__(1024) void extras_kernel(float* __restrict__ stats, uint64_t* __restrict__ step_dev,
+                                                      int K, float inv_T, int N,
                                                       const uint8_t* __restrict__ reset,
                                                       const uint8_t* __restrict__ time_out,
                                                       const int64_t* __restrict__ levels, float* __restrict__ means,
@@ -1749,6 +1756,8 @@ __global__ __launch_bounds__(1024) void extras_kernel(const float* __restrict__ 
     if (lane == 0) lsum[wv] = ls;
   }
   __syncthreads();
+  if (tid <= K) stats[tid] = 0.f;  // every thread read cnt before the barrier
+  if (tid == 0 && step_dev) *step_dev += 1;
   if (levels && tid == 0 && cnt > 0.f) {
     double t = 0.0;
     for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += lsum[w];
@@ -1759,7 +1768,8 @@ __global__ __launch_bounds__(1024) void extras_kernel(const float* __restrict__ 
 }
 }  // namespace lgx
 
-int lgx_episode_extras(lgx_env* env, float* means, float* level_mean, uint8_t* time_outs, void* hip_stream) {
+int lgx_episode_extras(lgx_env* env, float* means, float* level_mean, uint8_t* time_outs, uint64_t* step_dev,
+                       void* hip_stream) {
   if (!env) return -2;
   if (!env->bound) return fail(env, "lgx_episode_extras before lgx_bind");
   const lgx_buffers& b = env->buffers;
@@ -1767,13 +1777,14 @@ int lgx_episode_extras(lgx_env* env, float* means, float* level_mean, uint8_t* t
   if (level_mean && !b.terrain_levels) return fail(env, "lgx_episode_extras: level_mean needs terrain_levels");
   if (time_outs && (!b.reset || !b.time_out)) return fail(env, "lgx_episode_extras: time_outs needs reset/time_out");
   const int KS = env->params.num_reward_terms + (env->params.has_termination_reward ? 1 : 0);
-  if (KS > 1024) return fail(env, "lgx_episode_extras: too many reward terms");
+  if (KS + 1 > 1024) return fail(env, "lgx_episode_extras: too many reward terms");
   hipStream_t st = (hipStream_t)hip_stream;
   // torch divides a tensor by a Python scalar as a multiply by the fp32 reciprocal
-  hipLaunchKernelGGL(lgx::extras_kernel, dim3(1), dim3(1024), 0, st, b.episode_stats, KS,
+  hipLaunchKernelGGL(lgx::extras_kernel, dim3(1), dim3(1024), 0, st, b.episode_stats, step_dev, KS,
                      1.0f / env->params.max_episode_length_s, env->params.num_envs, time_outs ? b.reset : nullptr,
                      b.time_out, level_mean ? b.terrain_levels : nullptr, means, level_mean, time_outs);
   HIP_OK(hipGetLastError());
+  env->stats_clean = true;
   return 0;
 }
 

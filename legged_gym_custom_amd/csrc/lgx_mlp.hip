@@ -1096,6 +1096,7 @@ __global__ __launch_bounds__(256) void act_head_kernel(lgx_act_head_args p) {
     const float d = a - m;
     lp += -(d * d) / (2.0f * (sd * sd)) - logf(sd) - c;
     p.actions[k] = a;
+    if (p.actions_copy) p.actions_copy[k] = a;
     p.mu[k] = m;
     p.sigma[k] = sd;
   }

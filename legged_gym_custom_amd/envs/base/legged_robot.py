@@ -50,13 +50,14 @@ class LeggedRobot(BaseTask):
     # ------------------------------------------------------------------ step
     def step(self, actions):
         """legged_robot.py:67-100 as one kernel launch; returns the reference's 8-tuple."""
-        self.actions_in.copy_(actions, non_blocking=True)
-        # the counter the kernel reads lives on the device (lgx_step_dev), so a captured
-        # rollout replays with the right step numbers; the host mirror follows
+        if actions.data_ptr() != self.actions_in.data_ptr():  # the PPO act head may write it in place
+            self.actions_in.copy_(actions, non_blocking=True)
+        # the counter the kernel reads lives on the device (lgx_step_dev; it holds the NEXT
+        # step's number and lgx_episode_extras advances it), so a captured rollout replays with
+        # the right step numbers; the host mirror follows
         self._csc += 1
-        self._step_dev.add_(1)
         self._native.step_dev(self.seed, self._step_dev, torch.cuda.current_stream(self.device).cuda_stream)
-        self._update_extras()
+        self._update_extras(advance_step=True)
         return (self.obs_buf, self.privileged_obs_buf, self.critic_obs_buf, self.estimated_obs_buf, self.scan_obs_buf,
                 self.rew_buf, self.reset_buf, self.extras)
 
@@ -71,14 +72,15 @@ class LeggedRobot(BaseTask):
         self.reset_buf[env_ids] = True
         self._update_extras()
 
-    def _update_extras(self):
+    def _update_extras(self, advance_step=False):
         """extras['episode'] / ['time_outs'] with the reference's stale-when-no-reset
         semantics (go2.py:246-263, Appendix B Q5): one lgx_episode_extras launch (no host
         sync); _update_extras_torch states the same in torch ops (tests compare them)."""
         cur, to = self.cfg.terrain.curriculum, self.cfg.env.send_timeouts
         self._native.episode_extras(self._episode_means, self._terrain_level_mean if cur else None,
                                     self._extras_time_outs if to else None,
-                                    torch.cuda.current_stream(self.device).cuda_stream)
+                                    torch.cuda.current_stream(self.device).cuda_stream,
+                                    self._step_dev if advance_step else None)
         self._publish_extras()
 
     def _publish_extras(self):
@@ -110,7 +112,7 @@ class LeggedRobot(BaseTask):
     def common_step_counter(self, value):
         self._csc = int(value)
         if hasattr(self, "_step_dev"):
-            self._step_dev.fill_(self._csc)
+            self._step_dev.fill_(self._csc + 1)  # the number the next step reads
 
     def advance_step_counter(self, k):
         """Host mirror after a replayed capture that already advanced the device counter k times."""

@@ -165,6 +165,7 @@ class PPO:
             self.start_val, self.end_val, self.start_step, self.duration = 0.0, 0.1, 0, 1
         self.actor_critic = actor_critic.to(self.device)
         self.storage = None
+        self.act_dst = None  # optional [num_envs, A] device buffer the act head also writes (the env's input)
         self.estimator = estimator.to(self.device)
         ac = self.actor_critic
         self.on_gpu = str(device).startswith("cuda")
@@ -301,10 +302,12 @@ class PPO:
                 mean, t.values = hip_mlp.forward_group([(ac.actor, (obs, latent, scan_latent, estimated_obs)),
                                                         (ac.critic, critic_obs)])
                 eps = torch.randn_like(mean)
-                hip_mlp.act_head(mean, ac.std.detach(), eps, s.actions[k], s.mu[k], s.sigma[k], s.actions_log_prob[k])
+                dst = self.act_dst if self.act_dst is not None and self.act_dst.shape == mean.shape else None
+                hip_mlp.act_head(mean, ac.std.detach(), eps, s.actions[k], s.mu[k], s.sigma[k], s.actions_log_prob[k],
+                                 actions_copy=dst)
             t.actions, t.action_mean, t.action_sigma = s.actions[k], s.mu[k], s.sigma[k]
             t.actions_log_prob = s.actions_log_prob[k].view(-1)
-            return t.actions
+            return t.actions if dst is None else dst
         estimated_obs = self.estimator(obs)
         (t.observations, t.privileged_observations, t.critic_observations, t.true_estimated_observations,
          t.scan_observations) = self.storage.record_observations(obs, privileged_obs, critic_obs, true_estimated_obs,

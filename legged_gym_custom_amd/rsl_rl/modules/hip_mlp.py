@@ -90,7 +90,7 @@ class CopyDesc(C.Structure):
 class ActHeadArgs(C.Structure):
     """Mirror of lgx_act_head_args."""
     _fields_ = [(n, C.c_void_p) for n in ("mean", "std", "eps", "actions", "mu", "sigma", "logp")] + \
-               [("B", C.c_int32), ("A", C.c_int32)]
+               [("B", C.c_int32), ("A", C.c_int32), ("actions_copy", C.c_void_p)]
 
 
 class TransitionArgs(C.Structure):
@@ -229,11 +229,15 @@ def gather_rows(srcs, idx):
     return outs
 
 
-def act_head(mean, std, eps, actions, mu, sigma, logp):
-    """a = mean + std * eps and the Normal log-prob row sums, written into storage rows."""
+def act_head(mean, std, eps, actions, mu, sigma, logp, actions_copy=None):
+    """a = mean + std * eps and the Normal log-prob row sums, written into storage rows (and
+    the actions also into `actions_copy`, e.g. the env's input buffer, when given)."""
     B, A = mean.shape
+    if actions_copy is not None and (actions_copy.shape != mean.shape or not actions_copy.is_contiguous()):
+        raise MlpLibError("act_head: actions_copy must be a contiguous [B, A] buffer")
     args = ActHeadArgs(mean.data_ptr(), std.data_ptr(), eps.data_ptr(), actions.data_ptr(), mu.data_ptr(),
-                       sigma.data_ptr(), logp.data_ptr(), B, A)
+                       sigma.data_ptr(), logp.data_ptr(), B, A,
+                       None if actions_copy is None else actions_copy.data_ptr())
     _check(lib().lgx_act_head(C.byref(args), _stream()), "lgx_act_head")
 
 

@@ -89,6 +89,11 @@ class OnPolicyRunner:
                               total_obs_shape=[env.num_obs], privileged_obs_shape=[env.num_privileged_obs],
                               critic_obs_shape=[env.num_critic_obs], estimated_obs_shape=[env.num_estimated_obs],
                               scan_obs_shape=[env.num_scan_obs], action_shape=[env.num_actions])
+        # the act head writes the actions straight into the env's input buffer as well, so
+        # env.step has nothing to copy
+        dst = getattr(env, "actions_in", None)
+        if torch.is_tensor(dst) and dst.is_cuda and dst.device == torch.device(device) and dst.is_contiguous():
+            self.alg.act_dst = dst
         self.log_dir = log_dir if self.rank == 0 else None
         self.writer = None
         self.tot_timesteps = 0

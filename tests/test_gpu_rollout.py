@@ -58,7 +58,7 @@ def test_graph_rollout_equals_eager():
         for k in ("obs", "rew", "dones", "root", "ring"):
             torch.testing.assert_close(b[k], a[k], rtol=0, atol=0, msg=f"iteration {i} {k}")
         assert a["n"] == b["n"]
-    assert int(env_b._step_dev) == env_b.common_step_counter
+    assert int(env_b._step_dev) == env_b.common_step_counter + 1  # the next step's number
 
 
 def test_native_episode_extras_match_torch():
@@ -74,13 +74,23 @@ def test_native_episode_extras_match_torch():
     env.episode_length_buf[:] = torch.randint(0, int(env.max_episode_length), (env.num_envs,), device="cuda:0",
                                               generator=g)
     seen_reset = seen_to = 0
+    stream = torch.cuda.current_stream().cuda_stream
     for _ in range(40):
         prev = [t.clone() for t in (env._episode_means, env._terrain_level_mean, env._extras_time_outs)]
-        env.step(torch.randn(env.num_envs, env.num_actions, device="cuda:0", generator=g))
+        # env.step without its extras launch, so the statistics can be kept for the torch side
+        env.actions_in.copy_(torch.randn(env.num_envs, env.num_actions, device="cuda:0", generator=g))
+        env._csc += 1
+        env._native.step_dev(env.seed, env._step_dev, stream)
+        stats = env.episode_stats.clone()
+        step_no = int(env._step_dev)
+        env._update_extras(advance_step=True)
+        assert int(env._step_dev) == step_no + 1 and not env.episode_stats.any()  # consumed, advanced
         nat = [t.clone() for t in (env._episode_means, env._terrain_level_mean, env._extras_time_outs)]
         for t, p in zip((env._episode_means, env._terrain_level_mean, env._extras_time_outs), prev):
             t.copy_(p)
+        env.episode_stats.copy_(stats)
         env._update_extras_torch()
+        env.episode_stats.zero_()
         torch.testing.assert_close(nat[0], env._episode_means, rtol=2e-7, atol=0)
         torch.testing.assert_close(nat[1], env._terrain_level_mean, rtol=1e-6, atol=1e-6)
         assert torch.equal(nat[2], env._extras_time_outs)
