@@ -238,6 +238,13 @@ class LeggedRobot(BaseTask):
         self.command_ranges = class_to_dict(self.cfg.commands.ranges)
         if self.cfg.terrain.mesh_type not in ("heightfield", "trimesh"):
             self.cfg.terrain.curriculum = False
+        if getattr(self.cfg.commands, "curriculum", False):
+            # go2.py:80-107,222: the command ranges grow from the mean tracking reward of the
+            # envs resetting at every max_episode_length-th step, and that very step's resamples
+            # already use the new range — a grid-wide reduction inside the fused step. Off in
+            # every shipped config; refused rather than silently ignored.
+            raise NotImplementedError("commands.curriculum=True (go2.py:80-107) is not supported by the fused "
+                                      "env step; set cfg.commands.curriculum = False")
         self.max_episode_length_s = self.cfg.env.episode_length_s
         self.max_episode_length = np.ceil(self.max_episode_length_s / self.dt)
         self.cfg.domain_rand.push_interval = np.ceil(self.cfg.domain_rand.push_interval_s / self.dt)

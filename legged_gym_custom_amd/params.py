@@ -41,6 +41,18 @@ def reward_terms(cfg, dt):
     return names, ids, vals, term
 
 
+def go2_proprio_layout(num_dof=12):
+    """The Go2 current-observation vector (go2.py:506-515) as ordered (field, width) slots:
+    the order the env kernel writes (lgx_env.hip compute_observations) and the deploy
+    observation builder fills (deploy/base/deploy_base.py). Phase = sin/cos of the FR, FL,
+    BL, BR gait phases (go2.py:497-504)."""
+    return (("ang_vel", 3), ("roll_pitch", 2), ("command", 3), ("dof_pos", num_dof), ("dof_vel", num_dof),
+            ("actions", num_dof), ("phase", 8))
+
+
+GO2_PHASE_LEGS = ("fr", "fl", "bl", "br")
+
+
 def noise_vector(cfg, go2):
     p = cfg.env.num_proprio
     v = np.zeros(p, dtype=np.float32)

@@ -280,7 +280,13 @@ class PPO:
     def act(self, obs, privileged_obs, critic_obs, true_estimated_obs, scan_obs, adaptation_mode=False):
         """ppo.py:129-153: the rollout actor sees the ESTIMATOR's output (Q12). The
         observations are stored at act time (RolloutStorage.record_observations): the env
-        overwrites its buffers in place during the step that follows."""
+        overwrites its buffers in place during the step that follows.
+
+        Aliasing (GPU rollout with `act_dst` set by the runner): the returned tensor IS the
+        env's action input buffer (`env.actions_in`), which the act head writes together with
+        this step's storage row, bit-identical to it (tests/test_gpu_rollout.py). It is
+        overwritten by the next act(); a caller that keeps actions across steps must clone()
+        them. Without `act_dst` (or on the CPU) the storage row / transition tensor is returned."""
         t = self.transition
         ac = self.actor_critic
         if self._gpu_rollout():

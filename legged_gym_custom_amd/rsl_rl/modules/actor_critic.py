@@ -43,7 +43,9 @@ class ActorCritic(nn.Module):
                                         hidden_dims=scan_encoder_hidden_dims, activation="elu")
         self.std = nn.Parameter(init_noise_std * torch.ones(num_actions))
         self.distribution = None
-        Normal.set_default_validate_args(False)
+        # the reference ASSIGNS False to Normal.set_default_validate_args (actor_critic.py:135),
+        # which leaves argument validation on; nothing to do here (the HIP paths never build a
+        # Normal: lgx_act_head / the fused loss heads)
 
     def reset(self, dones=None):
         pass

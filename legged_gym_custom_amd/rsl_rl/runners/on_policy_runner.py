@@ -40,6 +40,14 @@ class _CsvWriter:
         self._f.flush()
 
 
+def reseed_for_rank(seed, rank):
+    """torch CPU and device generators keyed by (seed, rank), after the weight broadcast."""
+    s = (int(seed) if int(seed) >= 0 else 0) * 1000003 + int(rank)
+    torch.manual_seed(s)
+    if torch.cuda.is_available():
+        torch.cuda.manual_seed_all(s)
+
+
 def _make_writer(log_dir):
     try:
         from torch.utils.tensorboard import SummaryWriter
@@ -75,6 +83,10 @@ class OnPolicyRunner:
             for p in list(actor_critic.parameters()) + list(estimator.parameters()):
                 p.data = p.data.to(device)
                 dist.broadcast(p.data, 0)
+            # ...but independent draws per rank from here on (policy noise, the episode-length
+            # randomisation, minibatch permutations): rank r's envs must not replay rank 0's
+            # exploration noise, so the shards behave like one GPU with world x num_envs envs
+            reseed_for_rank(int(train_cfg.get("seed", 1)), self.rank)
         a = self.alg_cfg
         self.alg = PPO(actor_critic=actor_critic, estimator=estimator, num_learning_epochs=a["num_learning_epochs"],
                        num_mini_batches=a["num_mini_batches"], clip_param=a["clip_param"], gamma=a["gamma"],

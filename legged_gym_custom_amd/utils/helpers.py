@@ -41,6 +41,8 @@ def update_class_from_dict(obj, d):
 
 
 def set_seed(seed):
+    """helpers.py:set_seed; returns the seed it resolved (-1 draws one), which make_env
+    stores in cfg.seed so the env's Philox streams follow it too."""
     if seed == -1:
         seed = np.random.randint(0, 10000)
     print("Setting seed: {}".format(seed))
@@ -51,6 +53,7 @@ def set_seed(seed):
     if torch.cuda.is_available():
         torch.cuda.manual_seed(seed)
         torch.cuda.manual_seed_all(seed)
+    return seed
 
 
 class SimParams:

@@ -37,7 +37,7 @@ class TaskRegistry:
         if env_cfg is None:
             env_cfg, _ = self.get_cfgs(name)
         env_cfg, _ = update_cfg_from_args(env_cfg, None, args)
-        set_seed(env_cfg.seed)
+        env_cfg.seed = set_seed(env_cfg.seed)  # -1 resolved here, so the env kernel's RNG follows it
         sim_params = parse_sim_params(args, {"sim": class_to_dict(env_cfg.sim)})
         env = task_class(cfg=env_cfg, sim_params=sim_params, physics_engine=args.physics_engine,
                          sim_device=args.sim_device, headless=args.headless)

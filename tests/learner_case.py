@@ -1,0 +1,124 @@
+"""Deterministic inputs of the learner fixtures (tests/golden/learner_<case>.npz).
+
+Shared by tools/gen_learner_golden.py, which runs the REFERENCE rsl_rl
+(/root/reference/rsl_rl: ActorCritic, MlpEstimator, PPO, RolloutStorage) on them, and by
+tests/test_learner_golden.py / test_gpu_learner_golden.py, which run this build's PPO
+on the same inputs. Everything is drawn from numpy PCG64 streams keyed by (case seed,
+purpose), so the inputs are identical on every machine and never have to be stored:
+the fixture holds only the reference's OUTPUTS.
+
+Sequence recorded (the runner's first two iterations, on_policy_runner.py:143-186):
+  rollout A  T steps of PPO.act(adaptation_mode=True) + process_env_step   (it 0, Q14)
+  returns A  PPO.compute_returns(last critic obs)
+  dagger     PPO.update_dagger()                                            (ppo.py:309-349)
+  rollout B  T steps of PPO.act(adaptation_mode=False) + process_env_step
+  returns B
+  update     total_updates := TOTAL_UPDATES (ROA coefficient 0.025), PPO.update()  (ppo.py:182-293)
+The Normal sample of act() is a + std * eps with eps injected (actor_critic.py:207), and
+the minibatch permutation of each update is injected (rollout_storage.py:142).
+"""
+import zlib
+
+import numpy as np
+
+N, T = 64, 24
+TOTAL_UPDATES = 10000.0  # ppo.py:218-220: stage 0.5 of 5000..15000 -> coefficient 0.025
+SAMPLE = 2048            # entries kept per large tensor (plus its fp64 sum / sum of squares)
+
+CASES = {
+    # go2 network shapes (go2_config.py:180-200; estimator defaults support_networks.py:45) with
+    # the base config's adaptive KL schedule (legged_robot_config.py:213) to cover it
+    "go2": dict(seed=11, P=52, H=10, priv=29, critic=736, est=3, scan=132, A=12,
+                actor=[512, 256, 128], critic_h=[512, 256, 128], priv_h=[64, 20], scan_h=[128, 64],
+                est_h=[128, 64], latent=20, scan_out=32, lr=2e-4, est_lr=1e-3, schedule="adaptive",
+                desired_kl=0.01, entropy=0.01, epochs=5, minibatches=4, gamma=0.99, lam=0.95, clip=0.2,
+                max_grad_norm=1.0),
+    # go2_parkour (go2_parkour_config.py:173-198)
+    "go2_parkour": dict(seed=12, P=52, H=10, priv=29, critic=736, est=3, scan=132, A=12,
+                        actor=[512, 256, 128], critic_h=[512, 256, 128], priv_h=[64, 20], scan_h=[128, 64],
+                        est_h=[256, 128], latent=20, scan_out=32, lr=2e-4, est_lr=1e-4, schedule="fixed",
+                        desired_kl=0.01, entropy=0.01, epochs=5, minibatches=4, gamma=0.99, lam=0.95, clip=0.2,
+                        max_grad_norm=1.0),
+}
+
+
+def _rng(case, *key):
+    return np.random.default_rng([CASES[case]["seed"], *key])
+
+
+def _key(name):
+    return zlib.crc32(name.encode())
+
+
+def weights(case, named_shapes):
+    """{name: fp32 array} for every parameter: U(+-1/sqrt(fan_in)) like torch's Linear/Conv
+    default bound, std U(0.7, 1.3) (so enforce_max_std clamps some entries)."""
+    fan = {}
+    for name, shape in named_shapes:
+        if len(shape) >= 2:
+            fan[name.rsplit(".", 1)[0]] = int(np.prod(shape[1:]))
+    out = {}
+    for name, shape in named_shapes:
+        g = _rng(case, 1, _key(name))
+        if name == "std":
+            out[name] = g.uniform(0.7, 1.3, size=shape).astype(np.float32)
+        else:
+            b = 1.0 / np.sqrt(fan[name.rsplit(".", 1)[0]])
+            out[name] = g.uniform(-b, b, size=shape).astype(np.float32)
+    return out
+
+
+def rollout_inputs(case, which, t):
+    """Step t of rollout `which` (0 = A, 1 = B): observations, eps, rewards, dones, time_outs."""
+    c = CASES[case]
+    g = _rng(case, 2, which, t)
+    nobs = c["P"] * (c["H"] + 1)
+    d = {
+        "obs": g.standard_normal((N, nobs), dtype=np.float32),
+        "priv": (0.5 * g.standard_normal((N, c["priv"]))).astype(np.float32),
+        "critic": g.standard_normal((N, c["critic"]), dtype=np.float32),
+        "est": (0.5 * g.standard_normal((N, c["est"]))).astype(np.float32),
+        "scan": g.uniform(-1.0, 1.0, size=(N, c["scan"])).astype(np.float32),
+        "eps": g.standard_normal((N, c["A"]), dtype=np.float32),
+        "rewards": (0.5 * g.standard_normal(N)).astype(np.float32),
+    }
+    dones = g.random(N) < 0.08
+    d["dones"] = dones
+    d["time_outs"] = dones & (g.random(N) < 0.5)
+    return d
+
+
+def last_critic(case, which):
+    c = CASES[case]
+    return _rng(case, 3, which).standard_normal((N, c["critic"]), dtype=np.float32)
+
+
+def permutation(case, which):
+    return _rng(case, 4, which).permutation(N * T).astype(np.int64)
+
+
+def sample_index(name, size):
+    """Fixed entry subset of a flattened tensor (all of it when small)."""
+    if size <= SAMPLE:
+        return np.arange(size, dtype=np.int64)
+    return np.sort(np.random.default_rng([7, _key(name)]).choice(size, SAMPLE, replace=False)).astype(np.int64)
+
+
+def record(out, prefix, name, arr):
+    """Store a tensor's sampled entries and its full fp64 sum / sum of squares."""
+    flat = np.asarray(arr, dtype=np.float32).reshape(-1)
+    idx = sample_index(name, flat.size)
+    out[f"{prefix}.{name}.v"] = flat[idx]
+    out[f"{prefix}.{name}.sum"] = np.float64(flat.astype(np.float64).sum())
+    out[f"{prefix}.{name}.sumsq"] = np.float64((flat.astype(np.float64) ** 2).sum())
+
+
+def compare(d, prefix, name, arr, rtol, atol, stat_rtol=None):
+    """assert a tensor matches what `record` stored (sampled entries; sum/sumsq loosely)."""
+    flat = np.asarray(arr, dtype=np.float32).reshape(-1)
+    idx = sample_index(name, flat.size)
+    np.testing.assert_allclose(flat[idx], d[f"{prefix}.{name}.v"], rtol=rtol, atol=atol, err_msg=f"{prefix}.{name}")
+    if stat_rtol is not None:
+        s2 = float((flat.astype(np.float64) ** 2).sum())
+        ref2 = float(d[f"{prefix}.{name}.sumsq"])
+        assert abs(s2 - ref2) <= stat_rtol * max(ref2, 1e-30) + 1e-12, (prefix, name, s2, ref2)

@@ -131,3 +131,39 @@ def test_sharded_update_equals_union_update(sharded, union):
     torch.testing.assert_close(sharded[0]["params"], union["params"], rtol=1e-4, atol=2e-6)
     assert sharded[0]["lr"] == pytest.approx(union["lr"], rel=1e-12)
     torch.testing.assert_close(sharded[0]["adapt_grads"], union["adapt_grads"], rtol=1e-3, atol=1e-7)
+
+
+def _runner_worker(rank, port, out):
+    """A runner per rank (oracle env, CPU): identical initial weights (broadcast), then
+    per-rank generators, so rank r's exploration noise is not rank 0's."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        import cpu_env
+        from legged_gym_custom_amd import model as mdl, params as prm
+        from legged_gym_custom_amd.envs import task_registry_configs
+        from legged_gym_custom_amd.rsl_rl.runners import OnPolicyRunner
+        from legged_gym_custom_amd.utils.helpers import class_to_dict
+        cfg, tcfg = task_registry_configs("go2")
+        cfg.env.num_envs = 8
+        m = mdl.load_model(cfg.asset.file, cfg.asset.foot_name)
+        P = prm.build_task_params(cfg, m, 8)
+        env = cpu_env.OracleVecEnv(cfg, m, P, mdl.to_struct(m))
+        tcfg.runner.num_steps_per_env = 2
+        torch.manual_seed(1)  # same seed on both ranks, as set_seed does
+        r = OnPolicyRunner(env, class_to_dict(tcfg), None, device="cpu")
+        o = r.env.get_observations()
+        with torch.no_grad():
+            a = r.alg.actor_critic.act(o, r.env.get_privileged_observations(), r.env.get_estimated_observations(),
+                                       r.env.get_scan_observations())
+        out[rank] = {"w": r.alg.actor_critic.actor[0].weight.detach().clone(), "noise": a - r.alg.actor_critic.action_mean}
+    finally:
+        dist.destroy_process_group()
+
+
+def test_ranks_share_weights_but_not_noise():
+    out = mp.Manager().dict()
+    mp.spawn(_runner_worker, args=(_port(), out), nprocs=WORLD, join=True)
+    assert torch.equal(out[0]["w"], out[1]["w"])
+    assert not torch.allclose(out[0]["noise"], out[1]["noise"])

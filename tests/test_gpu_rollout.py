@@ -97,3 +97,26 @@ def test_native_episode_extras_match_torch():
         seen_reset += int(env.reset_buf.any())
         seen_to += int(env._extras_time_outs.any())
     assert seen_reset > 0 and seen_to > 0
+
+
+def test_act_head_feeds_env_the_stored_actions():
+    """std > 0: the act head writes the sampled actions into the storage row AND the env's
+    input buffer (act_dst); they are bit-identical, and the env steps on clip(storage row)
+    (legged_robot.py:74-75), which is the action whose log-prob was stored."""
+    env, runner = _setup(False)
+    with torch.no_grad():
+        runner.alg.actor_critic.std.fill_(0.7)
+    alg = runner.alg
+    assert alg.act_dst is not None and alg.act_dst.data_ptr() == env.actions_in.data_ptr()
+    obs = [env.get_observations(), env.get_privileged_observations(), env.get_critic_observations(),
+           env.get_estimated_observations(), env.get_scan_observations()]
+    for k in range(3):
+        with torch.inference_mode():
+            a = alg.act(*obs)
+            stored = alg.storage.actions[k].clone()
+            assert torch.equal(env.actions_in, stored) and torch.equal(a, stored)
+            r = env.step(a)
+            clip = env.cfg.normalization.clip_actions
+            assert torch.equal(env.actions, torch.clamp(stored, -clip, clip))
+            alg.process_env_step(r[5], r[6], r[7])
+        assert stored.std() > 0.3  # really sampled

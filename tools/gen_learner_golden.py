@@ -1,0 +1,214 @@
+#!/usr/bin/env python3
+"""Learner golden-vector generator: runs the REFERENCE rsl_rl (read-only, imported from
+/root/reference/rsl_rl in this container) on the deterministic inputs of
+tests/learner_case.py and records its outputs as tests/golden/learner_<case>.npz.
+Test infrastructure only: the reference code never travels; only the .npz data does.
+
+Recorded per case (go2 and go2_parkour network shapes, N=64 envs, T=24 steps):
+  * state_dict key/shape list and the optimizers' param-group layout (meta JSON);
+  * rollout A (adaptation mode) and B: per step PPO.act outputs (actions, values,
+    log-probs, mean, sigma; ppo.py:129-153 / actor_critic.py:190-226) and the stored
+    rewards after the time-out bootstrap (ppo.py:156-171);
+  * compute_returns: returns and normalised advantages (rollout_storage.py:110-124);
+  * update_dagger: the adaptation encoder after it, its Adam moments, the mean loss;
+  * update: the pre-clip gradients of minibatch 0 (hooked at clip_grad_norm_), the
+    returned losses, the learning rate, every parameter after the update and the Adam
+    moments (sampled entries + fp64 sum/sum-of-squares per tensor; learner_case.record).
+Injected: the Normal sample (loc + scale * eps) and torch.randperm.
+
+Usage:  python tools/gen_learner_golden.py  [case ...]
+"""
+import json
+import os
+import sys
+import types
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+REF_RSL = "/root/reference/rsl_rl"
+sys.dont_write_bytecode = True
+sys.path.insert(0, REF_RSL)
+sys.path.append(os.path.join(REPO, "tests"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.nn as nn  # noqa: E402
+
+_tb = types.ModuleType("torch.utils.tensorboard")
+_tb.SummaryWriter = type("SummaryWriter", (), {"__init__": lambda self, *a, **k: None})
+sys.modules["torch.utils.tensorboard"] = _tb
+
+import rsl_rl  # noqa: E402
+from rsl_rl.algorithms import PPO  # noqa: E402
+from rsl_rl.modules import ActorCritic  # noqa: E402
+from rsl_rl.modules.support_networks import MlpEstimator  # noqa: E402
+
+import learner_case as LC  # noqa: E402
+
+assert os.path.realpath(rsl_rl.__file__).startswith(os.path.realpath(REF_RSL)), rsl_rl.__file__
+
+
+class _Inject:
+    """eps for Normal.sample and the permutation for torch.randperm."""
+    eps = None
+    perm = None
+
+
+_orig_randperm = torch.randperm
+
+
+def _sample(self, sample_shape=torch.Size()):
+    with torch.no_grad():
+        if _Inject.eps is None or tuple(self.loc.shape) != tuple(_Inject.eps.shape):
+            return torch.normal(self.loc.expand(self._extended_shape(sample_shape)),
+                                self.scale.expand(self._extended_shape(sample_shape)))
+        return self.loc + self.scale * _Inject.eps
+
+
+def _randperm(n, *a, **k):
+    if _Inject.perm is not None and n == _Inject.perm.numel():
+        return _Inject.perm.clone()
+    return _orig_randperm(n, *a, **k)
+
+
+torch.distributions.Normal.sample = _sample
+torch.randperm = _randperm
+
+
+def build(case):
+    c = LC.CASES[case]
+    torch.manual_seed(0)
+    ac = ActorCritic(num_proprio=c["P"], num_privileged_obs=c["priv"], num_critic_obs=c["critic"],
+                     num_estimated_obs=c["est"], num_scan_obs=c["scan"], num_actions=c["A"],
+                     history_buffer_length=c["H"], actor_hidden_dims=c["actor"], critic_hidden_dims=c["critic_h"],
+                     priv_encoder_hidden_dims=c["priv_h"], scan_encoder_hidden_dims=c["scan_h"],
+                     latent_encoder_output_dim=c["latent"], scan_encoder_output_dim=c["scan_out"], activation="elu",
+                     init_noise_std=1.0)
+    est = MlpEstimator(num_proprio=c["P"], history_buffer_length=c["H"], output_dim=c["est"],
+                       hidden_dims=c["est_h"], activation="elu", use_history=True)
+    w = LC.weights(case, [(k, tuple(v.shape)) for k, v in ac.state_dict().items()])
+    ac.load_state_dict({k: torch.from_numpy(v) for k, v in w.items()})
+    we = LC.weights(case, [("estimator." + k, tuple(v.shape)) for k, v in est.state_dict().items()])
+    est.load_state_dict({k[len("estimator."):]: torch.from_numpy(v) for k, v in we.items()})
+    alg = PPO(ac, est, num_learning_epochs=c["epochs"], num_mini_batches=c["minibatches"], clip_param=c["clip"],
+              gamma=c["gamma"], lam=c["lam"], value_loss_coef=1.0, entropy_coef=c["entropy"], learning_rate=c["lr"],
+              estimator_learning_rate=c["est_lr"], max_grad_norm=c["max_grad_norm"], use_clipped_value_loss=True,
+              schedule=c["schedule"], desired_kl=c["desired_kl"], device="cpu")
+    alg.init_storage(LC.N, LC.T, [c["P"] * (c["H"] + 1)], [c["priv"]], [c["critic"]], [c["est"]], [c["scan"]],
+                     [c["A"]])
+    return alg
+
+
+def rollout(alg, case, which, out, adaptation_mode):
+    pre = f"roll{which}"
+    for t in range(LC.T):
+        d = LC.rollout_inputs(case, which, t)
+        x = {k: torch.from_numpy(v) for k, v in d.items()}
+        _Inject.eps = x["eps"]
+        alg.act(x["obs"], x["priv"], x["critic"], x["est"], x["scan"], adaptation_mode=adaptation_mode)
+        tr = alg.transition
+        out[f"{pre}.{t}.actions"] = tr.actions.numpy().copy()
+        out[f"{pre}.{t}.values"] = tr.values.numpy().copy()
+        out[f"{pre}.{t}.logp"] = tr.actions_log_prob.numpy().copy()
+        out[f"{pre}.{t}.mu"] = tr.action_mean.numpy().copy()
+        out[f"{pre}.{t}.sigma"] = tr.action_sigma.numpy().copy()
+        alg.process_env_step(x["rewards"], x["dones"], {"time_outs": x["time_outs"]})
+        _Inject.eps = None
+    s = alg.storage
+    out[f"{pre}.rewards"] = s.rewards.numpy().copy()
+    alg.compute_returns(torch.from_numpy(LC.last_critic(case, which)))
+    out[f"{pre}.returns"] = s.returns.numpy().copy()
+    out[f"{pre}.advantages"] = s.advantages.numpy().copy()
+
+
+def named_params(alg):
+    ac, est = alg.actor_critic, alg.estimator
+    return [(k, p) for k, p in ac.named_parameters()] + [("estimator." + k, p) for k, p in est.named_parameters()]
+
+
+def adam_state(opt, names_of):
+    """{param name: (exp_avg, exp_avg_sq, step)} of an optimizer."""
+    res = {}
+    for grp in opt.param_groups:
+        for p in grp["params"]:
+            st = opt.state.get(p, {})
+            if "exp_avg" in st:
+                res[names_of[id(p)]] = (st["exp_avg"].numpy(), st["exp_avg_sq"].numpy(), float(st["step"]))
+    return res
+
+
+def main(cases):
+    for case in cases:
+        alg = build(case)
+        out = {"case": np.array(case), "torch_version": np.array(torch.__version__), "N": LC.N, "T": LC.T}
+        names_of = {id(p): n for n, p in named_params(alg)}
+        meta = {"state_dict": [[k, list(v.shape)] for k, v in alg.actor_critic.state_dict().items()],
+                "estimator_state_dict": [[k, list(v.shape)] for k, v in alg.estimator.state_dict().items()],
+                "optimizer_param_groups": [[names_of[id(p)] for p in g["params"]] for g in alg.optimizer.param_groups],
+                "adaptation_optimizer": [names_of[id(p)] for p in alg.adaptation_optimizer.param_groups[0]["params"]],
+                "estimator_optimizer": [names_of[id(p)] for p in alg.estimator_optimizer.param_groups[0]["params"]],
+                "optimizer_hyper": {k: v for k, v in alg.optimizer.param_groups[0].items()
+                                    if k != "params" and isinstance(v, (int, float, bool, tuple, type(None)))}}
+        out["meta_json"] = np.array(json.dumps(meta))
+
+        # ---- iteration 0: adaptation-mode rollout + DAgger (on_policy_runner.py:147, 182-183)
+        rollout(alg, case, 0, out, adaptation_mode=True)
+        _Inject.perm = torch.from_numpy(LC.permutation(case, 0))
+        out["dagger.loss"] = np.float64(alg.update_dagger())
+        _Inject.perm = None
+        for n, p in named_params(alg):
+            if n.startswith("adaptation_encoder_."):
+                out[f"dagger.param.{n}"] = p.detach().numpy().copy()
+                out[f"dagger.grad.{n}"] = p.grad.numpy().copy()  # stale: seen by the next PPO clip
+        for n, (m, v, step) in adam_state(alg.adaptation_optimizer, names_of).items():
+            out[f"dagger.exp_avg.{n}"] = m.copy()
+            out[f"dagger.exp_avg_sq.{n}"] = v.copy()
+            out["dagger.step"] = np.float64(step)
+
+        # ---- iteration 1: rollout + PPO/ROA update
+        rollout(alg, case, 1, out, adaptation_mode=False)
+        alg.total_updates = LC.TOTAL_UPDATES
+        grads0 = {}
+        orig_clip = nn.utils.clip_grad_norm_
+
+        def clip_hook(params, max_norm, *a, **k):
+            # minibatch 0 calls it for the estimator, then for actor_critic.parameters()
+            params = list(params)
+            key = "est" if all(names_of[id(p)].startswith("estimator.") for p in params) else "main"
+            first = key not in grads0
+            if first:
+                grads0[key] = {names_of[id(p)]: p.grad.detach().numpy().copy() for p in params
+                               if p.grad is not None}
+            total = orig_clip(params, max_norm, *a, **k)
+            if first:
+                grads0[key + "_norm"] = float(total)
+            return total
+
+        nn.utils.clip_grad_norm_ = clip_hook
+        _Inject.perm = torch.from_numpy(LC.permutation(case, 1))
+        mv, ms, mr, coef, me = alg.update()
+        _Inject.perm = None
+        nn.utils.clip_grad_norm_ = orig_clip
+        out["update.losses"] = np.array([mv, ms, mr, coef, me], dtype=np.float64)
+        out["update.learning_rate"] = np.float64(alg.learning_rate)
+        out["update.grad_norm0"] = np.array([grads0["est_norm"], grads0["main_norm"]], dtype=np.float64)
+        for key in ("est", "main"):
+            for n, g in grads0[key].items():
+                LC.record(out, "grad0", n, g)
+        for n, p in named_params(alg):
+            LC.record(out, "after", n, p.detach().numpy())
+        steps = {}
+        for oname in ("optimizer", "estimator_optimizer"):
+            for n, (m, v, step) in adam_state(getattr(alg, oname), names_of).items():
+                LC.record(out, "exp_avg", n, m)
+                LC.record(out, "exp_avg_sq", n, v)
+                steps[oname] = step
+        out["update.steps"] = np.array([steps["optimizer"], steps["estimator_optimizer"]], dtype=np.float64)
+        path = os.path.join(REPO, "tests", "golden", f"learner_{case}.npz")
+        np.savez_compressed(path, **out)
+        print(f"wrote {path}: losses {out['update.losses']}, lr {alg.learning_rate}, "
+              f"{os.path.getsize(path) / 1e6:.2f} MB")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:] or list(LC.CASES))
