@@ -23,6 +23,16 @@ LGX_DEV float row_sums_32(float x) {
   return a + b;
 }
 
+// Sum over lanes 0..15 (DPP row 0), returned to every lane. Lanes 0..15 must be active;
+// the other rows' values are ignored.
+LGX_DEV float row0_sum16(float x) {
+  x += dpp_shr_t<0x111>(x);
+  x += dpp_shr_t<0x112>(x);
+  x += dpp_shr_t<0x114>(x);
+  x += dpp_shr_t<0x118>(x);
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 15));
+}
+
 LGX_DEV int lane_id() { return __lane_id(); }
 
 // ---------------------------------------------------------------- Philox4x32-10

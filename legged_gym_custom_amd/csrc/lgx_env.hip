@@ -49,13 +49,15 @@ struct Scratch {  // per-env post-physics scalars (go2.py:357-367, 279-328)
 };
 
 // LDS arena time-shared by phase (dynamics temporaries -> constraint rows -> post-physics
-// staging): J [n][NU], M⁻¹Jᵀ [n][NU] and, for n <= AMAX rows, A = J M⁻¹ Jᵀ [n][n]
+// staging). Constraint rows are stored sparse: row r = [base part (6) | the 3 joints of
+// leg rleg[r]] (J9), with z_r = S⁻¹ (J_b − X_l J_l) and g_r = D_l⁻¹ J_l (ZG, see dynamics);
+// for n <= AMAX rows also A = J M⁻¹ Jᵀ [n][n].
 constexpr int ARENA = 2200;
 constexpr int AMAX = 32;
+constexpr int RW = 9;  // sparse row width
 static_assert(NSLOT + LGX_MAX_PROPRIO + MAXHIST + LGX_MAX_HEIGHT_POINTS <= ARENA,
               "post-physics staging must fit the arena");
-static_assert(2 * MAXR * NU <= ARENA, "arena must hold J and M^-1 J^T at MAXR rows");
-static_assert(2 * AMAX * NU + AMAX * AMAX <= ARENA, "arena must hold J, M^-1 J^T and A at AMAX rows");
+static_assert(2 * MAXR * RW + AMAX * AMAX <= ARENA, "arena must hold J9, ZG (MAXR rows) and A (AMAX rows)");
 
 struct Sh {
   // --- post-physics per-env scalars (written by lane 0, read by all lanes)
@@ -72,15 +74,19 @@ struct Sh {
   // --- kinematics per dynamic link
   float R[NL][9], P[NL][3], Ax[NL][3], W[NL][3], V[NL][3], Al[NL][3], Ao[NL][3], C[NL][3], I[NL][6], m[NL];
   // --- dynamics
-  float Bc[NJ][6], Dinv[4][6], X[NJ][6], L[21], hj[NJ], hb[6], us[NU], up[NU];
+  float Bc[NJ][6], Dinv[4][6], X[NJ][6], Sinv[6][6], us[NU], up[NU];
   // --- constraints (J, M⁻¹Jᵀ and A live in the arena below)
   float Arr[MAXR], tgt[MAXR], lam[MAXR];
-  int rkind[MAXR];
+  int rkind[MAXR], rleg[MAXR];
   int cbody[MAXC];
   float cn[MAXC][3];  // contact normals (terrain); tangents follow from contact_tangents
   int nrows, nlim, ncon;
   float cf[LGX_MAX_BODIES][3];
   float rbz[LGX_MAX_BODIES];
+#ifdef LGX_PHASE_CLOCK
+  uint64_t phlast;
+  uint32_t phacc[16];
+#endif
   // --- one arena, three phases (never live at the same time)
   union {
     struct {  // post-physics staging
@@ -90,15 +96,32 @@ struct Sh {
       float heights[LGX_MAX_HEIGHT_POINTS];
     };
     struct {  // dynamics() temporaries
-      float red[NL][16];  // per-link partials about p0: m, h(3), Ip(6), F(3), N(3)
-      float tot[16];
       float Fw[NL][3], Nw[NL][3];  // per-link COM wrench (bias)
-      float Dl[4][6];
-      float S[4][21];
+      float Dl[4][6];              // leg blocks of the joint-space inertia (xx yy zz xy xz yz)
     };
     float arena[ARENA];  // constraint rows: J, M⁻¹Jᵀ, A (see ARENA)
   };
 };
+
+// ---- per-phase cycle counters (dev builds only: -DLGX_PHASE_CLOCK, tools/phase_clock.py).
+// Lane 0 accumulates s_memtime deltas per phase in LDS; the kernel's end writes them to
+// g_phase_out[env][phase]. Compiled out of the product library.
+#ifdef LGX_PHASE_CLOCK
+constexpr int NPH = 16;
+__device__ uint32_t* g_phase_out = nullptr;
+#define PH(k)                                              \
+  do {                                                     \
+    if (lane == 0) {                                       \
+      const uint64_t _t = clock64();                       \
+      s.phacc[k] += (uint32_t)(_t - s.phlast);             \
+      s.phlast = _t;                                       \
+    }                                                      \
+  } while (0)
+#else
+#define PH(k) \
+  do {        \
+  } while (0)
+#endif
 
 // ============================================================== physics helpers
 #pragma clang fp contract(fast)
@@ -123,52 +146,6 @@ LGX_DEV float sym3(const float* S, int i, int j) {
 }
 // packed symmetric 6x6 index (lower, row-major)
 LGX_DEV int pk(int i, int j) { return i >= j ? i * (i + 1) / 2 + j : j * (j + 1) / 2 + i; }
-
-// x = M⁻¹ b for one right-hand side, by the base Schur complement (one lane).
-// Loops over joints/legs are deliberately NOT unrolled: unrolled, the compiler hoists
-// all ~190 LDS operands into VGPRs and the kernel drops to one wave per SIMD.
-LGX_DEV void mass_solve(const Sh& s, const float* b, float* x) {  // b may alias x
-  float y0 = b[0], y1 = b[1], y2 = b[2], y3 = b[3], y4 = b[4], y5 = b[5];
-#pragma unroll 1
-  for (int j = 0; j < NJ; ++j) {
-    const float bj = b[6 + j];
-    const float* Xj = s.X[j];
-    y0 -= Xj[0] * bj; y1 -= Xj[1] * bj; y2 -= Xj[2] * bj;
-    y3 -= Xj[3] * bj; y4 -= Xj[4] * bj; y5 -= Xj[5] * bj;
-  }
-  // L Lᵀ z = y (packed lower Cholesky factor)
-  float z[6] = {y0, y1, y2, y3, y4, y5};
-#pragma unroll
-  for (int i = 0; i < 6; ++i) {
-    float t = z[i];
-#pragma unroll
-    for (int k = 0; k < i; ++k) t -= s.L[pk(i, k)] * z[k];
-    z[i] = t / s.L[pk(i, i)];
-  }
-#pragma unroll
-  for (int i = 5; i >= 0; --i) {
-    float t = z[i];
-#pragma unroll
-    for (int k = i + 1; k < 6; ++k) t -= s.L[pk(k, i)] * z[k];
-    z[i] = t / s.L[pk(i, i)];
-  }
-#pragma unroll
-  for (int r = 0; r < 6; ++r) x[r] = z[r];
-#pragma unroll 1
-  for (int l = 0; l < 4; ++l) {
-    float rhs[3];
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-      const int j = 3 * l + a;
-      const float* Bj = s.Bc[j];
-      rhs[a] = b[6 + j] - (Bj[0] * z[0] + Bj[1] * z[1] + Bj[2] * z[2] + Bj[3] * z[3] + Bj[4] * z[4] + Bj[5] * z[5]);
-    }
-    const float* Di = s.Dinv[l];
-    x[6 + 3 * l + 0] = Di[0] * rhs[0] + Di[3] * rhs[1] + Di[4] * rhs[2];
-    x[6 + 3 * l + 1] = Di[3] * rhs[0] + Di[1] * rhs[1] + Di[5] * rhs[2];
-    x[6 + 3 * l + 2] = Di[4] * rhs[0] + Di[5] * rhs[1] + Di[2] * rhs[2];
-  }
-}
 
 // forward kinematics, velocities and bias accelerations (lane 0: base; lanes 0..3: legs)
 LGX_DEV void kinematics(Sh& s, const lgx_model* M, int lane) {
@@ -231,46 +208,62 @@ LGX_DEV void kinematics(Sh& s, const lgx_model* M, int lane) {
   __syncthreads();
 }
 
-// composite-inertia mass-matrix blocks, bias forces and the base Schur complement.
-// Spread over lanes so that no lane holds more than one link/joint/entry worth of state:
-//   D1 lanes 0..12  per-link COM wrench (F, N) and base partials about p0
-//   D2 lanes 0..11  joint bias h_j and coupling column B_j;  lanes 16..39  leg block D
-//   D3 lanes 0..3   D_l⁻¹, X_l = B_l D_l⁻¹, Schur term X_l B_lᵀ;  lane 4  base sums
-//   D4 lane 0       S = A_bb - Σ X_l B_lᵀ and its Cholesky factor
-__device__ __noinline__ void dynamics(Sh& s, const lgx_task_params* Pm, int lane) {
+// Mass matrix M = [A B; Bᵀ D] over u = [base origin velocity, ω | 12 joint rates] (D block
+// diagonal over the 4 chains) and bias h, factored so that every later product with M⁻¹ is
+// a short lane-parallel chain instead of one lane's serial solve:
+//   X = B D⁻¹ (s.X[j][r] = X[r][j]),  S = A − X Bᵀ (base Schur complement),  S⁻¹ (s.Sinv)
+//   M⁻¹ f = [z ; D⁻¹ f_J − Xᵀ z]  with  z = S⁻¹ (f_B − X f_J)
+//   J M⁻¹ Jᵀ = y_rᵀ S⁻¹ y_s + [leg_r = leg_s] J_r,Jᵀ D_l⁻¹ J_s,J  with  y = J_B − X J_J
+// Lanes:
+//   D1 lanes 0..12  per-link COM wrench (lane 12: the base); the 16 base sums about p0
+//                   (mass, first moment, inertia, wrench) by DPP row reductions
+//   D2 lanes 0..11  joint bias h_j and coupling column B_j;  lanes 16..39 leg block D_l
+//   D3 lanes 0..11  D_l⁻¹ (row a), X_j; the 21 Schur sums by DPP; every lane factors S in
+//                   registers (Cholesky); lanes 0..5 write column `lane` of S⁻¹
+struct DynOut {
+  float hb[6];    // base bias (uniform)
+  float hj;       // lane j < 12: joint bias
+  float xj[6];    // lane j < 12: X_j
+  float dinv[3];  // lane j < 12: row a of D_l⁻¹
+};
+
+LGX_DEV void dynamics(Sh& s, const lgx_task_params* Pm, int lane, DynOut& o) {
   const f3 g = ld3(Pm->gravity);
   const f3 p0 = ld3(s.P[0]);
-  if (lane < NL) {  // ---- D1
-    const int k = lane;
-    f3 c = ld3(s.C[k]), w = ld3(s.W[k]), al = ld3(s.Al[k]);
-    f3 rl = c - ld3(s.P[k]);
-    f3 acc = ld3(s.Ao[k]) + cross(al, rl) + cross(w, cross(w, rl));
+  float tot[16];
+  {  // ---- D1
+    const int k = lane < NJ ? lane + 1 : 0;
+    const f3 c = ld3(s.C[k]), w = ld3(s.W[k]), al = ld3(s.Al[k]);
+    const f3 rl = c - ld3(s.P[k]);
+    const f3 acc = ld3(s.Ao[k]) + cross(al, rl) + cross(w, cross(w, rl));
     const float m = s.m[k];
-    f3 F = (acc - g) * m;
-    f3 N = symv(s.I[k], al) + cross(w, symv(s.I[k], w));
-    st3(s.Fw[k], F);
-    st3(s.Nw[k], N);
-    f3 r = c - p0;
-    float rr = dot(r, r);
-    float* rd = s.red[k];
-    rd[0] = m; rd[1] = m * r.x; rd[2] = m * r.y; rd[3] = m * r.z;
-    rd[4] = s.I[k][0] + m * (rr - r.x * r.x);
-    rd[5] = s.I[k][1] + m * (rr - r.y * r.y);
-    rd[6] = s.I[k][2] + m * (rr - r.z * r.z);
-    rd[7] = s.I[k][3] - m * r.x * r.y;
-    rd[8] = s.I[k][4] - m * r.x * r.z;
-    rd[9] = s.I[k][5] - m * r.y * r.z;
-    f3 Nt = cross(r, F) + N;
-    rd[10] = F.x; rd[11] = F.y; rd[12] = F.z; rd[13] = Nt.x; rd[14] = Nt.y; rd[15] = Nt.z;
+    const float* Ik = s.I[k];
+    const f3 F = (acc - g) * m;
+    const f3 N = symv(Ik, al) + cross(w, symv(Ik, w));
+    if (lane <= NJ) {
+      st3(s.Fw[k], F);
+      st3(s.Nw[k], N);
+    }
+    const f3 r = c - p0;
+    const float rr = dot(r, r);
+    const f3 Nt = cross(r, F) + N;
+    const float on = lane <= NJ ? 1.f : 0.f;
+    const float rd[16] = {m, m * r.x, m * r.y, m * r.z,
+                          Ik[0] + m * (rr - r.x * r.x), Ik[1] + m * (rr - r.y * r.y), Ik[2] + m * (rr - r.z * r.z),
+                          Ik[3] - m * r.x * r.y, Ik[4] - m * r.x * r.z, Ik[5] - m * r.y * r.z,
+                          F.x, F.y, F.z, Nt.x, Nt.y, Nt.z};
+#pragma unroll
+    for (int q = 0; q < 16; ++q) tot[q] = row0_sum16(rd[q] * on);
   }
   __syncthreads();
+  const int j = lane < NJ ? lane : NJ - 1, l = j / 3, a = j % 3;
   if (lane < NJ) {  // ---- D2a: joint j (leg l, chain position a)
-    const int j = lane, l = j / 3, a = j % 3;
     const int kj = 1 + j;
     const f3 ax = ld3(s.Ax[kj]), pj = ld3(s.P[kj]);
     f3 acc = mk(0, 0, 0), hl = mk(0, 0, 0), bang = mk(0, 0, 0);
-#pragma unroll 1
-    for (int i = a; i < 3; ++i) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      if (i < a) continue;
       const int k = 1 + 3 * l + i;
       const f3 c = ld3(s.C[k]);
       const f3 d = c - pj;
@@ -279,81 +272,101 @@ __device__ __noinline__ void dynamics(Sh& s, const lgx_task_params* Pm, int lane
       hl = hl + d * m;
       bang = bang + cross(c - p0, cross(ax, d)) * m + symv(s.I[k], ax);
     }
-    s.hj[j] = dot(ax, acc);
-    f3 blin = cross(ax, hl);
+    o.hj = dot(ax, acc);
+    const f3 blin = cross(ax, hl);
     float* Bj = s.Bc[j];
     Bj[0] = blin.x; Bj[1] = blin.y; Bj[2] = blin.z; Bj[3] = bang.x; Bj[4] = bang.y; Bj[5] = bang.z;
   } else if (lane >= 16 && lane < 40) {  // ---- D2b: leg block entry (xx yy zz xy xz yz)
-    const int q = lane - 16, l = q / 6, e = q % 6;
+    const int q = lane - 16, lq = q / 6, e = q % 6;
     const int j1 = e < 3 ? e : (e == 5 ? 1 : 0);
     const int j2 = e < 3 ? e : (e == 3 ? 1 : 2);
-    const int k1 = 1 + 3 * l + j1, k2 = 1 + 3 * l + j2;
+    const int k1 = 1 + 3 * lq + j1, k2 = 1 + 3 * lq + j2;
     const f3 a1 = ld3(s.Ax[k1]), a2 = ld3(s.Ax[k2]), p1 = ld3(s.P[k1]), p2 = ld3(s.P[k2]);
     float acc = 0.f;
-#pragma unroll 1
-    for (int i = j2; i < 3; ++i) {
-      const int k = 1 + 3 * l + i;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      if (i < j2) continue;
+      const int k = 1 + 3 * lq + i;
       const f3 c = ld3(s.C[k]);
       acc += s.m[k] * dot(cross(a1, c - p1), cross(a2, c - p2)) + dot(a1, symv(s.I[k], a2));
     }
-    s.Dl[l][e] = acc;
+    s.Dl[lq][e] = acc;
   }
   __syncthreads();
-  if (lane < 4) {  // ---- D3: leg l (operands streamed from LDS, not held in VGPRs)
-    const int l = lane;
-    float Di[6];
-    sym3_inv(s.Dl[l], Di);
+  // ---- D3
+  float Di[6];
+  sym3_inv(s.Dl[l], Di);
+#pragma unroll
+  for (int c = 0; c < 3; ++c) o.dinv[c] = sym3(Di, a, c);
+  if (lane < NJ && a == 0) {
 #pragma unroll
     for (int q = 0; q < 6; ++q) s.Dinv[l][q] = Di[q];
-#pragma unroll 1
-    for (int r = 0; r < 6; ++r) {
-      const float b0 = s.Bc[3 * l][r], b1 = s.Bc[3 * l + 1][r], b2 = s.Bc[3 * l + 2][r];
-      s.X[3 * l + 0][r] = b0 * Di[0] + b1 * Di[3] + b2 * Di[4];
-      s.X[3 * l + 1][r] = b0 * Di[3] + b1 * Di[1] + b2 * Di[5];
-      s.X[3 * l + 2][r] = b0 * Di[4] + b1 * Di[5] + b2 * Di[2];
-    }
-#pragma unroll 1
-    for (int r = 0; r < 6; ++r) {
-      const float x0 = s.X[3 * l][r], x1 = s.X[3 * l + 1][r], x2 = s.X[3 * l + 2][r];
-#pragma unroll 1
-      for (int q = 0; q <= r; ++q)
-        s.S[l][pk(r, q)] = x0 * s.Bc[3 * l][q] + x1 * s.Bc[3 * l + 1][q] + x2 * s.Bc[3 * l + 2][q];
-    }
-  } else if (lane >= 16 && lane < 32) {  // base sums over the 13 links, one quantity per lane
-    const int q = lane - 16;
-    float t = 0.f;
-#pragma unroll 1
-    for (int k = 0; k < NL; ++k) t += s.red[k][q];
-    s.tot[q] = t;
   }
-  __syncthreads();
-  if (lane == 0) {  // ---- D4: A_bb - Σ S_l into s.L, then in-place packed Cholesky
-    const float* t = s.tot;
-    float* L = s.L;
-    const float Mt = t[0], Hx = t[1], Hy = t[2], Hz = t[3];
-    // A = [[M I, -[H]x], [[H]x, Ip]]  (generalized velocity = base origin velocity, w)
-    // lower block rows 3..5 (w), cols 0..2 (v) = [H]x = [[0,-Hz,Hy],[Hz,0,-Hx],[-Hy,Hx,0]]
-    const float A[21] = {Mt, 0.f, Mt, 0.f, 0.f, Mt, 0.f, -Hz, Hy, t[4], Hz, 0.f, -Hx, t[7], t[5],
-                         -Hy, Hx, 0.f, t[8], t[9], t[6]};
-#pragma unroll 1
-    for (int q = 0; q < 21; ++q) L[q] = A[q] - (s.S[0][q] + s.S[1][q] + s.S[2][q] + s.S[3][q]);
-#pragma unroll 1
-    for (int j = 0; j < 6; ++j) {
-      float d = L[pk(j, j)];
-      for (int k = 0; k < j; ++k) d -= L[pk(j, k)] * L[pk(j, k)];
-      const float ljj = sqrtf(fmaxf(d, 1e-12f));
-      L[pk(j, j)] = ljj;
-      const float inv = 1.0f / ljj;
-      for (int i = j + 1; i < 6; ++i) {
-        float v = L[pk(i, j)];
-        for (int k = 0; k < j; ++k) v -= L[pk(i, k)] * L[pk(j, k)];
-        L[pk(i, j)] = v * inv;
-      }
-    }
+  float bj[6];
+  {
+    const float* B0 = s.Bc[3 * l];
+    const float* B1 = s.Bc[3 * l + 1];
+    const float* B2 = s.Bc[3 * l + 2];
 #pragma unroll
-    for (int q = 0; q < 6; ++q) s.hb[q] = t[10 + q];
+    for (int r = 0; r < 6; ++r) {
+      const float b0 = B0[r], b1 = B1[r], b2 = B2[r];
+      o.xj[r] = o.dinv[0] * b0 + o.dinv[1] * b1 + o.dinv[2] * b2;
+      bj[r] = a == 0 ? b0 : (a == 1 ? b1 : b2);
+    }
   }
-  __syncthreads();
+  if (lane < NJ) {
+#pragma unroll
+    for (int r = 0; r < 6; ++r) s.X[j][r] = o.xj[r];
+  }
+  const float on = lane < NJ ? 1.f : 0.f;
+  // S = A_bb − Σ_j X_j B_jᵀ (packed lower); A_bb = [[M I, −[H]x], [[H]x, Ip]] (base origin
+  // velocity, ω), [H]x = [[0,−Hz,Hy],[Hz,0,−Hx],[−Hy,Hx,0]]
+  const float Mt = tot[0], Hx = tot[1], Hy = tot[2], Hz = tot[3];
+  const float Ab[21] = {Mt, 0.f, Mt, 0.f, 0.f, Mt, 0.f, -Hz, Hy, tot[4], Hz, 0.f, -Hx, tot[7], tot[5],
+                        -Hy, Hx, 0.f, tot[8], tot[9], tot[6]};
+  float L[21];
+#pragma unroll
+  for (int r = 0; r < 6; ++r)
+#pragma unroll
+    for (int c = 0; c <= r; ++c) L[pk(r, c)] = Ab[pk(r, c)] - row0_sum16(on * o.xj[r] * bj[c]);
+  float inv[6];
+#pragma unroll
+  for (int c = 0; c < 6; ++c) {
+    float d = L[pk(c, c)];
+#pragma unroll
+    for (int k = 0; k < c; ++k) d -= L[pk(c, k)] * L[pk(c, k)];
+    const float lcc = sqrtf(fmaxf(d, 1e-12f));
+    inv[c] = 1.0f / lcc;
+#pragma unroll
+    for (int r = c + 1; r < 6; ++r) {
+      float v = L[pk(r, c)];
+#pragma unroll
+      for (int k = 0; k < c; ++k) v -= L[pk(r, k)] * L[pk(c, k)];
+      L[pk(r, c)] = v * inv[c];
+    }
+  }
+  // column `lane` of S⁻¹ = L⁻ᵀ L⁻¹ e_lane
+  float x[6];
+#pragma unroll
+  for (int r = 0; r < 6; ++r) {
+    float t = lane == r ? 1.f : 0.f;
+#pragma unroll
+    for (int k = 0; k < r; ++k) t -= L[pk(r, k)] * x[k];
+    x[r] = t * inv[r];
+  }
+#pragma unroll
+  for (int r = 5; r >= 0; --r) {
+    float t = x[r];
+#pragma unroll
+    for (int k = r + 1; k < 6; ++k) t -= L[pk(k, r)] * x[k];
+    x[r] = t * inv[r];
+  }
+  if (lane < 6) {
+#pragma unroll
+    for (int r = 0; r < 6; ++r) s.Sinv[lane][r] = x[r];
+  }
+#pragma unroll
+  for (int q = 0; q < 6; ++q) o.hb[q] = tot[10 + q];
 }
 
 // ---- terrain contact (heightfield / trimesh)
@@ -562,25 +575,48 @@ LGX_DEV void substep(Sh& s, const lgx_model* M, const lgx_task_params* Pm, const
       s.tau[j] = fminf(fmaxf(t, -Pm->torque_limits[j]), Pm->torque_limits[j]);
     }
   }
+  PH(1);
   kinematics(s, M, lane);
+  PH(2);
 #if defined(LGX_DBG_STAGE) && LGX_DBG_STAGE == 1
   return;
 #endif
-  dynamics(s, Pm, lane);
+  DynOut dy;
+  dynamics(s, Pm, lane, dy);
+  const int jl_ = lane < NJ ? lane : NJ - 1, leg_ = jl_ / 3, pos_ = jl_ % 3;  // joint lanes' leg / chain position
+  // ---- free velocity u* = u + dt M⁻¹ f, f = [−h_B ; τ − h_J] (factored form, see dynamics)
+  const float fj = lane < NJ ? s.tau[lane] - dy.hj : 0.f;
+  if (lane < NJ) s.up[lane] = fj;  // scratch: f_J, read by the leg's lanes below
+  float vb[6];
+#pragma unroll
+  for (int r = 0; r < 6; ++r) vb[r] = -dy.hb[r] - row0_sum16(dy.xj[r] * fj);
+  __syncthreads();  // S⁻¹ (dynamics) and f_J visible
+  PH(3);
 #if defined(LGX_DBG_STAGE) && LGX_DBG_STAGE == 2
   return;
 #endif
-  // ---- free velocity u* = u + dt M⁻¹ (Sᵀτ - h): rhs assembled lane-parallel, solved in
-  //      place in LDS by lane 0, then scaled lane-parallel
-  if (lane < 6) s.us[lane] = -s.hb[lane];
-  else if (lane < NU) s.us[lane] = s.tau[lane - 6] - s.hj[lane - 6];
-  __syncthreads();
-  if (lane == 0) mass_solve(s, s.us, s.us);
-  __syncthreads();
-  if (lane < NU) {
-    const float u0 = lane < 3 ? s.vo[lane] : (lane < 6 ? s.wb[lane - 3] : s.thd[lane - 6]);
-    s.us[lane] = u0 + dt * s.us[lane];
+  {
+    float zb[6];
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+      const float* Si = s.Sinv[r];
+      zb[r] = Si[0] * vb[0] + Si[1] * vb[1] + Si[2] * vb[2] + Si[3] * vb[3] + Si[4] * vb[4] + Si[5] * vb[5];
+    }
+    if (lane < 6) {
+      const float* Si = s.Sinv[lane];
+      const float zl = Si[0] * vb[0] + Si[1] * vb[1] + Si[2] * vb[2] + Si[3] * vb[3] + Si[4] * vb[4] + Si[5] * vb[5];
+      const float u0 = lane < 3 ? s.vo[lane] : s.wb[lane - 3];
+      s.us[lane] = u0 + dt * zl;
+    }
+    if (lane < NJ) {
+      const float* fl = s.up + 3 * leg_;
+      float bot = dy.dinv[0] * fl[0] + dy.dinv[1] * fl[1] + dy.dinv[2] * fl[2];
+#pragma unroll
+      for (int r = 0; r < 6; ++r) bot -= dy.xj[r] * zb[r];
+      s.us[6 + lane] = s.thd[lane] + dt * bot;
+    }
   }
+  PH(4);
   // ---- constraint detection: joint limits (lanes 0..11), contacts (one candidate per lane)
   bool lim_lo = false, lim_hi = false;
   if (lane < NJ && M->joint_has_limits[lane + 1]) {
@@ -621,17 +657,19 @@ LGX_DEV void substep(Sh& s, const lgx_model* M, const lgx_task_params* Pm, const
     else tv = d / dt;
     return tv;
   };
-  float* const J = s.arena;                 // [nrows][NU]
-  float* const MJ = s.arena + nrows * NU;   // [nrows][NU]
-  float* const Am = s.arena + 2 * nrows * NU;  // [nrows][nrows] (A path)
+  float* const J9 = s.arena;                  // [nrows][RW]: J_B (6) | J of leg rleg (3)
+  float* const ZG = s.arena + MAXR * RW;      // [nrows][RW]: z_r (6) | g_r (3)
+  float* const Am = s.arena + 2 * MAXR * RW;  // [nrows][nrows] (A path)
   if (lim_lo || lim_hi) {
-    int r = __popcll(lmask & below);
+    const int r = __popcll(lmask & below);
+    float* jr = J9 + r * RW;
 #pragma unroll
-    for (int q = 0; q < NU; ++q) J[(r) * NU + q] = 0.f;
-    J[(r) * NU + 6 + lane] = lim_lo ? 1.f : -1.f;
-    float d = lim_lo ? (M->joint_lower[lane + 1] - s.th[lane]) : (s.th[lane] - M->joint_upper[lane + 1]);
+    for (int q = 0; q < RW; ++q) jr[q] = 0.f;
+    jr[6 + pos_] = lim_lo ? 1.f : -1.f;
+    const float d = lim_lo ? (M->joint_lower[lane + 1] - s.th[lane]) : (s.th[lane] - M->joint_upper[lane + 1]);
     s.tgt[r] = target(d);
     s.rkind[r] = 0;
+    s.rleg[r] = leg_;
   }
   if (act && crank < MAXC) {
     const int r0 = nlim + 3 * crank;
@@ -644,68 +682,100 @@ LGX_DEV void substep(Sh& s, const lgx_model* M, const lgx_task_params* Pm, const
     st3(s.cn[crank], dn);
     const int leg = ck > 0 ? (ck - 1) / 3 : -1;
     const int pos = ck > 0 ? (ck - 1) % 3 : -1;
-#pragma unroll 1
+    const int kl = ck > 0 ? 1 + 3 * leg : 1;
+    const f3 ax0 = ld3(s.Ax[kl]), ax1 = ld3(s.Ax[kl + 1]), ax2 = ld3(s.Ax[kl + 2]);
+    const f3 r0p = xc - ld3(s.P[kl]), r1p = xc - ld3(s.P[kl + 1]), r2p = xc - ld3(s.P[kl + 2]);
+    const f3 rb = xc - p0;
+#pragma unroll
     for (int t = 0; t < 3; ++t) {
       const int r = r0 + t;
       const f3 d = t == 0 ? dn : (t == 1 ? dt1 : dt2);
-      f3 ang = cross(xc - p0, d);
-      J[(r) * NU + 0] = d.x; J[(r) * NU + 1] = d.y; J[(r) * NU + 2] = d.z;
-      J[(r) * NU + 3] = ang.x; J[(r) * NU + 4] = ang.y; J[(r) * NU + 5] = ang.z;
-#pragma unroll 4
-      for (int q = 0; q < NJ; ++q) J[(r) * NU + 6 + q] = 0.f;
-      for (int i = 0; i <= pos; ++i) {
-        const int ki = 1 + 3 * leg + i;
-        J[(r) * NU + 6 + 3 * leg + i] = dot(ld3(s.Ax[ki]), cross(xc - ld3(s.P[ki]), d));
-      }
+      const f3 ang = cross(rb, d);
+      float* jr = J9 + r * RW;
+      jr[0] = d.x; jr[1] = d.y; jr[2] = d.z;
+      jr[3] = ang.x; jr[4] = ang.y; jr[5] = ang.z;
+      jr[6] = pos >= 0 ? dot(ax0, cross(r0p, d)) : 0.f;
+      jr[7] = pos >= 1 ? dot(ax1, cross(r1p, d)) : 0.f;
+      jr[8] = pos >= 2 ? dot(ax2, cross(r2p, d)) : 0.f;
       s.rkind[r] = t;
+      s.rleg[r] = leg;
       s.tgt[r] = t == 0 ? target(depth) : 0.f;
     }
     s.cbody[crank] = M->cand_body[lane];
   }
   if (lane == 0) { s.nrows = nrows; s.nlim = nlim; s.ncon = ncon; }
   __syncthreads();
+  PH(5);
 #if defined(LGX_DBG_STAGE) && LGX_DBG_STAGE == 3
   return;
 #endif
-  // ---- per-row M⁻¹Jᵀ column and diagonal of A = J M⁻¹ Jᵀ (one lane per row)
-  if (lane < nrows) {
-    mass_solve(s, J + lane * NU, MJ + lane * NU);
-    float a = 0.f;
-#pragma unroll 1
-    for (int q = 0; q < NU; ++q) a += J[(lane) * NU + q] * MJ[(lane) * NU + q];
-    s.Arr[lane] = a;
+  // ---- per row (one lane each): y = J_B − X_l J_l, z = S⁻¹ y, g = D_l⁻¹ J_l,
+  //      A_rr = y·z + J_l·g, w_r = J_r u*
+  const bool row_lane = lane < nrows;
+  float yr[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, jlr[3] = {0.f, 0.f, 0.f}, w0 = 0.f;
+  int lr = -1;
+  if (row_lane) {
+    const float* jr = J9 + lane * RW;
+    lr = s.rleg[lane];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      yr[q] = jr[q];
+      w0 += yr[q] * s.us[q];
+    }
+    float g[3] = {0.f, 0.f, 0.f};
+    if (lr >= 0) {
+#pragma unroll
+      for (int c = 0; c < 3; ++c) jlr[c] = jr[6 + c];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const float* Xc = s.X[3 * lr + c];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) yr[q] -= Xc[q] * jlr[c];
+        w0 += jlr[c] * s.us[6 + 3 * lr + c];
+      }
+      const float* Di = s.Dinv[lr];
+      g[0] = Di[0] * jlr[0] + Di[3] * jlr[1] + Di[4] * jlr[2];
+      g[1] = Di[3] * jlr[0] + Di[1] * jlr[1] + Di[5] * jlr[2];
+      g[2] = Di[4] * jlr[0] + Di[5] * jlr[1] + Di[2] * jlr[2];
+    }
+    float* zg = ZG + lane * RW;
+    float arr = jlr[0] * g[0] + jlr[1] * g[1] + jlr[2] * g[2];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      const float* Si = s.Sinv[q];
+      const float zq = Si[0] * yr[0] + Si[1] * yr[1] + Si[2] * yr[2] + Si[3] * yr[3] + Si[4] * yr[4] + Si[5] * yr[5];
+      zg[q] = zq;
+      arr += yr[q] * zq;
+    }
+    zg[6] = g[0]; zg[7] = g[1]; zg[8] = g[2];
+    s.Arr[lane] = arr;
     s.lam[lane] = 0.f;
   }
   __syncthreads();
+  PH(6);
 #if defined(LGX_DBG_STAGE) && LGX_DBG_STAGE == 4
   return;
 #endif
   if (nrows <= AMAX) {
-    // ---- projected Gauss-Seidel on A (oracle_physics.c step 4): lane r keeps the row
-    //      velocity w_r = J_r u and lambda_r; a row update is one readlane + scalar
-    //      projection + one FMA per lane with row r of A (no cross-lane reductions)
-    float w = 0.f, lam = 0.f;
-    if (lane < nrows) {
-      float mj[NU];
-#pragma unroll
-      for (int q = 0; q < NU; ++q) mj[q] = MJ[(lane) * NU + q];
-      float a = 0.f;
-#pragma unroll
-      for (int q = 0; q < NU; ++q) a += J[(lane) * NU + q] * s.us[q];
-      w = a;
-#pragma unroll 1
-      for (int r = 0; r < nrows; ++r) {  // column `lane` of A (A is symmetric: row r, entry lane)
-        const float* jr = J + r * NU;
-        float v = 0.f;
-#pragma unroll
-        for (int q = 0; q < NU; ++q) v += jr[q] * mj[q];
-        Am[r * nrows + lane] = v;
+    // ---- A = J M⁻¹ Jᵀ: lane r writes column r (A is symmetric: entry (s, r) = y_r·z_s +
+    //      [leg_r = leg_s] J_l,r·g_s)
+    if (row_lane) {
+#pragma unroll 2
+      for (int q = 0; q < nrows; ++q) {
+        const float* zg = ZG + q * RW;
+        float v = yr[0] * zg[0] + yr[1] * zg[1] + yr[2] * zg[2] + yr[3] * zg[3] + yr[4] * zg[4] + yr[5] * zg[5];
+        if (lr >= 0 && s.rleg[q] == lr) v += jlr[0] * zg[6] + jlr[1] * zg[7] + jlr[2] * zg[8];
+        Am[q * nrows + lane] = v;
       }
     }
     __syncthreads();
+    PH(7);
+    // ---- projected Gauss-Seidel on A (oracle_physics.c step 4): lane r keeps the row
+    //      velocity w_r = J_r u and lambda_r; a row update is one readlane + scalar
+    //      projection + one FMA per lane with row r of A (no cross-lane reductions)
+    float w = w0, lam = 0.f;
     const float mu = s.mu;
     auto rd = [](float v, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); };
-    const bool row_lane = lane < nrows;
     // per-row constants live in their row's lane (readlane, no LDS round trip in the sweep)
     const float tg = row_lane ? s.tgt[lane] : 0.f;
     const float ia = row_lane ? 1.0f / s.Arr[lane] : 0.f;
@@ -742,31 +812,66 @@ LGX_DEV void substep(Sh& s, const lgx_model* M, const lgx_task_params* Pm, const
     }
     if (row_lane) s.lam[lane] = lam;
     __syncthreads();
-    // u+ = u* + M⁻¹ Jᵀ lambda
-    if (lane < NU) {
-      float uc = s.us[lane];
-#pragma unroll 1
-      for (int r = 0; r < nrows; ++r) uc += MJ[(r) * NU + lane] * s.lam[r];
-      s.up[lane] = uc;
+    PH(8);
+    // ---- u+ = u* + M⁻¹ Jᵀ λ = u* + [Z ; G_J − Xᵀ Z]:  Z = Σ_r λ_r z_r,
+    //      G_j = Σ_{r on leg(j)} λ_r g_r[pos(j)]
+    float Z[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, G = 0.f;
+#pragma unroll 2
+    for (int r = 0; r < nrows; ++r) {
+      const float lr_ = s.lam[r];
+      const float* zg = ZG + r * RW;
+#pragma unroll
+      for (int q = 0; q < 6; ++q) Z[q] += lr_ * zg[q];
+      if (s.rleg[r] == leg_) G += lr_ * zg[6 + pos_];
+    }
+    if (lane < 6) {
+      float zl = 0.f;
+#pragma unroll
+      for (int q = 0; q < 6; ++q) zl = lane == q ? Z[q] : zl;
+      s.up[lane] = s.us[lane] + zl;
+    }
+    if (lane < NJ) {
+      float v = s.us[6 + lane] + G;
+#pragma unroll
+      for (int q = 0; q < 6; ++q) v -= dy.xj[q] * Z[q];
+      s.up[6 + lane] = v;
     }
     __syncthreads();
+    PH(9);
   } else {
-    // ---- wide systems: PGS in velocity space, generalized velocity over lanes 0..17
-    float uc = lane < NU ? s.us[lane] : 0.f;
+    // ---- wide systems: PGS in velocity space; lanes 0..11 hold the joint rates, lanes
+    //      12..17 the base velocity; M⁻¹ J_rᵀ is formed from (z_r, g_r) on the fly
+    const int bi = lane - NJ;
+    auto jcomp = [&](int r) {
+      const float* jr = J9 + r * RW;
+      if (lane < NJ) return s.rleg[r] == leg_ ? jr[6 + pos_] : 0.f;
+      return lane < NU ? jr[bi] : 0.f;
+    };
+    auto mjcomp = [&](int r) {
+      const float* zg = ZG + r * RW;
+      if (lane < NJ) {
+        float v = s.rleg[r] == leg_ ? zg[6 + pos_] : 0.f;
+#pragma unroll
+        for (int q = 0; q < 6; ++q) v -= dy.xj[q] * zg[q];
+        return v;
+      }
+      return lane < NU ? zg[bi] : 0.f;
+    };
+    float uc = lane < NJ ? s.us[6 + lane] : (lane < NU ? s.us[bi] : 0.f);
     const float mu = s.mu;
     for (int it = 0; it < Pm->solver_iterations; ++it) {
       for (int r = 0; r < nrows; ++r) {
         const int kind = s.rkind[r];
         if (kind == 0) {
-          float w = row_sums_32(lane < NU ? J[(r) * NU + lane] * uc : 0.f);
+          float w = row_sums_32(jcomp(r) * uc);
           float lo = s.lam[r];
           float ln = fmaxf(0.f, lo + (s.tgt[r] - w) / s.Arr[r]);
           float d = ln - lo;
-          if (lane < NU) uc += MJ[(r) * NU + lane] * d;
+          uc += mjcomp(r) * d;
           if (lane == 0) s.lam[r] = ln;
         } else {
-          float w1 = row_sums_32(lane < NU ? J[(r) * NU + lane] * uc : 0.f);
-          float w2 = row_sums_32(lane < NU ? J[(r + 1) * NU + lane] * uc : 0.f);
+          float w1 = row_sums_32(jcomp(r) * uc);
+          float w2 = row_sums_32(jcomp(r + 1) * uc);
           float o1 = s.lam[r], o2 = s.lam[r + 1];
           float l1 = o1 - w1 / s.Arr[r];
           float l2 = o2 - w2 / s.Arr[r + 1];
@@ -776,14 +881,16 @@ LGX_DEV void substep(Sh& s, const lgx_model* M, const lgx_task_params* Pm, const
             float sc = n > 0.f ? lim / n : 0.f;
             l1 *= sc; l2 *= sc;
           }
-          if (lane < NU) uc += MJ[(r) * NU + lane] * (l1 - o1) + MJ[(r + 1) * NU + lane] * (l2 - o2);
+          uc += mjcomp(r) * (l1 - o1) + mjcomp(r + 1) * (l2 - o2);
           if (lane == 0) { s.lam[r] = l1; s.lam[r + 1] = l2; }
           ++r;
         }
       }
     }
-    if (lane < NU) s.up[lane] = uc;
+    if (lane < NJ) s.up[6 + lane] = uc;
+    else if (lane < NU) s.up[bi] = uc;
     __syncthreads();
+    PH(8);
   }
   // ---- contact forces of the last substep, per reported body (world frame)
   if (last && lane < LGX_MAX_BODIES) {
@@ -834,6 +941,7 @@ LGX_DEV void substep(Sh& s, const lgx_model* M, const lgx_task_params* Pm, const
     s.th[lane] += dt * s.thd[lane];
   }
   __syncthreads();
+  PH(10);
 }
 
 #pragma clang fp contract(off)
@@ -1248,6 +1356,10 @@ __global__ __launch_bounds__(64, LGX_WAVES_PER_EU) void env_step_kernel(const lg
     s.mu = 0.5f * ((B.friction ? B.friction[e] : 1.f) + Pm->ground_friction);
   }
   if (lane < 3) s.cadd[lane] = B.mass_params ? B.mass_params[e * 4 + 1 + lane] : 0.f;
+#ifdef LGX_PHASE_CLOCK
+  if (lane < 16) s.phacc[lane] = 0u;
+  if (lane == 0) s.phlast = clock64();
+#endif
   __syncthreads();
 
   if (PHYSICS) {
@@ -1263,6 +1375,7 @@ __global__ __launch_bounds__(64, LGX_WAVES_PER_EU) void env_step_kernel(const lg
       st3(s.vo, vo);
     }
     __syncthreads();
+    PH(0);
     for (int sub = 0; sub < Pm->decimation; ++sub) substep<TERRAIN, ACTNET>(s, M, Pm, B, lane, sub == Pm->decimation - 1);
     // final kinematics for the rigid-body state tensor
     kinematics(s, M, lane);
@@ -1316,6 +1429,7 @@ __global__ __launch_bounds__(64, LGX_WAVES_PER_EU) void env_step_kernel(const lg
     }
     if (lane < D) B.torques[(size_t)e * D + lane] = s.tau[lane];
     __syncthreads();
+    PH(11);
   } else {
     // post-physics only: physics state supplied by the caller
     if (lane < NB) {
@@ -1334,6 +1448,7 @@ __global__ __launch_bounds__(64, LGX_WAVES_PER_EU) void env_step_kernel(const lg
   // Go2Robot.post_physics_step go2.py:345-387 / LeggedRobot legged_robot.py:103-138.
   // Per-env scalars: lane 0, into LDS. Vectors: lane-parallel from LDS.
   fill_uniforms(s, seed, gid, step, 0, lane, rng_blocks(Pm));
+  PH(12);
   const bool go2 = Pm->task_kind == LGX_TASK_GO2;
   if (lane == 0) {
     Scratch& x = s.x;
@@ -1402,6 +1517,7 @@ __global__ __launch_bounds__(64, LGX_WAVES_PER_EU) void env_step_kernel(const lg
     x.jump = B.rpy_phase ? B.rpy_phase[e * 8 + 7] : 0.f;  // set by the previous step's observations
   }
   __syncthreads();
+  PH(13);
   get_heights(Pm, B, s, lane);
   __syncthreads();
   // compute_reward legged_robot.py:216-237: lane k evaluates term k (alphabetical order)
@@ -1426,6 +1542,7 @@ __global__ __launch_bounds__(64, LGX_WAVES_PER_EU) void env_step_kernel(const lg
   __syncthreads();
   if (lane < KS) B.episode_sums[(size_t)e * KS + lane] += s.rterm[lane];
   __syncthreads();
+  PH(14);
   // reset_idx (go2.py:207-263)
   if (reset) reset_env(Pm, B, s, e, lane, true, false);
 
@@ -1542,6 +1659,12 @@ __global__ __launch_bounds__(64, LGX_WAVES_PER_EU) void env_step_kernel(const lg
   }
   if (B.measured_heights)
     for (int i = lane; i < Pm->num_height_points; i += 64) B.measured_heights[(size_t)e * Pm->num_height_points + i] = s.heights[i];
+#ifdef LGX_PHASE_CLOCK
+  __syncthreads();
+  PH(15);
+  __syncthreads();
+  if (g_phase_out && lane < NPH) g_phase_out[(size_t)e * NPH + lane] = s.phacc[lane];
+#endif
 }
 
 // BaseTask.reset -> reset_idx(env_ids) outside a step (RNG stream 1)
@@ -1787,6 +1910,13 @@ int lgx_episode_extras(lgx_env* env, float* means, float* level_mean, uint8_t* t
   env->stats_clean = true;
   return 0;
 }
+
+#ifdef LGX_PHASE_CLOCK
+// dev builds only: per-env phase cycle counters ([num_envs][16] uint32, device memory)
+int lgx_debug_phase_buffer(uint32_t* dev_ptr) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(lgx::g_phase_out), &dev_ptr, sizeof(dev_ptr)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 const char* lgx_last_error(const lgx_env* env) { return env ? env->err.c_str() : "null env"; }
 

@@ -1,7 +1,8 @@
+# GPU box: the whole -m gpu suite (verbose, per-test timeout), then one bench line.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider -rf > gpurun_out/pytest_gpu.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -v -p no:cacheprovider -rf --timeout 180 --timeout-method thread ${TESTS} > gpurun_out/pytest_gpu.log 2>&1
 rc=$?
 echo "pytest rc=$rc"
 tail -30 gpurun_out/pytest_gpu.log

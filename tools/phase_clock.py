@@ -1,0 +1,85 @@
+"""Per-phase cycle counts of the env-step kernel (dev tool).
+
+`python tools/phase_clock.py --build` (CPU container) compiles lib/liblgx_prof.so with
+-DLGX_PHASE_CLOCK; on the GPU box `python tools/phase_clock.py` runs the Go2 bench
+workload through it and prints, per phase, the mean/p50/p90 s_memtime cycles one env's
+wave spends there (summed over the 4 substeps), and the share of the wave's total.
+Env vars: TASK (go2), N (4096), K (10 timed steps)."""
+import ctypes as C
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIBDIR = os.path.join(ROOT, "legged_gym_custom_amd", "lib")
+PROF = os.path.join(LIBDIR, "liblgx_prof.so")
+PHASES = ["load", "pd", "kinematics", "dynamics", "free_vel", "detect+rows", "row_solves", "A_build", "pgs",
+          "u_update", "forces+integrate", "final_kin+writes", "uniforms", "post_scalar", "heights+rewards",
+          "reset+obs+writes"]
+
+
+def build():
+    src = os.path.join(ROOT, "legged_gym_custom_amd", "csrc", "lgx_env.hip")
+    extra = os.environ.get("EXTRA", "").split()
+    cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
+           "-DLGX_PHASE_CLOCK"] + extra + ["-o", PROF, src]
+    print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+
+
+def run():
+    os.environ["LGX_LIB"] = PROF
+    sys.path.insert(0, ROOT)
+    import torch
+    from legged_gym_custom_amd import _native
+    from legged_gym_custom_amd.envs import task_registry
+    from legged_gym_custom_amd.utils.helpers import get_args
+    task = os.environ.get("TASK", "go2")
+    n = int(os.environ.get("N", "4096"))
+    k = int(os.environ.get("K", "10"))
+    a = get_args([f"--task={task}", "--headless", f"--num_envs={n}", "--sim_device=cuda:0", "--rl_device=cuda:0",
+                  "--seed=1"])
+    env_cfg, _ = task_registry.get_cfgs(task)
+    if task.startswith("anymal"):
+        import tempfile
+        from legged_gym_custom_amd import actuator as act
+        path = os.path.join(tempfile.mkdtemp(), "sea.pt")
+        act.save_sea_archive(act.random_sea_weights(1, scale=0.3), path)
+        env_cfg.control.actuator_net_file = path
+    env, _ = task_registry.make_env(task, a, env_cfg)
+    L = _native.lib()
+    L.lgx_debug_phase_buffer.argtypes = [C.c_void_p]
+    buf = torch.zeros(n, 16, dtype=torch.int32, device="cuda:0")
+    g = torch.Generator(device="cuda:0").manual_seed(1234)
+    stream = torch.cuda.current_stream()
+    acc = torch.zeros(n, 16, dtype=torch.float64, device="cuda:0")
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ms = 0.0
+    for i in range(20 + k):
+        if i == 20:
+            assert L.lgx_debug_phase_buffer(C.c_void_p(buf.data_ptr())) == 0
+        env.actions_in.copy_(torch.clamp(torch.randn(n, env.num_actions, device="cuda:0", generator=g), -3.14, 3.14))
+        env.common_step_counter += 1
+        if i >= 20:
+            s.record()
+        env._native.step(env.seed, env.common_step_counter, stream.cuda_stream)
+        if i >= 20:
+            e.record()
+            torch.cuda.synchronize()
+            ms += s.elapsed_time(e)
+            acc += buf.double().remainder(2 ** 32)
+    acc /= k
+    tot = acc.sum(dim=1)
+    print(f"task {task} N={n}: kernel {ms / k * 1e3:.1f} us/launch; wave total cycles mean {tot.mean():.0f} "
+          f"p50 {tot.median():.0f} p90 {torch.quantile(tot, 0.9):.0f} (s_memtime clock)")
+    print(f"{'phase':18s} {'mean':>9s} {'p50':>9s} {'p90':>9s} {'share':>6s}")
+    for j, name in enumerate(PHASES):
+        c = acc[:, j]
+        print(f"{name:18s} {c.mean():9.0f} {c.median():9.0f} {torch.quantile(c, 0.9):9.0f} {c.mean() / tot.mean():6.1%}")
+
+
+if __name__ == "__main__":
+    if "--build" in sys.argv:
+        build()
+    else:
+        run()
