@@ -48,16 +48,36 @@ struct Scratch {  // per-env post-physics scalars (go2.py:357-367, 279-328)
   float jump;
 };
 
-// LDS arena time-shared by phase (dynamics temporaries -> constraint rows -> post-physics
-// staging). Constraint rows are stored sparse: row r = [base part (6) | the 3 joints of
-// leg rleg[r]] (J9), with z_r = S⁻¹ (J_b − X_l J_l) and g_r = D_l⁻¹ J_l (ZG, see dynamics);
-// for n <= AMAX rows also A = J M⁻¹ Jᵀ [n][n].
-constexpr int ARENA = 2200;
+// LDS arena (dynamic shared memory, sized per launch by arena_floats) time-shared by phase:
+//   dynamics   Fw, Nw [NL][3], Dl [4][6], tot [16]
+//   rows       ZG [MAXR][RW] at 0: z_r = S⁻¹ (J_b − X_l J_l) (6) | g_r = D_l⁻¹ J_l (3);
+//              J9 [MAXR][RW] at MAXR*RW: sparse row r = [base part (6) | the 3 joints of leg
+//              rleg[r]]; once J9 is in registers, the same region holds A = J M⁻¹ Jᵀ for
+//              n <= AMAX rows, packed lower-triangular (see dynamics)
+//   post       U [4 rng_blocks] | cur [P] | hist [H*P] | heights [Hp] (stg_* below)
+// Go2 needs 1080 floats (the rows), ANYmal's post-physics staging 1,924.
 constexpr int AMAX = 32;
 constexpr int RW = 9;  // sparse row width
-static_assert(NSLOT + LGX_MAX_PROPRIO + MAXHIST + LGX_MAX_HEIGHT_POINTS <= ARENA,
-              "post-physics staging must fit the arena");
-static_assert(2 * MAXR * RW + AMAX * AMAX <= ARENA, "arena must hold J9, ZG (MAXR rows) and A (AMAX rows)");
+constexpr int ROWS_FLOATS = 2 * MAXR * RW;
+static_assert(AMAX * (AMAX + 1) / 2 <= MAXR * RW, "packed A must fit the J9 region");
+extern __shared__ float lgx_dyn[];
+LGX_DEV int pk_lo(int r, int c) { return r * (r + 1) / 2 + c; }  // packed lower, r >= c
+struct DynTemps {
+  float Fw[NL][3], Nw[NL][3];  // per-link COM wrench (bias)
+  float Dl[4][6];              // leg blocks of the joint-space inertia (xx yy zz xy xz yz)
+  float tot[16];               // base sums about p0: m, h(3), Ip(6), F(3), N(3)
+};
+static_assert(sizeof(DynTemps) <= ROWS_FLOATS * sizeof(float), "dynamics temporaries fit the arena");
+LGX_DEV DynTemps& dtmp() { return *reinterpret_cast<DynTemps*>(lgx_dyn); }
+LGX_DEV float* stg_U() { return lgx_dyn; }
+LGX_DEV float* stg_cur(const lgx_task_params* Pm) { return lgx_dyn + 4 * rng_blocks(Pm); }
+LGX_DEV float* stg_hist(const lgx_task_params* Pm) { return stg_cur(Pm) + Pm->num_proprio; }
+LGX_DEV float* stg_heights(const lgx_task_params* Pm) { return stg_hist(Pm) + Pm->history_len * Pm->num_proprio; }
+static inline int64_t arena_floats(const lgx_task_params& p) {
+  const int64_t post = 4 * (9 + (p.num_proprio + 3) / 4) + p.num_proprio + (int64_t)p.history_len * p.num_proprio +
+                       p.num_height_points;
+  return post > ROWS_FLOATS ? post : ROWS_FLOATS;
+}
 
 struct Sh {
   // --- post-physics per-env scalars (written by lane 0, read by all lanes)
@@ -72,7 +92,7 @@ struct Sh {
   float th[NJ], thd[NJ], tau[NJ], act[NJ], kpm[NJ], kdm[NJ], ldv[NJ];
   float madd, cadd[3], mu;
   // --- kinematics per dynamic link
-  float R[NL][9], P[NL][3], Ax[NL][3], W[NL][3], V[NL][3], Al[NL][3], Ao[NL][3], C[NL][3], I[NL][6], m[NL];
+  float R[NL][9], P[NL][3], Ax[NL][3], W[NL][3], V[NL][3], C[NL][3], I[NL][6], m[NL];
   // --- dynamics
   float Bc[NJ][6], Dinv[4][6], X[NJ][6], Sinv[6][6], us[NU], up[NU];
   // --- constraints (J, M⁻¹Jᵀ and A live in the arena below)
@@ -87,20 +107,6 @@ struct Sh {
   uint64_t phlast;
   uint32_t phacc[16];
 #endif
-  // --- one arena, three phases (never live at the same time)
-  union {
-    struct {  // post-physics staging
-      float U[NSLOT];
-      float cur[LGX_MAX_PROPRIO];
-      float hist[MAXHIST];
-      float heights[LGX_MAX_HEIGHT_POINTS];
-    };
-    struct {  // dynamics() temporaries
-      float Fw[NL][3], Nw[NL][3];  // per-link COM wrench (bias)
-      float Dl[4][6];              // leg blocks of the joint-space inertia (xx yy zz xy xz yz)
-    };
-    float arena[ARENA];  // constraint rows: J, M⁻¹Jᵀ, A (see ARENA)
-  };
 };
 
 // ---- per-phase cycle counters (dev builds only: -DLGX_PHASE_CLOCK, tools/phase_clock.py).
@@ -126,6 +132,13 @@ __device__ uint32_t* g_phase_out = nullptr;
 // ============================================================== physics helpers
 #pragma clang fp contract(fast)
 
+// a pointer the compiler must treat as changed here (defeats loop-invariant hoisting)
+template <class T>
+LGX_DEV const T* opaque(const T* p) {
+  __asm__ volatile("" : "+s"(p));
+  return p;
+}
+
 // symmetric 3x3 (xx yy zz xy xz yz) inverse
 LGX_DEV void sym3_inv(const float* D, float* O) {
   float a = D[0], b = D[1], c = D[2], d = D[3], e = D[4], f = D[5];
@@ -147,63 +160,147 @@ LGX_DEV float sym3(const float* S, int i, int j) {
 // packed symmetric 6x6 index (lower, row-major)
 LGX_DEV int pk(int i, int j) { return i >= j ? i * (i + 1) / 2 + j : j * (j + 1) / 2 + i; }
 
-// forward kinematics, velocities and bias accelerations (lane 0: base; lanes 0..3: legs)
-LGX_DEV void kinematics(Sh& s, const lgx_model* M, int lane) {
-  if (lane == 0) {
-    quat_to_R(s.qb, s.R[0]);
+// lane i receives lane i-1's value (DPP row_shr:1; lanes 0..15 form one row)
+LGX_DEV float from_prev_lane(float x) { return dpp_shr_t<0x111>(x); }
+
+// Forward kinematics, velocities and bias accelerations, one lane per link: lane j < 12
+// is joint j / link j+1 (leg j/3, chain position j%3), lane 12 the base. A chain is three
+// deep: each of three rounds composes every lane with its parent's world state, then the
+// parent state moves one lane down the chain by DPP, so no lane waits on LDS. Writes the
+// link arrays the later phases read (R, P, Ax, W, V, C, I, m). With BIAS, the same lanes
+// also form the per-link COM wrench (Fw, Nw) and return the 16 base sums about p0 (mass,
+// first moment, inertia, wrench), reduced across lanes 0..15 by DPP (see dynamics).
+template <bool BIAS>
+LGX_DEV void kinematics(Sh& s, const lgx_model* M, const lgx_task_params* Pm, int lane) {
+  const int j = lane < NJ ? lane : NJ - 1;
+  const bool base = lane == NJ;  // the base rides the chain as a fixed joint at the root
+  const int a = base ? 0 : j % 3;
+  const int k = base ? 0 : j + 1;
+  // per-lane model constants (vector loads, L1-resident); identity joint for the base lane
+  const float bm = base ? 0.f : 1.f;
+  const f3 orig = ld3(M->joint_origin[j + 1]) * bm, al = ld3(M->joint_axis[j + 1]) * bm;
+  float Rj[9];
+  {
+    const float* Rjp = M->joint_rot[j + 1];
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      s.P[0][i] = s.pb[i]; s.W[0][i] = s.wb[i]; s.V[0][i] = s.vo[i];
-      s.Al[0][i] = 0.f; s.Ao[0][i] = 0.f; s.Ax[0][i] = 0.f;
-    }
-    float mb = M->link_mass[0] + s.madd;
-    f3 cl = mk(M->link_com[0][0] + s.cadd[0], M->link_com[0][1] + s.cadd[1], M->link_com[0][2] + s.cadd[2]);
-    st3(s.C[0], ld3(s.pb) + mv(s.R[0], cl));
-    s.m[0] = mb;
+    for (int q = 0; q < 9; ++q) Rj[q] = base ? ((q & 3) == 0 ? 1.f : 0.f) : Rjp[q];
   }
-  __syncthreads();
-  if (lane < 4) {
-    int par = 0;
+  // local rotation of joint j: joint frame, then the axis-angle rotation
+  const float th = base ? 0.f : s.th[j], thd = base ? 0.f : s.thd[j];
+  float Rl[9];
+  {
+    const float ct = cosf(th), st = sinf(th), t1 = 1.f - ct;
+    const float Ra[9] = {t1 * al.x * al.x + ct, t1 * al.x * al.y - st * al.z, t1 * al.x * al.z + st * al.y,
+                         t1 * al.x * al.y + st * al.z, t1 * al.y * al.y + ct, t1 * al.y * al.z - st * al.x,
+                         t1 * al.x * al.z - st * al.y, t1 * al.y * al.z + st * al.x, t1 * al.z * al.z + ct};
+    mm(Rj, Ra, Rl);
+  }
+  const f3 axl = mv(Rj, al);
+  // parent state, initially the base (uniform)
+  float Rp[9];
+  quat_to_R(s.qb, Rp);
+  f3 Pp = ld3(s.pb), Wp = ld3(s.wb), Vp = ld3(s.vo), Alp = mk(0.f, 0.f, 0.f), Aop = mk(0.f, 0.f, 0.f);
+  float R[9];
+  f3 P, ax, W, V, Al, Ao;
 #pragma unroll 1
-    for (int i = 0; i < 3; ++i) {
-      const int k = 1 + 3 * lane + i;
-      const float* Rp = s.R[par];
-      f3 o = mv(Rp, ld3(M->joint_origin[k]));
-      float RpRj[9];
-      mm(Rp, M->joint_rot[k], RpRj);
-      f3 al = ld3(M->joint_axis[k]);
-      float th = s.th[k - 1], ct = cosf(th), st = sinf(th), t1 = 1.f - ct;
-      float Ra[9] = {t1 * al.x * al.x + ct, t1 * al.x * al.y - st * al.z, t1 * al.x * al.z + st * al.y,
-                     t1 * al.x * al.y + st * al.z, t1 * al.y * al.y + ct, t1 * al.y * al.z - st * al.x,
-                     t1 * al.x * al.z - st * al.y, t1 * al.y * al.z + st * al.x, t1 * al.z * al.z + ct};
-      mm(RpRj, Ra, s.R[k]);
-      f3 ax = mv(RpRj, al);
-      st3(s.Ax[k], ax);
-      f3 pp = ld3(s.P[par]) + o;
-      st3(s.P[k], pp);
-      f3 wp = ld3(s.W[par]);
-      f3 wa = ax * s.thd[k - 1];
-      st3(s.W[k], wp + wa);
-      st3(s.V[k], ld3(s.V[par]) + cross(wp, o));
-      f3 alp = ld3(s.Al[par]);
-      st3(s.Al[k], alp + cross(wp, wa));
-      st3(s.Ao[k], ld3(s.Ao[par]) + cross(alp, o) + cross(wp, cross(wp, o)));
-      st3(s.C[k], pp + mv(s.R[k], ld3(M->link_com[k])));
-      s.m[k] = M->link_mass[k];
-      par = k;
+  for (int d = 0; d < 3; ++d) {
+    const f3 o = mv(Rp, orig);
+    ax = mv(Rp, axl);
+    mm(Rp, Rl, R);
+    P = Pp + o;
+    const f3 wa = ax * thd;
+    W = Wp + wa;
+    if constexpr (BIAS) {
+      Al = Alp + cross(Wp, wa);
+      Ao = Aop + cross(Alp, o) + cross(Wp, cross(Wp, o));
+    } else {
+      V = Vp + cross(Wp, o);
+    }
+    if (d < 2) {
+      const bool take = a == d + 1;
+#pragma unroll
+      for (int q = 0; q < 9; ++q) {
+        const float v = from_prev_lane(R[q]);
+        Rp[q] = take ? v : Rp[q];
+      }
+#define LGX_PASS(dst, src)                                                                          \
+  {                                                                                                 \
+    const float vx = from_prev_lane(src.x), vy = from_prev_lane(src.y), vz = from_prev_lane(src.z); \
+    dst.x = take ? vx : dst.x;                                                                      \
+    dst.y = take ? vy : dst.y;                                                                      \
+    dst.z = take ? vz : dst.z;                                                                      \
+  }
+      LGX_PASS(Pp, P)
+      LGX_PASS(Wp, W)
+      if constexpr (BIAS) {
+        LGX_PASS(Alp, Al)
+        LGX_PASS(Aop, Ao)
+      } else {
+        LGX_PASS(Vp, V)
+      }
+#undef LGX_PASS
     }
   }
-  // world inertia per link (lanes 0..12)
-  __syncthreads();
-  if (lane < NL) {
-    const float* R = s.R[lane];
-    const float* In = M->link_inertia[lane];
-    float Il[9] = {In[0], In[3], In[4], In[3], In[1], In[5], In[4], In[5], In[2]};
-    float T[9], Rt[9] = {R[0], R[3], R[6], R[1], R[4], R[7], R[2], R[5], R[8]}, O[9];
-    mm(R, Il, T);
-    mm(T, Rt, O);
-    s.I[lane][0] = O[0]; s.I[lane][1] = O[4]; s.I[lane][2] = O[8];
-    s.I[lane][3] = O[1]; s.I[lane][4] = O[2]; s.I[lane][5] = O[5];
+  const float* clp = M->link_com[k];
+  const float cb = base ? 1.f : 0.f;
+  const f3 cl = mk(clp[0] + cb * s.cadd[0], clp[1] + cb * s.cadd[1], clp[2] + cb * s.cadd[2]);
+  const f3 C = P + mv(R, cl);
+  if (lane <= NJ) {
+#pragma unroll
+    for (int q = 0; q < 9; ++q) s.R[k][q] = R[q];
+    st3(s.P[k], P);
+    st3(s.Ax[k], ax);
+    st3(s.W[k], W);
+    st3(s.C[k], C);
+    if constexpr (!BIAS) st3(s.V[k], V);
+  }
+  if constexpr (BIAS) {
+    const float m = M->link_mass[k] + cb * s.madd;
+    // world inertia about the COM: R I Rᵀ
+    float Iw[6];
+    {
+      const float* In = M->link_inertia[k];
+      const float Il[9] = {In[0], In[3], In[4], In[3], In[1], In[5], In[4], In[5], In[2]};
+      float T[9];
+      mm(R, Il, T);
+      Iw[0] = T[0] * R[0] + T[1] * R[1] + T[2] * R[2];
+      Iw[1] = T[3] * R[3] + T[4] * R[4] + T[5] * R[5];
+      Iw[2] = T[6] * R[6] + T[7] * R[7] + T[8] * R[8];
+      Iw[3] = T[0] * R[3] + T[1] * R[4] + T[2] * R[5];
+      Iw[4] = T[0] * R[6] + T[1] * R[7] + T[2] * R[8];
+      Iw[5] = T[3] * R[6] + T[4] * R[7] + T[5] * R[8];
+    }
+    const f3 g = ld3(Pm->gravity);
+    const f3 rl = C - P;
+    const f3 acc = Ao + cross(Al, rl) + cross(W, cross(W, rl));
+    const f3 F = (acc - g) * m;
+    const f3 N = symv(Iw, Al) + cross(W, symv(Iw, W));
+    if (lane <= NJ) {
+#pragma unroll
+      for (int q = 0; q < 6; ++q) s.I[k][q] = Iw[q];
+      s.m[k] = m;
+      st3(dtmp().Fw[k], F);
+      st3(dtmp().Nw[k], N);
+    }
+    // the 16 base sums about p0, reduced over lanes 0..15 (row 0) by a DPP scan whose
+    // total lands on lane 15
+    const f3 r = C - ld3(s.pb);
+    const float rr = dot(r, r);
+    const f3 Nt = cross(r, F) + N;
+    const float on = lane <= NJ ? 1.f : 0.f;
+    const float rd[16] = {m, m * r.x, m * r.y, m * r.z,
+                          Iw[0] + m * (rr - r.x * r.x), Iw[1] + m * (rr - r.y * r.y), Iw[2] + m * (rr - r.z * r.z),
+                          Iw[3] - m * r.x * r.y, Iw[4] - m * r.x * r.z, Iw[5] - m * r.y * r.z,
+                          F.x, F.y, F.z, Nt.x, Nt.y, Nt.z};
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      float x = rd[q] * on;
+      x += dpp_shr_t<0x111>(x);
+      x += dpp_shr_t<0x112>(x);
+      x += dpp_shr_t<0x114>(x);
+      x += dpp_shr_t<0x118>(x);
+      if (lane == 15) dtmp().tot[q] = x;
+    }
   }
   __syncthreads();
 }
@@ -215,8 +312,7 @@ LGX_DEV void kinematics(Sh& s, const lgx_model* M, int lane) {
 //   M⁻¹ f = [z ; D⁻¹ f_J − Xᵀ z]  with  z = S⁻¹ (f_B − X f_J)
 //   J M⁻¹ Jᵀ = y_rᵀ S⁻¹ y_s + [leg_r = leg_s] J_r,Jᵀ D_l⁻¹ J_s,J  with  y = J_B − X J_J
 // Lanes:
-//   D1 lanes 0..12  per-link COM wrench (lane 12: the base); the 16 base sums about p0
-//                   (mass, first moment, inertia, wrench) by DPP row reductions
+//   D1 (in kinematics<true>) per-link COM wrench; the 16 base sums about p0 by DPP
 //   D2 lanes 0..11  joint bias h_j and coupling column B_j;  lanes 16..39 leg block D_l
 //   D3 lanes 0..11  D_l⁻¹ (row a), X_j; the 21 Schur sums by DPP; every lane factors S in
 //                   registers (Cholesky); lanes 0..5 write column `lane` of S⁻¹
@@ -227,35 +323,9 @@ struct DynOut {
   float dinv[3];  // lane j < 12: row a of D_l⁻¹
 };
 
-LGX_DEV void dynamics(Sh& s, const lgx_task_params* Pm, int lane, DynOut& o) {
-  const f3 g = ld3(Pm->gravity);
+LGX_DEV void dynamics(Sh& s, int lane, DynOut& o) {
   const f3 p0 = ld3(s.P[0]);
-  float tot[16];
-  {  // ---- D1
-    const int k = lane < NJ ? lane + 1 : 0;
-    const f3 c = ld3(s.C[k]), w = ld3(s.W[k]), al = ld3(s.Al[k]);
-    const f3 rl = c - ld3(s.P[k]);
-    const f3 acc = ld3(s.Ao[k]) + cross(al, rl) + cross(w, cross(w, rl));
-    const float m = s.m[k];
-    const float* Ik = s.I[k];
-    const f3 F = (acc - g) * m;
-    const f3 N = symv(Ik, al) + cross(w, symv(Ik, w));
-    if (lane <= NJ) {
-      st3(s.Fw[k], F);
-      st3(s.Nw[k], N);
-    }
-    const f3 r = c - p0;
-    const float rr = dot(r, r);
-    const f3 Nt = cross(r, F) + N;
-    const float on = lane <= NJ ? 1.f : 0.f;
-    const float rd[16] = {m, m * r.x, m * r.y, m * r.z,
-                          Ik[0] + m * (rr - r.x * r.x), Ik[1] + m * (rr - r.y * r.y), Ik[2] + m * (rr - r.z * r.z),
-                          Ik[3] - m * r.x * r.y, Ik[4] - m * r.x * r.z, Ik[5] - m * r.y * r.z,
-                          F.x, F.y, F.z, Nt.x, Nt.y, Nt.z};
-#pragma unroll
-    for (int q = 0; q < 16; ++q) tot[q] = row0_sum16(rd[q] * on);
-  }
-  __syncthreads();
+  const float* tot = dtmp().tot;
   const int j = lane < NJ ? lane : NJ - 1, l = j / 3, a = j % 3;
   if (lane < NJ) {  // ---- D2a: joint j (leg l, chain position a)
     const int kj = 1 + j;
@@ -268,7 +338,7 @@ LGX_DEV void dynamics(Sh& s, const lgx_task_params* Pm, int lane, DynOut& o) {
       const f3 c = ld3(s.C[k]);
       const f3 d = c - pj;
       const float m = s.m[k];
-      acc = acc + cross(d, ld3(s.Fw[k])) + ld3(s.Nw[k]);
+      acc = acc + cross(d, ld3(dtmp().Fw[k])) + ld3(dtmp().Nw[k]);
       hl = hl + d * m;
       bang = bang + cross(c - p0, cross(ax, d)) * m + symv(s.I[k], ax);
     }
@@ -290,12 +360,12 @@ LGX_DEV void dynamics(Sh& s, const lgx_task_params* Pm, int lane, DynOut& o) {
       const f3 c = ld3(s.C[k]);
       acc += s.m[k] * dot(cross(a1, c - p1), cross(a2, c - p2)) + dot(a1, symv(s.I[k], a2));
     }
-    s.Dl[lq][e] = acc;
+    dtmp().Dl[lq][e] = acc;
   }
   __syncthreads();
   // ---- D3
   float Di[6];
-  sym3_inv(s.Dl[l], Di);
+  sym3_inv(dtmp().Dl[l], Di);
 #pragma unroll
   for (int c = 0; c < 3; ++c) o.dinv[c] = sym3(Di, a, c);
   if (lane < NJ && a == 0) {
@@ -547,8 +617,13 @@ LGX_DEV float sea_torque(const lgx_task_params* Pm, const lgx_buffers& B, int e,
 
 // one physics substep (legged_robot.py:80-85 loop body)
 template <bool TERRAIN, bool ACTNET>
-LGX_DEV void substep(Sh& s, const lgx_model* M, const lgx_task_params* Pm, const lgx_buffers& B, int lane,
+LGX_DEV void substep(Sh& s, const lgx_model* M_, const lgx_task_params* Pm_, const lgx_buffers& B, int lane,
                      bool last) {
+  // The model and task tables are re-read each substep (L1 / scalar-cache hits) rather than
+  // hoisted out of the decimation loop, where ~40 lane-indexed constants would otherwise stay
+  // live in VGPRs across the whole step.
+  const lgx_model* M = opaque(M_);
+  const lgx_task_params* Pm = opaque(Pm_);
   const float dt = Pm->sim_dt;
   // ---- PD torques: LeggedRobot._compute_torques legged_robot.py:440-478
   {
@@ -576,13 +651,13 @@ LGX_DEV void substep(Sh& s, const lgx_model* M, const lgx_task_params* Pm, const
     }
   }
   PH(1);
-  kinematics(s, M, lane);
+  kinematics<true>(s, M, Pm, lane);
   PH(2);
 #if defined(LGX_DBG_STAGE) && LGX_DBG_STAGE == 1
   return;
 #endif
   DynOut dy;
-  dynamics(s, Pm, lane, dy);
+  dynamics(s, lane, dy);
   const int jl_ = lane < NJ ? lane : NJ - 1, leg_ = jl_ / 3, pos_ = jl_ % 3;  // joint lanes' leg / chain position
   // ---- free velocity u* = u + dt M⁻¹ f, f = [−h_B ; τ − h_J] (factored form, see dynamics)
   const float fj = lane < NJ ? s.tau[lane] - dy.hj : 0.f;
@@ -657,9 +732,9 @@ LGX_DEV void substep(Sh& s, const lgx_model* M, const lgx_task_params* Pm, const
     else tv = d / dt;
     return tv;
   };
-  float* const J9 = s.arena;                  // [nrows][RW]: J_B (6) | J of leg rleg (3)
-  float* const ZG = s.arena + MAXR * RW;      // [nrows][RW]: z_r (6) | g_r (3)
-  float* const Am = s.arena + 2 * MAXR * RW;  // [nrows][nrows] (A path)
+  float* const ZG = lgx_dyn;                // [nrows][RW]: z_r (6) | g_r (3)
+  float* const J9 = lgx_dyn + MAXR * RW;    // [nrows][RW]: J_B (6) | J of leg rleg (3)
+  float* const Am = J9;                     // packed lower A (A path, after J9 is consumed)
   if (lim_lo || lim_hi) {
     const int r = __popcll(lmask & below);
     float* jr = J9 + r * RW;
@@ -757,57 +832,66 @@ LGX_DEV void substep(Sh& s, const lgx_model* M, const lgx_task_params* Pm, const
   return;
 #endif
   if (nrows <= AMAX) {
-    // ---- A = J M⁻¹ Jᵀ: lane r writes column r (A is symmetric: entry (s, r) = y_r·z_s +
-    //      [leg_r = leg_s] J_l,r·g_s)
+    // ---- A = J M⁻¹ Jᵀ, packed lower: lane r writes column r from row r down (entry (q, r) =
+    //      y_r·z_q + [leg_r = leg_q] J_l,r·g_q; J_l,r = 0 for rows without a leg part)
     if (row_lane) {
-#pragma unroll 2
+#pragma unroll 4
       for (int q = 0; q < nrows; ++q) {
         const float* zg = ZG + q * RW;
-        float v = yr[0] * zg[0] + yr[1] * zg[1] + yr[2] * zg[2] + yr[3] * zg[3] + yr[4] * zg[4] + yr[5] * zg[5];
-        if (lr >= 0 && s.rleg[q] == lr) v += jlr[0] * zg[6] + jlr[1] * zg[7] + jlr[2] * zg[8];
-        Am[q * nrows + lane] = v;
+        const float v = yr[0] * zg[0] + yr[1] * zg[1] + yr[2] * zg[2] + yr[3] * zg[3] + yr[4] * zg[4] + yr[5] * zg[5];
+        const float vl = jlr[0] * zg[6] + jlr[1] * zg[7] + jlr[2] * zg[8];
+        if (q >= lane) Am[pk_lo(q, lane)] = v + (s.rleg[q] == lr ? vl : 0.f);
       }
     }
     __syncthreads();
     PH(7);
-    // ---- projected Gauss-Seidel on A (oracle_physics.c step 4): lane r keeps the row
-    //      velocity w_r = J_r u and lambda_r; a row update is one readlane + scalar
-    //      projection + one FMA per lane with row r of A (no cross-lane reductions)
+    // ---- projected Gauss-Seidel on A (oracle_physics.c step 4). Rows are [nlim joint
+    //      limits | ncon × (normal, tangent, tangent)]. Lane r keeps the row velocity
+    //      w_r = J_r u and λ_r; a row update is readlanes + a scalar projection + one FMA
+    //      per lane with column `lane` of A row r. A contact's three A rows are loaded
+    //      one contact ahead.
     float w = w0, lam = 0.f;
     const float mu = s.mu;
     auto rd = [](float v, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); };
     // per-row constants live in their row's lane (readlane, no LDS round trip in the sweep)
     const float tg = row_lane ? s.tgt[lane] : 0.f;
     const float ia = row_lane ? 1.0f / s.Arr[lane] : 0.f;
-    const uint64_t pairs = __ballot(row_lane && s.rkind[lane] == 1);  // first row of each tangent pair
+    const int rlast = nrows - 3;  // first row of the last contact
+    const int lc = min(lane, nrows - 1);  // lanes past the rows read a valid (unused) entry
+    auto arow = [&](int r) { return Am[lc <= r ? pk_lo(r, lc) : pk_lo(lc, r)]; };  // A[r][lane]
     for (int it = 0; it < Pm->solver_iterations; ++it) {
-      for (int r = 0; r < nrows;) {
-        const bool pair = (pairs >> r) & 1ull;
-        const float a0 = row_lane ? Am[r * nrows + lane] : 0.f;
-        const float a1 = (pair && row_lane) ? Am[(r + 1) * nrows + lane] : 0.f;
-        if (!pair) {
-          const float wr = rd(w, r), lo = rd(lam, r);
-          const float ln = fmaxf(0.f, lo + (rd(tg, r) - wr) * rd(ia, r));
-          const float d = ln - lo;
-          if (lane == r) lam = ln;
-          w += a0 * d;
-          r += 1;
-        } else {
-          const float w1 = rd(w, r), w2 = rd(w, r + 1);
-          const float o1 = rd(lam, r), o2 = rd(lam, r + 1);
-          float l1 = o1 - w1 * rd(ia, r);
-          float l2 = o2 - w2 * rd(ia, r + 1);
-          const float lim = mu * rd(lam, r - 1);
-          const float n = sqrtf(l1 * l1 + l2 * l2);
-          if (n > lim) {
-            const float sc = n > 0.f ? lim / n : 0.f;
-            l1 *= sc; l2 *= sc;
-          }
-          if (lane == r) lam = l1;
-          if (lane == r + 1) lam = l2;
-          w += a0 * (l1 - o1) + a1 * (l2 - o2);
-          r += 2;
-        }
+      for (int r = 0; r < nlim; ++r) {
+        const float a0 = arow(r);
+        const float wr = rd(w, r), lo = rd(lam, r);
+        const float ln = fmaxf(0.f, lo + (rd(tg, r) - wr) * rd(ia, r));
+        if (lane == r) lam = ln;
+        w += a0 * (ln - lo);
+      }
+      if (ncon == 0) continue;
+      float n0 = arow(nlim), n1 = arow(nlim + 1), n2 = arow(nlim + 2);
+      for (int r = nlim; r < nrows; r += 3) {
+        const float a0 = n0, a1 = n1, a2 = n2;
+        const int rn = min(r + 3, rlast);
+        n0 = arow(rn);
+        n1 = arow(rn + 1);
+        n2 = arow(rn + 2);
+        // normal row
+        const float wr = rd(w, r), lo = rd(lam, r);
+        const float ln = fmaxf(0.f, lo + (rd(tg, r) - wr) * rd(ia, r));
+        if (lane == r) lam = ln;
+        w += a0 * (ln - lo);
+        // tangent pair, projected onto the friction disk |λ_t| <= μ λ_n
+        const float lim = mu * ln;
+        const float o1 = rd(lam, r + 1), o2 = rd(lam, r + 2);
+        float l1 = o1 - rd(w, r + 1) * rd(ia, r + 1);
+        float l2 = o2 - rd(w, r + 2) * rd(ia, r + 2);
+        const float nn = l1 * l1 + l2 * l2;
+        const float sc = nn > lim * lim ? lim * __builtin_amdgcn_rsqf(nn) : 1.0f;
+        l1 *= sc;
+        l2 *= sc;
+        if (lane == r + 1) lam = l1;
+        if (lane == r + 2) lam = l2;
+        w += a1 * (l1 - o1) + a2 * (l2 - o2);
       }
     }
     if (row_lane) s.lam[lane] = lam;
@@ -816,13 +900,14 @@ LGX_DEV void substep(Sh& s, const lgx_model* M, const lgx_task_params* Pm, const
     // ---- u+ = u* + M⁻¹ Jᵀ λ = u* + [Z ; G_J − Xᵀ Z]:  Z = Σ_r λ_r z_r,
     //      G_j = Σ_{r on leg(j)} λ_r g_r[pos(j)]
     float Z[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, G = 0.f;
-#pragma unroll 2
+#pragma unroll 4
     for (int r = 0; r < nrows; ++r) {
       const float lr_ = s.lam[r];
       const float* zg = ZG + r * RW;
 #pragma unroll
       for (int q = 0; q < 6; ++q) Z[q] += lr_ * zg[q];
-      if (s.rleg[r] == leg_) G += lr_ * zg[6 + pos_];
+      const float gq = pos_ == 0 ? zg[6] : (pos_ == 1 ? zg[7] : zg[8]);
+      G += s.rleg[r] == leg_ ? lr_ * gq : 0.f;
     }
     if (lane < 6) {
       float zl = 0.f;
@@ -831,9 +916,10 @@ LGX_DEV void substep(Sh& s, const lgx_model* M, const lgx_task_params* Pm, const
       s.up[lane] = s.us[lane] + zl;
     }
     if (lane < NJ) {
+      const float* Xj = s.X[lane];
       float v = s.us[6 + lane] + G;
 #pragma unroll
-      for (int q = 0; q < 6; ++q) v -= dy.xj[q] * Z[q];
+      for (int q = 0; q < 6; ++q) v -= Xj[q] * Z[q];
       s.up[6 + lane] = v;
     }
     __syncthreads();
@@ -851,8 +937,9 @@ LGX_DEV void substep(Sh& s, const lgx_model* M, const lgx_task_params* Pm, const
       const float* zg = ZG + r * RW;
       if (lane < NJ) {
         float v = s.rleg[r] == leg_ ? zg[6 + pos_] : 0.f;
+        const float* Xj = s.X[lane];
 #pragma unroll
-        for (int q = 0; q < 6; ++q) v -= dy.xj[q] * zg[q];
+        for (int q = 0; q < 6; ++q) v -= Xj[q] * zg[q];
         return v;
       }
       return lane < NU ? zg[bi] : 0.f;
@@ -1024,7 +1111,7 @@ LGX_DEV void resample_commands(const lgx_task_params* Pm, float* cmd, const floa
 LGX_DEV void reset_env(const lgx_task_params* Pm, const lgx_buffers& B, Sh& s, int e, int lane, bool after_init,
                        bool zero_carried) {
   const int D = Pm->num_dof;
-  const float* U = s.U;
+  const float* U = stg_U();
   if (lane == 0) {
     float* root = s.root;
     float* cmd = s.cmd;
@@ -1100,8 +1187,9 @@ LGX_DEV void fill_uniforms(Sh& s, uint64_t seed, uint32_t gid, uint64_t step, ui
     uint32_t o[4];
     philox4x32_10(gid, (uint32_t)step, (uint32_t)b | (stream << 16), (uint32_t)(step >> 32), (uint32_t)seed,
                   (uint32_t)(seed >> 32), o);
-    s.U[4 * b + 0] = u01(o[0]); s.U[4 * b + 1] = u01(o[1]);
-    s.U[4 * b + 2] = u01(o[2]); s.U[4 * b + 3] = u01(o[3]);
+    float* U = stg_U();
+    U[4 * b + 0] = u01(o[0]); U[4 * b + 1] = u01(o[1]);
+    U[4 * b + 2] = u01(o[2]); U[4 * b + 3] = u01(o[3]);
   }
   __syncthreads();
 }
@@ -1128,7 +1216,8 @@ LGX_DEV float reward_term(const lgx_task_params* Pm, const lgx_buffers& B, Sh& s
     case LGX_REW_ANG_VEL_XY: return sq(x.bav[0]) + sq(x.bav[1]);
     case LGX_REW_BASE_HEIGHT: {
       float acc = 0.0f;
-      for (int i = 0; i < Pm->num_height_points; ++i) acc += root[2] - s.heights[i];
+      const float* hts = stg_heights(Pm);
+      for (int i = 0; i < Pm->num_height_points; ++i) acc += root[2] - hts[i];
       return sq(acc / (float)Pm->num_height_points - Pm->base_height_target);
     }
     case LGX_REW_CALF_COLLISION:
@@ -1295,7 +1384,7 @@ LGX_DEV void get_heights(const lgx_task_params* Pm, const lgx_buffers& B, Sh& s,
   const int NP = Pm->num_height_points;
   const float* root = s.root;
   if (Pm->mesh_type == LGX_MESH_PLANE || B.height_samples == nullptr) {
-    for (int i = lane; i < NP; i += 64) s.heights[i] = 0.0f;
+    for (int i = lane; i < NP; i += 64) stg_heights(Pm)[i] = 0.0f;
     return;
   }
   float qz = root[5], qw = root[6];
@@ -1314,20 +1403,22 @@ LGX_DEV void get_heights(const lgx_task_params* Pm, const lgx_buffers& B, Sh& s,
     int16_t h3 = B.height_samples[ix * Pm->hf_cols + iy + 1];
     int16_t h = h1 < h2 ? h1 : h2;
     h = h < h3 ? h : h3;
-    s.heights[i] = (float)h * Pm->vertical_scale;
+    stg_heights(Pm)[i] = (float)h * Pm->vertical_scale;
   }
 }
 
 // ============================================================== kernels
 #ifndef LGX_WAVES_PER_EU
-#define LGX_WAVES_PER_EU 1
+#define LGX_WAVES_PER_EU 4
 #endif
 template <bool PHYSICS, bool TERRAIN, bool ACTNET>
 __global__ __launch_bounds__(64, LGX_WAVES_PER_EU) void env_step_kernel(const lgx_model* __restrict__ M,
-                                                      const lgx_task_params* __restrict__ Pm, lgx_buffers B,
-                                                      uint64_t seed, uint64_t step_arg,
-                                                      const uint64_t* __restrict__ step_dev) {
+                                                      const lgx_task_params* __restrict__ Pm,
+                                                      const lgx_buffers* __restrict__ Bp, uint64_t seed,
+                                                      uint64_t step_arg, const uint64_t* __restrict__ step_dev) {
   __shared__ Sh s;
+  // buffer pointers are read from device memory (scalar loads) when used, not held in SGPRs
+  const lgx_buffers& B = *Bp;
   // graph-replayable form: the step counter is read from device memory (lgx_step_dev)
   const uint64_t step = step_dev ? *step_dev : step_arg;
   const int e = blockIdx.x;
@@ -1350,7 +1441,7 @@ __global__ __launch_bounds__(64, LGX_WAVES_PER_EU) void env_step_kernel(const lg
     s.kdm[lane] = B.kp_kd ? B.kp_kd[((size_t)Pm->num_envs + e) * D + lane] : 1.f;
     s.ldv[lane] = B.last_dof_vel[(size_t)e * D + lane];
   }
-  if (lane < 13) s.hist[lane] = root_g[lane];  // staging
+  if (lane < 13) s.root[lane] = root_g[lane];
   if (lane == 0) {
     s.madd = B.mass_params ? B.mass_params[e * 4] : 0.f;
     s.mu = 0.5f * ((B.friction ? B.friction[e] : 1.f) + Pm->ground_friction);
@@ -1364,21 +1455,21 @@ __global__ __launch_bounds__(64, LGX_WAVES_PER_EU) void env_step_kernel(const lg
 
   if (PHYSICS) {
     if (lane == 0) {
-      float q[4] = {s.hist[3], s.hist[4], s.hist[5], s.hist[6]};
+      float q[4] = {s.root[3], s.root[4], s.root[5], s.root[6]};
       float n = rsqrtf(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
       for (int i = 0; i < 4; ++i) s.qb[i] = q[i] * n;
-      for (int i = 0; i < 3; ++i) { s.pb[i] = s.hist[i]; s.wb[i] = s.hist[10 + i]; }
+      for (int i = 0; i < 3; ++i) { s.pb[i] = s.root[i]; s.wb[i] = s.root[10 + i]; }
       float R[9];
       quat_to_R(s.qb, R);
       f3 rc = mv(R, mk(M->link_com[0][0] + s.cadd[0], M->link_com[0][1] + s.cadd[1], M->link_com[0][2] + s.cadd[2]));
-      f3 vo = ld3(s.hist + 7) - cross(ld3(s.wb), rc);  // COM velocity -> origin velocity
+      f3 vo = ld3(s.root + 7) - cross(ld3(s.wb), rc);  // COM velocity -> origin velocity
       st3(s.vo, vo);
     }
     __syncthreads();
     PH(0);
     for (int sub = 0; sub < Pm->decimation; ++sub) substep<TERRAIN, ACTNET>(s, M, Pm, B, lane, sub == Pm->decimation - 1);
     // final kinematics for the rigid-body state tensor
-    kinematics(s, M, lane);
+    kinematics<false>(s, M, Pm, lane);
     float root[13];
     {
       float R[9];
@@ -1391,7 +1482,7 @@ __global__ __launch_bounds__(64, LGX_WAVES_PER_EU) void env_step_kernel(const lg
       root[10] = s.wb[0]; root[11] = s.wb[1]; root[12] = s.wb[2];
     }
     __syncthreads();
-    if (lane < 13) s.hist[lane] = root[lane];
+    if (lane < 13) s.root[lane] = root[lane];
     // rigid body states, contact forces, torques -> HBM
     if (lane < NB) {
       const int k = M->body_link[lane];
@@ -1454,7 +1545,6 @@ __global__ __launch_bounds__(64, LGX_WAVES_PER_EU) void env_step_kernel(const lg
     Scratch& x = s.x;
     float* root = s.root;
     float* cmd = s.cmd;
-    for (int i = 0; i < 13; ++i) root[i] = s.hist[i];
     for (int i = 0; i < 4; ++i) cmd[i] = B.commands[e * 4 + i];
     const long long ep = B.episode_length[e] + 1;
     s.ep = ep;
@@ -1489,7 +1579,7 @@ __global__ __launch_bounds__(64, LGX_WAVES_PER_EU) void env_step_kernel(const lg
       x.yaw = atan2f(2.0f * (qw * qz + qx * qy), 1.0f - 2.0f * (qy * qy + qz * qz));
     }
     // _post_physics_step_callback go2.py:390-410
-    if (ep % Pm->resample_interval == 0) resample_commands(Pm, cmd, s.U, S_CMD, root + 3);
+    if (ep % Pm->resample_interval == 0) resample_commands(Pm, cmd, stg_U(), S_CMD, root + 3);
     if (Pm->heading_command) {
       const float fwd[3] = {1.f, 0.f, 0.f};
       float f[3];
@@ -1499,8 +1589,8 @@ __global__ __launch_bounds__(64, LGX_WAVES_PER_EU) void env_step_kernel(const lg
       cmd[2] = clipf(wrap_to_pi(cmd[3] - heading) * gain, -1.0f, 1.0f);
     }
     if (Pm->push_robots && (step % (uint64_t)Pm->push_interval == 0)) {
-      root[7] = rand_range(-Pm->max_push_vel_xy, Pm->max_push_vel_xy, s.U[S_PUSH + 0]);
-      root[8] = rand_range(-Pm->max_push_vel_xy, Pm->max_push_vel_xy, s.U[S_PUSH + 1]);
+      root[7] = rand_range(-Pm->max_push_vel_xy, Pm->max_push_vel_xy, stg_U()[S_PUSH + 0]);
+      root[8] = rand_range(-Pm->max_push_vel_xy, Pm->max_push_vel_xy, stg_U()[S_PUSH + 1]);
     }
     // check_termination go2.py:186-204
     int reset = 0;
@@ -1551,7 +1641,7 @@ __global__ __launch_bounds__(64, LGX_WAVES_PER_EU) void env_step_kernel(const lg
   const Scratch& x = s.x;
   if (go2 && Pm->parkour && lane == 0) {
     int outl = 0;
-    for (int i = 0; i < Pm->num_height_points; ++i) outl += fabsf(s.heights[i]) > 0.1f;
+    for (int i = 0; i < Pm->num_height_points; ++i) outl += fabsf(stg_heights(Pm)[i]) > 0.1f;
     s.x.jump = (float)(outl >= 8);
   }
   for (int i = lane; i < Pp; i += 64) {
@@ -1578,25 +1668,27 @@ __global__ __launch_bounds__(64, LGX_WAVES_PER_EU) void env_step_kernel(const lg
       else if (i < 12 + D) v = (s.th[i - 12] - Pm->default_dof_pos[i - 12]) * Pm->obs_scale_dof_pos;
       else if (i < 12 + 2 * D) v = s.thd[i - 12 - D] * Pm->obs_scale_dof_vel;
       else if (i < 12 + 2 * D + A) v = s.act[i - 12 - 2 * D];
-      else v = clipf(s.root[2] - 0.5f - s.heights[i - (12 + 2 * D + A)], -1.0f, 1.0f) * Pm->obs_scale_height;
+      else v = clipf(s.root[2] - 0.5f - stg_heights(Pm)[i - (12 + 2 * D + A)], -1.0f, 1.0f) * Pm->obs_scale_height;
     }
-    if (Pm->add_noise) v = v + (2.0f * s.U[S_NOISE + i] - 1.0f) * Pm->noise_vec[i];
-    s.cur[i] = v;
+    if (Pm->add_noise) v = v + (2.0f * stg_U()[S_NOISE + i] - 1.0f) * Pm->noise_vec[i];
+    stg_cur(Pm)[i] = v;
   }
   // stage the old history (obs[0:H*P]) in LDS; a reset env's history was zeroed (go2.py:238)
   float* hist_g = B.obs_history + (size_t)e * H * Pp;
-  for (int i = lane; i < H * Pp; i += 64) s.hist[16 + i] = reset ? 0.f : hist_g[i];
+  float* const hist = stg_hist(Pm);
+  const float* const cur = stg_cur(Pm);
+  for (int i = lane; i < H * Pp; i += 64) hist[i] = reset ? 0.f : hist_g[i];
   __syncthreads();
   const float co = Pm->clip_obs;
   float* obs = B.obs + (size_t)e * Pm->num_obs;
   float* cr = B.critic ? B.critic + (size_t)e * Pm->num_critic : nullptr;
   for (int i = lane; i < H * Pp; i += 64) {
-    float v = clipf(s.hist[16 + i], -co, co);
+    float v = clipf(hist[i], -co, co);
     obs[i] = v;
     if (go2 && cr) cr[i] = v;
   }
   for (int i = lane; i < Pp; i += 64) {
-    float v = clipf(s.cur[i], -co, co);
+    float v = clipf(cur[i], -co, co);
     obs[H * Pp + i] = v;
     if (go2 && cr) cr[H * Pp + i] = v;
   }
@@ -1619,7 +1711,7 @@ __global__ __launch_bounds__(64, LGX_WAVES_PER_EU) void env_step_kernel(const lg
       if (cr) cr[NO + Pm->num_priv + lane] = v;
     }
     for (int i = lane; i < Pm->num_scan; i += 64) {
-      float v = clipf(s.root[2] - 0.3f - s.heights[i], -1.0f, 1.0f);
+      float v = clipf(s.root[2] - 0.3f - stg_heights(Pm)[i], -1.0f, 1.0f);
       B.scan[(size_t)e * Pm->num_scan + i] = v;
       if (cr) cr[NO + Pm->num_priv + 3 + i] = clipf(v, -co, co);
     }
@@ -1627,7 +1719,7 @@ __global__ __launch_bounds__(64, LGX_WAVES_PER_EU) void env_step_kernel(const lg
   // history update go2.py:570-574
   const long long ep = s.ep;
   for (int i = lane; i < H * Pp; i += 64) {
-    float v = (ep <= 1) ? s.cur[i % Pp] : (i < (H - 1) * Pp ? s.hist[16 + i + Pp] : s.cur[i - (H - 1) * Pp]);
+    float v = (ep <= 1) ? cur[i % Pp] : (i < (H - 1) * Pp ? hist[i + Pp] : cur[i - (H - 1) * Pp]);
     hist_g[i] = v;
   }
   // last_* copies go2.py:380-384 and state write-back
@@ -1658,7 +1750,7 @@ __global__ __launch_bounds__(64, LGX_WAVES_PER_EU) void env_step_kernel(const lg
     B.rpy_phase[e * 8 + lane] = v;
   }
   if (B.measured_heights)
-    for (int i = lane; i < Pm->num_height_points; i += 64) B.measured_heights[(size_t)e * Pm->num_height_points + i] = s.heights[i];
+    for (int i = lane; i < Pm->num_height_points; i += 64) B.measured_heights[(size_t)e * Pm->num_height_points + i] = stg_heights(Pm)[i];
 #ifdef LGX_PHASE_CLOCK
   __syncthreads();
   PH(15);
@@ -1668,9 +1760,11 @@ __global__ __launch_bounds__(64, LGX_WAVES_PER_EU) void env_step_kernel(const lg
 }
 
 // BaseTask.reset -> reset_idx(env_ids) outside a step (RNG stream 1)
-__global__ __launch_bounds__(64) void reset_kernel(const lgx_task_params* __restrict__ Pm, lgx_buffers B,
+__global__ __launch_bounds__(64) void reset_kernel(const lgx_task_params* __restrict__ Pm,
+                                                   const lgx_buffers* __restrict__ Bp,
                                                    const uint8_t* __restrict__ mask, uint64_t seed, uint64_t call) {
   __shared__ Sh s;
+  const lgx_buffers& B = *Bp;
   const int e = blockIdx.x;
   const int lane = threadIdx.x;
   if (!mask[e]) return;
@@ -1702,6 +1796,7 @@ struct lgx_env {
   lgx_buffers buffers;
   lgx_model* d_model = nullptr;
   lgx_task_params* d_params = nullptr;
+  lgx_buffers* d_buffers = nullptr;  // device copy of `buffers` (kernels read pointers from it)
   int device = 0;
   bool bound = false;
   bool stats_clean = false;  // episode_stats zeroed by lgx_episode_extras and not written since
@@ -1745,13 +1840,14 @@ int lgx_create(const lgx_model* model, const lgx_task_params* params, int32_t de
     }
   if (model->num_candidates > LGX_MAX_CANDIDATES || model->num_bodies > LGX_MAX_BODIES)
     return fail(env, "too many contact candidates or bodies");
-  if (params->history_len * params->num_proprio > lgx::MAXHIST - 16) return fail(env, "history too long");
+  if (params->history_len * params->num_proprio > lgx::MAXHIST) return fail(env, "history too long");
   if (params->num_proprio > LGX_MAX_PROPRIO || params->num_height_points > LGX_MAX_HEIGHT_POINTS)
     return fail(env, "observation too large");
   if (params->num_reward_terms + 1 > 64) return fail(env, "too many reward terms");
   HIP_OK(hipSetDevice(device));
   HIP_OK(hipMalloc(&env->d_model, sizeof(lgx_model)));
   HIP_OK(hipMalloc(&env->d_params, sizeof(lgx_task_params)));
+  HIP_OK(hipMalloc(&env->d_buffers, sizeof(lgx_buffers)));
   HIP_OK(hipMemcpy(env->d_model, model, sizeof(lgx_model), hipMemcpyHostToDevice));
   HIP_OK(hipMemcpy(env->d_params, params, sizeof(lgx_task_params), hipMemcpyHostToDevice));
   return 0;
@@ -1787,6 +1883,8 @@ int lgx_bind(lgx_env* env, const lgx_buffers* b) {
   if (env->params.curriculum && (!b->terrain_levels || !b->terrain_types || !b->terrain_origins))
     return fail(env, "lgx_bind: terrain curriculum needs terrain_levels/terrain_types/terrain_origins");
   env->buffers = *b;
+  HIP_OK(hipSetDevice(env->device));
+  HIP_OK(hipMemcpy(env->d_buffers, b, sizeof(lgx_buffers), hipMemcpyHostToDevice));
   env->bound = true;
   env->stats_clean = false;
   return 0;
@@ -1807,7 +1905,8 @@ static int launch_step(lgx_env* env, uint64_t seed, uint64_t step, const uint64_
   auto kern = !physics ? lgx::env_step_kernel<false, false, false>
               : actnet ? (terrain ? lgx::env_step_kernel<true, true, true> : lgx::env_step_kernel<true, false, true>)
                        : (terrain ? lgx::env_step_kernel<true, true, false> : lgx::env_step_kernel<true, false, false>);
-  hipLaunchKernelGGL(kern, dim3(N), dim3(64), 0, st, env->d_model, env->d_params, env->buffers, seed, step,
+  const size_t dyn = sizeof(float) * (size_t)lgx::arena_floats(env->params);
+  hipLaunchKernelGGL(kern, dim3(N), dim3(64), dyn, st, env->d_model, env->d_params, env->d_buffers, seed, step,
                      step_dev);
   HIP_OK(hipGetLastError());
   return 0;
@@ -1840,8 +1939,9 @@ int lgx_reset_envs(lgx_env* env, const uint8_t* env_mask, uint64_t seed, uint64_
   if (env->buffers.episode_stats && !env->stats_clean)
     HIP_OK(hipMemsetAsync(env->buffers.episode_stats, 0, sizeof(float) * (KS + 1), st));
   env->stats_clean = false;
-  hipLaunchKernelGGL(lgx::reset_kernel, dim3(env->params.num_envs), dim3(64), 0, st, env->d_params, env->buffers,
-                     env_mask, seed, reset_call);
+  const size_t dyn = sizeof(float) * (size_t)lgx::arena_floats(env->params);
+  hipLaunchKernelGGL(lgx::reset_kernel, dim3(env->params.num_envs), dim3(64), dyn, st, env->d_params,
+                     env->d_buffers, env_mask, seed, reset_call);
   HIP_OK(hipGetLastError());
   return 0;
 }
@@ -1924,6 +2024,7 @@ void lgx_destroy(lgx_env* env) {
   if (!env) return;
   if (env->d_model) (void)hipFree(env->d_model);
   if (env->d_params) (void)hipFree(env->d_params);
+  if (env->d_buffers) (void)hipFree(env->d_buffers);
   delete env;
 }
 
