@@ -139,6 +139,11 @@ LGX_DEV const T* opaque(const T* p) {
   return p;
 }
 
+LGX_DEV int opaque_lane(int v) {
+  __asm__ volatile("" : "+v"(v));
+  return v;
+}
+
 // symmetric 3x3 (xx yy zz xy xz yz) inverse
 LGX_DEV void sym3_inv(const float* D, float* O) {
   float a = D[0], b = D[1], c = D[2], d = D[3], e = D[4], f = D[5];
@@ -567,8 +572,10 @@ template <int NIN>
 LGX_DEV void sea_lstm_layer(const float* __restrict__ w_ih, const float* __restrict__ w_hh,
                             const float* __restrict__ b_ih, const float* __restrict__ b_hh, const float* x, float* h,
                             float* c) {
+  // one hidden unit per iteration (not unrolled: only that unit's 4 gate rows of weights are
+  // live); c[u] / hn[u] are picked and placed by selects so the arrays stay in registers
   float hn[8];
-#pragma unroll
+#pragma unroll 1
   for (int u = 0; u < 8; ++u) {
     float g4[4];
 #pragma unroll
@@ -582,8 +589,16 @@ LGX_DEV void sea_lstm_layer(const float* __restrict__ w_ih, const float* __restr
       g4[q] = (a + b_ih[g]) + (b + b_hh[g]);
     }
     const float ig = sigmoidf_(g4[0]), fg = sigmoidf_(g4[1]), gg = tanhf(g4[2]), og = sigmoidf_(g4[3]);
-    c[u] = fg * c[u] + ig * gg;
-    hn[u] = og * tanhf(c[u]);
+    float cu = 0.f;
+#pragma unroll
+    for (int v = 0; v < 8; ++v) cu = v == u ? c[v] : cu;
+    cu = fg * cu + ig * gg;
+    const float hu = og * tanhf(cu);
+#pragma unroll
+    for (int v = 0; v < 8; ++v) {
+      c[v] = v == u ? cu : c[v];
+      hn[v] = v == u ? hu : hn[v];
+    }
   }
 #pragma unroll
   for (int u = 0; u < 8; ++u) h[u] = hn[u];
@@ -617,13 +632,15 @@ LGX_DEV float sea_torque(const lgx_task_params* Pm, const lgx_buffers& B, int e,
 
 // one physics substep (legged_robot.py:80-85 loop body)
 template <bool TERRAIN, bool ACTNET>
-LGX_DEV void substep(Sh& s, const lgx_model* M_, const lgx_task_params* Pm_, const lgx_buffers& B, int lane,
+LGX_DEV void substep(Sh& s, const lgx_model* M_, const lgx_task_params* Pm_, const lgx_buffers& B, int lane_,
                      bool last) {
   // The model and task tables are re-read each substep (L1 / scalar-cache hits) rather than
   // hoisted out of the decimation loop, where ~40 lane-indexed constants would otherwise stay
-  // live in VGPRs across the whole step.
+  // live in VGPRs across the whole step. Likewise the lane index, so that per-lane index and
+  // LDS-address arithmetic is recomputed each substep instead of being hoisted and spilled.
   const lgx_model* M = opaque(M_);
   const lgx_task_params* Pm = opaque(Pm_);
+  const int lane = opaque_lane(lane_);
   const float dt = Pm->sim_dt;
   // ---- PD torques: LeggedRobot._compute_torques legged_robot.py:440-478
   {
@@ -1408,11 +1425,14 @@ LGX_DEV void get_heights(const lgx_task_params* Pm, const lgx_buffers& B, Sh& s,
 }
 
 // ============================================================== kernels
-#ifndef LGX_WAVES_PER_EU
-#define LGX_WAVES_PER_EU 4
+// Occupancy target: 4 waves per SIMD (<= 128 VGPRs; the Go2 LDS image is 9.6 KB, so 4096
+// envs are one residency round on 256 CUs). The SEA-LSTM variant keeps its hidden states in
+// registers (fewer waves per SIMD; ANYmal's LDS image is 13 KB).
+#ifndef LGX_SEA_WAVES
+#define LGX_SEA_WAVES 2
 #endif
 template <bool PHYSICS, bool TERRAIN, bool ACTNET>
-__global__ __launch_bounds__(64, LGX_WAVES_PER_EU) void env_step_kernel(const lgx_model* __restrict__ M,
+__global__ __launch_bounds__(64, ACTNET ? LGX_SEA_WAVES : 4) void env_step_kernel(const lgx_model* __restrict__ M,
                                                       const lgx_task_params* __restrict__ Pm,
                                                       const lgx_buffers* __restrict__ Bp, uint64_t seed,
                                                       uint64_t step_arg, const uint64_t* __restrict__ step_dev) {
