@@ -166,22 +166,26 @@ class LeggedRobot(BaseTask):
             list(self.cfg.init_state.ang_vel)
         self.base_init_state = torch.tensor(base, dtype=torch.float, device=self.device)
         self._get_env_origins()
-        n = self.num_envs
+        # Setup-time randomisation is drawn for ALL global envs (the single-GPU draw order)
+        # and this shard's slice kept, so env k gets the same friction / mass / gains on any
+        # number of ranks.
+        n, total = self.num_envs, self.num_envs_total
+        sl = slice(self.env_id_offset, self.env_id_offset + n)
         dr = self.cfg.domain_rand
         # _process_rigid_shape_props legged_robot.py:318-329 (64 friction buckets, CPU RNG)
         if dr.randomize_friction:
-            bucket_ids = torch.randint(0, 64, (n, 1))
+            bucket_ids = torch.randint(0, 64, (total, 1))
             lo, hi = dr.friction_range
             buckets = (hi - lo) * torch.rand(64, 1) + lo
-            self.friction_coeffs = buckets[bucket_ids]
-        mass = np.zeros((n, 4), dtype=np.float32)
-        for i in range(n):
+            self.friction_coeffs = buckets[bucket_ids][sl]
+        mass = np.zeros((total, 4), dtype=np.float32)
+        for i in range(total):
             torch.rand(2, 1)  # start-pose xy jitter draw (legged_robot.py:867), kept for RNG order
             if dr.randomize_base_mass:
                 mass[i, 0] = np.random.uniform(dr.added_mass_range[0], dr.added_mass_range[1], size=(1,))[0]
             if getattr(dr, "randomize_center_of_mass", False):
                 mass[i, 1:4] = np.random.uniform(dr.added_com_range[0], dr.added_com_range[1], size=(3,))
-        self.privileged_mass_params = torch.from_numpy(mass).to(self.device)
+        self.privileged_mass_params = torch.from_numpy(mass[sl].copy()).to(self.device)
         names = self.body_names
         feet = [s for s in names if self.cfg.asset.foot_name in s]
         pen, term = [], []
@@ -310,7 +314,8 @@ class LeggedRobot(BaseTask):
             self._friction = torch.ones(n, device=dev) * self.cfg.terrain.dynamic_friction
         self.privileged_friction_coeffs = self._friction.view(n, 1)
         lo, hi = getattr(dr, "kp_kd_range", [1.0, 1.0])
-        self.kp_kd_multipliers = (hi - lo) * torch.rand(2, n, na, device=dev) + lo
+        self.kp_kd_multipliers = ((hi - lo) * torch.rand(2, self.num_envs_total, na, device=dev) + lo)[
+            :, self.env_id_offset:self.env_id_offset + n].contiguous()
         if not getattr(dr, "randomize_kp_kd", False):
             self.kp_kd_multipliers.fill_(1.0)
         self.default_dof_pos = torch.tensor([self.cfg.init_state.default_joint_angles[nm] for nm in self.dof_names],

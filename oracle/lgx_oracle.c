@@ -773,9 +773,13 @@ void oracle_clip_actions(const lgx_task_params* P, lgx_buffers* B) {
 /* full step: clip, decimation x (torques, physics substep), post-physics */
 void oracle_step(const lgx_model* M, const lgx_task_params* P, lgx_buffers* B, uint64_t seed, uint64_t step) {
   oracle_clip_actions(P, B);
+  /* envs are independent in the physics: OpenMP over envs (OMP_NUM_THREADS; 1 = serial) */
   for (int s = 0; s < P->decimation; ++s) {
-    for (int e = 0; e < P->num_envs; ++e) oracle_compute_torques(P, B, e);
-    for (int e = 0; e < P->num_envs; ++e) oracle_physics_substep(M, P, B, e);
+#pragma omp parallel for schedule(static)
+    for (int e = 0; e < P->num_envs; ++e) {
+      oracle_compute_torques(P, B, e);
+      oracle_physics_substep(M, P, B, e);
+    }
   }
   oracle_post_physics(P, B, seed, step);
 }

@@ -402,7 +402,7 @@ void oracle_physics_substep(const lgx_model* M, const lgx_task_params* P, lgx_bu
   for (int i = 0; i < NU; ++i) us[i] = u[i] + dt * acc[i];
 
   /* constraint rows */
-  static row_t rows[LGX_MAX_DOF * 2 + 3 * LGX_MAX_CONTACTS];
+  row_t rows[LGX_MAX_DOF * 2 + 3 * LGX_MAX_CONTACTS];
   int nr = 0;
   for (int j = 0; j < D; ++j) {
     int k = j + 1;
@@ -471,8 +471,8 @@ void oracle_physics_substep(const lgx_model* M, const lgx_task_params* P, lgx_bu
     rows[r].target = tv;
   }
   /* A = J M⁻¹ Jᵀ, b = J u* */
-  static double MiJ[LGX_MAX_DOF * 2 + 3 * LGX_MAX_CONTACTS][NU];
-  static double A[LGX_MAX_DOF * 2 + 3 * LGX_MAX_CONTACTS][LGX_MAX_DOF * 2 + 3 * LGX_MAX_CONTACTS];
+  double MiJ[LGX_MAX_DOF * 2 + 3 * LGX_MAX_CONTACTS][NU];
+  double A[LGX_MAX_DOF * 2 + 3 * LGX_MAX_CONTACTS][LGX_MAX_DOF * 2 + 3 * LGX_MAX_CONTACTS];
   double b[LGX_MAX_DOF * 2 + 3 * LGX_MAX_CONTACTS], lam[LGX_MAX_DOF * 2 + 3 * LGX_MAX_CONTACTS];
   for (int r = 0; r < nr; ++r) {
     memcpy(MiJ[r], rows[r].J, sizeof(double) * NU);

@@ -35,6 +35,12 @@ class Twin:
             if v is not None:
                 self.t[k].copy_(self.torch.from_numpy(_torchable(v)))
 
+    def pull(self):
+        """GPU buffers -> numpy (oracle) state, in place (the oracle holds pointers to them)."""
+        for k, v in self.o.a.items():
+            if v is not None:
+                v[...] = self.gpu(k)
+
     def gpu(self, k):
         v = self.t[k].cpu().numpy()
         return v.view(self.o.a[k].dtype) if self.o.a[k] is not None else v
