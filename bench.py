@@ -2,13 +2,17 @@
 """bench.py — BASELINE.json metric: env-steps/sec (whole node), Go2 flat, 4096 envs per GPU.
 
 One "step" = one rsl_rl learning iteration of the drop-in runner on synthetic Go2 flat
-terrain: 24 env steps (policy act + fused HIP env step + storage) + GAE + the PPO/ROA
-update (5 epochs x 4 minibatches) — i.e. Perf/total_fps of on_policy_runner.py:219.
-value = num_envs x 24 x world_size x K / (max over ranks of the timed K iterations).
+terrain: 24 env steps (policy act + fused HIP env step + storage + the per-step episode
+bookkeeping train.py's runner does, on_policy_runner.py:160-170) + GAE + the PPO/ROA update
+(5 epochs x 4 minibatches) — i.e. Perf/total_fps of on_policy_runner.py:219.
+value = num_envs x 24 x world_size x K / (max over ranks of the timed K iterations);
+`value_no_episode_tracking` is the same loop without the bookkeeping.
 
 Also reported: `roofline` of the env-step kernel (algorithmic bytes per launch over its
-HIP-event-timed duration vs 8 TB/s HBM), and `cpu_baseline`: the CPU oracle (C port of
-the same env step) + torch-CPU learner on a bounded sample, rank 0 at N=1 only.
+HIP-event-timed duration vs 8 TB/s HBM; the kernel is not HBM-bound: `roofline_valu` gives
+its VALU issue utilisation from the committed PMC profile), `roofline_learner`, and
+`cpu_baseline`: the CPU oracle (C port of the same env step, OpenMP over envs) + torch-CPU
+learner at the same shape (one iteration), rank 0 at N=1 only.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--num_envs 4096]
   N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -90,8 +94,9 @@ def learner_gemm_roofline(dev, rows=24576, reps=10):
 
 def committed_traffic(num_envs):
     """Env-step kernel HBM bytes per launch from the newest committed PMC profile
-    (profiles/<round>_env_traffic.json, made by tools/profile_round.sh: FETCH_SIZE x2 +
-    WRITE_SIZE, separate --pmc passes), when it was measured on this workload size."""
+    (profiles/<round>_env_traffic.json, made by tools/gpu/pmc_env.sh: FETCH_SIZE and
+    WRITE_SIZE from separate --pmc passes, corrected by the dword-access calibration), when
+    it was measured on this workload size."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_env_traffic.json")))
     if not files:
@@ -102,8 +107,38 @@ def committed_traffic(num_envs):
     return d["traffic_bytes_per_launch"], os.path.relpath(files[-1], ROOT)
 
 
-def cpu_baseline(num_envs=1024, iters=3, steps_per_env=24):
-    """Oracle env step (single-threaded C) + torch-CPU rsl_rl learner, same runner."""
+def committed_valu(num_envs):
+    """VALU issue utilisation of the env-step kernel from the newest committed PMC profile
+    (profiles/<round>_env_kernel_pmc.txt): every VALU instruction of a wave64 occupies its
+    SIMD for 4 cycles, so utilisation = 4 x SQ_INSTS_VALU / (1024 SIMDs x kernel cycles),
+    kernel cycles = GRBM_GUI_ACTIVE / 8 XCDs."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_env_kernel_pmc.txt")))
+    if not files:
+        return None
+    vals = {}
+    for line in open(files[-1]):
+        f = line.split()
+        if len(f) == 2 and f[0].isupper():
+            try:
+                vals[f[0]] = float(f[1])
+            except ValueError:
+                pass
+    if not {"SQ_INSTS_VALU", "GRBM_GUI_ACTIVE"} <= set(vals):
+        return None
+    cyc = vals["GRBM_GUI_ACTIVE"] / 8
+    used = 4 * vals["SQ_INSTS_VALU"]
+    cap = 1024 * cyc
+    return {"bound": "valu", "kernel": "lgx::env_step_kernel<true, false, false>",
+            "achieved": round(used / 1e6, 1), "peak": round(cap / 1e6, 1), "unit": "M VALU issue cycles per launch",
+            "frac": round(used / cap, 4), "valu_instructions_per_env_step": round(vals["SQ_INSTS_VALU"] / num_envs),
+            "source": os.path.relpath(files[-1], ROOT)}
+
+
+def cpu_baseline(num_envs=4096, iters=1, steps_per_env=24):
+    """Oracle env step (C, OpenMP over envs) + torch-CPU rsl_rl learner, same runner, at the
+    benchmark's shape (C2: 4096 envs x 24 steps), one timed iteration after a warm-up one, on
+    the host threads this process may use (OMP_NUM_THREADS; 16 per GPU on the GPU box)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import cpu_env
     from legged_gym_custom_amd import model as mdl, params as prm
@@ -116,7 +151,8 @@ def cpu_baseline(num_envs=1024, iters=3, steps_per_env=24):
     P = prm.build_task_params(cfg, m, num_envs)
     env = cpu_env.OracleVecEnv(cfg, m, P, mdl.to_struct(m))
     tcfg.runner.num_steps_per_env = steps_per_env
-    threads = min(16, os.cpu_count() or 1)
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
+    os.environ["OMP_NUM_THREADS"] = str(threads)  # the oracle's OpenMP env loop
     torch.set_num_threads(threads)
     torch.manual_seed(1)
     runner = OnPolicyRunner(env, class_to_dict(tcfg), None, device="cpu")
@@ -127,7 +163,7 @@ def cpu_baseline(num_envs=1024, iters=3, steps_per_env=24):
     return {"value": round(num_envs * steps_per_env * iters / dt, 1), "unit": "env-steps/s", "cores": threads,
             "kind": "port",
             "sample": f"{iters} PPO iteration(s) of Go2 flat at {num_envs} envs x {steps_per_env} steps on the host: "
-                      f"oracle/lgx_oracle.c env step (1 thread) + torch-CPU learner ({threads} threads)",
+                      f"oracle/lgx_oracle.c env step (OpenMP over envs) + torch-CPU learner, {threads} threads",
             "seconds": round(dt, 2)}
 
 
@@ -177,16 +213,26 @@ def main():
             dist.barrier()
         torch.cuda.synchronize(dev)
 
-    runner.learn(num_learning_iterations=args.warmup, init_at_random_ep_len=True)
-    barrier()
-    t0 = time.time()
-    runner.learn(num_learning_iterations=args.steps)
-    barrier()
-    elapsed = time.time() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
+    def timed(track):
+        """W warm-up + K timed iterations (barrier + synchronize both sides, max over ranks)."""
+        runner.track_episodes = track
+        runner.learn(num_learning_iterations=args.warmup, init_at_random_ep_len=True)
+        barrier()
+        t0 = time.time()
+        runner.learn(num_learning_iterations=args.steps)
+        barrier()
+        el = time.time() - t0
+        if world > 1:
+            t = torch.tensor([el], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = t.item()
+        return el, dict(runner.last_perf)
+
+    elapsed_nt, perf_nt = timed(False)  # iterations 0..W-1 warm-up (0 is a DAgger iteration), then W..W+K-1
+    # same window position for the tracked run (no DAgger iteration inside either window,
+    # it % 20 == 0, on_policy_runner.py:147)
+    runner.current_learning_iteration = 21
+    elapsed, perf = timed(True)  # the headline: as train.py runs it
     steps_per_iter = train_cfg.runner.num_steps_per_env
     total_env_steps = args.num_envs * steps_per_iter * world * args.steps
     value = total_env_steps / elapsed
@@ -227,15 +273,20 @@ def main():
             "config": {"workload": f"{args.task}, rsl_rl PPO/ROA iteration (24 env steps + 5x4 minibatch update)",
                        "num_envs_per_gpu": args.num_envs, "num_steps_per_env": steps_per_iter,
                        "global_envs": args.num_envs * world, "parallelism": f"env-sharded dp{world}"},
-            "collection_s": round(runner.last_perf.get("collection_time", 0.0), 4),
-            "learn_s": round(runner.last_perf.get("learn_time", 0.0), 4),
+            "value_no_episode_tracking": round(total_env_steps / elapsed_nt, 1),
+            "collection_s": round(perf.get("collection_time", 0.0), 4),
+            "learn_s": round(perf.get("learn_time", 0.0), 4),
             "env_kernel": {"avg_us": round(kern_avg_ms * 1e3, 2), "min_us": round(kern_ms[0] * 1e3, 2),
                            "env_steps_per_s": round(env.num_envs / (kern_avg_ms * 1e-3), 1)},
             "roofline": {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "bytes_per_env_step": bpe, "bytes_per_launch": launch_bytes,
-                         "traffic": None if traffic is None else round(traffic), "traffic_source": traffic_src},
+                         "traffic": None if traffic is None else round(traffic), "traffic_source": traffic_src,
+                         "note": "the kernel's algorithmic bytes vs HBM peak, as north_star asks; it is bound by "
+                                 "VALU issue and per-env latency, not HBM (roofline_valu, DESIGN.md 4.1)"},
         }
+        if args.task == "go2" and args.num_envs == 4096:
+            out["roofline_valu"] = committed_valu(args.num_envs)
         if args.task == "go2":
             out["roofline_learner"] = learner_gemm_roofline(dev)
         if world == 1 and not args.no_cpu_baseline:

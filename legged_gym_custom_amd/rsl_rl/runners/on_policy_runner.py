@@ -107,6 +107,9 @@ class OnPolicyRunner:
         if torch.is_tensor(dst) and dst.is_cuda and dst.device == torch.device(device) and dst.is_contiguous():
             self.alg.act_dst = dst
         self.log_dir = log_dir if self.rank == 0 else None
+        # per-step episode bookkeeping (on_policy_runner.py:160-170) runs whenever there is a
+        # log dir, as in the reference; bench.py also switches it on without one
+        self.track_episodes = False
         self.writer = None
         self.tot_timesteps = 0
         self.tot_time = 0
@@ -209,7 +212,7 @@ class OnPolicyRunner:
                      env.get_critic_observations().to(self.device), env.get_estimated_observations().to(self.device),
                      env.get_scan_observations().to(self.device)]
         self.alg.actor_critic.train()
-        track = self.log_dir is not None
+        track = self.log_dir is not None or self.track_episodes
         if track and self._stats is None:
             z = lambda *sh: torch.zeros(*sh, device=self.device)  # noqa: E731
             self._stats = {"cur_rew": z(env.num_envs), "cur_len": z(env.num_envs), "rew_ring": z(101),
