@@ -230,6 +230,25 @@ typedef struct lgx_transition_args {
 } lgx_transition_args;
 int32_t lgx_store_transition(const lgx_transition_args* args, void* stream);
 
+/* OnPolicyRunner.learn's per-step episode bookkeeping (on_policy_runner.py:160-170) in one
+ * launch, device-side form of its deques (rewbuffer/lenbuffer keep the last 100 completed
+ * episodes; ep_infos accumulate infos['episode']):
+ *   cur_rew += rewards;  cur_len += 1
+ *   for the done envs in env order (rank r of k): if r >= k - 100:
+ *       rew_ring[(ptr + r) % 100] = cur_rew;  len_ring[(ptr + r) % 100] = cur_len
+ *   ptr = (ptr + k) % 100;  n = min(n + k, 100);  cur_rew, cur_len = 0 where done
+ *   ep_sum[0:na] += ep_a[0:na];  ep_sum[na:na+nb] += ep_b[0:nb];  ep_cnt += 1  (ep_* optional)
+ * One workgroup; the done ranks come from a block-wide scan. Replaces the cumsum / where /
+ * scatter / masked_fill / stack sequence of the runner's torch form, bit for bit. */
+typedef struct lgx_track_args {
+  const float* rewards; const uint8_t* dones;
+  float* cur_rew; float* cur_len; float* rew_ring; float* len_ring;  /* rings: >= 100 floats */
+  int64_t* ptr; int64_t* n;
+  const float* ep_a; const float* ep_b; float* ep_sum; float* ep_cnt;
+  int32_t N, na, nb;
+} lgx_track_args;
+int32_t lgx_track_episodes(const lgx_track_args* args, void* stream);
+
 /* RolloutStorage.compute_returns (rollout_storage.py:110-124) over [T, N] rows, one thread
  * per env walking the steps backwards in torch's operation order:
  *   nt = 1 - dones[t];  delta = (rewards[t] + (nt*gamma) * V[t+1]) - V[t]   (V[T] = last_values)

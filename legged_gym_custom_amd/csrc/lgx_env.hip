@@ -85,6 +85,11 @@ struct Sh {
   float root[13], cmd[4], fat[4], lch[4];
   int lc[4];
   float rterm[64];
+  float jsum[16];  // per-env joint / height-point sums the reward terms share (joint_sums)
+  // post-physics inputs read at kernel start (their HBM latency hides behind the physics)
+  long long ep_prev;
+  int lc_prev[LGX_MAX_FEET];
+  float lch_prev[LGX_MAX_FEET], fat_prev[LGX_MAX_FEET], jump_prev;
   long long ep;
   int reset, tout;
   // --- physics state (base velocity kept as the ORIGIN velocity inside the step)
@@ -1211,38 +1216,84 @@ LGX_DEV void fill_uniforms(Sh& s, uint64_t seed, uint32_t gid, uint64_t step, ui
   __syncthreads();
 }
 
+// The sums over joints (and height points) that reward terms use, formed lane-parallel
+// (lane j = joint j, reduced over lanes 0..15 by a DPP scan; lane 15 writes them), so the
+// per-term lanes below do no joint loops. Summation order differs from torch's sum over a
+// dim by ~1 ulp of the sum (golden tests: 1e-5).
+enum JSum { J_ACTION_RATE, J_DELTA_TORQUES, J_DOF_ACC, J_DOF_ERROR, J_DOF_POS_LIMITS, J_DOF_VEL, J_DOF_VEL_LIMITS,
+            J_STAND_ABS, J_TORQUE_LIMITS, J_TORQUES, J_HIP_POS, J_THIGH_POS, J_CALF_POS, J_HEIGHT, J_N };
+LGX_DEV void joint_sums(const lgx_task_params* Pm, const lgx_buffers& B, Sh& s, int e, int lane) {
+  const int D = Pm->num_dof, A = Pm->num_actions;
+  const int j = lane < D ? lane : 0;
+  const float on = lane < D ? 1.0f : 0.0f;
+  const float la = B.last_actions[(size_t)e * A + j], lt = B.last_torques[(size_t)e * D + j];
+  const float q = s.th[j], qd = s.thd[j], tau = s.tau[j], q0 = Pm->default_dof_pos[j];
+  const float dq = q - q0;
+  float v[J_N];
+  v[J_ACTION_RATE] = sq(la - s.act[j]);
+  v[J_DELTA_TORQUES] = sq(tau - lt);
+  v[J_DOF_ACC] = sq((s.ldv[j] - qd) / Pm->dt);
+  v[J_DOF_ERROR] = sq(dq);
+  {
+    const float lo = q - Pm->dof_pos_limits[j][0], hi = q - Pm->dof_pos_limits[j][1];
+    float o = -(lo < 0.0f ? lo : 0.0f);
+    o += (hi > 0.0f ? hi : 0.0f);
+    v[J_DOF_POS_LIMITS] = o;
+  }
+  v[J_DOF_VEL] = sq(qd);
+  v[J_DOF_VEL_LIMITS] = clipf(fabsf(qd) - Pm->dof_vel_limits[j] * Pm->soft_dof_vel_limit, 0.0f, 1.0f);
+  v[J_STAND_ABS] = fabsf(dq);
+  {
+    const float t = fabsf(tau) - Pm->torque_limits[j] * Pm->soft_torque_limit;
+    v[J_TORQUE_LIMITS] = t > 0.0f ? t : 0.0f;
+  }
+  v[J_TORQUES] = sq(tau);
+  float hip = 0.f, thigh = 0.f, calf = 0.f;
+  for (int i = 0; i < 4; ++i) {
+    hip += Pm->hip_joint_idx[i] == j ? 1.f : 0.f;
+    thigh += Pm->thigh_joint_idx[i] == j ? 1.f : 0.f;
+    calf += Pm->calf_joint_idx[i] == j ? 1.f : 0.f;
+  }
+  v[J_HIP_POS] = hip * v[J_DOF_ERROR];
+  v[J_THIGH_POS] = thigh * v[J_DOF_ERROR];
+  v[J_CALF_POS] = calf * v[J_DOF_ERROR];
+  // height points: lane i < 16 sums points i, i + 16, ...
+  float hsum = 0.f;
+  if (lane < 16) {
+    const float* hts = stg_heights(Pm);
+    for (int i = lane; i < Pm->num_height_points; i += 16) hsum += s.root[2] - hts[i];
+  }
+#pragma unroll
+  for (int k = 0; k < J_N; ++k) {
+    float x = k == J_HEIGHT ? (lane < 16 ? hsum : 0.f) : v[k] * on;
+    x += dpp_shr_t<0x111>(x);
+    x += dpp_shr_t<0x112>(x);
+    x += dpp_shr_t<0x114>(x);
+    x += dpp_shr_t<0x118>(x);
+    if (lane == 15) s.jsum[k] = x;
+  }
+}
+
 // one reward term (lane k computes term k); mirrors oracle/lgx_oracle.c reward_term.
 // Side effects (kept from the reference): feet_air_time (go2.py:827-830) and the in-place
 // wrap of commands[:, 3] (go2.py:744, Q7) are written back to LDS by the owning lane.
 LGX_DEV float reward_term(const lgx_task_params* Pm, const lgx_buffers& B, Sh& s, int e, int id) {
-  const int D = Pm->num_dof, A = Pm->num_actions;
   const Scratch& x = s.x;
   const float* root = s.root;
   float* cmd = s.cmd;
-  const float* lact = B.last_actions + (size_t)e * A;
-  const float* ldv = s.ldv;
-  const float* ltq = B.last_torques + (size_t)e * D;
   const float* lch = s.lch;
   float* fat = s.fat;
   const int* lc = s.lc;
   float r = 0.0f;
   switch (id) {
-    case LGX_REW_ACTION_RATE:
-      for (int j = 0; j < A; ++j) r += sq(lact[j] - s.act[j]);
-      return r;
+    case LGX_REW_ACTION_RATE: return s.jsum[J_ACTION_RATE];
     case LGX_REW_ANG_VEL_XY: return sq(x.bav[0]) + sq(x.bav[1]);
-    case LGX_REW_BASE_HEIGHT: {
-      float acc = 0.0f;
-      const float* hts = stg_heights(Pm);
-      for (int i = 0; i < Pm->num_height_points; ++i) acc += root[2] - hts[i];
-      return sq(acc / (float)Pm->num_height_points - Pm->base_height_target);
-    }
+    case LGX_REW_BASE_HEIGHT:
+      return sq(s.jsum[J_HEIGHT] / (float)Pm->num_height_points - Pm->base_height_target);
     case LGX_REW_CALF_COLLISION:
       for (int i = 0; i < 4; ++i) { const float* c = s.cf[Pm->calf_idx[i]]; r += (float)(nrm3(c[0], c[1], c[2]) > 0.1f); }
       return r;
-    case LGX_REW_CALF_POS:
-      for (int i = 0; i < 4; ++i) { int j = Pm->calf_joint_idx[i]; r += sq(s.th[j] - Pm->default_dof_pos[j]); }
-      return r;
+    case LGX_REW_CALF_POS: return s.jsum[J_CALF_POS];
     case LGX_REW_CALF_SYMMETRY: {
       const int* c = Pm->calf_joint_idx;
       return fabsf(s.th[c[0]] - s.th[c[1]]) + fabsf(s.th[c[2]] - s.th[c[3]]);
@@ -1253,29 +1304,12 @@ LGX_DEV float reward_term(const lgx_task_params* Pm, const lgx_buffers& B, Sh& s
         r += (float)(nrm3(c[0], c[1], c[2]) > 0.1f);
       }
       return r;
-    case LGX_REW_DELTA_TORQUES:
-      for (int j = 0; j < D; ++j) r += sq(s.tau[j] - ltq[j]);
-      return r;
-    case LGX_REW_DOF_ACC:
-      for (int j = 0; j < D; ++j) r += sq((ldv[j] - s.thd[j]) / Pm->dt);
-      return r;
-    case LGX_REW_DOF_ERROR:
-      for (int j = 0; j < D; ++j) r += sq(s.th[j] - Pm->default_dof_pos[j]);
-      return r;
-    case LGX_REW_DOF_POS_LIMITS:
-      for (int j = 0; j < D; ++j) {
-        float lo = s.th[j] - Pm->dof_pos_limits[j][0], hi = s.th[j] - Pm->dof_pos_limits[j][1];
-        float o = -(lo < 0.0f ? lo : 0.0f);
-        o += (hi > 0.0f ? hi : 0.0f);
-        r += o;
-      }
-      return r;
-    case LGX_REW_DOF_VEL:
-      for (int j = 0; j < D; ++j) r += sq(s.thd[j]);
-      return r;
-    case LGX_REW_DOF_VEL_LIMITS:
-      for (int j = 0; j < D; ++j) r += clipf(fabsf(s.thd[j]) - Pm->dof_vel_limits[j] * Pm->soft_dof_vel_limit, 0.0f, 1.0f);
-      return r;
+    case LGX_REW_DELTA_TORQUES: return s.jsum[J_DELTA_TORQUES];
+    case LGX_REW_DOF_ACC: return s.jsum[J_DOF_ACC];
+    case LGX_REW_DOF_ERROR: return s.jsum[J_DOF_ERROR];
+    case LGX_REW_DOF_POS_LIMITS: return s.jsum[J_DOF_POS_LIMITS];
+    case LGX_REW_DOF_VEL: return s.jsum[J_DOF_VEL];
+    case LGX_REW_DOF_VEL_LIMITS: return s.jsum[J_DOF_VEL_LIMITS];
     case LGX_REW_FEET_AIR_TIME: {
       float rew = 0.0f;
       for (int f = 0; f < Pm->num_feet; ++f) {
@@ -1311,9 +1345,7 @@ LGX_DEV float reward_term(const lgx_task_params* Pm, const lgx_buffers& B, Sh& s
       float err = wrap_to_pi(desired - heading);
       return sq(err) * (float)(nrm3(cmd[0], cmd[1], cmd[2]) >= 0.2f);
     }
-    case LGX_REW_HIP_POS:
-      for (int i = 0; i < 4; ++i) { int j = Pm->hip_joint_idx[i]; r += sq(s.th[j] - Pm->default_dof_pos[j]); }
-      return r;
+    case LGX_REW_HIP_POS: return s.jsum[J_HIP_POS];
     case LGX_REW_JUMP_ZONE_FORWARD_VEL: {
       float fr = root[7] > 0.0f ? root[7] : 0.0f;
       return fr * (float)(x.jump > 0.0f) * (float)(nrm3(cmd[0], cmd[1], cmd[2]) >= 0.2f);
@@ -1349,9 +1381,7 @@ LGX_DEV float reward_term(const lgx_task_params* Pm, const lgx_buffers& B, Sh& s
       return rew / 2.0f;
     }
     case LGX_REW_REVERSE_PENALTY: return -(root[7] < 0.0f ? root[7] : 0.0f);
-    case LGX_REW_STAND_STILL:
-      for (int j = 0; j < D; ++j) r += fabsf(s.th[j] - Pm->default_dof_pos[j]);
-      return r * (float)(nrm2(cmd[0], cmd[1]) < 0.1f);
+    case LGX_REW_STAND_STILL: return s.jsum[J_STAND_ABS] * (float)(nrm2(cmd[0], cmd[1]) < 0.1f);
     case LGX_REW_STUMBLE_CALVES: {
       int any = 0;
       for (int i = 0; i < 4; ++i) { const float* c = s.cf[Pm->calf_idx[i]]; any |= nrm2(c[0], c[1]) > 5.0f * fabsf(c[2]); }
@@ -1362,22 +1392,13 @@ LGX_DEV float reward_term(const lgx_task_params* Pm, const lgx_buffers& B, Sh& s
       for (int f = 0; f < Pm->num_feet; ++f) { const float* c = s.cf[Pm->feet_idx[f]]; any |= nrm2(c[0], c[1]) > 5.0f * fabsf(c[2]); }
       return (float)any;
     }
-    case LGX_REW_THIGH_POS:
-      for (int i = 0; i < 4; ++i) { int j = Pm->thigh_joint_idx[i]; r += sq(s.th[j] - Pm->default_dof_pos[j]); }
-      return r;
+    case LGX_REW_THIGH_POS: return s.jsum[J_THIGH_POS];
     case LGX_REW_THIGH_SYMMETRY: {
       const int* c = Pm->thigh_joint_idx;
       return fabsf(s.th[c[0]] - s.th[c[1]]) + fabsf(s.th[c[2]] - s.th[c[3]]);
     }
-    case LGX_REW_TORQUE_LIMITS:
-      for (int j = 0; j < D; ++j) {
-        float v = fabsf(s.tau[j]) - Pm->torque_limits[j] * Pm->soft_torque_limit;
-        r += v > 0.0f ? v : 0.0f;
-      }
-      return r;
-    case LGX_REW_TORQUES:
-      for (int j = 0; j < D; ++j) r += sq(s.tau[j]);
-      return r;
+    case LGX_REW_TORQUE_LIMITS: return s.jsum[J_TORQUE_LIMITS];
+    case LGX_REW_TORQUES: return s.jsum[J_TORQUES];
     case LGX_REW_TRACKING_ANG_VEL: return expf(-sq(cmd[2] - x.bav[2]) / Pm->tracking_sigma);
     case LGX_REW_TRACKING_LIN_VEL: return expf(-(sq(cmd[0] - x.blv[0]) + sq(cmd[1] - x.blv[1])) / Pm->tracking_sigma);
     case LGX_REW_TRACKING_PITCH: {
@@ -1388,11 +1409,8 @@ LGX_DEV float reward_term(const lgx_task_params* Pm, const lgx_buffers& B, Sh& s
       float deg = x.roll * 57.29577951308232f;
       return expf(-sq(deg - Pm->roll_deg_target) / Pm->tracking_sigma);
     }
-    case LGX_REW_ZERO_CMD_DOF_ERROR: {
-      float zm = (float)(nrm3(cmd[0], cmd[1], cmd[2]) < 0.2f);
-      for (int j = 0; j < D; ++j) r += sq(s.th[j] - Pm->default_dof_pos[j]);
-      return r * zm;
-    }
+    case LGX_REW_ZERO_CMD_DOF_ERROR:
+      return s.jsum[J_DOF_ERROR] * (float)(nrm3(cmd[0], cmd[1], cmd[2]) < 0.2f);
     default: return 0.0f;
   }
 }
@@ -1467,6 +1485,16 @@ __global__ __launch_bounds__(64, ACTNET ? LGX_SEA_WAVES : 4) void env_step_kerne
     s.mu = 0.5f * ((B.friction ? B.friction[e] : 1.f) + Pm->ground_friction);
   }
   if (lane < 3) s.cadd[lane] = B.mass_params ? B.mass_params[e * 4 + 1 + lane] : 0.f;
+  if (lane < 4) s.cmd[lane] = B.commands[e * 4 + lane];
+  if (lane == 0) {
+    s.ep_prev = B.episode_length[e];
+    s.jump_prev = B.rpy_phase ? B.rpy_phase[e * 8 + 7] : 0.f;
+  }
+  if (Pm->task_kind == LGX_TASK_GO2 && lane < Pm->num_feet) {
+    s.lc_prev[lane] = B.last_contacts[e * Pm->num_feet + lane];
+    s.lch_prev[lane] = B.last_contact_heights[e * Pm->num_feet + lane];
+    s.fat_prev[lane] = B.feet_air_time ? B.feet_air_time[e * Pm->num_feet + lane] : 0.f;
+  }
 #ifdef LGX_PHASE_CLOCK
   if (lane < 16) s.phacc[lane] = 0u;
   if (lane == 0) s.phlast = clock64();
@@ -1565,8 +1593,7 @@ __global__ __launch_bounds__(64, ACTNET ? LGX_SEA_WAVES : 4) void env_step_kerne
     Scratch& x = s.x;
     float* root = s.root;
     float* cmd = s.cmd;
-    for (int i = 0; i < 4; ++i) cmd[i] = B.commands[e * 4 + i];
-    const long long ep = B.episode_length[e] + 1;
+    const long long ep = s.ep_prev + 1;
     s.ep = ep;
     const float g[3] = {0.f, 0.f, -1.f};
     quat_rotate_inverse(root + 3, root + 7, x.blv);
@@ -1583,14 +1610,14 @@ __global__ __launch_bounds__(64, ACTNET ? LGX_SEA_WAVES : 4) void env_step_kerne
       float msk = (nrm3(cmd[0], cmd[1], cmd[2]) < 0.2f) ? 0.0f : 1.0f;
       x.ph[0] = pfl * msk; x.ph[1] = pfr * msk; x.ph[2] = pbl * msk; x.ph[3] = pbr * msk;
       for (int f = 0; f < 4; ++f) {
-        int lcf = B.last_contacts[e * Pm->num_feet + f];
-        float lch = B.last_contact_heights[e * Pm->num_feet + f];
+        int lcf = s.lc_prev[f];
+        float lch = s.lch_prev[f];
         int curc = s.cf[Pm->feet_idx[f]][2] > 1.0f;
         x.contact[f] = curc || lcf;
         s.lc[f] = curc;
         x.feet_z[f] = s.rbz[Pm->feet_idx[f]];
         s.lch[f] = x.contact[f] ? x.feet_z[f] : lch;
-        if (B.feet_air_time) s.fat[f] = B.feet_air_time[e * Pm->num_feet + f];
+        if (B.feet_air_time) s.fat[f] = s.fat_prev[f];
       }
       // quaternion_to_euler go2.py:11-31
       float qx = root[3], qy = root[4], qz = root[5], qw = root[6];
@@ -1624,11 +1651,13 @@ __global__ __launch_bounds__(64, ACTNET ? LGX_SEA_WAVES : 4) void env_step_kerne
     if (Pm->parkour) reset |= root[2] < -1.0f;
     s.reset = reset;
     s.tout = tout;
-    x.jump = B.rpy_phase ? B.rpy_phase[e * 8 + 7] : 0.f;  // set by the previous step's observations
+    x.jump = s.jump_prev;  // set by the previous step's observations
   }
   __syncthreads();
   PH(13);
   get_heights(Pm, B, s, lane);
+  __syncthreads();
+  joint_sums(Pm, B, s, e, lane);
   __syncthreads();
   // compute_reward legged_robot.py:216-237: lane k evaluates term k (alphabetical order)
   const int K = Pm->num_reward_terms;

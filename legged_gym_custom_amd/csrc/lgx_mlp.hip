@@ -1577,6 +1577,84 @@ int32_t lgx_act_head(const lgx_act_head_args* a, void* stream) {
   return e == hipSuccess ? 0 : fail(hipGetErrorString(e));
 }
 
+}  // extern "C"
+
+namespace lgxm {
+// on_policy_runner.py:160-170 bookkeeping: one workgroup of 1024 threads, each owning a
+// contiguous chunk of envs; the done count per chunk is scanned across the block so every
+// done env knows its rank among all done envs (env order, as torch.cumsum gives).
+__global__ __launch_bounds__(1024) void track_kernel(lgx_track_args a) {
+  __shared__ int wsum[16];
+  __shared__ int k_all;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int chunk = (a.N + 1023) / 1024;
+  const int i0 = min(tid * chunk, a.N), i1 = min(i0 + chunk, a.N);
+  int cnt = 0;
+  for (int i = i0; i < i1; ++i) cnt += a.dones[i] != 0;
+  // inclusive scan over the block: within the wave by shuffles, then over the 16 waves
+  int x = cnt;
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[wv] = x;
+  __syncthreads();
+  if (tid == 0) {
+    int t = 0;
+    for (int w = 0; w < 16; ++w) {
+      const int v = wsum[w];
+      wsum[w] = t;
+      t += v;
+    }
+    k_all = t;
+  }
+  __syncthreads();
+  const int k = k_all;
+  int rank = wsum[wv] + x - cnt;  // exclusive prefix of this thread's chunk
+  const int64_t ptr = *a.ptr;
+  for (int i = i0; i < i1; ++i) {
+    const float r = a.cur_rew[i] + a.rewards[i];
+    const float l = a.cur_len[i] + 1.0f;
+    if (a.dones[i]) {
+      if (rank >= k - 100) {
+        const int slot = (int)((ptr + rank) % 100);
+        a.rew_ring[slot] = r;
+        a.len_ring[slot] = l;
+      }
+      ++rank;
+      a.cur_rew[i] = 0.f;
+      a.cur_len[i] = 0.f;
+    } else {
+      a.cur_rew[i] = r;
+      a.cur_len[i] = l;
+    }
+  }
+  __syncthreads();  // every thread read *ptr before it moves
+  if (tid == 0) {
+    *a.ptr = (ptr + k) % 100;
+    const int64_t n = *a.n + k;
+    *a.n = n < 100 ? n : 100;
+    if (a.ep_cnt) *a.ep_cnt += 1.0f;
+  }
+  if (a.ep_sum) {
+    if (tid < a.na) a.ep_sum[tid] += a.ep_a[tid];
+    else if (tid < a.na + a.nb) a.ep_sum[tid] += a.ep_b[tid - a.na];
+  }
+}
+}  // namespace lgxm
+
+extern "C" {
+
+int32_t lgx_track_episodes(const lgx_track_args* a, void* stream) {
+  if (!a || !a->rewards || !a->dones || !a->cur_rew || !a->cur_len || !a->rew_ring || !a->len_ring || !a->ptr ||
+      !a->n || a->N < 0 || a->na < 0 || a->nb < 0 || a->na + a->nb > 1024 ||
+      (a->ep_sum && (!a->ep_cnt || (a->na && !a->ep_a) || (a->nb && !a->ep_b))))
+    return fail("lgx_track_episodes: bad arguments");
+  hipLaunchKernelGGL(lgxm::track_kernel, dim3(1), dim3(1024), 0, static_cast<hipStream_t>(stream), *a);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : fail(hipGetErrorString(e));
+}
+
 int32_t lgx_store_transition(const lgx_transition_args* a, void* stream) {
   if (!a || !a->rewards || !a->dones || !a->values || !a->rewards_out || !a->dones_out || !a->values_out || a->B < 0)
     return fail("lgx_store_transition: bad arguments");

@@ -27,7 +27,8 @@ EXPORTED = ["lgx_mlp_abi_version", "lgx_mlp_sizeof_gemm_args", "lgx_mlp_pick_spl
             "lgx_copy_batch", "lgx_act_head", "lgx_store_transition", "lgx_splitk_reduce_batch",
             "lgx_aux_loss_forward", "lgx_aux_loss_backward", "lgx_ppo_tail", "lgx_gemm_group",
             "lgx_mlp_pick_split_group", "lgx_gae", "lgx_normalize_advantages",
-            "lgx_gather_rows", "lgx_transpose_batch", "lgx_loss_heads_forward", "lgx_loss_heads_backward"]
+            "lgx_gather_rows", "lgx_transpose_batch", "lgx_loss_heads_forward", "lgx_loss_heads_backward",
+            "lgx_track_episodes"]
 TAIL_MAX_LOSSES = 8
 COPY_MAX = 16
 SPLITK_MAX = 24
@@ -99,6 +100,13 @@ class TransitionArgs(C.Structure):
                                           "values_out")] + [("gamma", C.c_float), ("B", C.c_int32)]
 
 
+class TrackArgs(C.Structure):
+    """Mirror of lgx_track_args."""
+    _fields_ = [(n, C.c_void_p) for n in ("rewards", "dones", "cur_rew", "cur_len", "rew_ring", "len_ring", "ptr",
+                                          "n", "ep_a", "ep_b", "ep_sum", "ep_cnt")] + \
+        [("N", C.c_int32), ("na", C.c_int32), ("nb", C.c_int32)]
+
+
 class TransposeDesc(C.Structure):
     """Mirror of lgx_transpose_desc."""
     _fields_ = [("src", C.c_void_p), ("ld", C.c_int64), ("rows", C.c_int32), ("cols", C.c_int32),
@@ -142,6 +150,8 @@ def lib():
     L.lgx_act_head.restype = C.c_int32
     L.lgx_store_transition.argtypes = [vp, vp]
     L.lgx_store_transition.restype = C.c_int32
+    L.lgx_track_episodes.argtypes = [vp, vp]
+    L.lgx_track_episodes.restype = C.c_int32
     for fn in ("lgx_loss_heads_forward", "lgx_loss_heads_backward"):
         getattr(L, fn).argtypes = [vp, vp, vp]
         getattr(L, fn).restype = C.c_int32
@@ -246,6 +256,17 @@ def store_transition(rewards, dones, time_outs, values, rewards_out, dones_out, 
                           values.data_ptr(), rewards_out.data_ptr(), dones_out.data_ptr(), values_out.data_ptr(),
                           float(gamma), rewards.shape[0])
     _check(lib().lgx_store_transition(C.byref(args), _stream()), "lgx_store_transition")
+
+
+def track_episodes(rewards, dones, st, ep_a=None, ep_b=None):
+    """lgx_track_episodes on the runner's stats dict (on_policy_runner.py:160-170)."""
+    p = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+    args = TrackArgs(rewards.data_ptr(), dones.data_ptr(), st["cur_rew"].data_ptr(), st["cur_len"].data_ptr(),
+                     st["rew_ring"].data_ptr(), st["len_ring"].data_ptr(), st["ptr"].data_ptr(), st["n"].data_ptr(),
+                     p(ep_a), p(ep_b), p(st["ep_sum"] if ep_a is not None or ep_b is not None else None),
+                     p(st["ep_cnt"] if ep_a is not None or ep_b is not None else None), rewards.shape[0],
+                     0 if ep_a is None else ep_a.numel(), 0 if ep_b is None else ep_b.numel())
+    _check(lib().lgx_track_episodes(C.byref(args), _stream()), "lgx_track_episodes")
 
 
 def gae(rewards, dones, values, last_values, returns, advantages, gamma, lam, moments, ws, counter):

@@ -127,7 +127,10 @@ class OnPolicyRunner:
         """Device-side form of on_policy_runner.py:160-170 (no host sync, graph-capturable):
         rewbuffer/lenbuffer are 100-slot rings with the deque's keep-the-last-100 rule,
         and ep_infos are kept as per-step sums of infos['episode']."""
-        st = self._stats
+        if not self._track_native(rewards, dones, infos):
+            self._track_episodes_torch(self._stats, rewards, dones, infos)
+
+    def _track_episodes_torch(self, st, rewards, dones, infos):
         st["cur_rew"] += rewards
         st["cur_len"] += 1
         d = dones > 0
@@ -149,6 +152,49 @@ class OnPolicyRunner:
                     st["ep_sum"] = torch.zeros(len(st["ep_keys"]), device=self.device)
             st["ep_sum"] += torch.stack([ep[key].reshape(()).to(self.device).float() for key in st["ep_keys"]])
             st["ep_cnt"] += 1
+
+    def _track_native(self, rewards, dones, infos):
+        """One lgx_track_episodes launch for the whole bookkeeping when the buffers allow it
+        (HIP device, fp32 rewards, bool/uint8 dones, infos['episode'] values laid out as at most
+        two contiguous fp32 runs, e.g. the env's episode means and its terrain-level mean)."""
+        st = self._stats
+        if not (rewards.is_cuda and rewards.dtype == torch.float32 and dones.dtype in (torch.bool, torch.uint8)
+                and rewards.is_contiguous() and dones.is_contiguous()):
+            return False
+        runs = None
+        if "episode" in infos:
+            ep = infos["episode"]
+            if st["ep_keys"] is None:
+                st["ep_keys"] = list(ep.keys())
+                with torch.inference_mode(False):
+                    st["ep_sum"] = torch.zeros(len(st["ep_keys"]), device=self.device)
+            runs = st.get("ep_runs")
+            if runs is None:
+                runs = self._ep_runs([ep[k] for k in st["ep_keys"]])
+                st["ep_runs"] = runs
+            if runs is False:
+                return False
+        from legged_gym_custom_amd.rsl_rl.modules import hip_mlp as H
+        a, b = (runs + [None, None])[:2] if runs else (None, None)
+        H.track_episodes(rewards, dones.view(torch.uint8), st, a, b)
+        return True
+
+    @staticmethod
+    def _ep_runs(vals):
+        """Group 0-dim fp32 device tensors into <= 2 runs of consecutive storage (as tensors
+        over those runs), or False."""
+        runs, cur = [], None
+        for v in vals:
+            if not (torch.is_tensor(v) and v.is_cuda and v.dtype == torch.float32 and v.numel() == 1):
+                return False
+            if cur is not None and v.data_ptr() == cur[0].data_ptr() + 4 * cur[1]:
+                cur[1] += 1
+            else:
+                cur = [v, 1]
+                runs.append(cur)
+        if len(runs) > 2:
+            return False
+        return [torch.as_strided(t.reshape(-1), (n,), (1,)) for t, n in runs]
 
     def _rollout_step(self, adaptation_mode, track):
         """One env step of the rollout loop (on_policy_runner.py:147-170)."""

@@ -120,3 +120,38 @@ def test_act_head_feeds_env_the_stored_actions():
             assert torch.equal(env.actions, torch.clamp(stored, -clip, clip))
             alg.process_env_step(r[5], r[6], r[7])
         assert stored.std() > 0.3  # really sampled
+
+
+def test_native_episode_tracking_matches_torch_statement():
+    """lgx_track_episodes == the runner's torch statement of on_policy_runner.py:160-170,
+    bitwise, over steps with many (> 100, exercising keep-the-last-100) and few dones, with
+    infos['episode'] as the env lays it out (episode means + a separate terrain-level mean)."""
+    import types
+    import torch
+    from legged_gym_custom_amd.rsl_rl.runners.on_policy_runner import OnPolicyRunner
+    dev, n = "cuda", 4096
+
+    def stats():
+        z = lambda *sh: torch.zeros(*sh, device=dev)  # noqa: E731
+        return {"cur_rew": z(n), "cur_len": z(n), "rew_ring": z(101), "len_ring": z(101),
+                "ptr": torch.zeros((), dtype=torch.long, device=dev), "n": torch.zeros((), dtype=torch.long, device=dev),
+                "ep_keys": None, "ep_sum": None, "ep_cnt": z(())}
+    means, level = torch.zeros(15, device=dev), torch.zeros((), device=dev)
+    infos = {"episode": {**{f"rew_{i}": means[i] for i in range(15)}, "terrain_level": level}}
+    a = types.SimpleNamespace(_stats=stats(), device=dev, _ep_runs=OnPolicyRunner._ep_runs)
+    b = types.SimpleNamespace(_stats=stats(), device=dev)
+    g = torch.Generator(device=dev).manual_seed(3)
+    for k in range(60):
+        p = 0.05 if k % 3 == 0 else 0.004
+        rew = torch.randn(n, device=dev, generator=g)
+        dones = torch.rand(n, device=dev, generator=g) < p
+        means.copy_(torch.randn(15, device=dev, generator=g))
+        level.fill_(float(k))
+        assert OnPolicyRunner._track_native(a, rew, dones, infos)
+        OnPolicyRunner._track_episodes_torch(b, b._stats, rew, dones, infos)
+    torch.cuda.synchronize()
+    sa, sb = a._stats, b._stats
+    for key in ("cur_rew", "cur_len", "ptr", "n", "ep_sum", "ep_cnt"):
+        assert torch.equal(sa[key], sb[key]), key
+    for key in ("rew_ring", "len_ring"):
+        assert torch.equal(sa[key][:100], sb[key][:100]), key
