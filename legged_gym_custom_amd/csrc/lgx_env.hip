@@ -52,20 +52,20 @@ struct Scratch {  // per-env post-physics scalars (go2.py:357-367, 279-328)
 //   dynamics   Fw, Nw [NL][3], Dl [4][6], tot [16]
 //   rows       ZG [MAXR][RW] at 0: z_r = S⁻¹ (J_b − X_l J_l) (6) | g_r = D_l⁻¹ J_l (3);
 //              J9 [MAXR][RW] at MAXR*RW: sparse row r = [base part (6) | the 3 joints of leg
-//              rleg[r]]; once J9 is in registers, the same region holds A = J M⁻¹ Jᵀ for
-//              n <= AMAX rows, packed lower-triangular (see dynamics)
+//              rleg[r]]; once J9 is in registers, the same region holds A = J M⁻¹ Jᵀ [n][n]
+//              for n <= AMAX rows (see dynamics)
 //   post       U [4 rng_blocks] | cur [P] | hist [H*P] | heights [Hp] (stg_* below)
-// Go2 needs 1080 floats (the rows), ANYmal's post-physics staging 1,924.
-constexpr int AMAX = 32;
-constexpr int RW = 9;  // sparse row width
-constexpr int ROWS_FLOATS = 2 * MAXR * RW;
-static_assert(AMAX * (AMAX + 1) / 2 <= MAXR * RW, "packed A must fit the J9 region");
+// Go2 needs 1116 floats (the rows), ANYmal's post-physics staging 1,924.
+constexpr int AMAX = 24;  // rows per env step: p50 6, p99 15, max 27 (tools/phase_clock.py, r02)
+constexpr int RW = 9;     // sparse row width
+constexpr int J9_FLOATS = MAXR * RW > AMAX * AMAX ? MAXR * RW : AMAX * AMAX;
+constexpr int ROWS_FLOATS = MAXR * RW + J9_FLOATS;
 extern __shared__ float lgx_dyn[];
-LGX_DEV int pk_lo(int r, int c) { return r * (r + 1) / 2 + c; }  // packed lower, r >= c
 struct DynTemps {
   float Fw[NL][3], Nw[NL][3];  // per-link COM wrench (bias)
   float Dl[4][6];              // leg blocks of the joint-space inertia (xx yy zz xy xz yz)
   float tot[16];               // base sums about p0: m, h(3), Ip(6), F(3), N(3)
+  float Sp[21];                // Σ_j X_j B_jᵀ, packed lower
 };
 static_assert(sizeof(DynTemps) <= ROWS_FLOATS * sizeof(float), "dynamics temporaries fit the arena");
 LGX_DEV DynTemps& dtmp() { return *reinterpret_cast<DynTemps*>(lgx_dyn); }
@@ -110,7 +110,7 @@ struct Sh {
   float rbz[LGX_MAX_BODIES];
 #ifdef LGX_PHASE_CLOCK
   uint64_t phlast;
-  uint32_t phacc[16];
+  uint32_t phacc[20];
 #endif
 };
 
@@ -118,7 +118,7 @@ struct Sh {
 // Lane 0 accumulates s_memtime deltas per phase in LDS; the kernel's end writes them to
 // g_phase_out[env][phase]. Compiled out of the product library.
 #ifdef LGX_PHASE_CLOCK
-constexpr int NPH = 16;
+constexpr int NPH = 20;  // 16 phases + [16] max constraint rows, [17] wide-path substeps
 __device__ uint32_t* g_phase_out = nullptr;
 #define PH(k)                                              \
   do {                                                     \
@@ -398,17 +398,25 @@ LGX_DEV void dynamics(Sh& s, int lane, DynOut& o) {
 #pragma unroll
     for (int r = 0; r < 6; ++r) s.X[j][r] = o.xj[r];
   }
-  const float on = lane < NJ ? 1.f : 0.f;
-  // S = A_bb − Σ_j X_j B_jᵀ (packed lower); A_bb = [[M I, −[H]x], [[H]x, Ip]] (base origin
-  // velocity, ω), [H]x = [[0,−Hz,Hy],[Hz,0,−Hx],[−Hy,Hx,0]]
+  // the 21 Schur sums Σ_j X_j[r] B_j[c] (packed lower), one lane each over the 12 joints
+  __syncthreads();
+  if (lane < 21) {
+    const int q = lane;
+    const int r = (q >= 1) + (q >= 3) + (q >= 6) + (q >= 10) + (q >= 15), c = q - r * (r + 1) / 2;
+    float acc = 0.f;
+#pragma unroll
+    for (int jj = 0; jj < NJ; ++jj) acc += s.X[jj][r] * s.Bc[jj][c];
+    dtmp().Sp[q] = acc;
+  }
+  __syncthreads();
+  // S = A_bb − Σ_j X_j B_jᵀ; A_bb = [[M I, −[H]x], [[H]x, Ip]] (base origin velocity, ω),
+  // [H]x = [[0,−Hz,Hy],[Hz,0,−Hx],[−Hy,Hx,0]]
   const float Mt = tot[0], Hx = tot[1], Hy = tot[2], Hz = tot[3];
   const float Ab[21] = {Mt, 0.f, Mt, 0.f, 0.f, Mt, 0.f, -Hz, Hy, tot[4], Hz, 0.f, -Hx, tot[7], tot[5],
                         -Hy, Hx, 0.f, tot[8], tot[9], tot[6]};
   float L[21];
 #pragma unroll
-  for (int r = 0; r < 6; ++r)
-#pragma unroll
-    for (int c = 0; c <= r; ++c) L[pk(r, c)] = Ab[pk(r, c)] - row0_sum16(on * o.xj[r] * bj[c]);
+  for (int q = 0; q < 21; ++q) L[q] = Ab[q] - dtmp().Sp[q];
   float inv[6];
 #pragma unroll
   for (int c = 0; c < 6; ++c) {
@@ -756,7 +764,7 @@ LGX_DEV void substep(Sh& s, const lgx_model* M_, const lgx_task_params* Pm_, con
   };
   float* const ZG = lgx_dyn;                // [nrows][RW]: z_r (6) | g_r (3)
   float* const J9 = lgx_dyn + MAXR * RW;    // [nrows][RW]: J_B (6) | J of leg rleg (3)
-  float* const Am = J9;                     // packed lower A (A path, after J9 is consumed)
+  float* const Am = J9;                     // A [nrows][nrows] (A path, after J9 is consumed)
   if (lim_lo || lim_hi) {
     const int r = __popcll(lmask & below);
     float* jr = J9 + r * RW;
@@ -801,6 +809,12 @@ LGX_DEV void substep(Sh& s, const lgx_model* M_, const lgx_task_params* Pm_, con
     s.cbody[crank] = M->cand_body[lane];
   }
   if (lane == 0) { s.nrows = nrows; s.nlim = nlim; s.ncon = ncon; }
+#ifdef LGX_PHASE_CLOCK
+  if (lane == 0) {
+    s.phacc[16] = max(s.phacc[16], (uint32_t)nrows);
+    s.phacc[17] += nrows > AMAX ? 1u : 0u;
+  }
+#endif
   __syncthreads();
   PH(5);
 #if defined(LGX_DBG_STAGE) && LGX_DBG_STAGE == 3
@@ -854,40 +868,47 @@ LGX_DEV void substep(Sh& s, const lgx_model* M_, const lgx_task_params* Pm_, con
   return;
 #endif
   if (nrows <= AMAX) {
-    // ---- A = J M⁻¹ Jᵀ, packed lower: lane r writes column r from row r down (entry (q, r) =
-    //      y_r·z_q + [leg_r = leg_q] J_l,r·g_q; J_l,r = 0 for rows without a leg part)
+    // ---- A = J M⁻¹ Jᵀ: lane r writes column r (A is symmetric; entry (q, r) = y_r·z_q +
+    //      [leg_r = leg_q] J_l,r·g_q; J_l,r = 0 for rows without a leg part)
     if (row_lane) {
 #pragma unroll 4
       for (int q = 0; q < nrows; ++q) {
         const float* zg = ZG + q * RW;
         const float v = yr[0] * zg[0] + yr[1] * zg[1] + yr[2] * zg[2] + yr[3] * zg[3] + yr[4] * zg[4] + yr[5] * zg[5];
         const float vl = jlr[0] * zg[6] + jlr[1] * zg[7] + jlr[2] * zg[8];
-        if (q >= lane) Am[pk_lo(q, lane)] = v + (s.rleg[q] == lr ? vl : 0.f);
+        Am[q * nrows + lane] = v + (s.rleg[q] == lr ? vl : 0.f);
       }
     }
     __syncthreads();
     PH(7);
     // ---- projected Gauss-Seidel on A (oracle_physics.c step 4). Rows are [nlim joint
-    //      limits | ncon × (normal, tangent, tangent)]. Lane r keeps the row velocity
-    //      w_r = J_r u and λ_r; a row update is readlanes + a scalar projection + one FMA
-    //      per lane with column `lane` of A row r. A contact's three A rows are loaded
-    //      one contact ahead.
+    //      limits | ncon × (normal, tangent, tangent)]. Lane r keeps its row's velocity
+    //      w_r = J_r u, λ_r and constants; every lane forms its own row's candidate update
+    //      and only the row being swept keeps it (a select), so a row costs one readlane of
+    //      its Δλ, broadcast into w += A[·][r] Δλ. The tangent pair trades its two candidates
+    //      between neighbouring lanes by DPP for the friction-disk norm. A contact's three
+    //      A columns are loaded one contact ahead.
     float w = w0, lam = 0.f;
     const float mu = s.mu;
     auto rd = [](float v, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); };
-    // per-row constants live in their row's lane (readlane, no LDS round trip in the sweep)
+    auto wave_shl1 = [](float v) {  // lane x receives lane x + 1 (wave-wide shift)
+      return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xf, 0xf, false));
+    };
+    auto wave_shr1 = [](float v) {  // lane x receives lane x - 1
+      return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xf, 0xf, false));
+    };
     const float tg = row_lane ? s.tgt[lane] : 0.f;
     const float ia = row_lane ? 1.0f / s.Arr[lane] : 0.f;
     const int rlast = nrows - 3;  // first row of the last contact
     const int lc = min(lane, nrows - 1);  // lanes past the rows read a valid (unused) entry
-    auto arow = [&](int r) { return Am[lc <= r ? pk_lo(r, lc) : pk_lo(lc, r)]; };  // A[r][lane]
+    auto arow = [&](int r) { return Am[r * nrows + lc]; };  // A[r][lane]
     for (int it = 0; it < Pm->solver_iterations; ++it) {
       for (int r = 0; r < nlim; ++r) {
         const float a0 = arow(r);
-        const float wr = rd(w, r), lo = rd(lam, r);
-        const float ln = fmaxf(0.f, lo + (rd(tg, r) - wr) * rd(ia, r));
-        if (lane == r) lam = ln;
-        w += a0 * (ln - lo);
+        const float cand = fmaxf(0.f, lam + (tg - w) * ia);
+        const float d = rd(cand - lam, r);
+        lam = lane == r ? cand : lam;
+        w += a0 * d;
       }
       if (ncon == 0) continue;
       float n0 = arow(nlim), n1 = arow(nlim + 1), n2 = arow(nlim + 2);
@@ -898,22 +919,25 @@ LGX_DEV void substep(Sh& s, const lgx_model* M_, const lgx_task_params* Pm_, con
         n1 = arow(rn + 1);
         n2 = arow(rn + 2);
         // normal row
-        const float wr = rd(w, r), lo = rd(lam, r);
-        const float ln = fmaxf(0.f, lo + (rd(tg, r) - wr) * rd(ia, r));
-        if (lane == r) lam = ln;
-        w += a0 * (ln - lo);
+        const float cand = fmaxf(0.f, lam + (tg - w) * ia);
+        const float d = rd(cand - lam, r);
+        lam = lane == r ? cand : lam;
+        w += a0 * d;
         // tangent pair, projected onto the friction disk |λ_t| <= μ λ_n
-        const float lim = mu * ln;
-        const float o1 = rd(lam, r + 1), o2 = rd(lam, r + 2);
-        float l1 = o1 - rd(w, r + 1) * rd(ia, r + 1);
-        float l2 = o2 - rd(w, r + 2) * rd(ia, r + 2);
-        const float nn = l1 * l1 + l2 * l2;
+        const float lim = mu * rd(lam, r);
+        const float l = lam - w * ia;
+        // both shifts with every lane active (a DPP source lane outside EXEC reads 0), then
+        // the select: lane r + 1 takes r + 2's candidate, lane r + 2 takes r + 1's
+        float from_next = wave_shl1(l), from_prev = wave_shr1(l);
+        __asm__ volatile("" : "+v"(from_next), "+v"(from_prev));
+        const float other = lane == r + 1 ? from_next : from_prev;
+        const float nn = l * l + other * other;
         const float sc = nn > lim * lim ? lim * __builtin_amdgcn_rsqf(nn) : 1.0f;
-        l1 *= sc;
-        l2 *= sc;
-        if (lane == r + 1) lam = l1;
-        if (lane == r + 2) lam = l2;
-        w += a1 * (l1 - o1) + a2 * (l2 - o2);
+        const float lt = l * sc;
+        const float dl = lt - lam;
+        const float d1 = rd(dl, r + 1), d2 = rd(dl, r + 2);
+        lam = (lane == r + 1 || lane == r + 2) ? lt : lam;
+        w += a1 * d1 + a2 * d2;
       }
     }
     if (row_lane) s.lam[lane] = lam;
@@ -1496,7 +1520,7 @@ __global__ __launch_bounds__(64, ACTNET ? LGX_SEA_WAVES : 4) void env_step_kerne
     s.fat_prev[lane] = B.feet_air_time ? B.feet_air_time[e * Pm->num_feet + lane] : 0.f;
   }
 #ifdef LGX_PHASE_CLOCK
-  if (lane < 16) s.phacc[lane] = 0u;
+  if (lane < 20) s.phacc[lane] = 0u;
   if (lane == 0) s.phlast = clock64();
 #endif
   __syncthreads();

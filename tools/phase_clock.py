@@ -49,10 +49,11 @@ def run():
     env, _ = task_registry.make_env(task, a, env_cfg)
     L = _native.lib()
     L.lgx_debug_phase_buffer.argtypes = [C.c_void_p]
-    buf = torch.zeros(n, 16, dtype=torch.int32, device="cuda:0")
+    buf = torch.zeros(n, 20, dtype=torch.int32, device="cuda:0")
     g = torch.Generator(device="cuda:0").manual_seed(1234)
     stream = torch.cuda.current_stream()
-    acc = torch.zeros(n, 16, dtype=torch.float64, device="cuda:0")
+    acc = torch.zeros(n, 20, dtype=torch.float64, device="cuda:0")
+    rows = []
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ms = 0.0
     for i in range(20 + k):
@@ -68,8 +69,13 @@ def run():
             torch.cuda.synchronize()
             ms += s.elapsed_time(e)
             acc += buf.double().remainder(2 ** 32)
+            rows.append(buf[:, 16].clone())
     acc /= k
-    tot = acc.sum(dim=1)
+    tot = acc[:, :16].sum(dim=1)
+    r = torch.stack(rows).float()
+    print("constraint rows per env step (max over substeps): mean %.1f p50 %.0f p90 %.0f p99 %.0f max %.0f; "
+          "wide-path (> AMAX rows) substeps: %.2f %%" % (r.mean(), r.median(), torch.quantile(r, 0.9),
+                                                         torch.quantile(r, 0.99), r.max(), acc[:, 17].mean() / 4 * 100))
     print(f"task {task} N={n}: kernel {ms / k * 1e3:.1f} us/launch; wave total cycles mean {tot.mean():.0f} "
           f"p50 {tot.median():.0f} p90 {torch.quantile(tot, 0.9):.0f} (s_memtime clock)")
     print(f"{'phase':18s} {'mean':>9s} {'p50':>9s} {'p90':>9s} {'share':>6s}")
