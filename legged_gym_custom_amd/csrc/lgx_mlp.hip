@@ -45,6 +45,9 @@ constexpr int BM = 128, BKS = 32, NT = 256;
 #ifndef LGX_PF
 #define LGX_PF 2
 #endif
+#ifndef LGX_MV_ROWMAJOR
+#define LGX_MV_ROWMAJOR 1
+#endif
 constexpr int PF = LGX_PF;               // global-load register sets (prefetch depth in K steps)
 constexpr int PITCH = BKS;               // bf16 per LDS row (64 B, swizzled: lds_off)
 constexpr int A_ELEMS = BM * PITCH;      // one A image (hi or lo)
@@ -91,9 +94,14 @@ struct Stager {
   static constexpr int T = ROWS / 64;          // 8-k tasks per thread (KV)
   static constexpr int KG = ROWS / 32;         // k per thread (MV)
   static constexpr int NKQ = BKS / KG;         // k groups per step (MV): 8 or 16
-  // MV thread map: kq = tid % NKQ (k group), rg = tid / NKQ (4-row group): a wave's load
-  // instruction covers NKQ source rows (k) x 64 B or more, and each store's NKQ lanes fill
-  // one 64-B LDS row
+  // MV thread map. LGX_MV_ROWMAJOR (default): rg = tid % NRG (4-row group), kq = tid / NRG
+  // (k group): consecutive lanes read consecutive 16 B of one source row (k), so a wave's
+  // load is 2 (ROWS 128) or 4 (ROWS 64) fully contiguous row segments — the texture path
+  // coalesces it. Otherwise kq = tid % NKQ, rg = tid / NKQ: a load covers NKQ source rows
+  // x 64 B (4x the L1 accesses, measured) and each store's NKQ lanes fill one 64-B LDS row.
+  static constexpr int NRG = ROWS / 4;
+  __device__ __forceinline__ static int mv_kq(int tid) { return LGX_MV_ROWMAJOR ? tid / NRG : tid % NKQ; }
+  __device__ __forceinline__ static int mv_rg(int tid) { return LGX_MV_ROWMAJOR ? tid % NRG : tid / NKQ; }
 
   // Rows past the M/N edge are clamped to a valid row (their products only reach outputs
   // that are never stored), so loads stay vectorised at the edges; KGUARD (the last,
@@ -119,7 +127,7 @@ struct Stager {
         }
       }
     } else {  // MV / MVE
-      const int kq = tid % NKQ, rg = tid / NKQ;
+      const int kq = mv_kq(tid), rg = mv_rg(tid);
       const int k = k0 + kq * KG;
       if (MODE == MV || row0 + ROWS <= rows) {
         // MV: rows % 4 == 0 (host), so a 4-row group is all valid or all past the edge;
@@ -159,7 +167,7 @@ struct Stager {
       *reinterpret_cast<bf16x8*>(hi + off) = h;
       *reinterpret_cast<bf16x8*>(lo + off) = l;
     } else {
-      const int kq = tid % NKQ, rg = tid / NKQ;
+      const int kq = mv_kq(tid), rg = mv_rg(tid);
       const int kb = kq * KG;  // first k of this thread inside the step
       const int e = q;
       const int off = lds_off(rg * 4 + e, kb >> 3) + (kb & 7);
@@ -327,7 +335,7 @@ __device__ __forceinline__ void gemm_tile(const Params& p, const int L) {
     if (tn == 0) {
       static_assert(AM == MV || AM == MVE, "colsum needs the m-contiguous A stager");
       constexpr int SLOTS = SA::NKQ;
-      const int kq = tid % SLOTS, rg = tid / SLOTS;
+      const int kq = SA::mv_kq(tid), rg = SA::mv_rg(tid);
 #pragma unroll
       for (int e = 0; e < 4; ++e) cs[kq * BM + rg * 4 + e] = csum[e];
       __syncthreads();
