@@ -56,11 +56,15 @@ enum Mode { KV = 1, MV = 3, MVE = 4 };  // MVE: MV for a row count that is not a
 typedef float f32x4u __attribute__((ext_vector_type(4), aligned(4)));  // 4-B aligned float4
 
 // bf16 offset of 16-B chunk c (0..3) of row r in an LDS image: adjacent rows swap when
-// bit 2 of r is set (rows 4 apart land on opposite bank halves: MV stores), and the chunk
-// index is XORed with bits 1 and 3 of the physical row (ds_read_b128 lane groups).
+// bit 2 of r is set, and the chunk index is XORed with (b3, b3 ^ b4) of the physical row.
+// Found by exhaustive search over XOR swizzles (bank model of MI355X_MICROARCH.md §LDS):
+// the fragment reads (ds_read_b128) and the k-contiguous stores (ds_write_b128) are
+// conflict-free, the m/n-contiguous stores (ds_write_b64 / _b32, lane-contiguous rows)
+// 2-way (the old swizzle: 4-way).
 __device__ __forceinline__ int lds_off(int r, int c) {
   const int pr = r ^ ((r >> 2) & 1);
-  return pr * PITCH + 8 * (c ^ (((pr >> 1) & 1) | (((pr >> 3) & 1) << 1)));
+  const int b3 = (pr >> 3) & 1, b4 = (pr >> 4) & 1;
+  return pr * PITCH + 8 * (c ^ (b3 | ((b3 ^ b4) << 1)));
 }
 
 struct Params {
