@@ -85,11 +85,25 @@ def learner_gemm_roofline(dev, rows=24576, reps=10):
     t = s.elapsed_time(e) / reps * 1e-3
     flop = 2.0 * rows * sum(i * o for i, o in layers)
     achieved = 3 * flop / t / 1e12
-    return {"bound": "mfma", "kernel": "lgxm::gemm_group_kernel<2, 128> + splitk_reduce_batch",
-            "workload": f"all 17 weight gradients of one go2 minibatch ({rows} rows)", "achieved": round(achieved, 1),
-            "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4),
-            "us_per_launch": round(t * 1e6, 1), "fp32_equivalent_tflops": round(flop / t / 1e12, 1),
+    # algorithmic HBM bytes: every activation (X) and output gradient (dY) of the minibatch
+    # read once (fp32), every dW/db read and written once (accumulate)
+    nbytes = 4.0 * rows * sum(i + o for i, o in layers) + 2 * 4.0 * sum(i * o + o for i, o in layers)
+    gbs = nbytes / t / 1e9
+    # the binding roofline is the larger of the two ideal times (here HBM: 657 MB at 8 TB/s
+    # = 82 us vs 168 bf16 GFLOP at 2.5 PF/s = 67 us)
+    t_hbm, t_mfma = nbytes / (HBM_PEAK_GBS * 1e9), 3 * flop / (MFMA_BF16_PEAK_TFLOPS * 1e12)
+    mfma = {"achieved": round(achieved, 1), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4), "fp32_equivalent_tflops": round(flop / t / 1e12, 1),
             "note": "3xbf16 split: 3 bf16 MFMA products per fp32 multiply-add"}
+    hbm = {"achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
+           "algorithmic_bytes": int(nbytes)}
+    top = dict(hbm if t_hbm >= t_mfma else mfma)
+    top.pop("note", None)
+    return {"bound": "hbm" if t_hbm >= t_mfma else "mfma",
+            "kernel": "lgxm::gemm_group_kernel<2, 128> + splitk_reduce_batch",
+            "workload": f"all 17 weight gradients of one go2 minibatch ({rows} rows)", **top,
+            "us_per_launch": round(t * 1e6, 1), "ideal_us": {"hbm": round(t_hbm * 1e6, 1), "mfma": round(t_mfma * 1e6, 1)},
+            "hbm": hbm, "mfma": mfma}
 
 
 def committed_traffic(num_envs):

@@ -704,9 +704,14 @@ struct HeadRow {
 __device__ __forceinline__ HeadRow head_row(const lgx_ppo_head_args& p, int i, const float* stdv, const float* lstd) {
   const float l2pi = 0.9189385332046727f;  // log(sqrt(2 pi))
   float lp = 0.f;
-  for (int j = 0; j < p.A; ++j) {
-    const float d = p.actions[(int64_t)i * p.A + j] - p.mu[(int64_t)i * p.A + j];
-    lp += -(d * d) / (2.f * stdv[j] * stdv[j]) - lstd[j] - l2pi;
+  // unrolled to the action bound with a guard (same summation order): every row load is
+  // issued before the first use instead of one load round trip per action
+#pragma unroll
+  for (int j = 0; j < HMAXA; ++j) {
+    if (j < p.A) {
+      const float d = p.actions[(int64_t)i * p.A + j] - p.mu[(int64_t)i * p.A + j];
+      lp += -(d * d) / (2.f * stdv[j] * stdv[j]) - lstd[j] - l2pi;
+    }
   }
   HeadRow r;
   r.logp = lp;
@@ -734,10 +739,13 @@ __device__ __forceinline__ void ppo_head_fwd_body(const lgx_ppo_head_args& p) {
       v[1] += (R - val) * (R - val);
     }
     float kl = 0.f;
-    for (int j = 0; j < p.A; ++j) {
-      const float os = p.old_sigma[(int64_t)i * p.A + j], om = p.old_mu[(int64_t)i * p.A + j];
-      const float dm = om - p.mu[(int64_t)i * p.A + j];
-      kl += logf(stdv[j] / os + 1.0e-5f) + (os * os + dm * dm) / (2.f * (stdv[j] * stdv[j])) - 0.5f;
+#pragma unroll
+    for (int j = 0; j < HMAXA; ++j) {
+      if (j < p.A) {
+        const float os = p.old_sigma[(int64_t)i * p.A + j], om = p.old_mu[(int64_t)i * p.A + j];
+        const float dm = om - p.mu[(int64_t)i * p.A + j];
+        kl += logf(stdv[j] / os + 1.0e-5f) + (os * os + dm * dm) / (2.f * (stdv[j] * stdv[j])) - 0.5f;
+      }
     }
     v[2] += kl;
   }
@@ -842,9 +850,12 @@ __device__ __forceinline__ float aux_row_sq(const lgx_aux_loss_args& p, int64_t 
     const int w = min(AUX_CW, p.L - j0);
     aux_stage_p(p, ldp, i0, j0, w, st);
     if (i < p.B)
-      for (int j = 0; j < w; ++j) {
-        const float d = st[threadIdx.x * (AUX_CW + 1) + j] - p.a[(int64_t)i * p.L + j0 + j];
-        s += d * d;
+#pragma unroll
+      for (int j = 0; j < AUX_CW; ++j) {
+        if (j < w) {
+          const float d = st[threadIdx.x * (AUX_CW + 1) + j] - p.a[(int64_t)i * p.L + j0 + j];
+          s += d * d;
+        }
       }
   }
   return s;
@@ -861,6 +872,7 @@ __device__ __forceinline__ void aux_loss_fwd_body(const lgx_aux_loss_args& p) {
     if (i >= p.B) continue;
     v[0] += sqrtf(s);
     float q = 0.f;
+#pragma unroll 4
     for (int j = 0; j < p.E; ++j) {
       const float d = p.e[(int64_t)i * p.E + j] - p.t[(int64_t)i * p.E + j];
       q += d * d;
@@ -892,10 +904,13 @@ __device__ __forceinline__ void aux_loss_bwd_body(const lgx_aux_loss_args& p) {
     const int w = min(AUX_CW, p.L - j0);
     aux_stage_p(p, ldp, i0, j0, w, st);
     if (i < p.B)
-      for (int j = 0; j < w; ++j)
-        p.dp[(int64_t)i * p.L + j0 + j] = k * (st[threadIdx.x * (AUX_CW + 1) + j] - p.a[(int64_t)i * p.L + j0 + j]);
+#pragma unroll
+      for (int j = 0; j < AUX_CW; ++j)
+        if (j < w)
+          p.dp[(int64_t)i * p.L + j0 + j] = k * (st[threadIdx.x * (AUX_CW + 1) + j] - p.a[(int64_t)i * p.L + j0 + j]);
   }
   if (i >= p.B) return;
+#pragma unroll 4
   for (int j = 0; j < p.E; ++j)
     p.de[(int64_t)i * p.E + j] = ge * 2.f * (p.e[(int64_t)i * p.E + j] - p.t[(int64_t)i * p.E + j]);
 }
@@ -916,13 +931,22 @@ __global__ void loss_heads_bwd(lgx_ppo_head_args h, lgx_aux_loss_args a) {
 }
 
 // ---------------------------------------------------------------- PPO minibatch optimizer tail
-constexpr int TAIL_BLOCKS = 512;
+#ifndef LGX_TAIL_BLOCKS
+#define LGX_TAIL_BLOCKS 128
+#endif
+constexpr int TAIL_BLOCKS = LGX_TAIL_BLOCKS;  // each block ends with a release + counter atomic
 
+// four independent partial sums (loads in flight together), combined in a fixed order
 __device__ __forceinline__ float sumsq_range(const float* __restrict__ g, int64_t lo, int64_t hi, int64_t i0,
                                              int64_t stride) {
-  float s = 0.f;
-  for (int64_t i = lo + i0; i < hi; i += stride) s += g[i] * g[i];
-  return s;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  int64_t i = lo + i0;
+  for (; i + 3 * stride < hi; i += 4 * stride) {
+    const float a = g[i], b = g[i + stride], c = g[i + 2 * stride], d = g[i + 3 * stride];
+    s0 += a * a; s1 += b * b; s2 += c * c; s3 += d * d;
+  }
+  for (; i < hi; i += stride) s0 += g[i] * g[i];
+  return (s0 + s1) + (s2 + s3);
 }
 
 // grid TAIL_BLOCKS: squared norms (estimator; main + adaptation) -> the last block turns
