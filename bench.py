@@ -11,8 +11,9 @@ value = num_envs x 24 x world_size x K / (max over ranks of the timed K iteratio
 Also reported: `roofline` of the env-step kernel (algorithmic bytes per launch over its
 HIP-event-timed duration vs 8 TB/s HBM; the kernel is not HBM-bound: `roofline_valu` gives
 its VALU issue utilisation from the committed PMC profile), `roofline_learner`, and
-`cpu_baseline`: the CPU oracle (C port of the same env step, OpenMP over envs) + torch-CPU
-learner at the same shape (one iteration), rank 0 at N=1 only.
+`cpu_baseline`: the same framework on the host (--sim_device=cpu --rl_device=cpu: liblgx.so's
+host backend, OpenMP over envs, + the torch-CPU learner) at the same shape (one iteration),
+rank 0 at N=1 only.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--num_envs 4096]
   N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -150,35 +151,33 @@ def committed_valu(num_envs):
 
 
 def cpu_baseline(num_envs=4096, iters=1, steps_per_env=24):
-    """Oracle env step (C, OpenMP over envs) + torch-CPU rsl_rl learner, same runner, at the
-    benchmark's shape (C2: 4096 envs x 24 steps), one timed iteration after a warm-up one, on
-    the host threads this process may use (OMP_NUM_THREADS; 16 per GPU on the GPU box)."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import cpu_env
-    from legged_gym_custom_amd import model as mdl, params as prm
-    from legged_gym_custom_amd.envs import task_registry_configs
-    from legged_gym_custom_amd.rsl_rl.runners import OnPolicyRunner
-    from legged_gym_custom_amd.utils.helpers import class_to_dict
-    cfg, tcfg = task_registry_configs("go2")
-    cfg.env.num_envs = num_envs
-    m = mdl.load_model(cfg.asset.file, cfg.asset.foot_name)
-    P = prm.build_task_params(cfg, m, num_envs)
-    env = cpu_env.OracleVecEnv(cfg, m, P, mdl.to_struct(m))
-    tcfg.runner.num_steps_per_env = steps_per_env
+    """The same framework on the host: `--sim_device=cpu --rl_device=cpu` (helpers.py:174-177)
+    — liblgx.so's host backend (OpenMP over envs) for the env step and the torch-CPU rsl_rl
+    learner, through the same task registry and runner, at the benchmark's shape (C2: 4096 envs
+    x 24 steps); one timed iteration after a warm-up one, on the host threads this process may
+    use (OMP_NUM_THREADS; 16 per GPU on the GPU box)."""
+    from legged_gym_custom_amd.envs import task_registry
+    from legged_gym_custom_amd.utils.helpers import get_args
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
-    os.environ["OMP_NUM_THREADS"] = str(threads)  # the oracle's OpenMP env loop
     torch.set_num_threads(threads)
-    torch.manual_seed(1)
-    runner = OnPolicyRunner(env, class_to_dict(tcfg), None, device="cpu")
+    a = get_args(["--task=go2", "--headless", f"--num_envs={num_envs}", "--sim_device=cpu", "--rl_device=cpu",
+                  "--seed=1"])
+    env, _ = task_registry.make_env("go2", a)
+    _, tcfg = task_registry.get_cfgs("go2")
+    tcfg.runner.num_steps_per_env = steps_per_env
+    runner, _ = task_registry.make_alg_runner(env, args=a, train_cfg=tcfg, log_root=None)
     runner.learn(1, init_at_random_ep_len=True)  # warm-up (also a DAgger iteration: it=0)
     t0 = time.time()
     runner.learn(iters)
     dt = time.time() - t0
+    perf = dict(runner.last_perf)
     return {"value": round(num_envs * steps_per_env * iters / dt, 1), "unit": "env-steps/s", "cores": threads,
             "kind": "port",
-            "sample": f"{iters} PPO iteration(s) of Go2 flat at {num_envs} envs x {steps_per_env} steps on the host: "
-                      f"oracle/lgx_oracle.c env step (OpenMP over envs) + torch-CPU learner, {threads} threads",
-            "seconds": round(dt, 2)}
+            "sample": f"{iters} PPO iteration(s) of Go2 flat at {num_envs} envs x {steps_per_env} steps on the host "
+                      f"(--sim_device=cpu --rl_device=cpu): liblgx.so host-backend env step (OpenMP) + torch-CPU "
+                      f"learner, {threads} threads",
+            "seconds": round(dt, 2), "collection_s": round(perf.get("collection_time", 0.0), 3),
+            "learn_s": round(perf.get("learn_time", 0.0), 3)}
 
 
 def main():

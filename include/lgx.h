@@ -280,7 +280,12 @@ int64_t lgx_sizeof_model(void);
 int64_t lgx_sizeof_task_params(void);
 int64_t lgx_sizeof_buffers(void);
 
-/* device >= 0: HIP device ordinal. */
+/* device >= 0: HIP device ordinal; every bound buffer is device memory, work is
+ * stream-ordered on the stream passed to each call.
+ * device < 0: the host backend (the reference's --sim_device=cpu, helpers.py:174-177):
+ * the same step on the CPU, OpenMP over envs (OMP_NUM_THREADS), every bound buffer and the
+ * lgx_step_dev / lgx_episode_extras counters are host memory, stream arguments are ignored
+ * and each call returns when its work is done. */
 int lgx_create(const lgx_model* model, const lgx_task_params* params, int32_t device, lgx_env** out);
 int lgx_bind(lgx_env* env, const lgx_buffers* buffers);
 /* one env step: decimation physics substeps + post-physics. step_counter is the

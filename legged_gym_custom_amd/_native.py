@@ -1,6 +1,7 @@
 """ctypes binding of liblgx.so (include/lgx.h). The product path calls ONLY this
-library for the env step; if it is missing or no HIP device is present, it raises —
-there is no CPU fallback."""
+library for the env step; if it is missing it raises. A HIP device index runs the
+kernels (buffers on that device); device -1 runs the library's host backend (buffers in
+host memory) — chosen explicitly by --sim_device=cpu, never as a fallback."""
 import ctypes as C
 import os
 
@@ -55,6 +56,8 @@ class NativeEnv:
         self._L = lib()
         self.model = model_struct
         self.params = params_struct
+        self.device_index = int(device_index)
+        self._dev_type = "cpu" if self.device_index < 0 else "cuda"
         self.handle = C.c_void_p()
         rc = self._L.lgx_create(C.byref(model_struct), C.byref(params_struct), device_index, C.byref(self.handle))
         self._check(rc, "lgx_create")
@@ -67,7 +70,8 @@ class NativeEnv:
             raise LgxError(f"{what} failed ({rc}): {msg}")
 
     def bind(self, tensors):
-        """tensors: dict field -> torch tensor (contiguous, on the HIP device) or None."""
+        """tensors: dict field -> torch tensor (contiguous; on the HIP device, or on the CPU for
+        device -1) or None."""
         for name in _abi.BUFFER_FIELDS:
             t = tensors.get(name)
             if t is None:
@@ -75,8 +79,9 @@ class NativeEnv:
                 continue
             if not t.is_contiguous():
                 raise LgxError(f"buffer {name} must be contiguous")
-            if t.device.type != "cuda":
-                raise LgxError(f"buffer {name} must live on the HIP device (got {t.device})")
+            if t.device.type != self._dev_type:
+                where = "host memory (device -1)" if self._dev_type == "cpu" else "the HIP device"
+                raise LgxError(f"buffer {name} must live in {where} (got {t.device})")
             setattr(self.buffers, name, t.data_ptr())
             self._keep[name] = t
         self._check(self._L.lgx_bind(self.handle, C.byref(self.buffers)), "lgx_bind")

@@ -1,5 +1,6 @@
 """Build the HIP libraries in-tree for gfx950 with hipcc:
-  lib/liblgx.so      env step (csrc/lgx_env.hip, include/lgx.h)
+  lib/liblgx.so      env step (csrc/lgx_env.hip, include/lgx.h) + its host backend
+                     (csrc/lgx_env_host.cpp, g++ -fopenmp, linked in: lgx_create(device=-1))
   lib/liblgx_mlp.so  learner MLP GEMMs (csrc/lgx_mlp.hip, include/lgx_mlp.h)"""
 import os
 import subprocess
@@ -9,7 +10,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 INC = os.path.join(os.path.dirname(HERE), "include")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 LIBS = {
-    "liblgx.so": (["lgx_env.hip"], ["lgx_device.h"], ["lgx.h"]),
+    "liblgx.so": (["lgx_env.hip"], ["lgx_device.h", "lgx_host.h", "lgx_env_host.cpp"], ["lgx.h"]),
     "liblgx_mlp.so": (["lgx_mlp.hip"], [], ["lgx_mlp.h"]),
 }
 OUT = os.path.join(HERE, "lib", "liblgx.so")
@@ -31,16 +32,38 @@ def needs_build(name="liblgx.so"):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+def _host_objects(name, verbose):
+    """liblgx.so's host backend: compiled by g++ with OpenMP (libgomp, as torch's CPU ops)."""
+    if name != "liblgx.so":
+        return []
+    src = os.path.join(HERE, "csrc", "lgx_env_host.cpp")
+    obj = os.path.join(HERE, "lib", "lgx_env_host.o")
+    cmd = ["g++", "-O3", "-std=c++17", "-fPIC", "-fopenmp", "-ffp-contract=off", "-fno-fast-math", "-Wall",
+           "-c", "-o", obj, src]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    gomp = subprocess.run(["g++", "-print-file-name=libgomp.so"], check=True, capture_output=True,
+                          text=True).stdout.strip()
+    return [obj, gomp]
+
+
 def build_one(name, force=False, verbose=False):
     src, _, out = _paths(name)
     if not force and not needs_build(name):
         return out
     os.makedirs(os.path.dirname(out), exist_ok=True)
-    cmd = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-ffp-contract=off", "-o", out + ".tmp"] + src
-    if verbose:
-        print(" ".join(cmd))
-    subprocess.run(cmd, check=True)
+    hip = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off"]
+    extra = _host_objects(name, verbose)
+    if extra:  # compile the HIP source alone (hipcc reads inputs after a .hip file as HIP), then link
+        obj = out[:-3] + "_hip.o"
+        cmds = [hip + ["-c", "-o", obj] + src, ["hipcc", "-shared", "-o", out + ".tmp", obj] + extra]
+    else:
+        cmds = [hip + ["-shared", "-o", out + ".tmp"] + src]
+    for cmd in cmds:
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.run(cmd, check=True)
     os.replace(out + ".tmp", out)
     return out
 

@@ -21,6 +21,7 @@
 
 #include "../../include/lgx.h"
 #include "lgx_device.h"
+#include "lgx_host.h"
 
 namespace lgx {
 
@@ -1861,6 +1862,8 @@ __global__ __launch_bounds__(64) void reset_kernel(const lgx_task_params* __rest
 }  // namespace lgx
 
 // ============================================================== C ABI
+#include <stdio.h>
+
 #include <string>
 
 struct lgx_env {
@@ -1871,6 +1874,7 @@ struct lgx_env {
   lgx_task_params* d_params = nullptr;
   lgx_buffers* d_buffers = nullptr;  // device copy of `buffers` (kernels read pointers from it)
   int device = 0;
+  bool host = false;         // device < 0: the host backend (lgx_env_host.cpp), host buffers
   bool bound = false;
   bool stats_clean = false;  // episode_stats zeroed by lgx_episode_extras and not written since
   std::string err;
@@ -1917,6 +1921,35 @@ int lgx_create(const lgx_model* model, const lgx_task_params* params, int32_t de
   if (params->num_proprio > LGX_MAX_PROPRIO || params->num_height_points > LGX_MAX_HEIGHT_POINTS)
     return fail(env, "observation too large");
   if (params->num_reward_terms + 1 > 64) return fail(env, "too many reward terms");
+  // observation layout the step writes (go2.py:467-574 / legged_robot.py:240-273): obs =
+  // [history (H x P) | current (P)]; Go2 critic = [obs | priv | est (3) | scan]. A config whose
+  // declared sizes disagree (the reference's anymal_c_flat: 48-wide obs, 235-wide proprio)
+  // fails here — the reference fails at its first compute_observations (torch.cat shapes).
+  {
+    const lgx_task_params& p = *params;
+    const int D = p.num_dof, A = p.num_actions;
+    const int want_p = p.task_kind == LGX_TASK_GO2 ? 8 + 2 * D + A + 8
+                                                   : 12 + 2 * D + A + (p.measure_heights ? p.num_height_points : 0);
+    char msg[256];
+    if (p.num_proprio != want_p) {
+      snprintf(msg, sizeof msg, "num_proprio %d != %d (the observation terms of this task)", p.num_proprio, want_p);
+      return fail(env, msg);
+    }
+    if (p.num_obs != (p.history_len + 1) * p.num_proprio) {
+      snprintf(msg, sizeof msg, "num_observations %d != (history_buffer_length + 1) * num_proprio = %d", p.num_obs,
+               (p.history_len + 1) * p.num_proprio);
+      return fail(env, msg);
+    }
+    if (p.task_kind == LGX_TASK_GO2 &&
+        (p.num_priv != 5 + 2 * D || p.num_est != 3 || p.num_scan > p.num_height_points ||
+         p.num_critic != p.num_obs + p.num_priv + p.num_est + p.num_scan))
+      return fail(env, "Go2 privileged/estimated/scan/critic observation sizes do not match the step's layout");
+    if (p.num_feet > LGX_MAX_FEET) return fail(env, "too many feet");
+  }
+  if (device < 0) {  // host backend: no device state; every buffer is host memory
+    env->host = true;
+    return 0;
+  }
   HIP_OK(hipSetDevice(device));
   HIP_OK(hipMalloc(&env->d_model, sizeof(lgx_model)));
   HIP_OK(hipMalloc(&env->d_params, sizeof(lgx_task_params)));
@@ -1956,6 +1989,11 @@ int lgx_bind(lgx_env* env, const lgx_buffers* b) {
   if (env->params.curriculum && (!b->terrain_levels || !b->terrain_types || !b->terrain_origins))
     return fail(env, "lgx_bind: terrain curriculum needs terrain_levels/terrain_types/terrain_origins");
   env->buffers = *b;
+  if (env->host) {
+    env->bound = true;
+    env->stats_clean = false;
+    return 0;
+  }
   HIP_OK(hipSetDevice(env->device));
   HIP_OK(hipMemcpy(env->d_buffers, b, sizeof(lgx_buffers), hipMemcpyHostToDevice));
   env->bound = true;
@@ -1970,6 +2008,13 @@ static int launch_step(lgx_env* env, uint64_t seed, uint64_t step, const uint64_
   hipStream_t st = (hipStream_t)stream;
   const int N = env->params.num_envs;
   const int KS = env->params.num_reward_terms + (env->params.has_termination_reward ? 1 : 0);
+  if (env->host) {
+    if (env->buffers.episode_stats && !env->stats_clean)
+      for (int k = 0; k <= KS; ++k) env->buffers.episode_stats[k] = 0.f;
+    env->stats_clean = false;
+    lgxh::step(&env->model, &env->params, &env->buffers, seed, step_dev ? *step_dev : step, physics);
+    return 0;
+  }
   if (env->buffers.episode_stats && !env->stats_clean)
     HIP_OK(hipMemsetAsync(env->buffers.episode_stats, 0, sizeof(float) * (KS + 1), st));
   env->stats_clean = false;
@@ -2009,6 +2054,13 @@ int lgx_reset_envs(lgx_env* env, const uint8_t* env_mask, uint64_t seed, uint64_
   if (!env_mask) return fail(env, "lgx_reset_envs: env_mask is NULL");
   hipStream_t st = (hipStream_t)hip_stream;
   const int KS = env->params.num_reward_terms + (env->params.has_termination_reward ? 1 : 0);
+  if (env->host) {
+    if (env->buffers.episode_stats && !env->stats_clean)
+      for (int k = 0; k <= KS; ++k) env->buffers.episode_stats[k] = 0.f;
+    env->stats_clean = false;
+    lgxh::reset(&env->params, &env->buffers, env_mask, seed, reset_call);
+    return 0;
+  }
   if (env->buffers.episode_stats && !env->stats_clean)
     HIP_OK(hipMemsetAsync(env->buffers.episode_stats, 0, sizeof(float) * (KS + 1), st));
   env->stats_clean = false;
@@ -2074,6 +2126,11 @@ int lgx_episode_extras(lgx_env* env, float* means, float* level_mean, uint8_t* t
   if (time_outs && (!b.reset || !b.time_out)) return fail(env, "lgx_episode_extras: time_outs needs reset/time_out");
   const int KS = env->params.num_reward_terms + (env->params.has_termination_reward ? 1 : 0);
   if (KS + 1 > 1024) return fail(env, "lgx_episode_extras: too many reward terms");
+  if (env->host) {
+    lgxh::episode_extras(&env->params, &b, means, level_mean, time_outs, step_dev);
+    env->stats_clean = true;
+    return 0;
+  }
   hipStream_t st = (hipStream_t)hip_stream;
   // torch divides a tensor by a Python scalar as a multiply by the fp32 reciprocal
   hipLaunchKernelGGL(lgx::extras_kernel, dim3(1), dim3(1024), 0, st, b.episode_stats, step_dev, KS,
@@ -2095,6 +2152,10 @@ const char* lgx_last_error(const lgx_env* env) { return env ? env->err.c_str() :
 
 void lgx_destroy(lgx_env* env) {
   if (!env) return;
+  if (env->host) {
+    delete env;
+    return;
+  }
   if (env->d_model) (void)hipFree(env->d_model);
   if (env->d_params) (void)hipFree(env->d_params);
   if (env->d_buffers) (void)hipFree(env->d_buffers);

@@ -3,7 +3,8 @@
 Same attributes and getters the runner reads (num_envs, num_obs, num_proprio,
 num_privileged_obs, num_critic_obs, num_estimated_obs, num_scan_obs,
 history_buffer_length, num_actions; get_*_observations; reset(); step()).
-The simulator handle is the MI355X env-step library (liblgx.so); there is no viewer.
+The simulator handle is the MI355X env-step library (liblgx.so: HIP kernels for
+sim_device=cuda:N, its host backend for sim_device=cpu); there is no viewer.
 """
 import sys
 
@@ -16,14 +17,17 @@ class BaseTask:
         self.physics_engine = physics_engine
         self.sim_device = sim_device
         dev = torch.device(sim_device)
-        if dev.type != "cuda":
-            raise RuntimeError(
-                f"sim_device={sim_device}: the env step runs only as HIP kernels on an MI355X "
-                "(liblgx.so); there is no CPU simulator. Use --sim_device=cuda:N.")
-        if not torch.cuda.is_available():
-            raise RuntimeError("no HIP device visible: liblgx.so needs an MI355X")
-        self.sim_device_id = dev.index if dev.index is not None else torch.cuda.current_device()
-        self.device = f"cuda:{self.sim_device_id}"
+        if dev.type == "cpu":
+            # --sim_device=cpu (helpers.py:174-177): liblgx.so's host backend, OpenMP over envs
+            self.sim_device_id = -1
+            self.device = "cpu"
+        elif dev.type == "cuda":
+            if not torch.cuda.is_available():
+                raise RuntimeError("no HIP device visible: --sim_device=cuda needs an MI355X (or use --sim_device=cpu)")
+            self.sim_device_id = dev.index if dev.index is not None else torch.cuda.current_device()
+            self.device = f"cuda:{self.sim_device_id}"
+        else:
+            raise RuntimeError(f"sim_device={sim_device}: use cuda:N (HIP kernels) or cpu (host backend)")
         self.headless = True  # rendering is out of scope (play/viewer)
         self.graphics_device_id = -1
 

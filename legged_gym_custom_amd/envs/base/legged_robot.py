@@ -2,7 +2,7 @@
 
 The whole env step (legged_robot.py:67-100: clip, decimation x {PD torque, simulate},
 post_physics_step, obs clip) is ONE HIP kernel launch of liblgx.so (lgx_step), one
-wavefront per env. This class owns the torch buffers (same names/shapes as the
+wavefront per env (--sim_device=cpu: the same entry point on the library's host backend). This class owns the torch buffers (same names/shapes as the
 reference, env-major), builds the model/params once, binds the buffers to the native
 env, and keeps the reference's Python-visible surface: step/reset/reset_idx, the
 8-tuple return, extras['time_outs'/'episode'], common_step_counter, buffer attributes.
@@ -56,7 +56,7 @@ class LeggedRobot(BaseTask):
         # step's number and lgx_episode_extras advances it), so a captured rollout replays with
         # the right step numbers; the host mirror follows
         self._csc += 1
-        self._native.step_dev(self.seed, self._step_dev, torch.cuda.current_stream(self.device).cuda_stream)
+        self._native.step_dev(self.seed, self._step_dev, self._stream())
         self._update_extras(advance_step=True)
         return (self.obs_buf, self.privileged_obs_buf, self.critic_obs_buf, self.estimated_obs_buf, self.scan_obs_buf,
                 self.rew_buf, self.reset_buf, self.extras)
@@ -67,7 +67,7 @@ class LeggedRobot(BaseTask):
             env_ids = env_ids.to(self.device)
         mask = torch.zeros(self.num_envs, dtype=torch.uint8, device=self.device)
         mask[env_ids] = 1
-        self._native.reset_envs(mask, self.seed, self._reset_calls, torch.cuda.current_stream(self.device).cuda_stream)
+        self._native.reset_envs(mask, self.seed, self._reset_calls, self._stream())
         self._reset_calls += 1
         self.reset_buf[env_ids] = True
         self._update_extras()
@@ -79,7 +79,7 @@ class LeggedRobot(BaseTask):
         cur, to = self.cfg.terrain.curriculum, self.cfg.env.send_timeouts
         self._native.episode_extras(self._episode_means, self._terrain_level_mean if cur else None,
                                     self._extras_time_outs if to else None,
-                                    torch.cuda.current_stream(self.device).cuda_stream,
+                                    self._stream(),
                                     self._step_dev if advance_step else None)
         self._publish_extras()
 
@@ -103,6 +103,10 @@ class LeggedRobot(BaseTask):
         if self.cfg.env.send_timeouts:
             self._extras_time_outs.copy_(torch.where(self.reset_buf.any(), self.time_out_buf, self._extras_time_outs))
         self._publish_extras()
+
+    def _stream(self):
+        """The HIP stream the env's launches are ordered on (0 for the host backend)."""
+        return torch.cuda.current_stream(self.device).cuda_stream if self.sim_device_id >= 0 else 0
 
     @property
     def common_step_counter(self):

@@ -1,5 +1,6 @@
-"""Bind one buffer layout to both the CPU oracle (numpy) and liblgx.so (torch on the GPU)
-so parity tests can run both on identical inputs and diff every field."""
+"""Bind one buffer layout to both the CPU oracle (numpy) and liblgx.so (torch on the GPU,
+or host tensors for the library's host backend, device="cpu") so parity tests can run both
+on identical inputs and diff every field."""
 import numpy as np
 
 import driver
@@ -10,8 +11,9 @@ def _torchable(v):
 
 
 class Twin:
-    def __init__(self, P, M_struct, num_reward_slots, terrain=None):
-        """terrain: None or (height_samples, mesh_words[, levels, types, origins])."""
+    def __init__(self, P, M_struct, num_reward_slots, terrain=None, device="cuda"):
+        """terrain: None or (height_samples, mesh_words[, levels, types, origins]);
+        device: "cuda" (HIP kernels) or "cpu" (liblgx.so's host backend, lgx_create(-1))."""
         import torch
         from legged_gym_custom_amd import _native
         self.torch = torch
@@ -20,8 +22,9 @@ class Twin:
             self.o.set_terrain(*terrain)
         self.t = {}
         for k, v in self.o.a.items():
-            self.t[k] = None if v is None else torch.from_numpy(_torchable(v).copy()).cuda()
-        self.native = _native.NativeEnv(M_struct, P, 0)
+            self.t[k] = None if v is None else torch.from_numpy(_torchable(v).copy()).to(device)
+        self.device = device
+        self.native = _native.NativeEnv(M_struct, P, 0 if device == "cuda" else -1)
         self.native.bind(self.t)
         self.P = P
 
@@ -46,7 +49,8 @@ class Twin:
         return v.view(self.o.a[k].dtype) if self.o.a[k] is not None else v
 
     def stream(self):
-        return self.torch.cuda.current_stream().cuda_stream
+        return self.torch.cuda.current_stream().cuda_stream if self.device == "cuda" else 0
 
     def sync(self):
-        self.torch.cuda.synchronize()
+        if self.device == "cuda":
+            self.torch.cuda.synchronize()

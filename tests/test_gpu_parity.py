@@ -14,11 +14,12 @@ import golden_util as G
 pytestmark = pytest.mark.gpu
 
 
-def _twin(n, task="go2", terrain=None, ter=None):
+def _twin(n, task="go2", terrain=None, ter=None, device="cuda"):
     from native_util import Twin
     from legged_gym_custom_amd import model as mdl
     cfg, m, P = G.go2_setup(n, task, terrain=ter)
-    return cfg, m, P, Twin(P, mdl.to_struct(m), P.num_reward_terms + P.has_termination_reward, terrain=terrain)
+    return cfg, m, P, Twin(P, mdl.to_struct(m), P.num_reward_terms + P.has_termination_reward, terrain=terrain,
+                           device=device)
 
 
 def _close(got, want, atol=1e-5, rtol=1e-5):
@@ -31,12 +32,18 @@ def _close(got, want, atol=1e-5, rtol=1e-5):
 @pytest.mark.parametrize("name,task", [("go2_flat_n64.npz", "go2"), ("go2_parkour_n64.npz", "go2_parkour"),
                                        ("anymal_c_rough_n64.npz", "anymal_c_rough")])
 def test_post_physics_matches_reference_golden(name, task):
+    golden_replay(name, task, "cuda")
+
+
+def golden_replay(name, task, device):
+    """Replay a golden fixture through lgx_reset_envs + lgx_post_physics on `device`
+    ("cuda": the HIP kernels; "cpu": liblgx.so's host backend)."""
     from native_util import Twin
     from legged_gym_custom_amd import model as mdl
     d = G.load(name)
     N = int(d["num_envs"])
     cfg, m, P, terrain, sea = G.fixture_setup(d, task)
-    tw = Twin(P, mdl.to_struct(m), P.num_reward_terms + P.has_termination_reward, terrain=terrain)
+    tw = Twin(P, mdl.to_struct(m), P.num_reward_terms + P.has_termination_reward, terrain=terrain, device=device)
     go2 = task.startswith("go2")
     NB, PP = P.num_bodies, P.num_proprio
     a, t = tw.a, tw.t
@@ -45,7 +52,7 @@ def test_post_physics_matches_reference_golden(name, task):
     a["kp_kd"][:] = d["kp_kd_multipliers"]
     a["env_origins"][:] = d["env_origins"]
     tw.push()
-    mask = tw.torch.ones(N, dtype=tw.torch.uint8, device="cuda")
+    mask = tw.torch.ones(N, dtype=tw.torch.uint8, device=device)
     tw.native.reset_envs(mask, int(d["seed"]), 0, tw.stream())
     tw.sync()
     assert _close(tw.gpu("root_states"), d["reset0_state.root_states"])
@@ -99,6 +106,10 @@ def test_post_physics_matches_reference_golden(name, task):
 
 
 def test_sea_actuator_matches_torch_lstm():
+    sea_vs_torch("cuda")
+
+
+def sea_vs_torch(device):
     """The kernel's per-substep SEA net (anymal.py:71-81) against the torch fp32
     reference of the same op (actuator.SeaLSTM = the archive's LSTMsea), over 4 chained
     substeps of one full env step with the oracle's PD-free torques; the LSTM state the
@@ -110,7 +121,11 @@ def test_sea_actuator_matches_torch_lstm():
     cfg, m, P = G.go2_setup(n, "anymal_c_flat", sea_seed=5)
     P.push_robots = 0
     P.decimation = 1
-    tw = Twin(P, mdl.to_struct(m), P.num_reward_terms + P.has_termination_reward)
+    # the flat config's observation sizes are inconsistent (lgx_create refuses them): use the
+    # 48-term proprio it implies
+    P.num_proprio = 48
+    P.num_obs = 48 * (P.history_len + 1)
+    tw = Twin(P, mdl.to_struct(m), P.num_reward_terms + P.has_termination_reward, device=device)
     rng = np.random.default_rng(2)
     a = tw.a
     a["root_states"][:, 2] = 0.6
@@ -160,10 +175,14 @@ def _random_state(tw, P, rng, n):
 
 
 def test_full_step_matches_oracle():
+    full_step_vs_oracle("cuda")
+
+
+def full_step_vs_oracle(device):
     n = 64
-    cfg, m, P, tw = _twin(n)
+    cfg, m, P, tw = _twin(n, device=device)
     P.push_robots = 0
-    tw.native = type(tw.native)(tw.native.model, P, 0)
+    tw.native = type(tw.native)(tw.native.model, P, tw.native.device_index)
     tw.native.bind(tw.t)
     rng = np.random.default_rng(7)
     _random_state(tw, P, rng, n)

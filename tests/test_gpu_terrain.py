@@ -39,6 +39,10 @@ def _ground(ter, x, y):
 
 @pytest.mark.parametrize("mesh", ["trimesh", "heightfield"])
 def test_full_step_on_terrain_matches_oracle(mesh):
+    terrain_step_vs_oracle(mesh, "cuda")
+
+
+def terrain_step_vs_oracle(mesh, device):
     from native_util import Twin
     from legged_gym_custom_amd import model as mdl, params as prm
     n = 64
@@ -48,7 +52,8 @@ def test_full_step_on_terrain_matches_oracle(mesh):
     P = prm.build_task_params(cfg, m, n, go2=True, terrain_shape=(ter.tot_rows, ter.tot_cols))
     P.push_robots = 0
     P.curriculum = 0
-    tw = Twin(P, mdl.to_struct(m), P.num_reward_terms + P.has_termination_reward, terrain=(ter.heightsamples, words))
+    tw = Twin(P, mdl.to_struct(m), P.num_reward_terms + P.has_termination_reward, terrain=(ter.heightsamples, words),
+              device=device)
     rng = np.random.default_rng(11)
     a = tw.a
     a["friction"][:] = rng.uniform(0.3, 1.2, n)

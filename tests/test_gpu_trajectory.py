@@ -31,7 +31,7 @@ BOUNDS = {  # field: (atol, rtol), one step from identical inputs (observed maxi
     "torques": (5e-3, 1e-4), "commands": (1e-6, 0.0)}
 
 
-def _twin(n, task="go2", push=True, decimation=None):
+def _twin(n, task="go2", push=True, decimation=None, device="cuda"):
     from native_util import Twin
     from legged_gym_custom_amd import model as mdl
     cfg, m, P = G.go2_setup(n, task)
@@ -39,7 +39,7 @@ def _twin(n, task="go2", push=True, decimation=None):
         P.push_robots = 0
     if decimation is not None:
         P.decimation = decimation
-    tw = Twin(P, mdl.to_struct(m), P.num_reward_terms + P.has_termination_reward)
+    tw = Twin(P, mdl.to_struct(m), P.num_reward_terms + P.has_termination_reward, device=device)
     return cfg, P, tw
 
 
@@ -50,7 +50,7 @@ def _init(tw, P, n, rng):
     a["mass_params"][:, 1:] = rng.uniform(-0.05, 0.05, (n, 3))
     a["kp_kd"][:] = rng.uniform(0.9, 1.1, a["kp_kd"].shape)
     tw.push()
-    mask = tw.torch.ones(n, dtype=tw.torch.uint8, device="cuda")
+    mask = tw.torch.ones(n, dtype=tw.torch.uint8, device=tw.device)
     tw.native.reset_envs(mask, 5, 0, tw.stream())
     tw.sync()
     tw.pull()
@@ -59,8 +59,12 @@ def _init(tw, P, n, rng):
 
 
 def test_resynced_trajectory_matches_oracle():
-    n, steps = 64, 200
-    cfg, P, tw = _twin(n)
+    resynced_trajectory("cuda", 200)
+
+
+def resynced_trajectory(device, steps):
+    n = 64
+    cfg, P, tw = _twin(n, device=device)
     rng = np.random.default_rng(11)
     _init(tw, P, n, rng)
     worst = {k: 0.0 for k in BOUNDS}
@@ -97,8 +101,12 @@ def _stats(hist):
 
 
 def test_free_running_trajectory_statistics():
-    n, steps = 128, 1000
-    cfg, P, tw = _twin(n)
+    free_running_statistics("cuda", 1000)
+
+
+def free_running_statistics(device, steps):
+    n = 128
+    cfg, P, tw = _twin(n, device=device)
     rng = np.random.default_rng(3)
     _init(tw, P, n, rng)
     go, gg = [], []
