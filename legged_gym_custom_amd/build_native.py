@@ -68,6 +68,18 @@ def build_one(name, force=False, verbose=False):
     return out
 
 
+def build_env_variant(out, flags, verbose=True):
+    """A dev build of liblgx.so with extra compile flags (e.g. -DLGX_PHASE_CLOCK) at `out`."""
+    src, _, _ = _paths("liblgx.so")
+    obj = out[:-3] + "_hip.o"
+    hip = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off"] + list(flags)
+    for cmd in (hip + ["-c", "-o", obj] + src, ["hipcc", "-shared", "-o", out, obj] + _host_objects("liblgx.so", verbose)):
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.run(cmd, check=True)
+    return out
+
+
 def build(force=False, verbose=False):
     for name in LIBS:
         build_one(name, force=force, verbose=verbose)

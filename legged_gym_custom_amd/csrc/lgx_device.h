@@ -6,21 +6,9 @@
 #define LGX_DEV __device__ __forceinline__
 
 // ---------------------------------------------------------------- wave helpers
-// Sum over lanes 0..31 of a wave64 (lanes >= 32 ignored), returned to every lane.
-// DPP row_shr 1,2,4,8 builds per-row (16-lane) inclusive sums; lanes 15 and 31 hold
-// the row totals, read back with v_readlane (no LDS round trip).
 template <int CTRL>
 LGX_DEV float dpp_shr_t(float x) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xf, 0xf, false));
-}
-LGX_DEV float row_sums_32(float x) {
-  x += dpp_shr_t<0x111>(x);
-  x += dpp_shr_t<0x112>(x);
-  x += dpp_shr_t<0x114>(x);
-  x += dpp_shr_t<0x118>(x);
-  float a = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 15));
-  float b = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 31));
-  return a + b;
 }
 
 // Sum over lanes 0..15 (DPP row 0), returned to every lane. Lanes 0..15 must be active;

@@ -6,13 +6,14 @@
 //
 // Physics (replaces PhysX `gym.simulate`, legged_robot.py:79-85; spec in DESIGN.md):
 //   lanes 0..11  PD torques (legged_robot.py:440-478)
-//   lanes 0..3   forward kinematics / composite inertia / bias of one leg chain each
-//   lane  0      6x6 Schur complement of the base (mass matrix is [A B; Bᵀ D], D block
-//                diagonal over the 4 chains) + its Cholesky factor
+//   lanes 0..12  kinematics, one lane per joint (lane 12 the base), parent state passed down
+//                the chain by DPP; per-link COM wrench and the base sums about p0
+//   lanes 0..39  mass matrix [A B; Bᵀ D] factored lane-parallel: joint bias and coupling,
+//                leg blocks D_l, X = B D⁻¹, the 21 Schur sums, S⁻¹ by a register Cholesky
 //   lanes 0..63  contact candidates (one sphere centre per lane) -> ballot-compacted rows
-//   lanes 0..R-1 one constraint row each: Jacobian row, M⁻¹Jᵀ column (Schur solve), A_rr
-//   lanes 0..17  projected Gauss-Seidel: the generalized velocity is spread over lanes,
-//                each row residual J_r·u is a DPP row reduction, u += M⁻¹J_rᵀ Δλ
+//   lanes 0..R-1 one constraint row each: Jacobian row, M⁻¹Jᵀ column (Schur solve), A_rr,
+//                then projected Gauss-Seidel on A = J M⁻¹ Jᵀ (lane r holds row r's velocity
+//                and impulse; A stored in LDS, or formed per row for a fallen robot's rows)
 // Post-physics (Go2Robot.post_physics_step go2.py:345-387, LeggedRobot legged_robot.py:
 //   103-138): uniform scalar control flow per env; vector outputs written lane-parallel.
 #include <hip/hip_runtime.h>
@@ -53,13 +54,19 @@ struct Scratch {  // per-env post-physics scalars (go2.py:357-367, 279-328)
 //   dynamics   Fw, Nw [NL][3], Dl [4][6], tot [16]
 //   rows       ZG [MAXR][RW] at 0: z_r = S⁻¹ (J_b − X_l J_l) (6) | g_r = D_l⁻¹ J_l (3);
 //              J9 [MAXR][RW] at MAXR*RW: sparse row r = [base part (6) | the 3 joints of leg
-//              rleg[r]]; once J9 is in registers, the same region holds A = J M⁻¹ Jᵀ [n][n]
-//              for n <= AMAX rows (see dynamics)
+//              rleg[r]]; once J9 is in registers, the same region holds A = J M⁻¹ Jᵀ: square
+//              [n][n] for n <= ASQ rows, packed lower triangle for ASQ < n <= AMAX (see substep)
 //   post       U [4 rng_blocks] | cur [P] | hist [H*P] | heights [Hp] (stg_* below)
 // Go2 needs 1116 floats (the rows), ANYmal's post-physics staging 1,924.
-constexpr int AMAX = 24;  // rows per env step: p50 6, p99 15, max 27 (tools/phase_clock.py, r02)
+// Rows per env step: p50 9, p99 15, max 27 (tools/phase_clock.py, r02). The launch time is
+// the slowest wave's, so the rare env above ASQ rows must not fall to the velocity-space sweep
+// (a launch with one such env took 25-65 % longer): up to AMAX rows A is kept as a packed
+// lower triangle in the same LDS.
+constexpr int ASQ = 24;   // square A up to here
+constexpr int AMAX = 33;  // packed-triangle A up to here (33 * 34 / 2 = 561 <= 24 * 24)
 constexpr int RW = 9;     // sparse row width
-constexpr int J9_FLOATS = MAXR * RW > AMAX * AMAX ? MAXR * RW : AMAX * AMAX;
+constexpr int A_FLOATS = ASQ * ASQ > AMAX * (AMAX + 1) / 2 ? ASQ * ASQ : AMAX * (AMAX + 1) / 2;
+constexpr int J9_FLOATS = MAXR * RW > A_FLOATS ? MAXR * RW : A_FLOATS;
 constexpr int ROWS_FLOATS = MAXR * RW + J9_FLOATS;
 extern __shared__ float lgx_dyn[];
 struct DynTemps {
@@ -103,7 +110,7 @@ struct Sh {
   float Bc[NJ][6], Dinv[4][6], X[NJ][6], Sinv[6][6], us[NU], up[NU];
   // --- constraints (J, M⁻¹Jᵀ and A live in the arena below)
   float Arr[MAXR], tgt[MAXR], lam[MAXR];
-  int rkind[MAXR], rleg[MAXR];
+  int rleg[MAXR];
   int cbody[MAXC];
   float cn[MAXC][3];  // contact normals (terrain); tangents follow from contact_tangents
   int nrows, nlim, ncon;
@@ -774,7 +781,6 @@ LGX_DEV void substep(Sh& s, const lgx_model* M_, const lgx_task_params* Pm_, con
     jr[6 + pos_] = lim_lo ? 1.f : -1.f;
     const float d = lim_lo ? (M->joint_lower[lane + 1] - s.th[lane]) : (s.th[lane] - M->joint_upper[lane + 1]);
     s.tgt[r] = target(d);
-    s.rkind[r] = 0;
     s.rleg[r] = leg_;
   }
   if (act && crank < MAXC) {
@@ -803,7 +809,6 @@ LGX_DEV void substep(Sh& s, const lgx_model* M_, const lgx_task_params* Pm_, con
       jr[6] = pos >= 0 ? dot(ax0, cross(r0p, d)) : 0.f;
       jr[7] = pos >= 1 ? dot(ax1, cross(r1p, d)) : 0.f;
       jr[8] = pos >= 2 ? dot(ax2, cross(r2p, d)) : 0.f;
-      s.rkind[r] = t;
       s.rleg[r] = leg;
       s.tgt[r] = t == 0 ? target(depth) : 0.f;
     }
@@ -868,27 +873,33 @@ LGX_DEV void substep(Sh& s, const lgx_model* M_, const lgx_task_params* Pm_, con
 #if defined(LGX_DBG_STAGE) && LGX_DBG_STAGE == 4
   return;
 #endif
-  if (nrows <= AMAX) {
-    // ---- A = J M⁻¹ Jᵀ: lane r writes column r (A is symmetric; entry (q, r) = y_r·z_q +
-    //      [leg_r = leg_q] J_l,r·g_q; J_l,r = 0 for rows without a leg part)
-    if (row_lane) {
+  // ---- A = J M⁻¹ Jᵀ: entry (q, r) = y_r·z_q + [leg_r = leg_q] J_l,r·g_q (J_l,r = 0 for rows
+  //      without a leg part). Up to ASQ rows lane r stores column r of a square [q][r] image;
+  //      up to AMAX the lower triangle q >= r packed at q (q + 1) / 2 + r; beyond (a fallen
+  //      robot: up to 12 + 3 * MAXC rows) the PGS forms A[r][lane] from z_r, g_r (LDS) and the
+  //      lane's own y, J_l (registers) each time it needs it — the same numbers, nothing stored.
+  const bool tri = nrows > ASQ, stored = nrows <= AMAX;
+  if (stored && row_lane) {
 #pragma unroll 4
-      for (int q = 0; q < nrows; ++q) {
-        const float* zg = ZG + q * RW;
-        const float v = yr[0] * zg[0] + yr[1] * zg[1] + yr[2] * zg[2] + yr[3] * zg[3] + yr[4] * zg[4] + yr[5] * zg[5];
-        const float vl = jlr[0] * zg[6] + jlr[1] * zg[7] + jlr[2] * zg[8];
-        Am[q * nrows + lane] = v + (s.rleg[q] == lr ? vl : 0.f);
-      }
+    for (int q = 0; q < nrows; ++q) {
+      const float* zg = ZG + q * RW;
+      const float v = yr[0] * zg[0] + yr[1] * zg[1] + yr[2] * zg[2] + yr[3] * zg[3] + yr[4] * zg[4] + yr[5] * zg[5];
+      const float vl = jlr[0] * zg[6] + jlr[1] * zg[7] + jlr[2] * zg[8];
+      const float a = v + (s.rleg[q] == lr ? vl : 0.f);
+      if (!tri) Am[q * nrows + lane] = a;
+      else if (q >= lane) Am[q * (q + 1) / 2 + lane] = a;
     }
-    __syncthreads();
-    PH(7);
-    // ---- projected Gauss-Seidel on A (oracle_physics.c step 4). Rows are [nlim joint
-    //      limits | ncon × (normal, tangent, tangent)]. Lane r keeps its row's velocity
-    //      w_r = J_r u, λ_r and constants; every lane forms its own row's candidate update
-    //      and only the row being swept keeps it (a select), so a row costs one readlane of
-    //      its Δλ, broadcast into w += A[·][r] Δλ. The tangent pair trades its two candidates
-    //      between neighbouring lanes by DPP for the friction-disk norm. A contact's three
-    //      A columns are loaded one contact ahead.
+  }
+  __syncthreads();
+  PH(7);
+  // ---- projected Gauss-Seidel on A (oracle_physics.c step 4). Rows are [nlim joint
+  //      limits | ncon × (normal, tangent, tangent)]. Lane r keeps its row's velocity
+  //      w_r = J_r u, λ_r and constants; every lane forms its own row's candidate update
+  //      and only the row being swept keeps it (a select), so a row costs one readlane of
+  //      its Δλ, broadcast into w += A[·][r] Δλ. The tangent pair trades its two candidates
+  //      between neighbouring lanes by DPP for the friction-disk norm. A contact's three
+  //      A columns are loaded one contact ahead.
+  {
     float w = w0, lam = 0.f;
     const float mu = s.mu;
     auto rd = [](float v, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); };
@@ -902,50 +913,68 @@ LGX_DEV void substep(Sh& s, const lgx_model* M_, const lgx_task_params* Pm_, con
     const float ia = row_lane ? 1.0f / s.Arr[lane] : 0.f;
     const int rlast = nrows - 3;  // first row of the last contact
     const int lc = min(lane, nrows - 1);  // lanes past the rows read a valid (unused) entry
-    auto arow = [&](int r) { return Am[r * nrows + lc]; };  // A[r][lane]
-    for (int it = 0; it < Pm->solver_iterations; ++it) {
-      for (int r = 0; r < nlim; ++r) {
-        const float a0 = arow(r);
-        const float cand = fmaxf(0.f, lam + (tg - w) * ia);
-        const float d = rd(cand - lam, r);
-        lam = lane == r ? cand : lam;
-        w += a0 * d;
+    // A[r][lane]: square, from the packed triangle (row r up to the diagonal, then column r),
+    // or formed on the fly (lanes past the rows have y = J_l = 0 and read 0)
+    const int tl = lc * (lc + 1) / 2;
+    auto arow_sq = [&](int r) { return Am[r * nrows + lc]; };
+    auto arow_tri = [&](int r) { return Am[lc <= r ? r * (r + 1) / 2 + lc : tl + r]; };
+    auto arow_otf = [&](int r) {
+      const float* zg = ZG + r * RW;
+      const float v = yr[0] * zg[0] + yr[1] * zg[1] + yr[2] * zg[2] + yr[3] * zg[3] + yr[4] * zg[4] + yr[5] * zg[5];
+      const float vl = jlr[0] * zg[6] + jlr[1] * zg[7] + jlr[2] * zg[8];
+      return v + (s.rleg[r] == lr ? vl : 0.f);
+    };
+    // the sweeps, instantiated for each form of A (the square one carries no index selects)
+    auto sweeps = [&](auto arow) {
+      for (int it = 0; it < Pm->solver_iterations; ++it) {
+        for (int r = 0; r < nlim; ++r) {
+          const float a0 = arow(r);
+          const float cand = fmaxf(0.f, lam + (tg - w) * ia);
+          const float d = rd(cand - lam, r);
+          lam = lane == r ? cand : lam;
+          w += a0 * d;
+        }
+        if (ncon == 0) continue;
+        float n0 = arow(nlim), n1 = arow(nlim + 1), n2 = arow(nlim + 2);
+        for (int r = nlim; r < nrows; r += 3) {
+          const float a0 = n0, a1 = n1, a2 = n2;
+          const int rn = min(r + 3, rlast);
+          n0 = arow(rn);
+          n1 = arow(rn + 1);
+          n2 = arow(rn + 2);
+          // normal row
+          const float cand = fmaxf(0.f, lam + (tg - w) * ia);
+          const float d = rd(cand - lam, r);
+          lam = lane == r ? cand : lam;
+          w += a0 * d;
+          // tangent pair, projected onto the friction disk |λ_t| <= μ λ_n
+          const float lim = mu * rd(lam, r);
+          const float l = lam - w * ia;
+          // both shifts with every lane active (a DPP source lane outside EXEC reads 0), then
+          // the select: lane r + 1 takes r + 2's candidate, lane r + 2 takes r + 1's
+          float from_next = wave_shl1(l), from_prev = wave_shr1(l);
+          __asm__ volatile("" : "+v"(from_next), "+v"(from_prev));
+          const float other = lane == r + 1 ? from_next : from_prev;
+          const float nn = l * l + other * other;
+          const float sc = nn > lim * lim ? lim * __builtin_amdgcn_rsqf(nn) : 1.0f;
+          const float lt = l * sc;
+          const float dl = lt - lam;
+          const float d1 = rd(dl, r + 1), d2 = rd(dl, r + 2);
+          lam = (lane == r + 1 || lane == r + 2) ? lt : lam;
+          w += a1 * d1 + a2 * d2;
+        }
       }
-      if (ncon == 0) continue;
-      float n0 = arow(nlim), n1 = arow(nlim + 1), n2 = arow(nlim + 2);
-      for (int r = nlim; r < nrows; r += 3) {
-        const float a0 = n0, a1 = n1, a2 = n2;
-        const int rn = min(r + 3, rlast);
-        n0 = arow(rn);
-        n1 = arow(rn + 1);
-        n2 = arow(rn + 2);
-        // normal row
-        const float cand = fmaxf(0.f, lam + (tg - w) * ia);
-        const float d = rd(cand - lam, r);
-        lam = lane == r ? cand : lam;
-        w += a0 * d;
-        // tangent pair, projected onto the friction disk |λ_t| <= μ λ_n
-        const float lim = mu * rd(lam, r);
-        const float l = lam - w * ia;
-        // both shifts with every lane active (a DPP source lane outside EXEC reads 0), then
-        // the select: lane r + 1 takes r + 2's candidate, lane r + 2 takes r + 1's
-        float from_next = wave_shl1(l), from_prev = wave_shr1(l);
-        __asm__ volatile("" : "+v"(from_next), "+v"(from_prev));
-        const float other = lane == r + 1 ? from_next : from_prev;
-        const float nn = l * l + other * other;
-        const float sc = nn > lim * lim ? lim * __builtin_amdgcn_rsqf(nn) : 1.0f;
-        const float lt = l * sc;
-        const float dl = lt - lam;
-        const float d1 = rd(dl, r + 1), d2 = rd(dl, r + 2);
-        lam = (lane == r + 1 || lane == r + 2) ? lt : lam;
-        w += a1 * d1 + a2 * d2;
-      }
-    }
+    };
+    if (!stored) sweeps(arow_otf);
+    else if (tri) sweeps(arow_tri);
+    else sweeps(arow_sq);
     if (row_lane) s.lam[lane] = lam;
-    __syncthreads();
-    PH(8);
-    // ---- u+ = u* + M⁻¹ Jᵀ λ = u* + [Z ; G_J − Xᵀ Z]:  Z = Σ_r λ_r z_r,
-    //      G_j = Σ_{r on leg(j)} λ_r g_r[pos(j)]
+  }
+  __syncthreads();
+  PH(8);
+  // ---- u+ = u* + M⁻¹ Jᵀ λ = u* + [Z ; G_J − Xᵀ Z]:  Z = Σ_r λ_r z_r,
+  //      G_j = Σ_{r on leg(j)} λ_r g_r[pos(j)]
+  {
     float Z[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, G = 0.f;
 #pragma unroll 4
     for (int r = 0; r < nrows; ++r) {
@@ -969,63 +998,9 @@ LGX_DEV void substep(Sh& s, const lgx_model* M_, const lgx_task_params* Pm_, con
       for (int q = 0; q < 6; ++q) v -= Xj[q] * Z[q];
       s.up[6 + lane] = v;
     }
-    __syncthreads();
-    PH(9);
-  } else {
-    // ---- wide systems: PGS in velocity space; lanes 0..11 hold the joint rates, lanes
-    //      12..17 the base velocity; M⁻¹ J_rᵀ is formed from (z_r, g_r) on the fly
-    const int bi = lane - NJ;
-    auto jcomp = [&](int r) {
-      const float* jr = J9 + r * RW;
-      if (lane < NJ) return s.rleg[r] == leg_ ? jr[6 + pos_] : 0.f;
-      return lane < NU ? jr[bi] : 0.f;
-    };
-    auto mjcomp = [&](int r) {
-      const float* zg = ZG + r * RW;
-      if (lane < NJ) {
-        float v = s.rleg[r] == leg_ ? zg[6 + pos_] : 0.f;
-        const float* Xj = s.X[lane];
-#pragma unroll
-        for (int q = 0; q < 6; ++q) v -= Xj[q] * zg[q];
-        return v;
-      }
-      return lane < NU ? zg[bi] : 0.f;
-    };
-    float uc = lane < NJ ? s.us[6 + lane] : (lane < NU ? s.us[bi] : 0.f);
-    const float mu = s.mu;
-    for (int it = 0; it < Pm->solver_iterations; ++it) {
-      for (int r = 0; r < nrows; ++r) {
-        const int kind = s.rkind[r];
-        if (kind == 0) {
-          float w = row_sums_32(jcomp(r) * uc);
-          float lo = s.lam[r];
-          float ln = fmaxf(0.f, lo + (s.tgt[r] - w) / s.Arr[r]);
-          float d = ln - lo;
-          uc += mjcomp(r) * d;
-          if (lane == 0) s.lam[r] = ln;
-        } else {
-          float w1 = row_sums_32(jcomp(r) * uc);
-          float w2 = row_sums_32(jcomp(r + 1) * uc);
-          float o1 = s.lam[r], o2 = s.lam[r + 1];
-          float l1 = o1 - w1 / s.Arr[r];
-          float l2 = o2 - w2 / s.Arr[r + 1];
-          float lim = mu * s.lam[r - 1];
-          float n = sqrtf(l1 * l1 + l2 * l2);
-          if (n > lim) {
-            float sc = n > 0.f ? lim / n : 0.f;
-            l1 *= sc; l2 *= sc;
-          }
-          uc += mjcomp(r) * (l1 - o1) + mjcomp(r + 1) * (l2 - o2);
-          if (lane == 0) { s.lam[r] = l1; s.lam[r + 1] = l2; }
-          ++r;
-        }
-      }
-    }
-    if (lane < NJ) s.up[6 + lane] = uc;
-    else if (lane < NU) s.up[bi] = uc;
-    __syncthreads();
-    PH(8);
   }
+  __syncthreads();
+  PH(9);
   // ---- contact forces of the last substep, per reported body (world frame)
   if (last && lane < LGX_MAX_BODIES) {
     float f[3] = {0.f, 0.f, 0.f};

@@ -36,6 +36,8 @@ def lib():
         _lib.oracle_physics_substep.argtypes = [vp, vp, vp, i32]
         _lib.oracle_energy.argtypes = [vp, vp, vp, i32]
         _lib.oracle_energy.restype = C.c_double
+        _lib.oracle_debug_rows.argtypes = [i32]
+        _lib.oracle_debug_rows.restype = i32
     return _lib
 
 
@@ -114,3 +116,9 @@ class OracleEnv:
 
     def energy(self, e):
         return lib().oracle_energy(C.byref(self.M), C.byref(self.P), C.byref(self.B), e)
+
+
+def last_rows(n):
+    """Constraint rows of each env's latest physics substep (numpy int array)."""
+    L = lib()
+    return np.array([L.oracle_debug_rows(e) for e in range(n)])

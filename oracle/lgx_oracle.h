@@ -18,6 +18,8 @@ void oracle_clip_actions(const lgx_task_params* P, lgx_buffers* B);
 void oracle_step(const lgx_model* M, const lgx_task_params* P, lgx_buffers* B, uint64_t seed, uint64_t step);
 /* physics diagnostics (tests): kinetic + potential energy, total momentum */
 double oracle_energy(const lgx_model* M, const lgx_task_params* P, const lgx_buffers* B, int env);
+/* constraint rows of env's latest physics substep */
+int oracle_debug_rows(int env);
 int64_t oracle_sizeof_params(void);
 int64_t oracle_sizeof_model(void);
 int64_t oracle_sizeof_buffers(void);

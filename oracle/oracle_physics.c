@@ -379,6 +379,12 @@ double oracle_energy(const lgx_model* M, const lgx_task_params* P, const lgx_buf
   return E;
 }
 
+/* constraint rows of each env's latest substep (test diagnostics: which solve path the
+   kernel took — square A up to 24 rows, packed triangle up to 33, per-row A beyond) */
+#define ORACLE_ROWS_MAX_ENVS 65536
+static int g_rows[ORACLE_ROWS_MAX_ENVS];
+int oracle_debug_rows(int e) { return e >= 0 && e < ORACLE_ROWS_MAX_ENVS ? g_rows[e] : -1; }
+
 void oracle_physics_substep(const lgx_model* M, const lgx_task_params* P, lgx_buffers* B, int e) {
   const int D = P->num_dof;
   const double dt = P->sim_dt;
@@ -455,6 +461,7 @@ void oracle_physics_substep(const lgx_model* M, const lgx_task_params* P, lgx_bu
     cbody[nc] = M->cand_body[c];
     ++nc;
   }
+  if (e < ORACLE_ROWS_MAX_ENVS) g_rows[e] = nr;
   /* convert depths to velocity targets (Baumgarte) */
   for (int r = 0; r < nr; ++r) {
     if (rows[r].kind != 0) continue;

@@ -237,3 +237,60 @@ def test_standing_invariants_full_n():
     env2 = run()
     assert torch.equal(env.root_states, env2.root_states)
     assert torch.equal(env.obs_buf, env2.obs_buf)
+
+
+def crowded_states(tw, P, rng, n, z=(0.06, 0.16)):
+    """Robots tilted up to ~80 deg with the base low over the ground: z (0.06, 0.16) puts the
+    base on it (~48-row constraint systems: A formed per row), (0.2, 0.27) gives a mix of
+    <= 24 (square A), 25-33 (packed-triangle A) and > 33 rows. Contact termination is off
+    (n_termination = 0) and no robot is upside down, so no env resets and the physics of every
+    env is compared."""
+    _random_state(tw, P, rng, n)
+    a = tw.a
+    root = a["root_states"]
+    ax = rng.normal(size=(n, 3))
+    ax[:, 2] *= 0.2  # mostly roll / pitch
+    ax /= np.linalg.norm(ax, axis=1, keepdims=True)
+    ang = rng.uniform(0.2, 1.4, n)
+    root[:, 3:6] = ax * np.sin(ang / 2)[:, None]
+    root[:, 6] = np.cos(ang / 2)
+    root[:, 2] = rng.uniform(z[0], z[1], n)
+    root[:, 7:13] = rng.normal(0, 0.2, (n, 6))
+    q0 = np.array(P.default_dof_pos[:12], np.float32)
+    a["dof_state"][:, :, 0] = q0 + rng.normal(0, 0.5, (n, 12))
+
+
+def crowded_contacts_vs_oracle(device, z=(0.06, 0.16)):
+    n = 64
+    cfg, m, P, tw = _twin(n, device=device)
+    P.push_robots = 0
+    P.n_termination = 0
+    tw.native = type(tw.native)(tw.native.model, P, tw.native.device_index)  # the oracle reads P in place
+    tw.native.bind(tw.t)
+    rng = np.random.default_rng(21)
+    crowded_states(tw, P, rng, n, z)
+    tw.push()
+    tw.o.step(3, 11)
+    tw.native.step(3, 11, tw.stream())
+    tw.sync()
+    a = tw.a
+    assert (a["reset"] == 0).all()
+    import driver
+    rows = driver.last_rows(n)  # the oracle's row count per env (the kernel's solve path)
+    if z[0] < 0.1:
+        assert (rows > 33).sum() >= n // 2, rows
+    else:
+        assert ((rows > 24) & (rows <= 33)).sum() >= 8 and (rows <= 24).sum() >= 8, rows
+    # the ground carries the fallen robots on several bodies
+    touching = (np.abs(a["contact_forces"]).sum(-1) > 1.0).sum(1)
+    assert touching.mean() > 1.5, touching
+    np.testing.assert_allclose(tw.gpu("torques"), a["torques"], atol=2e-2, rtol=1e-3)
+    np.testing.assert_allclose(tw.gpu("root_states"), a["root_states"], atol=2e-3, rtol=1e-3)
+    np.testing.assert_allclose(tw.gpu("dof_state"), a["dof_state"], atol=2e-3, rtol=1e-3)
+    np.testing.assert_allclose(tw.gpu("contact_forces"), a["contact_forces"], atol=0.5, rtol=2e-2)
+    np.testing.assert_allclose(tw.gpu("rigid_body_states"), a["rigid_body_states"], atol=2e-3, rtol=1e-3)
+
+
+@pytest.mark.parametrize("z", [(0.06, 0.16), (0.2, 0.27)])
+def test_crowded_contacts_match_oracle(z):
+    crowded_contacts_vs_oracle("cuda", z)

@@ -74,3 +74,8 @@ def test_train_c1_on_cpu():
     assert torch.isfinite(env.obs_buf).all() and torch.isfinite(env.root_states).all()
     assert int(env.episode_length_buf.max()) > 0
     assert all(torch.isfinite(p).all() for p in runner.alg.actor_critic.parameters())
+
+
+@pytest.mark.parametrize("z", [(0.06, 0.16), (0.2, 0.27)])
+def test_host_crowded_contacts_match_oracle(z):
+    T.crowded_contacts_vs_oracle("cpu", z)

@@ -4,7 +4,8 @@
 -DLGX_PHASE_CLOCK; on the GPU box `python tools/phase_clock.py` runs the Go2 bench
 workload through it and prints, per phase, the mean/p50/p90 s_memtime cycles one env's
 wave spends there (summed over the 4 substeps), and the share of the wave's total.
-Env vars: TASK (go2), N (4096), K (10 timed steps)."""
+Env vars: TASK (go2), N (4096), K (10 timed steps), STATE=crowded (tilted robots at the ground
+before every step: many contacts)."""
 import ctypes as C
 import os
 import subprocess
@@ -13,18 +14,15 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIBDIR = os.path.join(ROOT, "legged_gym_custom_amd", "lib")
 PROF = os.path.join(LIBDIR, "liblgx_prof.so")
+sys.path.insert(0, ROOT)
 PHASES = ["load", "pd", "kinematics", "dynamics", "free_vel", "detect+rows", "row_solves", "A_build", "pgs",
           "u_update", "forces+integrate", "final_kin+writes", "uniforms", "post_scalar", "heights+rewards",
           "reset+obs+writes"]
 
 
 def build():
-    src = os.path.join(ROOT, "legged_gym_custom_amd", "csrc", "lgx_env.hip")
-    extra = os.environ.get("EXTRA", "").split()
-    cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
-           "-DLGX_PHASE_CLOCK"] + extra + ["-o", PROF, src]
-    print(" ".join(cmd))
-    subprocess.run(cmd, check=True)
+    from legged_gym_custom_amd import build_native
+    build_native.build_env_variant(PROF, ["-DLGX_PHASE_CLOCK"] + os.environ.get("EXTRA", "").split())
 
 
 def run():
@@ -54,12 +52,23 @@ def run():
     stream = torch.cuda.current_stream()
     acc = torch.zeros(n, 20, dtype=torch.float64, device="cuda:0")
     rows = []
+    per_step = []
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ms = 0.0
     for i in range(20 + k):
         if i == 20:
             assert L.lgx_debug_phase_buffer(C.c_void_p(buf.data_ptr())) == 0
         env.actions_in.copy_(torch.clamp(torch.randn(n, env.num_actions, device="cuda:0", generator=g), -3.14, 3.14))
+        if os.environ.get("STATE") in ("crowded", "tilted"):  # tilted robots at the ground (many contacts)
+            ax = torch.randn(n, 3, device="cuda:0", generator=g)
+            ax[:, 2] *= 0.2
+            ax /= ax.norm(dim=1, keepdim=True)
+            ang = 0.2 + 1.2 * torch.rand(n, device="cuda:0", generator=g)
+            env.root_states[:, 3:6] = ax * torch.sin(ang / 2)[:, None]
+            env.root_states[:, 6] = torch.cos(ang / 2)
+            z0, z1 = (0.06, 0.16) if os.environ["STATE"] == "crowded" else (0.13, 0.19)
+            env.root_states[:, 2] = z0 + (z1 - z0) * torch.rand(n, device="cuda:0", generator=g)
+            env.root_states[:, 7:13] = 0.2 * torch.randn(n, 6, device="cuda:0", generator=g)
         env.common_step_counter += 1
         if i >= 20:
             s.record()
@@ -68,14 +77,22 @@ def run():
             e.record()
             torch.cuda.synchronize()
             ms += s.elapsed_time(e)
-            acc += buf.double().remainder(2 ** 32)
+            cyc = buf.double().remainder(2 ** 32)
+            acc += cyc
             rows.append(buf[:, 16].clone())
+            wt = cyc[:, :16].sum(dim=1)
+            j = int(wt.argmax())
+            per_step.append((s.elapsed_time(e) * 1e3, float(wt.median()), float(wt.max()), int(buf[j, 16]),
+                             int(buf[j, 17]), float(torch.quantile(wt, 0.999))))
     acc /= k
     tot = acc[:, :16].sum(dim=1)
     r = torch.stack(rows).float()
     print("constraint rows per env step (max over substeps): mean %.1f p50 %.0f p90 %.0f p99 %.0f max %.0f; "
           "wide-path (> AMAX rows) substeps: %.2f %%" % (r.mean(), r.median(), torch.quantile(r, 0.9),
                                                          torch.quantile(r, 0.99), r.max(), acc[:, 17].mean() / 4 * 100))
+    print("per step: kernel us | wave cycles p50 / p99.9 / max | slowest env: rows, wide substeps")
+    for us, med, p999, mx, rw, wide in [(a_, b_, f_, c_, d_, e_) for a_, b_, c_, d_, e_, f_ in per_step]:
+        print(f"  {us:7.1f} | {med:8.0f} {p999:8.0f} {mx:8.0f} | {rw:3d} {wide:2d}")
     print(f"task {task} N={n}: kernel {ms / k * 1e3:.1f} us/launch; wave total cycles mean {tot.mean():.0f} "
           f"p50 {tot.median():.0f} p90 {torch.quantile(tot, 0.9):.0f} (s_memtime clock)")
     print(f"{'phase':18s} {'mean':>9s} {'p50':>9s} {'p90':>9s} {'share':>6s}")
