@@ -257,7 +257,11 @@ __device__ __forceinline__ void gemm_tile(const Params& p, const int L) {
   float va[PF][SA::R], vb[PF][SB::R];  // PF register sets: loads run PF steps ahead
   float csum[4] = {0.f, 0.f, 0.f, 0.f};
   auto gload = [&](float (&va)[SA::R], float (&vb)[SB::R], int k0) {
+#ifdef LGX_EXP_NO_KGUARD  // experiment: no guarded path compiled in (wrong for K % 32 != 0)
+    if (true) {
+#else
     if (k0 + BKS <= kend) {
+#endif
       SA::template load<false>(p.A, p.lda, m0, p.M, k0, kend, tid, va);
       SB::template load<false>(p.B, p.ldb, n0, p.N, k0, kend, tid, vb);
     } else {
