@@ -10,7 +10,7 @@ value = num_envs x 24 x world_size x K / (max over ranks of the timed K iteratio
 
 Also reported: `roofline` of the env-step kernel (algorithmic bytes per launch over its
 HIP-event-timed duration vs 8 TB/s HBM; the kernel is not HBM-bound: `roofline_valu` gives
-its VALU issue utilisation from the committed PMC profile), `roofline_learner`, and
+its VALU issue utilisation and wait fraction from the committed PMC profile), `roofline_learner`, and
 `cpu_baseline`: the same framework on the host (--sim_device=cpu --rl_device=cpu: liblgx.so's
 host backend, OpenMP over envs, + the torch-CPU learner) at the same shape (one iteration),
 rank 0 at N=1 only.
@@ -124,9 +124,11 @@ def committed_traffic(num_envs):
 
 def committed_valu(num_envs):
     """VALU issue utilisation of the env-step kernel from the newest committed PMC profile
-    (profiles/<round>_env_kernel_pmc.txt): every VALU instruction of a wave64 occupies its
-    SIMD for 4 cycles, so utilisation = 4 x SQ_INSTS_VALU / (1024 SIMDs x kernel cycles),
-    kernel cycles = GRBM_GUI_ACTIVE / 8 XCDs."""
+    (profiles/<round>_env_kernel_pmc.txt): on CDNA4 a wave64 VALU instruction issues over 2
+    cycles (SIMD-32; MI355X_MICROARCH.md), so utilisation = 2 x SQ_INSTS_VALU / (1024 SIMDs x
+    kernel cycles), kernel cycles = GRBM_GUI_ACTIVE / 8 XCDs. Beside it the wait fraction
+    (SQ_WAIT_ANY / SQ_WAVE_CYCLES) and LDS instructions per env step: the kernel is
+    latency-bound (LDS round trips of the LDS-resident per-env state, DPP/readlane chains)."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_env_kernel_pmc.txt")))
     if not files:
@@ -142,12 +144,19 @@ def committed_valu(num_envs):
     if not {"SQ_INSTS_VALU", "GRBM_GUI_ACTIVE"} <= set(vals):
         return None
     cyc = vals["GRBM_GUI_ACTIVE"] / 8
-    used = 4 * vals["SQ_INSTS_VALU"]
+    used = 2 * vals["SQ_INSTS_VALU"]
     cap = 1024 * cyc
-    return {"bound": "valu", "kernel": "lgx::env_step_kernel<true, false, false>",
-            "achieved": round(used / 1e6, 1), "peak": round(cap / 1e6, 1), "unit": "M VALU issue cycles per launch",
-            "frac": round(used / cap, 4), "valu_instructions_per_env_step": round(vals["SQ_INSTS_VALU"] / num_envs),
-            "source": os.path.relpath(files[-1], ROOT)}
+    out = {"bound": "valu", "kernel": "lgx::env_step_kernel<true, false, false>",
+           "achieved": round(used / 1e6, 1), "peak": round(cap / 1e6, 1), "unit": "M VALU issue cycles per launch",
+           "frac": round(used / cap, 4), "valu_instructions_per_env_step": round(vals["SQ_INSTS_VALU"] / num_envs),
+           "source": os.path.relpath(files[-1], ROOT)}
+    if {"SQ_WAIT_ANY", "SQ_WAVE_CYCLES"} <= set(vals):
+        out["wait_fraction"] = round(vals["SQ_WAIT_ANY"] / vals["SQ_WAVE_CYCLES"], 3)
+    if "SQ_INSTS_LDS" in vals:
+        out["lds_instructions_per_env_step"] = round(vals["SQ_INSTS_LDS"] / num_envs)
+    out["note"] = ("VALU pipe partly busy; the waves wait on LDS / memory (wait_fraction) and on dependent "
+                   "DPP / readlane chains: latency-bound at 4 waves per SIMD (DESIGN.md 4.1)")
+    return out
 
 
 def cpu_baseline(num_envs=4096, iters=1, steps_per_env=24):
@@ -296,7 +305,8 @@ def main():
                          "bytes_per_env_step": bpe, "bytes_per_launch": launch_bytes,
                          "traffic": None if traffic is None else round(traffic), "traffic_source": traffic_src,
                          "note": "the kernel's algorithmic bytes vs HBM peak, as north_star asks; it is bound by "
-                                 "VALU issue and per-env latency, not HBM (roofline_valu, DESIGN.md 4.1)"},
+                                 "per-env latency (LDS round trips, dependent lane exchanges), not HBM (roofline_valu, "
+                                 "DESIGN.md 4.1)"},
         }
         if args.task == "go2" and args.num_envs == 4096:
             out["roofline_valu"] = committed_valu(args.num_envs)
