@@ -13,7 +13,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIBDIR = os.path.join(ROOT, "legged_gym_custom_amd", "lib")
-PROF = os.path.join(LIBDIR, "liblgx_prof.so")
+PROF = os.environ.get("PROF_LIB") or os.path.join(LIBDIR, "liblgx_prof.so")
 sys.path.insert(0, ROOT)
 PHASES = ["load", "pd", "kinematics", "dynamics", "free_vel", "detect+rows", "row_solves", "A_build", "pgs",
           "u_update", "forces+integrate", "final_kin+writes", "uniforms", "post_scalar", "heights+rewards",
