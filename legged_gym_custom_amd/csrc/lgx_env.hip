@@ -98,6 +98,9 @@ struct Sh {
   long long ep_prev;
   int lc_prev[LGX_MAX_FEET];
   float lch_prev[LGX_MAX_FEET], fat_prev[LGX_MAX_FEET], jump_prev;
+  float la_prev[NJ], lt_prev[NJ];     // last_actions / last_torques (reward joint sums)
+  float es[LGX_MAX_REWARDS + 4];      // episode_sums row (updated by this step's terms)
+  float fric;                         // raw friction coefficient (privileged obs)
   long long ep;
   int reset, tout;
   // --- physics state (base velocity kept as the ORIGIN velocity inside the step)
@@ -1131,7 +1134,7 @@ LGX_DEV void resample_commands(const lgx_task_params* Pm, float* cmd, const floa
 // command state is in LDS (s.root, s.th, s.thd, s.cmd, s.ep): lane 0 does the scalar part,
 // lanes write the per-env buffer rows. Called under a uniform branch.
 LGX_DEV void reset_env(const lgx_task_params* Pm, const lgx_buffers& B, Sh& s, int e, int lane, bool after_init,
-                       bool zero_carried) {
+                       bool zero_carried, bool sums_in_lds) {
   const int D = Pm->num_dof;
   const float* U = stg_U();
   if (lane == 0) {
@@ -1197,7 +1200,8 @@ LGX_DEV void reset_env(const lgx_task_params* Pm, const lgx_buffers& B, Sh& s, i
   const int K = Pm->num_reward_terms + (Pm->has_termination_reward ? 1 : 0);
   if (lane < K) {
     float* es = B.episode_sums + (size_t)e * K + lane;
-    if (B.episode_stats) atomicAdd(B.episode_stats + lane, *es);
+    const float sum = sums_in_lds ? s.es[lane] : *es;  // in a step: this step's updated row, staged in LDS
+    if (B.episode_stats) atomicAdd(B.episode_stats + lane, sum);
     *es = 0.f;
   }
   if (lane == 0 && B.episode_stats) atomicAdd(B.episode_stats + K, 1.0f);
@@ -1226,7 +1230,8 @@ LGX_DEV void joint_sums(const lgx_task_params* Pm, const lgx_buffers& B, Sh& s, 
   const int D = Pm->num_dof, A = Pm->num_actions;
   const int j = lane < D ? lane : 0;
   const float on = lane < D ? 1.0f : 0.0f;
-  const float la = B.last_actions[(size_t)e * A + j], lt = B.last_torques[(size_t)e * D + j];
+  const float la = s.la_prev[j], lt = s.lt_prev[j];  // prefetched at kernel start
+  (void)A;
   const float q = s.th[j], qd = s.thd[j], tau = s.tau[j], q0 = Pm->default_dof_pos[j];
   const float dq = q - q0;
   float v[J_N];
@@ -1489,6 +1494,14 @@ __global__ __launch_bounds__(64, ACTNET ? LGX_SEA_WAVES : 4) void env_step_kerne
   if (lane == 0) {
     s.ep_prev = B.episode_length[e];
     s.jump_prev = B.rpy_phase ? B.rpy_phase[e * 8 + 7] : 0.f;
+    s.fric = B.friction ? B.friction[e] : 1.f;
+  }
+  // inputs the post-physics phase reads (their latency hides behind the physics)
+  if (lane < A) s.la_prev[lane] = B.last_actions[(size_t)e * A + lane];
+  if (lane < D) s.lt_prev[lane] = B.last_torques[(size_t)e * D + lane];
+  {
+    const int KS0 = Pm->num_reward_terms + (Pm->has_termination_reward ? 1 : 0);
+    if (lane < KS0) s.es[lane] = B.episode_sums[(size_t)e * KS0 + lane];
   }
   if (Pm->task_kind == LGX_TASK_GO2 && lane < Pm->num_feet) {
     s.lc_prev[lane] = B.last_contacts[e * Pm->num_feet + lane];
@@ -1586,6 +1599,19 @@ __global__ __launch_bounds__(64, ACTNET ? LGX_SEA_WAVES : 4) void env_step_kerne
   // ================================================================ post-physics
   // Go2Robot.post_physics_step go2.py:345-387 / LeggedRobot legged_robot.py:103-138.
   // Per-env scalars: lane 0, into LDS. Vectors: lane-parallel from LDS.
+  // the old observation history (read back at the end of the step) in flight from here on:
+  // the first HV x 64 entries into registers (all of Go2's 5 x 52)
+  constexpr int HV = 5;
+  float hv[HV];
+  {
+    const int HPn = Pm->history_len * Pm->num_proprio;
+    const float* hsrc = B.obs_history + (size_t)e * HPn;
+#pragma unroll
+    for (int t = 0; t < HV; ++t) {
+      const int i = lane + 64 * t;
+      hv[t] = i < HPn ? hsrc[i] : 0.f;
+    }
+  }
   fill_uniforms(s, seed, gid, step, 0, lane, rng_blocks(Pm));
   PH(12);
   const bool go2 = Pm->task_kind == LGX_TASK_GO2;
@@ -1679,11 +1705,15 @@ __global__ __launch_bounds__(64, ACTNET ? LGX_SEA_WAVES : 4) void env_step_kerne
     B.time_out[e] = (uint8_t)s.tout;
   }
   __syncthreads();
-  if (lane < KS) B.episode_sums[(size_t)e * KS + lane] += s.rterm[lane];
+  if (lane < KS) {
+    const float v = s.es[lane] + s.rterm[lane];
+    s.es[lane] = v;
+    B.episode_sums[(size_t)e * KS + lane] = v;
+  }
   __syncthreads();
   PH(14);
   // reset_idx (go2.py:207-263)
-  if (reset) reset_env(Pm, B, s, e, lane, true, false);
+  if (reset) reset_env(Pm, B, s, e, lane, true, false, true);
 
   // compute_observations go2.py:467-574 / legged_robot.py:240-273
   const int Pp = Pm->num_proprio, H = Pm->history_len;
@@ -1726,7 +1756,12 @@ __global__ __launch_bounds__(64, ACTNET ? LGX_SEA_WAVES : 4) void env_step_kerne
   float* hist_g = B.obs_history + (size_t)e * H * Pp;
   float* const hist = stg_hist(Pm);
   const float* const cur = stg_cur(Pm);
-  for (int i = lane; i < H * Pp; i += 64) hist[i] = reset ? 0.f : hist_g[i];
+#pragma unroll
+  for (int t = 0; t < HV; ++t) {
+    const int i = lane + 64 * t;
+    if (i < H * Pp) hist[i] = reset ? 0.f : hv[t];
+  }
+  for (int i = lane + 64 * HV; i < H * Pp; i += 64) hist[i] = reset ? 0.f : hist_g[i];
   __syncthreads();
   const float co = Pm->clip_obs;
   float* obs = B.obs + (size_t)e * Pm->num_obs;
@@ -1746,8 +1781,8 @@ __global__ __launch_bounds__(64, ACTNET ? LGX_SEA_WAVES : 4) void env_step_kerne
     // priv = [mass params (4), friction, kp-1 (D), kd-1 (D)]
     for (int i = lane; i < Pm->num_priv; i += 64) {
       float v;
-      if (i < 4) v = B.mass_params[e * 4 + i];
-      else if (i == 4) v = B.friction[e];
+      if (i < 4) v = i == 0 ? s.madd : s.cadd[i - 1];  // mass_params row, staged at kernel start
+      else if (i == 4) v = s.fric;
       else if (i < 5 + D) v = s.kpm[i - 5] - 1.0f;
       else v = s.kdm[i - 5 - D] - 1.0f;
       v = clipf(v, -co, co);
@@ -1824,7 +1859,7 @@ __global__ __launch_bounds__(64) void reset_kernel(const lgx_task_params* __rest
   __syncthreads();
   // an external reset (BaseTask.reset -> reset_idx) only exists once the env is built,
   // i.e. with init_done set: the terrain curriculum applies (legged_robot.py:551-552)
-  reset_env(Pm, B, s, e, lane, true, true);
+  reset_env(Pm, B, s, e, lane, true, true, false);
   if (lane < 13) B.root_states[(size_t)e * 13 + lane] = s.root[lane];
   if (lane < D) {
     B.dof_state[((size_t)e * D + lane) * 2] = s.th[lane];
