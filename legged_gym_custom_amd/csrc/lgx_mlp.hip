@@ -705,17 +705,25 @@ struct HeadRow {
   float logp, ratio;
 };
 
-__device__ __forceinline__ HeadRow head_row(const lgx_ppo_head_args& p, int i, const float* stdv, const float* lstd) {
+// One row's action-wide inputs, loaded up front at clamped columns (columns past A repeat the
+// last one and are discarded by selects): no branch around a load, so all of a row's loads
+// are in flight together (a guarded or late load is a round trip of its own, ~0.3 us).
+template <int NA>
+__device__ __forceinline__ void load_cols(const float* __restrict__ x, int i, int A, float (&v)[NA]) {
+#pragma unroll
+  for (int j = 0; j < NA; ++j) v[j] = x[(int64_t)i * A + min(j, A - 1)];
+}
+
+template <int NA>
+__device__ __forceinline__ HeadRow head_row(const lgx_ppo_head_args& p, int i, const float* stdv, const float* lstd,
+                                            const float (&act)[NA], const float (&mu)[NA]) {
   const float l2pi = 0.9189385332046727f;  // log(sqrt(2 pi))
   float lp = 0.f;
-  // unrolled to the action bound with a guard (same summation order): every row load is
-  // issued before the first use instead of one load round trip per action
 #pragma unroll
-  for (int j = 0; j < HMAXA; ++j) {
-    if (j < p.A) {
-      const float d = p.actions[(int64_t)i * p.A + j] - p.mu[(int64_t)i * p.A + j];
-      lp += -(d * d) / (2.f * stdv[j] * stdv[j]) - lstd[j] - l2pi;
-    }
+  for (int j = 0; j < NA; ++j) {  // same summation order as the reference's sum over actions
+    const float d = act[j] - mu[j];
+    const float t = -(d * d) / (2.f * stdv[j] * stdv[j]) - lstd[j] - l2pi;
+    lp = j < p.A ? lp + t : lp;
   }
   HeadRow r;
   r.logp = lp;
@@ -723,20 +731,30 @@ __device__ __forceinline__ HeadRow head_row(const lgx_ppo_head_args& p, int i, c
   return r;
 }
 
+template <int NA>
 __device__ __forceinline__ void ppo_head_fwd_body(const lgx_ppo_head_args& p) {
   __shared__ float red[4 * 4];
   __shared__ float stdv[HMAXA], lstd[HMAXA];
-  if (threadIdx.x < p.A) { stdv[threadIdx.x] = p.std[threadIdx.x]; lstd[threadIdx.x] = logf(p.std[threadIdx.x]); }
+  if (threadIdx.x < HMAXA) {  // columns past A repeat the last one (read by the clamped, discarded terms)
+    const float sd = p.std[min((int)threadIdx.x, p.A - 1)];
+    stdv[threadIdx.x] = sd;
+    lstd[threadIdx.x] = logf(sd);
+  }
   __syncthreads();
   float v[3] = {0.f, 0.f, 0.f};
   for (int i = blockIdx.x * HT + threadIdx.x; i < p.B; i += gridDim.x * HT) {
-    const HeadRow h = head_row(p, i, stdv, lstd);
+    float act[NA], mu[NA], os[NA], om[NA];
+    load_cols(p.actions, i, p.A, act);
+    load_cols(p.mu, i, p.A, mu);
+    load_cols(p.old_sigma, i, p.A, os);
+    load_cols(p.old_mu, i, p.A, om);
+    const HeadRow h = head_row<NA>(p, i, stdv, lstd, act, mu);
     const float a = p.adv[i];
     const float s1 = -a * h.ratio, s2 = -a * fminf(fmaxf(h.ratio, 1.f - p.clip), 1.f + p.clip);
     v[0] += fmaxf(s1, s2);
     const float val = p.value[i], R = p.returns[i];
+    const float tv = (p.clipped_value ? p.target_values : p.value)[i];  // unconditional load
     if (p.clipped_value) {
-      const float tv = p.target_values[i];
       const float vc = tv + fminf(fmaxf(val - tv, -p.clip), p.clip);
       v[1] += fmaxf((val - R) * (val - R), (vc - R) * (vc - R));
     } else {
@@ -744,12 +762,10 @@ __device__ __forceinline__ void ppo_head_fwd_body(const lgx_ppo_head_args& p) {
     }
     float kl = 0.f;
 #pragma unroll
-    for (int j = 0; j < HMAXA; ++j) {
-      if (j < p.A) {
-        const float os = p.old_sigma[(int64_t)i * p.A + j], om = p.old_mu[(int64_t)i * p.A + j];
-        const float dm = om - p.mu[(int64_t)i * p.A + j];
-        kl += logf(stdv[j] / os + 1.0e-5f) + (os * os + dm * dm) / (2.f * (stdv[j] * stdv[j])) - 0.5f;
-      }
+    for (int j = 0; j < NA; ++j) {
+      const float dm = om[j] - mu[j];
+      const float t = logf(stdv[j] / os[j] + 1.0e-5f) + (os[j] * os[j] + dm * dm) / (2.f * (stdv[j] * stdv[j])) - 0.5f;
+      kl = j < p.A ? kl + t : kl;
     }
     v[2] += kl;
   }
@@ -772,17 +788,25 @@ __device__ __forceinline__ void ppo_head_fwd_body(const lgx_ppo_head_args& p) {
   }
 }
 
+template <int NA>
 __device__ __forceinline__ void ppo_head_bwd_body(const lgx_ppo_head_args& p) {
   __shared__ float red[4 * HMAXA];
   __shared__ float stdv[HMAXA], lstd[HMAXA];
-  if (threadIdx.x < p.A) { stdv[threadIdx.x] = p.std[threadIdx.x]; lstd[threadIdx.x] = logf(p.std[threadIdx.x]); }
+  if (threadIdx.x < HMAXA) {  // columns past A repeat the last one (read by the clamped, discarded terms)
+    const float sd = p.std[min((int)threadIdx.x, p.A - 1)];
+    stdv[threadIdx.x] = sd;
+    lstd[threadIdx.x] = logf(sd);
+  }
   __syncthreads();
   const float gs = p.g[0] / p.B, gv = p.g[1] / p.B, ge = p.g[2];
-  float ds[HMAXA];
+  float ds[NA];
 #pragma unroll
-  for (int j = 0; j < HMAXA; ++j) ds[j] = 0.f;
+  for (int j = 0; j < NA; ++j) ds[j] = 0.f;
   for (int i = blockIdx.x * HT + threadIdx.x; i < p.B; i += gridDim.x * HT) {
-    const HeadRow h = head_row(p, i, stdv, lstd);
+    float act[NA], mu[NA];
+    load_cols(p.actions, i, p.A, act);
+    load_cols(p.mu, i, p.A, mu);
+    const HeadRow h = head_row<NA>(p, i, stdv, lstd, act, mu);
     const float a = p.adv[i];
     const float lo = 1.f - p.clip, hi = 1.f + p.clip;
     const float s1 = -a * h.ratio, s2 = -a * fminf(fmaxf(h.ratio, lo), hi);
@@ -793,18 +817,18 @@ __device__ __forceinline__ void ppo_head_bwd_body(const lgx_ppo_head_args& p) {
     const float dratio = gs * (w1 * -a + w2 * -a * in);
     const float dlogp = dratio * h.ratio;
 #pragma unroll
-    for (int j = 0; j < HMAXA; ++j) {
+    for (int j = 0; j < NA; ++j) {
+      const float d = act[j] - mu[j];
+      const float var = stdv[j] * stdv[j];
       if (j < p.A) {
-        const float d = p.actions[(int64_t)i * p.A + j] - p.mu[(int64_t)i * p.A + j];
-        const float var = stdv[j] * stdv[j];
         p.dmu[(int64_t)i * p.A + j] = dlogp * d / var;
         ds[j] += dlogp * (d * d / (var * stdv[j]) - 1.f / stdv[j]);
       }
     }
     const float val = p.value[i], R = p.returns[i];
+    const float tv = (p.clipped_value ? p.target_values : p.value)[i];
     float dv;
     if (p.clipped_value) {
-      const float tv = p.target_values[i];
       const float vc = tv + fminf(fmaxf(val - tv, -p.clip), p.clip);
       const float l1 = (val - R) * (val - R), l2 = (vc - R) * (vc - R);
       const float u1 = l1 > l2 ? 1.f : (l1 == l2 ? 0.5f : 0.f);
@@ -815,12 +839,12 @@ __device__ __forceinline__ void ppo_head_bwd_body(const lgx_ppo_head_args& p) {
     }
     p.dvalue[i] = dv;
   }
-  block_sum<HMAXA>(ds, red);
+  block_sum<NA>(ds, red);
   if (threadIdx.x == 0)
     for (int j = 0; j < p.A; ++j) p.ws[blockIdx.x * HMAXA + j] = ds[j];
   if (last_block(p.counter)) {
-    float t[HMAXA];
-    final_sum<HMAXA>(p.ws, HMAXA, gridDim.x, t, red);
+    float t[NA];
+    final_sum<NA>(p.ws, HMAXA, gridDim.x, t, red);
     if (threadIdx.x == 0) {
       for (int j = 0; j < p.A; ++j) {  // entropy: d(sum_j log std_j)/d std_j
         const float d = t[j] + ge / stdv[j];
@@ -836,33 +860,72 @@ __device__ __forceinline__ void ppo_head_bwd_body(const lgx_ppo_head_args& p) {
 // with coalesced loads: p is usually a column span of the actor-input buffer (row stride
 // ld_p), where one row per thread would touch a separate cache line per lane and load.
 constexpr int AUX_CW = 16;
+constexpr int AUX_EU = 8;  // estimator columns per unrolled group
+// Every load below is unconditional (row and column clamped into range, the extra values
+// discarded by selects or by guarded stores): a load under a branch is a round trip of its
+// own, and these kernels are a few dependent round trips long.
 __device__ __forceinline__ void aux_stage_p(const lgx_aux_loss_args& p, int64_t ldp, int i0, int j0, int w,
                                             float* st) {
   __syncthreads();
-  for (int k = threadIdx.x; k < HT * w; k += HT) {
-    const int r = k / w, j = k % w;
-    if (i0 + r < p.B) st[r * (AUX_CW + 1) + j] = p.p[(int64_t)(i0 + r) * ldp + j0 + j];
+  const int n = HT * w;
+  // k / w through a float reciprocal (k < 4096, w <= 16: the product is within 1e-3 of the
+  // quotient and 1/32 of the next integer, so floor is exact) — an integer division by a
+  // run-time w is ~40 instructions, and one wave per SIMD pays every one of them
+  const float rw = 1.f / (float)w;
+  float x[AUX_CW];
+#pragma unroll
+  for (int u = 0; u < AUX_CW; ++u) {
+    const int k = min((int)threadIdx.x + HT * u, n - 1);
+    const int r = (int)(((float)k + 0.5f) * rw), j = k - r * w;
+    x[u] = p.p[(int64_t)min(i0 + r, p.B - 1) * ldp + j0 + j];
+  }
+#pragma unroll
+  for (int u = 0; u < AUX_CW; ++u) {
+    const int k = (int)threadIdx.x + HT * u;
+    const int r = (int)(((float)k + 0.5f) * rw), j = k - r * w;
+    if (k < n) st[r * (AUX_CW + 1) + j] = x[u];
   }
   __syncthreads();
 }
 
-// sum_j (p[i, j] - a[i, j])^2 in column order for row i = i0 + threadIdx.x (block-uniform call)
+// sum_j (p[i, j] - a[i, j])^2 in column order for row i = i0 + threadIdx.x (block-uniform call;
+// rows past B return a value of a clamped row, unused)
 __device__ __forceinline__ float aux_row_sq(const lgx_aux_loss_args& p, int64_t ldp, int i0, float* st) {
-  const int i = i0 + threadIdx.x;
+  const int64_t ic = min(i0 + (int)threadIdx.x, p.B - 1);
   float s = 0.f;
   for (int j0 = 0; j0 < p.L; j0 += AUX_CW) {
     const int w = min(AUX_CW, p.L - j0);
-    aux_stage_p(p, ldp, i0, j0, w, st);
-    if (i < p.B)
+    float a[AUX_CW];
 #pragma unroll
-      for (int j = 0; j < AUX_CW; ++j) {
-        if (j < w) {
-          const float d = st[threadIdx.x * (AUX_CW + 1) + j] - p.a[(int64_t)i * p.L + j0 + j];
-          s += d * d;
-        }
-      }
+    for (int j = 0; j < AUX_CW; ++j) a[j] = p.a[ic * p.L + j0 + min(j, w - 1)];
+    aux_stage_p(p, ldp, i0, j0, w, st);
+#pragma unroll
+    for (int j = 0; j < AUX_CW; ++j) {
+      const float d = st[threadIdx.x * (AUX_CW + 1) + j] - a[j];
+      s = j < w ? s + d * d : s;
+    }
   }
   return s;
+}
+
+// sum_j (e[i, j] - t[i, j])^2 in column order
+__device__ __forceinline__ float aux_est_sq(const lgx_aux_loss_args& p, int64_t i) {
+  float q = 0.f;
+  for (int j0 = 0; j0 < p.E; j0 += AUX_EU) {
+    float e[AUX_EU], t[AUX_EU];
+#pragma unroll
+    for (int u = 0; u < AUX_EU; ++u) {
+      const int64_t c = i * p.E + min(j0 + u, p.E - 1);
+      e[u] = p.e[c];
+      t[u] = p.t[c];
+    }
+#pragma unroll
+    for (int u = 0; u < AUX_EU; ++u) {
+      const float d = e[u] - t[u];
+      q = j0 + u < p.E ? q + d * d : q;
+    }
+  }
+  return q;
 }
 
 __device__ __forceinline__ void aux_loss_fwd_body(const lgx_aux_loss_args& p) {
@@ -873,14 +936,9 @@ __device__ __forceinline__ void aux_loss_fwd_body(const lgx_aux_loss_args& p) {
   for (int i0 = blockIdx.x * HT; i0 < p.B; i0 += gridDim.x * HT) {
     const float s = aux_row_sq(p, ldp, i0, st);
     const int i = i0 + threadIdx.x;
+    const float q = aux_est_sq(p, min(i, p.B - 1));
     if (i >= p.B) continue;
     v[0] += sqrtf(s);
-    float q = 0.f;
-#pragma unroll 4
-    for (int j = 0; j < p.E; ++j) {
-      const float d = p.e[(int64_t)i * p.E + j] - p.t[(int64_t)i * p.E + j];
-      q += d * d;
-    }
     const float nq = sqrtf(q);  // torch: norm(dim=1).pow(2)
     v[1] += nq * nq;
   }
@@ -900,37 +958,48 @@ __device__ __forceinline__ void aux_loss_fwd_body(const lgx_aux_loss_args& p) {
 __device__ __forceinline__ void aux_loss_bwd_body(const lgx_aux_loss_args& p) {
   __shared__ float st[HT * (AUX_CW + 1)];
   const int i0 = blockIdx.x * HT, i = i0 + threadIdx.x;
+  const int64_t ic = min(i, p.B - 1);
   const float gr = p.g[0] / p.B, ge = p.g[1] / p.B;
   const int64_t ldp = p.ld_p > 0 ? p.ld_p : p.L;
   const float n = sqrtf(aux_row_sq(p, ldp, i0, st));
   const float k = n > 0.f ? gr / n : 0.f;
   for (int j0 = 0; j0 < p.L; j0 += AUX_CW) {
     const int w = min(AUX_CW, p.L - j0);
-    aux_stage_p(p, ldp, i0, j0, w, st);
-    if (i < p.B)
+    float a[AUX_CW];
 #pragma unroll
-      for (int j = 0; j < AUX_CW; ++j)
-        if (j < w)
-          p.dp[(int64_t)i * p.L + j0 + j] = k * (st[threadIdx.x * (AUX_CW + 1) + j] - p.a[(int64_t)i * p.L + j0 + j]);
+    for (int j = 0; j < AUX_CW; ++j) a[j] = p.a[ic * p.L + j0 + min(j, w - 1)];
+    aux_stage_p(p, ldp, i0, j0, w, st);
+#pragma unroll
+    for (int j = 0; j < AUX_CW; ++j)
+      if (i < p.B && j < w) p.dp[ic * p.L + j0 + j] = k * (st[threadIdx.x * (AUX_CW + 1) + j] - a[j]);
   }
-  if (i >= p.B) return;
-#pragma unroll 4
-  for (int j = 0; j < p.E; ++j)
-    p.de[(int64_t)i * p.E + j] = ge * 2.f * (p.e[(int64_t)i * p.E + j] - p.t[(int64_t)i * p.E + j]);
+  for (int j0 = 0; j0 < p.E; j0 += AUX_EU) {
+#pragma unroll
+    for (int u = 0; u < AUX_EU; ++u) {
+      const int64_t c = ic * p.E + min(j0 + u, p.E - 1);
+      const float d = ge * 2.f * (p.e[c] - p.t[c]);
+      if (i < p.B && j0 + u < p.E) p.de[c] = d;
+    }
+  }
 }
 
-__global__ void ppo_head_fwd(lgx_ppo_head_args p) { ppo_head_fwd_body(p); }
-__global__ void ppo_head_bwd(lgx_ppo_head_args p) { ppo_head_bwd_body(p); }
-__global__ void aux_loss_fwd(lgx_aux_loss_args p) { aux_loss_fwd_body(p); }
-__global__ void aux_loss_bwd(lgx_aux_loss_args p) { aux_loss_bwd_body(p); }
+// NA: action columns unrolled (A <= NA; the go2/anymal heads have 12)
+template <int NA>
+__global__ __launch_bounds__(HT) void ppo_head_fwd(lgx_ppo_head_args p) { ppo_head_fwd_body<NA>(p); }
+template <int NA>
+__global__ __launch_bounds__(HT) void ppo_head_bwd(lgx_ppo_head_args p) { ppo_head_bwd_body<NA>(p); }
+__global__ __launch_bounds__(HT) void aux_loss_fwd(lgx_aux_loss_args p) { aux_loss_fwd_body(p); }
+__global__ __launch_bounds__(HT) void aux_loss_bwd(lgx_aux_loss_args p) { aux_loss_bwd_body(p); }
 // both heads in one launch: blockIdx.y = 0 the PPO head, 1 the ROA/estimator losses (each
 // y-slice is the single-head grid, with its own counter)
-__global__ void loss_heads_fwd(lgx_ppo_head_args h, lgx_aux_loss_args a) {
-  if (blockIdx.y == 0) ppo_head_fwd_body(h);
+template <int NA>
+__global__ __launch_bounds__(HT) void loss_heads_fwd(lgx_ppo_head_args h, lgx_aux_loss_args a) {
+  if (blockIdx.y == 0) ppo_head_fwd_body<NA>(h);
   else aux_loss_fwd_body(a);
 }
-__global__ void loss_heads_bwd(lgx_ppo_head_args h, lgx_aux_loss_args a) {
-  if (blockIdx.y == 0) ppo_head_bwd_body(h);
+template <int NA>
+__global__ __launch_bounds__(HT) void loss_heads_bwd(lgx_ppo_head_args h, lgx_aux_loss_args a) {
+  if (blockIdx.y == 0) ppo_head_bwd_body<NA>(h);
   else aux_loss_bwd_body(a);
 }
 
@@ -1248,8 +1317,8 @@ static int head_check(const lgx_ppo_head_args* a) {
 int32_t lgx_ppo_head_forward(const lgx_ppo_head_args* a, void* stream) {
   if (head_check(a)) return -1;
   if (!a->out || !a->old_mu || !a->old_sigma) return fail("lgx_ppo_head_forward: null out/old_mu/old_sigma");
-  hipLaunchKernelGGL(lgxm::ppo_head_fwd, dim3(lgxm::head_grid(a->B)), dim3(lgxm::HT), 0,
-                     static_cast<hipStream_t>(stream), *a);
+  hipLaunchKernelGGL(a->A <= 12 ? lgxm::ppo_head_fwd<12> : lgxm::ppo_head_fwd<lgxm::HMAXA>, dim3(lgxm::head_grid(a->B)),
+                     dim3(lgxm::HT), 0, static_cast<hipStream_t>(stream), *a);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : fail(hipGetErrorString(e));
 }
@@ -1257,8 +1326,8 @@ int32_t lgx_ppo_head_forward(const lgx_ppo_head_args* a, void* stream) {
 int32_t lgx_ppo_head_backward(const lgx_ppo_head_args* a, void* stream) {
   if (head_check(a)) return -1;
   if (!a->g || !a->dmu || !a->dvalue || !a->dstd) return fail("lgx_ppo_head_backward: null g/dmu/dvalue/dstd");
-  hipLaunchKernelGGL(lgxm::ppo_head_bwd, dim3(lgxm::head_grid(a->B)), dim3(lgxm::HT), 0,
-                     static_cast<hipStream_t>(stream), *a);
+  hipLaunchKernelGGL(a->A <= 12 ? lgxm::ppo_head_bwd<12> : lgxm::ppo_head_bwd<lgxm::HMAXA>, dim3(lgxm::head_grid(a->B)),
+                     dim3(lgxm::HT), 0, static_cast<hipStream_t>(stream), *a);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : fail(hipGetErrorString(e));
 }
@@ -1287,8 +1356,8 @@ int32_t lgx_loss_heads_forward(const lgx_ppo_head_args* h, const lgx_aux_loss_ar
   if (!a || a->B != h->B || a->L < 1 || a->E < 1 || !a->p || !a->a || !a->e || !a->t || !a->out || !a->ws ||
       !a->counter)
     return fail("lgx_loss_heads_forward: bad aux arguments");
-  hipLaunchKernelGGL(lgxm::loss_heads_fwd, dim3(lgxm::head_grid(h->B), 2), dim3(lgxm::HT), 0,
-                     static_cast<hipStream_t>(stream), *h, *a);
+  hipLaunchKernelGGL(h->A <= 12 ? lgxm::loss_heads_fwd<12> : lgxm::loss_heads_fwd<lgxm::HMAXA>, dim3(lgxm::head_grid(h->B), 2),
+                     dim3(lgxm::HT), 0, static_cast<hipStream_t>(stream), *h, *a);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : fail(hipGetErrorString(e));
 }
@@ -1298,8 +1367,8 @@ int32_t lgx_loss_heads_backward(const lgx_ppo_head_args* h, const lgx_aux_loss_a
   if (!h->g || !h->dmu || !h->dvalue || !h->dstd) return fail("lgx_loss_heads_backward: null g/dmu/dvalue/dstd");
   if (!a || a->B != h->B || a->L < 1 || a->E < 1 || !a->p || !a->a || !a->e || !a->t || !a->g || !a->dp || !a->de)
     return fail("lgx_loss_heads_backward: bad aux arguments");
-  hipLaunchKernelGGL(lgxm::loss_heads_bwd, dim3(lgxm::head_grid(h->B), 2), dim3(lgxm::HT), 0,
-                     static_cast<hipStream_t>(stream), *h, *a);
+  hipLaunchKernelGGL(h->A <= 12 ? lgxm::loss_heads_bwd<12> : lgxm::loss_heads_bwd<lgxm::HMAXA>, dim3(lgxm::head_grid(h->B), 2),
+                     dim3(lgxm::HT), 0, static_cast<hipStream_t>(stream), *h, *a);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : fail(hipGetErrorString(e));
 }
