@@ -197,15 +197,18 @@ int32_t lgx_ppo_tail(const lgx_ppo_tail_args* args, void* stream);
 
 /* Up to LGX_COPY_MAX device-to-device copies in one launch (the storage writes of one
  * rollout step). Each entry: nbytes from src to dst; 16-byte aligned entries whose size
- * is a multiple of 16 take the vector path. */
+ * is a multiple of 16 take the vector path. dst_stride is read by lgx_gather_rows only. */
 #define LGX_COPY_MAX 16
 typedef struct lgx_copy_desc {
   const void* src; void* dst; int64_t nbytes;
+  int64_t dst_stride;  /* lgx_gather_rows: bytes between destination rows (0: nbytes, packed) */
 } lgx_copy_desc;
 int32_t lgx_copy_batch(const lgx_copy_desc* descs, int32_t n, void* stream);
 /* Row gather of up to LGX_COPY_MAX row-major buffers in one launch (the storage permuted once
- * per update, rollout_storage.py:134-181): dst row r = src row idx[r] (r < rows), row_bytes
- * each (16-B vector path when row_bytes and both bases are 16-B aligned). */
+ * per update, rollout_storage.py:134-181): dst row r (at dst + r * dst_stride) = src row
+ * idx[r] (r < rows), nbytes each; a strided destination places rows inside a wider buffer
+ * (the update's actor-input rows). 16-B vector path when nbytes, dst_stride and both bases
+ * are 16-B aligned; rows * (nbytes / 4) < 2^31. */
 int32_t lgx_gather_rows(const lgx_copy_desc* descs, int32_t n, const int64_t* idx, int64_t rows, void* stream);
 
 /* PPO.act action head (actor_critic.py:205-226 + ppo.py:141-146) for a diagonal Gaussian:

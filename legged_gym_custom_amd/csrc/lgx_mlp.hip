@@ -1168,27 +1168,32 @@ __global__ __launch_bounds__(256) void copy_batch_kernel(CopyBatch cb) {
 }
 
 // blockIdx.y = entry (nbytes = bytes per row); threads stride over (row, chunk) pairs
+// item i = (row r, chunk c) with 32-bit index math (host: rows * per < 2^31); the
+// destination row stride may exceed the row (rows placed inside a wider buffer)
 __global__ __launch_bounds__(256) void gather_rows_kernel(CopyBatch cb, const int64_t* __restrict__ idx, int64_t rows) {
   const lgx_copy_desc& d = cb.d[blockIdx.y];
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool vec = ((reinterpret_cast<uintptr_t>(d.src) | reinterpret_cast<uintptr_t>(d.dst) | (uintptr_t)d.nbytes) &
-                    15) == 0;
+  const uint32_t stride = gridDim.x * blockDim.x;
+  const uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t dstr = d.dst_stride > 0 ? d.dst_stride : d.nbytes;
+  const bool vec = ((reinterpret_cast<uintptr_t>(d.src) | reinterpret_cast<uintptr_t>(d.dst) | (uintptr_t)d.nbytes |
+                     (uintptr_t)dstr) & 15) == 0;
   if (vec) {
-    const int64_t per = d.nbytes >> 4;
+    const uint32_t per = (uint32_t)(d.nbytes >> 4), tpr = (uint32_t)(dstr >> 4);
+    const uint32_t n = (uint32_t)rows * per;
     const float4* __restrict__ s = reinterpret_cast<const float4*>(d.src);
     float4* __restrict__ t = reinterpret_cast<float4*>(d.dst);
-    for (int64_t i = i0; i < rows * per; i += stride) {
-      const int64_t r = i / per, c = i - r * per;
-      t[i] = s[idx[r] * per + c];
+    for (uint32_t i = i0; i < n; i += stride) {
+      const uint32_t r = i / per, c = i - r * per;
+      t[(int64_t)r * tpr + c] = s[idx[r] * per + c];
     }
   } else {
-    const int64_t per = d.nbytes >> 2;  // 4-B elements (host checks)
+    const uint32_t per = (uint32_t)(d.nbytes >> 2), tpr = (uint32_t)(dstr >> 2);  // 4-B elements (host checks)
+    const uint32_t n = (uint32_t)rows * per;
     const float* __restrict__ s = reinterpret_cast<const float*>(d.src);
     float* __restrict__ t = reinterpret_cast<float*>(d.dst);
-    for (int64_t i = i0; i < rows * per; i += stride) {
-      const int64_t r = i / per, c = i - r * per;
-      t[i] = s[idx[r] * per + c];
+    for (uint32_t i = i0; i < n; i += stride) {
+      const uint32_t r = i / per, c = i - r * per;
+      t[(int64_t)r * tpr + c] = s[idx[r] * per + c];
     }
   }
 }
@@ -1664,6 +1669,9 @@ int32_t lgx_gather_rows(const lgx_copy_desc* descs, int32_t n, const int64_t* id
   for (int i = 0; i < n; ++i) {
     if (descs[i].nbytes < 0 || descs[i].nbytes % 4 != 0 || (descs[i].nbytes > 0 && (!descs[i].src || !descs[i].dst)))
       return fail("lgx_gather_rows: bad entry (row bytes must be a multiple of 4)");
+    if (descs[i].dst_stride != 0 && (descs[i].dst_stride < descs[i].nbytes || descs[i].dst_stride % 4 != 0))
+      return fail("lgx_gather_rows: dst_stride must be 0 or a multiple of 4 >= the row bytes");
+    if (rows * (descs[i].nbytes / 4) >= (int64_t)1 << 31) return fail("lgx_gather_rows: rows * row elements >= 2^31");
     cb.d[i] = descs[i];
     most = descs[i].nbytes > most ? descs[i].nbytes : most;
   }

@@ -85,7 +85,7 @@ class TailArgs(C.Structure):
 
 class CopyDesc(C.Structure):
     """Mirror of lgx_copy_desc."""
-    _fields_ = [("src", C.c_void_p), ("dst", C.c_void_p), ("nbytes", C.c_int64)]
+    _fields_ = [("src", C.c_void_p), ("dst", C.c_void_p), ("nbytes", C.c_int64), ("dst_stride", C.c_int64)]
 
 
 class ActHeadArgs(C.Structure):
@@ -221,12 +221,23 @@ def copy_batch(dsts, srcs):
     _check(lib().lgx_copy_batch(descs, n, _stream()), "lgx_copy_batch")
 
 
-def gather_rows(srcs, idx):
-    """[t.index_select(0, idx) for t in srcs] (contiguous fp32/4-B tensors) in one launch."""
+def gather_rows(srcs, idx, dsts=None):
+    """[t.index_select(0, idx) for t in srcs] (contiguous fp32/4-B tensors) in one launch.
+    dsts (optional, per source): a preallocated [len(idx), width] destination with unit column
+    stride and any row stride (e.g. a column span of a wider buffer), or None for a new
+    contiguous tensor. Returns the destinations."""
     if idx.dtype != torch.int64:
         raise MlpLibError("gather_rows: int64 indices only")
     idx = idx.contiguous()
-    outs = [torch.empty((idx.numel(),) + tuple(t.shape[1:]), device=t.device, dtype=t.dtype) for t in srcs]
+    dsts = list(dsts) if dsts is not None else [None] * len(srcs)
+    outs = []
+    for t, d in zip(srcs, dsts):
+        if d is None:
+            d = torch.empty((idx.numel(),) + tuple(t.shape[1:]), device=t.device, dtype=t.dtype)
+        elif (d.dim() != 2 or d.shape[0] != idx.numel() or d.shape[1] * 4 != (t.numel() // max(1, t.shape[0])) * 4
+              or d.stride(1) != 1 or d.dtype != t.dtype):
+            raise MlpLibError("gather_rows: a destination must be [rows, width] with unit column stride")
+        outs.append(d)
     for i in range(0, len(srcs), COPY_MAX):
         chunk = list(zip(srcs[i:i + COPY_MAX], outs[i:i + COPY_MAX]))
         descs = (CopyDesc * COPY_MAX)()
@@ -235,6 +246,7 @@ def gather_rows(srcs, idx):
                 raise MlpLibError("gather_rows: contiguous 4-byte tensors only")
             descs[k].src, descs[k].dst = x.data_ptr(), o.data_ptr()
             descs[k].nbytes = (x.numel() // max(1, x.shape[0])) * 4
+            descs[k].dst_stride = o.stride(0) * 4 if o.dim() == 2 else 0
         _check(lib().lgx_gather_rows(descs, len(chunk), idx.data_ptr(), idx.numel(), _stream()), "lgx_gather_rows")
     return outs
 

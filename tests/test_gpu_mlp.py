@@ -419,6 +419,16 @@ def test_gather_rows_matches_index_select():
     idx = torch.randperm(rows, device=dev, generator=g)[:3000]
     for a, b in zip(H.gather_rows(srcs, idx), [t.index_select(0, idx) for t in srcs]):
         assert torch.equal(a, b)
+    # strided destinations: column spans of wider buffers (16-B pitch: vector path; odd
+    # pitch: element path), the columns around them untouched
+    for pitch in (628, 627):
+        wide = torch.full((3000, pitch), -7.0, device=dev)
+        outs = H.gather_rows([srcs[0], srcs[3], srcs[1]], idx, [wide[:, :572], wide[:, 624:627], None])
+        assert outs[0].data_ptr() == wide.data_ptr()
+        assert torch.equal(wide[:, :572], srcs[0].index_select(0, idx))
+        assert torch.equal(wide[:, 624:627], srcs[3].index_select(0, idx))
+        assert torch.equal(outs[2], srcs[1].index_select(0, idx))
+        assert bool((wide[:, 572:624] == -7.0).all()) and bool((wide[:, 627:] == -7.0).all())
 
 
 def test_transpose_batch_matches_torch():
