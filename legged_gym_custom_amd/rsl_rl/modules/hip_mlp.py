@@ -901,12 +901,23 @@ class _AdaptationFn(torch.autograd.Function):
         C1, C2, C3, k1, s1, k2, s2, L1, L2 = dims
         Bn, H, P = h.shape
         dev = h.device
-        x = _rowmajor(h.reshape(Bn * H, P))
-        y0 = linear_forward(x, fc_w, fc_b, True)                         # [B, H, C1]
+        # no gradient wanted and h the first H of Hs > H blocks of a contiguous [B, Hs * P]
+        # buffer (the history inside the obs rows): the per-step layer runs on all Hs blocks
+        # of every row, read in place, instead of on a packed copy of the H history blocks
+        # (the conv windows below only read blocks < H); one copy of B x H x P floats less
+        Hs = h.stride(0) // P if h.stride(2) == 1 and h.stride(1) == P and h.stride(0) % P == 0 else 0
+        inplace = (not any(ctx.needs_input_grad) and Hs > H and
+                   h.storage_offset() + Bn * Hs * P <= h.untyped_storage().nbytes() // h.element_size())
+        if inplace:
+            x = h.as_strided((Bn * Hs, P), (P, 1))
+        else:
+            Hs = H
+            x = _rowmajor(h.reshape(Bn * H, P))
+        y0 = linear_forward(x, fc_w, fc_b, True)                         # [B, Hs, C1]
         W1 = _conv_w(c1_w)
         y1 = torch.empty(Bn, L1, C2, device=dev)
         for t in range(L1):
-            gemm_raw(y0.data_ptr() + 4 * t * s1 * C1, H * C1, 1, W1.data_ptr(), W1.stride(0), 1,
+            gemm_raw(y0.data_ptr() + 4 * t * s1 * C1, Hs * C1, 1, W1.data_ptr(), W1.stride(0), 1,
                      y1.data_ptr() + 4 * t * C2, L1 * C2, Bn, C2, k1 * C1, EPI_BIAS | EPI_ELU, c1_b.data_ptr())
         W2 = _conv_w(c2_w)
         y2 = torch.empty(Bn, L2, C3, device=dev)
@@ -917,7 +928,8 @@ class _AdaptationFn(torch.autograd.Function):
         out = linear_forward(y2.reshape(Bn, L2 * C3), Wf, f_b, True)
         ctx.dims = dims
         ctx.params = (fc_w, fc_b, c1_w, c1_b, c2_w, c2_b, f_w, f_b)
-        ctx.save_for_backward(x, y0, y1, y2, out, W1, W2, Wf)
+        if not inplace:  # (the in-place path wants no gradient)
+            ctx.save_for_backward(x, y0, y1, y2, out, W1, W2, Wf)
         return out
 
     @staticmethod

@@ -104,6 +104,22 @@ def test_adaptation_encoder_matches_torch_fp64():
         torch.testing.assert_close(p.grad.double().cpu(), pr.grad, rtol=1e-3, atol=1e-4 * scale, msg=n)
 
 
+def test_adaptation_encoder_inplace_history_bitwise():
+    """ActorCritic.adaptation_encoder on obs rows without grad reads the history blocks in
+    place (the per-step layer over all 11 blocks of each row): bitwise equal to the packed
+    path (a contiguous copy of the history), which the grad-enabled call takes."""
+    from legged_gym_custom_amd.rsl_rl.modules.support_networks import AdaptationEncoder
+    torch.manual_seed(0)
+    enc = AdaptationEncoder(num_proprio=52, history_buffer_length=10, output_dim=20).to(dev)
+    obs = torch.randn(3000, 572, device=dev)
+    hist = obs[:, :-52].reshape(-1, 10, 52)
+    with torch.no_grad():
+        a = enc(hist)                       # in place (strided view of obs)
+        b = enc(hist.contiguous())          # packed
+    c = enc(hist)                           # grad enabled: packed path inside
+    assert torch.equal(a, b) and torch.equal(a, c.detach())
+
+
 @pytest.mark.parametrize("clipped", [True, False])
 def test_ppo_head_matches_torch_autograd(clipped):
     """lgx_ppo_head_{forward,backward} vs the reference's loss code (ppo.py:196-262 over
