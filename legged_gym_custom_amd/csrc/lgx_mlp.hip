@@ -50,7 +50,6 @@ constexpr int BM = 128, BKS = 32, NT = 256;
 #endif
 constexpr int PF = LGX_PF;               // global-load register sets (prefetch depth in K steps)
 constexpr int PITCH = BKS;               // bf16 per LDS row (64 B, swizzled: lds_off)
-constexpr int A_ELEMS = BM * PITCH;      // one A image (hi or lo)
 enum Mode { KV = 1, MV = 3, MVE = 4 };  // MVE: MV for a row count that is not a multiple of 4
 
 typedef float f32x4u __attribute__((ext_vector_type(4), aligned(4)));  // 4-B aligned float4
@@ -236,10 +235,14 @@ __device__ __forceinline__ float elu(float v) {
 }
 
 // One output tile (logical index L: n fastest, then m, then the K split) of one GEMM.
-template <int AM, int BMODE, bool COLSUM, int BN_>
+// BM_ rows x BN_ columns; 4 waves as 2 (rows) x 2 (columns), each BM_/2 x BN_/2. BM_ = 64
+// serves the rollout's 4096-row forward launches (twice the blocks, half the work per K step).
+template <int AM, int BMODE, bool COLSUM, int BN_, int BM_ = BM>
 __device__ __forceinline__ void gemm_tile(const Params& p, const int L) {
-  using SA = Stager<AM, BM>;
+  using SA = Stager<AM, BM_>;
   using SB = Stager<BMODE, BN_>;
+  constexpr int MI = BM_ / 32;             // 16-row MFMA tiles per wave
+  constexpr int A_ELEMS = BM_ * PITCH;     // one A image (hi or lo)
   constexpr int NJ = BN_ / 32;             // 16-wide MFMA column tiles per wave
   constexpr int B_ELEMS = BN_ * PITCH;
   constexpr int STAGE = 2 * A_ELEMS + 2 * B_ELEMS;
@@ -248,11 +251,11 @@ __device__ __forceinline__ void gemm_tile(const Params& p, const int L) {
   const int tm = (L / p.tiles_n) % p.tiles_m;
   const int z = L / (p.tiles_n * p.tiles_m);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int m0 = tm * BM, n0 = tn * BN_;
+  const int m0 = tm * BM_, n0 = tn * BN_;
   const int kbeg = z * p.kchunk;
   const int kend = min(p.K, kbeg + p.kchunk);
   const int nsteps = kend > kbeg ? (kend - kbeg + BKS - 1) / BKS : 0;
-  const int wm = (wave & 1) * 64, wn = (wave >> 1) * (BN_ / 2);
+  const int wm = (wave & 1) * (BM_ / 2), wn = (wave >> 1) * (BN_ / 2);
 
   float va[PF][SA::R], vb[PF][SB::R];  // PF register sets: loads run PF steps ahead
   float csum[4] = {0.f, 0.f, 0.f, 0.f};
@@ -276,9 +279,9 @@ __device__ __forceinline__ void gemm_tile(const Params& p, const int L) {
     if constexpr (COLSUM) SA::colsum(va, csum);
   };
 
-  f32x4 acc[4][NJ];
+  f32x4 acc[MI][NJ];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
@@ -300,7 +303,7 @@ __device__ __forceinline__ void gemm_tile(const Params& p, const int L) {
       bl[j] = *reinterpret_cast<const bf16x8*>(blo + off);
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < MI; ++i) {
       const int off = lds_off(wm + i * 16 + fr, fc);
       const bf16x8 ah = *reinterpret_cast<const bf16x8*>(ahi + off);
       const bf16x8 al = *reinterpret_cast<const bf16x8*>(alo + off);
@@ -345,12 +348,12 @@ __device__ __forceinline__ void gemm_tile(const Params& p, const int L) {
       constexpr int SLOTS = SA::NKQ;
       const int kq = SA::mv_kq(tid), rg = SA::mv_rg(tid);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) cs[kq * BM + rg * 4 + e] = csum[e];
+      for (int e = 0; e < 4; ++e) cs[kq * BM_ + rg * 4 + e] = csum[e];
       __syncthreads();
-      if (tid < BM) {
+      if (tid < BM_) {
         float v = 0.f;
 #pragma unroll
-        for (int sl = 0; sl < SLOTS; ++sl) v += cs[sl * BM + tid];
+        for (int sl = 0; sl < SLOTS; ++sl) v += cs[sl * BM_ + tid];
         if (m0 + tid < p.M) p.colsum_ws[(int64_t)z * p.M + m0 + tid] = v;
       }
     }
@@ -358,10 +361,10 @@ __device__ __forceinline__ void gemm_tile(const Params& p, const int L) {
   }
 
   // epilogue through LDS: MFMA C/D map (col = lane & 15, row = (lane >> 4) * 4 + r) into a
-  // [BM][BN_ + 4] fp32 image, then row-contiguous float4 reads/writes of C (and act).
+  // [BM_][BN_ + 4] fp32 image, then row-contiguous float4 reads/writes of C (and act).
   constexpr int CP = BN_ + 4;
   constexpr int CH = BN_ / 4;              // float4 chunks per row
-  constexpr int IT = BM * CH / NT;         // chunks per thread
+  constexpr int IT = BM_ * CH / NT;         // chunks per thread
   const bool part = p.split > 1;
   const bool delu = !part && (p.epi & LGX_EPI_DELU);
   // ELU outputs of the previous layer: issue every load before the tile is even staged
@@ -385,7 +388,7 @@ __device__ __forceinline__ void gemm_tile(const Params& p, const int L) {
   }
   const int ec = lane & 15, er = (lane >> 4) * 4;
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
 #pragma unroll
@@ -467,7 +470,7 @@ struct GroupParams {
 };
 static_assert(sizeof(GroupParams) <= 4096, "kernel argument segment");
 
-template <int KIND, int BN_>
+template <int KIND, int BN_, int BM_ = BM>
 __global__ __launch_bounds__(NT, 2) void gemm_group_kernel(GroupParams g) {
   const int x = blockIdx.x & 7, j = blockIdx.x >> 3;
   if (j >= g.per_xcd) return;
@@ -478,10 +481,10 @@ __global__ __launch_bounds__(NT, 2) void gemm_group_kernel(GroupParams g) {
   if (l >= p.tiles) return;
   const int m = g.mode[i];
   if constexpr (KIND == G_FWD) {
-    gemm_tile<KV, KV, false, BN_>(p, l);
+    gemm_tile<KV, KV, false, BN_, BM_>(p, l);
   } else if constexpr (KIND == G_DX) {
-    if (m) gemm_tile<KV, MVE, false, BN_>(p, l);
-    else gemm_tile<KV, MV, false, BN_>(p, l);
+    if (m) gemm_tile<KV, MVE, false, BN_, BM_>(p, l);
+    else gemm_tile<KV, MV, false, BN_, BM_>(p, l);
   } else {
     if (m == 0) gemm_tile<MV, MV, true, BN_>(p, l);
     else if (m == 1) gemm_tile<MVE, MV, true, BN_>(p, l);
@@ -1081,9 +1084,9 @@ __global__ __launch_bounds__(256) void tail_adam(lgx_ppo_tail_args p) {
 }
 
 // dynamic LDS: two K-step stages of hi/lo A and B images, or the fp32 C image (reused)
-constexpr size_t lds_bytes(int bn) {
-  const size_t stages = 2 * (2 * A_ELEMS + 2 * bn * PITCH) * sizeof(__bf16);
-  const size_t cimg = (size_t)BM * (bn + 4) * sizeof(float);
+constexpr size_t lds_bytes(int bn, int bm = BM) {
+  const size_t stages = 2 * (2 * bm * PITCH + 2 * bn * PITCH) * sizeof(__bf16);
+  const size_t cimg = (size_t)bm * (bn + 4) * sizeof(float);
   return stages > cimg ? stages : cimg;
 }
 
@@ -1139,6 +1142,20 @@ static int tile_n_for(int M, int N, bool rows_are_batch) {
   if (forced == 64 || forced == 128) return forced;
   if (rows_are_batch && M <= 8192) return 64;
   return tile_n(N);
+}
+
+// Rows per tile of a grouped launch: 64 for forward launches over few rows with 64-wide tiles
+// (the rollout's 4096-env batches: twice the blocks per launch, so twice the waves per CU to
+// hide each K step's latency), else BM. LGX_MLP_BM=128 forces the 128-row tile (dev knob).
+static int group_tile_m(int kind, int M, int bn) {
+  static int forced = -1;
+  if (forced < 0) {
+    const char* e = getenv("LGX_MLP_BM");
+    forced = e ? atoi(e) : 0;
+  }
+  if (forced == 128) return lgxm::BM;
+  if (forced == 64) return kind != lgxm::G_DW && bn == 64 ? 64 : lgxm::BM;  // dev: every 64-wide fwd / dx launch
+  return kind == lgxm::G_FWD && bn == 64 && M <= 8192 ? 64 : lgxm::BM;
 }
 
 // ================================================================ rollout bookkeeping
@@ -1535,10 +1552,11 @@ int32_t lgx_gemm_group(const lgx_gemm_args* args, int32_t n, void* stream) {
       std::swap(g.mode[k], g.mode[k - 1]);
     }
   const int bn = tile_n_for(maxm, maxn, kind != G_DW);
+  const int bm = group_tile_m(kind, maxm, bn);
   int total = 0;
   for (int i = 0; i < g.n; ++i) {
     Params& p = g.p[i];
-    p.tiles_m = (p.M + BM - 1) / BM;
+    p.tiles_m = (p.M + bm - 1) / bm;
     p.tiles_n = (p.N + bn - 1) / bn;
     p.tiles = p.tiles_m * p.tiles_n * p.split;
     g.start[i] = total;
@@ -1560,7 +1578,11 @@ int32_t lgx_gemm_group(const lgx_gemm_args* args, int32_t n, void* stream) {
   } else {                                                                                                      \
     hipLaunchKernelGGL((gemm_group_kernel<K, 64>), dim3(grid), dim3(NT), lds_bytes(64), s, g);                 \
   }
-  if (kind == G_FWD) {
+  if (kind == G_FWD && bm == 64) {
+    hipLaunchKernelGGL((gemm_group_kernel<G_FWD, 64, 64>), dim3(grid), dim3(NT), lds_bytes(64, 64), s, g);
+  } else if (kind == G_DX && bm == 64) {
+    hipLaunchKernelGGL((gemm_group_kernel<G_DX, 64, 64>), dim3(grid), dim3(NT), lds_bytes(64, 64), s, g);
+  } else if (kind == G_FWD) {
     LGX_GROUP_LAUNCH(G_FWD)
   } else if (kind == G_DX) {
     LGX_GROUP_LAUNCH(G_DX)
