@@ -1145,9 +1145,9 @@ static int tile_n_for(int M, int N, bool rows_are_batch) {
 }
 
 // Rows per tile of a grouped launch: 64 for forward launches over few rows with 64-wide tiles
-// (the rollout's 4096-env batches: twice the blocks per launch, so twice the waves per CU to
-// hide each K step's latency), else BM. LGX_MLP_BM=128 forces the 128-row tile (dev knob).
-static int group_tile_m(int kind, int M, int bn) {
+// and fewer than 2 blocks per CU at 128 rows (the rollout's 4096-env batches: twice the blocks
+// per launch, so twice the waves per CU to hide each K step's latency), else BM. LGX_MLP_BM=128 forces the 128-row tile (dev knob).
+static int group_tile_m(int kind, int M, int bn, int64_t tiles128) {
   static int forced = -1;
   if (forced < 0) {
     const char* e = getenv("LGX_MLP_BM");
@@ -1155,7 +1155,9 @@ static int group_tile_m(int kind, int M, int bn) {
   }
   if (forced == 128) return lgxm::BM;
   if (forced == 64) return kind != lgxm::G_DW && bn == 64 ? 64 : lgxm::BM;  // dev: every 64-wide fwd / dx launch
-  return kind == lgxm::G_FWD && bn == 64 && M <= 8192 ? 64 : lgxm::BM;
+  // (a launch that already has 2 blocks per CU at 128 rows — the 4096-row actor/critic
+  // layer 0, 512 tiles — measured faster with them: 32 vs 35 us)
+  return kind == lgxm::G_FWD && bn == 64 && M <= 8192 && tiles128 < 512 ? 64 : lgxm::BM;
 }
 
 // ================================================================ rollout bookkeeping
@@ -1552,7 +1554,10 @@ int32_t lgx_gemm_group(const lgx_gemm_args* args, int32_t n, void* stream) {
       std::swap(g.mode[k], g.mode[k - 1]);
     }
   const int bn = tile_n_for(maxm, maxn, kind != G_DW);
-  const int bm = group_tile_m(kind, maxm, bn);
+  int64_t tiles128 = 0;
+  for (int i = 0; i < g.n; ++i)
+    tiles128 += (int64_t)((g.p[i].M + BM - 1) / BM) * ((g.p[i].N + bn - 1) / bn) * g.p[i].split;
+  const int bm = group_tile_m(kind, maxm, bn, tiles128);
   int total = 0;
   for (int i = 0; i < g.n; ++i) {
     Params& p = g.p[i];
