@@ -1144,10 +1144,11 @@ static int tile_n_for(int M, int N, bool rows_are_batch) {
   return tile_n(N);
 }
 
-// Rows per tile of a grouped launch: 64 for forward launches over few rows with 64-wide tiles
-// and fewer than 2 blocks per CU at 128 rows (the rollout's 4096-env batches: twice the blocks
-// per launch, so twice the waves per CU to hide each K step's latency), else BM. LGX_MLP_BM=128 forces the 128-row tile (dev knob).
-static int group_tile_m(int kind, int M, int bn, int64_t tiles128) {
+// Rows per tile of a grouped launch: 64 for forward-kind launches (forward, and input
+// gradients on transposed weights) with 64-wide tiles and fewer than 2 blocks per CU at 128
+// rows — the rollout's 4096-env batches and the update's narrow layers: twice the blocks per
+// launch, so twice the waves per CU to hide each K step's latency — else BM. LGX_MLP_BM=128 forces the 128-row tile (dev knob).
+static int group_tile_m(int kind, int bn, int64_t tiles128) {
   static int forced = -1;
   if (forced < 0) {
     const char* e = getenv("LGX_MLP_BM");
@@ -1157,7 +1158,7 @@ static int group_tile_m(int kind, int M, int bn, int64_t tiles128) {
   if (forced == 64) return kind != lgxm::G_DW && bn == 64 ? 64 : lgxm::BM;  // dev: every 64-wide fwd / dx launch
   // (a launch that already has 2 blocks per CU at 128 rows — the 4096-row actor/critic
   // layer 0, 512 tiles — measured faster with them: 32 vs 35 us)
-  return kind == lgxm::G_FWD && bn == 64 && M <= 8192 && tiles128 < 512 ? 64 : lgxm::BM;
+  return kind == lgxm::G_FWD && bn == 64 && tiles128 < 512 ? 64 : lgxm::BM;
 }
 
 // ================================================================ rollout bookkeeping
@@ -1557,7 +1558,7 @@ int32_t lgx_gemm_group(const lgx_gemm_args* args, int32_t n, void* stream) {
   int64_t tiles128 = 0;
   for (int i = 0; i < g.n; ++i)
     tiles128 += (int64_t)((g.p[i].M + BM - 1) / BM) * ((g.p[i].N + bn - 1) / bn) * g.p[i].split;
-  const int bm = group_tile_m(kind, maxm, bn, tiles128);
+  const int bm = group_tile_m(kind, bn, tiles128);
   int total = 0;
   for (int i = 0; i < g.n; ++i) {
     Params& p = g.p[i];
