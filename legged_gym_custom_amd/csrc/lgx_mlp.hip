@@ -476,7 +476,11 @@ __global__ __launch_bounds__(NT, 2) void gemm_group_kernel(GroupParams g) {
   if (j >= g.per_xcd) return;
   int i = 0;
   while (i + 1 < g.n && j >= g.start[i + 1]) ++i;
+#ifdef LGX_GROUP_PARAMS_COPY
+  const Params p = g.p[i];
+#else
   const Params& p = g.p[i];
+#endif
   const int l = x * (g.start[i + 1] - g.start[i]) + (j - g.start[i]);
   if (l >= p.tiles) return;
   const int m = g.mode[i];
@@ -1012,16 +1016,36 @@ __global__ __launch_bounds__(HT) void loss_heads_bwd(lgx_ppo_head_args h, lgx_au
 #endif
 constexpr int TAIL_BLOCKS = LGX_TAIL_BLOCKS;  // each block ends with a release + counter atomic
 
-// four independent partial sums (loads in flight together), combined in a fixed order
+// A flat segment [lo, hi) of the 16-B aligned grads/params/moments buffers as a scalar head
+// (up to the first multiple of 4), a float4 body [a, b) and a scalar tail: every segment
+// offset is arbitrary, the buffers' bases are aligned (torch allocations), so the body of
+// every array is float4-aligned at the same indices.
+__device__ __forceinline__ void body4(int64_t lo, int64_t hi, int64_t& a, int64_t& b) {
+  a = min(hi, (lo + 3) & ~(int64_t)3);
+  b = max(a, hi & ~(int64_t)3);
+}
+
+// squared norm partial of one thread: float4 body, two loads in flight per pass, four
+// accumulators (one per lane of the float4) combined in a fixed order
 __device__ __forceinline__ float sumsq_range(const float* __restrict__ g, int64_t lo, int64_t hi, int64_t i0,
                                              int64_t stride) {
+  int64_t a, b;
+  body4(lo, hi, a, b);
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-  int64_t i = lo + i0;
-  for (; i + 3 * stride < hi; i += 4 * stride) {
-    const float a = g[i], b = g[i + stride], c = g[i + 2 * stride], d = g[i + 3 * stride];
-    s0 += a * a; s1 += b * b; s2 += c * c; s3 += d * d;
+  const float4* g4 = reinterpret_cast<const float4*>(g + a);
+  const int64_t n4 = (b - a) >> 2;
+  int64_t j = i0;
+  for (; j + stride < n4; j += 2 * stride) {
+    const float4 x = g4[j], y = g4[j + stride];
+    s0 += x.x * x.x; s1 += x.y * x.y; s2 += x.z * x.z; s3 += x.w * x.w;
+    s0 += y.x * y.x; s1 += y.y * y.y; s2 += y.z * y.z; s3 += y.w * y.w;
   }
-  for (; i < hi; i += stride) s0 += g[i] * g[i];
+  if (j < n4) {
+    const float4 x = g4[j];
+    s0 += x.x * x.x; s1 += x.y * x.y; s2 += x.z * x.z; s3 += x.w * x.w;
+  }
+  if (i0 < a - lo) s0 += g[lo + i0] * g[lo + i0];
+  if (i0 < hi - b) s1 += g[b + i0] * g[b + i0];
   return (s0 + s1) + (s2 + s3);
 }
 
@@ -1066,6 +1090,36 @@ __global__ __launch_bounds__(256) void tail_norms(lgx_ppo_tail_args p) {
   }
 }
 
+// Adam over one segment: float4 body (params, grads, moments at the same aligned indices),
+// scalar head and tail
+__device__ __forceinline__ void adam_range(const lgx_ppo_tail_args& p, int64_t lo, int64_t hi, int64_t i0,
+                                           int64_t stride, float c, float b1, float b2, float eps, float ss,
+                                           float sq) {
+  int64_t a, b;
+  body4(lo, hi, a, b);
+  float4* P = reinterpret_cast<float4*>(p.params + a);
+  const float4* G = reinterpret_cast<const float4*>(p.grads + a);
+  float4* M = reinterpret_cast<float4*>(p.exp_avg + a);
+  float4* V = reinterpret_cast<float4*>(p.exp_avg_sq + a);
+  for (int64_t j = i0; j < (b - a) >> 2; j += stride) {
+    float4 x = P[j], m = M[j], v = V[j];
+    const float4 g = G[j];
+    adam1(x.x, g.x * c, m.x, v.x, b1, b2, eps, ss, sq);
+    adam1(x.y, g.y * c, m.y, v.y, b1, b2, eps, ss, sq);
+    adam1(x.z, g.z * c, m.z, v.z, b1, b2, eps, ss, sq);
+    adam1(x.w, g.w * c, m.w, v.w, b1, b2, eps, ss, sq);
+    P[j] = x; M[j] = m; V[j] = v;
+  }
+  if (i0 < a - lo) {
+    const int64_t i = lo + i0;
+    adam1(p.params[i], p.grads[i] * c, p.exp_avg[i], p.exp_avg_sq[i], b1, b2, eps, ss, sq);
+  }
+  if (i0 < hi - b) {
+    const int64_t i = b + i0;
+    adam1(p.params[i], p.grads[i] * c, p.exp_avg[i], p.exp_avg_sq[i], b1, b2, eps, ss, sq);
+  }
+}
+
 __global__ __launch_bounds__(256) void tail_adam(lgx_ppo_tail_args p) {
   const float* sc = p.ws + 2 * TAIL_BLOCKS;
   const float ce = sc[0], cm = sc[1];
@@ -1076,11 +1130,18 @@ __global__ __launch_bounds__(256) void tail_adam(lgx_ppo_tail_args p) {
   const float ssm = lrm / bcm1, sqm = sqrtf(bcm2), sse = p.est_lr / bce1, sqe = sqrtf(bce2);
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  for (int64_t i = p.main_lo + i0; i < p.main_hi; i += stride)
-    adam1(p.params[i], p.grads[i] * cm, p.exp_avg[i], p.exp_avg_sq[i], p.b1_main, p.b2_main, p.eps_main, ssm, sqm);
-  for (int64_t i = p.est_lo + i0; i < p.est_hi; i += stride)
-    adam1(p.params[i], p.grads[i] * ce, p.exp_avg[i], p.exp_avg_sq[i], p.b1_est, p.b2_est, p.eps_est, sse, sqe);
-  for (int64_t i = p.adapt_lo + i0; i < p.adapt_hi; i += stride) p.grads[i] *= cm;
+  adam_range(p, p.main_lo, p.main_hi, i0, stride, cm, p.b1_main, p.b2_main, p.eps_main, ssm, sqm);
+  adam_range(p, p.est_lo, p.est_hi, i0, stride, ce, p.b1_est, p.b2_est, p.eps_est, sse, sqe);
+  int64_t a, b;
+  body4(p.adapt_lo, p.adapt_hi, a, b);
+  float4* g4 = reinterpret_cast<float4*>(p.grads + a);
+  for (int64_t j = i0; j < (b - a) >> 2; j += stride) {
+    float4 x = g4[j];
+    x.x *= cm; x.y *= cm; x.z *= cm; x.w *= cm;
+    g4[j] = x;
+  }
+  if (i0 < a - p.adapt_lo) p.grads[p.adapt_lo + i0] *= cm;
+  if (i0 < p.adapt_hi - b) p.grads[b + i0] *= cm;
 }
 
 // dynamic LDS: two K-step stages of hi/lo A and B images, or the fp32 C image (reused)
@@ -1607,7 +1668,10 @@ int32_t lgx_mlp_pick_split_group(const int32_t* M, const int32_t* N, const int32
     if (M[i] < 0 || N[i] < 0 || K[i] < 0) return fail("lgx_mlp_pick_split_group: negative size");
     maxn = std::max(maxn, (int)N[i]);
   }
-  const int bn = tile_n(maxn), slots = group_slots(bn);
+  const int bn = tile_n(maxn);
+  // LGX_DW_SLOTS: dev knob (block budget of the grouped weight-gradient launch)
+  const char* knob = getenv("LGX_DW_SLOTS");
+  const int slots = knob ? std::max(64, atoi(knob)) : group_slots(bn);
   // equal K chunks for every problem: the smallest chunk (a multiple of the K step, at least
   // 256 rows) whose block count fits one residency wave; every split >= 2 (bias gradient)
   int chunk = 256;
