@@ -48,7 +48,8 @@ constexpr int BM = 128, BKS = 32, NT = 256;
 #ifndef LGX_MV_ROWMAJOR
 #define LGX_MV_ROWMAJOR 1
 #endif
-constexpr int PF = LGX_PF;               // global-load register sets (prefetch depth in K steps)
+// LGX_PF: global-load register sets (prefetch depth in K steps), gemm_tile's PF (3 measured
+// slower for every launch: 246 VGPRs in the weight-gradient tile)
 constexpr int PITCH = BKS;               // bf16 per LDS row (64 B, swizzled: lds_off)
 enum Mode { KV = 1, MV = 3, MVE = 4 };  // MVE: MV for a row count that is not a multiple of 4
 
@@ -237,7 +238,7 @@ __device__ __forceinline__ float elu(float v) {
 // One output tile (logical index L: n fastest, then m, then the K split) of one GEMM.
 // BM_ rows x BN_ columns; 4 waves as 2 (rows) x 2 (columns), each BM_/2 x BN_/2. BM_ = 64
 // serves the rollout's 4096-row forward launches (twice the blocks, half the work per K step).
-template <int AM, int BMODE, bool COLSUM, int BN_, int BM_ = BM>
+template <int AM, int BMODE, bool COLSUM, int BN_, int BM_ = BM, int PF = LGX_PF>
 __device__ __forceinline__ void gemm_tile(const Params& p, const int L) {
   using SA = Stager<AM, BM_>;
   using SB = Stager<BMODE, BN_>;
@@ -476,20 +477,24 @@ __global__ __launch_bounds__(NT, 2) void gemm_group_kernel(GroupParams g) {
   if (j >= g.per_xcd) return;
   int i = 0;
   while (i + 1 < g.n && j >= g.start[i + 1]) ++i;
-#ifdef LGX_GROUP_PARAMS_COPY
-  const Params p = g.p[i];
-#else
-  const Params& p = g.p[i];
-#endif
   const int l = x * (g.start[i + 1] - g.start[i]) + (j - g.start[i]);
-  if (l >= p.tiles) return;
   const int m = g.mode[i];
+  // Forward kinds take a register copy of their problem's parameters (the tile loop then
+  // reads them from SGPRs, not by a scalar load from the argument segment every K step:
+  // forward launches 3-5 % shorter); the weight-gradient tile measured 14 % slower with
+  // the copy (more SGPRs live across its loop), so it keeps the reference.
   if constexpr (KIND == G_FWD) {
+    const Params p = g.p[i];
+    if (l >= p.tiles) return;
     gemm_tile<KV, KV, false, BN_, BM_>(p, l);
   } else if constexpr (KIND == G_DX) {
+    const Params p = g.p[i];
+    if (l >= p.tiles) return;
     if (m) gemm_tile<KV, MVE, false, BN_, BM_>(p, l);
     else gemm_tile<KV, MV, false, BN_, BM_>(p, l);
   } else {
+    const Params& p = g.p[i];
+    if (l >= p.tiles) return;
     if (m == 0) gemm_tile<MV, MV, true, BN_>(p, l);
     else if (m == 1) gemm_tile<MVE, MV, true, BN_>(p, l);
     else if (m == 2) gemm_tile<MV, MVE, true, BN_>(p, l);
