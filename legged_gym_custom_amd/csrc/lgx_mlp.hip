@@ -1210,6 +1210,17 @@ static int tile_n_for(int M, int N, bool rows_are_batch) {
   return tile_n(N);
 }
 
+// Tile width of a grouped weight-gradient launch (LGX_DW_BN: dev knob, 64 or 128)
+static int dw_tile_n(int N) {
+  static int forced = -1;
+  if (forced < 0) {
+    const char* e = getenv("LGX_DW_BN");
+    forced = e ? atoi(e) : 0;
+  }
+  if (forced == 64 || forced == 128) return forced;
+  return tile_n_for(0, N, false);
+}
+
 // Rows per tile of a grouped launch: 64 for forward-kind launches (forward, and input
 // gradients on transposed weights) with 64-wide tiles and fewer than 2 blocks per CU at 128
 // rows — the rollout's 4096-env batches and the update's narrow layers: twice the blocks per
@@ -1620,7 +1631,7 @@ int32_t lgx_gemm_group(const lgx_gemm_args* args, int32_t n, void* stream) {
       std::swap(g.p[k], g.p[k - 1]);
       std::swap(g.mode[k], g.mode[k - 1]);
     }
-  const int bn = tile_n_for(maxm, maxn, kind != G_DW);
+  const int bn = kind == G_DW ? dw_tile_n(maxn) : tile_n_for(maxm, maxn, true);
   int64_t tiles128 = 0;
   for (int i = 0; i < g.n; ++i)
     tiles128 += (int64_t)((g.p[i].M + BM - 1) / BM) * ((g.p[i].N + bn - 1) / bn) * g.p[i].split;
@@ -1673,7 +1684,7 @@ int32_t lgx_mlp_pick_split_group(const int32_t* M, const int32_t* N, const int32
     if (M[i] < 0 || N[i] < 0 || K[i] < 0) return fail("lgx_mlp_pick_split_group: negative size");
     maxn = std::max(maxn, (int)N[i]);
   }
-  const int bn = tile_n(maxn);
+  const int bn = dw_tile_n(maxn);
   // LGX_DW_SLOTS: dev knob (block budget of the grouped weight-gradient launch)
   const char* knob = getenv("LGX_DW_SLOTS");
   const int slots = knob ? std::max(64, atoi(knob)) : group_slots(bn);
