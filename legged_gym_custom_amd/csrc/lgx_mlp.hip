@@ -659,7 +659,10 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, 
 }
 
 // ---------------------------------------------------------------- PPO loss head
-constexpr int HT = 256;     // threads per block (rows per block and grid-stride pass)
+#ifndef LGX_HT
+#define LGX_HT 256
+#endif
+constexpr int HT = LGX_HT;  // threads per block (rows per block and grid-stride pass)
 // one row per thread (grid-stride loops, so any grid is correct; fewer blocks measured slower)
 static unsigned head_grid(int B) { return (unsigned)((B + HT - 1) / HT); }
 constexpr int HMAXA = 16;   // max actions
@@ -680,7 +683,11 @@ __device__ void block_sum(float (&v)[NV], float* red) {
   __syncthreads();
   if (threadIdx.x == 0)
 #pragma unroll
-    for (int k = 0; k < NV; ++k) v[k] = red[k] + red[NV + k] + red[2 * NV + k] + red[3 * NV + k];
+    for (int k = 0; k < NV; ++k) {
+      float t = red[k];
+      for (int w = 1; w < (int)(blockDim.x >> 6); ++w) t += red[w * NV + k];  // waves in order
+      v[k] = t;
+    }
 }
 
 // The last block to finish reduces the per-block partials. Thread 0 wrote this block's

@@ -1030,7 +1030,7 @@ class _PPOHeadFn(torch.autograd.Function):
         mu_, value_, actions_, old_logp_, adv_, tv_, ret_, old_mu_, old_sigma_ = ts
         std_ = std.contiguous()
         out = torch.empty(4, device=dev) if out is None else out
-        ws = torch.empty(16 * ((B + 255) // 256), device=dev)
+        ws = torch.empty(16 * ((B + 63) // 64), device=dev)  # per-block partials, blocks of >= 64 rows
         a = HeadArgs(mu=mu_.data_ptr(), value=value_.data_ptr(), std=std_.data_ptr(), actions=actions_.data_ptr(),
                      old_logp=old_logp_.data_ptr(), adv=adv_.data_ptr(), target_values=tv_.data_ptr(),
                      returns=ret_.data_ptr(), old_mu=old_mu_.data_ptr(), old_sigma=old_sigma_.data_ptr(), B=B, A=A,
@@ -1059,7 +1059,7 @@ class _PPOHeadFn(torch.autograd.Function):
         direct = sp.requires_grad and sp.is_leaf and sp.grad is not None and sp.grad.is_contiguous() and \
             not sp._backward_hooks
         dstd = sp.grad if direct else torch.empty_like(std)
-        ws = torch.empty(16 * ((B + 255) // 256), device=dev)
+        ws = torch.empty(16 * ((B + 63) // 64), device=dev)  # per-block partials, blocks of >= 64 rows
         a = HeadArgs(mu=mu.data_ptr(), value=value.data_ptr(), std=std.data_ptr(), actions=actions.data_ptr(),
                      old_logp=old_logp.data_ptr(), adv=adv.data_ptr(), target_values=tv.data_ptr(),
                      returns=ret.data_ptr(), B=B, A=A, clip=ctx.clip, clipped_value=ctx.clipped, g=g.data_ptr(),
@@ -1092,7 +1092,7 @@ class _AuxLossFn(torch.autograd.Function):
         E = e.shape[1]
         dev = p.device
         out = torch.empty(2, device=dev) if out is None else out
-        ws = torch.empty(2 * ((B + 255) // 256), device=dev)
+        ws = torch.empty(2 * ((B + 63) // 64), device=dev)  # per-block partials, blocks of >= 64 rows
         args = AuxArgs(p=p.data_ptr(), a=a.data_ptr(), L=L, e=e.data_ptr(), t=t.data_ptr(), E=E, B=B,
                        out=out.data_ptr(), ws=ws.data_ptr(), counter=_counter(dev, "aux").data_ptr())
         _check(lib().lgx_aux_loss_forward(C.byref(args), _stream()), "lgx_aux_loss_forward")
@@ -1137,8 +1137,8 @@ class _LossHeadsFn(torch.autograd.Function):
         a_, e_, t_ = (x.contiguous() for x in (a, e, t))
         out = torch.empty(4, device=dev) if out is None else out
         out_aux = torch.empty(2, device=dev) if out_aux is None else out_aux
-        ws = torch.empty(16 * ((B + 255) // 256), device=dev)
-        ws_aux = torch.empty(2 * ((B + 255) // 256), device=dev)
+        ws = torch.empty(16 * ((B + 63) // 64), device=dev)  # per-block partials, blocks of >= 64 rows
+        ws_aux = torch.empty(2 * ((B + 63) // 64), device=dev)  # per-block partials, blocks of >= 64 rows
         h = HeadArgs(mu=mu_.data_ptr(), value=value_.data_ptr(), std=std_.data_ptr(), actions=actions_.data_ptr(),
                      old_logp=old_logp_.data_ptr(), adv=adv_.data_ptr(), target_values=tv_.data_ptr(),
                      returns=ret_.data_ptr(), old_mu=old_mu_.data_ptr(), old_sigma=old_sigma_.data_ptr(), B=B, A=A,
@@ -1171,7 +1171,7 @@ class _LossHeadsFn(torch.autograd.Function):
         dstd = sp.grad if direct else torch.empty_like(std)
         dp = torch.empty(p.shape, device=dev, dtype=torch.float32)  # contiguous even when p is a span
         de = torch.empty_like(e)
-        ws = torch.empty(16 * ((B + 255) // 256), device=dev)
+        ws = torch.empty(16 * ((B + 63) // 64), device=dev)  # per-block partials, blocks of >= 64 rows
         h = HeadArgs(mu=mu.data_ptr(), value=value.data_ptr(), std=std.data_ptr(), actions=actions.data_ptr(),
                      old_logp=old_logp.data_ptr(), adv=adv.data_ptr(), target_values=tv.data_ptr(),
                      returns=ret.data_ptr(), B=B, A=A, clip=ctx.clip, clipped_value=ctx.clipped, g=g.data_ptr(),
