@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define LGX_MLP_ABI_VERSION 4
+#define LGX_MLP_ABI_VERSION 5
 
 enum {
   LGX_EPI_BIAS = 1,  /* + bias[n] */
@@ -197,7 +197,8 @@ int32_t lgx_ppo_tail(const lgx_ppo_tail_args* args, void* stream);
 
 /* Up to LGX_COPY_MAX device-to-device copies in one launch (the storage writes of one
  * rollout step). Each entry: nbytes from src to dst; 16-byte aligned entries whose size
- * is a multiple of 16 take the vector path. dst_stride is read by lgx_gather_rows only. */
+ * is a multiple of 16 take the vector path. dst_stride is read by lgx_gather_rows only
+ * (added in ABI v5: the descriptor is 32 bytes; v4 callers used 24). */
 #define LGX_COPY_MAX 16
 typedef struct lgx_copy_desc {
   const void* src; void* dst; int64_t nbytes;

@@ -663,6 +663,8 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, 
 #define LGX_HT 256
 #endif
 constexpr int HT = LGX_HT;  // threads per block (rows per block and grid-stride pass)
+// the loss heads' cross-wave scratch (red[4 * ...]) holds at most 4 waves
+static_assert(HT % 64 == 0 && HT >= 64 && HT <= 256, "LGX_HT: 64..256 threads, whole waves");
 // one row per thread (grid-stride loops, so any grid is correct; fewer blocks measured slower)
 static unsigned head_grid(int B) { return (unsigned)((B + HT - 1) / HT); }
 constexpr int HMAXA = 16;   // max actions

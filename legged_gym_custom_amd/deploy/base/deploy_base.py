@@ -174,6 +174,7 @@ class BaseController:
         self.smoothed_cmd = np.zeros(3, dtype=np.float32)
         self.projected_gravity = np.array([0.0, 0.0, -1.0], dtype=np.float32)
         self.phase = 0.0
+        self.roll = self.pitch = self.yaw = 0.0  # last tick's IMU angles, offsets applied (deploy_base.py:184,219-220)
         self.obs = np.zeros(cfg.num_obs, dtype=np.float32)
         self._proprio = ProprioBuilder(cfg)
         self._history = ObsHistory(cfg.buffer_length, cfg.num_proprio)
@@ -184,6 +185,11 @@ class BaseController:
     @property
     def obs_history(self):
         return self._history.rows
+
+    @property
+    def first_step_ever(self):
+        """True until the first observation fills the history (deploy_base.py:47,237-238)."""
+        return not self._history.primed
 
     @property
     def mode(self):
@@ -220,6 +226,10 @@ class BaseController:
     def build_observation(self, elapsed_time_s):
         """This tick's policy input, (1, num_obs) clipped: [history before this tick | current]."""
         self.projected_gravity = self._get_gravity_orientation(self.base_quat)
+        c = self.cfg
+        roll, pitch, self.yaw = quaternion_to_euler(self.base_quat)
+        self.roll = roll + c.roll_offset * (np.pi / 180)
+        self.pitch = pitch + c.pitch_offset * (np.pi / 180)
         self.phase = self._proprio.gait_phase(elapsed_time_s)
         state = {"ang_vel": self.ang_vel, "quat": self.base_quat, "cmd": self.cmd, "qj": self.qj, "dqj": self.dqj,
                  "actions": self.actions}

@@ -20,7 +20,7 @@ import torch.nn as nn
 _LIB_PATH = os.environ.get("LGX_MLP_LIB") or os.path.join(
     os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))), "lib", "liblgx_mlp.so")
 _lib = None
-ABI_VERSION = 4
+ABI_VERSION = 5
 EPI_BIAS, EPI_ELU, EPI_DELU, EPI_ACCUM = 1, 2, 4, 8
 EXPORTED = ["lgx_mlp_abi_version", "lgx_mlp_sizeof_gemm_args", "lgx_mlp_pick_split", "lgx_gemm",
             "lgx_mlp_last_error", "lgx_adam_step", "lgx_ppo_head_forward", "lgx_ppo_head_backward",
@@ -897,7 +897,8 @@ def _conv_dims(mod, H):
 
 class _AdaptationFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, h, dims, fc_w, fc_b, c1_w, c1_b, c2_w, c2_b, f_w, f_b):
+    def forward(ctx, h, dims, want_grad, fc_w, fc_b, c1_w, c1_b, c2_w, c2_b, f_w, f_b):
+        global ADAPT_INPLACE_CALLS
         C1, C2, C3, k1, s1, k2, s2, L1, L2 = dims
         Bn, H, P = h.shape
         dev = h.device
@@ -906,9 +907,12 @@ class _AdaptationFn(torch.autograd.Function):
         # of every row, read in place, instead of on a packed copy of the H history blocks
         # (the conv windows below only read blocks < H); one copy of B x H x P floats less
         Hs = h.stride(0) // P if h.stride(2) == 1 and h.stride(1) == P and h.stride(0) % P == 0 else 0
-        inplace = (not any(ctx.needs_input_grad) and Hs > H and
+        # (ctx.needs_input_grad reports requires_grad whatever the grad mode, so the caller
+        # decides: want_grad = grad mode on and some input requires grad)
+        inplace = (not want_grad and Hs > H and
                    h.storage_offset() + Bn * Hs * P <= h.untyped_storage().nbytes() // h.element_size())
         if inplace:
+            ADAPT_INPLACE_CALLS += 1
             x = h.as_strided((Bn * Hs, P), (P, 1))
         else:
             Hs = H
@@ -979,7 +983,10 @@ class _AdaptationFn(torch.autograd.Function):
         dh = None
         if ctx.needs_input_grad[0]:
             dh = linear_input_grad(g0, fc_w, None).reshape(Bn, H, -1)
-        return (dh, None) + (None,) * 8
+        return (dh, None, None) + (None,) * 8
+
+
+ADAPT_INPLACE_CALLS = 0  # forwards that took the in-place history read (tests check it ran)
 
 
 def adaptation_forward(mod, hist):
@@ -991,7 +998,8 @@ def adaptation_forward(mod, hist):
                          f"{mod.fc_final[0].in_features} (the reference assumes history 10, Q17)")
     ps = (mod.fc_encoder[0].weight, mod.fc_encoder[0].bias, mod.conv_layers[0].weight, mod.conv_layers[0].bias,
           mod.conv_layers[2].weight, mod.conv_layers[2].bias, mod.fc_final[0].weight, mod.fc_final[0].bias)
-    return _AdaptationFn.apply(hist, dims, *ps)
+    want_grad = torch.is_grad_enabled() and (hist.requires_grad or any(p.requires_grad for p in ps))
+    return _AdaptationFn.apply(hist, dims, want_grad, *ps)
 
 
 # ---------------------------------------------------------------------------------------

@@ -1,5 +1,7 @@
 """TaskRegistry — drop-in for legged_gym/utils/task_registry.py:14-128."""
 import os
+
+import numpy as np
 from datetime import datetime
 from typing import Tuple
 
@@ -37,7 +39,7 @@ class TaskRegistry:
         if env_cfg is None:
             env_cfg, _ = self.get_cfgs(name)
         env_cfg, _ = update_cfg_from_args(env_cfg, None, args)
-        env_cfg.seed = set_seed(env_cfg.seed)  # -1 resolved here, so the env kernel's RNG follows it
+        env_cfg.seed = set_seed(_shared_seed(env_cfg.seed))  # -1 resolved here, so the env kernel's RNG follows it
         sim_params = parse_sim_params(args, {"sim": class_to_dict(env_cfg.sim)})
         env = task_class(cfg=env_cfg, sim_params=sim_params, physics_engine=args.physics_engine,
                          sim_device=args.sim_device, headless=args.headless)
@@ -54,6 +56,10 @@ class TaskRegistry:
         elif name is not None:
             print(f"'train_cfg' provided -> Ignoring 'name={name}'")
         _, train_cfg = update_cfg_from_args(None, train_cfg, args)
+        if train_cfg.seed == -1 and getattr(getattr(env, "cfg", None), "seed", -1) != -1:
+            # the env resolved -1 (once, shared by all ranks): the runner's per-rank reseed
+            # follows the same value
+            train_cfg.seed = env.cfg.seed
         if log_root == "default":
             log_root = os.path.join(LEGGED_GYM_ROOT_DIR, "logs", train_cfg.runner.experiment_name)
             log_dir = os.path.join(log_root, datetime.now().strftime("%b%d_%H-%M-%S") + "_" + train_cfg.runner.run_name)
@@ -67,6 +73,18 @@ class TaskRegistry:
             print(f"Loading model from: {resume_path}")
             runner.load(resume_path)
         return runner, train_cfg
+
+
+def _shared_seed(seed):
+    """seed -1 draws a random seed; under world size > 1 rank 0 draws it and broadcasts it,
+    so every rank's setup randomisation (drawn over all global envs, then sliced) and env
+    Philox streams come from the same value (two shards == one env)."""
+    import torch.distributed as dist
+    if seed != -1 or not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1):
+        return seed
+    box = [int(np.random.randint(0, 10000)) if dist.get_rank() == 0 else None]
+    dist.broadcast_object_list(box, src=0)
+    return box[0]
 
 
 task_registry = TaskRegistry()

@@ -115,12 +115,17 @@ def test_deploy_observation_equals_env_observation(cfg):
         obs = c.build_observation(float(a["episode_length"][e]) * dt)
         np.testing.assert_allclose(obs[0, -52:].numpy(), a["obs"][e, -52:], atol=2e-5, rtol=1e-5,
                                    err_msg=f"env {e}")
+        # the reference's attributes of the same tick (deploy_base.py:184,219-220)
+        np.testing.assert_allclose([c.roll, c.pitch], obs[0, -52 + 3:-52 + 5].numpy(), atol=1e-6)
+        assert np.isfinite(c.yaw)
 
 
 def test_history_fill_then_roll(cfg):
     c = _controller(cfg)
     c.base_quat = np.array([1, 0, 0, 0], np.float32)
+    assert c.first_step_ever
     o1 = c.build_observation(0.0)
+    assert not c.first_step_ever
     assert torch.all(o1[0, :52 * 10] == 0)  # network input: zero history on the first tick
     first = c.obs_history.copy()
     assert np.all(first == first[0])         # then filled with the first observation

@@ -113,11 +113,18 @@ def test_adaptation_encoder_inplace_history_bitwise():
     enc = AdaptationEncoder(num_proprio=52, history_buffer_length=10, output_dim=20).to(dev)
     obs = torch.randn(3000, 572, device=dev)
     hist = obs[:, :-52].reshape(-1, 10, 52)
+    from legged_gym_custom_amd.rsl_rl.modules import hip_mlp
+    n0 = hip_mlp.ADAPT_INPLACE_CALLS
     with torch.no_grad():
         a = enc(hist)                       # in place (strided view of obs)
+        assert hip_mlp.ADAPT_INPLACE_CALLS == n0 + 1, "the in-place branch did not run"
         b = enc(hist.contiguous())          # packed
+    with torch.inference_mode():
+        d = enc(hist)
+    assert hip_mlp.ADAPT_INPLACE_CALLS == n0 + 2
     c = enc(hist)                           # grad enabled: packed path inside
-    assert torch.equal(a, b) and torch.equal(a, c.detach())
+    assert hip_mlp.ADAPT_INPLACE_CALLS == n0 + 2
+    assert torch.equal(a, b) and torch.equal(a, c.detach()) and torch.equal(a, d)
 
 
 @pytest.mark.parametrize("clipped", [True, False])
