@@ -215,12 +215,22 @@ int32_t lgx_gather_rows(const lgx_copy_desc* descs, int32_t n, const int64_t* id
 /* PPO.act action head (actor_critic.py:205-226 + ppo.py:141-146) for a diagonal Gaussian:
  *   a = mean + std * eps,  logp_i = sum_j -(a-mean)^2/(2 std_j^2) - log std_j - log sqrt(2 pi)
  * (torch.distributions.Normal.log_prob op order), written straight into the storage rows:
- * actions [B,A], mu [B,A] (= mean), sigma [B,A] (= std broadcast), logp [B]. */
+ * actions [B,A], mu [B,A] (= mean), sigma [B,A] (= std broadcast), logp [B].
+ * eps: a given [B,A] standard-normal sample, or NULL: drawn in the kernel per (global env
+ * env_offset + row, env step *step_dev, action) from the env's Philox4x32-10 counter layout on
+ * stream LGX_ACT_NOISE_STREAM (Box-Muller) — the noise of an env does not depend on which
+ * rank or shard steps it, so sharded rollouts equal one GPU's. step_dev: the env's device step
+ * counter (lgx_step_dev; the number of the step these actions drive). Fields after
+ * actions_copy: ABI v5. */
+#define LGX_ACT_NOISE_STREAM 2
 typedef struct lgx_act_head_args {
   const float* mean; const float* std; const float* eps;
   float* actions; float* mu; float* sigma; float* logp;
   int32_t B, A;
   float* actions_copy;       /* optional second destination of the actions (the env's input buffer) */
+  const int64_t* step_dev;   /* eps == NULL: device step counter */
+  uint64_t seed;             /* eps == NULL: the env's seed (Philox key) */
+  int64_t env_offset;        /* eps == NULL: global id of row 0 */
 } lgx_act_head_args;
 int32_t lgx_act_head(const lgx_act_head_args* args, void* stream);
 

@@ -29,6 +29,7 @@
 #include <stdlib.h>
 
 #include "../../include/lgx_mlp.h"
+#include "lgx_device.h"  // philox4x32_10 / u01: the env's counter RNG (the act head's noise)
 
 #ifndef LGX_ELU_EXACT
 #define LGX_ELU_EXACT 0
@@ -1304,15 +1305,35 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(CopyBatch cb, const in
   }
 }
 
+// Standard normal of action j of global env `gid` at env step `step` (eps == NULL mode):
+// Philox4x32-10 with the env's counter layout on stream LGX_ACT_NOISE_STREAM, block j / 4;
+// its 4 uniforms make 2 Box-Muller pairs, action j takes cos (even j) or sin (odd j) of
+// pair (j / 2) % 2. oracle/philox.py act_noise states the same.
+__device__ __forceinline__ float act_noise(uint64_t seed, uint32_t gid, uint64_t step, int j) {
+  uint32_t o[4];
+  philox4x32_10(gid, (uint32_t)step, (uint32_t)(j >> 2) | ((uint32_t)LGX_ACT_NOISE_STREAM << 16),
+                (uint32_t)(step >> 32), (uint32_t)seed, (uint32_t)(seed >> 32), o);
+  const int p = j & 2;
+  const float u1 = 1.0f - u01(o[p]);  // (0, 1]
+  const float u2 = u01(o[p + 1]);
+  const float r = sqrtf(-2.0f * logf(u1));
+  const float th = 6.28318530717958647692f * u2;
+  return (j & 1) ? r * sinf(th) : r * cosf(th);
+}
+
 __global__ __launch_bounds__(256) void act_head_kernel(lgx_act_head_args p) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= p.B) return;
   const float c = 0.91893853320467274178f;  // log(sqrt(2 pi))
+  const bool draw = p.eps == nullptr;
+  const uint64_t step = draw ? (uint64_t)*p.step_dev : 0;
+  const uint32_t gid = (uint32_t)(p.env_offset + i);
   float lp = 0.0f;
   for (int j = 0; j < p.A; ++j) {
     const size_t k = (size_t)i * p.A + j;
     const float m = p.mean[k], sd = p.std[j];
-    const float a = m + sd * p.eps[k];
+    const float e = draw ? act_noise(p.seed, gid, step, j) : p.eps[k];
+    const float a = m + sd * e;
     const float d = a - m;
     lp += -(d * d) / (2.0f * (sd * sd)) - logf(sd) - c;
     p.actions[k] = a;
@@ -1802,8 +1823,10 @@ int32_t lgx_gather_rows(const lgx_copy_desc* descs, int32_t n, const int64_t* id
 }
 
 int32_t lgx_act_head(const lgx_act_head_args* a, void* stream) {
-  if (!a || !a->mean || !a->std || !a->eps || !a->actions || !a->mu || !a->sigma || !a->logp || a->B < 0 || a->A <= 0)
+  if (!a || !a->mean || !a->std || !a->actions || !a->mu || !a->sigma || !a->logp || a->B < 0 || a->A <= 0)
     return fail("lgx_act_head: bad arguments");
+  if (!a->eps && (!a->step_dev || a->env_offset < 0 || a->env_offset + a->B > (int64_t)UINT32_MAX))
+    return fail("lgx_act_head: eps == NULL needs step_dev and a 32-bit global env range");
   if (a->B == 0) return 0;
   hipLaunchKernelGGL(lgxm::act_head_kernel, dim3((a->B + 255) / 256), dim3(256), 0, static_cast<hipStream_t>(stream),
                      *a);

@@ -166,6 +166,10 @@ class PPO:
         self.actor_critic = actor_critic.to(self.device)
         self.storage = None
         self.act_dst = None  # optional [num_envs, A] device buffer the act head also writes (the env's input)
+        # optional (seed, device step counter, global env offset) of the env: the act head then
+        # draws the exploration noise per (global env, env step) in the kernel (Philox) instead
+        # of torch.randn_like, so env shards on several ranks sample what one GPU would
+        self.act_noise = None
         self.estimator = estimator.to(self.device)
         ac = self.actor_critic
         self.on_gpu = str(device).startswith("cuda")
@@ -307,10 +311,11 @@ class PPO:
                 latent = ac.adaptation_encoder(obs) if adaptation_mode else outs[2]
                 mean, t.values = hip_mlp.forward_group([(ac.actor, (obs, latent, scan_latent, estimated_obs)),
                                                         (ac.critic, critic_obs)])
-                eps = torch.randn_like(mean)
+                noise = self.act_noise
+                eps = torch.randn_like(mean) if noise is None else None
                 dst = self.act_dst if self.act_dst is not None and self.act_dst.shape == mean.shape else None
                 hip_mlp.act_head(mean, ac.std.detach(), eps, s.actions[k], s.mu[k], s.sigma[k], s.actions_log_prob[k],
-                                 actions_copy=dst)
+                                 actions_copy=dst, noise=noise)
             t.actions, t.action_mean, t.action_sigma = s.actions[k], s.mu[k], s.sigma[k]
             t.actions_log_prob = s.actions_log_prob[k].view(-1)
             return t.actions if dst is None else dst

@@ -91,7 +91,8 @@ class CopyDesc(C.Structure):
 class ActHeadArgs(C.Structure):
     """Mirror of lgx_act_head_args."""
     _fields_ = [(n, C.c_void_p) for n in ("mean", "std", "eps", "actions", "mu", "sigma", "logp")] + \
-               [("B", C.c_int32), ("A", C.c_int32), ("actions_copy", C.c_void_p)]
+               [("B", C.c_int32), ("A", C.c_int32), ("actions_copy", C.c_void_p), ("step_dev", C.c_void_p),
+                ("seed", C.c_uint64), ("env_offset", C.c_int64)]
 
 
 class TransitionArgs(C.Structure):
@@ -251,15 +252,26 @@ def gather_rows(srcs, idx, dsts=None):
     return outs
 
 
-def act_head(mean, std, eps, actions, mu, sigma, logp, actions_copy=None):
+def act_head(mean, std, eps, actions, mu, sigma, logp, actions_copy=None, noise=None):
     """a = mean + std * eps and the Normal log-prob row sums, written into storage rows (and
-    the actions also into `actions_copy`, e.g. the env's input buffer, when given)."""
+    the actions also into `actions_copy`, e.g. the env's input buffer, when given).
+    eps None: `noise` = (seed, step_dev, env_offset) and the kernel draws eps per global env
+    and env step (Philox, lgx_mlp.h LGX_ACT_NOISE_STREAM)."""
     B, A = mean.shape
     if actions_copy is not None and (actions_copy.shape != mean.shape or not actions_copy.is_contiguous()):
         raise MlpLibError("act_head: actions_copy must be a contiguous [B, A] buffer")
-    args = ActHeadArgs(mean.data_ptr(), std.data_ptr(), eps.data_ptr(), actions.data_ptr(), mu.data_ptr(),
-                       sigma.data_ptr(), logp.data_ptr(), B, A,
-                       None if actions_copy is None else actions_copy.data_ptr())
+    if eps is None:
+        if noise is None:
+            raise MlpLibError("act_head: eps=None needs noise=(seed, step_dev, env_offset)")
+        seed, step_dev, off = noise
+        if step_dev.dtype != torch.int64 or step_dev.device != mean.device:
+            raise MlpLibError("act_head: step_dev must be an int64 tensor on the actions' device")
+        extra = (step_dev.data_ptr(), int(seed) & 0xFFFFFFFFFFFFFFFF, int(off))
+    else:
+        extra = (None, 0, 0)
+    args = ActHeadArgs(mean.data_ptr(), std.data_ptr(), None if eps is None else eps.data_ptr(), actions.data_ptr(),
+                       mu.data_ptr(), sigma.data_ptr(), logp.data_ptr(), B, A,
+                       None if actions_copy is None else actions_copy.data_ptr(), *extra)
     _check(lib().lgx_act_head(C.byref(args), _stream()), "lgx_act_head")
 
 

@@ -106,6 +106,10 @@ class OnPolicyRunner:
         dst = getattr(env, "actions_in", None)
         if torch.is_tensor(dst) and dst.is_cuda and dst.device == torch.device(device) and dst.is_contiguous():
             self.alg.act_dst = dst
+            step_dev = getattr(env, "_step_dev", None)
+            if torch.is_tensor(step_dev) and step_dev.device == dst.device and hasattr(env, "env_id_offset"):
+                # exploration noise per (global env, env step), drawn in the act head
+                self.alg.act_noise = (int(env.seed), step_dev, int(env.env_id_offset))
         self.log_dir = log_dir if self.rank == 0 else None
         # per-step episode bookkeeping (on_policy_runner.py:160-170) runs whenever there is a
         # log dir, as in the reference; bench.py also switches it on without one
@@ -251,8 +255,7 @@ class OnPolicyRunner:
         if self.log_dir is not None and self.writer is None:
             self.writer = _make_writer(self.log_dir)
         if init_at_random_ep_len:
-            self.env.episode_length_buf = torch.randint_like(self.env.episode_length_buf,
-                                                             high=int(self.env.max_episode_length))
+            self.env.episode_length_buf = self._random_episode_lengths()
         env = self.env
         self._obs = [env.get_observations().to(self.device), env.get_privileged_observations().to(self.device),
                      env.get_critic_observations().to(self.device), env.get_estimated_observations().to(self.device),
@@ -305,6 +308,21 @@ class OnPolicyRunner:
         self.current_learning_iteration += num_learning_iterations
         if self.log_dir is not None:
             self.save(os.path.join(self.log_dir, "model_{}.pt".format(self.current_learning_iteration)))
+
+    def _random_episode_lengths(self):
+        """on_policy_runner.py:121-122 (uniform in [0, max_episode_length)). An env shard
+        (env_id_offset / num_envs_total) takes its slice of one draw over all global envs from a
+        generator keyed by the env seed, so ranks start the episodes one GPU would."""
+        env = self.env
+        buf = env.episode_length_buf
+        total = getattr(env, "num_envs_total", None)
+        off = getattr(env, "env_id_offset", None)
+        seed = getattr(env, "seed", None)
+        if total is None or off is None or seed is None:
+            return torch.randint_like(buf, high=int(env.max_episode_length))
+        g = torch.Generator().manual_seed(int(seed) & 0x7FFFFFFFFFFFFFFF)
+        full = torch.randint(int(env.max_episode_length), (int(total),), generator=g, dtype=buf.dtype)
+        return full[int(off):int(off) + env.num_envs].to(buf.device)
 
     def _host_stats(self):
         """One transfer per iteration: the rings (last <=100 completed episodes, oldest

@@ -40,6 +40,7 @@ def num_blocks(num_proprio):
 
 STREAM_STEP = 0       # draws inside env.step()
 STREAM_RESET = 1      # draws inside an external reset_idx() call (BaseTask.reset)
+STREAM_ACT = 2        # the PPO act head's exploration noise (lgx_mlp.h LGX_ACT_NOISE_STREAM)
 
 
 def philox4x32_10(c0, c1, c2, c3, k0, k1):
@@ -88,6 +89,20 @@ def uniform_table(seed, env_ids, step, stream=STREAM_STEP, num_blocks=NUM_BLOCKS
         out[:, 4 * b + 1] = to_uniform(x1)
         out[:, 4 * b + 2] = to_uniform(x2)
         out[:, 4 * b + 3] = to_uniform(x3)
+    return out
+
+
+def act_noise(seed, env_ids, step, num_actions):
+    """[len(env_ids), num_actions] standard normals the act head draws when it is given no
+    eps (lgx_mlp.hip act_noise): block j // 4 of stream STREAM_ACT, Box-Muller on uniforms
+    (u[p], u[p + 1]), p = j & 2, with u1 = 1 - u[p]; cos for even j, sin for odd j (float64 here)."""
+    u = uniform_table(seed, env_ids, step, STREAM_ACT, (num_actions + 3) // 4).astype(np.float64)
+    out = np.empty((u.shape[0], num_actions))
+    for j in range(num_actions):
+        b, p = j >> 2, j & 2
+        r = np.sqrt(-2.0 * np.log(1.0 - u[:, 4 * b + p]))
+        th = 2.0 * np.pi * u[:, 4 * b + p + 1]
+        out[:, j] = r * (np.sin(th) if j & 1 else np.cos(th))
     return out
 
 

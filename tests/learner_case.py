@@ -16,12 +16,19 @@ Sequence recorded (the runner's first two iterations, on_policy_runner.py:143-18
   update     total_updates := TOTAL_UPDATES (ROA coefficient 0.025), PPO.update()  (ppo.py:182-293)
 The Normal sample of act() is a + std * eps with eps injected (actor_critic.py:207), and
 the minibatch permutation of each update is injected (rollout_storage.py:142).
+
+Cases run at N=64 envs (384-row minibatches) except go2_c2: C2's exact shapes, N=4096, T=24,
+so the update's minibatches are 24,576 rows as in the bench (rollout_storage.py:141) and the
+HIP GEMMs take their production tile shapes, split-K picks and grids. Its per-step rollout
+outputs are stored sampled (`record`) instead of whole (`sampled_rollout`).
+Also recorded: the parameters after minibatch 0's optimizer steps (one Adam step each: the
+tight parameter check) and the Adam moments after the update.
 """
 import zlib
 
 import numpy as np
 
-N, T = 64, 24
+N, T = 64, 24            # default envs per case (CASES[...]["N"] overrides), steps per rollout
 TOTAL_UPDATES = 10000.0  # ppo.py:218-220: stage 0.5 of 5000..15000 -> coefficient 0.025
 SAMPLE = 2048            # entries kept per large tensor (plus its fp64 sum / sum of squares)
 
@@ -39,7 +46,18 @@ CASES = {
                         est_h=[256, 128], latent=20, scan_out=32, lr=2e-4, est_lr=1e-4, schedule="fixed",
                         desired_kl=0.01, entropy=0.01, epochs=5, minibatches=4, gamma=0.99, lam=0.95, clip=0.2,
                         max_grad_norm=1.0),
+    # C2: go2 at 4096 envs (24,576-row minibatches), the go2 train config's fixed schedule
+    "go2_c2": dict(seed=13, N=4096, sampled_rollout=True, P=52, H=10, priv=29, critic=736, est=3, scan=132, A=12,
+                   actor=[512, 256, 128], critic_h=[512, 256, 128], priv_h=[64, 20], scan_h=[128, 64],
+                   est_h=[128, 64], latent=20, scan_out=32, lr=2e-4, est_lr=1e-3, schedule="fixed",
+                   desired_kl=0.01, entropy=0.01, epochs=5, minibatches=4, gamma=0.99, lam=0.95, clip=0.2,
+                   max_grad_norm=1.0),
 }
+SMALL_CASES = [k for k, c in CASES.items() if c.get("N", N) <= 64]  # the CPU suite's cases
+
+
+def n_envs(case):
+    return CASES[case].get("N", N)
 
 
 def _rng(case, *key):
@@ -71,6 +89,7 @@ def weights(case, named_shapes):
 def rollout_inputs(case, which, t):
     """Step t of rollout `which` (0 = A, 1 = B): observations, eps, rewards, dones, time_outs."""
     c = CASES[case]
+    N = n_envs(case)
     g = _rng(case, 2, which, t)
     nobs = c["P"] * (c["H"] + 1)
     d = {
@@ -90,11 +109,11 @@ def rollout_inputs(case, which, t):
 
 def last_critic(case, which):
     c = CASES[case]
-    return _rng(case, 3, which).standard_normal((N, c["critic"]), dtype=np.float32)
+    return _rng(case, 3, which).standard_normal((n_envs(case), c["critic"]), dtype=np.float32)
 
 
 def permutation(case, which):
-    return _rng(case, 4, which).permutation(N * T).astype(np.int64)
+    return _rng(case, 4, which).permutation(n_envs(case) * T).astype(np.int64)
 
 
 def sample_index(name, size):

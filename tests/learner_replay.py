@@ -36,7 +36,7 @@ def build(case, device, use_graphs=None):
               gamma=c["gamma"], lam=c["lam"], value_loss_coef=1.0, entropy_coef=c["entropy"], learning_rate=c["lr"],
               estimator_learning_rate=c["est_lr"], max_grad_norm=c["max_grad_norm"], use_clipped_value_loss=True,
               schedule=c["schedule"], desired_kl=c["desired_kl"], device=device, use_graphs=use_graphs)
-    alg.init_storage(LC.N, LC.T, [c["P"] * (c["H"] + 1)], [c["priv"]], [c["critic"]], [c["est"]], [c["scan"]],
+    alg.init_storage(LC.n_envs(case), LC.T, [c["P"] * (c["H"] + 1)], [c["priv"]], [c["critic"]], [c["est"]], [c["scan"]],
                      [c["A"]])
     return alg
 
@@ -99,7 +99,21 @@ def run(case, device, use_graphs=None):
     alg._precompute()
     alg._minibatch_grads(alg._minibatches()[0])
     res["grad0"] = {n: _np(p.grad) for n, p in named_params(alg)}
+    # the parameters after minibatch 0's optimizer steps: snapshot at the first _minibatch_step
+    # (the first update runs eagerly before any graph is captured; capture calls it again and
+    # then takes no snapshot)
+    mb0 = {}
+    step = alg._minibatch_step
+
+    def first_step():
+        step()
+        if not mb0:
+            mb0.update({n: p.detach().clone() for n, p in named_params(alg)})
+
+    alg._minibatch_step = first_step
     mv, ms, mr, coef, me = alg.update()
+    del alg._minibatch_step
+    res["mb0"] = {n: _np(p) for n, p in mb0.items()}
     res["update.losses"] = np.array([mv, ms, mr, coef, me])
     res["update.learning_rate"] = alg.learning_rate
     res["after"] = {n: _np(p) for n, p in named_params(alg)}

@@ -3,6 +3,7 @@
 Bound per output: |C - C64| <= 3e-5 * sum_k |A(m,k) B(k,n)| + 1e-6 — the split's
 ~2^-16 relative product error plus fp32 accumulation; TF32 (what the reference trains
 with, train.py:39) would need ~5e-4 * sum|ab|."""
+import numpy as np
 import pytest
 import torch
 
@@ -201,6 +202,21 @@ def test_rollout_bookkeeping_kernels_match_torch():
     torch.testing.assert_close(mu, mean, rtol=0, atol=0)
     torch.testing.assert_close(sig, std.expand(B, A), rtol=0, atol=0)
     torch.testing.assert_close(lp.view(-1), dist.log_prob(want_a).sum(-1), rtol=1e-6, atol=1e-5)
+    # eps drawn in the kernel (Philox per global env and env step, oracle/philox.py act_noise)
+    import philox
+    step_dev = torch.tensor([123457], dtype=torch.int64, device="cuda")
+    act2 = torch.empty(B, A, device="cuda")
+    hip_mlp.act_head(mean, std, None, act2, mu, sig, lp, noise=(7, step_dev, 3000))
+    want_eps = philox.act_noise(7, np.arange(3000, 3000 + B), 123457, A)
+    got_eps = ((act2 - mean) / std).double().cpu().numpy()
+    np.testing.assert_allclose(got_eps, want_eps, atol=2e-5 * (1 + np.abs(want_eps)).max())
+    dist2 = torch.distributions.Normal(mean, mean * 0.0 + std)
+    torch.testing.assert_close(lp.view(-1), dist2.log_prob(act2).sum(-1), rtol=1e-6, atol=1e-5)
+    # a shard: rows of global envs 3500.. are the same draws as rows 500.. above
+    act3 = torch.empty(B - 500, A, device="cuda")
+    hip_mlp.act_head(mean[500:].contiguous(), std, None, act3, torch.empty_like(act3), torch.empty_like(act3),
+                     torch.empty(B - 500, 1, device="cuda"), noise=(7, step_dev, 3500))
+    assert torch.equal(act3, act2[500:])
     # transition: r + gamma * V * time_out
     r = torch.randn(B, device="cuda", generator=g)
     v = torch.randn(B, 1, device="cuda", generator=g)

@@ -204,9 +204,11 @@ def full_step_vs_oracle(device):
     np.testing.assert_allclose(tw.gpu("rew")[ok], a["rew"][ok], atol=1e-3, rtol=1e-2)
 
 
-def test_standing_invariants_full_n():
-    """N=4096, default pose, zero actions: robots land and stand; total normal force
-    balances gravity; no NaN; deterministic bitwise across two runs."""
+@pytest.mark.parametrize("n", [4096, 32768])
+def test_standing_invariants_full_n(n):
+    """N=4096 (C2) and 32768 (C5's whole-node env count on one GPU), default pose, zero
+    actions: robots land and stand; total normal force balances gravity; no NaN;
+    deterministic bitwise across two runs."""
     import torch
     from legged_gym_custom_amd.envs import task_registry_configs
     from legged_gym_custom_amd.envs.go2.go2 import Go2Robot
@@ -214,7 +216,7 @@ def test_standing_invariants_full_n():
 
     def run():
         cfg, _ = task_registry_configs("go2")
-        cfg.env.num_envs = 4096
+        cfg.env.num_envs = n
         cfg.domain_rand.push_robots = False
         cfg.noise.add_noise = False
         set_seed(0)

@@ -23,7 +23,7 @@ import learner_case as LC
 import learner_replay as R
 
 
-@pytest.fixture(scope="module", params=list(LC.CASES))
+@pytest.fixture(scope="module", params=LC.SMALL_CASES)  # (go2_c2, 4096 envs: the GPU suite)
 def replay(request):
     case = request.param
     d = R.load(case)
@@ -75,3 +75,11 @@ def test_update_losses_lr_params_moments(replay):
     for n, m in res["exp_avg"].items():
         LC.compare(d, "exp_avg", n, m, rtol=1e-3, atol=1e-7)
         LC.compare(d, "exp_avg_sq", n, res["exp_avg_sq"][n], rtol=1e-3, atol=1e-12)
+
+
+def test_update_minibatch0_adam_step(replay):
+    """Parameters after minibatch 0's single Adam step (+-lr by the gradient's sign)."""
+    case, d, res, _ = replay
+    for n, p in res["mb0"].items():
+        if f"mb0.{n}.v" in d:
+            LC.compare(d, "mb0", n, p, rtol=0, atol=1e-7)

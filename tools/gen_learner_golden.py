@@ -4,7 +4,8 @@
 tests/learner_case.py and records its outputs as tests/golden/learner_<case>.npz.
 Test infrastructure only: the reference code never travels; only the .npz data does.
 
-Recorded per case (go2 and go2_parkour network shapes, N=64 envs, T=24 steps):
+Recorded per case (go2 and go2_parkour network shapes at N=64 envs; go2 at C2's 4096 envs;
+T=24 steps):
   * state_dict key/shape list and the optimizers' param-group layout (meta JSON);
   * rollout A (adaptation mode) and B: per step PPO.act outputs (actions, values,
     log-probs, mean, sigma; ppo.py:129-153 / actor_critic.py:190-226) and the stored
@@ -12,6 +13,7 @@ Recorded per case (go2 and go2_parkour network shapes, N=64 envs, T=24 steps):
   * compute_returns: returns and normalised advantages (rollout_storage.py:110-124);
   * update_dagger: the adaptation encoder after it, its Adam moments, the mean loss;
   * update: the pre-clip gradients of minibatch 0 (hooked at clip_grad_norm_), the
+    parameters after minibatch 0's Adam steps (hooked at the optimizers' step), the
     returned losses, the learning rate, every parameter after the update and the Adam
     moments (sampled entries + fp64 sum/sum-of-squares per tensor; learner_case.record).
 Injected: the Normal sample (loc + scale * eps) and torch.randperm.
@@ -94,31 +96,40 @@ def build(case):
               gamma=c["gamma"], lam=c["lam"], value_loss_coef=1.0, entropy_coef=c["entropy"], learning_rate=c["lr"],
               estimator_learning_rate=c["est_lr"], max_grad_norm=c["max_grad_norm"], use_clipped_value_loss=True,
               schedule=c["schedule"], desired_kl=c["desired_kl"], device="cpu")
-    alg.init_storage(LC.N, LC.T, [c["P"] * (c["H"] + 1)], [c["priv"]], [c["critic"]], [c["est"]], [c["scan"]],
+    alg.init_storage(LC.n_envs(case), LC.T, [c["P"] * (c["H"] + 1)], [c["priv"]], [c["critic"]], [c["est"]], [c["scan"]],
                      [c["A"]])
     return alg
 
 
 def rollout(alg, case, which, out, adaptation_mode):
     pre = f"roll{which}"
+    sampled = LC.CASES[case].get("sampled_rollout", False)
+
+    def put(key, arr):
+        if sampled:  # (large case: sampled entries + fp64 sums, learner_case.record)
+            prefix, name = key.rsplit(".", 1)
+            LC.record(out, prefix, name, arr.numpy())
+        else:
+            out[key] = arr.numpy().copy()
+
     for t in range(LC.T):
         d = LC.rollout_inputs(case, which, t)
         x = {k: torch.from_numpy(v) for k, v in d.items()}
         _Inject.eps = x["eps"]
         alg.act(x["obs"], x["priv"], x["critic"], x["est"], x["scan"], adaptation_mode=adaptation_mode)
         tr = alg.transition
-        out[f"{pre}.{t}.actions"] = tr.actions.numpy().copy()
-        out[f"{pre}.{t}.values"] = tr.values.numpy().copy()
-        out[f"{pre}.{t}.logp"] = tr.actions_log_prob.numpy().copy()
-        out[f"{pre}.{t}.mu"] = tr.action_mean.numpy().copy()
-        out[f"{pre}.{t}.sigma"] = tr.action_sigma.numpy().copy()
+        put(f"{pre}.{t}.actions", tr.actions)
+        put(f"{pre}.{t}.values", tr.values)
+        put(f"{pre}.{t}.logp", tr.actions_log_prob)
+        put(f"{pre}.{t}.mu", tr.action_mean)
+        put(f"{pre}.{t}.sigma", tr.action_sigma)
         alg.process_env_step(x["rewards"], x["dones"], {"time_outs": x["time_outs"]})
         _Inject.eps = None
     s = alg.storage
-    out[f"{pre}.rewards"] = s.rewards.numpy().copy()
+    put(f"{pre}.rewards", s.rewards)
     alg.compute_returns(torch.from_numpy(LC.last_critic(case, which)))
-    out[f"{pre}.returns"] = s.returns.numpy().copy()
-    out[f"{pre}.advantages"] = s.advantages.numpy().copy()
+    put(f"{pre}.returns", s.returns)
+    put(f"{pre}.advantages", s.advantages)
 
 
 def named_params(alg):
@@ -140,7 +151,7 @@ def adam_state(opt, names_of):
 def main(cases):
     for case in cases:
         alg = build(case)
-        out = {"case": np.array(case), "torch_version": np.array(torch.__version__), "N": LC.N, "T": LC.T}
+        out = {"case": np.array(case), "torch_version": np.array(torch.__version__), "N": LC.n_envs(case), "T": LC.T}
         names_of = {id(p): n for n, p in named_params(alg)}
         meta = {"state_dict": [[k, list(v.shape)] for k, v in alg.actor_critic.state_dict().items()],
                 "estimator_state_dict": [[k, list(v.shape)] for k, v in alg.estimator.state_dict().items()],
@@ -185,10 +196,31 @@ def main(cases):
             return total
 
         nn.utils.clip_grad_norm_ = clip_hook
+        # the parameters after minibatch 0's optimizer steps (one Adam step each; ppo.py:228-231
+        # for the estimator, :273-276 for the rest)
+        mb0 = {}
+
+        def once(opt, key):
+            step = opt.step
+
+            def wrapped(*a, **k):
+                r = step(*a, **k)
+                if key not in mb0:
+                    mb0[key] = {names_of[id(p)]: p.detach().numpy().copy() for g in opt.param_groups
+                                for p in g["params"]}
+                return r
+            opt.step = wrapped
+
+        once(alg.optimizer, "main")
+        once(alg.estimator_optimizer, "est")
         _Inject.perm = torch.from_numpy(LC.permutation(case, 1))
         mv, ms, mr, coef, me = alg.update()
         _Inject.perm = None
         nn.utils.clip_grad_norm_ = orig_clip
+        del alg.optimizer.step, alg.estimator_optimizer.step
+        for key in ("main", "est"):
+            for n, p in mb0[key].items():
+                LC.record(out, "mb0", n, p)
         out["update.losses"] = np.array([mv, ms, mr, coef, me], dtype=np.float64)
         out["update.learning_rate"] = np.float64(alg.learning_rate)
         out["update.grad_norm0"] = np.array([grads0["est_norm"], grads0["main_norm"]], dtype=np.float64)
