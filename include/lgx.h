@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define LGX_ABI_VERSION 4
+#define LGX_ABI_VERSION 5
 
 #define LGX_MAX_DOF 12
 #define LGX_MAX_LINKS 16          /* dynamic links: base + 12 leg links (+spare) */
@@ -271,6 +271,11 @@ typedef struct lgx_buffers {
   float* sea_cell;
   /* device-side reductions for extras['episode'] (go2.py:246-249): [K+1] sums + count */
   float* episode_stats;
+  /* NaN/Inf guard (ABI v5): an env whose physics state went non-finite in a
+     step is given a finite stand-in state and reset; blew_up[e] = 1 for that step (0
+     otherwise), blowup_count accumulates such events. Both optional. */
+  uint8_t* blew_up;            /* [N] */
+  uint32_t* blowup_count;      /* [1] */
 } lgx_buffers;
 
 typedef struct lgx_env lgx_env;

@@ -5,7 +5,7 @@ sizeof against the values the native library (and the oracle) report.
 """
 import ctypes as C
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 MAX_DOF = 12
 MAX_LINKS = 16
 MAX_BODIES = 24
@@ -126,6 +126,7 @@ class Buffers(C.Structure):
         "base_lin_vel", "base_ang_vel", "projected_gravity", "rpy_phase", "measured_heights",
         "friction", "mass_params", "kp_kd", "env_origins", "terrain_levels", "terrain_types",
         "terrain_origins", "height_samples", "terrain_mesh", "sea_hidden", "sea_cell", "episode_stats",
+        "blew_up", "blowup_count",
     ]]
 
 

@@ -103,6 +103,7 @@ struct Sh {
   float fric;                         // raw friction coefficient (privileged obs)
   long long ep;
   int reset, tout;
+  int blew;  // this step's physics went non-finite (NaN/Inf guard; the env is reset)
   // --- physics state (base velocity kept as the ORIGIN velocity inside the step)
   float qb[4], pb[3], vo[3], wb[3];
   float th[NJ], thd[NJ], tau[NJ], act[NJ], kpm[NJ], kdm[NJ], ldv[NJ];
@@ -1492,6 +1493,7 @@ __global__ __launch_bounds__(64, ACTNET ? LGX_SEA_WAVES : 4) void env_step_kerne
   if (lane < 3) s.cadd[lane] = B.mass_params ? B.mass_params[e * 4 + 1 + lane] : 0.f;
   if (lane < 4) s.cmd[lane] = B.commands[e * 4 + lane];
   if (lane == 0) {
+    s.blew = 0;
     s.ep_prev = B.episode_length[e];
     s.jump_prev = B.rpy_phase ? B.rpy_phase[e * 8 + 7] : 0.f;
     s.fric = B.friction ? B.friction[e] : 1.f;
@@ -1529,6 +1531,33 @@ __global__ __launch_bounds__(64, ACTNET ? LGX_SEA_WAVES : 4) void env_step_kerne
     __syncthreads();
     PH(0);
     for (int sub = 0; sub < Pm->decimation; ++sub) substep<TERRAIN, ACTNET>(s, M, Pm, B, lane, sub == Pm->decimation - 1);
+    __syncthreads();
+    // NaN/Inf guard (SURVEY.md §5 "Failure detection"; the reference has none): a state that
+    // went non-finite in any substep stays non-finite, so one check after the substeps sees it.
+    // Such an env gets a finite stand-in state (default joint pose at its start position, at
+    // rest, no torques / contact forces / actions), is flagged in blew_up, counted, and reset
+    // below by the normal masked path, so no NaN reaches its observations, rewards or the
+    // learner. Other envs are untouched.
+    {
+      bool bad = false;
+      if (lane < D) bad = !(isfinite(s.th[lane]) && isfinite(s.thd[lane]) && isfinite(s.tau[lane]));
+      if (lane < A) bad = bad || !isfinite(s.act[lane]);
+      if (lane < 3) bad = bad || !(isfinite(s.pb[lane]) && isfinite(s.vo[lane]) && isfinite(s.wb[lane]));
+      if (lane < 4) bad = bad || !isfinite(s.qb[lane]);
+      if (lane < NB) bad = bad || !(isfinite(s.cf[lane][0]) && isfinite(s.cf[lane][1]) && isfinite(s.cf[lane][2]));
+      if (__ballot(bad) != 0ull) {
+        if (lane < D) { s.th[lane] = Pm->default_dof_pos[lane]; s.thd[lane] = 0.f; s.tau[lane] = 0.f; }
+        if (lane < A) { s.act[lane] = 0.f; B.actions[(size_t)e * A + lane] = 0.f; }
+        if (lane < 3) { s.pb[lane] = isfinite(s.root[lane]) ? s.root[lane] : 0.f; s.vo[lane] = 0.f; s.wb[lane] = 0.f; }
+        if (lane < 4) s.qb[lane] = lane == 3 ? 1.f : 0.f;
+        if (lane < NB) { s.cf[lane][0] = 0.f; s.cf[lane][1] = 0.f; s.cf[lane][2] = 0.f; }
+        if (lane == 0) {
+          s.blew = 1;
+          if (B.blowup_count) atomicAdd(B.blowup_count, 1u);
+        }
+      }
+      __syncthreads();
+    }
     // final kinematics for the rigid-body state tensor
     kinematics<false>(s, M, Pm, lane);
     float root[13];
@@ -1675,6 +1704,7 @@ __global__ __launch_bounds__(64, ACTNET ? LGX_SEA_WAVES : 4) void env_step_kerne
     reset |= tout;
     reset |= x.pg[2] > 0.0f;
     if (Pm->parkour) reset |= root[2] < -1.0f;
+    reset |= s.blew;  // NaN/Inf guard
     s.reset = reset;
     s.tout = tout;
     x.jump = s.jump_prev;  // set by the previous step's observations
@@ -1703,6 +1733,7 @@ __global__ __launch_bounds__(64, ACTNET ? LGX_SEA_WAVES : 4) void env_step_kerne
     B.rew[e] = rew;
     B.reset[e] = (uint8_t)reset;
     B.time_out[e] = (uint8_t)s.tout;
+    if (B.blew_up) B.blew_up[e] = (uint8_t)s.blew;
   }
   __syncthreads();
   if (lane < KS) {

@@ -12,6 +12,7 @@
 // Post-physics follows legged_robot.py / go2.py statement order with no fp contraction
 // (built with -ffp-contract=off), like the kernel's golden-pinned tail.
 #include <math.h>
+#include <cmath>
 #include <omp.h>
 #include <stdint.h>
 #include <string.h>
@@ -1009,6 +1010,7 @@ static void env_step(Env& s, const lgx_model* M, const lgx_task_params* P, const
   memcpy(s.cmd, B->commands + e * 4, sizeof(s.cmd));
   const long long ep_prev = B->episode_length[e];
   const float jump_prev = B->rpy_phase ? B->rpy_phase[e * 8 + 7] : 0.f;
+  int blew = 0;  // NaN/Inf guard
 
   if (physics) {
     const float* r0 = s.root;
@@ -1020,6 +1022,23 @@ static void env_step(Env& s, const lgx_model* M, const lgx_task_params* P, const
     const v3 rc = rot(R, V(M->link_com[0][0] + s.cadd[0], M->link_com[0][1] + s.cadd[1], M->link_com[0][2] + s.cadd[2]));
     S3(s.vo, L3(r0 + 7) - cross(L3(s.wb), rc));  // COM velocity -> origin velocity
     for (int sub = 0; sub < P->decimation; ++sub) substep(s, M, P, B, e, sub == P->decimation - 1);
+    // NaN/Inf guard (the kernel's rule, lgx_env.hip): a non-finite state after the substeps
+    // becomes a finite stand-in and the env is reset below
+    bool bad = false;
+    for (int j = 0; j < D; ++j) bad = bad || !(std::isfinite(s.th[j]) && std::isfinite(s.thd[j]) && std::isfinite(s.tau[j]));
+    for (int j = 0; j < A; ++j) bad = bad || !std::isfinite(s.act[j]);
+    for (int i = 0; i < 3; ++i) bad = bad || !(std::isfinite(s.pb[i]) && std::isfinite(s.vo[i]) && std::isfinite(s.wb[i]));
+    for (int i = 0; i < 4; ++i) bad = bad || !std::isfinite(s.qb[i]);
+    for (int b = 0; b < NB; ++b)
+      for (int i = 0; i < 3; ++i) bad = bad || !std::isfinite(s.cf[b][i]);
+    if (bad) {
+      for (int j = 0; j < D; ++j) { s.th[j] = P->default_dof_pos[j]; s.thd[j] = 0.f; s.tau[j] = 0.f; }
+      for (int j = 0; j < A; ++j) { s.act[j] = 0.f; B->actions[(size_t)e * A + j] = 0.f; }
+      for (int i = 0; i < 3; ++i) { s.pb[i] = std::isfinite(s.root[i]) ? s.root[i] : 0.f; s.vo[i] = 0.f; s.wb[i] = 0.f; }
+      for (int i = 0; i < 4; ++i) s.qb[i] = i == 3 ? 1.f : 0.f;
+      for (int b = 0; b < NB; ++b) s.cf[b][0] = s.cf[b][1] = s.cf[b][2] = 0.f;
+      blew = 1;
+    }
     kinematics<false>(s, M, P);
     quat_R(s.qb, R);
     const v3 rc2 = rot(R, V(M->link_com[0][0] + s.cadd[0], M->link_com[0][1] + s.cadd[1], M->link_com[0][2] + s.cadd[2]));
@@ -1106,6 +1125,7 @@ static void env_step(Env& s, const lgx_model* M, const lgx_task_params* P, const
   reset |= tout;
   reset |= s.pg[2] > 0.0f;
   if (P->parkour) reset |= root[2] < -1.0f;
+  reset |= blew;
   s.jump = jump_prev;
   get_heights(P, B, s);
   joint_sums(P, B, s, e);
@@ -1125,6 +1145,11 @@ static void env_step(Env& s, const lgx_model* M, const lgx_task_params* P, const
   B->rew[e] = rew;
   B->reset[e] = (uint8_t)reset;
   B->time_out[e] = (uint8_t)tout;
+  if (B->blew_up) B->blew_up[e] = (uint8_t)blew;
+  if (blew && B->blowup_count) {
+#pragma omp atomic
+    *B->blowup_count += 1u;
+  }
   for (int k = 0; k < KS; ++k) B->episode_sums[(size_t)e * KS + k] += s.rterm[k];
   if (reset) reset_env(P, B, s, e, false, stats);  // reset_idx go2.py:207-263
 

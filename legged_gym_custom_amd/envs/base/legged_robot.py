@@ -351,6 +351,10 @@ class LeggedRobot(BaseTask):
         self._episode_means = z(ks)
         self._terrain_level_mean = z(())
         self._extras_time_outs = z(n, dtype=torch.bool)
+        # NaN/Inf guard outputs (lgx_buffers.blew_up / blowup_count): per step, the envs whose
+        # physics state went non-finite (given a finite stand-in state and reset); the count
+        self.blew_up_buf = z(n, dtype=torch.bool)
+        self._blowup_count = torch.zeros(1, dtype=torch.int32, device=dev)
         self._native = _native.NativeEnv(model_struct, self.task_params, self.sim_device_id)
         self._bind()
 
@@ -374,8 +378,14 @@ class LeggedRobot(BaseTask):
             "env_origins": self.env_origins, "episode_stats": self.episode_stats,
             "terrain_levels": getattr(self, "terrain_levels", None), "terrain_types": getattr(self, "terrain_types", None),
             "terrain_origins": getattr(self, "terrain_origins", None), "height_samples": self.height_samples,
-            "terrain_mesh": self._terrain_mesh, **self._sea_buffers,
+            "terrain_mesh": self._terrain_mesh, "blew_up": self.blew_up_buf, "blowup_count": self._blowup_count,
+            **self._sea_buffers,
         })
+
+    @property
+    def physics_blowups(self):
+        """Number of env steps whose physics went non-finite since creation (host sync)."""
+        return int(self._blowup_count.item())
 
     def _setup_actuator(self, P):
         """PD control (legged_robot.py:440-478) lives in the kernel; subclasses with an

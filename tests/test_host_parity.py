@@ -79,3 +79,7 @@ def test_train_c1_on_cpu():
 @pytest.mark.parametrize("z", [(0.06, 0.16), (0.2, 0.27)])
 def test_host_crowded_contacts_match_oracle(z):
     T.crowded_contacts_vs_oracle("cpu", z)
+
+
+def test_host_nan_guard_resets_only_the_blown_up_env():
+    T.nan_guard("cpu")
