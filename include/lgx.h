@@ -213,6 +213,20 @@ typedef struct lgx_task_params {
   float sea_w_ih0[32 * 2], sea_w_hh0[32 * 8], sea_b_ih0[32], sea_b_hh0[32];
   float sea_w_ih1[32 * 8], sea_w_hh1[32 * 8], sea_b_ih1[32], sea_b_hh1[32];
   float sea_lin_w[8];
+  /* command curriculum (ABI v5), run by lgx_command_curriculum on steps whose
+     common_step_counter is a multiple of max_episode_length (reset_idx, go2.py:221-223 /
+     legged_robot.py:176-177): if mean(tracking_lin_vel episode sum of the envs reset in that
+     step) / max_episode_length > curriculum_threshold, lin_vel_x := (clip(lo - delta,
+     lo_min, lo_max), clip(hi + delta, 0, hi_max)) in double, numpy's clip (min(max(x, a), b)).
+     1: Go2Robot.update_command_curriculum (go2.py:80-107: delta = vel_increment, lo_min =
+        max_reverse_vel, lo_max = 0, or lo - delta when max_reverse_vel >= 0; hi_max =
+        max_forward_vel); 2: LeggedRobot's (legged_robot.py:580-591: delta 0.05, lo in
+        [-max_curriculum, 0], hi_max = max_curriculum). 0: off. */
+  int32_t command_curriculum;
+  int32_t curriculum_term;          /* index of tracking_lin_vel among the reward terms */
+  float curriculum_threshold;       /* fp32(0.8 * reward_scales['tracking_lin_vel']) (dt-scaled) */
+  int32_t curriculum_lo_free;       /* 1: lo_max = lo - delta (go2, max_reverse_vel >= 0) */
+  double curriculum_delta, curriculum_lo_min, curriculum_lo_max, curriculum_hi_max;
 } lgx_task_params;
 
 /* Every per-env buffer the step reads/writes. NULL = not present. */
@@ -276,6 +290,13 @@ typedef struct lgx_buffers {
      otherwise), blowup_count accumulates such events. Both optional. */
   uint8_t* blew_up;            /* [N] */
   uint32_t* blowup_count;      /* [1] */
+  /* command ranges as mutable state (ABI v5; the command curriculum's): [8] double, (lo, hi)
+     of lin_vel_x, lin_vel_y, ang_vel_yaw, heading — the reference's Python floats. When set,
+     every command resample reads them (else the params' cmd_* ranges). */
+  double* command_ranges;
+  float* curriculum_vals;      /* [N] an env's tracking_lin_vel episode sum at its in-step reset */
+  float* command_range_log;    /* [4] extras['episode'] values: go2 max_command_x, min_command_x,
+                                  max_command_y, max_command_yaw; base: max x, max y, max yaw */
 } lgx_buffers;
 
 typedef struct lgx_env lgx_env;
@@ -319,6 +340,17 @@ int lgx_reset_envs(lgx_env* env, const uint8_t* env_mask, uint64_t seed, uint64_
  * after the step, so the rollout's device step counter needs no separate launch. */
 int lgx_episode_extras(lgx_env* env, float* means, float* level_mean, uint8_t* time_outs, uint64_t* step_dev,
                        void* hip_stream);
+/* update_command_curriculum (go2.py:80-107 / legged_robot.py:580-591) for the step just run,
+ * between lgx_step(_dev) and lgx_episode_extras: on a curriculum step (step % max_episode_length
+ * == 0, step from d_step_counter if given, else step_counter) it forms the mean of
+ * curriculum_vals over the envs with reset[e] (or takes global_sum_count = {sum, count}, device
+ * doubles, e.g. all-reduced over env shards), updates command_ranges / command_range_log, and
+ * if the range changed re-resamples the commands of this step's reset envs with the new range
+ * (same Philox draws) and rewrites the command entries of their observation, critic and history
+ * rows — so the step's resets see the updated range, as in the reference. One launch; nothing
+ * happens on other steps. Needs params.command_curriculum and the three buffers bound. */
+int lgx_command_curriculum(lgx_env* env, uint64_t seed, uint64_t step_counter, const uint64_t* d_step_counter,
+                           const double* global_sum_count, void* hip_stream);
 const char* lgx_last_error(const lgx_env* env);
 void lgx_destroy(lgx_env* env);
 

@@ -109,6 +109,9 @@ class TaskParams(C.Structure):
         ("sea_w_ih0", f32 * 64), ("sea_w_hh0", f32 * 256), ("sea_b_ih0", f32 * 32), ("sea_b_hh0", f32 * 32),
         ("sea_w_ih1", f32 * 256), ("sea_w_hh1", f32 * 256), ("sea_b_ih1", f32 * 32), ("sea_b_hh1", f32 * 32),
         ("sea_lin_w", f32 * 8),
+        ("command_curriculum", i32), ("curriculum_term", i32), ("curriculum_threshold", f32),
+        ("curriculum_lo_free", i32), ("curriculum_delta", C.c_double), ("curriculum_lo_min", C.c_double),
+        ("curriculum_lo_max", C.c_double), ("curriculum_hi_max", C.c_double),
     ]
 
 
@@ -126,7 +129,7 @@ class Buffers(C.Structure):
         "base_lin_vel", "base_ang_vel", "projected_gravity", "rpy_phase", "measured_heights",
         "friction", "mass_params", "kp_kd", "env_origins", "terrain_levels", "terrain_types",
         "terrain_origins", "height_samples", "terrain_mesh", "sea_hidden", "sea_cell", "episode_stats",
-        "blew_up", "blowup_count",
+        "blew_up", "blowup_count", "command_ranges", "curriculum_vals", "command_range_log",
     ]]
 
 

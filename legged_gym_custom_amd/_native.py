@@ -33,6 +33,7 @@ def lib():
     L.lgx_physics.argtypes = [vp, vp]
     L.lgx_reset_envs.argtypes = [vp, vp, u64, u64, vp]
     L.lgx_episode_extras.argtypes = [vp, vp, vp, vp, vp, vp]
+    L.lgx_command_curriculum.argtypes = [vp, u64, u64, vp, vp, vp]
     L.lgx_last_error.argtypes = [vp]
     L.lgx_last_error.restype = C.c_char_p
     L.lgx_destroy.argtypes = [vp]
@@ -46,7 +47,7 @@ def lib():
 
 EXPORTED = ["lgx_abi_version", "lgx_sizeof_model", "lgx_sizeof_task_params", "lgx_sizeof_buffers", "lgx_create",
             "lgx_bind", "lgx_step", "lgx_step_dev", "lgx_post_physics", "lgx_physics", "lgx_reset_envs", "lgx_last_error",
-            "lgx_destroy", "lgx_episode_extras"]
+            "lgx_destroy", "lgx_episode_extras", "lgx_command_curriculum"]
 
 
 class NativeEnv:
@@ -101,6 +102,14 @@ class NativeEnv:
         self._keep["_mask"] = mask
         self._check(self._L.lgx_reset_envs(self.handle, C.c_void_p(mask.data_ptr()), seed, call, C.c_void_p(stream)),
                     "lgx_reset_envs")
+
+    def command_curriculum(self, seed, step, global_sum_count, stream):
+        """lgx_command_curriculum; `step`: a device int64 scalar (the step counter lgx_step_dev
+        read) or an int; global_sum_count: None or a device float64 [2] {sum, count}."""
+        p = lambda t: None if t is None else C.c_void_p(t.data_ptr())  # noqa: E731
+        dev = hasattr(step, "data_ptr")
+        self._check(self._L.lgx_command_curriculum(self.handle, seed, 0 if dev else int(step), p(step) if dev else None,
+                                                   p(global_sum_count), C.c_void_p(stream)), "lgx_command_curriculum")
 
     def episode_extras(self, means, level_mean, time_outs, stream, step_dev=None):
         """lgx_episode_extras into the given device tensors (level_mean / time_outs: None = skip);

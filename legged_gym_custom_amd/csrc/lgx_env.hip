@@ -1100,19 +1100,33 @@ LGX_DEV float rand_range(float lo, float hi, float u) {
   float span = (float)((double)hi - (double)lo);
   return span * u + lo;
 }
+// torch_rand_float(lo, hi) with the reference's Python-float (double) bounds: (hi - lo) and lo
+// enter the fp32 tensor ops as fp32 scalars
+LGX_DEV float rand_range_d(double lo, double hi, float u) { return (float)(hi - lo) * u + (float)lo; }
 
 // Go2Robot._resample_commands go2.py:413-464 / LeggedRobot legged_robot.py:406-437
-LGX_DEV void resample_commands(const lgx_task_params* Pm, float* cmd, const float* U, int slot0, const float* quat) {
+// R: the mutable command ranges (lgx_buffers.command_ranges, double [8]) or NULL (params' ranges)
+LGX_DEV void resample_commands(const lgx_task_params* Pm, const double* R, float* cmd, const float* U, int slot0,
+                               const float* quat) {
   if (Pm->has_user_command) {
     for (int i = 0; i < 4; ++i) cmd[i] = Pm->user_command[i];
     return;
   }
-  cmd[0] = rand_range(Pm->cmd_lin_vel_x[0], Pm->cmd_lin_vel_x[1], U[slot0 + 0]);
-  cmd[1] = rand_range(Pm->cmd_lin_vel_y[0], Pm->cmd_lin_vel_y[1], U[slot0 + 1]);
-  if (Pm->heading_command)
-    cmd[3] = rand_range(Pm->cmd_heading[0], Pm->cmd_heading[1], U[slot0 + 2]);
-  else
-    cmd[2] = rand_range(Pm->cmd_ang_vel_yaw[0], Pm->cmd_ang_vel_yaw[1], U[slot0 + 2]);
+  if (R) {
+    cmd[0] = rand_range_d(R[0], R[1], U[slot0 + 0]);
+    cmd[1] = rand_range_d(R[2], R[3], U[slot0 + 1]);
+    if (Pm->heading_command)
+      cmd[3] = rand_range_d(R[6], R[7], U[slot0 + 2]);
+    else
+      cmd[2] = rand_range_d(R[4], R[5], U[slot0 + 2]);
+  } else {
+    cmd[0] = rand_range(Pm->cmd_lin_vel_x[0], Pm->cmd_lin_vel_x[1], U[slot0 + 0]);
+    cmd[1] = rand_range(Pm->cmd_lin_vel_y[0], Pm->cmd_lin_vel_y[1], U[slot0 + 1]);
+    if (Pm->heading_command)
+      cmd[3] = rand_range(Pm->cmd_heading[0], Pm->cmd_heading[1], U[slot0 + 2]);
+    else
+      cmd[2] = rand_range(Pm->cmd_ang_vel_yaw[0], Pm->cmd_ang_vel_yaw[1], U[slot0 + 2]);
+  }
   float keep = (float)(nrm2(cmd[0], cmd[1]) > 0.2f);
   cmd[0] = cmd[0] * keep;
   cmd[1] = cmd[1] * keep;
@@ -1167,7 +1181,7 @@ LGX_DEV void reset_env(const lgx_task_params* Pm, const lgx_buffers& B, Sh& s, i
       root[1] = root[1] + rand_range(-1.0f, 1.0f, U[S_ROOT_XY + 1]);
     }
     for (int i = 0; i < 6; ++i) root[7 + i] = rand_range(-0.5f, 0.5f, U[S_ROOT_VEL + i]);
-    resample_commands(Pm, cmd, U, S_RCMD, root + 3);
+    resample_commands(Pm, B.command_ranges, cmd, U, S_RCMD, root + 3);
     s.ep = 0;
   }
   // _reset_dofs legged_robot.py:481-506: q = q0 + U(0, 0.9), qd = 0
@@ -1203,6 +1217,8 @@ LGX_DEV void reset_env(const lgx_task_params* Pm, const lgx_buffers& B, Sh& s, i
     float* es = B.episode_sums + (size_t)e * K + lane;
     const float sum = sums_in_lds ? s.es[lane] : *es;  // in a step: this step's updated row, staged in LDS
     if (B.episode_stats) atomicAdd(B.episode_stats + lane, sum);
+    // the command curriculum's input (go2.py:87): this env's tracking_lin_vel sum at its reset
+    if (sums_in_lds && B.curriculum_vals && lane == Pm->curriculum_term) B.curriculum_vals[e] = sum;
     *es = 0.f;
   }
   if (lane == 0 && B.episode_stats) atomicAdd(B.episode_stats + K, 1.0f);
@@ -1681,7 +1697,7 @@ __global__ __launch_bounds__(64, ACTNET ? LGX_SEA_WAVES : 4) void env_step_kerne
       x.yaw = atan2f(2.0f * (qw * qz + qx * qy), 1.0f - 2.0f * (qy * qy + qz * qz));
     }
     // _post_physics_step_callback go2.py:390-410
-    if (ep % Pm->resample_interval == 0) resample_commands(Pm, cmd, stg_U(), S_CMD, root + 3);
+    if (ep % Pm->resample_interval == 0) resample_commands(Pm, B.command_ranges, cmd, stg_U(), S_CMD, root + 3);
     if (Pm->heading_command) {
       const float fwd[3] = {1.f, 0.f, 0.f};
       float f[3];
@@ -2179,6 +2195,115 @@ int lgx_episode_extras(lgx_env* env, float* means, float* level_mean, uint8_t* t
                      b.time_out, level_mean ? b.terrain_levels : nullptr, means, level_mean, time_outs);
   HIP_OK(hipGetLastError());
   env->stats_clean = true;
+  return 0;
+}
+
+namespace lgx {
+// One uniform of the env step's Philox table (fill_uniforms: slot = 4 * block + word).
+LGX_DEV float step_uniform(uint64_t seed, uint32_t gid, uint64_t step, int slot) {
+  uint32_t o[4];
+  philox4x32_10(gid, (uint32_t)step, (uint32_t)(slot >> 2), (uint32_t)(step >> 32), (uint32_t)seed,
+                (uint32_t)(seed >> 32), o);
+  return u01(o[slot & 3]);
+}
+
+// update_command_curriculum (go2.py:80-107 / legged_robot.py:580-591) after a step: one block.
+// The mean runs over the envs reset in this step (reset_idx's env_ids); their pre-reset
+// tracking_lin_vel sums were left in curriculum_vals by the step kernel. When the range
+// changes, the reset envs' commands are resampled again from the same uniforms with the new
+// range (reset_idx resamples after the curriculum, go2.py:222-230) and the command entries of
+// their observation rows are rewritten (a reset env's history is zero in obs and all copies of
+// the current observation in obs_history, go2.py:570-574).
+__global__ __launch_bounds__(1024) void curriculum_kernel(const lgx_task_params* __restrict__ Pm,
+                                                          const lgx_buffers* __restrict__ Bp, uint64_t seed,
+                                                          uint64_t step_arg, const uint64_t* __restrict__ step_dev,
+                                                          const double* __restrict__ global_sc) {
+  const lgx_buffers& B = *Bp;
+  const uint64_t step = step_dev ? *step_dev : step_arg;
+  if (step % (uint64_t)Pm->max_episode_length != 0) return;
+  __shared__ double red_s[16], red_c[16];
+  __shared__ int changed;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, N = Pm->num_envs;
+  double sm = 0.0, ct = 0.0;
+  if (!global_sc)
+    for (int i = tid; i < N; i += blockDim.x)
+      if (B.reset[i]) { sm += (double)B.curriculum_vals[i]; ct += 1.0; }
+  for (int o = 32; o > 0; o >>= 1) { sm += __shfl_down(sm, o, 64); ct += __shfl_down(ct, o, 64); }
+  if (lane == 0) { red_s[wv] = sm; red_c[wv] = ct; }
+  __syncthreads();
+  if (tid == 0) {
+    double S = 0.0, Cn = 0.0;
+    if (global_sc) { S = global_sc[0]; Cn = global_sc[1]; }
+    else
+      for (int w = 0; w < (int)(blockDim.x >> 6); ++w) { S += red_s[w]; Cn += red_c[w]; }
+    int ch = 0;
+    // torch.mean (fp32) / max_episode_length, compared in fp32 (no reset: reset_idx returns early)
+    const float mean = Cn > 0.0 ? ((float)S / (float)Cn) / (float)Pm->max_episode_length : 0.f;
+    if (Cn > 0.0 && mean > Pm->curriculum_threshold) {
+      double* R = B.command_ranges;
+      const double lo = R[0], hi = R[1], d = Pm->curriculum_delta;
+      const double lo_max = Pm->curriculum_lo_free ? lo - d : Pm->curriculum_lo_max;
+      const double nlo = fmin(fmax(lo - d, Pm->curriculum_lo_min), lo_max);  // np.clip
+      const double nhi = fmin(fmax(hi + d, 0.0), Pm->curriculum_hi_max);
+      ch = (nlo != lo) || (nhi != hi);
+      R[0] = nlo;
+      R[1] = nhi;
+      float* L = B.command_range_log;
+      if (L) {
+        if (Pm->command_curriculum == 1) { L[0] = (float)nhi; L[1] = (float)nlo; L[2] = (float)R[3]; L[3] = (float)R[5]; }
+        else { L[0] = (float)nhi; L[1] = (float)R[3]; L[2] = (float)R[5]; }
+      }
+    }
+    changed = ch;
+  }
+  __syncthreads();
+  if (!changed) return;
+  const bool go2 = Pm->task_kind == LGX_TASK_GO2;
+  const int Pp = Pm->num_proprio, H = Pm->history_len, c0 = go2 ? 5 : 9;
+  const float co = Pm->clip_obs;
+  for (int e = tid; e < N; e += blockDim.x) {
+    if (!B.reset[e]) continue;
+    const uint32_t gid = (uint32_t)(Pm->env_id_offset + e);
+    float U[4];  // the reset's command draws (slots S_RCMD..+3)
+    for (int k = 0; k < 4; ++k) U[k] = step_uniform(seed, gid, step, S_RCMD + k);
+    float cmd[4];
+    for (int k = 0; k < 4; ++k) cmd[k] = B.commands[e * 4 + k];
+    const float* quat = B.root_states + (size_t)e * 13 + 3;
+    resample_commands(Pm, B.command_ranges, cmd, U, 0, quat);
+    for (int k = 0; k < 4; ++k) B.commands[e * 4 + k] = cmd[k];
+    float* obs = B.obs + (size_t)e * Pm->num_obs;
+    float* cr = (go2 && B.critic) ? B.critic + (size_t)e * Pm->num_critic : nullptr;
+    float* hist = B.obs_history + (size_t)e * H * Pp;
+    for (int j = 0; j < 3; ++j) {
+      const int i = c0 + j;
+      float v = cmd[j] * Pm->commands_scale[j];
+      if (Pm->add_noise) v = v + (2.0f * step_uniform(seed, gid, step, S_NOISE + i) - 1.0f) * Pm->noise_vec[i];
+      const float vc = clipf(v, -co, co);
+      obs[H * Pp + i] = vc;
+      if (cr) cr[H * Pp + i] = vc;
+      for (int t = 0; t < H; ++t) hist[t * Pp + i] = v;  // reset env: every history row = current obs
+    }
+  }
+}
+}  // namespace lgx
+
+int lgx_command_curriculum(lgx_env* env, uint64_t seed, uint64_t step_counter, const uint64_t* d_step_counter,
+                           const double* global_sum_count, void* hip_stream) {
+  if (!env) return -2;
+  if (!env->bound) return fail(env, "lgx_command_curriculum before lgx_bind");
+  const lgx_buffers& b = env->buffers;
+  if (!env->params.command_curriculum) return fail(env, "lgx_command_curriculum: params.command_curriculum is 0");
+  if (!b.command_ranges || !b.curriculum_vals || !b.reset || !b.commands || !b.obs || !b.obs_history)
+    return fail(env, "lgx_command_curriculum: command_ranges, curriculum_vals, reset, commands, obs, obs_history "
+                     "must be bound");
+  if (env->host) {
+    lgxh::command_curriculum(&env->params, &b, seed, d_step_counter ? *d_step_counter : step_counter,
+                             global_sum_count);
+    return 0;
+  }
+  hipLaunchKernelGGL(lgx::curriculum_kernel, dim3(1), dim3(1024), 0, (hipStream_t)hip_stream, env->d_params,
+                     env->d_buffers, seed, step_counter, d_step_counter, global_sum_count);
+  HIP_OK(hipGetLastError());
   return 0;
 }
 

@@ -675,6 +675,8 @@ static inline float sqr(float x) { return x * x; }
 static inline float len3(float a, float b, float c) { return sqrtf(a * a + b * b + c * c); }
 static inline float len2(float a, float b) { return sqrtf(a * a + b * b); }
 static inline float urange(float lo, float hi, float u) { return (float)((double)hi - (double)lo) * u + lo; }
+// with the reference's Python-float (double) bounds (lgx_buffers.command_ranges)
+static inline float urange_d(double lo, double hi, float u) { return (float)(hi - lo) * u + (float)lo; }
 
 static int rng_blocks(const lgx_task_params* P) { return 9 + (P->num_proprio + 3) / 4; }
 static void fill_uniforms(Env& s, const lgx_task_params* P, uint64_t seed, uint32_t gid, uint64_t step,
@@ -688,17 +690,28 @@ static void fill_uniforms(Env& s, const lgx_task_params* P, uint64_t seed, uint3
 }
 
 // Go2Robot._resample_commands go2.py:413-464 / LeggedRobot legged_robot.py:406-437
-static void resample_commands(const lgx_task_params* P, float* cmd, const float* U, int slot0, const float* quat) {
+// R: lgx_buffers.command_ranges (mutable, double [8]) or NULL (the params' ranges)
+static void resample_commands(const lgx_task_params* P, const double* R, float* cmd, const float* U, int slot0,
+                              const float* quat) {
   if (P->has_user_command) {
     for (int i = 0; i < 4; ++i) cmd[i] = P->user_command[i];
     return;
   }
-  cmd[0] = urange(P->cmd_lin_vel_x[0], P->cmd_lin_vel_x[1], U[slot0 + 0]);
-  cmd[1] = urange(P->cmd_lin_vel_y[0], P->cmd_lin_vel_y[1], U[slot0 + 1]);
-  if (P->heading_command)
-    cmd[3] = urange(P->cmd_heading[0], P->cmd_heading[1], U[slot0 + 2]);
-  else
-    cmd[2] = urange(P->cmd_ang_vel_yaw[0], P->cmd_ang_vel_yaw[1], U[slot0 + 2]);
+  if (R) {
+    cmd[0] = urange_d(R[0], R[1], U[slot0 + 0]);
+    cmd[1] = urange_d(R[2], R[3], U[slot0 + 1]);
+    if (P->heading_command)
+      cmd[3] = urange_d(R[6], R[7], U[slot0 + 2]);
+    else
+      cmd[2] = urange_d(R[4], R[5], U[slot0 + 2]);
+  } else {
+    cmd[0] = urange(P->cmd_lin_vel_x[0], P->cmd_lin_vel_x[1], U[slot0 + 0]);
+    cmd[1] = urange(P->cmd_lin_vel_y[0], P->cmd_lin_vel_y[1], U[slot0 + 1]);
+    if (P->heading_command)
+      cmd[3] = urange(P->cmd_heading[0], P->cmd_heading[1], U[slot0 + 2]);
+    else
+      cmd[2] = urange(P->cmd_ang_vel_yaw[0], P->cmd_ang_vel_yaw[1], U[slot0 + 2]);
+  }
   const float keep = (float)(len2(cmd[0], cmd[1]) > 0.2f);
   cmd[0] = cmd[0] * keep;
   cmd[1] = cmd[1] * keep;
@@ -745,7 +758,7 @@ static void reset_env(const lgx_task_params* P, const lgx_buffers* B, Env& s, in
     root[1] = root[1] + urange(-1.0f, 1.0f, U[S_ROOT_XY + 1]);
   }
   for (int i = 0; i < 6; ++i) root[7 + i] = urange(-0.5f, 0.5f, U[S_ROOT_VEL + i]);
-  resample_commands(P, s.cmd, U, S_RCMD, root + 3);
+  resample_commands(P, B->command_ranges, s.cmd, U, S_RCMD, root + 3);
   s.ep = 0;
   for (int j = 0; j < D; ++j) {  // legged_robot.py:481-506
     s.th[j] = P->default_dof_pos[j] + urange(0.0f, 0.9f, U[S_DOF + j]);
@@ -775,6 +788,8 @@ static void reset_env(const lgx_task_params* P, const lgx_buffers* B, Env& s, in
     }
   const int K = P->num_reward_terms + (P->has_termination_reward ? 1 : 0);
   float* es = B->episode_sums + (size_t)e * K;
+  // the command curriculum's input (go2.py:87): the tracking_lin_vel sum at an in-step reset
+  if (!zero_carried && B->curriculum_vals) B->curriculum_vals[e] = es[P->curriculum_term];
   for (int k = 0; k < K; ++k) {
     stats[k] = es[k];
     es[k] = 0.f;
@@ -1107,7 +1122,7 @@ static void env_step(Env& s, const lgx_model* M, const lgx_task_params* P, const
     s.yaw = atan2f(2.0f * (qw * qz + qx * qy), 1.0f - 2.0f * (qy * qy + qz * qz));
   }
   // _post_physics_step_callback go2.py:390-410
-  if (ep % P->resample_interval == 0) resample_commands(P, cmd, s.U, S_CMD, root + 3);
+  if (ep % P->resample_interval == 0) resample_commands(P, B->command_ranges, cmd, s.U, S_CMD, root + 3);
   if (P->heading_command) {
     const float fwd[3] = {1.f, 0.f, 0.f};
     float f[3];
@@ -1337,6 +1352,67 @@ void episode_extras(const lgx_task_params* P, const lgx_buffers* B, float* means
   }
   for (int k = 0; k <= KS; ++k) st[k] = 0.f;
   if (step_counter) *step_counter += 1;
+}
+
+// update_command_curriculum (go2.py:80-107 / legged_robot.py:580-591): the kernel's rule
+// (lgx_env.hip curriculum_kernel), envs in order
+void command_curriculum(const lgx_task_params* P, const lgx_buffers* B, uint64_t seed, uint64_t step,
+                        const double* global_sum_count) {
+  if (step % (uint64_t)P->max_episode_length != 0) return;
+  const int N = P->num_envs;
+  double S = 0.0, Cn = 0.0;
+  if (global_sum_count) {
+    S = global_sum_count[0];
+    Cn = global_sum_count[1];
+  } else {
+    for (int e = 0; e < N; ++e)
+      if (B->reset[e]) { S += (double)B->curriculum_vals[e]; Cn += 1.0; }
+  }
+  if (Cn <= 0.0) return;
+  const float mean = ((float)S / (float)Cn) / (float)P->max_episode_length;
+  if (!(mean > P->curriculum_threshold)) return;
+  double* R = B->command_ranges;
+  const double lo = R[0], hi = R[1], d = P->curriculum_delta;
+  const double lo_max = P->curriculum_lo_free ? lo - d : P->curriculum_lo_max;
+  const double nlo = std::min(std::max(lo - d, P->curriculum_lo_min), lo_max);  // np.clip
+  const double nhi = std::min(std::max(hi + d, 0.0), P->curriculum_hi_max);
+  const bool changed = nlo != lo || nhi != hi;
+  R[0] = nlo;
+  R[1] = nhi;
+  if (float* L = B->command_range_log) {
+    if (P->command_curriculum == 1) { L[0] = (float)nhi; L[1] = (float)nlo; L[2] = (float)R[3]; L[3] = (float)R[5]; }
+    else { L[0] = (float)nhi; L[1] = (float)R[3]; L[2] = (float)R[5]; }
+  }
+  if (!changed) return;
+  const bool go2 = P->task_kind == LGX_TASK_GO2;
+  const int Pp = P->num_proprio, H = P->history_len, c0 = go2 ? 5 : 9;
+  const float co = P->clip_obs;
+  for (int e = 0; e < N; ++e) {
+    if (!B->reset[e]) continue;
+    const uint32_t gid = (uint32_t)(P->env_id_offset + e);
+    auto uni = [&](int slot) {
+      uint32_t o[4];
+      philox(gid, (uint32_t)step, (uint32_t)(slot >> 2), (uint32_t)(step >> 32), (uint32_t)seed,
+             (uint32_t)(seed >> 32), o);
+      return unit(o[slot & 3]);
+    };
+    float U[4];
+    for (int k = 0; k < 4; ++k) U[k] = uni(S_RCMD + k);
+    float* cmd = B->commands + e * 4;
+    resample_commands(P, R, cmd, U, 0, B->root_states + (size_t)e * 13 + 3);
+    float* obs = B->obs + (size_t)e * P->num_obs;
+    float* cr = (go2 && B->critic) ? B->critic + (size_t)e * P->num_critic : nullptr;
+    float* hist = B->obs_history + (size_t)e * H * Pp;
+    for (int j = 0; j < 3; ++j) {
+      const int i = c0 + j;
+      float v = cmd[j] * P->commands_scale[j];
+      if (P->add_noise) v = v + (2.0f * uni(S_NOISE + i) - 1.0f) * P->noise_vec[i];
+      const float vc = clampf(v, -co, co);
+      obs[H * Pp + i] = vc;
+      if (cr) cr[H * Pp + i] = vc;
+      for (int t = 0; t < H; ++t) hist[t * Pp + i] = v;
+    }
+  }
 }
 
 int threads() { return omp_get_max_threads(); }

@@ -17,6 +17,9 @@ void reset(const lgx_task_params* P, const lgx_buffers* B, const uint8_t* mask, 
 // lgx_episode_extras on host buffers
 void episode_extras(const lgx_task_params* P, const lgx_buffers* B, float* means, float* level_mean,
                     uint8_t* time_outs, uint64_t* step_counter);
+// lgx_command_curriculum on host buffers
+void command_curriculum(const lgx_task_params* P, const lgx_buffers* B, uint64_t seed, uint64_t step,
+                        const double* global_sum_count);
 // the worker threads the host backend uses (OpenMP)
 int threads();
 

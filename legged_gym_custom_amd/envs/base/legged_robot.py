@@ -57,9 +57,29 @@ class LeggedRobot(BaseTask):
         # the right step numbers; the host mirror follows
         self._csc += 1
         self._native.step_dev(self.seed, self._step_dev, self._stream())
+        if self._cmd_curriculum:
+            self._command_curriculum()
         self._update_extras(advance_step=True)
         return (self.obs_buf, self.privileged_obs_buf, self.critic_obs_buf, self.estimated_obs_buf, self.scan_obs_buf,
                 self.rew_buf, self.reset_buf, self.extras)
+
+    def _command_curriculum(self):
+        """update_command_curriculum for the step just run (one launch; a no-op unless the
+        step is a multiple of max_episode_length). Env shards: the mean runs over the reset
+        envs of every rank — one all-reduce of {sum, count} on those steps (the host knows
+        them: common_step_counter), so the rollout of such a run is not graph-captured."""
+        gsc = None
+        if self.num_envs_total > self.num_envs and self._csc % int(self.max_episode_length) == 0:
+            m = self.reset_buf
+            gsc = torch.stack([torch.where(m, self._curriculum_vals, 0.0).double().sum(), m.double().sum()])
+            torch.distributed.all_reduce(gsc)
+        self._native.command_curriculum(self.seed, self._step_dev, gsc, self._stream())
+
+    @property
+    def graph_capturable(self):
+        """Whether the runner may capture the rollout as one graph (not with a sharded
+        command curriculum: it all-reduces on host-known steps)."""
+        return not (self._cmd_curriculum and self.num_envs_total > self.num_envs)
 
     def reset_idx(self, env_ids):
         """reset_idx outside a step (BaseTask.reset): masked reset on device (RNG stream 1)."""
@@ -88,6 +108,11 @@ class LeggedRobot(BaseTask):
             self.extras["episode"] = {"rew_" + k: self._episode_means[i] for i, k in enumerate(self._episode_keys)}
             if self.cfg.terrain.curriculum:
                 self.extras["episode"]["terrain_level"] = self._terrain_level_mean
+            if self._cmd_curriculum:  # go2.py:255-259 / legged_robot.py:206-209
+                keys = (["max_command_x", "min_command_x", "max_command_y", "max_command_yaw"]
+                        if self.TASK_KIND == _abi.TASK_GO2 else ["max_command_x", "max_command_y", "max_command_yaw"])
+                for i, k in enumerate(keys):
+                    self.extras["episode"][k] = self._command_range_log[i]
         if self.cfg.env.send_timeouts:
             self.extras["time_outs"] = self._extras_time_outs
 
@@ -246,13 +271,6 @@ class LeggedRobot(BaseTask):
         self.command_ranges = class_to_dict(self.cfg.commands.ranges)
         if self.cfg.terrain.mesh_type not in ("heightfield", "trimesh"):
             self.cfg.terrain.curriculum = False
-        if getattr(self.cfg.commands, "curriculum", False):
-            # go2.py:80-107,222: the command ranges grow from the mean tracking reward of the
-            # envs resetting at every max_episode_length-th step, and that very step's resamples
-            # already use the new range — a grid-wide reduction inside the fused step. Off in
-            # every shipped config; refused rather than silently ignored.
-            raise NotImplementedError("commands.curriculum=True (go2.py:80-107) is not supported by the fused "
-                                      "env step; set cfg.commands.curriculum = False")
         self.max_episode_length_s = self.cfg.env.episode_length_s
         self.max_episode_length = np.ceil(self.max_episode_length_s / self.dt)
         self.cfg.domain_rand.push_interval = np.ceil(self.cfg.domain_rand.push_interval_s / self.dt)
@@ -348,9 +366,27 @@ class LeggedRobot(BaseTask):
         self.episode_sums_buf = z(n, ks)
         self.episode_sums = {k: self.episode_sums_buf[:, i] for i, k in enumerate(self._episode_keys)}
         self.episode_stats = z(ks + 1)
-        self._episode_means = z(ks)
-        self._terrain_level_mean = z(())
+        # extras['episode'] values in key order in one buffer (the runner's native episode
+        # tracking reads them as contiguous runs): rew_* means | terrain_level | command range log
+        self._extras_vals = z(ks + 1 + 4)
+        self._episode_means = self._extras_vals[:ks]
+        self._terrain_level_mean = self._extras_vals[ks]
+        self._command_range_log = self._extras_vals[ks + 1:]
         self._extras_time_outs = z(n, dtype=torch.bool)
+        # command curriculum (go2.py:80-107 / legged_robot.py:580-591): the ranges are device
+        # state (double, the reference's Python floats) updated by lgx_command_curriculum
+        self._cmd_curriculum = bool(getattr(self.cfg.commands, "curriculum", False))
+        self._command_ranges_buf = self._curriculum_vals = None
+        if self._cmd_curriculum:
+            r = self.cfg.commands.ranges
+            self._command_ranges_buf = torch.tensor(list(r.lin_vel_x) + list(r.lin_vel_y) + list(r.ang_vel_yaw) +
+                                                    list(r.heading), dtype=torch.float64, device=dev)
+            self._curriculum_vals = z(n)
+            go2 = self.TASK_KIND == _abi.TASK_GO2
+            log = ([r.lin_vel_x[1], r.lin_vel_x[0], r.lin_vel_y[1], r.ang_vel_yaw[1]] if go2
+                   else [r.lin_vel_x[1], r.lin_vel_y[1], r.ang_vel_yaw[1], 0.0])
+            self._command_range_log.copy_(torch.tensor(log, dtype=torch.float32))
+            self.command_ranges = _DeviceCommandRanges(self._command_ranges_buf)
         # NaN/Inf guard outputs (lgx_buffers.blew_up / blowup_count): per step, the envs whose
         # physics state went non-finite (given a finite stand-in state and reset); the count
         self.blew_up_buf = z(n, dtype=torch.bool)
@@ -379,6 +415,8 @@ class LeggedRobot(BaseTask):
             "terrain_levels": getattr(self, "terrain_levels", None), "terrain_types": getattr(self, "terrain_types", None),
             "terrain_origins": getattr(self, "terrain_origins", None), "height_samples": self.height_samples,
             "terrain_mesh": self._terrain_mesh, "blew_up": self.blew_up_buf, "blowup_count": self._blowup_count,
+            "command_ranges": self._command_ranges_buf, "curriculum_vals": self._curriculum_vals,
+            "command_range_log": self._command_range_log if self._cmd_curriculum else None,
             **self._sea_buffers,
         })
 
@@ -401,3 +439,29 @@ class LeggedRobot(BaseTask):
             else:
                 self.reward_scales[key] *= self.dt
         self.reward_names = [k for k in self.reward_scales if k != "termination"]
+
+
+class _DeviceCommandRanges(dict):
+    """self.command_ranges under the command curriculum: {'lin_vel_x': [lo, hi], ...} read
+    from the device ranges the curriculum updates (a host read per access)."""
+    _KEYS = ("lin_vel_x", "lin_vel_y", "ang_vel_yaw", "heading")
+
+    def __init__(self, buf):
+        super().__init__()
+        self._buf = buf
+        for k in self._KEYS:
+            dict.__setitem__(self, k, None)
+
+    def __getitem__(self, key):
+        i = self._KEYS.index(key)
+        return [float(v) for v in self._buf[2 * i:2 * i + 2].tolist()]
+
+    def __setitem__(self, key, value):
+        i = self._KEYS.index(key)
+        self._buf[2 * i:2 * i + 2] = torch.tensor([float(value[0]), float(value[1])], dtype=torch.float64)
+
+    def values(self):
+        return [self[k] for k in self._KEYS]
+
+    def items(self):
+        return [(k, self[k]) for k in self._KEYS]

@@ -198,6 +198,27 @@ def build_task_params(cfg, model, num_envs, num_envs_total=None, env_id_offset=0
     for i, (a, b) in enumerate(zip(rid, rs)):
         P.reward_ids[i] = a
         P.reward_scales[i] = b
+    # command curriculum (go2.py:80-107 / legged_robot.py:580-591; lgx.h command_curriculum)
+    c = cfg.commands
+    if getattr(c, "curriculum", False):
+        if "tracking_lin_vel" not in rn:
+            # the reference indexes episode_sums['tracking_lin_vel'] (KeyError without the term)
+            raise KeyError("commands.curriculum needs the tracking_lin_vel reward term")
+        P.curriculum_term = rn.index("tracking_lin_vel")
+        P.curriculum_threshold = float(np.float32(0.8 * rs[P.curriculum_term]))
+        if go2:
+            P.command_curriculum = 1
+            P.curriculum_delta = float(c.vel_increment)
+            P.curriculum_lo_min = float(c.max_reverse_vel)
+            P.curriculum_lo_max = 0.0
+            P.curriculum_lo_free = int(c.max_reverse_vel >= 0.0)
+            P.curriculum_hi_max = float(c.max_forward_vel)
+        else:
+            P.command_curriculum = 2
+            P.curriculum_delta = 0.05
+            P.curriculum_lo_min = -float(c.max_curriculum)
+            P.curriculum_lo_max = 0.0
+            P.curriculum_hi_max = float(c.max_curriculum)
     P.only_positive_rewards = int(cfg.rewards.only_positive_rewards)
     P.has_termination_reward = int(term_scale is not None)
     P.termination_scale = term_scale or 0.0

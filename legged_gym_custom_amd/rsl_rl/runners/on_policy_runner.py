@@ -217,7 +217,7 @@ class OnPolicyRunner:
 
     def _graphable(self, adaptation_mode):
         return (self.use_graphs and not adaptation_mode and self.device.startswith("cuda")
-                and hasattr(self.env, "advance_step_counter"))
+                and hasattr(self.env, "advance_step_counter") and getattr(self.env, "graph_capturable", True))
 
     def _rollout(self, adaptation_mode, track):
         key = ("rollout", track)

@@ -63,6 +63,12 @@ static float rand_range(float lo, float hi, float u) {
   float r = span * u;
   return r + lo;
 }
+/* the same with Python-float bounds: (hi - lo) in double, then an fp32 scalar in the tensor ops */
+static float rand_range_d(double lo, double hi, float u) {
+  float span = (float)(hi - lo);
+  float r = span * u;
+  return r + (float)lo;
+}
 
 /* ------------------------------------------------------------ small fp32 math */
 /* isaacgym torch_utils.quat_rotate_inverse (xyzw): a - b + c */
@@ -229,12 +235,22 @@ static void resample_commands(const lgx_task_params* P, lgx_buffers* B, int e, u
     for (int i = 0; i < 4; ++i) cmd[i] = P->user_command[i];
     return;
   }
-  cmd[0] = rand_range(P->cmd_lin_vel_x[0], P->cmd_lin_vel_x[1], urand(seed, gid, step, stream, slot0 + 0));
-  cmd[1] = rand_range(P->cmd_lin_vel_y[0], P->cmd_lin_vel_y[1], urand(seed, gid, step, stream, slot0 + 1));
-  if (P->heading_command)
-    cmd[3] = rand_range(P->cmd_heading[0], P->cmd_heading[1], urand(seed, gid, step, stream, slot0 + 2));
-  else
-    cmd[2] = rand_range(P->cmd_ang_vel_yaw[0], P->cmd_ang_vel_yaw[1], urand(seed, gid, step, stream, slot0 + 2));
+  const double* R = B->command_ranges; /* self.command_ranges (Python floats), when bound */
+  if (R) {
+    cmd[0] = rand_range_d(R[0], R[1], urand(seed, gid, step, stream, slot0 + 0));
+    cmd[1] = rand_range_d(R[2], R[3], urand(seed, gid, step, stream, slot0 + 1));
+    if (P->heading_command)
+      cmd[3] = rand_range_d(R[6], R[7], urand(seed, gid, step, stream, slot0 + 2));
+    else
+      cmd[2] = rand_range_d(R[4], R[5], urand(seed, gid, step, stream, slot0 + 2));
+  } else {
+    cmd[0] = rand_range(P->cmd_lin_vel_x[0], P->cmd_lin_vel_x[1], urand(seed, gid, step, stream, slot0 + 0));
+    cmd[1] = rand_range(P->cmd_lin_vel_y[0], P->cmd_lin_vel_y[1], urand(seed, gid, step, stream, slot0 + 1));
+    if (P->heading_command)
+      cmd[3] = rand_range(P->cmd_heading[0], P->cmd_heading[1], urand(seed, gid, step, stream, slot0 + 2));
+    else
+      cmd[2] = rand_range(P->cmd_ang_vel_yaw[0], P->cmd_ang_vel_yaw[1], urand(seed, gid, step, stream, slot0 + 2));
+  }
   float keep = (float)(norm2(cmd[0], cmd[1]) > 0.2f);
   cmd[0] = cmd[0] * keep;
   cmd[1] = cmd[1] * keep;
@@ -654,7 +670,28 @@ void oracle_post_physics(const lgx_task_params* P, lgx_buffers* B, uint64_t seed
     B->rew[e] = rew;
     any_reset |= reset;
   }
-  /* reset_idx (per env; curriculum only reads per-env data) */
+  /* reset_idx: update_command_curriculum first (go2.py:221-223 / legged_robot.py:176-177),
+     on steps where common_step_counter % max_episode_length == 0, over the resetting envs */
+  if (P->command_curriculum && any_reset && step % (uint64_t)P->max_episode_length == 0) {
+    float sum = 0.0f;
+    int cnt = 0;
+    for (int e = 0; e < N; ++e)
+      if (B->reset[e]) { sum += B->episode_sums[(size_t)e * KS + P->curriculum_term]; ++cnt; }
+    float mean = (sum / (float)cnt) / (float)P->max_episode_length; /* torch.mean (fp32) / max_episode_length */
+    if (mean > P->curriculum_threshold) {
+      double* R = B->command_ranges;
+      double d = P->curriculum_delta, lo = R[0] - d, hi = R[1] + d;
+      double lo_max = P->curriculum_lo_free ? R[0] - d : P->curriculum_lo_max;
+      /* np.clip(x, a, b) = minimum(maximum(x, a), b) */
+      lo = lo < P->curriculum_lo_min ? P->curriculum_lo_min : lo;
+      lo = lo > lo_max ? lo_max : lo;
+      hi = hi < 0.0 ? 0.0 : hi;
+      hi = hi > P->curriculum_hi_max ? P->curriculum_hi_max : hi;
+      R[0] = lo;
+      R[1] = hi;
+    }
+  }
+  /* per env (the terrain curriculum only reads per-env data) */
   for (int e = 0; e < N; ++e)
     if (B->reset[e]) reset_env(P, B, e, seed, step, 0, 1);
   (void)any_reset;

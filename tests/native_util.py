@@ -28,6 +28,14 @@ class Twin:
         self.native.bind(self.t)
         self.P = P
 
+    def enable_curriculum(self, d):
+        """Bind the command-curriculum buffers (initial ranges from fixture d) on both sides."""
+        import golden_util as G
+        G.enable_curriculum(self.o, d)
+        for k in ("command_ranges", "curriculum_vals", "command_range_log"):
+            self.t[k] = self.torch.from_numpy(self.o.a[k].copy()).to(self.device)
+        self.native.bind(self.t)
+
     @property
     def a(self):
         return self.o.a

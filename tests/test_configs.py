@@ -45,16 +45,16 @@ def test_config_matches_reference(task):
     assert not problems, "\n".join(problems[:40])
 
 
-def test_command_curriculum_is_refused_loudly():
-    """go2.py:80-107 (command curriculum) is not part of the fused step: asking for it
-    raises before anything is built, instead of being silently ignored."""
+def test_command_curriculum_needs_the_tracking_term():
+    """commands.curriculum (go2.py:80-107) reads episode_sums['tracking_lin_vel']; without
+    that reward term the reference raises KeyError at the first curriculum step — here at
+    build time, before anything is launched."""
     import pytest
-    from legged_gym_custom_amd.envs import task_registry
-    from legged_gym_custom_amd.utils.helpers import get_args
-    env_cfg, _ = task_registry.get_cfgs("go2")
+    from legged_gym_custom_amd import model as mdl, params as prm
+    from legged_gym_custom_amd.envs import task_registry_configs
+    env_cfg, _ = task_registry_configs("go2")
     env_cfg.commands.curriculum = True
-    try:
-        with pytest.raises(NotImplementedError, match="curriculum"):
-            task_registry.make_env("go2", get_args(["--task=go2", "--headless", "--num_envs=4"]), env_cfg=env_cfg)
-    finally:
-        env_cfg.commands.curriculum = False
+    env_cfg.rewards.scales.tracking_lin_vel = 0.0
+    m = mdl.load_model(env_cfg.asset.file, env_cfg.asset.foot_name)
+    with pytest.raises(KeyError, match="tracking_lin_vel"):
+        prm.build_task_params(env_cfg, m, 4)

@@ -19,8 +19,7 @@ import test_gpu_terrain as TT
 import test_gpu_trajectory as TJ
 
 
-@pytest.mark.parametrize("name,task", [("go2_flat_n64.npz", "go2"), ("go2_parkour_n64.npz", "go2_parkour"),
-                                       ("anymal_c_rough_n64.npz", "anymal_c_rough")])
+@pytest.mark.parametrize("name,task", T.GOLDEN_CASES)
 def test_host_post_physics_matches_reference_golden(name, task):
     T.golden_replay(name, task, "cpu")
 
@@ -83,3 +82,7 @@ def test_host_crowded_contacts_match_oracle(z):
 
 def test_host_nan_guard_resets_only_the_blown_up_env():
     T.nan_guard("cpu")
+
+
+def test_host_command_curriculum_env():
+    T.command_curriculum_env("cpu")

@@ -69,6 +69,9 @@ def replay(name, task):
     a["env_origins"][:] = d["env_origins"]
     if terrain is not None:
         o.set_terrain(*terrain)
+    curriculum = "command_ranges0" in d
+    if curriculum:
+        G.enable_curriculum(o, d)
     # BaseTask.reset(): reset_idx(all) outside a step (RNG stream 1, call 0), after init
     o.reset_envs(np.ones(N, bool), seed=int(d["seed"]), call=0, after_init=1)
     assert _close(a["root_states"], d["reset0_state.root_states"])
@@ -93,7 +96,12 @@ def replay(name, task):
         rb[:, list(P.feet_idx[:4]), 0:3] = S("physics.feet_pos")
         o.compute_torques()
         a["episode_stats"][:] = 0
+        for k in d.files:  # episode sums the fixture set before this step
+            if k.startswith(f"steps.{t}.inject."):
+                a["episode_sums"][:, list(cfg_reward_names(P, d)).index(k.rsplit(".", 1)[1])] = d[k]
         o.post_physics(int(d["seed"]), int(S("csc_in")) + 1)
+        if curriculum:
+            np.testing.assert_array_equal(a["command_ranges"], S("out.command_ranges"), err_msg=f"step {t}")
         checks = [
             ("torques", a["torques"], S("out.torques")),
             ("rew", a["rew"], S("out.rew_buf")),
@@ -135,7 +143,13 @@ def replay(name, task):
     print("worst abs errors:", {k: f"{v:.2e}" for k, v in worst.items()})
 
 
+def cfg_reward_names(P, d):
+    return [str(x) for x in d["reward_names"] if str(x) != "termination"]
+
+
 @pytest.mark.parametrize("name,task", [("go2_flat_n64.npz", "go2"), ("go2_parkour_n64.npz", "go2_parkour"),
-                                       ("anymal_c_rough_n64.npz", "anymal_c_rough")])
+                                       ("anymal_c_rough_n64.npz", "anymal_c_rough"),
+                                       ("go2_cmd_curriculum_n64.npz", "go2"), ("go2_cmd_curriculum_rev_n64.npz", "go2"),
+                                       ("anymal_cmd_curriculum_n64.npz", "anymal_c_rough")])
 def test_oracle_replays_reference_steps(name, task):
     replay(name, task)

@@ -417,7 +417,16 @@ def snapshot(env, keys):
     return out
 
 
-def run_fixture(task, n, steps, seed, path, ep_init=None, csc0=0, overrides=None, physics=None, terrain=False):
+def _ranges8(env):
+    r = env.command_ranges
+    return np.array(list(r["lin_vel_x"]) + list(r["lin_vel_y"]) + list(r["ang_vel_yaw"]) + list(r["heading"]),
+                    dtype=np.float64)
+
+
+def run_fixture(task, n, steps, seed, path, ep_init=None, csc0=0, overrides=None, physics=None, terrain=False,
+                inject=None):
+    """inject: optional {step t: {reward name: fp32 [n] episode sums}} written into the
+    reference's episode_sums before step t (recorded; the replay writes the same)."""
     env, cfg = build_env(task, n, seed, overrides)
     physics = physics or scripted_physics
     state_keys = STATE_KEYS + (["terrain_levels", "env_origins"] if terrain else [])
@@ -445,6 +454,13 @@ def run_fixture(task, n, steps, seed, path, ep_init=None, csc0=0, overrides=None
         rec["height_samples_sha1"] = np.array(hashlib.sha1(env.height_samples.numpy().tobytes()).hexdigest())
         rec["np_seed"] = np.array(seed)
 
+    curriculum = bool(getattr(cfg.commands, "curriculum", False))
+    if curriculum:
+        rec["command_ranges0"] = _ranges8(env)
+        c = cfg.commands
+        rec["curriculum_cfg"] = np.array([getattr(c, k, np.nan) for k in
+                                          ("vel_increment", "max_forward_vel", "max_reverse_vel", "max_curriculum")],
+                                         dtype=np.float64)
     # ---- BaseTask.reset(): external reset_idx(all) then step(zeros) ------------
     env.external_reset(torch.arange(n))
     rec["reset0_state"] = {k: getattr(env, k).detach().clone().numpy() for k in state_keys}
@@ -475,6 +491,9 @@ def run_fixture(task, n, steps, seed, path, ep_init=None, csc0=0, overrides=None
         acts = torch.from_numpy(rng.normal(0, 1.5, (n, 12))).float() if t > 0 else torch.zeros(n, 12)
         ep_in = env.episode_length_buf.clone().numpy()
         csc_in = env.common_step_counter
+        inj = (inject or {}).get(t)
+        for name, vals in (inj or {}).items():
+            env.episode_sums[name][:] = torch.from_numpy(np.asarray(vals, np.float32))
         pre = one_step(acts)
         o = {}
         o["obs_cur"] = env.obs_buf[:, -env.num_proprio:].numpy().copy()
@@ -496,10 +515,18 @@ def run_fixture(task, n, steps, seed, path, ep_init=None, csc0=0, overrides=None
                                            dtype=np.float64)
         if hasattr(env, "roll"):
             o["roll"] = env.roll.numpy().copy(); o["pitch"] = env.pitch.numpy().copy()
+        if curriculum:
+            o["command_ranges"] = _ranges8(env)
+            ep = env.extras.get("episode", {})
+            o["extras_command"] = np.array([float(ep.get(k, np.nan)) for k in
+                                            ("max_command_x", "min_command_x", "max_command_y", "max_command_yaw")])
         phys = {"root_states": pre["root_states"], "dof_state": pre["dof_state"],
                 "contact_forces": pre["contact_forces"],
                 "feet_pos": pre["rigid_body_states"].reshape(n, env.num_bodies, 13)[:, env.feet_indices.numpy(), 0:3].copy()}
-        steps_rec.append({"csc_in": csc_in, "ep_in": ep_in, "actions_raw": acts.numpy(), "physics": phys, "out": o})
+        st = {"csc_in": csc_in, "ep_in": ep_in, "actions_raw": acts.numpy(), "physics": phys, "out": o}
+        if inj:
+            st["inject"] = {name: np.asarray(v, np.float32) for name, v in inj.items()}
+        steps_rec.append(st)
     rec["final_obs_history"] = env.obs_history_buf.numpy().copy()
     if env._sea_w is not None:
         rec["sea_seed"] = np.array(seed)
@@ -537,6 +564,36 @@ if __name__ == "__main__":
         # curriculum trimesh, SEA actuator net (synthetic weights) for the torques
         run_fixture("anymal_c_rough", 64, 20, 1, os.path.join(REPO, "tests", "golden", "anymal_c_rough_n64.npz"),
                     csc0=390, physics=scripted_physics_course, terrain=True)
+    if "curriculum" in which:
+        # the command curriculum (go2.py:80-107 / legged_robot.py:580-591) on the step whose
+        # common_step_counter is 1000: every env's tracking_lin_vel episode sum is set before
+        # it to 0.9 x the episode maximum, so the envs resetting there (time-outs placed at
+        # ep 999, flipped robots) pass the 0.8 threshold and the range grows by delta
+        def cur(rev, lo=-0.5):
+            def ov(c):
+                c.commands.curriculum = True
+                c.commands.ranges.lin_vel_x = [lo, 0.6]
+                if hasattr(c.commands, "max_reverse_vel"):
+                    c.commands.max_reverse_vel = rev
+            return ov
+
+        def full(task, n, frac=0.9):
+            cfg_, _ = task_registry.get_cfgs(task)
+            dt = cfg_.control.decimation * cfg_.sim.dt
+            scale = cfg_.rewards.scales.tracking_lin_vel * dt
+            ml = int(np.ceil(cfg_.env.episode_length_s / dt))
+            return {2: {"tracking_lin_vel": np.full(n, frac * scale * ml, np.float32)}}
+        gd = os.path.join(REPO, "tests", "golden")
+        run_fixture("go2", 64, 6, 2, os.path.join(gd, "go2_cmd_curriculum_n64.npz"), csc0=998,
+                    overrides=cur(-1.0), inject=full("go2", 64))
+        # max_reverse_vel >= 0 (go2_parkour's sprint setting): the lower bound's np.clip has
+        # a_max = lo - delta, so it moves down by delta without a floor
+        run_fixture("go2", 64, 6, 3, os.path.join(gd, "go2_cmd_curriculum_rev_n64.npz"), csc0=998,
+                    overrides=cur(0.5, lo=0.1), inject=full("go2", 64))
+        # LeggedRobot.update_command_curriculum (+-0.05 within max_curriculum) on ANYmal rough
+        run_fixture("anymal_c_rough", 64, 5, 4, os.path.join(gd, "anymal_cmd_curriculum_n64.npz"), csc0=998,
+                    overrides=cur(None), inject=full("anymal_c_rough", 64), physics=scripted_physics_course,
+                    terrain=True)
     if "go2_parkour" in which:
         # C4 task on its full terrain (12 x 20 gap courses); robots spread along the
         # courses so the scan, jump flags, hole termination and curriculum all fire
