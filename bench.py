@@ -159,12 +159,13 @@ def committed_valu(num_envs):
     return out
 
 
-def cpu_baseline(num_envs=4096, iters=1, steps_per_env=24):
+def cpu_baseline(num_envs=4096, iters=3, steps_per_env=24):
     """The same framework on the host: `--sim_device=cpu --rl_device=cpu` (helpers.py:174-177)
     — liblgx.so's host backend (OpenMP over envs) for the env step and the torch-CPU rsl_rl
     learner, through the same task registry and runner, at the benchmark's shape (C2: 4096 envs
-    x 24 steps); one timed iteration after a warm-up one, on the host threads this process may
-    use (OMP_NUM_THREADS; 16 per GPU on the GPU box)."""
+    x 24 steps): a warm-up iteration, then `iters` timed PPO iterations, reported as the median
+    (SURVEY.md §8d), on the host threads this process may use (OMP_NUM_THREADS: 16 per GPU on
+    the GPU box, whose `nproc` counts the whole shared machine; both are recorded)."""
     from legged_gym_custom_amd.envs import task_registry
     from legged_gym_custom_amd.utils.helpers import get_args
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
@@ -176,17 +177,82 @@ def cpu_baseline(num_envs=4096, iters=1, steps_per_env=24):
     tcfg.runner.num_steps_per_env = steps_per_env
     runner, _ = task_registry.make_alg_runner(env, args=a, train_cfg=tcfg, log_root=None)
     runner.learn(1, init_at_random_ep_len=True)  # warm-up (also a DAgger iteration: it=0)
-    t0 = time.time()
-    runner.learn(iters)
-    dt = time.time() - t0
-    perf = dict(runner.last_perf)
-    return {"value": round(num_envs * steps_per_env * iters / dt, 1), "unit": "env-steps/s", "cores": threads,
-            "kind": "port",
-            "sample": f"{iters} PPO iteration(s) of Go2 flat at {num_envs} envs x {steps_per_env} steps on the host "
-                      f"(--sim_device=cpu --rl_device=cpu): liblgx.so host-backend env step (OpenMP) + torch-CPU "
-                      f"learner, {threads} threads",
-            "seconds": round(dt, 2), "collection_s": round(perf.get("collection_time", 0.0), 3),
+    times, perfs = [], []
+    for _ in range(iters):
+        t0 = time.time()
+        runner.learn(1)
+        times.append(time.time() - t0)
+        perfs.append(dict(runner.last_perf))
+    order = sorted(range(iters), key=lambda i: times[i])
+    mid = order[iters // 2]
+    dt, perf = times[mid], perfs[mid]
+    return {"value": round(num_envs * steps_per_env / dt, 1), "unit": "env-steps/s", "cores": threads,
+            "nproc": os.cpu_count(), "kind": "port",
+            "sample": f"median of {iters} PPO iterations of Go2 flat at {num_envs} envs x {steps_per_env} steps on "
+                      f"the host (--sim_device=cpu --rl_device=cpu): liblgx.so host-backend env step (OpenMP) + "
+                      f"torch-CPU learner, {threads} threads",
+            "seconds": [round(t, 2) for t in times], "collection_s": round(perf.get("collection_time", 0.0), 3),
             "learn_s": round(perf.get("learn_time", 0.0), 3)}
+
+
+def rollout_only(args, runner, env, dev, world, rank, barrier):
+    """C3: ANYmal-C rough trimesh + height scan, the env step plus the actor /
+    critic / encoder forward in privileged-latent mode, 24 steps per iteration as the runner's
+    (graph-replayed) rollout; no update — the reference's ANYmal learner cannot run (its
+    train config lacks the runner keys, Q16, and AdaptationEncoder needs history 10, Q17)."""
+    steps = runner.num_steps_per_env
+    runner._obs = [env.get_observations().to(dev), env.get_privileged_observations().to(dev),
+                   env.get_critic_observations().to(dev), env.get_estimated_observations().to(dev),
+                   env.get_scan_observations().to(dev)]
+
+    def iters(n):
+        for _ in range(n):
+            with torch.inference_mode():
+                runner._rollout(False, False)
+            runner.alg.storage.clear()
+            runner._capture_rollout(False)
+
+    iters(args.warmup + 1)  # (the first eager rollout, then the capture)
+    barrier()
+    t0 = time.time()
+    iters(args.steps)
+    barrier()
+    el = time.time() - t0
+    if world > 1:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = t.item()
+    # env kernel alone (HIP events on the launch stream)
+    stream = torch.cuda.current_stream(dev)
+    g = torch.Generator(device=dev).manual_seed(1234)
+    n_k = args.kernel_iters
+    acts = torch.randn(n_k, env.num_envs, env.num_actions, device=dev, generator=g)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_k)]
+    for i in range(n_k):
+        env.actions_in.copy_(acts[i])
+        env.common_step_counter += 1
+        evs[i][0].record(stream)
+        env._native.step(env.seed, env.common_step_counter, stream.cuda_stream)
+        evs[i][1].record(stream)
+    torch.cuda.synchronize(dev)
+    kern_ms = sorted(a.elapsed_time(b) for a, b in evs)
+    kern_avg = sum(kern_ms) / len(kern_ms)
+    if rank == 0:
+        total = args.num_envs * steps * world * args.steps
+        print(json.dumps({
+            "metric": f"env-steps/sec, {args.task} {args.num_envs} envs per GPU (env step + actor forward, "
+                      f"privileged latent)", "value": round(total / el, 1), "unit": "env-steps/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": f"synthetic ({args.task}: generated rough trimesh, random-init networks and SEA-LSTM weights, "
+                    f"seed 1)",
+            "config": {"workload": f"{args.task} rollout: {steps} x (act in privileged-latent mode + env step)",
+                       "num_envs_per_gpu": args.num_envs, "num_steps_per_env": steps,
+                       "global_envs": args.num_envs * world, "parallelism": f"env-sharded dp{world}"},
+            "env_kernel": {"avg_us": round(kern_avg * 1e3, 2), "min_us": round(kern_ms[0] * 1e3, 2),
+                           "env_steps_per_s": round(env.num_envs / (kern_avg * 1e-3), 1)}}))
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def main():
@@ -197,7 +263,8 @@ def main():
     ap.add_argument("--num_envs", type=int, default=4096)
     ap.add_argument("--no_cpu_baseline", action="store_true")
     ap.add_argument("--kernel_iters", type=int, default=50)
-    ap.add_argument("--task", default="go2", help="go2 (the BASELINE metric) | go2_parkour (C4, informative)")
+    ap.add_argument("--task", default="go2", help="go2 (the BASELINE metric) | go2_parkour (C4) | anymal_c_rough "
+                                                  "(C3: rollout only)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -225,7 +292,17 @@ def main():
     from legged_gym_custom_amd.utils.helpers import get_args
     a = get_args([f"--task={args.task}", "--headless", f"--num_envs={args.num_envs}", f"--sim_device={dev}",
                   f"--rl_device={dev}", "--seed=1"])
-    env, env_cfg = task_registry.make_env(args.task, a)
+    env_cfg = None
+    if args.task.startswith("anymal"):
+        # the reference's trained actuator archive does not ship with this build:
+        # a synthetic SEA-LSTM archive of the same layout, written here
+        import tempfile
+        from legged_gym_custom_amd import actuator as act
+        env_cfg, _ = task_registry.get_cfgs(args.task)
+        sea = os.path.join(tempfile.mkdtemp(prefix="lgx_sea_"), "sea.pt")
+        act.save_sea_archive(act.random_sea_weights(1, scale=0.3), sea)
+        env_cfg.control.actuator_net_file = sea
+    env, env_cfg = task_registry.make_env(args.task, a, env_cfg=env_cfg)
     _, train_cfg = task_registry.get_cfgs(args.task)
     runner, _ = task_registry.make_alg_runner(env, args=a, train_cfg=train_cfg, log_root=None)
 
@@ -250,6 +327,8 @@ def main():
             el = t.item()
         return el, dict(runner.last_perf)
 
+    if args.task.startswith("anymal"):
+        return rollout_only(args, runner, env, dev, world, rank, barrier)
     elapsed_nt, perf_nt = timed(False)  # iterations 0..W-1 warm-up (0 is a DAgger iteration), then W..W+K-1
     # same window position for the tracked run (no DAgger iteration inside either window,
     # it % 20 == 0, on_policy_runner.py:147)

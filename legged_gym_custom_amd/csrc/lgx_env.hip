@@ -79,11 +79,20 @@ static_assert(sizeof(DynTemps) <= ROWS_FLOATS * sizeof(float), "dynamics tempora
 LGX_DEV DynTemps& dtmp() { return *reinterpret_cast<DynTemps*>(lgx_dyn); }
 LGX_DEV float* stg_U() { return lgx_dyn; }
 LGX_DEV float* stg_cur(const lgx_task_params* Pm) { return lgx_dyn + 4 * rng_blocks(Pm); }
+// The old observation history is staged in LDS when it is short (Go2: 10 x 52 = 520); a long
+// one (ANYmal: 5 x 235 = 1175, 4.7 KB) is shifted in place in HBM instead (post-physics below),
+// which keeps ANYmal's arena at the Go2 size: 9.9 KB of LDS per env, 16 envs per CU.
+constexpr int HIST_LDS_MAX = 640;
+__host__ __device__ inline bool hist_in_lds(const lgx_task_params* Pm) {
+  return Pm->history_len * Pm->num_proprio <= HIST_LDS_MAX || Pm->num_proprio < 64;
+}
 LGX_DEV float* stg_hist(const lgx_task_params* Pm) { return stg_cur(Pm) + Pm->num_proprio; }
-LGX_DEV float* stg_heights(const lgx_task_params* Pm) { return stg_hist(Pm) + Pm->history_len * Pm->num_proprio; }
+LGX_DEV float* stg_heights(const lgx_task_params* Pm) {
+  return stg_hist(Pm) + (hist_in_lds(Pm) ? Pm->history_len * Pm->num_proprio : 0);
+}
 static inline int64_t arena_floats(const lgx_task_params& p) {
-  const int64_t post = 4 * (9 + (p.num_proprio + 3) / 4) + p.num_proprio + (int64_t)p.history_len * p.num_proprio +
-                       p.num_height_points;
+  const int64_t post = 4 * (9 + (p.num_proprio + 3) / 4) + p.num_proprio +
+                       (hist_in_lds(&p) ? (int64_t)p.history_len * p.num_proprio : 0) + p.num_height_points;
   return post > ROWS_FLOATS ? post : ROWS_FLOATS;
 }
 
@@ -1469,7 +1478,7 @@ LGX_DEV void get_heights(const lgx_task_params* Pm, const lgx_buffers& B, Sh& s,
 // envs are one residency round on 256 CUs). The SEA-LSTM variant keeps its hidden states in
 // registers (fewer waves per SIMD; ANYmal's LDS image is 13 KB).
 #ifndef LGX_SEA_WAVES
-#define LGX_SEA_WAVES 2
+#define LGX_SEA_WAVES 4
 #endif
 template <bool PHYSICS, bool TERRAIN, bool ACTNET>
 __global__ __launch_bounds__(64, ACTNET ? LGX_SEA_WAVES : 4) void env_step_kernel(const lgx_model* __restrict__ M,
@@ -1803,20 +1812,46 @@ __global__ __launch_bounds__(64, ACTNET ? LGX_SEA_WAVES : 4) void env_step_kerne
   float* hist_g = B.obs_history + (size_t)e * H * Pp;
   float* const hist = stg_hist(Pm);
   const float* const cur = stg_cur(Pm);
-#pragma unroll
-  for (int t = 0; t < HV; ++t) {
-    const int i = lane + 64 * t;
-    if (i < H * Pp) hist[i] = reset ? 0.f : hv[t];
-  }
-  for (int i = lane + 64 * HV; i < H * Pp; i += 64) hist[i] = reset ? 0.f : hist_g[i];
-  __syncthreads();
+  const bool hl = hist_in_lds(Pm);
+  const long long ep = s.ep;
   const float co = Pm->clip_obs;
   float* obs = B.obs + (size_t)e * Pm->num_obs;
   float* cr = B.critic ? B.critic + (size_t)e * Pm->num_critic : nullptr;
-  for (int i = lane; i < H * Pp; i += 64) {
-    float v = clipf(hist[i], -co, co);
-    obs[i] = v;
-    if (go2 && cr) cr[i] = v;
+  if (hl) {
+#pragma unroll
+    for (int t = 0; t < HV; ++t) {
+      const int i = lane + 64 * t;
+      if (i < H * Pp) hist[i] = reset ? 0.f : hv[t];
+    }
+    for (int i = lane + 64 * HV; i < H * Pp; i += 64) hist[i] = reset ? 0.f : hist_g[i];
+  }
+  __syncthreads();
+  if (hl) {
+    for (int i = lane; i < H * Pp; i += 64) {
+      float v = clipf(hist[i], -co, co);
+      obs[i] = v;
+      if (go2 && cr) cr[i] = v;
+    }
+  } else {
+    // long history, shifted in place: entry i of the old history goes to obs[i], and the new
+    // history's entry i is old entry i + P (or the current observation, go2.py:570-574).
+    // Chunks of 64 in increasing i: a chunk reads old entries >= its own first index (P >= 64)
+    // and writes only its own 64, after its reads are consumed — no entry is overwritten
+    // before it is read.
+    const int HP = H * Pp, HP1 = (H - 1) * Pp;
+#pragma unroll
+    for (int t = 0; t < (MAXHIST + 63) / 64; ++t) {
+      const int i = lane + 64 * t;
+      if (64 * t >= HP) break;
+      if (i < HP) {
+        const float old = reset ? 0.f : (t < HV ? hv[t < HV ? t : 0] : hist_g[i]);
+        const float v = clipf(old, -co, co);
+        obs[i] = v;
+        if (go2 && cr) cr[i] = v;
+        const float nv = (ep <= 1) ? cur[i % Pp] : (i < HP1 ? hist_g[i + Pp] : cur[i - HP1]);
+        hist_g[i] = nv;
+      }
+    }
   }
   for (int i = lane; i < Pp; i += 64) {
     float v = clipf(cur[i], -co, co);
@@ -1847,12 +1882,12 @@ __global__ __launch_bounds__(64, ACTNET ? LGX_SEA_WAVES : 4) void env_step_kerne
       if (cr) cr[NO + Pm->num_priv + 3 + i] = clipf(v, -co, co);
     }
   }
-  // history update go2.py:570-574
-  const long long ep = s.ep;
-  for (int i = lane; i < H * Pp; i += 64) {
-    float v = (ep <= 1) ? cur[i % Pp] : (i < (H - 1) * Pp ? hist[i + Pp] : cur[i - (H - 1) * Pp]);
-    hist_g[i] = v;
-  }
+  // history update go2.py:570-574 (the long-history path wrote it above)
+  if (hl)
+    for (int i = lane; i < H * Pp; i += 64) {
+      float v = (ep <= 1) ? cur[i % Pp] : (i < (H - 1) * Pp ? hist[i + Pp] : cur[i - (H - 1) * Pp]);
+      hist_g[i] = v;
+    }
   // last_* copies go2.py:380-384 and state write-back
   if (lane < A) B.last_actions[(size_t)e * A + lane] = s.act[lane];
   if (lane < D) {

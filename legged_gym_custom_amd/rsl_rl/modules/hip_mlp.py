@@ -512,6 +512,9 @@ def linear_forward(x, W, b, elu, out=None):
     M, K = x.shape
     N = W.shape[0]
     y = out if out is not None else torch.empty(M, N, device=x.device, dtype=torch.float32)
+    if K == 0:  # nn.Linear on an empty input: the bias on every row
+        bb = b.detach()
+        return y.copy_((torch.nn.functional.elu(bb) if elu else bb).expand_as(y))
     _run(GemmArgs(A=_ptr(x), lda=x.stride(0), a_kcontig=1, B=_ptr(W), ldb=W.stride(0), b_kcontig=1,
                   C=_ptr(y), ldc=y.stride(0), M=M, N=N, K=K, epilogue=EPI_BIAS | (EPI_ELU if elu else 0),
                   bias=_ptr(b), split_k=1))
@@ -723,7 +726,13 @@ def _group_forward(xs, chains, finals=None):
                     raise MlpLibError("forward_group: output span shape does not match the chain")
                 if y is None:
                     y = torch.empty(hs[c].shape[0], Ws[d].shape[0], device=hs[c].device, dtype=torch.float32)
-                args.append(_fwd_args(hs[c], Ws[d], bs[d], flags[d], y))
+                if hs[c].shape[1] == 0:
+                    # a layer on an empty input (e.g. ANYmal's scan encoder, num_scan_obs = 0):
+                    # nn.Linear gives its bias on every row
+                    bb = bs[d].detach()
+                    y.copy_((torch.nn.functional.elu(bb) if flags[d] else bb).expand_as(y))
+                else:
+                    args.append(_fwd_args(hs[c], Ws[d], bs[d], flags[d], y))
                 outs[c].append(y)
                 hs[c] = y
         run_group(args)

@@ -10,7 +10,7 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB = os.path.join(HERE, "build", "liblgx_oracle.so")
+LIB = os.environ.get("LGX_ORACLE_LIB") or os.path.join(HERE, "build", "liblgx_oracle.so")  # (sanitizer builds)
 
 _lib = None
 

@@ -516,3 +516,22 @@ def test_fused_loss_heads_match_separate_heads_bitwise():
         assert torch.equal(x, y)
     for x, y in zip(run(True, span=True), ref):
         assert torch.equal(x, y)
+
+
+def test_group_forward_on_empty_input_gives_the_bias():
+    """A chain whose input has no columns (ANYmal's scan encoder: num_scan_obs = 0) — nn.Linear
+    on [rows, 0] is its bias on every row — inside a grouped launch beside a normal chain."""
+    from legged_gym_custom_amd.rsl_rl.modules.support_networks import ScanEncoder
+    torch.manual_seed(0)
+    enc = ScanEncoder(num_scan_obs=0, output_dim=32, hidden_dims=[128, 64]).to(dev)
+    other = ScanEncoder(num_scan_obs=20, output_dim=16, hidden_dims=[32]).to(dev)
+    x0 = torch.zeros(300, 0, device=dev)
+    x1 = torch.randn(300, 20, device=dev)
+    with torch.no_grad():
+        got0, got1 = H.forward_group([enc.group_item(x0), other.group_item(x1)])
+        alone = enc(x0)  # the module's own (single-chain) forward
+        ref0 = enc.scan_encoder.cpu()(torch.zeros(300, 0))
+        ref1 = other.scan_encoder.cpu()(x1.cpu())
+    torch.testing.assert_close(alone.cpu(), ref0, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(got0.cpu(), ref0, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(got1.cpu(), ref1, rtol=1e-4, atol=1e-4)
