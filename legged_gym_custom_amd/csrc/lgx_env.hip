@@ -664,6 +664,84 @@ LGX_DEV float sea_torque(const lgx_task_params* Pm, const lgx_buffers& B, int e,
   return Pm->sea_out_scale * (y + Pm->sea_lin_b);
 }
 
+// The same actuator net lane-parallel over hidden units (the kernel's form): lane L serves unit
+// u = L & 7 of joint j = 8 * pass + (L >> 3) — joints 0..7, then 8..11 on lanes 0..31 — and holds
+// only that unit's h and c of both layers. A gate row's dot product over the 8 units of a layer
+// takes the joint's other units by ds_swizzle inside the 8-lane group; every sum runs in the order
+// of sea_torque above (the host backend's and the oracle's), so the torques are the same. Weight
+// rows are lane-indexed (vector loads of the params, L1-resident): 1/8 of the per-lane work and
+// transcendentals of one-joint-per-lane, and 4 state values per lane instead of 32.
+template <int K>
+LGX_DEV float unit_of(float v) {  // unit K of this lane's 8-lane group
+  return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), 0x18 | (K << 5)));
+}
+LGX_DEV void unit_vec(float v, float (&o)[8]) {
+  o[0] = unit_of<0>(v); o[1] = unit_of<1>(v); o[2] = unit_of<2>(v); o[3] = unit_of<3>(v);
+  o[4] = unit_of<4>(v); o[5] = unit_of<5>(v); o[6] = unit_of<6>(v); o[7] = unit_of<7>(v);
+}
+// one LSTM cell step for unit u: returns (h, c) in place; xin: the layer input (NIN values, the
+// same for the 8 lanes of a joint), hall: the layer's old h of all 8 units
+template <int NIN>
+LGX_DEV void sea_unit(const float* __restrict__ w_ih, const float* __restrict__ w_hh, const float* __restrict__ b_ih,
+                      const float* __restrict__ b_hh, int u, const float* xin, const float (&hall)[8], float& h,
+                      float& c) {
+  float g4[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int g = q * 8 + u;
+    float a = 0.0f, b = 0.0f;
+#pragma unroll
+    for (int k = 0; k < NIN; ++k) a += w_ih[g * NIN + k] * xin[k];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) b += w_hh[g * 8 + k] * hall[k];
+    g4[q] = (a + b_ih[g]) + (b + b_hh[g]);
+    __builtin_amdgcn_sched_barrier(0);  // one gate row's weights live at a time (VGPR budget)
+  }
+  const float ig = sigmoidf_(g4[0]), fg = sigmoidf_(g4[1]), gg = tanhf(g4[2]), og = sigmoidf_(g4[3]);
+  c = fg * c + ig * gg;
+  h = og * tanhf(c);
+}
+// all 12 joints' SEA torques into s.tau (every lane of the wave takes part)
+#ifdef LGX_SEA_INLINE
+LGX_DEV
+#else
+// a call: its registers do not add to the substep's live set (inlined, 54 VGPRs spill at the
+// 4-waves-per-SIMD budget)
+__device__ __attribute__((noinline))
+#endif
+void sea_torques_lanes(Sh& s, const lgx_task_params* Pm, const lgx_buffers& B, int e, int lane) {
+  const size_t NT = (size_t)Pm->num_envs * Pm->num_dof;
+  const int u = lane & 7;
+#pragma unroll 1
+  for (int pass = 0; pass < 2; ++pass) {
+    const int j = pass * 8 + (lane >> 3);
+    const bool on = j < NJ;  // pass 1: lanes 0..31 (joints 8..11); lanes 32..63 follow along
+    const int jj = on ? j : NJ - 1;
+    const size_t r = (size_t)e * Pm->num_dof + jj;
+    float h0 = B.sea_hidden[r * 8 + u], c0 = B.sea_cell[r * 8 + u];
+    float h1 = B.sea_hidden[(NT + r) * 8 + u], c1 = B.sea_cell[(NT + r) * 8 + u];
+    const float in0 = (s.act[jj] * Pm->action_scale + Pm->default_dof_pos[jj]) - s.th[jj];
+    const float x[2] = {in0 * Pm->sea_in_scale[0], s.thd[jj] * Pm->sea_in_scale[1]};
+    float hall[8];
+    unit_vec(h0, hall);
+    sea_unit<2>(Pm->sea_w_ih0, Pm->sea_w_hh0, Pm->sea_b_ih0, Pm->sea_b_hh0, u, x, hall, h0, c0);
+    float x1[8];
+    unit_vec(h0, x1);    // layer 1 input: the new layer-0 h of the 8 units
+    unit_vec(h1, hall);  // layer 1's old h
+    sea_unit<8>(Pm->sea_w_ih1, Pm->sea_w_hh1, Pm->sea_b_ih1, Pm->sea_b_hh1, u, x1, hall, h1, c1);
+    if (on) {
+      B.sea_hidden[r * 8 + u] = h0; B.sea_cell[r * 8 + u] = c0;
+      B.sea_hidden[(NT + r) * 8 + u] = h1; B.sea_cell[(NT + r) * 8 + u] = c1;
+    }
+    float y8[8];
+    unit_vec(h1, y8);
+    float y = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) y += Pm->sea_lin_w[k] * y8[k];
+    if (on && u == 0) s.tau[j] = Pm->sea_out_scale * (y + Pm->sea_lin_b);
+  }
+}
+
 // one physics substep (legged_robot.py:80-85 loop body)
 template <bool TERRAIN, bool ACTNET>
 LGX_DEV void substep(Sh& s, const lgx_model* M_, const lgx_task_params* Pm_, const lgx_buffers& B, int lane_,
@@ -679,10 +757,16 @@ LGX_DEV void substep(Sh& s, const lgx_model* M_, const lgx_task_params* Pm_, con
   // ---- PD torques: LeggedRobot._compute_torques legged_robot.py:440-478
   {
 #pragma clang fp contract(off)
-    if (ACTNET && lane < NJ) {
-      const int j = lane;
-      s.tau[j] = sea_torque(Pm, B, blockIdx.x, j, (s.act[j] * Pm->action_scale + Pm->default_dof_pos[j]) - s.th[j],
-                            s.thd[j]);
+    if (ACTNET) {
+#ifdef LGX_SEA_PER_JOINT  // (the one-joint-per-lane form, for A/B)
+      if (lane < NJ) {
+        const int j = lane;
+        s.tau[j] = sea_torque(Pm, B, blockIdx.x, j, (s.act[j] * Pm->action_scale + Pm->default_dof_pos[j]) - s.th[j],
+                              s.thd[j]);
+      }
+#else
+      sea_torques_lanes(s, Pm, B, blockIdx.x, lane);
+#endif
     } else if (lane < NJ) {
       const int j = lane;
       float as = s.act[j] * Pm->action_scale;

@@ -92,13 +92,15 @@ __device__ __forceinline__ void split8(const float* v, bf16x8& h, bf16x8& l) {
   }
 }
 
-// Staging of one operand tile [ROWS][BKS] — R = ROWS/8 floats per thread.
-template <int MODE, int ROWS>
+// Staging of one operand tile [ROWS][BKS] by NTH threads — R = ROWS * BKS / NTH floats per thread
+// (256 threads: ROWS / 8).
+template <int MODE, int ROWS, int NTH = NT>
 struct Stager {
-  static constexpr int R = ROWS / 8;
-  static constexpr int T = ROWS / 64;          // 8-k tasks per thread (KV)
-  static constexpr int KG = ROWS / 32;         // k per thread (MV)
+  static constexpr int R = ROWS * BKS / NTH;
+  static constexpr int T = 4 * ROWS / NTH;     // 8-k tasks per thread (KV)
+  static constexpr int KG = ROWS * BKS / (4 * NTH);  // k per thread (MV)
   static constexpr int NKQ = BKS / KG;         // k groups per step (MV): 8 or 16
+  static_assert(T >= 1 && KG >= 2, "tile too small for the thread count");
   // MV thread map. LGX_MV_ROWMAJOR (default): rg = tid % NRG (4-row group), kq = tid / NRG
   // (k group): consecutive lanes read consecutive 16 B of one source row (k), so a wave's
   // load is 2 (ROWS 128) or 4 (ROWS 64) fully contiguous row segments — the texture path
@@ -117,7 +119,7 @@ struct Stager {
     if (MODE == KV) {
 #pragma unroll
       for (int t = 0; t < T; ++t) {
-        const int idx = tid + t * NT, r = idx >> 2, g = idx & 3;
+        const int idx = tid + t * NTH, r = idx >> 2, g = idx & 3;
         const int row = min(row0 + r, rows - 1), k = k0 + g * 8;
         const float* q = p + (int64_t)row * ld + k;
         float* o = v + t * 8;
@@ -165,7 +167,7 @@ struct Stager {
   __device__ __forceinline__ static void store_part(__bf16* hi, __bf16* lo, int tid, const float (&v)[R], int q) {
     if (MODE == KV) {
       const int t = q;
-      const int idx = tid + t * NT, r = idx >> 2, g = idx & 3;
+      const int idx = tid + t * NTH, r = idx >> 2, g = idx & 3;
       bf16x8 h, l;
       split8(v + t * 8, h, l);
       const int off = lds_off(r, g);
@@ -237,15 +239,18 @@ __device__ __forceinline__ float elu(float v) {
 }
 
 // One output tile (logical index L: n fastest, then m, then the K split) of one GEMM.
-// BM_ rows x BN_ columns; 4 waves as 2 (rows) x 2 (columns), each BM_/2 x BN_/2. BM_ = 64
-// serves the rollout's 4096-row forward launches (twice the blocks, half the work per K step).
-template <int AM, int BMODE, bool COLSUM, int BN_, int BM_ = BM, int PF = LGX_PF>
+// BM_ rows x BN_ columns; NW = 4 waves as 2 (rows) x 2 (columns), each BM_/2 x BN_/2, or NW = 8
+// as 2 x 4, each BM_/2 x BN_/4 (half the MFMAs and staging per wave: twice the waves in flight
+// on the same LDS). BM_ = 64 serves the rollout's 4096-row forward launches (twice the blocks,
+// half the work per K step).
+template <int AM, int BMODE, bool COLSUM, int BN_, int BM_ = BM, int PF = LGX_PF, int NW = 4>
 __device__ __forceinline__ void gemm_tile(const Params& p, const int L) {
-  using SA = Stager<AM, BM_>;
-  using SB = Stager<BMODE, BN_>;
+  constexpr int NTH = 64 * NW;
+  using SA = Stager<AM, BM_, NTH>;
+  using SB = Stager<BMODE, BN_, NTH>;
   constexpr int MI = BM_ / 32;             // 16-row MFMA tiles per wave
   constexpr int A_ELEMS = BM_ * PITCH;     // one A image (hi or lo)
-  constexpr int NJ = BN_ / 32;             // 16-wide MFMA column tiles per wave
+  constexpr int NJ = BN_ / (8 * NW);       // 16-wide MFMA column tiles per wave
   constexpr int B_ELEMS = BN_ * PITCH;
   constexpr int STAGE = 2 * A_ELEMS + 2 * B_ELEMS;
   extern __shared__ __align__(16) __bf16 lds[];
@@ -257,7 +262,7 @@ __device__ __forceinline__ void gemm_tile(const Params& p, const int L) {
   const int kbeg = z * p.kchunk;
   const int kend = min(p.K, kbeg + p.kchunk);
   const int nsteps = kend > kbeg ? (kend - kbeg + BKS - 1) / BKS : 0;
-  const int wm = (wave & 1) * (BM_ / 2), wn = (wave >> 1) * (BN_ / 2);
+  const int wm = (wave & 1) * (BM_ / 2), wn = (wave >> 1) * (BN_ / (NW / 2));
 
   float va[PF][SA::R], vb[PF][SB::R];  // PF register sets: loads run PF steps ahead
   float csum[4] = {0.f, 0.f, 0.f, 0.f};
@@ -366,7 +371,7 @@ __device__ __forceinline__ void gemm_tile(const Params& p, const int L) {
   // [BM_][BN_ + 4] fp32 image, then row-contiguous float4 reads/writes of C (and act).
   constexpr int CP = BN_ + 4;
   constexpr int CH = BN_ / 4;              // float4 chunks per row
-  constexpr int IT = BM_ * CH / NT;         // chunks per thread
+  constexpr int IT = BM_ * CH / NTH;        // chunks per thread
   const bool part = p.split > 1;
   const bool delu = !part && (p.epi & LGX_EPI_DELU);
   // ELU outputs of the previous layer: issue every load before the tile is even staged
@@ -374,7 +379,7 @@ __device__ __forceinline__ void gemm_tile(const Params& p, const int L) {
   if (delu) {
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
-      const int idx = tid + it * NT;
+      const int idx = tid + it * NTH;
       const int m = m0 + idx / CH, n = n0 + (idx % CH) * 4;
       const float* ap = p.act + (int64_t)m * p.ld_act + n;
       if (m < p.M && n + 4 <= p.N) {
@@ -402,7 +407,7 @@ __device__ __forceinline__ void gemm_tile(const Params& p, const int L) {
   const bool accum = !part && (p.epi & LGX_EPI_ACCUM);
 #pragma unroll
   for (int it = 0; it < IT; ++it) {
-    const int idx = tid + it * NT;
+    const int idx = tid + it * NTH;
     const int row = idx / CH, c = (idx % CH) * 4;
     const int m = m0 + row, n = n0 + c;
     if (m >= p.M || n >= p.N) continue;
@@ -472,8 +477,10 @@ struct GroupParams {
 };
 static_assert(sizeof(GroupParams) <= 4096, "kernel argument segment");
 
-template <int KIND, int BN_, int BM_ = BM>
-__global__ __launch_bounds__(NT, 2) void gemm_group_kernel(GroupParams g) {
+// NW = 8 (512-thread blocks, 128 x 128 tiles only): two blocks per CU are 4 waves per SIMD,
+// so at most 128 VGPRs (launch bound)
+template <int KIND, int BN_, int BM_ = BM, int NW = 4>
+__global__ __launch_bounds__(64 * NW, NW == 8 ? 4 : 2) void gemm_group_kernel(GroupParams g) {
   const int x = blockIdx.x & 7, j = blockIdx.x >> 3;
   if (j >= g.per_xcd) return;
   int i = 0;
@@ -487,19 +494,19 @@ __global__ __launch_bounds__(NT, 2) void gemm_group_kernel(GroupParams g) {
   if constexpr (KIND == G_FWD) {
     const Params p = g.p[i];
     if (l >= p.tiles) return;
-    gemm_tile<KV, KV, false, BN_, BM_>(p, l);
+    gemm_tile<KV, KV, false, BN_, BM_, LGX_PF, NW>(p, l);
   } else if constexpr (KIND == G_DX) {
     const Params p = g.p[i];
     if (l >= p.tiles) return;
-    if (m) gemm_tile<KV, MVE, false, BN_, BM_>(p, l);
-    else gemm_tile<KV, MV, false, BN_, BM_>(p, l);
+    if (m) gemm_tile<KV, MVE, false, BN_, BM_, LGX_PF, NW>(p, l);
+    else gemm_tile<KV, MV, false, BN_, BM_, LGX_PF, NW>(p, l);
   } else {
     const Params& p = g.p[i];
     if (l >= p.tiles) return;
-    if (m == 0) gemm_tile<MV, MV, true, BN_>(p, l);
-    else if (m == 1) gemm_tile<MVE, MV, true, BN_>(p, l);
-    else if (m == 2) gemm_tile<MV, MVE, true, BN_>(p, l);
-    else gemm_tile<MVE, MVE, true, BN_>(p, l);
+    if (m == 0) gemm_tile<MV, MV, true, BN_, BM, LGX_PF, NW>(p, l);
+    else if (m == 1) gemm_tile<MVE, MV, true, BN_, BM, LGX_PF, NW>(p, l);
+    else if (m == 2) gemm_tile<MV, MVE, true, BN_, BM, LGX_PF, NW>(p, l);
+    else gemm_tile<MVE, MVE, true, BN_, BM, LGX_PF, NW>(p, l);
   }
 }
 
@@ -1248,6 +1255,21 @@ static int group_tile_m(int kind, int bn, int64_t tiles128) {
   return kind == lgxm::G_FWD && bn == 64 && tiles128 < 512 ? 64 : lgxm::BM;
 }
 
+// Waves per block of the 128 x 128 grouped launches: 8 for the forward and input-gradient kinds
+// (4 waves per SIMD at 108-122 VGPRs instead of 2 at 194-210: +1.5-2 % per iteration, r03,
+// profiles/r03_gemm_waves.txt), 4 for the weight gradient (8 measured equal, and its bias-gradient
+// sums would change order vs the single-launch path). Dev knobs: LGX_MLP_NW, LGX_MLP_NW_DW (4 or 8).
+static int group_waves(int kind) {
+  static int fwd = -1, dw = -1;
+  if (fwd < 0) {
+    const char* e = getenv("LGX_MLP_NW");
+    fwd = e ? (atoi(e) == 4 ? 4 : 8) : 8;
+    const char* d = getenv("LGX_MLP_NW_DW");
+    dw = d && atoi(d) == 8 ? 8 : 4;
+  }
+  return kind == lgxm::G_DW ? dw : fwd;
+}
+
 // ================================================================ rollout bookkeeping
 namespace lgxm {
 
@@ -1679,8 +1701,17 @@ int32_t lgx_gemm_group(const lgx_gemm_args* args, int32_t n, void* stream) {
   g.per_xcd = total;
   const int grid = 8 * total;
   hipStream_t s = static_cast<hipStream_t>(stream);
+  const int nw = group_waves(kind);
 #define LGX_GROUP_LAUNCH(K)                                                                                     \
-  if (bn == 128) {                                                                                              \
+  if (bn == 128 && nw == 8) {                                                                                   \
+    static bool attr8 = false;                                                                                  \
+    if (!attr8) {                                                                                               \
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_group_kernel<K, 128, BM, 8>),              \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes(128));               \
+      attr8 = true;                                                                                             \
+    }                                                                                                           \
+    hipLaunchKernelGGL((gemm_group_kernel<K, 128, BM, 8>), dim3(grid), dim3(512), lds_bytes(128), s, g);       \
+  } else if (bn == 128) {                                                                                       \
     static bool attr = false;                                                                                   \
     if (!attr) {                                                                                                \
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_group_kernel<K, 128>),                     \
