@@ -702,11 +702,11 @@ LGX_DEV void sea_unit(const float* __restrict__ w_ih, const float* __restrict__ 
   h = og * tanhf(c);
 }
 // all 12 joints' SEA torques into s.tau (every lane of the wave takes part)
-#ifdef LGX_SEA_INLINE
+#ifndef LGX_SEA_CALL
+// inlined (54 VGPRs spill at the 4-waves-per-SIMD budget, yet C3's kernel is 589 us against 611
+// as a call and 642 one joint per lane: profiles/r03_bench_anymal_c_rough_sea_waves.txt)
 LGX_DEV
 #else
-// a call: its registers do not add to the substep's live set (inlined, 54 VGPRs spill at the
-// 4-waves-per-SIMD budget)
 __device__ __attribute__((noinline))
 #endif
 void sea_torques_lanes(Sh& s, const lgx_task_params* Pm, const lgx_buffers& B, int e, int lane) {
