@@ -583,6 +583,137 @@ LGX_DEV TerrainHit terrain_contact(const lgx_task_params* Pm, const lgx_buffers&
   return h;
 }
 
+// The same query for every contact candidate of the wave at once, the work spread over lanes:
+// each candidate lane (cand) bounds its cell range, drops out when its sphere is above every
+// vertex the range can reach (a conservative block maximum packed in the mesh words' bits
+// 20-31, utils/terrain_utils.pack_mesh: such a sphere is farther than r + contact_margin from
+// the surface, so it forms no row either way), and the remaining (candidate, cell) tasks run
+// 64 per round, one per lane; each candidate lane then folds its tasks' closest points in the
+// serial loop's (i, j, triangle) order with the same strict comparison, so the result equals
+// terrain_contact's exactly. One-candidate-per-lane made a wave as slow as its candidate with
+// the most cells (25 cells x 2 triangles for a 0.1 m sphere) for all 22 (ANYmal) or 55 (Go2)
+// lanes at once. Scratch: the LDS arena (rows are formed after detection).
+constexpr int MESH_BLOCK = 8;  // vertices per block side of the packed block maxima
+LGX_DEV float mesh_block_bound(uint32_t w) {  // block max height (raw units), or +inf if absent
+  return (w >> 31) ? (float)((int)((w >> 20) & 0x7ffu) * 32 - 32768) : 3.0e38f;
+}
+LGX_DEV TerrainHit terrain_contact_wave(const lgx_task_params* Pm, const lgx_buffers& B, f3 x, float r, bool cand,
+                                        int lane) {
+  const float hs = Pm->horizontal_scale, vs = Pm->vertical_scale;
+  const int rows = Pm->hf_rows, cols = Pm->hf_cols;
+  const uint32_t* mesh = B.terrain_mesh;
+  int cnt = 0, ci = 0, cj = 0, i0 = 0, j0 = 0, w = 1;
+  f3 p = mk(0.f, 0.f, 0.f);
+  if (cand) {
+    const float gx = x.x + Pm->border_size, gy = x.y + Pm->border_size;
+    ci = (int)floorf(gx / hs);
+    cj = (int)floorf(gy / hs);
+    p = mk(gx - (float)ci * hs, gy - (float)cj * hs, x.z);
+    i0 = max(ci + (int)ceilf((p.x - r) / hs) - 2, 0);
+    const int i1 = min(ci + (int)floorf((p.x + r) / hs) + 1, rows - 2);
+    j0 = max(cj + (int)ceilf((p.y - r) / hs) - 2, 0);
+    const int j1 = min(cj + (int)floorf((p.y + r) / hs) + 1, cols - 2);
+    if (i1 >= i0 && j1 >= j0) {
+      w = j1 - j0 + 1;
+      cnt = (i1 - i0 + 1) * w;
+      if (i1 + 1 - i0 < MESH_BLOCK && j1 + 1 - j0 < MESH_BLOCK) {  // <= 2 blocks a side: the corners see them all
+        const float hb = fmaxf(fmaxf(mesh_block_bound(mesh[(size_t)i0 * cols + j0]),
+                                     mesh_block_bound(mesh[(size_t)i0 * cols + j1 + 1])),
+                               fmaxf(mesh_block_bound(mesh[(size_t)(i1 + 1) * cols + j0]),
+                                     mesh_block_bound(mesh[(size_t)(i1 + 1) * cols + j1 + 1])));
+        if (hb < 1.0e38f && p.z - r - Pm->contact_margin > hb * vs + 1e-4f) cnt = 0;
+      }
+    }
+  }
+  // inclusive prefix of the task counts over lanes
+  int endp = cnt;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int v = __shfl_up(endp, d, 64);
+    if (lane >= d) endp += v;
+  }
+  const int total = __shfl(endp, 63, 64);
+  int* const T_end = reinterpret_cast<int*>(lgx_dyn);
+  int* const T_ci = T_end + 64;
+  int* const T_cj = T_end + 128;
+  int* const T_i0 = T_end + 192;
+  int* const T_j0 = T_end + 256;
+  int* const T_w = T_end + 320;
+  float* const T_p = lgx_dyn + 384;        // [3][64]
+  float* const R_ = lgx_dyn + 576;         // results [8][64]: d2, q(3), fn(3), zs
+  T_end[lane] = endp; T_ci[lane] = ci; T_cj[lane] = cj; T_i0[lane] = i0; T_j0[lane] = j0; T_w[lane] = w;
+  T_p[lane] = p.x; T_p[64 + lane] = p.y; T_p[128 + lane] = p.z;
+  float best = 3.0e38f, zs = -3.0e38f;
+  f3 q = mk(0.f, 0.f, -3.0e38f), fn = mk(0.f, 0.f, 1.f);
+  const int mystart = endp - cnt;
+  for (int base = 0; base < total; base += 64) {
+    __syncthreads();  // the tables (first round) / the previous round's results are read
+    const int t = base + lane;
+    float td2 = 3.0e38f, tz = -3.0e38f;
+    f3 tq = mk(0.f, 0.f, -3.0e38f), tfn = mk(0.f, 0.f, 1.f);
+    if (t < total) {
+      int lo = 0, hi = 63;  // owner: the first lane whose inclusive end exceeds t
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (T_end[mid] > t) hi = mid; else lo = mid + 1;
+      }
+      const int c = lo;
+      const int k = t - (c ? T_end[c - 1] : 0);  // task index within candidate c
+      const int wc = T_w[c];
+      const int i = T_i0[c] + k / wc, j = T_j0[c] + k % wc;
+      const int cci = T_ci[c], ccj = T_cj[c];
+      const f3 pc = mk(T_p[c], T_p[64 + c], T_p[128 + c]);
+      const f3 v00 = mesh_vertex(mesh, cols, i, j, cci, ccj, hs, vs);
+      const f3 v01 = mesh_vertex(mesh, cols, i, j + 1, cci, ccj, hs, vs);
+      const f3 v10 = mesh_vertex(mesh, cols, i + 1, j, cci, ccj, hs, vs);
+      const f3 v11 = mesh_vertex(mesh, cols, i + 1, j + 1, cci, ccj, hs, vs);
+#pragma unroll
+      for (int tri = 0; tri < 2; ++tri) {
+        const f3 a = v00, b = tri == 0 ? v11 : v10, cc = tri == 0 ? v01 : v11;
+        const f3 cpt = closest_on_triangle(pc, a, b, cc);
+        const f3 dd = pc - cpt;
+        const float d2 = dot(dd, dd);
+        if (d2 < td2) { td2 = d2; tq = cpt; tfn = cross(b - a, cc - a); }
+        float z;
+        if (height_in_triangle(pc, a, b, cc, z)) tz = fmaxf(tz, z);
+      }
+    }
+    R_[lane] = td2;
+    R_[64 + lane] = tq.x; R_[128 + lane] = tq.y; R_[192 + lane] = tq.z;
+    R_[256 + lane] = tfn.x; R_[320 + lane] = tfn.y; R_[384 + lane] = tfn.z;
+    R_[448 + lane] = tz;
+    __syncthreads();
+    if (cnt > 0) {  // this candidate's tasks of the round, in order
+      const int a0 = max(mystart, base) - base, a1 = min(endp, base + 64) - base;
+      for (int sl = a0; sl < a1; ++sl) {
+        const float d2 = R_[sl];
+        if (d2 < best) {
+          best = d2;
+          q = mk(R_[64 + sl], R_[128 + sl], R_[192 + sl]);
+          fn = mk(R_[256 + sl], R_[320 + sl], R_[384 + sl]);
+        }
+        zs = fmaxf(zs, R_[448 + sl]);
+      }
+    }
+  }
+  __syncthreads();  // the arena is the constraint rows' next
+  TerrainHit h;
+  if (best >= 3.0e38f) {  // culled, outside the field, or no candidate: nothing to touch
+    h.depth = -3.0e38f;
+    h.n = mk(0.f, 0.f, 1.f);
+    return h;
+  }
+  const float dist = sqrtf(best);
+  const bool below = p.z < zs;
+  h.depth = below ? r + dist : r - dist;
+  if (dist > 1e-6f) {
+    h.n = (p - q) * ((below ? -1.0f : 1.0f) / dist);
+  } else {
+    h.n = fn * rsqrtf(fmaxf(dot(fn, fn), 1e-30f));
+  }
+  return h;
+}
+
 // tangent pair of a contact normal; (0,0,1) -> (1,0,0), (0,1,0) like the plane rows
 LGX_DEV void contact_tangents(f3 n, f3& t1, f3& t2) {
   f3 a = mk(n.z, 0.f, -n.x);  // e_y x n
@@ -840,20 +971,36 @@ LGX_DEV void substep(Sh& s, const lgx_model* M_, const lgx_task_params* Pm_, con
   float depth = 0.f;
   int ck = 0;
   constexpr bool plane = !TERRAIN;  // the launch picks the variant from mesh_type
-  if (lane < M->num_candidates) {
-    ck = M->cand_link[lane];
-    xc = ld3(s.P[ck]) + mv(s.R[ck], ld3(M->cand_pos[lane]));
-    const float r = M->cand_radius[lane];
-    if constexpr (plane) {
+  if constexpr (plane) {
+    if (lane < M->num_candidates) {
+      ck = M->cand_link[lane];
+      xc = ld3(s.P[ck]) + mv(s.R[ck], ld3(M->cand_pos[lane]));
+      const float r = M->cand_radius[lane];
       depth = r - xc.z;
       xc.z -= r;
-    } else {
-      const TerrainHit th = terrain_contact(Pm, B, xc, r);
+      act = depth > -Pm->contact_margin;
+    }
+  } else {
+    const bool cand = lane < M->num_candidates;
+    float r = 0.f;
+    if (cand) {
+      ck = M->cand_link[lane];
+      xc = ld3(s.P[ck]) + mv(s.R[ck], ld3(M->cand_pos[lane]));
+      r = M->cand_radius[lane];
+    }
+#ifdef LGX_TERRAIN_PER_LANE  // (the one-candidate-per-lane query, for A/B)
+    TerrainHit th;
+    th.depth = -3.0e38f;
+    if (cand) th = terrain_contact(Pm, B, xc, r);
+#else
+    const TerrainHit th = terrain_contact_wave(Pm, B, xc, r, cand, lane);
+#endif
+    if (cand) {
       depth = th.depth;
       nrm = th.n;
       xc = xc - nrm * r;  // deepest sphere point
+      act = depth > -Pm->contact_margin;
     }
-    act = depth > -Pm->contact_margin;
   }
   uint64_t cmask = __ballot(act);
   uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));

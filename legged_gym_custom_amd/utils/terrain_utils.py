@@ -305,4 +305,23 @@ def pack_mesh(height_field_raw, horizontal_scale, vertical_scale, slope_threshol
         dx, dy = slope_moves(hf, slope_threshold * (horizontal_scale / vertical_scale))
     word |= (dx + 1).astype(np.uint32) << np.uint32(16)
     word |= (dy + 1).astype(np.uint32) << np.uint32(18)
-    return word
+    return word | mesh_block_bits(hf)
+
+
+MESH_BLOCK = 8  # lgx_env.hip MESH_BLOCK
+
+
+def mesh_block_bits(hf, block=MESH_BLOCK):
+    """Bits 20-31 of every mesh word: a conservative maximum height of the vertex's 8 x 8 block
+    (bits 20-30: q = ceil((max + 32768) / 32), decoded as 32 q - 32768 >= max; bit 31: present —
+    absent when q would not fit 11 bits). The kernel's contact query skips spheres above every
+    vertex their cell range can reach (lgx_env.hip terrain_contact_wave)."""
+    h = hf.astype(np.int64)
+    R, C = h.shape
+    pr, pc = -R % block, -C % block
+    hp = np.pad(h, ((0, pr), (0, pc)), constant_values=np.iinfo(np.int16).min)
+    bm = hp.reshape((R + pr) // block, block, (C + pc) // block, block).max(axis=(1, 3))
+    q = -((-(bm + 32768)) // 32)  # ceil
+    ok = q <= 2047
+    bits = np.where(ok, (q.clip(0, 2047).astype(np.uint32) << np.uint32(20)) | np.uint32(1 << 31), np.uint32(0))
+    return np.repeat(np.repeat(bits, block, axis=0), block, axis=1)[:R, :C].astype(np.uint32)
