@@ -68,7 +68,10 @@ def scan_trace_height():
     return 0.3 + float(np.median(first))
 
 
-def rollout(run="parkour_v12_ft_iii", n=64, steps=1000, vx=1.0, seed=3):
+def rollout(run="parkour_v12_ft_iii", n=64, steps=1000, vx=1.0, seed=3, est_source="net", period=None):
+    """est_source: "net" (the shipped estimator.pt, as deploy_base.py:248-264) or "true" (the
+    env's true estimated observation, v_body * lin_vel scale — what a trained estimator
+    approximates: PPO.update trains it toward exactly that, ppo.py:224-231)."""
     import driver
     from legged_gym_custom_amd.envs import task_registry_configs
     from legged_gym_custom_amd import model as mdl, params as prm
@@ -81,6 +84,8 @@ def rollout(run="parkour_v12_ft_iii", n=64, steps=1000, vx=1.0, seed=3):
     cfg.noise.add_noise = False
     cfg.domain_rand.push_robots = False
     cfg.commands.user_command = [vx, 0.0, 0.0, 0.0]
+    if period is not None:  # gait clock (the deploy config's is 0.35 s, deploy/configs/go2.yaml:21)
+        cfg.env.period = period
     cfg.env.num_envs = n
     m = mdl.load_model(cfg.asset.file, cfg.asset.foot_name)
     P = prm.build_task_params(cfg, m, n, go2=True)
@@ -100,7 +105,8 @@ def rollout(run="parkour_v12_ft_iii", n=64, steps=1000, vx=1.0, seed=3):
         for k in range(steps):
             obs = torch.from_numpy(a["obs"].copy())
             hist = obs[:, :H * Pp].reshape(n, H, Pp)
-            e = est(obs)
+            e_net = est(obs)
+            e = e_net if est_source == "net" else torch.from_numpy(a["est"].copy())
             parts = [obs, ad(hist)] + ([scan(torch.from_numpy(a["scan"].copy()))] if scan is not None else []) + [e]
             x = torch.cat(parts, dim=-1)
             a["actions_in"][:] = pol(x).numpy()
@@ -109,7 +115,7 @@ def rollout(run="parkour_v12_ft_iii", n=64, steps=1000, vx=1.0, seed=3):
             if k >= 100:  # after the start transient
                 z.append(a["root_states"][:, 2].copy())
                 vxs.append(a["base_lin_vel"][:, 0].copy())
-                vest.append(e[:, 0].numpy() / cfg.normalization.obs_scales.lin_vel)
+                vest.append(e_net[:, 0].numpy() / cfg.normalization.obs_scales.lin_vel)
                 contact.append(a["contact_forces"][:, feet, 2] > 1.0)
                 phase.append(a["rpy_phase"][:, 3:7].copy())  # fl fr bl br, [0, 1)
     z, vxs, vest, contact, phase = map(np.array, (z, vxs, vest, contact, phase))
@@ -118,7 +124,7 @@ def rollout(run="parkour_v12_ft_iii", n=64, steps=1000, vx=1.0, seed=3):
     thr = 2.0 * cfg.rewards.percent_time_on_ground - 1.0
     stance = np.sin(2 * np.pi * phase) <= thr
     return {
-        "run": run, "task_settings": task, "envs": n, "steps": steps, "command_vx": vx,
+        "run": run, "estimator_input": est_source, "task_settings": task, "gait_period": cfg.env.period, "envs": n, "steps": steps, "command_vx": vx,
         "survival": float(alive.mean()),
         "base_height_mean": float(z[:, alive].mean()), "base_height_std": float(z[:, alive].std()),
         "scan_trace_height": scan_trace_height(),
@@ -132,7 +138,14 @@ def rollout(run="parkour_v12_ft_iii", n=64, steps=1000, vx=1.0, seed=3):
 
 if __name__ == "__main__":
     args = sys.argv[1:]
+    est_source = "true" if "--true-est" in args else "net"
+    period = None
+    if "--period" in args:
+        i = args.index("--period")
+        period = float(args[i + 1])
+        del args[i:i + 2]
+    args = [x for x in args if x != "--true-est"]
     res = rollout(args[0] if args else "parkour_v12_ft_iii", *(int(v) for v in args[1:3]),
-                  *(float(v) for v in args[3:4]))
+                  *(float(v) for v in args[3:4]), est_source=est_source, period=period)
     for k, v in res.items():
         print(f"{k:28s} {v}")
