@@ -1327,23 +1327,20 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(CopyBatch cb, const in
   }
 }
 
-// Standard normal of action j of global env `gid` at env step `step` (eps == NULL mode):
-// Philox4x32-10 with the env's counter layout on stream LGX_ACT_NOISE_STREAM, block j / 4;
-// its 4 uniforms make 2 Box-Muller pairs, action j takes cos (even j) or sin (odd j) of
-// pair (j / 2) % 2. oracle/philox.py act_noise states the same.
-__device__ __forceinline__ float act_noise(uint64_t seed, uint32_t gid, uint64_t step, int j) {
-  uint32_t o[4];
-  philox4x32_10(gid, (uint32_t)step, (uint32_t)(j >> 2) | ((uint32_t)LGX_ACT_NOISE_STREAM << 16),
-                (uint32_t)(step >> 32), (uint32_t)seed, (uint32_t)(seed >> 32), o);
-  const int p = j & 2;
-  const float u1 = 1.0f - u01(o[p]);  // (0, 1]
-  const float u2 = u01(o[p + 1]);
-  const float r = sqrtf(-2.0f * logf(u1));
-  const float th = 6.28318530717958647692f * u2;
-  return (j & 1) ? r * sinf(th) : r * cosf(th);
-}
-
+// eps == NULL: the standard normal of action j of global env `gid` at env step `step` is
+// Philox4x32-10 with the env's counter layout on stream LGX_ACT_NOISE_STREAM, block j / 4; its
+// 4 uniforms make 2 Box-Muller pairs (u1 = 1 - u[2q], u2 = u[2q + 1], r = sqrt(-2 log u1),
+// theta = 2 pi u2), action j takes r cos theta (even j) or r sin theta (odd j) of pair
+// (j / 2) % 2. oracle/philox.py act_noise states the same.
 __global__ __launch_bounds__(256) void act_head_kernel(lgx_act_head_args p) {
+  // std and log std once per block; the noise of 4 actions from one Philox call (act_noise's
+  // definition: 2 Box-Muller pairs per block of 4), not one call per action
+  __shared__ float s_sd[HMAXA], s_lsd[HMAXA];
+  if ((int)threadIdx.x < p.A) {
+    s_sd[threadIdx.x] = p.std[threadIdx.x];
+    s_lsd[threadIdx.x] = logf(p.std[threadIdx.x]);
+  }
+  __syncthreads();
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= p.B) return;
   const float c = 0.91893853320467274178f;  // log(sqrt(2 pi))
@@ -1351,17 +1348,39 @@ __global__ __launch_bounds__(256) void act_head_kernel(lgx_act_head_args p) {
   const uint64_t step = draw ? (uint64_t)*p.step_dev : 0;
   const uint32_t gid = (uint32_t)(p.env_offset + i);
   float lp = 0.0f;
-  for (int j = 0; j < p.A; ++j) {
-    const size_t k = (size_t)i * p.A + j;
-    const float m = p.mean[k], sd = p.std[j];
-    const float e = draw ? act_noise(p.seed, gid, step, j) : p.eps[k];
-    const float a = m + sd * e;
-    const float d = a - m;
-    lp += -(d * d) / (2.0f * (sd * sd)) - logf(sd) - c;
-    p.actions[k] = a;
-    if (p.actions_copy) p.actions_copy[k] = a;
-    p.mu[k] = m;
-    p.sigma[k] = sd;
+  for (int b = 0; b * 4 < p.A; ++b) {
+    float e4[4];
+    if (draw) {
+      uint32_t o[4];
+      philox4x32_10(gid, (uint32_t)step, (uint32_t)b | ((uint32_t)LGX_ACT_NOISE_STREAM << 16), (uint32_t)(step >> 32),
+                    (uint32_t)p.seed, (uint32_t)(p.seed >> 32), o);
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const float u1 = 1.0f - u01(o[2 * q]);
+        const float u2 = u01(o[2 * q + 1]);
+        const float r = sqrtf(-2.0f * logf(u1));
+        const float th = 6.28318530717958647692f * u2;
+        e4[2 * q] = r * cosf(th);
+        e4[2 * q + 1] = r * sinf(th);
+      }
+    } else {
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) e4[jj] = 4 * b + jj < p.A ? p.eps[(size_t)i * p.A + 4 * b + jj] : 0.f;
+    }
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int j = 4 * b + jj;
+      if (j >= p.A) break;
+      const size_t k = (size_t)i * p.A + j;
+      const float m = p.mean[k], sd = s_sd[j];
+      const float a = m + sd * e4[jj];
+      const float d = a - m;
+      lp += -(d * d) / (2.0f * (sd * sd)) - s_lsd[j] - c;
+      p.actions[k] = a;
+      if (p.actions_copy) p.actions_copy[k] = a;
+      p.mu[k] = m;
+      p.sigma[k] = sd;
+    }
   }
   p.logp[i] = lp;
 }
@@ -1854,7 +1873,8 @@ int32_t lgx_gather_rows(const lgx_copy_desc* descs, int32_t n, const int64_t* id
 }
 
 int32_t lgx_act_head(const lgx_act_head_args* a, void* stream) {
-  if (!a || !a->mean || !a->std || !a->actions || !a->mu || !a->sigma || !a->logp || a->B < 0 || a->A <= 0)
+  if (!a || !a->mean || !a->std || !a->actions || !a->mu || !a->sigma || !a->logp || a->B < 0 || a->A <= 0 ||
+      a->A > lgxm::HMAXA)
     return fail("lgx_act_head: bad arguments");
   if (!a->eps && (!a->step_dev || a->env_offset < 0 || a->env_offset + a->B > (int64_t)UINT32_MAX))
     return fail("lgx_act_head: eps == NULL needs step_dev and a 32-bit global env range");
