@@ -316,18 +316,26 @@ __device__ __forceinline__ void gemm_tile(const Params& p, const int L) {
       const bf16x8 al = *reinterpret_cast<const bf16x8*>(alo + off);
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
+#ifdef LGX_EXP_NOMFMA  // experiment (timing only): fragments read, no MFMA
+        acc[i][j][0] += (float)al[0] + (float)bh[j][0] + (float)ah[1] + (float)bl[j][1];
+#else
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh[j], acc[i][j], 0, 0, 0);
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl[j], acc[i][j], 0, 0, 0);
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh[j], acc[i][j], 0, 0, 0);
+#endif
       }
     }
+#ifndef LGX_EXP_NOSTORE  // experiment (timing only): no staging split / LDS stores in the loop
     if (st) sstore(va, vb, nbuf);
+#endif
   };
   // step s: MFMAs on LDS[s&1] with step s+1 (registers loaded two steps ago) staged into
   // LDS[(s+1)&1]; refill those registers with step s+3; one barrier.
   auto step = [&](int s, float (&ra)[SA::R], float (&rb)[SB::R]) {
     compute(s & 1, s + 1 < nsteps, (s + 1) & 1, ra, rb);
+#ifndef LGX_EXP_NOLOAD  // experiment (timing only): no global loads in the loop
     if (s + 1 + PF < nsteps) gload(ra, rb, kbeg + (s + 1 + PF) * BKS);
+#endif
     __syncthreads();
   };
 

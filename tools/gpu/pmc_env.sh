@@ -4,7 +4,7 @@
 set -o pipefail
 TAG=${1:-r02}
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/pmc_env_$TAG
+O=$R/gpurun_out/pmc_env_${TAG}_${TASK:-go2}
 rm -rf $O; mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
 i=0

@@ -11,6 +11,11 @@ import sys
 
 src, tag = sys.argv[1], sys.argv[2]
 CALIB_BYTES = 512 << 20
+TASK = os.environ.get("TASK", "go2")
+N = int(os.environ.get("N", "4096"))
+# bench.py reads the newest <round>_env_kernel_pmc.txt / <round>_env_traffic.json (the Go2 bench
+# workload); the other tasks' files carry the task name so they never match those globs
+STEM = f"{tag}_env" if TASK == "go2" else f"{tag}_env_{TASK}"
 
 
 def counters(sub, match):
@@ -38,21 +43,21 @@ for sub, ctr in (("c1", "FETCH_SIZE"), ("c2", "WRITE_SIZE")):
         vals, _, _ = counters(sub, kern)
         if ctr in vals:
             cal[f"{kern.strip('(')}:{ctr}"] = vals[ctr] * 1024 / CALIB_BYTES
-lines = [f"# rocprofv3 --pmc passes over tools/env_kernel_driver.py (Go2 flat, 4096 envs): per-launch means; kernel {kname}",
+lines = [f"# rocprofv3 --pmc passes over tools/env_kernel_driver.py ({TASK}, {N} envs): per-launch means; kernel {kname}",
          "# (SQ_* cycle counters in quad-cycles). Calibration (tools/calib/hbm_calib, 512 MiB, counter bytes / true bytes):"]
 lines += [f"#   {k:28s} {v:.3f}" for k, v in sorted(cal.items())]
 for k in sorted(env):
     lines.append(f"   {k:36s} {env[k]:16.0f}")
 if "SQ_WAVE_CYCLES" in env:
     lines.append(f"   wait fraction SQ_WAIT_ANY/SQ_WAVE_CYCLES = {env.get('SQ_WAIT_ANY', 0) / env['SQ_WAVE_CYCLES']:.3f}")
-    lines.append(f"   VALU instructions per env step = {env.get('SQ_INSTS_VALU', 0) / 4096:.0f}, SALU {env.get('SQ_INSTS_SALU', 0) / 4096:.0f}, LDS {env.get('SQ_INSTS_LDS', 0) / 4096:.0f}")
+    lines.append(f"   VALU instructions per env step = {env.get('SQ_INSTS_VALU', 0) / N:.0f}, SALU {env.get('SQ_INSTS_SALU', 0) / N:.0f}, LDS {env.get('SQ_INSTS_LDS', 0) / N:.0f}")
 txt = "\n".join(lines)
-open(os.path.join(src, f"{tag}_env_kernel_pmc.txt"), "w").write(txt + "\n")
+open(os.path.join(src, f"{STEM}_kernel_pmc.txt"), "w").write(txt + "\n")
 print(txt)
 fr = cal.get("read_dword:FETCH_SIZE")
 wr = cal.get("write_dword:WRITE_SIZE")
 if "FETCH_SIZE" in env and "WRITE_SIZE" in env and fr and wr:
-    res = {"kernel": kname, "workload": "go2 flat, 4096 envs, actions N(0,1) clipped (tools/env_kernel_driver.py)",
+    res = {"kernel": kname, "workload": f"{TASK}, {N} envs, actions N(0,1) clipped (tools/env_kernel_driver.py)",
            "FETCH_SIZE_KiB_raw": env["FETCH_SIZE"], "WRITE_SIZE_KiB_raw": env["WRITE_SIZE"],
            "calibration": {"dword_read_fetch_ratio": fr, "dword_write_ratio": wr,
                            "dwordx4_read_fetch_ratio": cal.get("read_dwordx4:FETCH_SIZE")},
@@ -60,5 +65,5 @@ if "FETCH_SIZE" in env and "WRITE_SIZE" in env and fr and wr:
     res["traffic_bytes_per_launch"] = res["fetch_bytes_corrected"] + res["write_bytes"]
     res["correction"] = ("counter KiB -> bytes, divided by the counter/true ratio measured on dword-per-lane "
                          "coalesced reads and writes of a 512 MiB buffer (tools/calib/hbm_calib.hip)")
-    json.dump(res, open(os.path.join(src, f"{tag}_env_traffic.json"), "w"), indent=1)
+    json.dump(res, open(os.path.join(src, f"{STEM}_traffic.json"), "w"), indent=1)
     print(json.dumps(res, indent=1))
