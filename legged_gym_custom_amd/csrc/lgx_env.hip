@@ -165,14 +165,6 @@ LGX_DEV const T* opaque(const T* p) {
   return p;
 }
 
-// the same, ordered after `dep` is computed: loads through the result cannot be issued before
-// the work that produces `dep` (bounds how many weights are live at once)
-template <class T>
-LGX_DEV const T* opaque_after(const T* p, float dep) {
-  __asm__ volatile("" : "+s"(p) : "v"(dep));
-  return p;
-}
-
 LGX_DEV int opaque_lane(int v) {
   __asm__ volatile("" : "+v"(v));
   return v;
@@ -814,36 +806,10 @@ template <int K>
 LGX_DEV float unit_of(float v) {  // unit K of this lane's 8-lane group
   return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), 0x18 | (K << 5)));
 }
-LGX_DEV void unit_vec(float v, float (&o)[8]) {
-  o[0] = unit_of<0>(v); o[1] = unit_of<1>(v); o[2] = unit_of<2>(v); o[3] = unit_of<3>(v);
-  o[4] = unit_of<4>(v); o[5] = unit_of<5>(v); o[6] = unit_of<6>(v); o[7] = unit_of<7>(v);
-}
-// one LSTM cell step for unit u: returns (h, c) in place; xin: the layer input (NIN values, the
-// same for the 8 lanes of a joint), hall: the layer's old h of all 8 units
-template <int NIN>
-LGX_DEV void sea_unit(const float* __restrict__ w_ih, const float* __restrict__ w_hh, const float* __restrict__ b_ih,
-                      const float* __restrict__ b_hh, int u, const float* xin, const float (&hall)[8], float& h,
-                      float& c) {
-  float g4[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int g = q * 8 + u;
-    float a = 0.0f, b = 0.0f;
-#pragma unroll
-    for (int k = 0; k < NIN; ++k) a += w_ih[g * NIN + k] * xin[k];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) b += w_hh[g * 8 + k] * hall[k];
-    g4[q] = (a + b_ih[g]) + (b + b_hh[g]);
-    __builtin_amdgcn_sched_barrier(0);  // one gate row's weights live at a time (VGPR budget)
-  }
-  const float ig = sigmoidf_(g4[0]), fg = sigmoidf_(g4[1]), gg = tanhf(g4[2]), og = sigmoidf_(g4[3]);
-  c = fg * c + ig * gg;
-  h = og * tanhf(c);
-}
-// The same cell step with the k loop outermost: the other units' values are taken by ds_swizzle
+// One LSTM cell step for unit u with the k loop outermost: the other units' values are taken by ds_swizzle
 // as each k is consumed and the four gates accumulate side by side, so neither an 8-value copy of
 // the units (hall / the layer-1 input) nor a gate row of weights is ever live at once. Every sum
-// keeps sea_unit's order (a and b each accumulate k = 0..NIN-1 / 0..7, then (a + b_ih) + (b + b_hh)).
+// keeps sea_lstm_layer's order (a and b each accumulate k = 0..NIN-1 / 0..7, then (a + b_ih) + (b + b_hh)).
 // XSW: the layer input is the new layer-0 h of the group's units (swizzled from xs) instead of xin.
 template <int NIN, bool XSW>
 LGX_DEV void sea_unit_k(const float* __restrict__ w_ih, const float* __restrict__ w_hh,
@@ -885,116 +851,9 @@ LGX_DEV void sea_unit_k(const float* __restrict__ w_ih, const float* __restrict_
   c = fg * c + ig * gg;
   h = og * tanhf(c);
 }
-// Two units per lane, all 12 joints in one pass: lane L serves joint L >> 2 (lanes 0..47) and units
-// p = L & 3 (lo) and p + 4 (hi); a joint's units are exchanged by ds_swizzle inside its 4-lane group.
-// Against one unit per lane in two passes: the same instructions, half the swizzles, and two
-// independent cells per lane instead of two passes one after the other. Same sums, same order.
-template <int K>
-LGX_DEV float quad_of(float v) {  // lane K of this lane's 4-lane group
-  return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), 0x1C | (K << 5)));
-}
-template <int K>
-LGX_DEV float unit2(float lo, float hi) {  // unit K of the joint
-  return K < 4 ? quad_of<K & 3>(lo) : quad_of<K & 3>(hi);
-}
-#define LGX_UNIT2_CASES(v_lo, v_hi, k, out)                                        \
-  switch (k) {                                                                     \
-    case 0: out = unit2<0>(v_lo, v_hi); break; case 1: out = unit2<1>(v_lo, v_hi); break; \
-    case 2: out = unit2<2>(v_lo, v_hi); break; case 3: out = unit2<3>(v_lo, v_hi); break; \
-    case 4: out = unit2<4>(v_lo, v_hi); break; case 5: out = unit2<5>(v_lo, v_hi); break; \
-    case 6: out = unit2<6>(v_lo, v_hi); break; default: out = unit2<7>(v_lo, v_hi); break; \
-  }
-LGX_DEV void sea_cell(const float (&g)[4], float& h, float& c) {
-  const float ig = sigmoidf_(g[0]), fg = sigmoidf_(g[1]), gg = tanhf(g[2]), og = sigmoidf_(g[3]);
-  c = fg * c + ig * gg;
-  h = og * tanhf(c);
-}
-// units p and p + 4 of one layer; XSW: the layer input is the new layer-0 h (xs_lo / xs_hi).
-// The weights stream in groups of SEA_KG k's (8 * SEA_KG values): a group's loads are issued once
-// the previous group's first products are done (opaque_after), so about two groups are live at a
-// time instead of the compiler issuing all of a layer's ~100 weight loads up front and spilling.
-#ifndef SEA_KG
-#define SEA_KG 1
-#endif
-template <int NIN, bool XSW>
-LGX_DEV void sea_pair_k(const float* __restrict__ w_ih, const float* __restrict__ w_hh,
-                        const float* __restrict__ b_ih, const float* __restrict__ b_hh, int p, const float* xin,
-                        float xs_lo, float xs_hi, float hold_lo, float hold_hi, float& h_lo, float& c_lo,
-                        float& h_hi, float& c_hi) {
-  float a0[4] = {0.0f, 0.0f, 0.0f, 0.0f}, a1[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-  float b0[4] = {0.0f, 0.0f, 0.0f, 0.0f}, b1[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-  const float* wi = w_ih;
-  float dep = hold_lo;  // the last group's first product (orders the next group's loads)
-#pragma unroll
-  for (int k = 0; k < NIN; ++k) {
-    if (k % SEA_KG == 0) wi = opaque_after(w_ih, dep);
-    float xk;
-    if constexpr (XSW) {
-      LGX_UNIT2_CASES(xs_lo, xs_hi, k, xk)
-    } else {
-      xk = xin[k];
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      a0[q] += wi[(q * 8 + p) * NIN + k] * xk;
-      a1[q] += wi[(q * 8 + p + 4) * NIN + k] * xk;
-    }
-    if (k % SEA_KG == 0) dep = a0[0];
-  }
-  const float* wh = w_hh;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    if (k % SEA_KG == 0) wh = opaque_after(w_hh, dep);
-    float hk;
-    LGX_UNIT2_CASES(hold_lo, hold_hi, k, hk)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      b0[q] += wh[(q * 8 + p) * 8 + k] * hk;
-      b1[q] += wh[(q * 8 + p + 4) * 8 + k] * hk;
-    }
-    if (k % SEA_KG == 0) dep = b0[0];
-  }
-  const float* bi = opaque_after(b_ih, dep);
-  const float* bh = opaque_after(b_hh, dep);
-  float g0[4], g1[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    g0[q] = (a0[q] + bi[q * 8 + p]) + (b0[q] + bh[q * 8 + p]);
-    g1[q] = (a1[q] + bi[q * 8 + p + 4]) + (b1[q] + bh[q * 8 + p + 4]);
-  }
-  sea_cell(g0, h_lo, c_lo);
-  sea_cell(g1, h_hi, c_hi);
-}
-LGX_DEV void sea_torques_pairs(Sh& s, const lgx_task_params* Pm, const lgx_buffers& B, int e, int lane) {
-  const size_t NT = (size_t)Pm->num_envs * Pm->num_dof;
-  const int p = lane & 3, j = lane >> 2;
-  const bool on = j < NJ;  // lanes 48..63 follow along on joint 11
-  const int jj = on ? j : NJ - 1;
-  const size_t r = (size_t)e * Pm->num_dof + jj;
-  const size_t i0 = r * 8 + p, i1 = (NT + r) * 8 + p;  // layer 0 / layer 1 state of unit p
-  float h0l = B.sea_hidden[i0], h0h = B.sea_hidden[i0 + 4], c0l = B.sea_cell[i0], c0h = B.sea_cell[i0 + 4];
-  float h1l = B.sea_hidden[i1], h1h = B.sea_hidden[i1 + 4], c1l = B.sea_cell[i1], c1h = B.sea_cell[i1 + 4];
-  const float in0 = (s.act[jj] * Pm->action_scale + Pm->default_dof_pos[jj]) - s.th[jj];
-  const float x[2] = {in0 * Pm->sea_in_scale[0], s.thd[jj] * Pm->sea_in_scale[1]};
-  sea_pair_k<2, false>(Pm->sea_w_ih0, Pm->sea_w_hh0, Pm->sea_b_ih0, Pm->sea_b_hh0, p, x, 0.0f, 0.0f, h0l, h0h, h0l,
-                       c0l, h0h, c0h);
-  sea_pair_k<8, true>(Pm->sea_w_ih1, Pm->sea_w_hh1, Pm->sea_b_ih1, Pm->sea_b_hh1, p, nullptr, h0l, h0h, h1l, h1h,
-                      h1l, c1l, h1h, c1h);
-  if (on) {
-    B.sea_hidden[i0] = h0l; B.sea_hidden[i0 + 4] = h0h; B.sea_cell[i0] = c0l; B.sea_cell[i0 + 4] = c0h;
-    B.sea_hidden[i1] = h1l; B.sea_hidden[i1 + 4] = h1h; B.sea_cell[i1] = c1l; B.sea_cell[i1 + 4] = c1h;
-  }
-  float y = 0.0f;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    float hk;
-    LGX_UNIT2_CASES(h1l, h1h, k, hk)
-    y += Pm->sea_lin_w[k] * hk;
-  }
-  if (on && p == 0) s.tau[j] = Pm->sea_out_scale * (y + Pm->sea_lin_b);
-}
 // all 12 joints' SEA torques into s.tau (every lane of the wave takes part), one unit per lane
-// over two passes (the kernel's form; the pair form above for A/B: -DLGX_SEA_PAIRS)
+// over two passes. (Two units per lane in one pass measured 425-459 us vs 433 for C3's kernel,
+// with 33-38 spilled VGPRs: not kept, profiles/r03_sea_spill_fix.txt.)
 #ifndef LGX_SEA_CALL
 // inlined (54 VGPRs spill at the 4-waves-per-SIMD budget, yet C3's kernel is 589 us against 611
 // as a call and 642 one joint per lane: profiles/r03_bench_anymal_c_rough_sea_waves.txt)
@@ -1066,8 +925,6 @@ LGX_DEV void substep(Sh& s, const lgx_model* M_, const lgx_task_params* Pm_, con
         s.tau[j] = sea_torque(Pm, B, blockIdx.x, j, (s.act[j] * Pm->action_scale + Pm->default_dof_pos[j]) - s.th[j],
                               s.thd[j]);
       }
-#elif defined(LGX_SEA_PAIRS)
-      sea_torques_pairs(s, Pm, B, blockIdx.x, lane);
 #else
       sea_torques_lanes(s, Pm, B, blockIdx.x, lane);
 #endif
