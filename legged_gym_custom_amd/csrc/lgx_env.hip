@@ -165,6 +165,21 @@ LGX_DEV const T* opaque(const T* p) {
   return p;
 }
 
+// XCD-aware env order. The hardware deals consecutive blocks to the 8 XCDs in turn, and env e's
+// rows ([N,13] root state, [N,24] dof state, ...) share 128-B lines with env e +- 1's, so neighbouring
+// envs are given blocks of the same XCD (one L2 fetches the shared line once): XCD x = b % 8 runs
+// the contiguous env range [x*q + min(x, r), ...) of q + (x < r) envs (N = 8q + r) — a bijection
+// of [0, N). LGX_ENV_LINEAR: env = block (for A/B).
+LGX_DEV int env_of_block(int b, int n) {
+#ifdef LGX_ENV_LINEAR
+  (void)n;
+  return b;
+#else
+  const int q = n >> 3, r = n & 7, x = b & 7, j = b >> 3;
+  return x * q + min(x, r) + j;
+#endif
+}
+
 LGX_DEV int opaque_lane(int v) {
   __asm__ volatile("" : "+v"(v));
   return v;
@@ -922,11 +937,12 @@ LGX_DEV void substep(Sh& s, const lgx_model* M_, const lgx_task_params* Pm_, con
 #ifdef LGX_SEA_PER_JOINT  // (the one-joint-per-lane form, for A/B)
       if (lane < NJ) {
         const int j = lane;
-        s.tau[j] = sea_torque(Pm, B, blockIdx.x, j, (s.act[j] * Pm->action_scale + Pm->default_dof_pos[j]) - s.th[j],
+        s.tau[j] = sea_torque(Pm, B, env_of_block(blockIdx.x, gridDim.x), j,
+                              (s.act[j] * Pm->action_scale + Pm->default_dof_pos[j]) - s.th[j],
                               s.thd[j]);
       }
 #else
-      sea_torques_lanes(s, Pm, B, blockIdx.x, lane);
+      sea_torques_lanes(s, Pm, B, env_of_block(blockIdx.x, gridDim.x), lane);
 #endif
     } else if (lane < NJ) {
       const int j = lane;
@@ -1751,7 +1767,7 @@ __global__ __launch_bounds__(64, ACTNET ? LGX_SEA_WAVES : 4) void env_step_kerne
   const lgx_buffers& B = *Bp;
   // graph-replayable form: the step counter is read from device memory (lgx_step_dev)
   const uint64_t step = step_dev ? *step_dev : step_arg;
-  const int e = blockIdx.x;
+  const int e = env_of_block(blockIdx.x, gridDim.x);
   const int lane = threadIdx.x;
   const int D = Pm->num_dof, A = Pm->num_actions, NB = Pm->num_bodies;
   const uint32_t gid = (uint32_t)(Pm->env_id_offset + e);
