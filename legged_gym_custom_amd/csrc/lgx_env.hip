@@ -180,6 +180,10 @@ LGX_DEV int env_of_block(int b, int n) {
 #endif
 }
 
+#ifndef LGX_ROW_PRIO
+#define LGX_ROW_PRIO 9  // 0: no priority
+#endif
+
 LGX_DEV int opaque_lane(int v) {
   __asm__ volatile("" : "+v"(v));
   return v;
@@ -1053,6 +1057,15 @@ LGX_DEV void substep(Sh& s, const lgx_model* M_, const lgx_task_params* Pm_, con
   int crank = __popcll(cmask & below);
   int ncon = min(__popcll(cmask), MAXC);
   const int nrows = nlim + 3 * ncon;
+#if LGX_ROW_PRIO > 0
+  // Issue priority by constraint-system size (s_setprio 0..3 above 0 / t / 2t / 3t rows): a
+  // launch lasts as long as its slowest wave, and the waves with the largest systems are the
+  // slow ones; the SIMD's other waves have the slack (profiles/r03_wave_priority.txt).
+  if (nrows > LGX_ROW_PRIO * 3) __builtin_amdgcn_s_setprio(3);
+  else if (nrows > LGX_ROW_PRIO * 2) __builtin_amdgcn_s_setprio(2);
+  else if (nrows > LGX_ROW_PRIO) __builtin_amdgcn_s_setprio(1);
+  else __builtin_amdgcn_s_setprio(0);
+#endif
   auto target = [&](float d) {
     float tv;
     if (d > Pm->slop) tv = fminf(Pm->baumgarte * (d - Pm->slop) / dt, Pm->max_depenetration_vel);
