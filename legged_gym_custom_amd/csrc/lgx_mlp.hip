@@ -1341,56 +1341,67 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(CopyBatch cb, const in
 // theta = 2 pi u2), action j takes r cos theta (even j) or r sin theta (odd j) of pair
 // (j / 2) % 2. oracle/philox.py act_noise states the same.
 __global__ __launch_bounds__(256) void act_head_kernel(lgx_act_head_args p) {
-  // std and log std once per block; the noise of 4 actions from one Philox call (act_noise's
-  // definition: 2 Box-Muller pairs per block of 4), not one call per action
+  // four lanes per row: lane q of a row's group handles actions 4q..4q+3 (one Philox call: the
+  // 2 Box-Muller pairs of act_noise's block q); lane 0 then sums the row's log-prob terms in
+  // action order (the same sum as one lane looping over the actions). std and log std once per block.
   __shared__ float s_sd[HMAXA], s_lsd[HMAXA];
   if ((int)threadIdx.x < p.A) {
     s_sd[threadIdx.x] = p.std[threadIdx.x];
     s_lsd[threadIdx.x] = logf(p.std[threadIdx.x]);
   }
   __syncthreads();
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= p.B) return;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int i = t >> 2, q = t & 3;  // row, block of 4 actions (B * 4 threads: whole groups)
+  const bool row = i < p.B, on = row && 4 * q < p.A;
   const float c = 0.91893853320467274178f;  // log(sqrt(2 pi))
-  const bool draw = p.eps == nullptr;
-  const uint64_t step = draw ? (uint64_t)*p.step_dev : 0;
-  const uint32_t gid = (uint32_t)(p.env_offset + i);
-  float lp = 0.0f;
-  for (int b = 0; b * 4 < p.A; ++b) {
+  float term[4] = {0.f, 0.f, 0.f, 0.f};
+  if (on) {
     float e4[4];
-    if (draw) {
+    if (p.eps == nullptr) {
+      const uint64_t step = (uint64_t)*p.step_dev;
+      const uint32_t gid = (uint32_t)(p.env_offset + i);
       uint32_t o[4];
-      philox4x32_10(gid, (uint32_t)step, (uint32_t)b | ((uint32_t)LGX_ACT_NOISE_STREAM << 16), (uint32_t)(step >> 32),
+      philox4x32_10(gid, (uint32_t)step, (uint32_t)q | ((uint32_t)LGX_ACT_NOISE_STREAM << 16), (uint32_t)(step >> 32),
                     (uint32_t)p.seed, (uint32_t)(p.seed >> 32), o);
 #pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const float u1 = 1.0f - u01(o[2 * q]);
-        const float u2 = u01(o[2 * q + 1]);
+      for (int h = 0; h < 2; ++h) {
+        const float u1 = 1.0f - u01(o[2 * h]);
+        const float u2 = u01(o[2 * h + 1]);
         const float r = sqrtf(-2.0f * logf(u1));
         const float th = 6.28318530717958647692f * u2;
-        e4[2 * q] = r * cosf(th);
-        e4[2 * q + 1] = r * sinf(th);
+        e4[2 * h] = r * cosf(th);
+        e4[2 * h + 1] = r * sinf(th);
       }
     } else {
 #pragma unroll
-      for (int jj = 0; jj < 4; ++jj) e4[jj] = 4 * b + jj < p.A ? p.eps[(size_t)i * p.A + 4 * b + jj] : 0.f;
+      for (int jj = 0; jj < 4; ++jj) e4[jj] = 4 * q + jj < p.A ? p.eps[(size_t)i * p.A + 4 * q + jj] : 0.f;
     }
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) {
-      const int j = 4 * b + jj;
+      const int j = 4 * q + jj;
       if (j >= p.A) break;
       const size_t k = (size_t)i * p.A + j;
       const float m = p.mean[k], sd = s_sd[j];
       const float a = m + sd * e4[jj];
       const float d = a - m;
-      lp += -(d * d) / (2.0f * (sd * sd)) - s_lsd[j] - c;
+      term[jj] = -(d * d) / (2.0f * (sd * sd)) - s_lsd[j] - c;
       p.actions[k] = a;
       if (p.actions_copy) p.actions_copy[k] = a;
       p.mu[k] = m;
       p.sigma[k] = sd;
     }
   }
-  p.logp[i] = lp;
+  // the row's terms to its lane 0, summed in action order
+  float all[HMAXA];
+#pragma unroll
+  for (int qq = 0; qq < 4; ++qq)
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) all[4 * qq + jj] = __shfl(term[jj], (threadIdx.x & ~3) + qq, 64);
+  if (row && q == 0) {
+    float lp = 0.0f;
+    for (int j = 0; j < p.A; ++j) lp += all[j];
+    p.logp[i] = lp;
+  }
 }
 
 __global__ __launch_bounds__(256) void transition_kernel(lgx_transition_args p) {
@@ -1887,8 +1898,8 @@ int32_t lgx_act_head(const lgx_act_head_args* a, void* stream) {
   if (!a->eps && (!a->step_dev || a->env_offset < 0 || a->env_offset + a->B > (int64_t)UINT32_MAX))
     return fail("lgx_act_head: eps == NULL needs step_dev and a 32-bit global env range");
   if (a->B == 0) return 0;
-  hipLaunchKernelGGL(lgxm::act_head_kernel, dim3((a->B + 255) / 256), dim3(256), 0, static_cast<hipStream_t>(stream),
-                     *a);
+  hipLaunchKernelGGL(lgxm::act_head_kernel, dim3((unsigned)((4 * (int64_t)a->B + 255) / 256)), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), *a);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : fail(hipGetErrorString(e));
 }

@@ -939,16 +939,20 @@ class _AdaptationFn(torch.autograd.Function):
             Hs = H
             x = _rowmajor(h.reshape(Bn * H, P))
         y0 = linear_forward(x, fc_w, fc_b, True)                         # [B, Hs, C1]
+        # each conv's output positions are independent GEMMs: one grouped launch per conv
+        # (bit-identical to launching them one by one)
         W1 = _conv_w(c1_w)
         y1 = torch.empty(Bn, L1, C2, device=dev)
-        for t in range(L1):
-            gemm_raw(y0.data_ptr() + 4 * t * s1 * C1, Hs * C1, 1, W1.data_ptr(), W1.stride(0), 1,
-                     y1.data_ptr() + 4 * t * C2, L1 * C2, Bn, C2, k1 * C1, EPI_BIAS | EPI_ELU, c1_b.data_ptr())
+        run_group([GemmArgs(A=y0.data_ptr() + 4 * t * s1 * C1, lda=Hs * C1, a_kcontig=1, B=W1.data_ptr(),
+                            ldb=W1.stride(0), b_kcontig=1, C=y1.data_ptr() + 4 * t * C2, ldc=L1 * C2, M=Bn, N=C2,
+                            K=k1 * C1, epilogue=EPI_BIAS | EPI_ELU, bias=c1_b.data_ptr(), split_k=1)
+                   for t in range(L1)])
         W2 = _conv_w(c2_w)
         y2 = torch.empty(Bn, L2, C3, device=dev)
-        for t in range(L2):
-            gemm_raw(y1.data_ptr() + 4 * t * s2 * C2, L1 * C2, 1, W2.data_ptr(), W2.stride(0), 1,
-                     y2.data_ptr() + 4 * t * C3, L2 * C3, Bn, C3, k2 * C2, EPI_BIAS | EPI_ELU, c2_b.data_ptr())
+        run_group([GemmArgs(A=y1.data_ptr() + 4 * t * s2 * C2, lda=L1 * C2, a_kcontig=1, B=W2.data_ptr(),
+                            ldb=W2.stride(0), b_kcontig=1, C=y2.data_ptr() + 4 * t * C3, ldc=L2 * C3, M=Bn, N=C3,
+                            K=k2 * C2, epilogue=EPI_BIAS | EPI_ELU, bias=c2_b.data_ptr(), split_k=1)
+                   for t in range(L2)])
         Wf = _final_w(f_w, C3, L2)
         out = linear_forward(y2.reshape(Bn, L2 * C3), Wf, f_b, True)
         ctx.dims = dims
