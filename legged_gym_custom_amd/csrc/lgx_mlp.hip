@@ -136,9 +136,9 @@ struct Stager {
     } else {  // MV / MVE
       const int kq = mv_kq(tid), rg = mv_rg(tid);
       const int k = k0 + kq * KG;
-      if (MODE == MV || row0 + ROWS <= rows) {
-        // MV: rows % 4 == 0 (host), so a 4-row group is all valid or all past the edge;
-        // MVE: an interior tile (a block-uniform branch)
+      if (MODE == MV) {
+        // rows % 4 == 0 (host), or an interior tile (interior_bits), so a 4-row group is
+        // all valid or all past the edge
         const int row = min(row0 + rg * 4, rows - 4);
 #pragma unroll
         for (int kk = 0; kk < KG; ++kk) {
@@ -266,24 +266,27 @@ __device__ __forceinline__ void gemm_tile(const Params& p, const int L) {
 
   float va[PF][SA::R], vb[PF][SB::R];  // PF register sets: loads run PF steps ahead
   float csum[4] = {0.f, 0.f, 0.f, 0.f};
-  auto gload = [&](float (&va)[SA::R], float (&vb)[SB::R], int k0) {
-#ifdef LGX_EXP_NO_KGUARD  // experiment: no guarded path compiled in (wrong for K % 32 != 0)
-    if (true) {
-#else
-    if (k0 + BKS <= kend) {
-#endif
-      SA::template load<false>(p.A, p.lda, m0, p.M, k0, kend, tid, va);
-      SB::template load<false>(p.B, p.ldb, n0, p.N, k0, kend, tid, vb);
-    } else {
-      SA::template load<true>(p.A, p.lda, m0, p.M, k0, kend, tid, va);
-      SB::template load<true>(p.B, p.ldb, n0, p.N, k0, kend, tid, vb);
-    }
+  // The chunk's full K steps run in a straight-line pipeline: their loads are unconditional
+  // (a prefetch past the last full step re-reads that step; it is staged into a buffer that is
+  // never computed) and unguarded, so hipcc's wait counting sees the same pending loads on
+  // every trip and waits only for the older register set (vmcnt(N)) before staging it. With
+  // the loads behind `if (step exists)` and guarded/unguarded branches (round 2-3), every
+  // staging drained ALL pending loads (vmcnt(0)): one step of latency hiding instead of PF.
+  // A partial last step (K chunk % 32 != 0) is loaded guarded (zero-filled k >= kend) and
+  // computed once after the loop — the same products in the same order.
+  const int nfull = kend > kbeg ? (kend - kbeg) / BKS : 0;
+  auto gloadU = [&](float (&va)[SA::R], float (&vb)[SB::R], int t) {
+    const int k0 = kbeg + min(t, nfull - 1) * BKS;
+    SA::template load<false>(p.A, p.lda, m0, p.M, k0, kend, tid, va);
+    SB::template load<false>(p.B, p.ldb, n0, p.N, k0, kend, tid, vb);
   };
-  auto sstore = [&](const float (&va)[SA::R], const float (&vb)[SB::R], int buf) {
+  auto sstore = [&](const float (&va)[SA::R], const float (&vb)[SB::R], int buf, bool cs_on) {
     __bf16* base = lds + buf * STAGE;
     SA::store(base, base + A_ELEMS, tid, va);
     SB::store(base + 2 * A_ELEMS, base + 2 * A_ELEMS + B_ELEMS, tid, vb);
-    if constexpr (COLSUM) SA::colsum(va, csum);
+    if constexpr (COLSUM) {
+      if (cs_on) SA::colsum(va, csum);
+    }
   };
 
   f32x4 acc[MI][NJ];
@@ -293,10 +296,10 @@ __device__ __forceinline__ void gemm_tile(const Params& p, const int L) {
     for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int fr = lane & 15, fc = lane >> 4;
-  // MFMAs of one K step on LDS[buf]; when `st`, the next step's registers (va, vb) are then
-  // split and stored into LDS[nbuf]. (Spreading those stores between the MFMA groups, with
-  // or without sched_group_barrier / s_setprio, measured the same: tools/gemm_variants.py.)
-  auto compute = [&](int buf, bool st, int nbuf, const float (&va)[SA::R], const float (&vb)[SB::R]) {
+  // MFMAs of one K step on LDS[buf]. (Spreading the next step's staging stores between the
+  // MFMA groups, with or without sched_group_barrier / s_setprio, measured the same:
+  // tools/gemm_variants.py.)
+  auto compute = [&](int buf) {
     const __bf16* base = lds + buf * STAGE;
     const __bf16* ahi = base;
     const __bf16* alo = base + A_ELEMS;
@@ -325,34 +328,46 @@ __device__ __forceinline__ void gemm_tile(const Params& p, const int L) {
 #endif
       }
     }
-#ifndef LGX_EXP_NOSTORE  // experiment (timing only): no staging split / LDS stores in the loop
-    if (st) sstore(va, vb, nbuf);
-#endif
   };
-  // step s: MFMAs on LDS[s&1] with step s+1 (registers loaded two steps ago) staged into
-  // LDS[(s+1)&1]; refill those registers with step s+3; one barrier.
-  auto step = [&](int s, float (&ra)[SA::R], float (&rb)[SB::R]) {
-    compute(s & 1, s + 1 < nsteps, (s + 1) & 1, ra, rb);
+  // full step s: MFMAs on LDS[s&1], then step s+1 (registers loaded PF steps ago) staged into
+  // LDS[(s+1)&1] (garbage after the last full step: never computed, kept out of the bias
+  // gradient), those registers refilled with step s+1+PF; one barrier.
+  auto stepU = [&](int s, float (&ra)[SA::R], float (&rb)[SB::R]) {
+    compute(s & 1);
+#ifndef LGX_EXP_NOSTORE  // experiment (timing only): no staging split / LDS stores in the loop
+    sstore(ra, rb, (s + 1) & 1, s + 1 < nfull);
+#endif
 #ifndef LGX_EXP_NOLOAD  // experiment (timing only): no global loads in the loop
-    if (s + 1 + PF < nsteps) gload(ra, rb, kbeg + (s + 1 + PF) * BKS);
+    gloadU(ra, rb, s + 1 + PF);
 #endif
     __syncthreads();
   };
 
-  if (nsteps > 0) {
-    gload(va[0], vb[0], kbeg);
-    sstore(va[0], vb[0], 0);
+  if (nfull > 0) {
+    gloadU(va[0], vb[0], 0);
+    sstore(va[0], vb[0], 0, true);
 #pragma unroll
-    for (int j = 1; j <= PF; ++j)
-      if (j < nsteps) gload(va[j % PF], vb[j % PF], kbeg + j * BKS);
+    for (int j = 1; j <= PF; ++j) gloadU(va[j % PF], vb[j % PF], j);
   }
   __syncthreads();
   // step s stages register set (s + 1) % PF (step s + 1, loaded PF steps earlier) and refills
   // it with step s + 1 + PF
-  for (int s = 0; s < nsteps; s += PF) {
+  int s = 0;
+  for (; s + PF <= nfull; s += PF) {
 #pragma unroll
-    for (int j = 0; j < PF; ++j)
-      if (s + j < nsteps) step(s + j, va[(j + 1) % PF], vb[(j + 1) % PF]);
+    for (int j = 0; j < PF; ++j) stepU(s + j, va[(j + 1) % PF], vb[(j + 1) % PF]);
+  }
+#pragma unroll
+  for (int j = 0; j + 1 < PF; ++j)
+    if (s + j < nfull) stepU(s + j, va[(j + 1) % PF], vb[(j + 1) % PF]);
+  if (nsteps > nfull) {  // the partial last step, zero-filled past kend
+    const int k0 = kbeg + nfull * BKS;
+    SA::template load<true>(p.A, p.lda, m0, p.M, k0, kend, tid, va[0]);
+    SB::template load<true>(p.B, p.ldb, n0, p.N, k0, kend, tid, vb[0]);
+    sstore(va[0], vb[0], nfull & 1, true);
+    __syncthreads();
+    compute(nfull & 1);
+    __syncthreads();
   }
 
   float* cs = reinterpret_cast<float*>(lds);
@@ -461,11 +476,27 @@ __device__ __forceinline__ int xcd_tile(int tiles) {
   return (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
 }
 
+// An MVE operand (row count not a multiple of 4) on a tile whose rows all lie inside it takes
+// the MV stager (same loads, values and stores): MVE's interior/edge branch would otherwise
+// sit inside the K loop's loads, where it breaks hipcc's wait counting (gemm_tile). Bit 0:
+// the tile's N rows (B of the input gradient) are interior, bit 1: its M rows.
+template <int BM_, int BN_>
+__device__ __forceinline__ int interior_bits(const Params& p, int L) {
+  const int tn = L % p.tiles_n, tm = (L / p.tiles_n) % p.tiles_m;
+  return (tn * BN_ + BN_ <= p.N ? 1 : 0) | (tm * BM_ + BM_ <= p.M ? 2 : 0);
+}
+
 template <int AM, int BMODE, bool COLSUM, int BN_>
 __global__ __launch_bounds__(NT, 2) void gemm_kernel(Params p) {
   const int L = xcd_tile(p.tiles);
   if (L >= p.tiles) return;
-  gemm_tile<AM, BMODE, COLSUM, BN_>(p, L);
+  constexpr int AI = AM == MVE ? MV : AM, BI = BMODE == MVE ? MV : BMODE;  // interior-tile stagers
+  const int ib = interior_bits<BM, BN_>(p, L);
+  const bool a_in = AM != MVE || (ib & 2), b_in = BMODE != MVE || (ib & 1);
+  if (a_in && b_in) gemm_tile<AI, BI, COLSUM, BN_>(p, L);
+  else if (a_in) gemm_tile<AI, BMODE, COLSUM, BN_>(p, L);
+  else if (b_in) gemm_tile<AM, BI, COLSUM, BN_>(p, L);
+  else gemm_tile<AM, BMODE, COLSUM, BN_>(p, L);
 }
 
 // ---------------------------------------------------------------- grouped launch
@@ -506,14 +537,16 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 4 : 2) void gemm_group_kernel(Gr
   } else if constexpr (KIND == G_DX) {
     const Params p = g.p[i];
     if (l >= p.tiles) return;
-    if (m) gemm_tile<KV, MVE, false, BN_, BM_, LGX_PF, NW>(p, l);
+    if (m & ~interior_bits<BM_, BN_>(p, l)) gemm_tile<KV, MVE, false, BN_, BM_, LGX_PF, NW>(p, l);
     else gemm_tile<KV, MV, false, BN_, BM_, LGX_PF, NW>(p, l);
   } else {
     const Params& p = g.p[i];
     if (l >= p.tiles) return;
-    if (m == 0) gemm_tile<MV, MV, true, BN_, BM, LGX_PF, NW>(p, l);
-    else if (m == 1) gemm_tile<MVE, MV, true, BN_, BM, LGX_PF, NW>(p, l);
-    else if (m == 2) gemm_tile<MV, MVE, true, BN_, BM, LGX_PF, NW>(p, l);
+    const int ib = interior_bits<BM, BN_>(p, l);
+    const int e = m & ~((ib >> 1) | ((ib & 1) << 1));  // mode bit 0: A (M rows), bit 1: B (N rows)
+    if (e == 0) gemm_tile<MV, MV, true, BN_, BM, LGX_PF, NW>(p, l);
+    else if (e == 1) gemm_tile<MVE, MV, true, BN_, BM, LGX_PF, NW>(p, l);
+    else if (e == 2) gemm_tile<MV, MVE, true, BN_, BM, LGX_PF, NW>(p, l);
     else gemm_tile<MVE, MVE, true, BN_, BM, LGX_PF, NW>(p, l);
   }
 }
