@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define LGX_MLP_ABI_VERSION 5
+#define LGX_MLP_ABI_VERSION 6
 
 enum {
   LGX_EPI_BIAS = 1,  /* + bias[n] */
@@ -71,6 +71,33 @@ int32_t lgx_gemm(const lgx_gemm_args* args, void* stream);
  * (bit-identical results). Entries must not write overlapping outputs. */
 #define LGX_GEMM_GROUP_MAX 20
 int32_t lgx_gemm_group(const lgx_gemm_args* args, int32_t n, void* stream);
+/* The narrow consecutive layers of up to LGX_CHAIN_MAX independent chains in ONE launch
+ * (the encoders' and estimator's layers after the first, the actor/critic 256->128->out
+ * tails, and the input-gradient passes back through them: rsl_rl actor_critic.py:64-87,
+ * support_networks.py:22-112). Layer l of a chain computes, for its `rows` rows,
+ *     C_l[m*ldc + n] = epilogue_l( sum_k A_l(m, k) * B_l[n*ldb + k] )
+ * with A_0(m, k) = A[m*lda + k] and A_l = C_{l-1} for l > 0 (the previous layer's output,
+ * kept on chip between layers and also written to C_{l-1}); K_0 = the chain's input width,
+ * K_l = N_{l-1}; every K_l, N_l <= LGX_CHAIN_MAXW. Epilogues: LGX_EPI_BIAS (+ LGX_EPI_ELU)
+ * for a forward pass, LGX_EPI_DELU (act = the ELU output at the same rows) for an input-
+ * gradient pass over transposed weights. Each layer's arithmetic and summation order are
+ * those of lgx_gemm with a_kcontig = b_kcontig = 1, split_k 1: bit-identical results. */
+#define LGX_CHAIN_MAX 4
+#define LGX_CHAIN_MAXL 3
+#define LGX_CHAIN_MAXW 256
+typedef struct lgx_chain_layer {
+  const float* B; int64_t ldb;       /* [N][K] k-contiguous (W for forward, W^T for input grad) */
+  float* C; int64_t ldc;
+  int32_t K, N, epilogue;
+  const float* bias;
+  const float* act; int64_t ld_act;
+} lgx_chain_layer;
+typedef struct lgx_chain_desc {
+  const float* A; int64_t lda;
+  int32_t rows, nlayers;             /* 1 <= nlayers <= LGX_CHAIN_MAXL */
+  lgx_chain_layer layers[LGX_CHAIN_MAXL];
+} lgx_chain_desc;
+int32_t lgx_chain(const lgx_chain_desc* chains, int32_t n, void* stream);
 /* Split-K factors for n weight-gradient GEMMs launched as one group: one K chunk for all
  * (a multiple of 32 rows, >= 256), the smallest whose block count fits one residency wave
  * of the chip; every split >= 2. */

@@ -551,6 +551,202 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 4 : 2) void gemm_group_kernel(Gr
   }
 }
 
+// ---------------------------------------------------------------- chain launch (lgx_chain)
+// The narrow tail layers of up to LGX_CHAIN_MAX chains in one launch. A block owns BR rows of
+// one chain and 4 waves; the activations between layers never leave the CU: the chain input's
+// rows are split once into an LDS image (bf16 hi | lo planes, [BR][IP], zero past K, pitch
+// IP = width + 8 bf16: fragment reads conflict-free); every layer reads its A fragments from
+// the image and, after a barrier, overwrites it with its own output, split (fp32 copies go to
+// HBM: the backward pass and the next launch read them). B fragments (weight rows,
+// k-contiguous, L2-resident) go straight from global memory into registers, two K steps
+// ahead; the next layer's first two steps and the input-gradient epilogue's ELU outputs are
+// requested before the current layer's results are written, so their latency overlaps it.
+// Wave w owns the 16-wide output column tiles w, w + 4, ... (NJW of them) for all BR/16 row
+// tiles. Per output the MFMA sequence is gemm_tile's (32-deep K steps in order, lo*hi +
+// hi*lo + hi*hi, partial last step zero-filled in both operands) and so are the epilogues:
+// bit-identical to lgx_gemm.
+constexpr int CHMAX = LGX_CHAIN_MAX, CHMAXL = LGX_CHAIN_MAXL;
+struct ChainParams {
+  int n, ip;
+  int start[CHMAX + 1];  // prefix sums of the chains' row blocks
+  lgx_chain_desc c[CHMAX];
+};
+static_assert(sizeof(ChainParams) <= 4096, "kernel argument segment");
+
+// B fragment of tile t at K step s of layer L: W row n = 16 j + fr (clamped: a tile past N
+// computes nothing that is stored), k = 32 s + 8 fc .. + 8; past K (a partial step): zero,
+// from clamped addresses
+template <int NJW>
+__device__ __forceinline__ void chain_bload(const lgx_chain_layer& L, int s, int wave, int fr, int fc,
+                                            float (&b)[NJW][8]) {
+  const int k = s * BKS + fc * 8;
+#pragma unroll
+  for (int t = 0; t < NJW; ++t) {
+    const int n = min((wave + 4 * t) * 16 + fr, L.N - 1);
+    const float* row = L.B + n * (int)L.ldb;  // 32-bit lane offsets from a uniform base
+    if ((s + 1) * BKS <= L.K) {  // wave-uniform
+      const f32x4u x0 = *reinterpret_cast<const f32x4u*>(row + k);
+      const f32x4u x1 = *reinterpret_cast<const f32x4u*>(row + k + 4);
+      b[t][0] = x0.x; b[t][1] = x0.y; b[t][2] = x0.z; b[t][3] = x0.w;
+      b[t][4] = x1.x; b[t][5] = x1.y; b[t][6] = x1.z; b[t][7] = x1.w;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float x = row[min(k + j, L.K - 1)];
+        b[t][j] = k + j < L.K ? x : 0.f;
+      }
+    }
+  }
+}
+
+template <int BR, int NJW>
+__global__ __launch_bounds__(NT, 2) void chain_kernel(ChainParams P) {
+  constexpr int MI = BR / 16;
+  extern __shared__ __align__(16) __bf16 lds[];
+  const int ip = P.ip;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fc = lane >> 4;
+  const int blk = blockIdx.x;
+  if (blk >= P.start[P.n]) return;
+  int ci = 0;
+  while (ci + 1 < P.n && blk >= P.start[ci + 1]) ++ci;
+  const lgx_chain_desc& c = P.c[ci];
+  const int rows = c.rows, r0 = (blk - P.start[ci]) * BR;
+  __bf16* ih = lds;            // image planes [BR][ip]
+  __bf16* il = lds + BR * ip;
+
+  float b0[NJW][8], b1[NJW][8];  // B register sets: K steps s (b0) and s + 1 (b1)
+  {
+    const lgx_chain_layer& L0 = c.layers[0];
+    const int ns = (L0.K + BKS - 1) / BKS;
+    chain_bload<NJW>(L0, 0, wave, fr, fc, b0);
+    chain_bload<NJW>(L0, min(1, ns - 1), wave, fr, fc, b1);
+    // the chain input's rows (clamped at the edge, as gemm_tile) -> the image, zero past K
+    const int K = L0.K, c8 = ns * 4;
+    const float* a0 = c.A + (int64_t)r0 * c.lda;
+    for (int idx = tid; idx < BR * c8; idx += NT) {
+      const int r = idx / c8, k = (idx % c8) * 8;
+      const float* q = a0 + (min(r0 + r, rows - 1) - r0) * (int)c.lda + k;
+      float v[8];
+      if (k + 8 <= K) {
+        const f32x4u x0 = *reinterpret_cast<const f32x4u*>(q);
+        const f32x4u x1 = *reinterpret_cast<const f32x4u*>(q + 4);
+        v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w; v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = k + j < K ? q[j] : 0.f;
+      }
+      bf16x8 h, l;
+      split8(v, h, l);
+      *reinterpret_cast<bf16x8*>(ih + r * ip + k) = h;
+      *reinterpret_cast<bf16x8*>(il + r * ip + k) = l;
+    }
+  }
+  __syncthreads();
+
+  for (int li = 0; li < c.nlayers; ++li) {
+    const lgx_chain_layer& L = c.layers[li];
+    const int K = L.K, N = L.N, ntile = (N + 15) / 16;
+    const int nsteps = (K + BKS - 1) / BKS;
+    // the input-gradient epilogue's ELU outputs, requested before the K loop
+    float yv[MI][NJW][4];
+    const int mlast = rows - 1 - r0;  // last valid row of the block (local)
+    if (L.epilogue & LGX_EPI_DELU) {
+      const float* y0 = L.act + (int64_t)r0 * L.ld_act;
+#pragma unroll
+      for (int t = 0; t < NJW; ++t) {
+        const int n = min((wave + 4 * t) * 16 + fr, N - 1);
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) yv[i][t][r] = y0[min(i * 16 + fc * 4 + r, mlast) * (int)L.ld_act + n];
+      }
+    }
+    f32x4 acc[MI][NJW];
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int t = 0; t < NJW; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    auto mma = [&](const float (&b)[NJW][8], int s) {
+      bf16x8 bh[NJW], bl[NJW];
+#pragma unroll
+      for (int t = 0; t < NJW; ++t) split8(b[t], bh[t], bl[t]);
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int off = (i * 16 + fr) * ip + s * BKS + fc * 8;
+        const bf16x8 ah = *reinterpret_cast<const bf16x8*>(ih + off);
+        const bf16x8 al = *reinterpret_cast<const bf16x8*>(il + off);
+#pragma unroll
+        for (int t = 0; t < NJW; ++t) {
+          if (wave + 4 * t < ntile) {  // wave-uniform
+            acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh[t], acc[i][t], 0, 0, 0);
+            acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl[t], acc[i][t], 0, 0, 0);
+            acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh[t], acc[i][t], 0, 0, 0);
+          }
+        }
+      }
+    };
+    // steps s, s + 1 are in b0, b1; each refill requests s + 2 (clamped to the last step)
+    int s = 0;
+    for (; s + 2 <= nsteps; s += 2) {
+      mma(b0, s);
+      if (s + 2 < nsteps) chain_bload<NJW>(L, s + 2, wave, fr, fc, b0);
+      mma(b1, s + 1);
+      if (s + 3 < nsteps) chain_bload<NJW>(L, s + 3, wave, fr, fc, b1);
+    }
+    if (s < nsteps) mma(b0, s);
+    const bool next = li + 1 < c.nlayers;
+    if (next) {  // the next layer's first two steps
+      const lgx_chain_layer& Ln = c.layers[li + 1];
+      const int ns = (Ln.K + BKS - 1) / BKS;
+      chain_bload<NJW>(Ln, 0, wave, fr, fc, b0);
+      chain_bload<NJW>(Ln, min(1, ns - 1), wave, fr, fc, b1);
+    }
+    __syncthreads();  // every wave is done reading the image
+
+    // epilogue: lane holds rows 4 fc + r (r < 4) of column fr of each tile
+    float* c0 = L.C + (int64_t)r0 * L.ldc;
+#pragma unroll
+    for (int t = 0; t < NJW; ++t) {
+      const int j = wave + 4 * t;
+      if (j >= ntile) continue;
+      const int n = j * 16 + fr;
+      const bool nok = n < N;
+      const float bn = (L.epilogue & LGX_EPI_BIAS) && nok ? L.bias[n] : 0.f;
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int ml = i * 16 + fc * 4 + r;
+          float v = acc[i][t][r];
+          if (L.epilogue & LGX_EPI_BIAS) v += bn;
+          if (L.epilogue & LGX_EPI_ELU) v = elu(v);
+          if (L.epilogue & LGX_EPI_DELU) {
+            const float y = yv[i][t][r];
+            v *= y > 0.f ? 1.f : y + 1.f;
+          }
+          if (!nok) v = 0.f;
+          if (nok && ml <= mlast) c0[ml * (int)L.ldc + n] = v;
+          if (next) {
+            const __bf16 h = (__bf16)v;
+            ih[ml * ip + n] = h;
+            il[ml * ip + n] = (__bf16)(v - (float)h);
+          }
+        }
+      }
+    }
+    if (next) {  // zero the image's columns [16 ntile, next K padded to 32)
+      const int z0 = ntile * 16, z1 = ((N + 31) / 32) * 32;
+      for (int idx = tid; idx < BR * (z1 - z0); idx += NT) {
+        const int r = idx / (z1 - z0), k = z0 + idx % (z1 - z0);
+        ih[r * ip + k] = (__bf16)0.f;
+        il[r * ip + k] = (__bf16)0.f;
+      }
+      __syncthreads();
+    }
+  }
+}
+
 // C (=|+=) epilogue(sum_z ws[z]) and colsum[m] (=|+=) sum_z colsum_ws[z][m]. Each thread owns
 // 4 consecutive outputs (float4 when N % 4 == 0) and walks the splits with 4 independent
 // accumulators (z mod 4) combined in a fixed order: deterministic, memory-level parallel.
@@ -1805,6 +2001,65 @@ int32_t lgx_gemm_group(const lgx_gemm_args* args, int32_t n, void* stream) {
     LGX_GROUP_LAUNCH(G_DW)
   }
 #undef LGX_GROUP_LAUNCH
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : fail(hipGetErrorString(e));
+}
+
+int32_t lgx_chain(const lgx_chain_desc* chains, int32_t n, void* stream) {
+  using namespace lgxm;
+  if (n < 0 || n > LGX_CHAIN_MAX || (n > 0 && !chains)) return fail("lgx_chain: 0 <= n <= LGX_CHAIN_MAX");
+  ChainParams P;
+  P.n = 0;
+  int maxw = 0, maxn = 0, maxrows = 0;
+  for (int i = 0; i < n; ++i) {
+    const lgx_chain_desc& d = chains[i];
+    if (d.rows < 0 || d.nlayers < 1 || d.nlayers > LGX_CHAIN_MAXL) return fail("lgx_chain: rows >= 0, 1 <= nlayers <= LGX_CHAIN_MAXL");
+    if (d.rows == 0) continue;
+    if (!d.A || d.lda < d.layers[0].K) return fail("lgx_chain: bad input");
+    for (int l = 0; l < d.nlayers; ++l) {
+      const lgx_chain_layer& L = d.layers[l];
+      if (L.K < 1 || L.N < 1 || L.K > LGX_CHAIN_MAXW || L.N > LGX_CHAIN_MAXW)
+        return fail("lgx_chain: layer widths must lie in [1, LGX_CHAIN_MAXW]");
+      if (l > 0 && L.K != d.layers[l - 1].N) return fail("lgx_chain: K of a layer must be N of the previous one");
+      if (!L.B || L.ldb < L.K || !L.C || L.ldc < L.N) return fail("lgx_chain: bad layer operands");
+      if (L.epilogue & ~(LGX_EPI_BIAS | LGX_EPI_ELU | LGX_EPI_DELU)) return fail("lgx_chain: epilogue bits BIAS/ELU/DELU only");
+      if (((L.epilogue & LGX_EPI_BIAS) && !L.bias) || ((L.epilogue & LGX_EPI_DELU) && (!L.act || L.ld_act < L.N)))
+        return fail("lgx_chain: epilogue operand missing");
+      maxw = std::max(maxw, std::max((int)L.K, (int)L.N));
+      maxn = std::max(maxn, (int)L.N);
+    }
+    P.c[P.n++] = d;
+    maxrows = std::max(maxrows, (int)d.rows);
+  }
+  if (P.n == 0) return 0;
+  // 64-row blocks for narrow chains over many rows, else 32 (LDS: 2 images x 2 planes)
+  const int br = (maxw <= 128 && maxrows > 8192) ? 64 : 32;
+  P.ip = ((maxw + 31) / 32) * 32 + 8;
+  int total = 0;
+  for (int i = 0; i < P.n; ++i) {
+    P.start[i] = total;
+    total += (P.c[i].rows + br - 1) / br;
+  }
+  P.start[P.n] = total;
+  const int njw = ((maxn + 15) / 16 + 3) / 4;  // 16-wide column tiles per wave
+  const size_t lds = (size_t)2 * br * P.ip * sizeof(__bf16);  // one image, hi | lo
+  hipStream_t s = static_cast<hipStream_t>(stream);
+#define LGX_CHAIN_LAUNCH(BR_, NJ_)                                                                     \
+  {                                                                                                    \
+    static bool attr = false;                                                                          \
+    if (!attr) {                                                                                       \
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&chain_kernel<BR_, NJ_>),                \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 2 * BR_ * (256 + 8) * 2);  \
+      attr = true;                                                                                     \
+    }                                                                                                  \
+    hipLaunchKernelGGL((chain_kernel<BR_, NJ_>), dim3(total), dim3(NT), lds, s, P);                   \
+  }
+  if (br == 64) {
+    if (njw == 1) LGX_CHAIN_LAUNCH(64, 1) else LGX_CHAIN_LAUNCH(64, 2)
+  } else {
+    if (njw == 1) LGX_CHAIN_LAUNCH(32, 1) else if (njw == 2) LGX_CHAIN_LAUNCH(32, 2) else LGX_CHAIN_LAUNCH(32, 4)
+  }
+#undef LGX_CHAIN_LAUNCH
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : fail(hipGetErrorString(e));
 }

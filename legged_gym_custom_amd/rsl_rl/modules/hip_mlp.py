@@ -20,7 +20,7 @@ import torch.nn as nn
 _LIB_PATH = os.environ.get("LGX_MLP_LIB") or os.path.join(
     os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))), "lib", "liblgx_mlp.so")
 _lib = None
-ABI_VERSION = 5
+ABI_VERSION = 6
 EPI_BIAS, EPI_ELU, EPI_DELU, EPI_ACCUM = 1, 2, 4, 8
 EXPORTED = ["lgx_mlp_abi_version", "lgx_mlp_sizeof_gemm_args", "lgx_mlp_pick_split", "lgx_gemm",
             "lgx_mlp_last_error", "lgx_adam_step", "lgx_ppo_head_forward", "lgx_ppo_head_backward",
@@ -28,12 +28,18 @@ EXPORTED = ["lgx_mlp_abi_version", "lgx_mlp_sizeof_gemm_args", "lgx_mlp_pick_spl
             "lgx_aux_loss_forward", "lgx_aux_loss_backward", "lgx_ppo_tail", "lgx_gemm_group",
             "lgx_mlp_pick_split_group", "lgx_gae", "lgx_normalize_advantages",
             "lgx_gather_rows", "lgx_transpose_batch", "lgx_loss_heads_forward", "lgx_loss_heads_backward",
-            "lgx_track_episodes"]
+            "lgx_track_episodes", "lgx_chain"]
 TAIL_MAX_LOSSES = 8
 COPY_MAX = 16
 SPLITK_MAX = 24
 GROUP_MAX = 20
 TRANSPOSE_MAX = 24
+CHAIN_MAX, CHAIN_MAXL, CHAIN_MAXW = 4, 3, 256
+# lgx_chain serves batches of at most CHAIN_ROWS rows (the rollout's 4096-row act pass): at the
+# update's 24,576 rows one grouped launch per depth measured faster (profiles/r03_chain.txt).
+# Dev knobs: LGX_CHAIN=0 (never chain), LGX_CHAIN_ROWS (the row limit).
+USE_CHAIN = os.environ.get("LGX_CHAIN", "1") != "0"
+CHAIN_ROWS = int(os.environ.get("LGX_CHAIN_ROWS", "8192"))
 
 
 class GemmArgs(C.Structure):
@@ -114,6 +120,19 @@ class TransposeDesc(C.Structure):
                 ("dst", C.c_void_p)]
 
 
+class ChainLayer(C.Structure):
+    """Mirror of lgx_chain_layer."""
+    _fields_ = [("B", C.c_void_p), ("ldb", C.c_int64), ("C", C.c_void_p), ("ldc", C.c_int64),
+                ("K", C.c_int32), ("N", C.c_int32), ("epilogue", C.c_int32), ("bias", C.c_void_p),
+                ("act", C.c_void_p), ("ld_act", C.c_int64)]
+
+
+class ChainDesc(C.Structure):
+    """Mirror of lgx_chain_desc."""
+    _fields_ = [("A", C.c_void_p), ("lda", C.c_int64), ("rows", C.c_int32), ("nlayers", C.c_int32),
+                ("layers", ChainLayer * CHAIN_MAXL)]
+
+
 class GaeArgs(C.Structure):
     """Mirror of lgx_gae_args."""
     _fields_ = [(n, C.c_void_p) for n in ("rewards", "dones", "values", "last_values", "returns", "advantages")] + \
@@ -173,6 +192,8 @@ def lib():
     L.lgx_normalize_advantages.restype = C.c_int32
     L.lgx_splitk_reduce_batch.argtypes = [vp, C.c_int32, vp]
     L.lgx_splitk_reduce_batch.restype = C.c_int32
+    L.lgx_chain.argtypes = [vp, C.c_int32, vp]
+    L.lgx_chain.restype = C.c_int32
     if L.lgx_mlp_abi_version() != ABI_VERSION:
         raise MlpLibError("liblgx_mlp ABI version mismatch; rebuild")
     L.lgx_mlp_sizeof_gemm_args.restype = C.c_int32
@@ -408,6 +429,48 @@ def run_group(args):
         chunk = args[i:i + GROUP_MAX]
         arr = (GemmArgs * len(chunk))(*chunk)
         _check(lib().lgx_gemm_group(arr, len(chunk), _stream()), "lgx_gemm_group")
+
+
+def run_chain(descs):
+    """lgx_chain over a list of ChainDesc (chunks of CHAIN_MAX)."""
+    for i in range(0, len(descs), CHAIN_MAX):
+        chunk = descs[i:i + CHAIN_MAX]
+        arr = (ChainDesc * len(chunk))(*chunk)
+        _check(lib().lgx_chain(arr, len(chunk), _stream()), "lgx_chain")
+
+
+def _chain_desc(x, layers):
+    """ChainDesc for input x ([rows, K0], unit column stride) and layers
+    [(B, C, epilogue, bias, act), ...] (B [N, K] k-contiguous, C [rows, N])."""
+    d = ChainDesc(A=_ptr(x), lda=x.stride(0), rows=x.shape[0], nlayers=len(layers))
+    for l, (B, Cm, epi, bias, act) in enumerate(layers):
+        d.layers[l] = ChainLayer(B=_ptr(B), ldb=B.stride(0), C=_ptr(Cm), ldc=Cm.stride(0), K=B.shape[1],
+                                 N=B.shape[0], epilogue=epi, bias=_ptr(bias), act=_ptr(act),
+                                 ld_act=0 if act is None else act.stride(0))
+    return d
+
+
+def _narrow(W):
+    return W.shape[0] <= CHAIN_MAXW and W.shape[1] <= CHAIN_MAXW
+
+
+def _chain_start(chains, hs):
+    """First depth d0 from which every chain's remaining layers (2..CHAIN_MAXL of them, all
+    widths <= CHAIN_MAXW, non-empty input) run as one lgx_chain launch; None if none does."""
+    if not USE_CHAIN or len(chains) > CHAIN_MAX or not hs[0].is_cuda or max(h.shape[0] for h in hs) > CHAIN_ROWS:
+        return None
+    d0 = 0
+    for Ws, _b, _f in chains:
+        t = len(Ws)
+        while t > 0 and _narrow(Ws[t - 1]):
+            t -= 1
+        d0 = max(d0, t)
+    lens = [len(Ws) for Ws, _b, _f in chains]
+    if min(lens) - d0 < 1 or max(lens) - d0 < 2 or max(lens) - d0 > CHAIN_MAXL:
+        return None
+    if d0 == 0 and any(h.shape[1] == 0 for h in hs):
+        return None
+    return d0
 
 
 def pick_split_group(shapes):
@@ -717,7 +780,9 @@ def _group_forward(xs, chains, finals=None):
     column stride, e.g. the latent columns of the actor-input buffer)."""
     outs = [[] for _ in chains]
     hs = [_rowmajor(x) for x in xs]
-    for d in range(max(len(c[2]) for c in chains)):
+    d0 = _chain_start(chains, hs)
+    depth = max(len(c[2]) for c in chains) if d0 is None else d0
+    for d in range(depth):
         args = []
         for c, (Ws, bs, flags) in enumerate(chains):
             if d < len(flags):
@@ -736,6 +801,20 @@ def _group_forward(xs, chains, finals=None):
                 outs[c].append(y)
                 hs[c] = y
         run_group(args)
+    if d0 is not None:  # the narrow tail of every chain: one launch, activations on chip
+        descs = []
+        for c, (Ws, bs, flags) in enumerate(chains):
+            layers = []
+            for d in range(d0, len(flags)):
+                y = finals[c] if finals is not None and finals[c] is not None and d == len(flags) - 1 else None
+                if y is not None and (y.shape != (hs[c].shape[0], Ws[d].shape[0]) or y.stride(1) != 1):
+                    raise MlpLibError("forward_group: output span shape does not match the chain")
+                if y is None:
+                    y = torch.empty(hs[c].shape[0], Ws[d].shape[0], device=hs[c].device, dtype=torch.float32)
+                layers.append((Ws[d], y, EPI_BIAS | (EPI_ELU if flags[d] else 0), bs[d], None))
+                outs[c].append(y)
+            descs.append(_chain_desc(hs[c], layers))
+        run_chain(descs)
     return outs
 
 
@@ -819,6 +898,29 @@ class _GroupFn(torch.autograd.Function):
                 spans[(c, 0)] = len(need_t)
                 need_t.append(wb[0][:, offs[first]:offs[last + 1]])
         wts = transpose_batch(need_t) if need_t else []
+        # the input gradients through the chains' narrow tails (layers i >= max(d0, 1), as the
+        # forward's lgx_chain) in one launch before the per-depth loop: chained[c] = (first
+        # layer covered, {i - 1: dY_{i-1}})
+        chained = [None] * len(meta)
+        chains_w = [(item[1][0::2], None, flags) for (_n, flags), item in zip(meta, st)]
+        d0 = _chain_start(chains_w, [item[0] for item in st]) if all(item[3] is not None for item in st) else None
+        if d0 is not None:
+            i_stop = max(d0, 1)
+            descs = []
+            for c, ((_n, flags), item) in enumerate(zip(meta, st)):
+                x, wb, outs, g, _p0 = item
+                n = len(flags)
+                layers, got = [], {}
+                for i in range(n - 1, i_stop - 1, -1):
+                    dx = torch.empty(g.shape[0], wb[2 * i].shape[1], device=g.device, dtype=torch.float32)
+                    yp = outs[i - 1] if flags[i - 1] else None
+                    layers.append((wts[spans[(c, i)]], dx, EPI_DELU if yp is not None else 0, None, yp))
+                    got[i - 1] = dx
+                if layers:
+                    descs.append(_chain_desc(_rowmajor(g), layers))
+                    chained[c] = (i_stop, got)
+            if descs:
+                run_chain(descs)
         for t in range(max(len(f) for _n, f in meta)):
             args, news = [], []
             for c, ((nparts, flags), item) in enumerate(zip(meta, st)):
@@ -831,6 +933,9 @@ class _GroupFn(torch.autograd.Function):
                 if ctx.needs_input_grad[1 + p0 + nparts + 2 * i] or ctx.needs_input_grad[2 + p0 + nparts + 2 * i]:
                     linear_weight_grad(g, inp, _grad_of(ctx.params[c][2 * i]), _grad_of(ctx.params[c][2 * i + 1]),
                                        accumulate=True)
+                if i > 0 and chained[c] is not None and i >= chained[c][0]:
+                    news.append((c, chained[c][1][i - 1]))  # formed by the chain launch
+                    continue
                 if i > 0:
                     dx = torch.empty(g.shape[0], wb[2 * i].shape[1], device=g.device, dtype=torch.float32)
                     args.append(_dxt_args(g, wts[spans[(c, i)]], outs[i - 1] if flags[i - 1] else None, dx))

@@ -410,6 +410,53 @@ def test_forward_group_matches_separate_chains_bitwise():
     assert all(torch.equal(a, b) for a, b in zip(o1, o3))
 
 
+@pytest.mark.parametrize("B", [3000, 9001])
+def test_chain_launch_matches_per_depth_launches_bitwise(B, monkeypatch):
+    """lgx_chain (the narrow tail layers of every chain in one launch, forward and input
+    gradient; 32-row blocks at 3000 rows, 64-row blocks at 9001) == one grouped launch per
+    depth (LGX_CHAIN=0): outputs, every parameter gradient and a parts input gradient,
+    bitwise — the encoders (tails from depth 1), the actor / critic (from depth 2)."""
+    from legged_gym_custom_amd.rsl_rl.modules.support_networks import _mlp
+    torch.manual_seed(11)
+    act = torch.nn.ELU()
+    enc = [_mlp(29, [64, 20], 20, act), _mlp(132, [128, 64], 32, act), _mlp(572, [128, 64], 3, act)]
+    ac = [_mlp(627, [512, 256, 128], 12, act), _mlp(736, [512, 256, 128], 1, act)]
+    enc, ac = [n.to(dev) for n in enc], [n.to(dev) for n in ac]
+    g = torch.Generator(device=dev).manual_seed(12)
+    xs = [torch.randn(B, d, device=dev, generator=g) for d in (29, 132, 572, 736)]
+    obs = torch.randn(B, 572, device=dev, generator=g)
+    seeds = [torch.randn(B, o, device=dev, generator=g) for o in (12, 1, 3)]
+    calls = []
+    orig = H.run_chain
+
+    def spy(descs):
+        calls.append(len(descs))
+        return orig(descs)
+
+    monkeypatch.setattr(H, "run_chain", spy)
+    monkeypatch.setattr(H, "CHAIN_ROWS", 1 << 30)  # the kernel at any row count (product: <= 8192)
+
+    def run(chain):
+        monkeypatch.setattr(H, "USE_CHAIN", chain)
+        for n in (*enc, *ac):
+            n.zero_grad(set_to_none=True)
+        with H.deferred_weight_grads():
+            lat = H.forward_group([(enc[0], xs[0]), (enc[1], xs[1]), (enc[2], xs[2])])
+            mu, v = H.forward_group([(ac[0], (obs, lat[0], lat[1], lat[2])), (ac[1], xs[3])])
+            torch.autograd.backward([mu, v, lat[2]], seeds)
+        return [t.detach().clone() for t in (*lat, mu, v)], [p.grad.clone() for n in (*enc, *ac) for p in n.parameters()]
+
+    o1, g1 = run(False)
+    assert not calls
+    o2, g2 = run(True)
+    assert calls == [3, 2, 2, 3]  # forward: encoders, actor/critic tails; backward: the same
+    assert all(torch.equal(a, b) for a, b in zip(o1, o2))
+    assert all(torch.equal(a, b) for a, b in zip(g1, g2))
+    with torch.no_grad():
+        lat = H.forward_group([(enc[0], xs[0]), (enc[1], xs[1]), (enc[2], xs[2])])
+    assert all(torch.equal(a, b) for a, b in zip(o1[:3], lat))
+
+
 def test_forward_group_output_spans_bitwise():
     """Chains whose last layer writes into column spans of a shared buffer (the update's
     latents inside the actor input) == the same chains writing their own outputs: outputs,
