@@ -46,6 +46,9 @@ constexpr int BM = 128, BKS = 32, NT = 256;
 #ifndef LGX_PF
 #define LGX_PF 2
 #endif
+#ifndef LGX_PF_DW  // the weight-gradient kind's prefetch depth (dev knob)
+#define LGX_PF_DW LGX_PF
+#endif
 #ifndef LGX_MV_ROWMAJOR
 #define LGX_MV_ROWMAJOR 1
 #endif
@@ -544,10 +547,10 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 4 : 2) void gemm_group_kernel(Gr
     if (l >= p.tiles) return;
     const int ib = interior_bits<BM, BN_>(p, l);
     const int e = m & ~((ib >> 1) | ((ib & 1) << 1));  // mode bit 0: A (M rows), bit 1: B (N rows)
-    if (e == 0) gemm_tile<MV, MV, true, BN_, BM, LGX_PF, NW>(p, l);
-    else if (e == 1) gemm_tile<MVE, MV, true, BN_, BM, LGX_PF, NW>(p, l);
-    else if (e == 2) gemm_tile<MV, MVE, true, BN_, BM, LGX_PF, NW>(p, l);
-    else gemm_tile<MVE, MVE, true, BN_, BM, LGX_PF, NW>(p, l);
+    if (e == 0) gemm_tile<MV, MV, true, BN_, BM, LGX_PF_DW, NW>(p, l);
+    else if (e == 1) gemm_tile<MVE, MV, true, BN_, BM, LGX_PF_DW, NW>(p, l);
+    else if (e == 2) gemm_tile<MV, MVE, true, BN_, BM, LGX_PF_DW, NW>(p, l);
+    else gemm_tile<MVE, MVE, true, BN_, BM, LGX_PF_DW, NW>(p, l);
   }
 }
 
