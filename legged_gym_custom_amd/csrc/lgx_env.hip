@@ -18,6 +18,7 @@
 //   103-138): uniform scalar control flow per env; vector outputs written lane-parallel.
 #include <hip/hip_runtime.h>
 #include <math.h>
+#include <stddef.h>
 #include <stdint.h>
 
 #include "../../include/lgx.h"
@@ -821,6 +822,24 @@ LGX_DEV float sea_torque(const lgx_task_params* Pm, const lgx_buffers& B, int e,
 // of sea_torque above (the host backend's and the oracle's), so the torques are the same. Weight
 // rows are lane-indexed (vector loads of the params, L1-resident): 1/8 of the per-lane work and
 // transcendentals of one-joint-per-lane, and 4 state values per lane instead of 32.
+// The SEA net's weight block: lgx_task_params from sea_in_scale through sea_lin_w (972 floats),
+// read either from the LDS arena copy (product) or from the params (LGX_SEA_GLOBAL_W, for A/B).
+#define SEA_OFF(f) ((int)((offsetof(lgx_task_params, f) - offsetof(lgx_task_params, sea_in_scale)) / sizeof(float)))
+constexpr int SEA_WN = (int)((offsetof(lgx_task_params, sea_lin_w) + sizeof(float) * 8 -
+                              offsetof(lgx_task_params, sea_in_scale)) / sizeof(float));
+static_assert(SEA_WN == 972, "the SEA weight block is contiguous in lgx_task_params");
+static_assert(SEA_WN <= ROWS_FLOATS, "the SEA weights fit the arena");
+#ifndef LGX_SEA_GLOBAL_W
+struct SeaW {
+  float* base;  // LDS
+  LGX_DEV const float* w(int off) const { return base + off; }
+};
+#else
+struct SeaW {
+  const lgx_task_params* Pm;
+  LGX_DEV const float* w(int off) const { return &Pm->sea_in_scale[0] + off; }
+};
+#endif
 template <int K>
 LGX_DEV float unit_of(float v) {  // unit K of this lane's 8-lane group
   return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), 0x18 | (K << 5)));
@@ -866,9 +885,21 @@ LGX_DEV void sea_unit_k(const float* __restrict__ w_ih, const float* __restrict_
   float g4[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) g4[q] = (a[q] + b_ih[q * 8 + u]) + (b[q] + b_hh[q * 8 + u]);
+#ifdef LGX_SEA_OCML
+  // dev knob: ocml expf / IEEE division / tanhf (the host backend's and the oracle's functions)
   const float ig = sigmoidf_(g4[0]), fg = sigmoidf_(g4[1]), gg = tanhf(g4[2]), og = sigmoidf_(g4[3]);
   c = fg * c + ig * gg;
   h = og * tanhf(c);
+#else
+  // the gates on the hardware exp / rcp (v_exp_f32, v_rcp_f32, ~1 ulp each: sigmoid within
+  // ~3e-7 relative, tanh(x) = 2 sigmoid(2x) - 1 within ~2e-7 absolute), ~40 instructions per
+  // unit fewer than ocml expf / division / tanhf: C3 kernel 389 -> 372 us
+  // (profiles/r03_sea_lds_fast.txt); ANYmal golden replay, SeaLSTM and oracle parity unchanged
+  auto sg = [](float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); };
+  const float ig = sg(g4[0]), fg = sg(g4[1]), gg = 2.0f * sg(2.0f * g4[2]) - 1.0f, og = sg(g4[3]);
+  c = fg * c + ig * gg;
+  h = og * (2.0f * sg(2.0f * c) - 1.0f);
+#endif
 }
 // all 12 joints' SEA torques into s.tau (every lane of the wave takes part), one unit per lane
 // over two passes. (Two units per lane in one pass measured 425-459 us vs 433 for C3's kernel,
@@ -883,6 +914,17 @@ __device__ __attribute__((noinline))
 void sea_torques_lanes(Sh& s, const lgx_task_params* Pm_, const lgx_buffers& B, int e, int lane) {
   const size_t NT = (size_t)Pm_->num_envs * Pm_->num_dof;
   const int u = lane & 7;
+#ifndef LGX_SEA_GLOBAL_W
+  // The net's 972 floats (sea_in_scale .. sea_lin_w, contiguous in lgx_task_params) are copied
+  // into the LDS arena, idle at the top of a substep (the previous substep's constraint rows
+  // are dead, this one's not yet formed): the ~120 lane-indexed weight reads of a pass become
+  // LDS reads instead of vector-memory loads (8 distinct addresses per wave instruction).
+  {
+    const float* src = &Pm_->sea_in_scale[0];
+    for (int i = lane; i < SEA_WN; i += 64) lgx_dyn[i] = src[i];
+    __syncthreads();
+  }
+#endif
 #pragma unroll 1
   for (int pass = 0; pass < 2; ++pass) {
     // the weights a lane reads do not depend on the pass: an opaque table pointer per pass keeps
@@ -892,6 +934,13 @@ void sea_torques_lanes(Sh& s, const lgx_task_params* Pm_, const lgx_buffers& B, 
 #else
     const lgx_task_params* Pm = Pm_;
 #endif
+#ifndef LGX_SEA_GLOBAL_W
+    int wb = 0;  // opaque per pass, as Pm
+    __asm__ volatile("" : "+s"(wb));
+    const SeaW W{lgx_dyn + wb};
+#else
+    const SeaW W{Pm};
+#endif
     const int j = pass * 8 + (lane >> 3);
     const bool on = j < NJ;  // pass 1: lanes 0..31 (joints 8..11); lanes 32..63 follow along
     const int jj = on ? j : NJ - 1;
@@ -900,8 +949,10 @@ void sea_torques_lanes(Sh& s, const lgx_task_params* Pm_, const lgx_buffers& B, 
     float h1 = B.sea_hidden[(NT + r) * 8 + u], c1 = B.sea_cell[(NT + r) * 8 + u];
     const float in0 = (s.act[jj] * Pm->action_scale + Pm->default_dof_pos[jj]) - s.th[jj];
     const float x[2] = {in0 * Pm->sea_in_scale[0], s.thd[jj] * Pm->sea_in_scale[1]};
-    sea_unit_k<2, false>(Pm->sea_w_ih0, Pm->sea_w_hh0, Pm->sea_b_ih0, Pm->sea_b_hh0, u, x, 0.0f, h0, h0, c0);
-    sea_unit_k<8, true>(Pm->sea_w_ih1, Pm->sea_w_hh1, Pm->sea_b_ih1, Pm->sea_b_hh1, u, nullptr, h0, h1, h1, c1);
+    sea_unit_k<2, false>(W.w(SEA_OFF(sea_w_ih0)), W.w(SEA_OFF(sea_w_hh0)), W.w(SEA_OFF(sea_b_ih0)),
+                         W.w(SEA_OFF(sea_b_hh0)), u, x, 0.0f, h0, h0, c0);
+    sea_unit_k<8, true>(W.w(SEA_OFF(sea_w_ih1)), W.w(SEA_OFF(sea_w_hh1)), W.w(SEA_OFF(sea_b_ih1)),
+                        W.w(SEA_OFF(sea_b_hh1)), u, nullptr, h0, h1, h1, c1);
     if (on) {
       B.sea_hidden[r * 8 + u] = h0; B.sea_cell[r * 8 + u] = c0;
       B.sea_hidden[(NT + r) * 8 + u] = h1; B.sea_cell[(NT + r) * 8 + u] = c1;
@@ -916,7 +967,7 @@ void sea_torques_lanes(Sh& s, const lgx_task_params* Pm_, const lgx_buffers& B, 
         case 4: hk = unit_of<4>(h1); break; case 5: hk = unit_of<5>(h1); break;
         case 6: hk = unit_of<6>(h1); break; default: hk = unit_of<7>(h1); break;
       }
-      y += Pm->sea_lin_w[k] * hk;
+      y += W.w(SEA_OFF(sea_lin_w))[k] * hk;
     }
     if (on && u == 0) s.tau[j] = Pm->sea_out_scale * (y + Pm->sea_lin_b);
   }
