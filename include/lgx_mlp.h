@@ -98,6 +98,24 @@ typedef struct lgx_chain_desc {
   lgx_chain_layer layers[LGX_CHAIN_MAXL];
 } lgx_chain_desc;
 int32_t lgx_chain(const lgx_chain_desc* chains, int32_t n, void* stream);
+/* The adaptation encoder's forward for a pass that needs no gradient (the PPO update's
+ * adaptation latents, rsl_rl ppo.py's ROA regulariser; support_networks.py:116-175) in ONE
+ * launch: per history position t < H, y0 = ELU(w0 x_t + b0) (Linear P -> C1, x_t = x[r*ldx +
+ * t*P ..]); y1 = ELU(Conv1d(C1 -> C2, k1, s1)); y2 = ELU(Conv1d(C2 -> C3, k2, s2)); out =
+ * ELU(wf flatten(y2) + bf). Conv weights tap-major [C_out][k*C_in], wf position-major
+ * [NO][L2*C3] (hip_mlp._conv_w / _final_w). Only `out` [B][NO] is written; each layer's
+ * arithmetic and summation order are those of lgx_gemm (bit-identical to the per-layer
+ * launches). Requires 16 * (H*C1 + L1*C2 + L2*C3) floats <= 64 KB. */
+typedef struct lgx_adapt_args {
+  const float* x; int64_t ldx;
+  int32_t B, H, P;
+  const float* w0; const float* b0; int32_t C1;
+  const float* w1; const float* b1; int32_t C2, k1, s1;
+  const float* w2; const float* b2; int32_t C3, k2, s2;
+  const float* wf; const float* bf; int32_t NO;
+  float* out; int64_t ldo;
+} lgx_adapt_args;
+int32_t lgx_adaptation_forward(const lgx_adapt_args* a, void* stream);
 /* Split-K factors for n weight-gradient GEMMs launched as one group: one K chunk for all
  * (a multiple of 32 rows, >= 256), the smallest whose block count fits one residency wave
  * of the chip; every split >= 2. */

@@ -24,6 +24,7 @@
 //   taken from the unsplit fp32 values), reduced in fixed order by splitk_reduce.
 #include <hip/hip_runtime.h>
 #include <algorithm>
+#include <limits.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -748,6 +749,103 @@ __global__ __launch_bounds__(NT, 2) void chain_kernel(ChainParams P) {
       __syncthreads();
     }
   }
+}
+
+// ---------------------------------------------------------------- adaptation encoder (lgx_adaptation_forward)
+// The adaptation encoder's forward without gradient (support_networks.py:116-175: per-position
+// Linear(P -> C1) + ELU, Conv1d(C1 -> C2, k1, s1) + ELU, Conv1d(C2 -> C3, k2, s2) + ELU, flatten,
+// Linear(L2*C3 -> NO) + ELU) for AR rows per block in ONE launch: only the H history positions the
+// convolutions read are formed, every intermediate stays in LDS (fp32, channels-last: position
+// t's channels at [t*C + c], so a conv window is one contiguous run) and only the latent goes to
+// HBM. Each stage is a GEMM over "virtual rows" (row, output position) whose A row is a window of
+// the previous stage; per output the MFMA sequence is gemm_tile's (32-deep K steps in order, fp32
+// values split hi/lo as they are read, lo*hi + hi*lo + hi*hi, zero past K) and so is the bias +
+// ELU epilogue: bit-identical to the per-layer launches of hip_mlp._AdaptationFn.
+constexpr int AR = 16;  // rows per block
+struct AdaptParams {
+  lgx_adapt_args a;
+  int L1, L2;
+};
+
+// one GEMM stage: vrows virtual rows, A(v, k) = lda_(v)[k] for k < K (a global or LDS row),
+// W [N][K] k-contiguous, epilogue bias + ELU, result to st_(v, n) for n < N
+template <class ALoad, class Store>
+__device__ __forceinline__ void adapt_stage(int vrows, int K, int N, const float* __restrict__ W,
+                                            const float* __restrict__ bias, ALoad lda_, Store st_) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fc = lane >> 4;
+  const int nrt = (vrows + 15) / 16, nct = (N + 15) / 16, nsteps = (K + BKS - 1) / BKS;
+  for (int item = wave; item < nrt * nct; item += NT / 64) {
+    const int rt = item / nct, ct = item % nct;
+    const int v = min(rt * 16 + fr, vrows - 1);
+    const int n = min(ct * 16 + fr, N - 1);
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    const float* arow = lda_(v);
+    const float* brow = W + n * K;
+    for (int s = 0; s < nsteps; ++s) {
+      const int k = s * BKS + fc * 8;
+      float av[8], bv[8];
+      if (k + 8 <= K) {  // vector loads (4-B alignment suffices for global dwordx4)
+        const f32x4u a0 = *reinterpret_cast<const f32x4u*>(arow + k), a1 = *reinterpret_cast<const f32x4u*>(arow + k + 4);
+        const f32x4u b0 = *reinterpret_cast<const f32x4u*>(brow + k), b1 = *reinterpret_cast<const f32x4u*>(brow + k + 4);
+        av[0] = a0.x; av[1] = a0.y; av[2] = a0.z; av[3] = a0.w; av[4] = a1.x; av[5] = a1.y; av[6] = a1.z; av[7] = a1.w;
+        bv[0] = b0.x; bv[1] = b0.y; bv[2] = b0.z; bv[3] = b0.w; bv[4] = b1.x; bv[5] = b1.y; bv[6] = b1.z; bv[7] = b1.w;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          av[j] = k + j < K ? arow[k + j] : 0.f;
+          bv[j] = k + j < K ? brow[k + j] : 0.f;
+        }
+      }
+      bf16x8 ah, al, bh, bl;
+      split8(av, ah, al);
+      split8(bv, bh, bl);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, acc, 0, 0, 0);
+    }
+    // C/D map: column fr of the tile, rows 4 fc + r
+    const int nn = ct * 16 + fr;
+    if (nn < N) {
+      const float bn = bias[nn];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int vv = rt * 16 + fc * 4 + r;
+        if (vv < vrows) st_(vv, nn, elu(acc[r] + bn));
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(NT) void adapt_fwd_kernel(AdaptParams P) {
+  const lgx_adapt_args& a = P.a;
+  extern __shared__ __align__(16) float alds[];
+  const int r0 = blockIdx.x * AR;
+  const int H = a.H, C1 = a.C1, C2 = a.C2, C3 = a.C3, L1 = P.L1, L2 = P.L2;
+  float* y0 = alds;                  // [AR][H*C1]
+  float* y1 = y0 + AR * H * C1;      // [AR][L1*C2]
+  float* y2 = y1 + AR * L1 * C2;     // [AR][L2*C3]
+  const int last = a.B - 1 - r0;     // last valid local row
+  const float* x0 = a.x + (int64_t)r0 * a.ldx;
+  const int ldx = (int)a.ldx, Pn = a.P;
+  // per-position Linear(P -> C1) over H positions: virtual row v = (r, t)
+  adapt_stage(AR * H, Pn, C1, a.w0, a.b0,
+              [&](int v) { return x0 + min(v / H, last) * ldx + (v % H) * Pn; },
+              [&](int v, int n, float y) { y0[(v / H) * (H * C1) + (v % H) * C1 + n] = y; });
+  __syncthreads();
+  // Conv1d(C1 -> C2, k1, s1): window t of row r = y0[r][t*s1*C1 .. + k1*C1)
+  adapt_stage(AR * L1, a.k1 * C1, C2, a.w1, a.b1,
+              [&](int v) { return (const float*)y0 + (v / L1) * (H * C1) + (v % L1) * a.s1 * C1; },
+              [&](int v, int n, float y) { y1[(v / L1) * (L1 * C2) + (v % L1) * C2 + n] = y; });
+  __syncthreads();
+  adapt_stage(AR * L2, a.k2 * C2, C3, a.w2, a.b2,
+              [&](int v) { return (const float*)y1 + (v / L2) * (L1 * C2) + (v % L2) * a.s2 * C2; },
+              [&](int v, int n, float y) { y2[(v / L2) * (L2 * C3) + (v % L2) * C3 + n] = y; });
+  __syncthreads();
+  adapt_stage(AR, L2 * C3, a.NO, a.wf, a.bf, [&](int v) { return (const float*)y2 + v * (L2 * C3); },
+              [&](int v, int n, float y) {
+                if (v <= last) a.out[(int64_t)(r0 + v) * a.ldo + n] = y;
+              });
 }
 
 // C (=|+=) epilogue(sum_z ws[z]) and colsum[m] (=|+=) sum_z colsum_ws[z][m]. Each thread owns
@@ -2004,6 +2102,31 @@ int32_t lgx_gemm_group(const lgx_gemm_args* args, int32_t n, void* stream) {
     LGX_GROUP_LAUNCH(G_DW)
   }
 #undef LGX_GROUP_LAUNCH
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : fail(hipGetErrorString(e));
+}
+
+int32_t lgx_adaptation_forward(const lgx_adapt_args* a, void* stream) {
+  using namespace lgxm;
+  if (!a) return fail("lgx_adaptation_forward: null args");
+  if (a->B < 0) return fail("lgx_adaptation_forward: B >= 0");
+  if (a->B == 0) return 0;
+  if (a->H < 1 || a->P < 1 || a->C1 < 1 || a->C2 < 1 || a->C3 < 1 || a->NO < 1 || a->k1 < 1 || a->s1 < 1 ||
+      a->k2 < 1 || a->s2 < 1)
+    return fail("lgx_adaptation_forward: dimensions must be positive");
+  AdaptParams P;
+  P.a = *a;
+  P.L1 = (a->H - a->k1) / a->s1 + 1;
+  P.L2 = (P.L1 - a->k2) / a->s2 + 1;
+  if (a->H < a->k1 || P.L1 < a->k2) return fail("lgx_adaptation_forward: history shorter than a kernel");
+  if (!a->x || a->ldx < (int64_t)a->H * a->P || !a->w0 || !a->b0 || !a->w1 || !a->b1 || !a->w2 || !a->b2 || !a->wf ||
+      !a->bf || !a->out || a->ldo < a->NO)
+    return fail("lgx_adaptation_forward: bad operands");
+  const int64_t floats = (int64_t)AR * ((int64_t)a->H * a->C1 + (int64_t)P.L1 * a->C2 + (int64_t)P.L2 * a->C3);
+  if (floats * 4 > 64 * 1024 || (int64_t)a->B * a->ldx > INT32_MAX)
+    return fail("lgx_adaptation_forward: sizes beyond the fused kernel's LDS / 32-bit offsets");
+  hipLaunchKernelGGL(adapt_fwd_kernel, dim3((unsigned)((a->B + AR - 1) / AR)), dim3(NT), (size_t)floats * 4,
+                     static_cast<hipStream_t>(stream), P);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : fail(hipGetErrorString(e));
 }

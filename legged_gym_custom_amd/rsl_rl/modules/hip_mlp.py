@@ -28,7 +28,7 @@ EXPORTED = ["lgx_mlp_abi_version", "lgx_mlp_sizeof_gemm_args", "lgx_mlp_pick_spl
             "lgx_aux_loss_forward", "lgx_aux_loss_backward", "lgx_ppo_tail", "lgx_gemm_group",
             "lgx_mlp_pick_split_group", "lgx_gae", "lgx_normalize_advantages",
             "lgx_gather_rows", "lgx_transpose_batch", "lgx_loss_heads_forward", "lgx_loss_heads_backward",
-            "lgx_track_episodes", "lgx_chain"]
+            "lgx_track_episodes", "lgx_chain", "lgx_adaptation_forward"]
 TAIL_MAX_LOSSES = 8
 COPY_MAX = 16
 SPLITK_MAX = 24
@@ -39,6 +39,8 @@ CHAIN_MAX, CHAIN_MAXL, CHAIN_MAXW = 4, 3, 256
 # update's 24,576 rows one grouped launch per depth measured faster (profiles/r03_chain.txt).
 # Dev knobs: LGX_CHAIN=0 (never chain), LGX_CHAIN_ROWS (the row limit).
 USE_CHAIN = os.environ.get("LGX_CHAIN", "1") != "0"
+# dev knob: LGX_ADAPT_FUSED=0 runs the no-gradient adaptation encoder as per-layer launches
+USE_ADAPT_FUSED = os.environ.get("LGX_ADAPT_FUSED", "1") != "0"
 CHAIN_ROWS = int(os.environ.get("LGX_CHAIN_ROWS", "8192"))
 
 
@@ -133,6 +135,16 @@ class ChainDesc(C.Structure):
                 ("layers", ChainLayer * CHAIN_MAXL)]
 
 
+class AdaptArgs(C.Structure):
+    """Mirror of lgx_adapt_args."""
+    _fields_ = [("x", C.c_void_p), ("ldx", C.c_int64), ("B", C.c_int32), ("H", C.c_int32), ("P", C.c_int32),
+                ("w0", C.c_void_p), ("b0", C.c_void_p), ("C1", C.c_int32),
+                ("w1", C.c_void_p), ("b1", C.c_void_p), ("C2", C.c_int32), ("k1", C.c_int32), ("s1", C.c_int32),
+                ("w2", C.c_void_p), ("b2", C.c_void_p), ("C3", C.c_int32), ("k2", C.c_int32), ("s2", C.c_int32),
+                ("wf", C.c_void_p), ("bf", C.c_void_p), ("NO", C.c_int32),
+                ("out", C.c_void_p), ("ldo", C.c_int64)]
+
+
 class GaeArgs(C.Structure):
     """Mirror of lgx_gae_args."""
     _fields_ = [(n, C.c_void_p) for n in ("rewards", "dones", "values", "last_values", "returns", "advantages")] + \
@@ -194,6 +206,8 @@ def lib():
     L.lgx_splitk_reduce_batch.restype = C.c_int32
     L.lgx_chain.argtypes = [vp, C.c_int32, vp]
     L.lgx_chain.restype = C.c_int32
+    L.lgx_adaptation_forward.argtypes = [vp, vp]
+    L.lgx_adaptation_forward.restype = C.c_int32
     if L.lgx_mlp_abi_version() != ABI_VERSION:
         raise MlpLibError("liblgx_mlp ABI version mismatch; rebuild")
     L.lgx_mlp_sizeof_gemm_args.restype = C.c_int32
@@ -1037,6 +1051,20 @@ class _AdaptationFn(torch.autograd.Function):
         # decides: want_grad = grad mode on and some input requires grad)
         inplace = (not want_grad and Hs > H and
                    h.storage_offset() + Bn * Hs * P <= h.untyped_storage().nbytes() // h.element_size())
+        if not want_grad and USE_ADAPT_FUSED and h.stride(2) == 1 and h.stride(1) == P and Bn > 0:
+            # no gradient: the whole encoder in one launch (lgx_adaptation_forward), reading the
+            # history rows in place; bit-identical to the per-layer launches below
+            if inplace:
+                ADAPT_INPLACE_CALLS += 1
+            W1, W2, Wf = _conv_w(c1_w), _conv_w(c2_w), _final_w(f_w, C3, L2)
+            out = torch.empty(Bn, f_w.shape[0], device=dev)
+            args = AdaptArgs(x=h.data_ptr(), ldx=h.stride(0), B=Bn, H=H, P=P, w0=_ptr(fc_w), b0=_ptr(fc_b), C1=C1,
+                             w1=_ptr(W1), b1=_ptr(c1_b), C2=C2, k1=k1, s1=s1, w2=_ptr(W2), b2=_ptr(c2_b), C3=C3,
+                             k2=k2, s2=s2, wf=_ptr(Wf), bf=_ptr(f_b), NO=f_w.shape[0], out=_ptr(out),
+                             ldo=out.stride(0))
+            _check(lib().lgx_adaptation_forward(C.byref(args), _stream()), "lgx_adaptation_forward")
+            ctx.dims = dims
+            return out
         if inplace:
             ADAPT_INPLACE_CALLS += 1
             x = h.as_strided((Bn * Hs, P), (P, 1))

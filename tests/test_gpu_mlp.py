@@ -128,6 +128,25 @@ def test_adaptation_encoder_inplace_history_bitwise():
     assert torch.equal(a, b) and torch.equal(a, c.detach()) and torch.equal(a, d)
 
 
+@pytest.mark.parametrize("B", [1, 2001, 98304])
+def test_adaptation_fused_forward_bitwise(B, monkeypatch):
+    """lgx_adaptation_forward (the whole encoder in one launch, no gradient) == the per-layer
+    launches (LGX_ADAPT_FUSED=0), bitwise, on the history read in place from obs rows and on a
+    packed history; B = 1, a ragged 2001, and the update's 98,304 rows."""
+    from legged_gym_custom_amd.rsl_rl.modules.support_networks import AdaptationEncoder
+    torch.manual_seed(7)
+    enc = AdaptationEncoder(num_proprio=52, history_buffer_length=10, output_dim=20).to(dev)
+    obs = torch.randn(B, 572, device=dev)
+    hist = obs[:, :-52].reshape(-1, 10, 52)
+    outs = {}
+    for fused in (True, False):
+        monkeypatch.setattr(H, "USE_ADAPT_FUSED", fused)
+        with torch.no_grad():
+            outs[fused] = (enc(hist), enc(hist.contiguous()))
+    assert torch.equal(outs[True][0], outs[False][0]) and torch.equal(outs[True][1], outs[False][1])
+    assert torch.equal(outs[True][0], outs[True][1])
+
+
 @pytest.mark.parametrize("clipped", [True, False])
 def test_ppo_head_matches_torch_autograd(clipped):
     """lgx_ppo_head_{forward,backward} vs the reference's loss code (ppo.py:196-262 over
