@@ -1,0 +1,106 @@
+/* lgx_s8.h — C ABI of liblgx_s8.so: the learner's GEMM core on pre-split operands (MI355X).
+ *
+ * Replaces the same nn.Linear + nn.ELU chains as lgx_mlp.h (reference rsl_rl
+ * modules/actor_critic.py:64-87, support_networks.py:22-112; forward ppo.py:186-206, backward
+ * ppo.py:262 / :207) inside the PPO update, with every GEMM operand stored PRE-SPLIT by the
+ * kernel that produced it instead of split in each GEMM's K loop.
+ *
+ * S8 layout ("split rows"). A logical fp32 matrix X[rows][cols] is stored as 4-byte words,
+ * row pitch `ld` elements (a multiple of 8; 16-B aligned rows). Columns are grouped by 8: group
+ * g of row r occupies bytes [32 g, 32 g + 32) of the row: 8 x bf16 hi, then 8 x bf16 lo, where
+ *     hi = bf16_rne(x),  lo = bf16_rne(x - hi)        (x ~ hi + lo to ~2^-17 relative)
+ * — the split the fp32 GEMMs of lgx_mlp.h perform on the fly, so the products are the same
+ * (3 x bf16 MFMA: lo*hi + hi*lo + hi*hi per 32-deep K step, fp32 accumulation).
+ * Pad columns [cols, ld) hold zeros. The producers write them in the last group of a row (the
+ * rest is never written), so an S8 buffer is allocated zeroed once and reused.
+ *
+ * One GEMM:  C[m][n] = epilogue( sum_k A(m, k) B(k, n) ), with each operand in one of two modes:
+ *     ROW  A(m, k) = S8 element (m, k) — k along the source row (forward X, W; input-grad dY)
+ *     TR   A(m, k) = S8 element (k, m) — k = source row (input-grad W; weight-grad dY and X)
+ * so  forward     Y  = X W^T + b     A = X ROW,  B = W ROW, then bias, ELU
+ *     input grad  dX = dY W          A = dY ROW, B = W TR,  then * ELU'(Y_prev) (Y_prev in S8)
+ *     weight grad dW = dY^T X        A = dY TR,  B = X TR,  split-K fp32 partials
+ * Operand contract: a ROW operand's pitch covers round_up(K, 32) columns (zeros past K in at
+ * least one of the two operands; the producers' zero pads give that); a TR operand's rows
+ * [K, round_up(K, 32)) exist (zero in at least one operand). Rows/columns past M or N are read
+ * clamped and never stored.
+ * All work is stream-ordered on `stream` (hipStream_t). Return 0 on success, negative on invalid
+ * arguments or launch failure (lgx_s8_last_error).
+ */
+#ifndef LGX_S8_H
+#define LGX_S8_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LGX_S8_ABI_VERSION 1
+
+enum { LGX_S8_FWD = 0, LGX_S8_DX = 1, LGX_S8_DW = 2 };  /* GEMM kinds (operand modes above) */
+
+enum {
+  LGX_S8_EPI_BIAS = 1,   /* FWD: + bias[n] */
+  LGX_S8_EPI_ELU = 2,    /* FWD: then ELU(alpha = 1) */
+  LGX_S8_EPI_DELU = 4,   /* DX: * ELU'(z) from the ELU output y = act (S8): y > 0 ? 1 : y + 1 */
+  LGX_S8_EPI_ACCUM = 8   /* DW with split 1: C += result */
+};
+
+typedef struct lgx_s8_gemm_args {
+  const void* A; int64_t lda;   /* S8 operands, pitch in elements */
+  const void* B; int64_t ldb;
+  int32_t M, N, K;
+  int32_t epilogue;             /* LGX_S8_EPI_* */
+  void* C; int64_t ldc;         /* FWD / DX: S8 output (optional if C32 is set) */
+  float* C32; int64_t ldc32;    /* FWD / DX: fp32 copy of the output (optional); DW: fp32 output
+                                   (split 1) or the partial workspace [split][M][N] (split > 1) */
+  const float* bias;            /* FWD, LGX_S8_EPI_BIAS: [N] */
+  const void* act; int64_t ld_act;      /* DX, LGX_S8_EPI_DELU: Y_prev (S8) */
+  const float* addend; int64_t ld_add;  /* DX (optional): + addend[m][n] for n < add_cols, after ELU' */
+  int32_t add_cols;
+  float* colsum_ws;             /* FWD / DX (optional): [tiles_m][N] fp32 column sums of the
+                                   output over each 128-row tile (the next weight gradient's
+                                   bias gradient, reduced with lgx_s8_reduce) */
+  int32_t split;                /* DW: K split (>= 1); kchunk = round_up(ceil(K / split), 32) */
+  int32_t pad0;
+} lgx_s8_gemm_args;
+
+/* fp32 -> S8 (weights after each optimizer step; the update's network inputs, gathered in the
+ * minibatch permutation; the loss heads' narrow gradients). Row r of dst = split of src row
+ * (idx ? idx[r] : r), zeros in columns [cols, round_up(cols, 8)). With colsum_ws set (cols <= 64)
+ * also the column sums of each 256-row block: colsum_ws[blk * cols + c] (blk = r / 256). */
+typedef struct lgx_s8_split_args {
+  const float* src; int64_t ld_src;
+  void* dst; int64_t ld_dst;    /* dst points at the S8 group of column 0 (a multiple of 8) */
+  int32_t rows, cols;
+  float* colsum_ws;
+  const int64_t* idx;           /* optional row gather (rollout_storage.py:141-147's permutation) */
+} lgx_s8_split_args;
+
+/* out[r * ld_out + c] (+)= sum_{s < nsplit} ws[s * stride + r * ld_ws + c], r < rows, c < cols
+ * (fixed order: deterministic) — split-K partials into weight gradients (also column spans:
+ * a weight whose input columns sit at other positions in S8 space), bias-gradient partials. */
+typedef struct lgx_s8_reduce_args {
+  const float* ws; int64_t stride, ld_ws;
+  float* out; int64_t ld_out;
+  int32_t rows, cols, nsplit, accumulate;
+} lgx_s8_reduce_args;
+
+#define LGX_S8_GROUP_MAX 20
+#define LGX_S8_BATCH_MAX 48
+#define LGX_S8_TILE_M 128        /* rows of one colsum_ws partial (FWD / DX) */
+#define LGX_S8_SPLIT_ROWS 256    /* rows of one lgx_s8_split colsum partial */
+
+int32_t lgx_s8_abi_version(void);
+int32_t lgx_s8_sizeof_gemm_args(void);
+const char* lgx_s8_last_error(void);
+/* n independent GEMMs of one kind in one launch (each problem's tiles dealt over the 8 XCDs). */
+int32_t lgx_s8_gemm_group(const lgx_s8_gemm_args* args, int32_t n, int32_t kind, void* stream);
+/* Split factors for n weight-gradient GEMMs sharing one launch (out[i] >= 1). */
+int32_t lgx_s8_pick_split(const int32_t* M, const int32_t* N, const int32_t* K, int32_t n, int32_t* out);
+int32_t lgx_s8_split(const lgx_s8_split_args* args, int32_t n, void* stream);
+int32_t lgx_s8_reduce(const lgx_s8_reduce_args* args, int32_t n, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -170,15 +170,10 @@ LGX_DEV const T* opaque(const T* p) {
 // rows ([N,13] root state, [N,24] dof state, ...) share 128-B lines with env e +- 1's, so neighbouring
 // envs are given blocks of the same XCD (one L2 fetches the shared line once): XCD x = b % 8 runs
 // the contiguous env range [x*q + min(x, r), ...) of q + (x < r) envs (N = 8q + r) — a bijection
-// of [0, N). LGX_ENV_LINEAR: env = block (for A/B).
+// of [0, N).
 LGX_DEV int env_of_block(int b, int n) {
-#ifdef LGX_ENV_LINEAR
-  (void)n;
-  return b;
-#else
   const int q = n >> 3, r = n & 7, x = b & 7, j = b >> 3;
   return x * q + min(x, r) + j;
-#endif
 }
 
 #ifndef LGX_ROW_PRIO
@@ -556,61 +551,16 @@ LGX_DEV bool height_in_triangle(f3 p, f3 a, f3 b, f3 c, float& z) {
   return true;
 }
 
-LGX_DEV TerrainHit terrain_contact(const lgx_task_params* Pm, const lgx_buffers& B, f3 x, float r) {
-  const float hs = Pm->horizontal_scale, vs = Pm->vertical_scale;
-  const int rows = Pm->hf_rows, cols = Pm->hf_cols;
-  const float gx = x.x + Pm->border_size, gy = x.y + Pm->border_size;
-  const int ci = (int)floorf(gx / hs), cj = (int)floorf(gy / hs);
-  const f3 p = mk(gx - (float)ci * hs, gy - (float)cj * hs, x.z);  // local to vertex (ci, cj)
-  // a cell's triangles span [i-1, i+2] hs after the +-1 shifts
-  const int i0 = max(ci + (int)ceilf((p.x - r) / hs) - 2, 0), i1 = min(ci + (int)floorf((p.x + r) / hs) + 1, rows - 2);
-  const int j0 = max(cj + (int)ceilf((p.y - r) / hs) - 2, 0), j1 = min(cj + (int)floorf((p.y + r) / hs) + 1, cols - 2);
-  const uint32_t* mesh = B.terrain_mesh;
-  float best = 3.0e38f, zs = -3.0e38f;
-  f3 q = mk(0.f, 0.f, -3.0e38f), fn = mk(0.f, 0.f, 1.f);
-  for (int i = i0; i <= i1; ++i) {
-    for (int j = j0; j <= j1; ++j) {
-      const f3 v00 = mesh_vertex(mesh, cols, i, j, ci, cj, hs, vs);
-      const f3 v01 = mesh_vertex(mesh, cols, i, j + 1, ci, cj, hs, vs);
-      const f3 v10 = mesh_vertex(mesh, cols, i + 1, j, ci, cj, hs, vs);
-      const f3 v11 = mesh_vertex(mesh, cols, i + 1, j + 1, ci, cj, hs, vs);
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const f3 a = v00, b = t == 0 ? v11 : v10, c = t == 0 ? v01 : v11;
-        const f3 cpt = closest_on_triangle(p, a, b, c);
-        const f3 d = p - cpt;
-        const float d2 = dot(d, d);
-        if (d2 < best) { best = d2; q = cpt; fn = cross(b - a, c - a); }
-        float z;
-        if (height_in_triangle(p, a, b, c, z)) zs = fmaxf(zs, z);
-      }
-    }
-  }
-  TerrainHit h;
-  if (best >= 3.0e38f) {  // outside the field: nothing to touch
-    h.depth = -3.0e38f;
-    h.n = mk(0.f, 0.f, 1.f);
-    return h;
-  }
-  const float dist = sqrtf(best);
-  const bool below = p.z < zs;
-  h.depth = below ? r + dist : r - dist;
-  if (dist > 1e-6f) {
-    h.n = (p - q) * ((below ? -1.0f : 1.0f) / dist);
-  } else {
-    h.n = fn * rsqrtf(fmaxf(dot(fn, fn), 1e-30f));
-  }
-  return h;
-}
-
-// The same query for every contact candidate of the wave at once, the work spread over lanes:
+// The trimesh contact query (closest point over the triangles of the cells a +-1 wall shift can
+// reach; the host backend's / oracle's terrain_contact state it serially) for every contact
+// candidate of the wave at once, the work spread over lanes:
 // each candidate lane (cand) bounds its cell range, drops out when its sphere is above every
 // vertex the range can reach (a conservative block maximum packed in the mesh words' bits
 // 20-31, utils/terrain_utils.pack_mesh: such a sphere is farther than r + contact_margin from
 // the surface, so it forms no row either way), and the remaining (candidate, cell) tasks run
 // 64 per round, one per lane; each candidate lane then folds its tasks' closest points in the
 // serial loop's (i, j, triangle) order with the same strict comparison, so the result equals
-// terrain_contact's exactly. One-candidate-per-lane made a wave as slow as its candidate with
+// the serial terrain_contact's exactly. One-candidate-per-lane made a wave as slow as its candidate with
 // the most cells (25 cells x 2 triangles for a 0.1 m sphere) for all 22 (ANYmal) or 55 (Go2)
 // lanes at once. Scratch: the LDS arena (rows are formed after detection).
 constexpr int MESH_BLOCK = 8;  // vertices per block side of the packed block maxima
@@ -746,100 +696,28 @@ LGX_DEV void contact_tangents(f3 n, f3& t1, f3& t2) {
   t2 = cross(n, t1);
 }
 
-// ---- ANYmal series-elastic actuator net (anymal.py:71-81)
-// One joint per lane: 2-layer LSTM(2 -> 8 -> 8) step + Linear(8 -> 1), torch.nn.LSTM gate
-// order i f g o, state [2, N*D, 8] in HBM (read and written once per substep). The
-// weights are wave-uniform (task params), so they stream through scalar loads; one
-// hidden unit's four gates are formed at a time to keep the live set small.
-LGX_DEV float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
-
-template <int NIN>
-LGX_DEV void sea_lstm_layer(const float* __restrict__ w_ih, const float* __restrict__ w_hh,
-                            const float* __restrict__ b_ih, const float* __restrict__ b_hh, const float* x, float* h,
-                            float* c) {
-  // one hidden unit per iteration (not unrolled: only that unit's 4 gate rows of weights are
-  // live); c[u] / hn[u] are picked and placed by selects so the arrays stay in registers
-  float hn[8];
-#pragma unroll 1
-  for (int u = 0; u < 8; ++u) {
-    float g4[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int g = q * 8 + u;
-      float a = 0.0f, b = 0.0f;
-#pragma unroll
-      for (int k = 0; k < NIN; ++k) a += w_ih[g * NIN + k] * x[k];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) b += w_hh[g * 8 + k] * h[k];
-      g4[q] = (a + b_ih[g]) + (b + b_hh[g]);
-    }
-    const float ig = sigmoidf_(g4[0]), fg = sigmoidf_(g4[1]), gg = tanhf(g4[2]), og = sigmoidf_(g4[3]);
-    float cu = 0.f;
-#pragma unroll
-    for (int v = 0; v < 8; ++v) cu = v == u ? c[v] : cu;
-    cu = fg * cu + ig * gg;
-    const float hu = og * tanhf(cu);
-#pragma unroll
-    for (int v = 0; v < 8; ++v) {
-      c[v] = v == u ? cu : c[v];
-      hn[v] = v == u ? hu : hn[v];
-    }
-  }
-#pragma unroll
-  for (int u = 0; u < 8; ++u) h[u] = hn[u];
-}
-
-LGX_DEV float sea_torque(const lgx_task_params* Pm, const lgx_buffers& B, int e, int j, float in0, float in1) {
-  const size_t NT = (size_t)Pm->num_envs * Pm->num_dof, r = (size_t)e * Pm->num_dof + j;
-  float4* hp0 = reinterpret_cast<float4*>(B.sea_hidden + r * 8);
-  float4* cp0 = reinterpret_cast<float4*>(B.sea_cell + r * 8);
-  float4* hp1 = reinterpret_cast<float4*>(B.sea_hidden + (NT + r) * 8);
-  float4* cp1 = reinterpret_cast<float4*>(B.sea_cell + (NT + r) * 8);
-  float h0[8], c0[8], h1[8], c1[8];
-  auto ld8 = [](const float4* p, float* v) {
-    const float4 a = p[0], b = p[1];
-    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-  };
-  auto st8 = [](float4* p, const float* v) {
-    p[0] = make_float4(v[0], v[1], v[2], v[3]);
-    p[1] = make_float4(v[4], v[5], v[6], v[7]);
-  };
-  ld8(hp0, h0); ld8(cp0, c0); ld8(hp1, h1); ld8(cp1, c1);
-  const float x[2] = {in0 * Pm->sea_in_scale[0], in1 * Pm->sea_in_scale[1]};
-  sea_lstm_layer<2>(Pm->sea_w_ih0, Pm->sea_w_hh0, Pm->sea_b_ih0, Pm->sea_b_hh0, x, h0, c0);
-  sea_lstm_layer<8>(Pm->sea_w_ih1, Pm->sea_w_hh1, Pm->sea_b_ih1, Pm->sea_b_hh1, h0, h1, c1);
-  st8(hp0, h0); st8(cp0, c0); st8(hp1, h1); st8(cp1, c1);
-  float y = 0.0f;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) y += Pm->sea_lin_w[k] * h1[k];
-  return Pm->sea_out_scale * (y + Pm->sea_lin_b);
-}
-
-// The same actuator net lane-parallel over hidden units (the kernel's form): lane L serves unit
+// ---- ANYmal series-elastic actuator net (anymal.py:71-81): 2-layer
+// LSTM(2 -> 8 -> 8) step + Linear(8 -> 1), torch.nn.LSTM gate order i f g o, state [2, N*D, 8] in
+// HBM (read and written once per substep). The serial per-joint statement of it is the host
+// backend's sea_torque (lgx_env_host.cpp) and the oracle's (oracle/lgx_oracle.c).
+// The actuator net lane-parallel over hidden units (the kernel's form): lane L serves unit
 // u = L & 7 of joint j = 8 * pass + (L >> 3) — joints 0..7, then 8..11 on lanes 0..31 — and holds
 // only that unit's h and c of both layers. A gate row's dot product over the 8 units of a layer
 // takes the joint's other units by ds_swizzle inside the 8-lane group; every sum runs in the order
-// of sea_torque above (the host backend's and the oracle's), so the torques are the same. Weight
+// of the serial sea_torque (the host backend's and the oracle's), so the torques are the same. Weight
 // rows are lane-indexed (vector loads of the params, L1-resident): 1/8 of the per-lane work and
 // transcendentals of one-joint-per-lane, and 4 state values per lane instead of 32.
 // The SEA net's weight block: lgx_task_params from sea_in_scale through sea_lin_w (972 floats),
-// read either from the LDS arena copy (product) or from the params (LGX_SEA_GLOBAL_W, for A/B).
+// read from its LDS arena copy.
 #define SEA_OFF(f) ((int)((offsetof(lgx_task_params, f) - offsetof(lgx_task_params, sea_in_scale)) / sizeof(float)))
 constexpr int SEA_WN = (int)((offsetof(lgx_task_params, sea_lin_w) + sizeof(float) * 8 -
                               offsetof(lgx_task_params, sea_in_scale)) / sizeof(float));
 static_assert(SEA_WN == 972, "the SEA weight block is contiguous in lgx_task_params");
 static_assert(SEA_WN <= ROWS_FLOATS, "the SEA weights fit the arena");
-#ifndef LGX_SEA_GLOBAL_W
 struct SeaW {
   float* base;  // LDS
   LGX_DEV const float* w(int off) const { return base + off; }
 };
-#else
-struct SeaW {
-  const lgx_task_params* Pm;
-  LGX_DEV const float* w(int off) const { return &Pm->sea_in_scale[0] + off; }
-};
-#endif
 template <int K>
 LGX_DEV float unit_of(float v) {  // unit K of this lane's 8-lane group
   return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), 0x18 | (K << 5)));
@@ -885,12 +763,6 @@ LGX_DEV void sea_unit_k(const float* __restrict__ w_ih, const float* __restrict_
   float g4[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) g4[q] = (a[q] + b_ih[q * 8 + u]) + (b[q] + b_hh[q * 8 + u]);
-#ifdef LGX_SEA_OCML
-  // dev knob: ocml expf / IEEE division / tanhf (the host backend's and the oracle's functions)
-  const float ig = sigmoidf_(g4[0]), fg = sigmoidf_(g4[1]), gg = tanhf(g4[2]), og = sigmoidf_(g4[3]);
-  c = fg * c + ig * gg;
-  h = og * tanhf(c);
-#else
   // the gates on the hardware exp / rcp (v_exp_f32, v_rcp_f32, ~1 ulp each: sigmoid within
   // ~3e-7 relative, tanh(x) = 2 sigmoid(2x) - 1 within ~2e-7 absolute), ~40 instructions per
   // unit fewer than ocml expf / division / tanhf: C3 kernel 389 -> 372 us
@@ -899,22 +771,15 @@ LGX_DEV void sea_unit_k(const float* __restrict__ w_ih, const float* __restrict_
   const float ig = sg(g4[0]), fg = sg(g4[1]), gg = 2.0f * sg(2.0f * g4[2]) - 1.0f, og = sg(g4[3]);
   c = fg * c + ig * gg;
   h = og * (2.0f * sg(2.0f * c) - 1.0f);
-#endif
 }
 // all 12 joints' SEA torques into s.tau (every lane of the wave takes part), one unit per lane
 // over two passes. (Two units per lane in one pass measured 425-459 us vs 433 for C3's kernel,
 // with 33-38 spilled VGPRs: not kept, profiles/r03_sea_spill_fix.txt.)
-#ifndef LGX_SEA_CALL
 // inlined (54 VGPRs spill at the 4-waves-per-SIMD budget, yet C3's kernel is 589 us against 611
 // as a call and 642 one joint per lane: profiles/r03_bench_anymal_c_rough_sea_waves.txt)
-LGX_DEV
-#else
-__device__ __attribute__((noinline))
-#endif
-void sea_torques_lanes(Sh& s, const lgx_task_params* Pm_, const lgx_buffers& B, int e, int lane) {
+LGX_DEV void sea_torques_lanes(Sh& s, const lgx_task_params* Pm_, const lgx_buffers& B, int e, int lane) {
   const size_t NT = (size_t)Pm_->num_envs * Pm_->num_dof;
   const int u = lane & 7;
-#ifndef LGX_SEA_GLOBAL_W
   // The net's 972 floats (sea_in_scale .. sea_lin_w, contiguous in lgx_task_params) are copied
   // into the LDS arena, idle at the top of a substep (the previous substep's constraint rows
   // are dead, this one's not yet formed): the ~120 lane-indexed weight reads of a pass become
@@ -924,23 +789,14 @@ void sea_torques_lanes(Sh& s, const lgx_task_params* Pm_, const lgx_buffers& B, 
     for (int i = lane; i < SEA_WN; i += 64) lgx_dyn[i] = src[i];
     __syncthreads();
   }
-#endif
 #pragma unroll 1
   for (int pass = 0; pass < 2; ++pass) {
     // the weights a lane reads do not depend on the pass: an opaque table pointer per pass keeps
     // them from being hoisted out of this loop (all ~130 live at once) and spilled
-#ifndef LGX_SEA_HOIST
     const lgx_task_params* Pm = opaque(Pm_);
-#else
-    const lgx_task_params* Pm = Pm_;
-#endif
-#ifndef LGX_SEA_GLOBAL_W
     int wb = 0;  // opaque per pass, as Pm
     __asm__ volatile("" : "+s"(wb));
     const SeaW W{lgx_dyn + wb};
-#else
-    const SeaW W{Pm};
-#endif
     const int j = pass * 8 + (lane >> 3);
     const bool on = j < NJ;  // pass 1: lanes 0..31 (joints 8..11); lanes 32..63 follow along
     const int jj = on ? j : NJ - 1;
@@ -989,16 +845,7 @@ LGX_DEV void substep(Sh& s, const lgx_model* M_, const lgx_task_params* Pm_, con
   {
 #pragma clang fp contract(off)
     if (ACTNET) {
-#ifdef LGX_SEA_PER_JOINT  // (the one-joint-per-lane form, for A/B)
-      if (lane < NJ) {
-        const int j = lane;
-        s.tau[j] = sea_torque(Pm, B, env_of_block(blockIdx.x, gridDim.x), j,
-                              (s.act[j] * Pm->action_scale + Pm->default_dof_pos[j]) - s.th[j],
-                              s.thd[j]);
-      }
-#else
       sea_torques_lanes(s, Pm, B, env_of_block(blockIdx.x, gridDim.x), lane);
-#endif
     } else if (lane < NJ) {
       const int j = lane;
       float as = s.act[j] * Pm->action_scale;
@@ -1020,9 +867,6 @@ LGX_DEV void substep(Sh& s, const lgx_model* M_, const lgx_task_params* Pm_, con
   PH(1);
   kinematics<true>(s, M, Pm, lane);
   PH(2);
-#if defined(LGX_DBG_STAGE) && LGX_DBG_STAGE == 1
-  return;
-#endif
   DynOut dy;
   dynamics(s, lane, dy);
   const int jl_ = lane < NJ ? lane : NJ - 1, leg_ = jl_ / 3, pos_ = jl_ % 3;  // joint lanes' leg / chain position
@@ -1034,9 +878,6 @@ LGX_DEV void substep(Sh& s, const lgx_model* M_, const lgx_task_params* Pm_, con
   for (int r = 0; r < 6; ++r) vb[r] = -dy.hb[r] - row0_sum16(dy.xj[r] * fj);
   __syncthreads();  // S⁻¹ (dynamics) and f_J visible
   PH(3);
-#if defined(LGX_DBG_STAGE) && LGX_DBG_STAGE == 2
-  return;
-#endif
   {
     float zb[6];
 #pragma unroll
@@ -1089,13 +930,7 @@ LGX_DEV void substep(Sh& s, const lgx_model* M_, const lgx_task_params* Pm_, con
       xc = ld3(s.P[ck]) + mv(s.R[ck], ld3(M->cand_pos[lane]));
       r = M->cand_radius[lane];
     }
-#ifdef LGX_TERRAIN_PER_LANE  // (the one-candidate-per-lane query, for A/B)
-    TerrainHit th;
-    th.depth = -3.0e38f;
-    if (cand) th = terrain_contact(Pm, B, xc, r);
-#else
     const TerrainHit th = terrain_contact_wave(Pm, B, xc, r, cand, lane);
-#endif
     if (cand) {
       depth = th.depth;
       nrm = th.n;
@@ -1177,9 +1012,6 @@ LGX_DEV void substep(Sh& s, const lgx_model* M_, const lgx_task_params* Pm_, con
 #endif
   __syncthreads();
   PH(5);
-#if defined(LGX_DBG_STAGE) && LGX_DBG_STAGE == 3
-  return;
-#endif
   // ---- per row (one lane each): y = J_B − X_l J_l, z = S⁻¹ y, g = D_l⁻¹ J_l,
   //      A_rr = y·z + J_l·g, w_r = J_r u*
   const bool row_lane = lane < nrows;
@@ -1224,9 +1056,6 @@ LGX_DEV void substep(Sh& s, const lgx_model* M_, const lgx_task_params* Pm_, con
   }
   __syncthreads();
   PH(6);
-#if defined(LGX_DBG_STAGE) && LGX_DBG_STAGE == 4
-  return;
-#endif
   // ---- A = J M⁻¹ Jᵀ: entry (q, r) = y_r·z_q + [leg_r = leg_q] J_l,r·g_q (J_l,r = 0 for rows
   //      without a leg part). Up to ASQ rows lane r stores column r of a square [q][r] image;
   //      up to AMAX the lower triangle q >= r packed at q (q + 1) / 2 + r; beyond (a fallen
@@ -1988,9 +1817,6 @@ __global__ __launch_bounds__(64, ACTNET ? LGX_SEA_WAVES : 4) void env_step_kerne
     __syncthreads();
   }
 
-#ifdef LGX_DEBUG_SKIP_POST
-  return;
-#endif
   // ================================================================ post-physics
   // Go2Robot.post_physics_step go2.py:345-387 / LeggedRobot legged_robot.py:103-138.
   // Per-env scalars: lane 0, into LDS. Vectors: lane-parallel from LDS.
@@ -2066,7 +1892,9 @@ __global__ __launch_bounds__(64, ACTNET ? LGX_SEA_WAVES : 4) void env_step_kerne
       const float* c = s.cf[Pm->termination_idx[i]];
       reset |= nrm3(c[0], c[1], c[2]) > 1.0f;
     }
-    int tout = ep > Pm->max_episode_length;
+    // a blown-up env (NaN/Inf guard) ends as a termination, never a time-out: its step is not
+    // bootstrapped (ppo.py:166-167) and earns no reward (the stand-in state is not a real one)
+    int tout = ep > Pm->max_episode_length && !s.blew;
     reset |= tout;
     reset |= x.pg[2] > 0.0f;
     if (Pm->parkour) reset |= root[2] < -1.0f;
@@ -2084,7 +1912,7 @@ __global__ __launch_bounds__(64, ACTNET ? LGX_SEA_WAVES : 4) void env_step_kerne
   // compute_reward legged_robot.py:216-237: lane k evaluates term k (alphabetical order)
   const int K = Pm->num_reward_terms;
   const int KS = K + (Pm->has_termination_reward ? 1 : 0);
-  if (lane < K) s.rterm[lane] = reward_term(Pm, B, s, e, Pm->reward_ids[lane]) * Pm->reward_scales[lane];
+  if (lane < K) s.rterm[lane] = s.blew ? 0.0f : reward_term(Pm, B, s, e, Pm->reward_ids[lane]) * Pm->reward_scales[lane];
   __syncthreads();
   const int reset = s.reset;
   if (lane == 0) {
@@ -2092,7 +1920,7 @@ __global__ __launch_bounds__(64, ACTNET ? LGX_SEA_WAVES : 4) void env_step_kerne
     for (int k = 0; k < K; ++k) rew += s.rterm[k];  // sequential, the reference's order
     if (Pm->only_positive_rewards) rew = rew < 0.0f ? 0.0f : rew;
     if (Pm->has_termination_reward) {
-      float v = (float)(reset && !s.tout) * Pm->termination_scale;
+      float v = (float)(reset && !s.tout && !s.blew) * Pm->termination_scale;
       rew += v;
       s.rterm[K] = v;
     }

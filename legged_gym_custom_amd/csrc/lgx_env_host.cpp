@@ -1136,7 +1136,7 @@ static void env_step(Env& s, const lgx_model* M, const lgx_task_params* P, const
   // check_termination go2.py:186-204
   int reset = 0;
   for (int i = 0; i < P->n_termination; ++i) reset |= fnorm(s.cf[P->termination_idx[i]]) > 1.0f;
-  const int tout = ep > P->max_episode_length;
+  const int tout = ep > P->max_episode_length && !blew;  // a blow-up is a termination (kernel)
   reset |= tout;
   reset |= s.pg[2] > 0.0f;
   if (P->parkour) reset |= root[2] < -1.0f;
@@ -1148,12 +1148,12 @@ static void env_step(Env& s, const lgx_model* M, const lgx_task_params* P, const
   const int K = P->num_reward_terms, KS = K + (P->has_termination_reward ? 1 : 0);
   float rew = 0.0f;
   for (int k = 0; k < K; ++k) {
-    s.rterm[k] = reward_term(P, s, P->reward_ids[k]) * P->reward_scales[k];
+    s.rterm[k] = blew ? 0.0f : reward_term(P, s, P->reward_ids[k]) * P->reward_scales[k];
   }
   for (int k = 0; k < K; ++k) rew += s.rterm[k];
   if (P->only_positive_rewards) rew = rew < 0.0f ? 0.0f : rew;
   if (P->has_termination_reward) {
-    const float v = (float)(reset && !tout) * P->termination_scale;
+    const float v = (float)(reset && !tout && !blew) * P->termination_scale;
     rew += v;
     s.rterm[K] = v;
   }

@@ -32,10 +32,6 @@
 #include "../../include/lgx_mlp.h"
 #include "lgx_device.h"  // philox4x32_10 / u01: the env's counter RNG (the act head's noise)
 
-#ifndef LGX_ELU_EXACT
-#define LGX_ELU_EXACT 0
-#endif
-
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
@@ -49,9 +45,6 @@ constexpr int BM = 128, BKS = 32, NT = 256;
 #endif
 #ifndef LGX_PF_DW  // the weight-gradient kind's prefetch depth (dev knob)
 #define LGX_PF_DW LGX_PF
-#endif
-#ifndef LGX_MV_ROWMAJOR
-#define LGX_MV_ROWMAJOR 1
 #endif
 // LGX_PF: global-load register sets (prefetch depth in K steps), gemm_tile's PF (3 measured
 // slower for every launch: 246 VGPRs in the weight-gradient tile)
@@ -105,14 +98,13 @@ struct Stager {
   static constexpr int KG = ROWS * BKS / (4 * NTH);  // k per thread (MV)
   static constexpr int NKQ = BKS / KG;         // k groups per step (MV): 8 or 16
   static_assert(T >= 1 && KG >= 2, "tile too small for the thread count");
-  // MV thread map. LGX_MV_ROWMAJOR (default): rg = tid % NRG (4-row group), kq = tid / NRG
-  // (k group): consecutive lanes read consecutive 16 B of one source row (k), so a wave's
-  // load is 2 (ROWS 128) or 4 (ROWS 64) fully contiguous row segments — the texture path
-  // coalesces it. Otherwise kq = tid % NKQ, rg = tid / NKQ: a load covers NKQ source rows
-  // x 64 B (4x the L1 accesses, measured) and each store's NKQ lanes fill one 64-B LDS row.
+  // MV thread map: rg = tid % NRG (4-row group), kq = tid / NRG (k group): consecutive lanes
+  // read consecutive 16 B of one source row (k), so a wave's load is 2 (ROWS 128) or 4 (ROWS 64)
+  // fully contiguous row segments — the texture path coalesces it (round 1's kq-fastest map
+  // covered NKQ source rows x 64 B per load: 4x the L1 accesses, measured).
   static constexpr int NRG = ROWS / 4;
-  __device__ __forceinline__ static int mv_kq(int tid) { return LGX_MV_ROWMAJOR ? tid / NRG : tid % NKQ; }
-  __device__ __forceinline__ static int mv_rg(int tid) { return LGX_MV_ROWMAJOR ? tid % NRG : tid / NKQ; }
+  __device__ __forceinline__ static int mv_kq(int tid) { return tid / NRG; }
+  __device__ __forceinline__ static int mv_rg(int tid) { return tid % NRG; }
 
   // Rows past the M/N edge are clamped to a valid row (their products only reach outputs
   // that are never stored), so loads stay vectorised at the edges; KGUARD (the last,
@@ -224,11 +216,8 @@ struct Stager {
 
 // ELU(alpha = 1): v > 0 ? v : expm1(v), branch-free. expm1 on v <= 0: a degree-8 Taylor
 // polynomial for v > -0.5 (truncation < 1.2e-8 relative), exp(v) - 1 below (v_exp_f32;
-// within ~3 ulp of expm1f at the switch, < 1 ulp past v = -1). LGX_ELU_EXACT: ocml expm1f.
+// within ~3 ulp of expm1f at the switch, < 1 ulp past v = -1).
 __device__ __forceinline__ float elu(float v) {
-#if LGX_ELU_EXACT
-  return v > 0.f ? v : expm1f(v);
-#else
   float q = fmaf(v, 1.f / 40320.f, 1.f / 5040.f);
   q = fmaf(v, q, 1.f / 720.f);
   q = fmaf(v, q, 1.f / 120.f);
@@ -239,7 +228,6 @@ __device__ __forceinline__ float elu(float v) {
   const float small = v * q;
   const float big = __expf(v) - 1.f;
   return v > 0.f ? v : (v > -0.5f ? small : big);
-#endif
 }
 
 // One output tile (logical index L: n fastest, then m, then the K split) of one GEMM.
@@ -323,13 +311,9 @@ __device__ __forceinline__ void gemm_tile(const Params& p, const int L) {
       const bf16x8 al = *reinterpret_cast<const bf16x8*>(alo + off);
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
-#ifdef LGX_EXP_NOMFMA  // experiment (timing only): fragments read, no MFMA
-        acc[i][j][0] += (float)al[0] + (float)bh[j][0] + (float)ah[1] + (float)bl[j][1];
-#else
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh[j], acc[i][j], 0, 0, 0);
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl[j], acc[i][j], 0, 0, 0);
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh[j], acc[i][j], 0, 0, 0);
-#endif
       }
     }
   };
@@ -338,12 +322,8 @@ __device__ __forceinline__ void gemm_tile(const Params& p, const int L) {
   // gradient), those registers refilled with step s+1+PF; one barrier.
   auto stepU = [&](int s, float (&ra)[SA::R], float (&rb)[SB::R]) {
     compute(s & 1);
-#ifndef LGX_EXP_NOSTORE  // experiment (timing only): no staging split / LDS stores in the loop
     sstore(ra, rb, (s + 1) & 1, s + 1 < nfull);
-#endif
-#ifndef LGX_EXP_NOLOAD  // experiment (timing only): no global loads in the loop
     gloadU(ra, rb, s + 1 + PF);
-#endif
     __syncthreads();
   };
 

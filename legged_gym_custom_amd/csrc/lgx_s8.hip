@@ -1,0 +1,665 @@
+// lgx_s8.hip — the learner's GEMM core on pre-split (S8) operands, gfx950 (include/lgx_s8.h).
+//
+// Every operand arrives as bf16 hi/lo planes interleaved per 8 columns (S8), written by the
+// kernel that produced it (forward / input-gradient epilogues here, lgx_s8_split for weights,
+// inputs and the loss heads' gradients). So the K loop moves bytes and multiplies: no fp32 ->
+// bf16 split, no VGPR round trip.
+//
+// Block: 256 threads = 4 waves as 2 x 2, output tile 128 x 128, each wave 64 x 64 = 4 x 4
+// tiles of v_mfma_f32_16x16x32_bf16; per product lo*hi + hi*lo + hi*hi (3 x bf16, fp32
+// accumulation; lgx_mlp.hip's order). K step 32, NS stages of LDS.
+// Staging: global_load_lds_dwordx4 (LDS-DMA; destination = wave base + 16 B x lane), 8 per wave
+// per K step, NS - 1 steps in flight across raw s_barriers with a counted vmcnt — no barrier
+// drains the DMA (cdna_hip_programming.md §5 "Pipelining across barriers"). Images:
+//   ROW operand (k along the source row): [128 rows][32 k] = 128-B rows, 8 slots of 16 B
+//       (hi g0, lo g0, hi g1, ...); fragments by ds_read_b128 (8 consecutive k of one row).
+//   TR operand (k = source row): [32 k][128 cols] = 512-B rows (the source row's 128-column
+//       span verbatim); fragments by ds_read_b64_tr_b16 (4 k x 16 columns, delivered per column).
+// The 16-B slots are XOR-swizzled by a function of the image row — applied to the DMA's per-lane
+// SOURCE address (the destination is lane-linear) and to the read address — so every fragment
+// read is bank-conflict free (tools/exp/s8_banks.py, MI355X_MICROARCH.md §LDS bank model).
+// Epilogue through an fp32 LDS image of the tile: FWD bias + ELU, DX * ELU'(y_prev) (+ addend),
+// both written as S8 (32 B per lane: 8 columns' hi + lo) and/or fp32, with the column sums of each
+// 128-row tile (the next weight gradient's bias gradient); DW fp32 split-K partials.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+
+#include "../../include/lgx_s8.h"
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4u __attribute__((ext_vector_type(4), aligned(4)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+#define LDS_AS __attribute__((address_space(3)))
+
+#ifndef LGX_S8_NS
+#define LGX_S8_NS 2
+#endif
+#ifndef LGX_S8_BK
+#define LGX_S8_BK 32
+#endif
+#ifndef LGX_S8_NW
+#define LGX_S8_NW 4
+#endif
+
+namespace lgxs {
+
+constexpr int BK = LGX_S8_BK, BT = 128, NW = LGX_S8_NW, NT = 64 * NW, GMAX = LGX_S8_GROUP_MAX;
+// waves as 2 (rows) x NW/2 (columns); each wave 64 x WN (WN = 64 or 32: NJ 16-wide tiles)
+constexpr int WN = BT / (NW / 2), NJ = WN / 16;
+static_assert(NW == 4 || NW == 8, "4 or 8 waves");
+static_assert(BK == 32 || BK == 64, "K step 32 or 64");
+constexpr int CP = BT + 4;  // fp32 epilogue image pitch (floats)
+
+// slot swizzles (16-B slot index XOR), image row -> mask
+__device__ __forceinline__ int fsw_row(int r) {
+  if constexpr (BK == 32) return ((r >> 1) & 1) | (((r >> 3) & 1) << 2);  // 8 slots per 128-B row
+  return (r & 15) ^ ((((r >> 2) ^ (r >> 3)) & 1) << 1);                     // 16 slots per 256-B row
+}
+__device__ __forceinline__ int fsw_tr(int k) { return (k & 1) | ((k & 2) << 1) | (k & 8); }
+
+struct Prob {
+  const char* A; const char* B;
+  int64_t lda, ldb;            // bytes
+  int M, N, K;
+  int tiles_m, tiles_n, tiles;  // tiles includes the split
+  int kchunk, epi;
+  char* C; int64_t ldc;         // bytes (S8)
+  float* C32; int64_t ldc32;    // floats
+  const float* bias;
+  const char* act; int64_t ld_act;  // bytes (S8)
+  const float* addend; int64_t ld_add;
+  int add_cols, pad;
+  float* colsum_ws;
+};
+
+struct Group {
+  int n, per_xcd;
+  int start[GMAX + 1];
+  Prob p[GMAX];
+};
+static_assert(sizeof(Group) <= 4096, "kernel argument segment");
+
+// An operand's staging geometry (one K step).
+template <bool TR>
+struct Op {
+  static constexpr int PITCH = TR ? BT * 4 : BK * 4;  // image row bytes
+  static constexpr int SLOTS = PITCH / 16;
+  static constexpr int RPI = 1024 / PITCH;            // image rows per DMA wave-instruction
+  static constexpr int NI = BT * BK * 4 / 1024;       // DMA wave-instructions per step (16)
+  static constexpr int PW = NI / NW;                  // per wave
+  static constexpr int IMG = BT * BK * 4;             // bytes (16 KB)
+
+  // per-lane 32-bit source offsets of this wave's instructions (step 0); t0 = tile's first m/n
+  __device__ __forceinline__ static void offsets(uint32_t (&off)[PW], int wave, int lane, int t0, int R,
+                                                 int64_t ld, int kbeg) {
+#pragma unroll
+    for (int j = 0; j < PW; ++j) {
+      const int i = wave + NW * j;
+      const int r = i * RPI + lane / SLOTS, ps = lane % SLOTS;
+      if (TR) {  // r = k (source row kbeg + r), columns t0 .. t0 + 127
+        const int ls = ps ^ fsw_tr(r);
+        const int64_t cb = std::min<int64_t>((int64_t)t0 * 4 + ls * 16, ld - 16);
+        off[j] = (uint32_t)((int64_t)(kbeg + r) * ld + cb);
+      } else {   // r = tile row (source row t0 + r, clamped), k from kbeg
+        const int ls = ps ^ fsw_row(r);
+        const int row = std::min(t0 + r, R - 1);
+        off[j] = (uint32_t)((int64_t)row * ld + (int64_t)kbeg * 4 + ls * 16);
+      }
+    }
+  }
+  // step s's source advance (uniform)
+  __device__ __forceinline__ static int64_t step_bytes(int64_t ld) { return TR ? (int64_t)BK * ld : BK * 4; }
+
+  // The DMA is issued by inline asm so that hipcc does not see an LDS write in flight: with the
+  // builtin it waits vmcnt(0) before every ds_read of the tile (alias analysis cannot separate
+  // the stages of one LDS array), which would serialise the load of step k + 1 with the compute
+  // of step k. The ring's own counted vmcnt + s_barrier order it (the main loop). `lds_addr` is
+  // the wave-uniform LDS byte address of this operand's image in the stage.
+  __device__ __forceinline__ static void issue(const char* base, const uint32_t (&off)[PW], uint32_t lds_addr,
+                                               int wave) {
+#pragma unroll
+    for (int j = 0; j < PW; ++j) {
+      const uint32_t m0 = lds_addr + (uint32_t)(wave + NW * j) * 1024u;
+      asm volatile(
+          "s_mov_b32 m0, %2\n\t"
+          "s_nop 0\n\t"
+          "global_load_lds_dwordx4 %0, %1"
+          :
+          : "v"(off[j]), "s"(base), "s"(m0)
+          : "memory", "m0");
+    }
+  }
+
+  // fragment (hi, lo) of 16 tile rows/cols starting at t (multiple of 16), k 32 kk .. 32 kk + 31
+  __device__ __forceinline__ static void frag(const char* img, int t, int kk, int lane, bf16x8& hi, bf16x8& lo) {
+    if (TR) {
+      const int G = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+      const int ls = 2 * ((t >> 3) + (p >> 1));
+      s16x4 h[2], l[2];
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const int k = 32 * kk + 8 * G + 4 * hh + q;
+        const char* row = img + k * PITCH + (p & 1) * 8;
+        const int f = fsw_tr(k);
+        h[hh] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(row + ((ls ^ f) << 4)));
+        l[hh] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(row + (((ls + 1) ^ f) << 4)));
+      }
+      const s16x8 H = {h[0][0], h[0][1], h[0][2], h[0][3], h[1][0], h[1][1], h[1][2], h[1][3]};
+      const s16x8 L = {l[0][0], l[0][1], l[0][2], l[0][3], l[1][0], l[1][1], l[1][2], l[1][3]};
+      hi = __builtin_bit_cast(bf16x8, H);
+      lo = __builtin_bit_cast(bf16x8, L);
+    } else {
+      const int r = t + (lane & 15), g = lane >> 4;
+      const int f = fsw_row(r);
+      const char* row = img + r * PITCH;
+      hi = *reinterpret_cast<const bf16x8*>(row + (((8 * kk + 2 * g) ^ f) << 4));
+      lo = *reinterpret_cast<const bf16x8*>(row + (((8 * kk + 2 * g + 1) ^ f) << 4));
+    }
+  }
+};
+
+__device__ __forceinline__ float elu(float v) {  // lgx_mlp.hip's ELU (same polynomial / exp switch)
+  float q = fmaf(v, 1.f / 40320.f, 1.f / 5040.f);
+  q = fmaf(v, q, 1.f / 720.f);
+  q = fmaf(v, q, 1.f / 120.f);
+  q = fmaf(v, q, 1.f / 24.f);
+  q = fmaf(v, q, 1.f / 6.f);
+  q = fmaf(v, q, 0.5f);
+  q = fmaf(v, q, 1.f);
+  const float small = v * q;
+  const float big = __expf(v) - 1.f;
+  return v > 0.f ? v : (v > -0.5f ? small : big);
+}
+
+__device__ __forceinline__ unsigned pack2(__bf16 a, __bf16 b) {
+  return (unsigned)__builtin_bit_cast(unsigned short, a) | ((unsigned)__builtin_bit_cast(unsigned short, b) << 16);
+}
+// 8 fp32 -> S8 group (32 B: hi x 8, lo x 8)
+__device__ __forceinline__ void store_s8(char* dst, const float (&v)[8]) {
+  __bf16 h[8], l[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    h[e] = (__bf16)v[e];
+    l[e] = (__bf16)(v[e] - (float)h[e]);
+  }
+  const u32x4 H = {pack2(h[0], h[1]), pack2(h[2], h[3]), pack2(h[4], h[5]), pack2(h[6], h[7])};
+  const u32x4 L = {pack2(l[0], l[1]), pack2(l[2], l[3]), pack2(l[4], l[5]), pack2(l[6], l[7])};
+  reinterpret_cast<u32x4*>(dst)[0] = H;
+  reinterpret_cast<u32x4*>(dst)[1] = L;
+}
+__device__ __forceinline__ void load_s8(const char* src, float (&v)[8]) {
+  const u32x4 H = reinterpret_cast<const u32x4*>(src)[0];
+  const u32x4 L = reinterpret_cast<const u32x4*>(src)[1];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    v[2 * e] = __uint_as_float(H[e] << 16) + __uint_as_float(L[e] << 16);
+    v[2 * e + 1] = __uint_as_float(H[e] & 0xffff0000u) + __uint_as_float(L[e] & 0xffff0000u);
+  }
+}
+
+template <int KIND, int NS>
+__global__ __launch_bounds__(NT, NW / 2) void s8_gemm_kernel(Group g) {
+  constexpr bool ATR = KIND == LGX_S8_DW, BTR = KIND != LGX_S8_FWD;
+  using OA = Op<ATR>;
+  using OB = Op<BTR>;
+  constexpr int STAGE = OA::IMG + OB::IMG;
+  extern __shared__ __align__(16) char lds[];
+
+  const int x = blockIdx.x & 7, jb = blockIdx.x >> 3;
+  if (jb >= g.per_xcd) return;
+  int pi = 0;
+  while (pi + 1 < g.n && jb >= g.start[pi + 1]) ++pi;
+  const Prob P = g.p[pi];
+  const int l = x * (g.start[pi + 1] - g.start[pi]) + (jb - g.start[pi]);
+  if (l >= P.tiles) return;
+  const int tn = l % P.tiles_n, tm = (l / P.tiles_n) % P.tiles_m, z = l / (P.tiles_n * P.tiles_m);
+  const int m0 = tm * BT, n0 = tn * BT;
+  const int kbeg = z * P.kchunk;
+  const int kend = std::min(P.K, kbeg + P.kchunk);
+  const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = (wave & 1) * 64, wn = (wave >> 1) * WN;
+
+  uint32_t offA[OA::PW], offB[OB::PW];
+  // ROW operands: source rows = tile rows (M or N); TR operands: source rows = k
+  OA::offsets(offA, wave, lane, m0, P.M, P.lda, kbeg);
+  OB::offsets(offB, wave, lane, n0, P.N, P.ldb, kbeg);
+  const int64_t sa = OA::step_bytes(P.lda), sb = OB::step_bytes(P.ldb);
+
+  const uint32_t lds0 = (uint32_t)(uintptr_t)((LDS_AS char*)lds);
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  auto issue = [&](int stage, int s) {
+    const uint32_t st = lds0 + (uint32_t)(stage * STAGE);
+    OA::issue(P.A + s * sa, offA, st, wv);
+    OB::issue(P.B + s * sb, offB, st + OA::IMG, wv);
+  };
+
+  f32x4 acc[4][NJ];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](int stage) {
+    const char* st = lds + stage * STAGE;
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      bf16x8 ah[4], al[4], bh[NJ], bl[NJ];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) OB::frag(st + OA::IMG, wn + 16 * j, kk, lane, bh[j], bl[j]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) OA::frag(st, wm + 16 * i, kk, lane, ah[i], al[i]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+        }
+    }
+  };
+
+  // pipeline: step s lives in stage s % NS; NS - 1 steps in flight. Each wave waits for its own
+  // DMA of step k (counted vmcnt: the younger steps stay in flight), then the barrier makes
+  // every wave's DMA of step k visible and retires every wave's reads of step k - 1, whose
+  // stage the next DMA overwrites.
+  constexpr int PW = OA::PW + OB::PW;  // DMA instructions per wave per step
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < nk) issue(s, s);
+  for (int k = 0; k < nk; ++k) {
+    if (k + NS - 2 < nk) {
+      if constexpr (NS == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      else if constexpr (NS == 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PW) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    asm volatile("s_barrier" ::: "memory");
+    if (k + NS - 1 < nk) issue((k + NS - 1) % NS, k + NS - 1);
+    compute(k % NS);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // ---- epilogue: the fp32 tile into LDS (MFMA C/D map: col = lane & 15, row = (lane >> 4) * 4 + r)
+  float* img = reinterpret_cast<float*>(lds);
+  {
+    const int ec = lane & 15, er = (lane >> 4) * 4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) img[(wm + 16 * i + er + r) * CP + wn + 16 * j + ec] = acc[i][j][r];
+  }
+  __syncthreads();
+
+  if constexpr (KIND == LGX_S8_DW) {
+    // fp32 rows (float4): split partial slab z, or the output itself (split 1, optional accumulate)
+    const bool part = P.tiles > P.tiles_m * P.tiles_n;
+    float* dst = part ? P.C32 + (int64_t)z * P.M * P.N : P.C32;
+    const int64_t ldd = part ? P.N : P.ldc32;
+    const bool accum = !part && (P.epi & LGX_S8_EPI_ACCUM);
+#pragma unroll
+    for (int it = 0; it < BT * BT / 4 / NT; ++it) {
+      const int idx = tid + it * NT;
+      const int row = idx >> 5, c = (idx & 31) * 4;
+      const int m = m0 + row, n = n0 + c;
+      if (m >= P.M || n >= P.N) continue;
+      const f32x4 t = *reinterpret_cast<const f32x4*>(img + row * CP + c);
+      float* d = dst + (int64_t)m * ldd + n;
+      if (n + 4 <= P.N) {
+        f32x4u o = {t[0], t[1], t[2], t[3]};
+        if (accum) o += *reinterpret_cast<const f32x4u*>(d);
+        *reinterpret_cast<f32x4u*>(d) = o;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (n + e < P.N) d[e] = accum ? d[e] + t[e] : t[e];
+      }
+    }
+    return;
+  }
+
+  // FWD / DX: thread = one 8-column group (g = tid & 15) of rows (tid >> 4) + RS it
+  constexpr int RS = NT / 16;  // row slots
+  const int gq = tid & 15, r0 = tid >> 4;
+  const int n = n0 + 8 * gq;
+  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float bias[8];
+  if constexpr (KIND == LGX_S8_FWD) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bias[e] = (P.epi & LGX_S8_EPI_BIAS) && n + e < P.N ? P.bias[n + e] : 0.f;
+  }
+#pragma unroll 2
+  for (int it = 0; it < BT / RS; ++it) {
+    const int row = r0 + RS * it, m = m0 + row;
+    if (m >= P.M || n >= P.N) continue;
+    const f32x4 t0 = *reinterpret_cast<const f32x4*>(img + row * CP + 8 * gq);
+    const f32x4 t1 = *reinterpret_cast<const f32x4*>(img + row * CP + 8 * gq + 4);
+    float v[8] = {t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
+    if constexpr (KIND == LGX_S8_FWD) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += bias[e];
+      if (P.epi & LGX_S8_EPI_ELU) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = elu(v[e]);
+      }
+    } else {
+      if (P.epi & LGX_S8_EPI_DELU) {
+        float y[8];
+        load_s8(P.act + (int64_t)m * P.ld_act + (n >> 3) * 32, y);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] *= y[e] > 0.f ? 1.f : y[e] + 1.f;
+      }
+      if (P.addend != nullptr) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (n + e < P.add_cols) v[e] += P.addend[(int64_t)m * P.ld_add + n + e];
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = n + e < P.N ? v[e] : 0.f;  // zero pad columns
+    if (P.C != nullptr) store_s8(P.C + (int64_t)m * P.ldc + (n >> 3) * 32, v);
+    if (P.C32 != nullptr) {
+      float* d = P.C32 + (int64_t)m * P.ldc32 + n;
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (n + e < P.N) d[e] = v[e];
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) cs[e] += v[e];
+  }
+  if (P.colsum_ws != nullptr) {  // column sums of this 128-row tile, fixed order
+    __syncthreads();
+    float* red = img;  // [RS row slots][128 columns]
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[r0 * BT + 8 * gq + e] = cs[e];
+    __syncthreads();
+    if (tid < BT && n0 + tid < P.N) {
+      float s = 0.f;
+#pragma unroll
+      for (int q = 0; q < RS; ++q) s += red[q * BT + tid];
+      P.colsum_ws[(int64_t)tm * P.N + n0 + tid] = s;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- fp32 -> S8 (+ column sums)
+struct SplitJob {
+  const float* src; int64_t ld_src;
+  char* dst; int64_t ld_dst;  // bytes
+  int rows, cols;
+  float* colsum_ws;
+  const int64_t* idx;
+  int blk0;  // first block of this job
+};
+struct SplitBatch {
+  int n;
+  SplitJob j[LGX_S8_BATCH_MAX];
+};
+static_assert(sizeof(SplitBatch) <= 4096, "kernel argument segment");
+
+// block = 256 rows of one job; thread = one 8-column group. Narrow jobs (<= 8 groups, the only
+// ones with column sums): thread t owns group t & 7 of rows (t >> 3) + 32 it (fixed order).
+__global__ __launch_bounds__(256) void s8_split_kernel(SplitBatch b) {
+  int ji = 0;
+  while (ji + 1 < b.n && (int)blockIdx.x >= b.j[ji + 1].blk0) ++ji;
+  const SplitJob J = b.j[ji];
+  const int blk = blockIdx.x - J.blk0;
+  const int rbase = blk * LGX_S8_SPLIT_ROWS;
+  const int G = (J.cols + 7) / 8;
+  const int tid = threadIdx.x;
+  auto one = [&](int r, int gg, float (&v)[8]) {
+    const int64_t sr = J.idx ? J.idx[r] : r;
+    const float* s = J.src + sr * J.ld_src + 8 * gg;
+    if (8 * gg + 8 <= J.cols) {
+      const f32x4u a = *reinterpret_cast<const f32x4u*>(s), b = *reinterpret_cast<const f32x4u*>(s + 4);
+      v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3]; v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = 8 * gg + e < J.cols ? s[e] : 0.f;
+    }
+    store_s8(J.dst + (int64_t)r * J.ld_dst + gg * 32, v);
+  };
+  if (G <= 8) {
+    const int gg = tid & 7;
+    float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int it = 0; it < LGX_S8_SPLIT_ROWS / 32; ++it) {
+      const int r = rbase + (tid >> 3) + 32 * it;
+      if (gg >= G || r >= J.rows) continue;
+      float v[8];
+      one(r, gg, v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) cs[e] += v[e];
+    }
+    if (J.colsum_ws != nullptr) {
+      __shared__ float red[32][64];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) red[tid >> 3][8 * gg + e] = cs[e];
+      __syncthreads();
+      if (tid < J.cols) {
+        float s = 0.f;
+        for (int q = 0; q < 32; ++q) s += red[q][tid];
+        J.colsum_ws[(int64_t)blk * J.cols + tid] = s;
+      }
+    }
+    return;
+  }
+  for (int idx = tid; idx < LGX_S8_SPLIT_ROWS * G; idx += 256) {
+    const int r = rbase + idx / G, gg = idx % G;
+    if (r >= J.rows) break;
+    float v[8];
+    one(r, gg, v);
+  }
+}
+
+struct ReduceBatch {
+  int n;
+  int64_t start[LGX_S8_BATCH_MAX + 1];  // prefix sums of rows * cols
+  lgx_s8_reduce_args j[LGX_S8_BATCH_MAX];
+};
+static_assert(sizeof(ReduceBatch) <= 4096, "kernel argument segment");
+
+__global__ __launch_bounds__(256) void s8_reduce_kernel(ReduceBatch b) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= b.start[b.n]) return;
+  int ji = 0;
+  while (ji + 1 < b.n && i >= b.start[ji + 1]) ++ji;
+  const lgx_s8_reduce_args& J = b.j[ji];
+  const int64_t e = i - b.start[ji];
+  const int64_t r = e / J.cols, c = e - r * J.cols;
+  const float* w = J.ws + r * J.ld_ws + c;
+  float s = 0.f;
+  for (int q = 0; q < J.nsplit; ++q) s += w[q * J.stride];
+  float* o = J.out + r * J.ld_out + c;
+  *o = J.accumulate ? *o + s : s;
+}
+
+}  // namespace lgxs
+
+// ---------------------------------------------------------------- host
+static thread_local char g_err[256] = "";
+static int fail(const char* msg) {
+  snprintf(g_err, sizeof g_err, "%s", msg);
+  return -1;
+}
+static int launched(const char* what) {
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    snprintf(g_err, sizeof g_err, "%s: %s", what, hipGetErrorString(e));
+    return -2;
+  }
+  return 0;
+}
+static int cdiv(int a, int b) { return (a + b - 1) / b; }
+
+template <int KIND>
+static void launch_gemm(const lgxs::Group& g, hipStream_t s) {
+  constexpr int NS = LGX_S8_NS;
+  constexpr int stage = 2 * lgxs::BT * lgxs::BK * 4;
+  constexpr int epi = lgxs::BT * lgxs::CP * 4;
+  constexpr int bytes = NS * stage > epi ? NS * stage : epi;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)lgxs::s8_gemm_kernel<KIND, NS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              bytes);
+    attr = true;
+  }
+  hipLaunchKernelGGL((lgxs::s8_gemm_kernel<KIND, NS>), dim3(8 * g.per_xcd), dim3(lgxs::NT), bytes, s, g);
+}
+
+extern "C" {
+
+int32_t lgx_s8_abi_version(void) { return LGX_S8_ABI_VERSION; }
+int32_t lgx_s8_sizeof_gemm_args(void) { return (int32_t)sizeof(lgx_s8_gemm_args); }
+const char* lgx_s8_last_error(void) { return g_err; }
+
+int32_t lgx_s8_pick_split(const int32_t* M, const int32_t* N, const int32_t* K, int32_t n, int32_t* out) {
+  if (n < 0 || n > LGX_S8_GROUP_MAX) return fail("lgx_s8_pick_split: 0 <= n <= LGX_S8_GROUP_MAX");
+  // one K chunk for every problem: the smallest that keeps the group within one residency
+  // round of 2 blocks per CU (256 CUs)
+  int64_t tiles = 0, kmax = 0;
+  for (int i = 0; i < n; ++i) {
+    if (M[i] <= 0 || N[i] <= 0 || K[i] < 0) return fail("lgx_s8_pick_split: bad shape");
+    tiles += (int64_t)cdiv(M[i], lgxs::BT) * cdiv(N[i], lgxs::BT);
+    kmax = std::max<int64_t>(kmax, K[i]);
+  }
+  const int64_t s = std::max<int64_t>(1, tiles ? 512 / tiles : 1);
+  const int64_t chunk = ((kmax + s - 1) / s + lgxs::BK - 1) / lgxs::BK * lgxs::BK;
+  for (int i = 0; i < n; ++i) out[i] = std::max(1, cdiv(K[i], (int)std::max<int64_t>(chunk, lgxs::BK)));
+  return 0;
+}
+
+int32_t lgx_s8_gemm_group(const lgx_s8_gemm_args* a, int32_t n, int32_t kind, void* stream) {
+  if (n < 0 || n > LGX_S8_GROUP_MAX) return fail("lgx_s8_gemm_group: 0 <= n <= LGX_S8_GROUP_MAX");
+  if (kind < LGX_S8_FWD || kind > LGX_S8_DW) return fail("lgx_s8_gemm_group: unknown kind");
+  lgxs::Group g;
+  memset(&g, 0, sizeof g);
+  int np = 0, acc = 0;
+  g.start[0] = 0;
+  for (int i = 0; i < n; ++i) {
+    const lgx_s8_gemm_args& q = a[i];
+    if (q.M < 0 || q.N < 0 || q.K < 0) return fail("lgx_s8_gemm_group: negative size");
+    if (q.M == 0 || q.N == 0) continue;
+    if (!q.A || !q.B) return fail("lgx_s8_gemm_group: null operand");
+    if (q.lda % 8 || q.ldb % 8) return fail("lgx_s8_gemm_group: S8 pitches must be multiples of 8");
+    if ((((uintptr_t)q.A) | ((uintptr_t)q.B)) & 15) return fail("lgx_s8_gemm_group: operands must be 16-B aligned");
+    const bool atr = kind == LGX_S8_DW, btr = kind != LGX_S8_FWD;
+    const int kp = cdiv(q.K, lgxs::BK) * lgxs::BK;
+    // the source extent the DMA may touch (lane offsets are 32-bit)
+    const int64_t abytes = atr ? (int64_t)kp * q.lda * 4 : (int64_t)q.M * q.lda * 4;
+    const int64_t bbytes = btr ? (int64_t)kp * q.ldb * 4 : (int64_t)q.N * q.ldb * 4;
+    if (abytes >= (1ll << 31) || bbytes >= (1ll << 31)) return fail("lgx_s8_gemm_group: operand spans >= 2 GB");
+    if (!atr && q.lda < kp) return fail("lgx_s8_gemm_group: ROW operand A pitch < round_up(K, 32)");
+    if (!btr && q.ldb < kp) return fail("lgx_s8_gemm_group: ROW operand B pitch < round_up(K, 32)");
+    if (atr && q.lda < 8) return fail("lgx_s8_gemm_group: TR operand A pitch");
+    lgxs::Prob& p = g.p[np];
+    p.A = (const char*)q.A;
+    p.B = (const char*)q.B;
+    p.lda = q.lda * 4;
+    p.ldb = q.ldb * 4;
+    p.M = q.M;
+    p.N = q.N;
+    p.K = q.K;
+    p.tiles_m = cdiv(q.M, lgxs::BT);
+    p.tiles_n = cdiv(q.N, lgxs::BT);
+    p.epi = q.epilogue;
+    p.C = (char*)q.C;
+    p.ldc = q.ldc * 4;
+    p.C32 = q.C32;
+    p.ldc32 = q.ldc32;
+    p.bias = q.bias;
+    p.act = (const char*)q.act;
+    p.ld_act = q.ld_act * 4;
+    p.addend = q.addend;
+    p.ld_add = q.ld_add;
+    p.add_cols = q.addend ? q.add_cols : 0;
+    p.colsum_ws = q.colsum_ws;
+    int split = 1;
+    if (kind == LGX_S8_DW) {
+      split = std::max(1, q.split);
+      if (!q.C32) return fail("lgx_s8_gemm_group: DW needs C32 (output or partial workspace)");
+      if (split == 1 && q.ldc32 < q.N) return fail("lgx_s8_gemm_group: ldc32 < N");
+    } else {
+      if (!q.C && !q.C32) return fail("lgx_s8_gemm_group: no output");
+      if (q.C && (q.ldc % 8 || (((uintptr_t)q.C) & 15))) return fail("lgx_s8_gemm_group: S8 output alignment");
+      if ((q.epilogue & LGX_S8_EPI_BIAS) && !q.bias) return fail("lgx_s8_gemm_group: bias epilogue without bias");
+      if ((q.epilogue & LGX_S8_EPI_DELU) && (!q.act || q.ld_act % 8 || (((uintptr_t)q.act) & 15)))
+        return fail("lgx_s8_gemm_group: ELU' epilogue needs an aligned S8 act");
+      if (q.C32 && q.ldc32 < q.N) return fail("lgx_s8_gemm_group: ldc32 < N");
+    }
+    const int ksteps = cdiv(q.K, lgxs::BK);
+    const int per = std::max(1, cdiv(ksteps, split));
+    p.kchunk = per * lgxs::BK;
+    split = std::max(1, cdiv(ksteps, per));
+    p.tiles = p.tiles_m * p.tiles_n * split;
+    acc += cdiv(p.tiles, 8);
+    g.start[++np] = acc;
+  }
+  g.n = np;
+  g.per_xcd = acc;
+  if (np == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  if (kind == LGX_S8_FWD) launch_gemm<LGX_S8_FWD>(g, s);
+  else if (kind == LGX_S8_DX) launch_gemm<LGX_S8_DX>(g, s);
+  else launch_gemm<LGX_S8_DW>(g, s);
+  return launched("lgx_s8_gemm_group");
+}
+
+int32_t lgx_s8_split(const lgx_s8_split_args* a, int32_t n, void* stream) {
+  if (n < 0 || n > LGX_S8_BATCH_MAX) return fail("lgx_s8_split: 0 <= n <= LGX_S8_BATCH_MAX");
+  lgxs::SplitBatch b;
+  memset(&b, 0, sizeof b);
+  int blocks = 0, k = 0;
+  for (int i = 0; i < n; ++i) {
+    const lgx_s8_split_args& q = a[i];
+    if (q.rows < 0 || q.cols < 0) return fail("lgx_s8_split: negative size");
+    if (q.rows == 0 || q.cols == 0) continue;
+    if (!q.src || !q.dst) return fail("lgx_s8_split: null pointer");
+    if (q.ld_dst % 8 || (((uintptr_t)q.dst) & 15) || q.ld_dst < cdiv(q.cols, 8) * 8)
+      return fail("lgx_s8_split: S8 destination alignment / pitch");
+    if (q.colsum_ws && q.cols > 64) return fail("lgx_s8_split: column sums for <= 64 columns only");
+    b.j[k] = lgxs::SplitJob{q.src, q.ld_src, (char*)q.dst, q.ld_dst * 4, q.rows, q.cols, q.colsum_ws, q.idx, blocks};
+    blocks += cdiv(q.rows, LGX_S8_SPLIT_ROWS);
+    ++k;
+  }
+  b.n = k;
+  if (!k) return 0;
+  hipLaunchKernelGGL(lgxs::s8_split_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, b);
+  return launched("lgx_s8_split");
+}
+
+int32_t lgx_s8_reduce(const lgx_s8_reduce_args* a, int32_t n, void* stream) {
+  if (n < 0 || n > LGX_S8_BATCH_MAX) return fail("lgx_s8_reduce: 0 <= n <= LGX_S8_BATCH_MAX");
+  lgxs::ReduceBatch b;
+  memset(&b, 0, sizeof b);
+  int k = 0;
+  b.start[0] = 0;
+  for (int i = 0; i < n; ++i) {
+    if (a[i].rows < 0 || a[i].cols < 0 || a[i].nsplit < 0) return fail("lgx_s8_reduce: negative size");
+    if (a[i].rows == 0 || a[i].cols == 0) continue;
+    if (!a[i].ws || !a[i].out) return fail("lgx_s8_reduce: null pointer");
+    if (a[i].rows > 1 && (a[i].ld_ws < a[i].cols || a[i].ld_out < a[i].cols)) return fail("lgx_s8_reduce: pitch < cols");
+    b.j[k] = a[i];
+    b.start[k + 1] = b.start[k] + (int64_t)a[i].rows * a[i].cols;
+    ++k;
+  }
+  b.n = k;
+  if (!k) return 0;
+  const int64_t tot = b.start[k];
+  hipLaunchKernelGGL(lgxs::s8_reduce_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, (hipStream_t)stream, b);
+  return launched("lgx_s8_reduce");
+}
+
+}  // extern "C"

@@ -441,9 +441,28 @@ class LeggedRobot(BaseTask):
         self.reward_names = [k for k in self.reward_scales if k != "termination"]
 
 
+class _RangePair(list):
+    """One [lo, hi] entry of _DeviceCommandRanges: item writes go through to the device ranges
+    (the reference idiom `self.command_ranges["lin_vel_x"][1] = v`, go2.py:96-107)."""
+
+    def __init__(self, owner, key, vals):
+        super().__init__(vals)
+        self._owner, self._key = owner, key
+
+    def __setitem__(self, i, v):
+        super().__setitem__(i, v)
+        if len(self) != 2:
+            raise ValueError("a command range is [lo, hi]")
+        self._owner[self._key] = list(self)
+
+    def __reduce__(self):  # a detached copy pickles as the plain [lo, hi] list
+        return (list, (list(self),))
+
+
 class _DeviceCommandRanges(dict):
     """self.command_ranges under the command curriculum: {'lin_vel_x': [lo, hi], ...} read
-    from the device ranges the curriculum updates (a host read per access)."""
+    from the device ranges the curriculum updates. Every read is a device-to-host copy (it
+    synchronises with the stream); item writes, whole or per end, go to the device."""
     _KEYS = ("lin_vel_x", "lin_vel_y", "ang_vel_yaw", "heading")
 
     def __init__(self, buf):
@@ -454,7 +473,7 @@ class _DeviceCommandRanges(dict):
 
     def __getitem__(self, key):
         i = self._KEYS.index(key)
-        return [float(v) for v in self._buf[2 * i:2 * i + 2].tolist()]
+        return _RangePair(self, key, [float(v) for v in self._buf[2 * i:2 * i + 2].tolist()])
 
     def __setitem__(self, key, value):
         i = self._KEYS.index(key)

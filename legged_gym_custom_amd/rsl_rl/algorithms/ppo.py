@@ -26,6 +26,7 @@ Reference quirk kept: clip_grad_norm_(actor_critic.parameters()) also sees the
 adaptation encoder's stale DAgger gradients (never zeroed by `optimizer`), and scales them.
 """
 import copy
+import os
 
 import torch
 import torch.distributed as dist
@@ -34,6 +35,11 @@ import torch.optim as optim
 from legged_gym_custom_amd.rsl_rl.modules import ActorCritic, hip_mlp
 from legged_gym_custom_amd.rsl_rl.modules.support_networks import MlpEstimator
 from legged_gym_custom_amd.rsl_rl.storage import RolloutStorage
+
+from .s8_update import S8Minibatch
+
+# the GPU minibatch on the pre-split GEMM core (s8_update.py); "0" selects the autograd path
+USE_S8 = os.environ.get("LGX_S8_UPDATE", "1") != "0"
 
 
 def _distributed():
@@ -224,6 +230,8 @@ class PPO:
         self._eager_updates = 0
         self.graph_mode = None  # "whole" | "phased" once captured
         self.phased_graphs = None  # None: phased iff world_size > 1 (tests force it on one GPU)
+        self.use_s8 = USE_S8 and self.on_gpu
+        self._s8 = None  # S8Minibatch, built at the first update (static buffers for the graphs)
 
     # ------------------------------------------------------------------ flat Adam (HIP)
     def _flatten_params_and_moments(self):
@@ -375,6 +383,15 @@ class PPO:
         ac = self.actor_critic
         g = self.grads
         s = self.storage
+        if self.on_gpu and self._s8 is not None:
+            # the pre-split GEMM core: forward, loss heads, backward and every gradient of the
+            # minibatch as a fixed kernel sequence (s8_update.py); gradients assigned, not added
+            adaptive = self.desired_kl is not None and self.schedule == "adaptive"
+            mb = self._perm.numel() // self.num_mini_batches
+            self._s8.run(idx.start // mb, [None if t is None else t[idx] for t in self._shuf], self._adapt_all[idx],
+                         self._head_out, self._aux_out, g.segment("kl") if adaptive else None)
+            ac.distribution = None
+            return
         if self.on_gpu:
             (obs_b, priv_b, critic_b, est_b, scan_b, actions_b, target_values_b, adv_b, returns_b, old_logp_b,
              old_mu_b, old_sigma_b) = [t[idx] for t in self._shuf]
@@ -526,6 +543,19 @@ class PPO:
         i is the same rows every epoch — a contiguous slice here instead of 12 gathers per
         minibatch), and sg(adaptation_encoder(obs)) for all samples (its weights change only
         in update_dagger)."""
+        if self.on_gpu and self._s8_plan() is not None:
+            with torch.no_grad():
+                flat = self.storage._flat()
+                self._s8.prepare(self._perm, flat)  # the network inputs, permuted, in S8
+                # the loss heads' fields (true est, actions, values, advantages, returns, log-probs,
+                # mu, sigma), permuted, fp32
+                sel = (3, 5, 6, 7, 8, 9, 10, 11)
+                got = hip_mlp.gather_rows([flat[k] for k in sel], self._perm)
+                self._shuf = [None] * 12
+                for k, t in zip(sel, got):
+                    self._shuf[k] = t
+                self._adapt_all = hip_mlp.gather_rows([self.actor_critic.adaptation_encoder(flat[0])], self._perm)[0]
+            return
         if self.on_gpu:
             with torch.no_grad():
                 # the actor input [obs | priv latent | scan latent | est] per row: the gather
@@ -549,6 +579,21 @@ class PPO:
                 # on the storage's own (contiguous) obs rows, then permuted: rows are
                 # independent, and the strided obs span would need a copy for the per-step view
                 self._adapt_all = hip_mlp.gather_rows([self.actor_critic.adaptation_encoder(flat[0])], self._perm)[0]
+
+    def _s8_plan(self):
+        """The S8 minibatch executor for the current storage shape (built outside graph capture,
+        at the first eager update), or None where its layout does not apply (legacy path)."""
+        if not self.use_s8:
+            return None
+        rows = self._perm.numel()
+        mb = rows // self.num_mini_batches
+        if self._s8 is not None and (self._s8.rows, self._s8.mb) == (rows, mb):
+            return self._s8
+        self._s8 = None
+        if torch.cuda.is_current_stream_capturing() or not S8Minibatch.supported(self, mb):
+            return None
+        self._s8 = S8Minibatch(self, rows, mb)
+        return self._s8
 
     def _update_body_eager(self):
         self._precompute()
@@ -595,6 +640,7 @@ class PPO:
         self._graphs = None
         self._eager_updates = 0
         self.graph_mode = None
+        self._s8 = None  # its argument lists hold parameter / gradient addresses
 
     def _run_update(self):
         if not self.use_graphs:

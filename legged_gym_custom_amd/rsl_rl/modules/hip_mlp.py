@@ -558,6 +558,15 @@ def linear_weight_grad(g, x, dW=None, db=None, accumulate=False):
     dev = g.device
     dW = torch.empty(N, K, device=dev, dtype=torch.float32) if dW is None else dW
     db = torch.empty(N, device=dev, dtype=torch.float32) if db is None else db
+    if K == 0:
+        # a layer on an empty input (ANYmal's scan encoder, num_scan_obs = 0): no weight entries,
+        # the bias gradient is sum_rows dY — no GEMM, so no split-K workspace left unwritten
+        s = g.sum(0)
+        if accumulate:
+            db.add_(s)
+        else:
+            db.copy_(s)
+        return dW, db
     if _pending_dw is not None:
         rng = [(dW.data_ptr(), dW.data_ptr() + 4 * (dW.stride(0) * (N - 1) + K)), (db.data_ptr(), db.data_ptr() + 4 * N)]
         if any(lo < h and l2 < hi for (lo, hi) in rng for (*_r, rs) in _pending_dw for (l2, h) in rs):
@@ -1051,7 +1060,11 @@ class _AdaptationFn(torch.autograd.Function):
         # decides: want_grad = grad mode on and some input requires grad)
         inplace = (not want_grad and Hs > H and
                    h.storage_offset() + Bn * Hs * P <= h.untyped_storage().nbytes() // h.element_size())
-        if not want_grad and USE_ADAPT_FUSED and h.stride(2) == 1 and h.stride(1) == P and Bn > 0:
+        # the fused kernel's limits (lgx_adaptation_forward): its intermediates fit 64 KB of LDS
+        # for 16 rows, row pitch >= H * P, 32-bit row offsets; beyond them, the per-layer launches
+        fits = (16 * (H * C1 + L1 * C2 + L2 * C3) * 4 <= 64 * 1024 and h.stride(0) >= H * P and
+                Bn * h.stride(0) <= 2 ** 31 - 1)
+        if not want_grad and USE_ADAPT_FUSED and fits and h.stride(2) == 1 and h.stride(1) == P and Bn > 0:
             # no gradient: the whole encoder in one launch (lgx_adaptation_forward), reading the
             # history rows in place; bit-identical to the per-layer launches below
             if inplace:

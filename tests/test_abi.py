@@ -8,7 +8,7 @@ import pytest
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
-HEADERS = {"lgx.h": "liblgx.so", "lgx_mlp.h": "liblgx_mlp.so"}
+HEADERS = {"lgx.h": "liblgx.so", "lgx_mlp.h": "liblgx_mlp.so", "lgx_s8.h": "liblgx_s8.so"}
 
 
 def _declared(header):
@@ -38,6 +38,8 @@ def test_python_bindings_cover_the_headers():
     from legged_gym_custom_amd.rsl_rl.modules import hip_mlp
     assert set(_declared("lgx.h")) <= set(_native.EXPORTED) | {n for n in _declared("lgx.h") if n.startswith("lgx_sizeof")}
     assert set(_declared("lgx_mlp.h")) == set(hip_mlp.EXPORTED)
+    from legged_gym_custom_amd.rsl_rl.modules import hip_s8
+    assert set(_declared("lgx_s8.h")) == set(hip_s8.EXPORTED)
 
 
 def test_struct_layouts_and_abi_versions(libs):
@@ -47,6 +49,9 @@ def test_struct_layouts_and_abi_versions(libs):
     assert L.lgx_abi_version() == _abi.ABI_VERSION
     M = hip_mlp.lib()  # checks abi version + sizeof(lgx_gemm_args)
     assert M.lgx_mlp_sizeof_gemm_args() == C.sizeof(hip_mlp.GemmArgs)
+    from legged_gym_custom_amd.rsl_rl.modules import hip_s8
+    S8 = hip_s8.lib()  # checks abi version + sizeof(lgx_s8_gemm_args)
+    assert S8.lgx_s8_sizeof_gemm_args() == C.sizeof(hip_s8.GemmArgs)
 
 
 def test_gemm_rejects_bad_arguments_without_touching_the_device(libs):

@@ -58,3 +58,18 @@ def test_command_curriculum_needs_the_tracking_term():
     m = mdl.load_model(env_cfg.asset.file, env_cfg.asset.foot_name)
     with pytest.raises(KeyError, match="tracking_lin_vel"):
         prm.build_task_params(env_cfg, m, 4)
+
+
+def test_device_command_ranges_write_through():
+    """command_ranges under the command curriculum lives in a device buffer: the reference's
+    per-end idiom `command_ranges["lin_vel_x"][1] = v` (go2.py:96-107) must reach it."""
+    import torch
+    from legged_gym_custom_amd.envs.base.legged_robot import _DeviceCommandRanges
+    buf = torch.tensor([-1.0, 1.0, -0.5, 0.5, -1.0, 1.0, -3.14, 3.14], dtype=torch.float64)
+    r = _DeviceCommandRanges(buf)
+    r["lin_vel_x"][1] = 2.5
+    r["lin_vel_y"][0] = -0.75
+    assert r["lin_vel_x"] == [-1.0, 2.5] and r["lin_vel_y"] == [-0.75, 0.5]
+    r["heading"] = [0.0, 1.0]
+    assert buf.tolist() == [-1.0, 2.5, -0.75, 0.5, -1.0, 1.0, 0.0, 1.0]
+    assert dict(r.items())["ang_vel_yaw"] == [-1.0, 1.0]

@@ -601,3 +601,32 @@ def test_group_forward_on_empty_input_gives_the_bias():
     torch.testing.assert_close(alone.cpu(), ref0, rtol=1e-4, atol=1e-5)
     torch.testing.assert_close(got0.cpu(), ref0, rtol=1e-4, atol=1e-5)
     torch.testing.assert_close(got1.cpu(), ref1, rtol=1e-4, atol=1e-4)
+
+
+def test_empty_input_layer_gradients_match_autograd():
+    """Backward through a chain whose input has no columns (ANYmal's scan encoder): the first
+    layer's bias gradient is sum_rows dY (no GEMM, no split-K workspace), inside a grouped
+    backward with deferred weight gradients, against nn.Linear autograd on the CPU."""
+    from legged_gym_custom_amd.rsl_rl.modules.support_networks import ScanEncoder
+    torch.manual_seed(1)
+    enc = ScanEncoder(num_scan_obs=0, output_dim=32, hidden_dims=[128, 64]).to(dev)
+    other = ScanEncoder(num_scan_obs=20, output_dim=16, hidden_dims=[32]).to(dev)
+    ref_enc = ScanEncoder(num_scan_obs=0, output_dim=32, hidden_dims=[128, 64])
+    ref_other = ScanEncoder(num_scan_obs=20, output_dim=16, hidden_dims=[32])
+    ref_enc.load_state_dict({k: v.cpu() for k, v in enc.state_dict().items()})
+    ref_other.load_state_dict({k: v.cpu() for k, v in other.state_dict().items()})
+    x0 = torch.zeros(300, 0, device=dev)
+    x1 = torch.randn(300, 20, device=dev)
+    w0 = torch.randn(300, 32, device=dev)
+    w1 = torch.randn(300, 16, device=dev)
+    for p in list(enc.parameters()) + list(other.parameters()):
+        p.grad = torch.zeros_like(p)  # defined buffers (as the flat-grad views)
+    with H.deferred_weight_grads():
+        y0, y1 = H.forward_group([enc.group_item(x0), other.group_item(x1)])
+        ((y0 * w0).sum() + (y1 * w1).sum()).backward()
+    r0, r1 = ref_enc(torch.zeros(300, 0)), ref_other(x1.cpu())
+    ((r0 * w0.cpu()).sum() + (r1 * w1.cpu()).sum()).backward()
+    for (n, p), q in zip(list(enc.named_parameters()) + list(other.named_parameters()),
+                         list(ref_enc.parameters()) + list(ref_other.parameters())):
+        assert torch.isfinite(p.grad).all(), n
+        torch.testing.assert_close(p.grad.cpu(), q.grad, rtol=1e-4, atol=1e-4, msg=n)

@@ -343,7 +343,7 @@ def nan_guard(device):
             env.step(a)
             hist.append({f: getattr(env, f).clone() for f in ("root_states", "dof_state", "obs_buf", "critic_obs_buf",
                                                               "rew_buf", "reset_buf", "blew_up_buf",
-                                                              "episode_length_buf")})
+                                                              "episode_length_buf", "time_out_buf")})
         return env, hist
 
     env, hi = run(True)
@@ -356,6 +356,8 @@ def nan_guard(device):
         assert not bool(a["blew_up_buf"][torch.arange(n) != bad].any())
         if k == k_inj:
             assert bool(a["reset_buf"][bad]) and int(a["episode_length_buf"][bad]) == 0
+            # a termination with no reward: not bootstrapped as a time-out, stand-in state unrewarded
+            assert float(a["rew_buf"][bad]) == 0.0 and not bool(a["time_out_buf"][bad])
         keep = torch.ones(n, dtype=torch.bool)
         keep[bad] = False
         for f, v in a.items():

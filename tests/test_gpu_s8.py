@@ -1,0 +1,182 @@
+"""The S8 GEMM core (liblgx_s8.so, include/lgx_s8.h) against fp64 references.
+
+Operands are S8 (bf16 hi/lo planes): the reference multiplies the SAME split values (hi + lo)
+in fp64, so what remains is the dropped lo*lo term (<= 2^-16 |a b|) and fp32 accumulation:
+    |C - C_ref| <= 2e-5 * sum_k |a_k b_k| + 1e-6          (stated tolerance, per element)
+Epilogues (bias + ELU; ELU' from an S8 y_prev; addend; zero pads; column sums) are checked
+against torch fp64 on the same values; the fp32 -> S8 split against torch's bf16 rounding
+(bit-exact)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+dev = "cuda:0"
+
+
+@pytest.fixture(scope="module")
+def S():
+    from legged_gym_custom_amd.rsl_rl.modules import hip_s8
+    hip_s8.lib()
+    return hip_s8
+
+
+def _bound(a, b):
+    return 2e-5 * (a.abs() @ b.abs()) + 1e-6
+
+
+def _s8(S, x, ld=None, rows_pad=None):
+    return S.to_s8_torch(x, ld=ld, rows_pad=rows_pad)
+
+
+def test_split_matches_torch_bf16_rounding_and_colsums(S):
+    g = torch.Generator(device="cpu").manual_seed(0)
+    for rows, cols in ((1, 1), (300, 13), (513, 64), (64, 627)):
+        x = (torch.randn(rows, cols, generator=g) * torch.logspace(-6, 3, cols)).to(dev)
+        buf = S.empty(rows, cols, dev)
+        cs = torch.zeros((rows + S.SPLIT_ROWS - 1) // S.SPLIT_ROWS, cols, device=dev) if cols <= 64 else None
+        S.split([S.split_job(x, buf.data_ptr(), buf.shape[1], colsum_ws=cs)])
+        torch.cuda.synchronize()
+        ref = S.to_s8_torch(x)
+        assert torch.equal(buf, ref), (rows, cols)
+        if cs is not None:
+            blocks = [x[i:i + S.SPLIT_ROWS].double().sum(0) for i in range(0, rows, S.SPLIT_ROWS)]
+            torch.testing.assert_close(cs.double(), torch.stack(blocks), rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 1, 1), (300, 200, 72), (24576 // 8, 627, 512), (129, 12, 128), (257, 130, 33)])
+def test_forward_bias_elu(S, M, N, K):
+    g = torch.Generator(device="cpu").manual_seed(M + N + K)
+    x = torch.randn(M, K, generator=g).to(dev)
+    W = (torch.randn(N, K, generator=g) * 0.1).to(dev)
+    b = torch.randn(N, generator=g).to(dev)
+    xs, Ws = _s8(S, x), _s8(S, W)
+    xv, Wv = S.from_s8(xs, M, K).double(), S.from_s8(Ws, N, K).double()
+    out = S.empty(M, N, dev)
+    y32 = torch.full((M, N + 3), float("nan"), device=dev)
+    cs = torch.zeros((M + 127) // 128, N, device=dev)
+    S.gemm_group([S.GemmArgs(A=xs.data_ptr(), lda=xs.shape[1], B=Ws.data_ptr(), ldb=Ws.shape[1], M=M, N=N, K=K,
+                             epilogue=S.EPI_BIAS | S.EPI_ELU, C=out.data_ptr(), ldc=out.shape[1], C32=y32.data_ptr(),
+                             ldc32=y32.stride(0), bias=b.data_ptr(), colsum_ws=cs.data_ptr())], S.FWD)
+    torch.cuda.synchronize()
+    z = xv @ Wv.t() + b.double()
+    ref = torch.nn.functional.elu(z)
+    bound = _bound(xv, Wv.t()) * 1.5 + 1e-6  # ELU' <= 1; its polynomial ~1e-8
+    y = y32[:, :N].double()
+    assert (y - ref).abs().le(bound).all(), float((y - ref).abs().max())
+    assert torch.isnan(y32[:, N:]).all()  # nothing past N in the fp32 copy
+    # the S8 output is the split of the fp32 output, pads zero
+    assert torch.equal(out, S.to_s8_torch(y32[:, :N].contiguous(), ld=out.shape[1], rows_pad=out.shape[0]))
+    blocks = torch.stack([y32[i:i + 128, :N].double().sum(0) for i in range(0, M, 128)])
+    torch.testing.assert_close(cs.double(), blocks, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 512, 256), (200, 627, 512), (64, 55, 512), (130, 128, 12), (33, 20, 1)])
+def test_input_grad_delu_addend(S, M, N, K):
+    """dX[m][n] = (sum_k dY[m][k] W[k][n]) * ELU'(y_prev) + addend (n < add_cols); W read TR."""
+    g = torch.Generator(device="cpu").manual_seed(7 * M + N + K)
+    dy = torch.randn(M, K, generator=g).to(dev)
+    W = (torch.randn(K, N, generator=g) * 0.1).to(dev)
+    yp = torch.nn.functional.elu(torch.randn(M, N, generator=g)).to(dev)
+    add = torch.randn(M, 17, generator=g).to(dev)
+    dys, Ws, yps = _s8(S, dy), _s8(S, W), _s8(S, yp)
+    dyv, Wv, ypv = S.from_s8(dys, M, K).double(), S.from_s8(Ws, K, N).double(), S.from_s8(yps, M, N).double()
+    out = S.empty(M, N, dev)
+    cs = torch.zeros((M + 127) // 128, N, device=dev)
+    S.gemm_group([S.GemmArgs(A=dys.data_ptr(), lda=dys.shape[1], B=Ws.data_ptr(), ldb=Ws.shape[1], M=M, N=N, K=K,
+                             epilogue=S.EPI_DELU, C=out.data_ptr(), ldc=out.shape[1], act=yps.data_ptr(),
+                             ld_act=yps.shape[1], addend=add.data_ptr(), ld_add=add.stride(0), add_cols=17,
+                             colsum_ws=cs.data_ptr())], S.DX)
+    torch.cuda.synchronize()
+    d = torch.where(ypv > 0, torch.ones_like(ypv), ypv + 1.0)
+    ref = (dyv @ Wv) * d
+    ref[:, :17] += add.double()[:, :min(17, N)] if N >= 17 else add.double()[:, :N]
+    got = S.from_s8(out, M, N).double()
+    bound = _bound(dyv, Wv) + 1e-5 * ref.abs() + 1e-6  # + the S8 output's own split (2^-17)
+    assert (got - ref).abs().le(bound).all(), float((got - ref).abs().max())
+    # the pad columns of the output's last group stay zero
+    hi, lo = S.planes(out, M, out.shape[1])
+    assert (hi[:, N:] == 0).all() and (lo[:, N:] == 0).all()
+    blocks = torch.stack([got[i:i + 128].sum(0) for i in range(0, M, 128)])
+    torch.testing.assert_close(cs.double(), blocks, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("rows,M,N,split", [(384, 12, 128, 1), (4096, 512, 627, 4), (2048, 20, 29, 3),
+                                             (1024, 130, 257, 2)])
+def test_weight_grad_split_k(S, rows, M, N, split):
+    """dW[m][n] = sum_r dY[r][m] X[r][n]: both operands TR; split-K partials + lgx_s8_reduce."""
+    g = torch.Generator(device="cpu").manual_seed(rows + M + N)
+    dy = torch.randn(rows, M, generator=g).to(dev)
+    x = torch.randn(rows, N, generator=g).to(dev)
+    dys, xs = _s8(S, dy), _s8(S, x)
+    dyv, xv = S.from_s8(dys, rows, M).double(), S.from_s8(xs, rows, N).double()
+    ref = dyv.t() @ xv
+    bound = _bound(dyv.t(), xv)
+    if split == 1:
+        out = torch.full((M, N), 0.5, device=dev)
+        S.gemm_group([S.GemmArgs(A=dys.data_ptr(), lda=dys.shape[1], B=xs.data_ptr(), ldb=xs.shape[1], M=M, N=N, K=rows,
+                                 epilogue=S.EPI_ACCUM, C32=out.data_ptr(), ldc32=N, split=1)], S.DW)
+        torch.cuda.synchronize()
+        assert ((out.double() - 0.5) - ref).abs().le(bound + 1e-6).all()
+        return
+    ws = torch.empty(split, M, N, device=dev)
+    S.gemm_group([S.GemmArgs(A=dys.data_ptr(), lda=dys.shape[1], B=xs.data_ptr(), ldb=xs.shape[1], M=M, N=N, K=rows,
+                             C32=ws.data_ptr(), ldc32=N, split=split)], S.DW)
+    out = torch.full((M, N), 0.25, device=dev)
+    S.reduce([S.flat_reduce(ws.data_ptr(), M * N, out.data_ptr(), M * N, split, accumulate=1)])
+    torch.cuda.synchronize()
+    assert ((out.double() - 0.25) - ref).abs().le(bound + 1e-6).all(), float(((out.double() - 0.25) - ref).abs().max())
+
+
+def test_grouped_launch_equals_single_launches(S):
+    """Several problems in one launch give the single launches' results bit for bit."""
+    g = torch.Generator(device="cpu").manual_seed(3)
+    rows = 1024
+    probs, bufs = [], []
+    for (M, N) in ((512, 627), (12, 128), (20, 29), (128, 256)):
+        dy = _s8(S, torch.randn(rows, M, generator=g).to(dev))
+        x = _s8(S, torch.randn(rows, N, generator=g).to(dev))
+        bufs.append((dy, x, M, N))
+    outs_g = [torch.zeros(M, N, device=dev) for (_d, _x, M, N) in bufs]
+    args = [S.GemmArgs(A=d.data_ptr(), lda=d.shape[1], B=x.data_ptr(), ldb=x.shape[1], M=M, N=N, K=rows,
+                       C32=o.data_ptr(), ldc32=N, split=1) for (d, x, M, N), o in zip(bufs, outs_g)]
+    S.gemm_group(args, S.DW)
+    outs_s = [torch.zeros(M, N, device=dev) for (_d, _x, M, N) in bufs]
+    for (d, x, M, N), o in zip(bufs, outs_s):
+        S.gemm_group([S.GemmArgs(A=d.data_ptr(), lda=d.shape[1], B=x.data_ptr(), ldb=x.shape[1], M=M, N=N, K=rows,
+                                 C32=o.data_ptr(), ldc32=N, split=1)], S.DW)
+    torch.cuda.synchronize()
+    for a, b in zip(outs_g, outs_s):
+        assert torch.equal(a, b)
+
+
+def test_rejects_bad_arguments(S):
+    import ctypes as C
+    L = S.lib()
+    a = S.GemmArgs(M=-1, N=1, K=1)
+    assert L.lgx_s8_gemm_group(C.byref(a), 1, S.FWD, None) < 0
+    a = S.GemmArgs(A=16, B=16, lda=12, ldb=32, M=4, N=4, K=4, C=16, ldc=32)
+    assert L.lgx_s8_gemm_group(C.byref(a), 1, S.FWD, None) < 0 and b"multiples of 8" in L.lgx_s8_last_error()
+    a = S.GemmArgs(A=16, B=16, lda=8, ldb=32, M=4, N=4, K=40, C=16, ldc=32)
+    assert L.lgx_s8_gemm_group(C.byref(a), 1, S.FWD, None) < 0 and b"pitch" in L.lgx_s8_last_error()
+    np.testing.assert_array_equal(S.pick_split([(512, 627, 24576)] * 2), [S.pick_split([(512, 627, 24576)] * 2)[0]] * 2)
+
+
+def test_gather_split_and_span_reduce(S):
+    """lgx_s8_split with a row permutation (the update's minibatch gather) and lgx_s8_reduce over
+    2-D column spans (a weight whose input columns sit elsewhere in S8 space)."""
+    g = torch.Generator(device="cpu").manual_seed(11)
+    src = torch.randn(3000, 100, generator=g).to(dev)
+    idx = torch.randperm(3000, generator=g)[:1000].to(dev)
+    buf = S.empty(1000, 100, dev)
+    S.split([S.split_job(src, buf.data_ptr(), buf.shape[1], idx=idx, rows=1000)])
+    ws = torch.randn(3, 20, 64, generator=g).to(dev)
+    out = torch.full((20, 50), 7.0, device=dev)
+    S.reduce([S.ReduceArgs(ws=ws.data_ptr() + 4 * 10, stride=20 * 64, ld_ws=64, out=out.data_ptr() + 4 * 5, ld_out=50,
+                           rows=20, cols=40, nsplit=3, accumulate=0)])
+    torch.cuda.synchronize()
+    assert torch.equal(buf, S.to_s8_torch(src[idx]))
+    ref = torch.full((20, 50), 7.0, device=dev)
+    ref[:, 5:45] = ws[0, :, 10:50] + ws[1, :, 10:50] + ws[2, :, 10:50]
+    assert torch.equal(out, ref)
