@@ -5,8 +5,11 @@ One "step" = one rsl_rl learning iteration of the drop-in runner on synthetic Go
 terrain: 24 env steps (policy act + fused HIP env step + storage + the per-step episode
 bookkeeping train.py's runner does, on_policy_runner.py:160-170) + GAE + the PPO/ROA update
 (5 epochs x 4 minibatches) — i.e. Perf/total_fps of on_policy_runner.py:219.
-value = num_envs x 24 x world_size x K / (max over ranks of the timed K iterations);
-`value_no_episode_tracking` is the same loop without the bookkeeping.
+value = num_envs x 24 x world_size x K / (max over ranks of the timed K iterations), the MEDIAN
+of 3 windows of K iterations each (`windows` lists all three, with the GPU shader clock read
+after each); `value_no_episode_tracking` is one window of the same loop without the bookkeeping.
+The windows avoid the runner's DAgger iterations (it % 20 == 0, on_policy_runner.py:147) when
+W + K <= 18.
 
 Also reported: `roofline` of the env-step kernel (algorithmic bytes per launch over its
 HIP-event-timed duration vs 8 TB/s HBM; the kernel is not HBM-bound: `roofline_valu` gives
@@ -50,21 +53,46 @@ def env_bytes_per_env_step(P, num_bodies, ks):
 MFMA_BF16_PEAK_TFLOPS = 2500.0  # dense bf16 (MI355X_MICROARCH.md); 3xbf16 = 3 MFMA products per fp32 MAC
 
 
+def sclk_mhz():
+    """The current shader clock (MHz) of the busiest GPU on this node, from the driver's sysfs
+    DPM table (the line marked '*'); None where it cannot be read."""
+    import glob
+    best = None
+    for f in glob.glob("/sys/class/drm/card*/device/pp_dpm_sclk"):
+        try:
+            for line in open(f):
+                if line.rstrip().endswith("*"):
+                    mhz = int(line.split(":")[1].strip().lower().split("mhz")[0])
+                    best = mhz if best is None else max(best, mhz)
+        except (OSError, ValueError, IndexError):
+            pass
+    return best
+
+
 def learner_gemm_roofline(dev, rows=24576, reps=10):
-    """The update's weight-gradient group (every dW/db of one go2 minibatch backward, one
-    lgx_gemm_group launch + its split-K reduction) timed with HIP events on its stream:
-    MFMA rate = 3 bf16 products x 2 x rows x sum(in x out) / time."""
-    from legged_gym_custom_amd.rsl_rl.modules import hip_mlp as H
+    """The update's weight-gradient group — every dW of one go2 minibatch backward in ONE
+    lgx_s8_gemm_group launch on pre-split (S8) operands, plus its split-K reduction launch —
+    timed with HIP events on its stream: MFMA rate = 3 bf16 products x 2 x rows x sum(in x out)
+    / time; HBM = the operands (4 B per element, S8 as fp32) read once."""
+    from legged_gym_custom_amd.rsl_rl.modules import hip_s8 as S
     layers = [(627, 512), (512, 256), (256, 128), (128, 12), (736, 512), (512, 256), (256, 128), (128, 1),
               (29, 64), (64, 20), (20, 20), (132, 128), (128, 64), (64, 32), (572, 128), (128, 64), (64, 3)]
     g = torch.Generator(device=dev).manual_seed(7)
-    data = [(torch.randn(rows, o, device=dev, generator=g), torch.randn(rows, i, device=dev, generator=g),
-             torch.zeros(o, i, device=dev), torch.zeros(o, device=dev)) for i, o in layers]
+    data = [(S.to_s8(torch.randn(rows, o, device=dev, generator=g)), S.to_s8(torch.randn(rows, i, device=dev, generator=g)),
+             torch.zeros(o, i, device=dev)) for i, o in layers]
+    splits = S.pick_split([(o, i, rows) for i, o in layers])
+    ws = torch.empty(sum(s * i * o for s, (i, o) in zip(splits, layers)), device=dev)
+    args, red, off = [], [], 0
+    for (dy, x, dW), s, (i, o) in zip(data, splits, layers):
+        w = ws.data_ptr() + 4 * off
+        args.append(S.GemmArgs(A=dy.data_ptr(), lda=dy.shape[1], B=x.data_ptr(), ldb=x.shape[1], M=o, N=i, K=rows,
+                               C32=w, ldc32=i, split=s))
+        red.append(S.flat_reduce(w, o * i, dW.data_ptr(), o * i, s))
+        off += s * o * i
 
     def once():
-        with H.deferred_weight_grads():
-            for dy, x, dW, db in data:
-                H.linear_weight_grad(dy, x, dW, db, accumulate=True)
+        S.gemm_group(args, S.DW)
+        S.reduce(red)
     side = torch.cuda.Stream(dev)
     side.wait_stream(torch.cuda.current_stream(dev))
     with torch.cuda.stream(side):
@@ -93,8 +121,8 @@ def learner_gemm_roofline(dev, rows=24576, reps=10):
     flop = 2.0 * rows * sum(i * o for i, o in layers)
     achieved = 3 * flop / t / 1e12
     # algorithmic HBM bytes: every activation (X) and output gradient (dY) of the minibatch
-    # read once (fp32), every dW/db read and written once (accumulate)
-    nbytes = 4.0 * rows * sum(i + o for i, o in layers) + 2 * 4.0 * sum(i * o + o for i, o in layers)
+    # read once (4 B per element: bf16 hi + lo), every dW written once
+    nbytes = 4.0 * rows * sum(i + o for i, o in layers) + 4.0 * sum(i * o for i, o in layers)
     gbs = nbytes / t / 1e9
     # the binding roofline is the larger of the two ideal times (here HBM: 657 MB at 8 TB/s
     # = 82 us vs 168 bf16 GFLOP at 2.5 PF/s = 67 us)
@@ -107,7 +135,7 @@ def learner_gemm_roofline(dev, rows=24576, reps=10):
     top = dict(hbm if t_hbm >= t_mfma else mfma)
     top.pop("note", None)
     return {"bound": "hbm" if t_hbm >= t_mfma else "mfma",
-            "kernel": "lgxm::gemm_group_kernel<2, 128> + splitk_reduce_batch",
+            "kernel": "lgxs::s8_gemm_kernel<2, 2> + s8_reduce_kernel",
             "workload": f"all 17 weight gradients of one go2 minibatch ({rows} rows)", **top,
             "us_per_launch": round(t * 1e6, 1), "ideal_us": {"hbm": round(t_hbm * 1e6, 1), "mfma": round(t_mfma * 1e6, 1)},
             "hbm": hbm, "mfma": mfma}
@@ -336,12 +364,17 @@ def main():
     if args.task.startswith("anymal"):
         return rollout_only(args, runner, env, dev, world, rank, barrier)
     elapsed_nt, perf_nt = timed(False)  # iterations 0..W-1 warm-up (0 is a DAgger iteration), then W..W+K-1
-    # same window position for the tracked run (no DAgger iteration inside either window,
-    # it % 20 == 0, on_policy_runner.py:147)
-    runner.current_learning_iteration = 21
-    elapsed, perf = timed(True)  # the headline: as train.py runs it
+    # the headline, as train.py runs it: 3 windows, each W warm-up + K timed iterations starting
+    # right after a DAgger iteration (it % 20 == 0, on_policy_runner.py:147), so none is inside
     steps_per_iter = train_cfg.runner.num_steps_per_env
     total_env_steps = args.num_envs * steps_per_iter * world * args.steps
+    windows = []
+    for w in range(3):
+        runner.current_learning_iteration = 20 * (w + 1) + 1
+        el_w, perf_w = timed(True)
+        windows.append((el_w, perf_w, sclk_mhz()))
+    order = sorted(range(3), key=lambda i: windows[i][0])
+    elapsed, perf, _clk = windows[order[1]]
     value = total_env_steps / elapsed
 
     # ---- env-step kernel alone (HIP events on the launch stream) -> roofline
@@ -381,6 +414,9 @@ def main():
                        "num_envs_per_gpu": args.num_envs, "num_steps_per_env": steps_per_iter,
                        "global_envs": args.num_envs * world, "parallelism": f"env-sharded dp{world}"},
             "value_no_episode_tracking": round(total_env_steps / elapsed_nt, 1),
+            "windows": [{"value": round(total_env_steps / el, 1), "ms_per_step": round(el / args.steps * 1e3, 3),
+                         "sclk_mhz": clk} for el, _p, clk in windows],
+            "window_spread": round((max(w[0] for w in windows) - min(w[0] for w in windows)) / elapsed, 4),
             "collection_s": round(perf.get("collection_time", 0.0), 4),
             "learn_s": round(perf.get("learn_time", 0.0), 4),
             "env_kernel": {"avg_us": round(kern_avg_ms * 1e3, 2), "min_us": round(kern_ms[0] * 1e3, 2),

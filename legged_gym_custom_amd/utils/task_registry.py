@@ -61,7 +61,9 @@ class TaskRegistry:
             # follows the same value
             train_cfg.seed = env.cfg.seed
         if log_root == "default":
-            log_root = os.path.join(LEGGED_GYM_ROOT_DIR, "logs", train_cfg.runner.experiment_name)
+            # LGX_LOG_ROOT (optional) relocates <repo>/logs, e.g. for a test running train.py
+            base = os.environ.get("LGX_LOG_ROOT") or os.path.join(LEGGED_GYM_ROOT_DIR, "logs")
+            log_root = os.path.join(base, train_cfg.runner.experiment_name)
             log_dir = os.path.join(log_root, datetime.now().strftime("%b%d_%H-%M-%S") + "_" + train_cfg.runner.run_name)
         elif log_root is None:
             log_dir = None

@@ -1,0 +1,31 @@
+"""The reference's own, unchanged legged_gym/scripts/train.py (train.py:35-48: `import isaacgym`,
+`from legged_gym.envs import *`, get_args, task_registry.make_env / make_alg_runner, learn) runs
+against this package — north_star's "train.py --task=go2 runs unchanged" — on the reference's CPU
+path (--sim_device=cpu --rl_device=cpu, config C1) for one iteration.
+
+Build-container only: the script is executed where it lies under /root/reference (never copied),
+in a fresh interpreter with PYTHONPATH = this repository (so `legged_gym`, `rsl_rl`, `isaacgym`
+resolve to its drop-in modules), no bytecode written and logs in a temporary directory. Skipped
+where /root/reference is absent (the GPU box)."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SCRIPT = "/root/reference/legged_gym/scripts/train.py"
+
+
+@pytest.mark.skipif(not os.path.exists(SCRIPT), reason="the reference tree is not on this machine")
+@pytest.mark.parametrize("task", ["go2", "go2_parkour"])
+def test_reference_train_script_runs_unchanged(task, tmp_path):
+    env = dict(os.environ, PYTHONPATH=REPO, PYTHONDONTWRITEBYTECODE="1", LGX_LOG_ROOT=str(tmp_path),
+               OMP_NUM_THREADS="4")
+    cmd = [sys.executable, SCRIPT, f"--task={task}", "--sim_device=cpu", "--rl_device=cpu", "--num_envs=64",
+           "--max_iterations=1", "--headless"]
+    r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
+    assert "Learning iteration 0/1" in r.stdout or "Learning iteration" in r.stdout, r.stdout[-2000:]
+    # the run wrote its log directory (and no file) under the temporary log root
+    assert any(os.scandir(str(tmp_path)))
