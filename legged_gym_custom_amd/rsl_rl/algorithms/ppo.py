@@ -40,6 +40,9 @@ from .s8_update import S8Minibatch
 
 # the GPU minibatch on the pre-split GEMM core (s8_update.py); "0" selects the autograd path
 USE_S8 = os.environ.get("LGX_S8_UPDATE", "1") != "0"
+# under RCCL ("nccl"), the per-minibatch gradient all-reduce is captured inside the one update
+# graph; "0" keeps the phased graphs (per-minibatch replays around host-issued all-reduces)
+GRAPH_ALLREDUCE = os.environ.get("LGX_GRAPH_ALLREDUCE", "1") != "0"
 
 
 def _distributed():
@@ -231,6 +234,9 @@ class PPO:
         self.graph_mode = None  # "whole" | "phased" once captured
         self.phased_graphs = None  # None: phased iff world_size > 1 (tests force it on one GPU)
         self.use_s8 = USE_S8 and self.on_gpu
+        # reduce the gradients over the process group even at world size 1 (tests of the
+        # distributed path's graph capture on one GPU)
+        self.allreduce_always = False
         self._s8 = None  # S8Minibatch, built at the first update (static buffers for the graphs)
 
     # ------------------------------------------------------------------ flat Adam (HIP)
@@ -520,8 +526,15 @@ class PPO:
             self.optimizer.step()
             self._sums.add_(self._losses)
 
+    def _reducing(self):
+        return _distributed() or (self.allreduce_always and dist.is_available() and dist.is_initialized())
+
+    def _captures_allreduce(self):
+        """RCCL collectives can be recorded in a hipGraph (gloo's host-side ones cannot)."""
+        return GRAPH_ALLREDUCE and dist.is_initialized() and dist.get_backend() == "nccl"
+
     def _allreduce_minibatch(self):
-        if _distributed():
+        if self._reducing():
             span = self.grads.span("main", "kl")
             dist.all_reduce(span)
             span.div_(dist.get_world_size())
@@ -609,14 +622,20 @@ class PPO:
         torch.cuda.synchronize(self.device)
         slices = self._minibatches()
         pool = torch.cuda.graph_pool_handle()
-        phased = _distributed() if self.phased_graphs is None else self.phased_graphs
+        reducing = self._reducing()
+        phased = (reducing and not self._captures_allreduce()) if self.phased_graphs is None else self.phased_graphs
         if not phased:
+            # one graph for the whole update; at world size > 1 under RCCL the per-minibatch
+            # all-reduce of [main | estimator | kl] is recorded in it (ppo.py:273-276: the
+            # global-norm clip after the reduce)
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, pool=pool):
                 self._precompute()
                 for _ in range(self.num_learning_epochs):
                     for idx in slices:
                         self._minibatch_grads(idx)
+                        if reducing:
+                            self._allreduce_minibatch()
                         self._minibatch_step()
             self._graphs = {"whole": g}
             self.graph_mode = "whole"

@@ -121,7 +121,7 @@ class OnPolicyRunner:
         self.last_perf = {}
         self.use_graphs = str(device).startswith("cuda")
         self._graphs = {}
-        self._eager_rollouts = 0
+        self._eager_rollouts = {}  # per adaptation mode
         self._stats = None
         self._obs = None
         _ = self.env.reset()
@@ -216,11 +216,16 @@ class OnPolicyRunner:
             self._track_episodes(rewards, dones, infos)
 
     def _graphable(self, adaptation_mode):
-        return (self.use_graphs and not adaptation_mode and self.device.startswith("cuda")
+        return (self.use_graphs and self.device.startswith("cuda")
                 and hasattr(self.env, "advance_step_counter") and getattr(self.env, "graph_capturable", True))
 
+    @staticmethod
+    def _rollout_key(adaptation_mode, track):
+        # one graph per (DAgger iteration's adaptation-mode rollout, PPO rollout) x tracking
+        return ("rollout", track) if not adaptation_mode else ("rollout", track, "adaptation")
+
     def _rollout(self, adaptation_mode, track):
-        key = ("rollout", track)
+        key = self._rollout_key(adaptation_mode, track)
         if self._graphable(adaptation_mode) and key in self._graphs:
             self._graphs[key].replay()
             self.alg.storage.step = self.num_steps_per_env
@@ -228,14 +233,17 @@ class OnPolicyRunner:
             return
         for _ in range(self.num_steps_per_env):
             self._rollout_step(adaptation_mode, track)
-        if not adaptation_mode:
-            self._eager_rollouts += 1
+        mode = bool(adaptation_mode)
+        self._eager_rollouts[mode] = self._eager_rollouts.get(mode, 0) + 1
 
-    def _capture_rollout(self, track):
-        """Record the 24-step rollout once (after one eager rollout has warmed every
-        kernel and the storage is empty). Capture does not execute anything."""
-        key = ("rollout", track)
-        if key in self._graphs or not self._graphable(False) or self._eager_rollouts < 1:
+    def _capture_rollout(self, track, adaptation_mode=False):
+        """Record the 24-step rollout of this mode once (after one eager rollout of it has
+        warmed every kernel and the storage is empty). Capture does not execute anything. The
+        DAgger iterations' rollout (adaptation mode: the latent from the adaptation encoder over
+        the observation history, ppo.py:135-141) gets its own graph."""
+        key = self._rollout_key(adaptation_mode, track)
+        if (key in self._graphs or not self._graphable(adaptation_mode)
+                or self._eager_rollouts.get(bool(adaptation_mode), 0) < 1):
             return
         torch.cuda.synchronize(self.device)
         csc, st0 = self.env.common_step_counter, self.alg.storage.step
@@ -244,7 +252,7 @@ class OnPolicyRunner:
         # state, which must stay a normal tensor for the update graph's capture
         with torch.inference_mode(False), torch.no_grad(), torch.cuda.graph(g):
             for _ in range(self.num_steps_per_env):
-                self._rollout_step(False, track)
+                self._rollout_step(adaptation_mode, track)
         self.env.common_step_counter = csc  # host mirror (capture advanced it, the device did not)
         self.alg.storage.step = st0
         self._graphs[key] = g
@@ -299,7 +307,7 @@ class OnPolicyRunner:
                 collection_time, learn_time = mid - start, stop - mid
             self.last_perf = {"collection_time": collection_time, "learn_time": learn_time,
                               "fps": self.num_steps_per_env * env.num_envs / (collection_time + learn_time)}
-            self._capture_rollout(track)
+            self._capture_rollout(track, use_adaptation_mode)
             if self.log_dir is not None:
                 rewbuffer, lenbuffer, ep_means = self._host_stats()
                 self.log(locals())
@@ -401,7 +409,7 @@ class OnPolicyRunner:
 
     def load(self, path, load_optimizer=True):
         self._graphs = {}
-        self._eager_rollouts = 0
+        self._eager_rollouts = {}
         loaded = torch.load(path, map_location=self.device, weights_only=True)
         self.alg.actor_critic.load_state_dict(loaded["model_state_dict"])
         if load_optimizer:

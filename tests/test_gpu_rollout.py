@@ -24,7 +24,7 @@ def _setup(use_graphs):
     return env, runner
 
 
-def _run(env, runner, iters):
+def _run(env, runner, iters, adaptation_mode=False):
     import torch as T
     z = lambda *sh: T.zeros(*sh, device="cuda:0")  # noqa: E731
     runner._stats = {"cur_rew": z(env.num_envs), "cur_len": z(env.num_envs), "rew_ring": z(101), "len_ring": z(101),
@@ -36,14 +36,14 @@ def _run(env, runner, iters):
     csc0 = env.common_step_counter
     for _ in range(iters):
         with T.inference_mode():
-            runner._rollout(False, True)
+            runner._rollout(adaptation_mode, True)
         s = runner.alg.storage
         snaps.append({"obs": s.observations.clone(), "rew": s.rewards.clone(), "dones": s.dones.clone(),
                       "root": env.root_states.clone(), "csc": env.common_step_counter - csc0,
                       "ring": runner._stats["rew_ring"][:100].clone(),  # slot 100 = discard (arbitrary)
                       "n": int(runner._stats["n"])})
         s.clear()
-        runner._capture_rollout(True)  # as learn() does after each iteration (no-op when eager)
+        runner._capture_rollout(True, adaptation_mode)  # as learn() does after each iteration (no-op when eager)
     return snaps
 
 
@@ -59,6 +59,21 @@ def test_graph_rollout_equals_eager():
             torch.testing.assert_close(b[k], a[k], rtol=0, atol=0, msg=f"iteration {i} {k}")
         assert a["n"] == b["n"]
     assert int(env_b._step_dev) == env_b.common_step_counter + 1  # the next step's number
+
+
+def test_graph_adaptation_rollout_equals_eager():
+    """The DAgger iterations' rollout (adaptation mode: the adaptation encoder's latent over the
+    observation history drives the actor, ppo.py:135-141) replayed from its own hipGraph equals
+    the eager loop bit for bit."""
+    env_a, run_a = _setup(False)
+    eager = _run(env_a, run_a, 4, adaptation_mode=True)
+    env_b, run_b = _setup(True)
+    graph = _run(env_b, run_b, 4, adaptation_mode=True)
+    assert ("rollout", True, "adaptation") in run_b._graphs and ("rollout", True) not in run_b._graphs
+    for i, (a, b) in enumerate(zip(eager, graph)):
+        assert a["csc"] == b["csc"] == 6 * (i + 1)
+        for k in ("obs", "rew", "dones", "root", "ring"):
+            torch.testing.assert_close(b[k], a[k], rtol=0, atol=0, msg=f"iteration {i} {k}")
 
 
 def test_native_episode_extras_match_torch():
