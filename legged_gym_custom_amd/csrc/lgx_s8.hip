@@ -96,7 +96,8 @@ struct Op {
   static constexpr int PW = NI / NW;                  // per wave
   static constexpr int IMG = BT * BK * 4;             // bytes (16 KB)
 
-  // per-lane 32-bit source offsets of this wave's instructions (step 0); t0 = tile's first m/n
+  // per-lane 32-bit source offsets of this wave's instructions (step 0); t0 = the tile's first
+  // m / n, R = M / N (the operand's extent along the tile), ld = row pitch (bytes)
   __device__ __forceinline__ static void offsets(uint32_t (&off)[PW], int wave, int lane, int t0, int R,
                                                  int64_t ld, int kbeg) {
 #pragma unroll
@@ -104,8 +105,11 @@ struct Op {
       const int i = wave + NW * j;
       const int r = i * RPI + lane / SLOTS, ps = lane % SLOTS;
       if (TR) {  // r = k (source row kbeg + r), columns t0 .. t0 + 127
+        // columns clamped to the operand's own groups [0, round_up(R, 8)) — the span the
+        // producer wrote — never the row pitch: an operand may start past column 0 of a wider
+        // row (a column span), and reading to the pitch would run past the buffer's last row
         const int ls = ps ^ fsw_tr(r);
-        const int64_t cb = std::min<int64_t>((int64_t)t0 * 4 + ls * 16, ld - 16);
+        const int64_t cb = std::min<int64_t>((int64_t)t0 * 4 + ls * 16, (int64_t)((R + 7) / 8) * 32 - 16);
         off[j] = (uint32_t)((int64_t)(kbeg + r) * ld + cb);
       } else {   // r = tile row (source row t0 + r, clamped), k from kbeg
         const int ls = ps ^ fsw_row(r);

@@ -19,7 +19,8 @@ the minibatch permutation of each update is injected (rollout_storage.py:142).
 
 Cases run at N=64 envs (384-row minibatches) except go2_c2: C2's exact shapes, N=4096, T=24,
 so the update's minibatches are 24,576 rows as in the bench (rollout_storage.py:141) and the
-HIP GEMMs take their production tile shapes, split-K picks and grids. Its per-step rollout
+HIP GEMMs take their production tile shapes, split-K picks and grids; and go2_parkour_c4: C4's,
+N=8192 (49,152-row minibatches, the parkour estimator). Its per-step rollout
 outputs are stored sampled (`record`) instead of whole (`sampled_rollout`).
 Also recorded: the parameters after minibatch 0's optimizer steps (one Adam step each: the
 tight parameter check) and the Adam moments after the update.
@@ -52,6 +53,13 @@ CASES = {
                    est_h=[128, 64], latent=20, scan_out=32, lr=2e-4, est_lr=1e-3, schedule="fixed",
                    desired_kl=0.01, entropy=0.01, epochs=5, minibatches=4, gamma=0.99, lam=0.95, clip=0.2,
                    max_grad_norm=1.0),
+    # C4: go2_parkour at 8192 envs (49,152-row minibatches, the [256, 128] estimator and the scan
+    # encoder at their production shape; go2_parkour_config.py:229,242,256)
+    "go2_parkour_c4": dict(seed=14, N=8192, sampled_rollout=True, P=52, H=10, priv=29, critic=736, est=3, scan=132,
+                           A=12, actor=[512, 256, 128], critic_h=[512, 256, 128], priv_h=[64, 20], scan_h=[128, 64],
+                           est_h=[256, 128], latent=20, scan_out=32, lr=2e-4, est_lr=1e-4, schedule="fixed",
+                           desired_kl=0.01, entropy=0.01, epochs=5, minibatches=4, gamma=0.99, lam=0.95, clip=0.2,
+                           max_grad_norm=1.0),
 }
 SMALL_CASES = [k for k, c in CASES.items() if c.get("N", N) <= 64]  # the CPU suite's cases
 
