@@ -102,18 +102,29 @@ def run(case, device, use_graphs=None):
     # the parameters after minibatch 0's optimizer steps: snapshot at the first _minibatch_step
     # (the first update runs eagerly before any graph is captured; capture calls it again and
     # then takes no snapshot)
-    mb0 = {}
+    mb0, e0, count = {}, {}, [0]
     step = alg._minibatch_step
+    names_of = {id(p): n for n, p in named_params(alg)}
 
     def first_step():
         step()
+        count[0] += 1
         if not mb0:
             mb0.update({n: p.detach().clone() for n, p in named_params(alg)})
+        if count[0] == alg.num_mini_batches:  # the Adam moments after epoch 0 (eager update)
+            for oname in ("optimizer", "estimator_optimizer"):
+                opt = getattr(alg, oname)
+                for grp in opt.param_groups:
+                    for p in grp["params"]:
+                        st = opt.state[p]
+                        e0[names_of[id(p)]] = (_np(st["exp_avg"]), _np(st["exp_avg_sq"]))
 
     alg._minibatch_step = first_step
     mv, ms, mr, coef, me = alg.update()
     del alg._minibatch_step
     res["mb0"] = {n: _np(p) for n, p in mb0.items()}
+    res["exp_avg_e0"] = {n: m for n, (m, v) in e0.items()}
+    res["exp_avg_sq_e0"] = {n: v for n, (m, v) in e0.items()}
     res["update.losses"] = np.array([mv, ms, mr, coef, me])
     res["update.learning_rate"] = alg.learning_rate
     res["after"] = {n: _np(p) for n, p in named_params(alg)}

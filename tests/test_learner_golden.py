@@ -77,6 +77,14 @@ def test_update_losses_lr_params_moments(replay):
         LC.compare(d, "exp_avg_sq", n, res["exp_avg_sq"][n], rtol=1e-3, atol=1e-12)
 
 
+def test_update_moments_after_epoch0(replay):
+    """The Adam moments after epoch 0's last minibatch (num_mini_batches steps)."""
+    case, d, res, _ = replay
+    for n, m in res["exp_avg_e0"].items():
+        LC.compare(d, "exp_avg_e0", n, m, rtol=1e-3, atol=1e-7)
+        LC.compare(d, "exp_avg_sq_e0", n, res["exp_avg_sq_e0"][n], rtol=1e-3, atol=1e-12)
+
+
 def test_update_minibatch0_adam_step(replay):
     """Parameters after minibatch 0's single Adam step (+-lr by the gradient's sign)."""
     case, d, res, _ = replay

@@ -13,12 +13,16 @@ T=24 steps):
   * compute_returns: returns and normalised advantages (rollout_storage.py:110-124);
   * update_dagger: the adaptation encoder after it, its Adam moments, the mean loss;
   * update: the pre-clip gradients of minibatch 0 (hooked at clip_grad_norm_), the
-    parameters after minibatch 0's Adam steps (hooked at the optimizers' step), the
-    returned losses, the learning rate, every parameter after the update and the Adam
-    moments (sampled entries + fp64 sum/sum-of-squares per tensor; learner_case.record).
+    parameters after minibatch 0's Adam steps (hooked at the optimizers' step), the Adam
+    moments after epoch 0 (num_mini_batches steps), the returned losses, the learning rate,
+    every parameter after the update and the Adam moments after it (sampled entries + fp64
+    sum/sum-of-squares per tensor; learner_case.record).
 Injected: the Normal sample (loc + scale * eps) and torch.randperm.
 
 Usage:  python tools/gen_learner_golden.py  [case ...]
+Run it with torch's default CPU thread count (no OMP_NUM_THREADS override): the CPU replay
+test compares the first Adam step at atol 1e-7, and the CPU GEMMs' summation order follows the
+thread count.
 """
 import json
 import os
@@ -197,22 +201,26 @@ def main(cases):
 
         nn.utils.clip_grad_norm_ = clip_hook
         # the parameters after minibatch 0's optimizer steps (one Adam step each; ppo.py:228-231
-        # for the estimator, :273-276 for the rest)
-        mb0 = {}
+        # for the estimator, :273-276 for the rest), and the Adam moments after epoch 0's last
+        # minibatch (num_mini_batches steps: before the update's sensitivity to rounding builds up)
+        mb0, e0, nsteps = {}, {}, {}
 
-        def once(opt, key):
+        def once(opt, key, oname):
             step = opt.step
 
             def wrapped(*a, **k):
                 r = step(*a, **k)
+                nsteps[key] = nsteps.get(key, 0) + 1
                 if key not in mb0:
                     mb0[key] = {names_of[id(p)]: p.detach().numpy().copy() for g in opt.param_groups
                                 for p in g["params"]}
+                if nsteps[key] == alg.num_mini_batches:
+                    e0[key] = {n: (m.copy(), v.copy()) for n, (m, v, _s) in adam_state(opt, names_of).items()}
                 return r
             opt.step = wrapped
 
-        once(alg.optimizer, "main")
-        once(alg.estimator_optimizer, "est")
+        once(alg.optimizer, "main", "optimizer")
+        once(alg.estimator_optimizer, "est", "estimator_optimizer")
         _Inject.perm = torch.from_numpy(LC.permutation(case, 1))
         mv, ms, mr, coef, me = alg.update()
         _Inject.perm = None
@@ -221,6 +229,9 @@ def main(cases):
         for key in ("main", "est"):
             for n, p in mb0[key].items():
                 LC.record(out, "mb0", n, p)
+            for n, (m, v) in e0[key].items():
+                LC.record(out, "exp_avg_e0", n, m)
+                LC.record(out, "exp_avg_sq_e0", n, v)
         out["update.losses"] = np.array([mv, ms, mr, coef, me], dtype=np.float64)
         out["update.learning_rate"] = np.float64(alg.learning_rate)
         out["update.grad_norm0"] = np.array([grads0["est_norm"], grads0["main_norm"]], dtype=np.float64)
