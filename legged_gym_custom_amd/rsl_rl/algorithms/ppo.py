@@ -529,6 +529,13 @@ class PPO:
     def _reducing(self):
         return _distributed() or (self.allreduce_always and dist.is_available() and dist.is_initialized())
 
+    @staticmethod
+    def capture_mode():
+        """hipGraph capture mode. Under a process group the capture is thread-local: RCCL's
+        watchdog thread polls the events of earlier eager collectives while this thread
+        captures, which a global-mode capture rejects (hipErrorStreamCaptureUnsupported)."""
+        return "thread_local" if dist.is_available() and dist.is_initialized() else "global"
+
     def _captures_allreduce(self):
         """RCCL collectives can be recorded in a hipGraph (gloo's host-side ones cannot)."""
         return GRAPH_ALLREDUCE and dist.is_initialized() and dist.get_backend() == "nccl"
@@ -622,6 +629,7 @@ class PPO:
         torch.cuda.synchronize(self.device)
         slices = self._minibatches()
         pool = torch.cuda.graph_pool_handle()
+        mode = self.capture_mode()
         reducing = self._reducing()
         phased = (reducing and not self._captures_allreduce()) if self.phased_graphs is None else self.phased_graphs
         if not phased:
@@ -629,7 +637,7 @@ class PPO:
             # all-reduce of [main | estimator | kl] is recorded in it (ppo.py:273-276: the
             # global-norm clip after the reduce)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=pool):
+            with torch.cuda.graph(g, pool=pool, capture_error_mode=mode):
                 self._precompute()
                 for _ in range(self.num_learning_epochs):
                     for idx in slices:
@@ -641,16 +649,16 @@ class PPO:
             self.graph_mode = "whole"
         else:
             gp = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(gp, pool=pool):
+            with torch.cuda.graph(gp, pool=pool, capture_error_mode=mode):
                 self._precompute()
             ga = []
             for idx in slices:
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, pool=pool):
+                with torch.cuda.graph(g, pool=pool, capture_error_mode=mode):
                     self._minibatch_grads(idx)
                 ga.append(g)
             gb = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(gb, pool=pool):
+            with torch.cuda.graph(gb, pool=pool, capture_error_mode=mode):
                 self._minibatch_step()
             self._graphs = {"P": gp, "A": ga, "B": gb}
             self.graph_mode = "phased"

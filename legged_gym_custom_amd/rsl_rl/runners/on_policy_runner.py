@@ -250,7 +250,8 @@ class OnPolicyRunner:
         g = torch.cuda.CUDAGraph()
         # no_grad, not inference_mode: capture registers the CUDA generator's graph-safe
         # state, which must stay a normal tensor for the update graph's capture
-        with torch.inference_mode(False), torch.no_grad(), torch.cuda.graph(g):
+        with torch.inference_mode(False), torch.no_grad(), \
+                torch.cuda.graph(g, capture_error_mode=self.alg.capture_mode()):
             for _ in range(self.num_steps_per_env):
                 self._rollout_step(adaptation_mode, track)
         self.env.common_step_counter = csc  # host mirror (capture advanced it, the device did not)

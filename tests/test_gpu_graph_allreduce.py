@@ -5,6 +5,7 @@ kl] between its backward and its optimizer tail (ppo.py:273-276) — eagerly in 
 captured graph in the other. Graph == eager, bit for bit, over three updates; the graph mode is
 "whole" (no per-minibatch replays around host-issued collectives)."""
 import os
+import queue
 import socket
 import sys
 
@@ -57,9 +58,16 @@ def test_update_graph_records_the_rccl_allreduce():
     q = ctx.Queue()
     p = ctx.Process(target=_worker, args=(0, _port(), q))
     p.start()
-    res = q.get(timeout=600)
+    res = None
+    for _ in range(320):  # the child reports or dies; never wait on a dead one
+        try:
+            res = q.get(timeout=0.5)
+            break
+        except queue.Empty:
+            if not p.is_alive():
+                break
     p.join(timeout=60)
-    assert p.exitcode == 0
+    assert res is not None and p.exitcode == 0, p.exitcode
     (w_eager, mode_eager, lr_eager), (w_graph, mode_graph, lr_graph) = res[False], res[True]
     assert mode_graph == "whole", mode_graph
     assert lr_graph == lr_eager
