@@ -5,9 +5,10 @@
 // inputs and the loss heads' gradients). So the K loop moves bytes and multiplies: no fp32 ->
 // bf16 split, no VGPR round trip.
 //
-// Block: 256 threads = 4 waves as 2 x 2, output tile 128 x 128, each wave 64 x 64 = 4 x 4
-// tiles of v_mfma_f32_16x16x32_bf16; per product lo*hi + hi*lo + hi*hi (3 x bf16, fp32
-// accumulation; lgx_mlp.hip's order). K step 32, NS stages of LDS.
+// Block: output tile BM x 128 (BM 128: 4 waves, 2 LDS stages, 2 blocks per CU; BM 256: 8 waves,
+// 3 stages, 1 block per CU — lgxs::Cfg), each wave 64 x 64 = 4 x 4 tiles of
+// v_mfma_f32_16x16x32_bf16; per product lo*hi + hi*lo + hi*hi (3 x bf16, fp32 accumulation;
+// lgx_mlp.hip's order). K step 32.
 // Staging: global_load_lds_dwordx4 (LDS-DMA; destination = wave base + 16 B x lane), 8 per wave
 // per K step, NS - 1 steps in flight across raw s_barriers with a counted vmcnt — no barrier
 // drains the DMA (cdna_hip_programming.md §5 "Pipelining across barriers"). Images:
@@ -38,24 +39,26 @@ typedef float f32x4u __attribute__((ext_vector_type(4), aligned(4)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 #define LDS_AS __attribute__((address_space(3)))
 
-#ifndef LGX_S8_NS
-#define LGX_S8_NS 2
-#endif
 #ifndef LGX_S8_BK
 #define LGX_S8_BK 32
 #endif
-#ifndef LGX_S8_NW
-#define LGX_S8_NW 4
+#ifndef LGX_S8_BIG
+#define LGX_S8_BIG 0  // bit (1 << kind): that kind runs on the 256-row tile configuration
 #endif
 
 namespace lgxs {
 
-constexpr int BK = LGX_S8_BK, BT = 128, NW = LGX_S8_NW, NT = 64 * NW, GMAX = LGX_S8_GROUP_MAX;
-// waves as 2 (rows) x NW/2 (columns); each wave 64 x WN (WN = 64 or 32: NJ 16-wide tiles)
-constexpr int WN = BT / (NW / 2), NJ = WN / 16;
-static_assert(NW == 4 || NW == 8, "4 or 8 waves");
+constexpr int BK = LGX_S8_BK, BN = 128, NJ = 4, GMAX = LGX_S8_GROUP_MAX;
 static_assert(BK == 32 || BK == 64, "K step 32 or 64");
-constexpr int CP = BT + 4;  // fp32 epilogue image pitch (floats)
+constexpr int CP = BN + 4;  // fp32 epilogue image pitch (floats)
+// Tile configurations: output tile BM x 128, BM / 32 waves as (BM / 64) x 2, each wave 64 x 64
+// (4 x 4 MFMA tiles). BM 128: 4 waves, NS 2 stages, 2 blocks per CU. BM 256: 8 waves, NS 3
+// stages of 48 KB, 1 block per CU — two steps of DMA in flight per CU instead of one, and a
+// quarter fewer L2 bytes per MFMA.
+template <int BM_>
+struct Cfg {
+  static constexpr int BM = BM_, NW = BM_ / 32, NT = 64 * NW, WR = BM_ / 64, NS = BM_ == 128 ? 2 : 3;
+};
 
 // slot swizzles (16-B slot index XOR), image row -> mask
 __device__ __forceinline__ int fsw_row(int r) {
@@ -87,14 +90,16 @@ struct Group {
 static_assert(sizeof(Group) <= 4096, "kernel argument segment");
 
 // An operand's staging geometry (one K step).
-template <bool TR>
+// T = the tile's extent along this operand (BM for A, BN for B); NW = waves of the block.
+template <bool TR, int T, int NW>
 struct Op {
-  static constexpr int PITCH = TR ? BT * 4 : BK * 4;  // image row bytes
+  static constexpr int PITCH = TR ? T * 4 : BK * 4;  // image row bytes
   static constexpr int SLOTS = PITCH / 16;
-  static constexpr int RPI = 1024 / PITCH;            // image rows per DMA wave-instruction
-  static constexpr int NI = BT * BK * 4 / 1024;       // DMA wave-instructions per step (16)
-  static constexpr int PW = NI / NW;                  // per wave
-  static constexpr int IMG = BT * BK * 4;             // bytes (16 KB)
+  static constexpr int RPI = 1024 / PITCH;           // image rows per DMA wave-instruction
+  static constexpr int NI = T * BK * 4 / 1024;       // DMA wave-instructions per step
+  static constexpr int PW = NI / NW;                 // per wave
+  static constexpr int IMG = T * BK * 4;             // bytes
+  static_assert(PW * NW == NI && RPI >= 1, "DMA split");
 
   // per-lane 32-bit source offsets of this wave's instructions (step 0); t0 = the tile's first
   // m / n, R = M / N (the operand's extent along the tile), ld = row pitch (bytes)
@@ -208,11 +213,12 @@ __device__ __forceinline__ void load_s8(const char* src, float (&v)[8]) {
   }
 }
 
-template <int KIND, int NS>
-__global__ __launch_bounds__(NT, NW / 2) void s8_gemm_kernel(Group g) {
+template <int KIND, int BM>
+__global__ __launch_bounds__(Cfg<BM>::NT, 2) __attribute__((amdgpu_waves_per_eu(1, 2))) void s8_gemm_kernel(Group g) {
   constexpr bool ATR = KIND == LGX_S8_DW, BTR = KIND != LGX_S8_FWD;
-  using OA = Op<ATR>;
-  using OB = Op<BTR>;
+  constexpr int NW = Cfg<BM>::NW, NT = Cfg<BM>::NT, NS = Cfg<BM>::NS;
+  using OA = Op<ATR, BM, NW>;
+  using OB = Op<BTR, BN, NW>;
   constexpr int STAGE = OA::IMG + OB::IMG;
   extern __shared__ __align__(16) char lds[];
 
@@ -224,13 +230,13 @@ __global__ __launch_bounds__(NT, NW / 2) void s8_gemm_kernel(Group g) {
   const int l = x * (g.start[pi + 1] - g.start[pi]) + (jb - g.start[pi]);
   if (l >= P.tiles) return;
   const int tn = l % P.tiles_n, tm = (l / P.tiles_n) % P.tiles_m, z = l / (P.tiles_n * P.tiles_m);
-  const int m0 = tm * BT, n0 = tn * BT;
+  const int m0 = tm * BM, n0 = tn * BN;
   const int kbeg = z * P.kchunk;
   const int kend = std::min(P.K, kbeg + P.kchunk);
   const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = (wave & 1) * 64, wn = (wave >> 1) * WN;
+  const int wm = (wave % Cfg<BM>::WR) * 64, wn = (wave / Cfg<BM>::WR) * 64;
 
   uint32_t offA[OA::PW], offB[OB::PW];
   // ROW operands: source rows = tile rows (M or N); TR operands: source rows = k
@@ -261,6 +267,10 @@ __global__ __launch_bounds__(NT, NW / 2) void s8_gemm_kernel(Group g) {
       for (int j = 0; j < NJ; ++j) OB::frag(st + OA::IMG, wn + 16 * j, kk, lane, bh[j], bl[j]);
 #pragma unroll
       for (int i = 0; i < 4; ++i) OA::frag(st, wm + 16 * i, kk, lane, ah[i], al[i]);
+      // every fragment read is issued before the first MFMA (the scheduler would otherwise
+      // re-load A fragments one at a time behind lgkmcnt(0), exposing the LDS latency 8 times
+      // per step); the MFMAs then wait on counted lgkmcnt in issue order
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -315,7 +325,7 @@ __global__ __launch_bounds__(NT, NW / 2) void s8_gemm_kernel(Group g) {
     const int64_t ldd = part ? P.N : P.ldc32;
     const bool accum = !part && (P.epi & LGX_S8_EPI_ACCUM);
 #pragma unroll
-    for (int it = 0; it < BT * BT / 4 / NT; ++it) {
+    for (int it = 0; it < BM * BN / 4 / NT; ++it) {
       const int idx = tid + it * NT;
       const int row = idx >> 5, c = (idx & 31) * 4;
       const int m = m0 + row, n = n0 + c;
@@ -339,14 +349,20 @@ __global__ __launch_bounds__(NT, NW / 2) void s8_gemm_kernel(Group g) {
   constexpr int RS = NT / 16;  // row slots
   const int gq = tid & 15, r0 = tid >> 4;
   const int n = n0 + 8 * gq;
-  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  constexpr int NH = BM / LGX_S8_TILE_M;  // column-sum partials per tile (one per 128 rows)
+  float cs[NH][8];
+#pragma unroll
+  for (int h = 0; h < NH; ++h)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) cs[h][e] = 0.f;
   float bias[8];
   if constexpr (KIND == LGX_S8_FWD) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) bias[e] = (P.epi & LGX_S8_EPI_BIAS) && n + e < P.N ? P.bias[n + e] : 0.f;
   }
-#pragma unroll 2
-  for (int it = 0; it < BT / RS; ++it) {
+#pragma unroll
+  for (int it = 0; it < BM / RS; ++it) {
+    const int h = RS * it / LGX_S8_TILE_M;  // compile-time: r0 < RS and RS divides 128
     const int row = r0 + RS * it, m = m0 + row;
     if (m >= P.M || n >= P.N) continue;
     const f32x4 t0 = *reinterpret_cast<const f32x4*>(img + row * CP + 8 * gq);
@@ -382,24 +398,29 @@ __global__ __launch_bounds__(NT, NW / 2) void s8_gemm_kernel(Group g) {
         if (n + e < P.N) d[e] = v[e];
     }
 #pragma unroll
-    for (int e = 0; e < 8; ++e) cs[e] += v[e];
+    for (int e = 0; e < 8; ++e) cs[h][e] += v[e];
   }
-  if (P.colsum_ws != nullptr) {  // column sums of this 128-row tile, fixed order
+  if (P.colsum_ws != nullptr) {  // column sums of each 128-row span of the tile, fixed order
     __syncthreads();
-    float* red = img;  // [RS row slots][128 columns]
+    float* red = img;  // [NH][RS row slots][128 columns]
 #pragma unroll
-    for (int e = 0; e < 8; ++e) red[r0 * BT + 8 * gq + e] = cs[e];
+    for (int h = 0; h < NH; ++h)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) red[(h * RS + r0) * BN + 8 * gq + e] = cs[h][e];
     __syncthreads();
-    if (tid < BT && n0 + tid < P.N) {
+    const int h = tid / BN, c = tid % BN;
+    if (tid < NH * BN && n0 + c < P.N && m0 + h * LGX_S8_TILE_M < P.M) {
       float s = 0.f;
 #pragma unroll
-      for (int q = 0; q < RS; ++q) s += red[q * BT + tid];
-      P.colsum_ws[(int64_t)tm * P.N + n0 + tid] = s;
+      for (int q = 0; q < RS; ++q) s += red[(h * RS + q) * BN + c];
+      P.colsum_ws[(int64_t)(tm * NH + h) * P.N + n0 + c] = s;
     }
   }
 }
 
 // ---------------------------------------------------------------- fp32 -> S8 (+ column sums)
+#define LGX_S8_SPLIT_WIDE 1024  // (row, 8-column group) items per block of a wide split job
+
 struct SplitJob {
   const float* src; int64_t ld_src;
   char* dst; int64_t ld_dst;  // bytes
@@ -414,8 +435,9 @@ struct SplitBatch {
 };
 static_assert(sizeof(SplitBatch) <= 4096, "kernel argument segment");
 
-// block = 256 rows of one job; thread = one 8-column group. Narrow jobs (<= 8 groups, the only
-// ones with column sums): thread t owns group t & 7 of rows (t >> 3) + 32 it (fixed order).
+// Narrow jobs (<= 8 groups, the only ones with column sums): block = 256 rows, thread t owns
+// group t & 7 of rows (t >> 3) + 32 it (fixed order). Wide jobs: block = SPLIT_WIDE (row, group)
+// items, so a few-row job (a weight matrix) still spreads over many blocks.
 __global__ __launch_bounds__(256) void s8_split_kernel(SplitBatch b) {
   int ji = 0;
   while (ji + 1 < b.n && (int)blockIdx.x >= b.j[ji + 1].blk0) ++ji;
@@ -460,8 +482,12 @@ __global__ __launch_bounds__(256) void s8_split_kernel(SplitBatch b) {
     }
     return;
   }
-  for (int idx = tid; idx < LGX_S8_SPLIT_ROWS * G; idx += 256) {
-    const int r = rbase + idx / G, gg = idx % G;
+  // wide jobs: block = SPLIT_WIDE consecutive (row, group) items, row-major
+  const int64_t i0 = (int64_t)blk * LGX_S8_SPLIT_WIDE;
+#pragma unroll
+  for (int k = 0; k < LGX_S8_SPLIT_WIDE / 256; ++k) {
+    const int64_t i = i0 + tid + 256 * k;
+    const int r = (int)(i / G), gg = (int)(i - (int64_t)r * G);
     if (r >= J.rows) break;
     float v[8];
     one(r, gg, v);
@@ -484,8 +510,18 @@ __global__ __launch_bounds__(256) void s8_reduce_kernel(ReduceBatch b) {
   const int64_t e = i - b.start[ji];
   const int64_t r = e / J.cols, c = e - r * J.cols;
   const float* w = J.ws + r * J.ld_ws + c;
+  // partials summed in split order; loaded 16 at a time so the bias jobs' long (one partial per
+  // 128-row tile) sums are not a chain of dependent memory latencies
   float s = 0.f;
-  for (int q = 0; q < J.nsplit; ++q) s += w[q * J.stride];
+  int q = 0;
+  for (; q + 16 <= J.nsplit; q += 16) {
+    float v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) v[u] = w[(int64_t)(q + u) * J.stride];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) s += v[u];
+  }
+  for (; q < J.nsplit; ++q) s += w[(int64_t)q * J.stride];
   float* o = J.out + r * J.ld_out + c;
   *o = J.accumulate ? *o + s : s;
 }
@@ -508,20 +544,23 @@ static int launched(const char* what) {
 }
 static int cdiv(int a, int b) { return (a + b - 1) / b; }
 
-template <int KIND>
+template <int KIND, int BM>
 static void launch_gemm(const lgxs::Group& g, hipStream_t s) {
-  constexpr int NS = LGX_S8_NS;
-  constexpr int stage = 2 * lgxs::BT * lgxs::BK * 4;
-  constexpr int epi = lgxs::BT * lgxs::CP * 4;
-  constexpr int bytes = NS * stage > epi ? NS * stage : epi;
+  using C = lgxs::Cfg<BM>;
+  constexpr int stage = (BM + lgxs::BN) * lgxs::BK * 4;
+  constexpr int epi = BM * lgxs::CP * 4;
+  constexpr int bytes = C::NS * stage > epi ? C::NS * stage : epi;
+  static_assert(bytes <= 160 * 1024, "LDS");
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)lgxs::s8_gemm_kernel<KIND, NS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)lgxs::s8_gemm_kernel<KIND, BM>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               bytes);
     attr = true;
   }
-  hipLaunchKernelGGL((lgxs::s8_gemm_kernel<KIND, NS>), dim3(8 * g.per_xcd), dim3(lgxs::NT), bytes, s, g);
+  hipLaunchKernelGGL((lgxs::s8_gemm_kernel<KIND, BM>), dim3(8 * g.per_xcd), dim3(C::NT), bytes, s, g);
 }
+// the row extent of the output tile each kind runs on
+static int tile_m(int kind) { return (LGX_S8_BIG >> kind) & 1 ? 256 : 128; }
 
 extern "C" {
 
@@ -534,12 +573,13 @@ int32_t lgx_s8_pick_split(const int32_t* M, const int32_t* N, const int32_t* K, 
   // one K chunk for every problem: the smallest that keeps the group within one residency
   // round of 2 blocks per CU (256 CUs)
   int64_t tiles = 0, kmax = 0;
+  const int bm = tile_m(LGX_S8_DW), slots = bm == 128 ? 512 : 256;
   for (int i = 0; i < n; ++i) {
     if (M[i] <= 0 || N[i] <= 0 || K[i] < 0) return fail("lgx_s8_pick_split: bad shape");
-    tiles += (int64_t)cdiv(M[i], lgxs::BT) * cdiv(N[i], lgxs::BT);
+    tiles += (int64_t)cdiv(M[i], bm) * cdiv(N[i], lgxs::BN);
     kmax = std::max<int64_t>(kmax, K[i]);
   }
-  const int64_t s = std::max<int64_t>(1, tiles ? 512 / tiles : 1);
+  const int64_t s = std::max<int64_t>(1, tiles ? slots / tiles : 1);
   const int64_t chunk = ((kmax + s - 1) / s + lgxs::BK - 1) / lgxs::BK * lgxs::BK;
   for (int i = 0; i < n; ++i) out[i] = std::max(1, cdiv(K[i], (int)std::max<int64_t>(chunk, lgxs::BK)));
   return 0;
@@ -551,6 +591,7 @@ int32_t lgx_s8_gemm_group(const lgx_s8_gemm_args* a, int32_t n, int32_t kind, vo
   lgxs::Group g;
   memset(&g, 0, sizeof g);
   int np = 0, acc = 0;
+  const int bm = tile_m(kind);
   g.start[0] = 0;
   for (int i = 0; i < n; ++i) {
     const lgx_s8_gemm_args& q = a[i];
@@ -576,8 +617,8 @@ int32_t lgx_s8_gemm_group(const lgx_s8_gemm_args* a, int32_t n, int32_t kind, vo
     p.M = q.M;
     p.N = q.N;
     p.K = q.K;
-    p.tiles_m = cdiv(q.M, lgxs::BT);
-    p.tiles_n = cdiv(q.N, lgxs::BT);
+    p.tiles_m = cdiv(q.M, bm);
+    p.tiles_n = cdiv(q.N, lgxs::BN);
     p.epi = q.epilogue;
     p.C = (char*)q.C;
     p.ldc = q.ldc * 4;
@@ -615,9 +656,15 @@ int32_t lgx_s8_gemm_group(const lgx_s8_gemm_args* a, int32_t n, int32_t kind, vo
   g.per_xcd = acc;
   if (np == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
-  if (kind == LGX_S8_FWD) launch_gemm<LGX_S8_FWD>(g, s);
-  else if (kind == LGX_S8_DX) launch_gemm<LGX_S8_DX>(g, s);
-  else launch_gemm<LGX_S8_DW>(g, s);
+  if (bm == 128) {
+    if (kind == LGX_S8_FWD) launch_gemm<LGX_S8_FWD, 128>(g, s);
+    else if (kind == LGX_S8_DX) launch_gemm<LGX_S8_DX, 128>(g, s);
+    else launch_gemm<LGX_S8_DW, 128>(g, s);
+  } else {
+    if (kind == LGX_S8_FWD) launch_gemm<LGX_S8_FWD, 256>(g, s);
+    else if (kind == LGX_S8_DX) launch_gemm<LGX_S8_DX, 256>(g, s);
+    else launch_gemm<LGX_S8_DW, 256>(g, s);
+  }
   return launched("lgx_s8_gemm_group");
 }
 
@@ -635,7 +682,8 @@ int32_t lgx_s8_split(const lgx_s8_split_args* a, int32_t n, void* stream) {
       return fail("lgx_s8_split: S8 destination alignment / pitch");
     if (q.colsum_ws && q.cols > 64) return fail("lgx_s8_split: column sums for <= 64 columns only");
     b.j[k] = lgxs::SplitJob{q.src, q.ld_src, (char*)q.dst, q.ld_dst * 4, q.rows, q.cols, q.colsum_ws, q.idx, blocks};
-    blocks += cdiv(q.rows, LGX_S8_SPLIT_ROWS);
+    const int64_t G = cdiv(q.cols, 8);
+    blocks += G <= 8 ? cdiv(q.rows, LGX_S8_SPLIT_ROWS) : (int)((q.rows * G + LGX_S8_SPLIT_WIDE - 1) / LGX_S8_SPLIT_WIDE);
     ++k;
   }
   b.n = k;

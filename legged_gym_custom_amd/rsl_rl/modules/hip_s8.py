@@ -154,11 +154,11 @@ def gemm_group(args, kind, L=None):
         _check(L.lgx_s8_gemm_group(arr, len(chunk), kind, _stream()), "lgx_s8_gemm_group")
 
 
-def pick_split(shapes):
+def pick_split(shapes, L=None):
     n = len(shapes)
     Iv = C.c_int32 * n
     Ms, Ns, Ks, out = Iv(*[s[0] for s in shapes]), Iv(*[s[1] for s in shapes]), Iv(*[s[2] for s in shapes]), Iv()
-    _check(lib().lgx_s8_pick_split(Ms, Ns, Ks, n, out), "lgx_s8_pick_split")
+    _check((L or lib()).lgx_s8_pick_split(Ms, Ns, Ks, n, out), "lgx_s8_pick_split")
     return list(out)
 
 

@@ -1,4 +1,6 @@
-"""Mean PMC counter values per kernel over rocprofv3 --pmc passes (dev tool): python pmc_summary.py <dir>."""
+"""Mean PMC counter values per kernel over rocprofv3 --pmc passes (dev tool):
+python pmc_summary.py <dir> [--by-grid]  (--by-grid: one entry per kernel and grid size, i.e. per
+launch shape)."""
 import collections
 import csv
 import glob
@@ -7,7 +9,10 @@ import sys
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in sorted(glob.glob(sys.argv[1] + "/p*/*/*_counter_collection.csv")):
     for r in csv.DictReader(open(f)):
-        agg[r["Kernel_Name"].split("(")[0][-48:]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        key = r["Kernel_Name"].split("(")[0][-48:]
+        if "--by-grid" in sys.argv:
+            key += f" grid={r.get('Grid_Size', '?')}"
+        agg[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, d in agg.items():
     if "lgx" not in k and "env_step" not in k:
         continue

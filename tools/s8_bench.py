@@ -95,6 +95,18 @@ def main():
                          ldb=Xs[(c, i)].shape[1], M=fo, N=fi, K=R, C32=w.data_ptr(), ldc32=fi, split=8)
               for (c, i, fi, fo), w in zip(layers, ws8)]
     out["dw_group_split8_us"] = timeit_many({k: (lambda L=L: S.gemm_group(dargs8, S.DW, L)) for k, L in libs.items()})
+    own = {}  # each variant at the split its own lgx_s8_pick_split chooses
+    for k, L in libs.items():
+        sp = S.pick_split(shapes, L)
+        wk = [torch.empty(q, fo, fi, device=dev) for q, (fo, fi, _r) in zip(sp, shapes)]
+        ak = [S.GemmArgs(A=DYs[(c, i)].data_ptr(), lda=DYs[(c, i)].shape[1], B=Xs[(c, i)].data_ptr(),
+                         ldb=Xs[(c, i)].shape[1], M=fo, N=fi, K=R, C32=w.data_ptr(), ldc32=fi, split=q)
+              for (c, i, fi, fo), w, q in zip(layers, wk, sp)]
+        rk = [S.flat_reduce(w.data_ptr(), fo * fi, d.data_ptr(), fo * fi, q)
+              for w, d, q, (fo, fi, _r) in zip(wk, dW, sp, shapes)]
+        own[k] = (lambda L=L, ak=ak, rk=rk, wk=wk: (S.gemm_group(ak, S.DW, L), S.reduce(rk, L)))
+        out[f"s8_splits_{k}"] = sp
+    out["dw_group_plus_reduce_own_split_us"] = timeit_many(own)
     ref_ws = None
     for k, L in libs.items():  # every variant computes the same partials (same MFMA order)
         for w in ws:
