@@ -42,8 +42,8 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 #ifndef LGX_S8_BK
 #define LGX_S8_BK 32
 #endif
-#ifndef LGX_S8_BIG
-#define LGX_S8_BIG 0  // bit (1 << kind): that kind runs on the 256-row tile configuration
+#ifndef LGX_S8_WIDE
+#define LGX_S8_WIDE 0  // bit (1 << kind): that kind's problems with M, N >= 256 run on the 256 x 256 kernel
 #endif
 
 namespace lgxs {
@@ -51,13 +51,21 @@ namespace lgxs {
 constexpr int BK = LGX_S8_BK, BN = 128, NJ = 4, GMAX = LGX_S8_GROUP_MAX;
 static_assert(BK == 32 || BK == 64, "K step 32 or 64");
 constexpr int CP = BN + 4;  // fp32 epilogue image pitch (floats)
-// Tile configurations: output tile BM x 128, BM / 32 waves as (BM / 64) x 2, each wave 64 x 64
-// (4 x 4 MFMA tiles). BM 128: 4 waves, NS 2 stages, 2 blocks per CU. BM 256: 8 waves, NS 3
-// stages of 48 KB, 1 block per CU — two steps of DMA in flight per CU instead of one, and a
-// quarter fewer L2 bytes per MFMA.
-template <int BM_>
+// Two kernels. s8_gemm_kernel: output tile 128 x 128, 4 waves as 2 x 2 (each 64 x 64 = 4 x 4
+// MFMA tiles), 2 LDS stages of 32 KB, 2 blocks per CU. s8_gemm256_kernel: 256 x 256, 8 waves as
+// 2 x 4 (each 128 x 64), 2 stages of 64 KB, 1 block per CU, the two wave rows a barrier apart.
+// Measured and not kept: 256 x 128 and 128 x 128 tiles at 3-4 stages and 1
+// block per CU (a block's waves in lock step).
 struct Cfg {
-  static constexpr int BM = BM_, NW = BM_ / 32, NT = 64 * NW, WR = BM_ / 64, NS = BM_ == 128 ? 2 : 3;
+  static constexpr int BM = 128, NS = 2, NW = 4, NT = 256, WR = 2;
+  static constexpr int LDS_STAGES = NS * (BM + BN) * BK * 4, LDS_EPI = BM * CP * 4;
+  static constexpr int LDS = LDS_STAGES > LDS_EPI ? LDS_STAGES : LDS_EPI;
+};
+struct Cfg256 {
+  static constexpr int BM = 256, BNW = 256, NW = 8, NT = 512, CPW = BNW + 4;
+  static constexpr int LDS_STAGES = 2 * (BM + BNW) * BK * 4, LDS_EPI = 128 * CPW * 4;
+  static constexpr int LDS = LDS_STAGES > LDS_EPI ? LDS_STAGES : LDS_EPI;
+  static_assert(LDS <= 160 * 1024, "LDS");
 };
 
 // slot swizzles (16-B slot index XOR), image row -> mask
@@ -213,10 +221,118 @@ __device__ __forceinline__ void load_s8(const char* src, float (&v)[8]) {
   }
 }
 
-template <int KIND, int BM>
-__global__ __launch_bounds__(Cfg<BM>::NT, 2) __attribute__((amdgpu_waves_per_eu(1, 2))) void s8_gemm_kernel(Group g) {
+// ---- epilogues over an fp32 LDS image [ROWS][CPI] of output rows m_base.., columns n_base..
+// DW: fp32 rows (float4): split partial slab z, or the output itself (split 1, optional accumulate)
+template <int NT, int ROWS, int COLS, int CPI>
+__device__ __forceinline__ void epi_dw(const Prob& P, const float* img, int m_base, int n_base, int z, int tid) {
+  const bool part = P.tiles > P.tiles_m * P.tiles_n;
+  float* dst = part ? P.C32 + (int64_t)z * P.M * P.N : P.C32;
+  const int64_t ldd = part ? P.N : P.ldc32;
+  const bool accum = !part && (P.epi & LGX_S8_EPI_ACCUM);
+  constexpr int Q = COLS / 4;  // float4 per row
+#pragma unroll
+  for (int it = 0; it < ROWS * Q / NT; ++it) {
+    const int idx = tid + it * NT;
+    const int row = idx / Q, c = (idx % Q) * 4;
+    const int m = m_base + row, n = n_base + c;
+    if (m >= P.M || n >= P.N) continue;
+    const f32x4 t = *reinterpret_cast<const f32x4*>(img + row * CPI + c);
+    float* d = dst + (int64_t)m * ldd + n;
+    if (n + 4 <= P.N) {
+      f32x4u o = {t[0], t[1], t[2], t[3]};
+      if (accum) o += *reinterpret_cast<const f32x4u*>(d);
+      *reinterpret_cast<f32x4u*>(d) = o;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (n + e < P.N) d[e] = accum ? d[e] + t[e] : t[e];
+    }
+  }
+}
+
+// FWD / DX: thread = one 8-column group (gq) of rows r0 + RS it; FWD bias + ELU, DX ELU'(y_prev)
+// (+ addend); S8 and/or fp32 out; the column sums of each 128-row span (partial part0 + h), in a
+// fixed order (the same order for every tile configuration: RS = 16 row slots)
+template <int KIND, int NT, int ROWS, int COLS, int CPI>
+__device__ __forceinline__ void epi_act(const Prob& P, float* img, int m_base, int n_base, int part0, int tid) {
+  constexpr int G = COLS / 8, RS = NT / G, NH = ROWS / LGX_S8_TILE_M;
+  static_assert(RS == 16 && ROWS % LGX_S8_TILE_M == 0, "epilogue row slots");
+  const int gq = tid % G, r0 = tid / G;
+  const int n = n_base + 8 * gq;
+  float cs[NH][8];
+#pragma unroll
+  for (int h = 0; h < NH; ++h)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) cs[h][e] = 0.f;
+  float bias[8];
+  if constexpr (KIND == LGX_S8_FWD) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bias[e] = (P.epi & LGX_S8_EPI_BIAS) && n + e < P.N ? P.bias[n + e] : 0.f;
+  }
+#pragma unroll
+  for (int it = 0; it < ROWS / RS; ++it) {
+    const int h = RS * it / LGX_S8_TILE_M;  // compile-time: r0 < RS and RS divides 128
+    const int row = r0 + RS * it, m = m_base + row;
+    if (m >= P.M || n >= P.N) continue;
+    const f32x4 t0 = *reinterpret_cast<const f32x4*>(img + row * CPI + 8 * gq);
+    const f32x4 t1 = *reinterpret_cast<const f32x4*>(img + row * CPI + 8 * gq + 4);
+    float v[8] = {t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
+    if constexpr (KIND == LGX_S8_FWD) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += bias[e];
+      if (P.epi & LGX_S8_EPI_ELU) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = elu(v[e]);
+      }
+    } else {
+      if (P.epi & LGX_S8_EPI_DELU) {
+        float y[8];
+        load_s8(P.act + (int64_t)m * P.ld_act + (n >> 3) * 32, y);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] *= y[e] > 0.f ? 1.f : y[e] + 1.f;
+      }
+      if (P.addend != nullptr) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (n + e < P.add_cols) v[e] += P.addend[(int64_t)m * P.ld_add + n + e];
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = n + e < P.N ? v[e] : 0.f;  // zero pad columns
+    if (P.C != nullptr) store_s8(P.C + (int64_t)m * P.ldc + (n >> 3) * 32, v);
+    if (P.C32 != nullptr) {
+      float* d = P.C32 + (int64_t)m * P.ldc32 + n;
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (n + e < P.N) d[e] = v[e];
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) cs[h][e] += v[e];
+  }
+  if (P.colsum_ws != nullptr) {
+    __syncthreads();
+    float* red = img;  // [NH][RS row slots][COLS]
+#pragma unroll
+    for (int h = 0; h < NH; ++h)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) red[(h * RS + r0) * COLS + 8 * gq + e] = cs[h][e];
+    __syncthreads();
+    for (int t = tid; t < NH * COLS; t += NT) {
+      const int h = t / COLS, c = t % COLS;
+      if (n_base + c < P.N && m_base + h * LGX_S8_TILE_M < P.M) {
+        float s = 0.f;
+#pragma unroll
+        for (int q = 0; q < RS; ++q) s += red[(h * RS + q) * COLS + c];
+        P.colsum_ws[(int64_t)(part0 + h) * P.N + n_base + c] = s;
+      }
+    }
+  }
+}
+
+template <int KIND>
+__global__ __launch_bounds__(Cfg::NT, 2) __attribute__((amdgpu_waves_per_eu(1, 2))) void s8_gemm_kernel(Group g) {
   constexpr bool ATR = KIND == LGX_S8_DW, BTR = KIND != LGX_S8_FWD;
-  constexpr int NW = Cfg<BM>::NW, NT = Cfg<BM>::NT, NS = Cfg<BM>::NS;
+  constexpr int BM = Cfg::BM, NW = Cfg::NW, NT = Cfg::NT, NS = Cfg::NS;
   using OA = Op<ATR, BM, NW>;
   using OB = Op<BTR, BN, NW>;
   constexpr int STAGE = OA::IMG + OB::IMG;
@@ -236,7 +352,7 @@ __global__ __launch_bounds__(Cfg<BM>::NT, 2) __attribute__((amdgpu_waves_per_eu(
   const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = (wave % Cfg<BM>::WR) * 64, wn = (wave / Cfg<BM>::WR) * 64;
+  const int wm = (wave % Cfg::WR) * 64, wn = (wave / Cfg::WR) * 64;
 
   uint32_t offA[OA::PW], offB[OB::PW];
   // ROW operands: source rows = tile rows (M or N); TR operands: source rows = k
@@ -317,104 +433,136 @@ __global__ __launch_bounds__(Cfg<BM>::NT, 2) __attribute__((amdgpu_waves_per_eu(
         for (int r = 0; r < 4; ++r) img[(wm + 16 * i + er + r) * CP + wn + 16 * j + ec] = acc[i][j][r];
   }
   __syncthreads();
+  if constexpr (KIND == LGX_S8_DW)
+    epi_dw<NT, BM, BN, CP>(P, img, m0, n0, z, tid);
+  else
+    epi_act<KIND, NT, BM, BN, CP>(P, img, m0, n0, tm * (BM / LGX_S8_TILE_M), tid);
+}
 
-  if constexpr (KIND == LGX_S8_DW) {
-    // fp32 rows (float4): split partial slab z, or the output itself (split 1, optional accumulate)
-    const bool part = P.tiles > P.tiles_m * P.tiles_n;
-    float* dst = part ? P.C32 + (int64_t)z * P.M * P.N : P.C32;
-    const int64_t ldd = part ? P.N : P.ldc32;
-    const bool accum = !part && (P.epi & LGX_S8_EPI_ACCUM);
-#pragma unroll
-    for (int it = 0; it < BM * BN / 4 / NT; ++it) {
-      const int idx = tid + it * NT;
-      const int row = idx >> 5, c = (idx & 31) * 4;
-      const int m = m0 + row, n = n0 + c;
-      if (m >= P.M || n >= P.N) continue;
-      const f32x4 t = *reinterpret_cast<const f32x4*>(img + row * CP + c);
-      float* d = dst + (int64_t)m * ldd + n;
-      if (n + 4 <= P.N) {
-        f32x4u o = {t[0], t[1], t[2], t[3]};
-        if (accum) o += *reinterpret_cast<const f32x4u*>(d);
-        *reinterpret_cast<f32x4u*>(d) = o;
-      } else {
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (n + e < P.N) d[e] = accum ? d[e] + t[e] : t[e];
-      }
-    }
-    return;
-  }
+// ---- 256 x 256 tile: 8 waves, wave (wr, wc) = (wave >> 2, wave & 3) owns rows 128 wr .. + 127,
+// columns 64 wc .. + 63 (8 x 4 MFMA tiles). Each 32-deep K step is 4 phases; a phase is a read
+// section R (this phase's fragments; phase 0 also the B fragments; phases 0 / 1 issue the next
+// step's LDS-DMA, A then B) and an MFMA section M (2 x 4 tiles x 3 products), each closed by a
+// raw s_barrier. The wave row wr = 1 runs one barrier behind wr = 0 (one extra barrier before
+// the loop, matched by one after it), so on every SIMD one wave's MFMAs overlap the other's
+// reads (cdna_hip_programming.md §5, the 256^2 8-phase template). Ordering (barrier counting,
+// one barrier of lag between the rows): every R ends with lgkmcnt(0), so a barrier retires the
+// reads before it (WAR: the next step's DMA overwrites the stage read one step earlier, issued
+// only after both rows passed their last read of it); phase 3's R waits vmcnt(0), two barriers
+// before the other row's first read of that stage (RAW).
+template <int KIND>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) void s8_gemm256_kernel(Group g) {
+  constexpr bool ATR = KIND == LGX_S8_DW, BTR = KIND != LGX_S8_FWD;
+  constexpr int T = 256, NW = 8, NT = 512, CPW = Cfg256::CPW;
+  using OA = Op<ATR, T, NW>;
+  using OB = Op<BTR, T, NW>;
+  constexpr int STAGE = OA::IMG + OB::IMG;
+  extern __shared__ __align__(16) char lds[];
 
-  // FWD / DX: thread = one 8-column group (g = tid & 15) of rows (tid >> 4) + RS it
-  constexpr int RS = NT / 16;  // row slots
-  const int gq = tid & 15, r0 = tid >> 4;
-  const int n = n0 + 8 * gq;
-  constexpr int NH = BM / LGX_S8_TILE_M;  // column-sum partials per tile (one per 128 rows)
-  float cs[NH][8];
+  const int x = blockIdx.x & 7, jb = blockIdx.x >> 3;
+  if (jb >= g.per_xcd) return;
+  int pi = 0;
+  while (pi + 1 < g.n && jb >= g.start[pi + 1]) ++pi;
+  const Prob P = g.p[pi];
+  const int l = x * (g.start[pi + 1] - g.start[pi]) + (jb - g.start[pi]);
+  if (l >= P.tiles) return;
+  const int tn = l % P.tiles_n, tm = (l / P.tiles_n) % P.tiles_m, z = l / (P.tiles_n * P.tiles_m);
+  const int m0 = tm * T, n0 = tn * T;
+  const int kbeg = z * P.kchunk;
+  const int kend = std::min(P.K, kbeg + P.kchunk);
+  const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+  const int wm = wr * 128, wn = wc * 64;
+  // a sub-tile entirely past M or N reads and multiplies nothing (wave-uniform)
+  const bool live = m0 + wm < P.M && n0 + wn < P.N;
+
+  uint32_t offA[OA::PW], offB[OB::PW];
+  OA::offsets(offA, wave, lane, m0, P.M, P.lda, kbeg);
+  OB::offsets(offB, wave, lane, n0, P.N, P.ldb, kbeg);
+  const int64_t sa = OA::step_bytes(P.lda), sb = OB::step_bytes(P.ldb);
+  const uint32_t lds0 = (uint32_t)(uintptr_t)((LDS_AS char*)lds);
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+
+  f32x4 acc[8][4];
 #pragma unroll
-  for (int h = 0; h < NH; ++h)
+  for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int e = 0; e < 8; ++e) cs[h][e] = 0.f;
-  float bias[8];
-  if constexpr (KIND == LGX_S8_FWD) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) bias[e] = (P.epi & LGX_S8_EPI_BIAS) && n + e < P.N ? P.bias[n + e] : 0.f;
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 bh[4], bl[4], ah[2], al[2];
+
+  if (nk > 0) {
+    OA::issue(P.A, offA, lds0, wv);
+    OB::issue(P.B, offB, lds0 + OA::IMG, wv);
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  asm volatile("s_barrier" ::: "memory");
+  if (wr == 1) asm volatile("s_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+
+  for (int k = 0; k < nk; ++k) {
+    const char* st = lds + (k & 1) * STAGE;
+    const uint32_t nst = lds0 + (uint32_t)(((k + 1) & 1) * STAGE);
+    const bool next = k + 1 < nk;
 #pragma unroll
-  for (int it = 0; it < BM / RS; ++it) {
-    const int h = RS * it / LGX_S8_TILE_M;  // compile-time: r0 < RS and RS divides 128
-    const int row = r0 + RS * it, m = m0 + row;
-    if (m >= P.M || n >= P.N) continue;
-    const f32x4 t0 = *reinterpret_cast<const f32x4*>(img + row * CP + 8 * gq);
-    const f32x4 t1 = *reinterpret_cast<const f32x4*>(img + row * CP + 8 * gq + 4);
-    float v[8] = {t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
-    if constexpr (KIND == LGX_S8_FWD) {
+    for (int ph = 0; ph < 4; ++ph) {
+      // R
+      if (live) {
+        if (ph == 0) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] += bias[e];
-      if (P.epi & LGX_S8_EPI_ELU) {
+          for (int j = 0; j < 4; ++j) OB::frag(st + OA::IMG, wn + 16 * j, 0, lane, bh[j], bl[j]);
+        }
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = elu(v[e]);
+        for (int i = 0; i < 2; ++i) OA::frag(st, wm + 32 * ph + 16 * i, 0, lane, ah[i], al[i]);
       }
-    } else {
-      if (P.epi & LGX_S8_EPI_DELU) {
-        float y[8];
-        load_s8(P.act + (int64_t)m * P.ld_act + (n >> 3) * 32, y);
+      if (ph == 0 && next) OA::issue(P.A + (k + 1) * sa, offA, nst, wv);
+      if (ph == 1 && next) OB::issue(P.B + (k + 1) * sb, offB, nst + OA::IMG, wv);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (ph == 3) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_barrier" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      // M
+      if (live) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] *= y[e] > 0.f ? 1.f : y[e] + 1.f;
-      }
-      if (P.addend != nullptr) {
+        for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int e = 0; e < 8; ++e)
-          if (n + e < P.add_cols) v[e] += P.addend[(int64_t)m * P.ld_add + n + e];
+          for (int j = 0; j < 4; ++j) {
+            f32x4& c = acc[2 * ph + i][j];
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh[j], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl[j], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh[j], c, 0, 0, 0);
+          }
       }
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_barrier" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
     }
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = n + e < P.N ? v[e] : 0.f;  // zero pad columns
-    if (P.C != nullptr) store_s8(P.C + (int64_t)m * P.ldc + (n >> 3) * 32, v);
-    if (P.C32 != nullptr) {
-      float* d = P.C32 + (int64_t)m * P.ldc32 + n;
-#pragma unroll
-      for (int e = 0; e < 8; ++e)
-        if (n + e < P.N) d[e] = v[e];
-    }
-#pragma unroll
-    for (int e = 0; e < 8; ++e) cs[h][e] += v[e];
   }
-  if (P.colsum_ws != nullptr) {  // column sums of each 128-row span of the tile, fixed order
-    __syncthreads();
-    float* red = img;  // [NH][RS row slots][128 columns]
+  if (wr == 0) asm volatile("s_barrier" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // ---- epilogue, one wave row (128 x 256) at a time through the LDS image [128][CPW]
+  float* img = reinterpret_cast<float*>(lds);
+  const int ec = lane & 15, er = (lane >> 4) * 4;
 #pragma unroll
-    for (int h = 0; h < NH; ++h)
+  for (int h = 0; h < 2; ++h) {
+    if (wr == h) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) red[(h * RS + r0) * BN + 8 * gq + e] = cs[h][e];
-    __syncthreads();
-    const int h = tid / BN, c = tid % BN;
-    if (tid < NH * BN && n0 + c < P.N && m0 + h * LGX_S8_TILE_M < P.M) {
-      float s = 0.f;
+      for (int i = 0; i < 8; ++i)
 #pragma unroll
-      for (int q = 0; q < RS; ++q) s += red[(h * RS + q) * BN + c];
-      P.colsum_ws[(int64_t)(tm * NH + h) * P.N + n0 + c] = s;
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) img[(16 * i + er + r) * CPW + wn + 16 * j + ec] = acc[i][j][r];
     }
+    __syncthreads();
+    if constexpr (KIND == LGX_S8_DW)
+      epi_dw<NT, 128, T, CPW>(P, img, m0 + 128 * h, n0, z, tid);
+    else
+      epi_act<KIND, NT, 128, T, CPW>(P, img, m0 + 128 * h, n0, tm * 2 + h, tid);
+    __syncthreads();
   }
 }
 
@@ -446,7 +594,7 @@ __global__ __launch_bounds__(256) void s8_split_kernel(SplitBatch b) {
   const int rbase = blk * LGX_S8_SPLIT_ROWS;
   const int G = (J.cols + 7) / 8;
   const int tid = threadIdx.x;
-  auto one = [&](int r, int gg, float (&v)[8]) {
+  auto load8 = [&](int r, int gg, float (&v)[8]) {
     const int64_t sr = J.idx ? J.idx[r] : r;
     const float* s = J.src + sr * J.ld_src + 8 * gg;
     if (8 * gg + 8 <= J.cols) {
@@ -456,6 +604,9 @@ __global__ __launch_bounds__(256) void s8_split_kernel(SplitBatch b) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = 8 * gg + e < J.cols ? s[e] : 0.f;
     }
+  };
+  auto one = [&](int r, int gg, float (&v)[8]) {
+    load8(r, gg, v);
     store_s8(J.dst + (int64_t)r * J.ld_dst + gg * 32, v);
   };
   if (G <= 8) {
@@ -482,16 +633,22 @@ __global__ __launch_bounds__(256) void s8_split_kernel(SplitBatch b) {
     }
     return;
   }
-  // wide jobs: block = SPLIT_WIDE consecutive (row, group) items, row-major
+  // wide jobs: block = SPLIT_WIDE consecutive (row, group) items, row-major; a thread's items
+  // are all loaded before any is stored (src and dst may not alias; the loads overlap)
+  constexpr int IT = LGX_S8_SPLIT_WIDE / 256;
   const int64_t i0 = (int64_t)blk * LGX_S8_SPLIT_WIDE;
+  float v[IT][8];
+  int rr[IT], gs[IT];
 #pragma unroll
-  for (int k = 0; k < LGX_S8_SPLIT_WIDE / 256; ++k) {
+  for (int k = 0; k < IT; ++k) {
     const int64_t i = i0 + tid + 256 * k;
-    const int r = (int)(i / G), gg = (int)(i - (int64_t)r * G);
-    if (r >= J.rows) break;
-    float v[8];
-    one(r, gg, v);
+    rr[k] = (int)(i / G);
+    gs[k] = (int)(i - (int64_t)rr[k] * G);
+    if (rr[k] < J.rows) load8(rr[k], gs[k], v[k]);
   }
+#pragma unroll
+  for (int k = 0; k < IT; ++k)
+    if (rr[k] < J.rows) store_s8(J.dst + (int64_t)rr[k] * J.ld_dst + gs[k] * 32, v[k]);
 }
 
 struct ReduceBatch {
@@ -544,23 +701,22 @@ static int launched(const char* what) {
 }
 static int cdiv(int a, int b) { return (a + b - 1) / b; }
 
-template <int KIND, int BM>
+template <int KIND, bool WIDE>
 static void launch_gemm(const lgxs::Group& g, hipStream_t s) {
-  using C = lgxs::Cfg<BM>;
-  constexpr int stage = (BM + lgxs::BN) * lgxs::BK * 4;
-  constexpr int epi = BM * lgxs::CP * 4;
-  constexpr int bytes = C::NS * stage > epi ? C::NS * stage : epi;
-  static_assert(bytes <= 160 * 1024, "LDS");
+  constexpr int lds = WIDE ? lgxs::Cfg256::LDS : lgxs::Cfg::LDS;
+  const void* fn = WIDE ? (const void*)lgxs::s8_gemm256_kernel<KIND> : (const void*)lgxs::s8_gemm_kernel<KIND>;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)lgxs::s8_gemm_kernel<KIND, BM>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              bytes);
+    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr = true;
   }
-  hipLaunchKernelGGL((lgxs::s8_gemm_kernel<KIND, BM>), dim3(8 * g.per_xcd), dim3(C::NT), bytes, s, g);
+  if constexpr (WIDE)
+    hipLaunchKernelGGL((lgxs::s8_gemm256_kernel<KIND>), dim3(8 * g.per_xcd), dim3(lgxs::Cfg256::NT), lds, s, g);
+  else
+    hipLaunchKernelGGL((lgxs::s8_gemm_kernel<KIND>), dim3(8 * g.per_xcd), dim3(lgxs::Cfg::NT), lds, s, g);
 }
-// the row extent of the output tile each kind runs on
-static int tile_m(int kind) { return (LGX_S8_BIG >> kind) & 1 ? 256 : 128; }
+// problems of this kind with M, N >= 256 run on the 256 x 256 kernel
+static bool wide(int kind, int M, int N) { return ((LGX_S8_WIDE >> kind) & 1) && M >= 256 && N >= 256; }
 
 extern "C" {
 
@@ -570,29 +726,35 @@ const char* lgx_s8_last_error(void) { return g_err; }
 
 int32_t lgx_s8_pick_split(const int32_t* M, const int32_t* N, const int32_t* K, int32_t n, int32_t* out) {
   if (n < 0 || n > LGX_S8_GROUP_MAX) return fail("lgx_s8_pick_split: 0 <= n <= LGX_S8_GROUP_MAX");
-  // one K chunk for every problem: the smallest that keeps the group within one residency
-  // round of 2 blocks per CU (256 CUs)
-  int64_t tiles = 0, kmax = 0;
-  const int bm = tile_m(LGX_S8_DW), slots = bm == 128 ? 512 : 256;
-  for (int i = 0; i < n; ++i) {
+  for (int i = 0; i < n; ++i)
     if (M[i] <= 0 || N[i] <= 0 || K[i] < 0) return fail("lgx_s8_pick_split: bad shape");
-    tiles += (int64_t)cdiv(M[i], bm) * cdiv(N[i], lgxs::BN);
-    kmax = std::max<int64_t>(kmax, K[i]);
+  // per launch (the 256 x 256 problems, then the 128 x 128 ones: lgx_s8_gemm_group's split of
+  // the group) one K chunk for every problem: the smallest that keeps the launch within one
+  // residency round (256 CUs x 1 or 2 blocks)
+  for (int w = 0; w < 2; ++w) {
+    const int tile = w ? 256 : 128, slots = w ? 256 : 512;
+    int64_t tiles = 0, kmax = 0;
+    for (int i = 0; i < n; ++i) {
+      if (wide(LGX_S8_DW, M[i], N[i]) != (bool)w) continue;
+      tiles += (int64_t)cdiv(M[i], tile) * cdiv(N[i], tile);
+      kmax = std::max<int64_t>(kmax, K[i]);
+    }
+    const int64_t s = std::max<int64_t>(1, tiles ? slots / tiles : 1);
+    const int64_t chunk = ((kmax + s - 1) / s + lgxs::BK - 1) / lgxs::BK * lgxs::BK;
+    for (int i = 0; i < n; ++i)
+      if (wide(LGX_S8_DW, M[i], N[i]) == (bool)w)
+        out[i] = std::max(1, cdiv(K[i], (int)std::max<int64_t>(chunk, lgxs::BK)));
   }
-  const int64_t s = std::max<int64_t>(1, tiles ? slots / tiles : 1);
-  const int64_t chunk = ((kmax + s - 1) / s + lgxs::BK - 1) / lgxs::BK * lgxs::BK;
-  for (int i = 0; i < n; ++i) out[i] = std::max(1, cdiv(K[i], (int)std::max<int64_t>(chunk, lgxs::BK)));
   return 0;
 }
 
 int32_t lgx_s8_gemm_group(const lgx_s8_gemm_args* a, int32_t n, int32_t kind, void* stream) {
   if (n < 0 || n > LGX_S8_GROUP_MAX) return fail("lgx_s8_gemm_group: 0 <= n <= LGX_S8_GROUP_MAX");
   if (kind < LGX_S8_FWD || kind > LGX_S8_DW) return fail("lgx_s8_gemm_group: unknown kind");
-  lgxs::Group g;
-  memset(&g, 0, sizeof g);
-  int np = 0, acc = 0;
-  const int bm = tile_m(kind);
-  g.start[0] = 0;
+  // two launches at most: the problems on the 256 x 256 kernel (gw), the rest (g)
+  lgxs::Group gs[2];
+  memset(gs, 0, sizeof gs);
+  int nps[2] = {0, 0}, accs[2] = {0, 0};
   for (int i = 0; i < n; ++i) {
     const lgx_s8_gemm_args& q = a[i];
     if (q.M < 0 || q.N < 0 || q.K < 0) return fail("lgx_s8_gemm_group: negative size");
@@ -609,7 +771,9 @@ int32_t lgx_s8_gemm_group(const lgx_s8_gemm_args* a, int32_t n, int32_t kind, vo
     if (!atr && q.lda < kp) return fail("lgx_s8_gemm_group: ROW operand A pitch < round_up(K, 32)");
     if (!btr && q.ldb < kp) return fail("lgx_s8_gemm_group: ROW operand B pitch < round_up(K, 32)");
     if (atr && q.lda < 8) return fail("lgx_s8_gemm_group: TR operand A pitch");
-    lgxs::Prob& p = g.p[np];
+    const int w = wide(kind, q.M, q.N);
+    const int tile = w ? 256 : 128;
+    lgxs::Prob& p = gs[w].p[nps[w]];
     p.A = (const char*)q.A;
     p.B = (const char*)q.B;
     p.lda = q.lda * 4;
@@ -617,8 +781,8 @@ int32_t lgx_s8_gemm_group(const lgx_s8_gemm_args* a, int32_t n, int32_t kind, vo
     p.M = q.M;
     p.N = q.N;
     p.K = q.K;
-    p.tiles_m = cdiv(q.M, bm);
-    p.tiles_n = cdiv(q.N, lgxs::BN);
+    p.tiles_m = cdiv(q.M, tile);
+    p.tiles_n = cdiv(q.N, tile);
     p.epi = q.epilogue;
     p.C = (char*)q.C;
     p.ldc = q.ldc * 4;
@@ -649,23 +813,28 @@ int32_t lgx_s8_gemm_group(const lgx_s8_gemm_args* a, int32_t n, int32_t kind, vo
     p.kchunk = per * lgxs::BK;
     split = std::max(1, cdiv(ksteps, per));
     p.tiles = p.tiles_m * p.tiles_n * split;
-    acc += cdiv(p.tiles, 8);
-    g.start[++np] = acc;
+    accs[w] += cdiv(p.tiles, 8);
+    gs[w].start[++nps[w]] = accs[w];
   }
-  g.n = np;
-  g.per_xcd = acc;
-  if (np == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
-  if (bm == 128) {
-    if (kind == LGX_S8_FWD) launch_gemm<LGX_S8_FWD, 128>(g, s);
-    else if (kind == LGX_S8_DX) launch_gemm<LGX_S8_DX, 128>(g, s);
-    else launch_gemm<LGX_S8_DW, 128>(g, s);
-  } else {
-    if (kind == LGX_S8_FWD) launch_gemm<LGX_S8_FWD, 256>(g, s);
-    else if (kind == LGX_S8_DX) launch_gemm<LGX_S8_DX, 256>(g, s);
-    else launch_gemm<LGX_S8_DW, 256>(g, s);
+  for (int w = 1; w >= 0; --w) {
+    lgxs::Group& g = gs[w];
+    g.n = nps[w];
+    g.per_xcd = accs[w];
+    if (g.n == 0) continue;
+    if (w) {
+      if (kind == LGX_S8_FWD) launch_gemm<LGX_S8_FWD, true>(g, s);
+      else if (kind == LGX_S8_DX) launch_gemm<LGX_S8_DX, true>(g, s);
+      else launch_gemm<LGX_S8_DW, true>(g, s);
+    } else {
+      if (kind == LGX_S8_FWD) launch_gemm<LGX_S8_FWD, false>(g, s);
+      else if (kind == LGX_S8_DX) launch_gemm<LGX_S8_DX, false>(g, s);
+      else launch_gemm<LGX_S8_DW, false>(g, s);
+    }
+    const int rc = launched("lgx_s8_gemm_group");
+    if (rc) return rc;
   }
-  return launched("lgx_s8_gemm_group");
+  return 0;
 }
 
 int32_t lgx_s8_split(const lgx_s8_split_args* a, int32_t n, void* stream) {
