@@ -160,6 +160,12 @@ class S8Minibatch:
             # colsum partials of dy[l] (the bias gradient of layer l): [tiles][out_l]
             p.cs = [torch.empty(max(self.tiles_m, self.nsb), W.shape[0], device=dev) for W in p.W]
         self.cs_lat = torch.empty(self.tiles_m, self.P2 - self.P0, device=dev)
+        # launch schedule: the level (grouped launch) of each chain's layer is its depth plus this
+        # shift — the critic and the estimator do not feed the actor, so they can share the
+        # actor's under-filled levels instead of running ahead of it (forward / input gradients)
+        # (measured on go2 at 24,576-row minibatches, tools/s8_levels.py: 765 -> 734 us per minibatch)
+        self.fwd_shift = {"critic": 3, "est": 3}
+        self.dx_shift = {"critic": 0, "est": 2}
         self._build(shapes)
 
     # ------------------------------------------------------------------ argument lists
@@ -221,11 +227,12 @@ class S8Minibatch:
             levels.setdefault(level, []).append(args)
         for p in (pr, sc, es, cr):
             A_ptr, lda, K = ins[p.name]
+            sh = self.fwd_shift.get(p.name, 0)
             for l in range(p.n):
                 last = l == p.n - 1
                 if not last:
                     o = p.out[l]
-                    put(l, self._fwd(p, l, A_ptr, lda, K, C=o.data_ptr(), ldc=o.shape[1]))
+                    put(l + sh, self._fwd(p, l, A_ptr, lda, K, C=o.data_ptr(), ldc=o.shape[1]))
                     A_ptr, lda, K = o.data_ptr(), o.shape[1], p.W[l].shape[0]
                     continue
                 if p is pr:
@@ -234,10 +241,10 @@ class S8Minibatch:
                 elif p is sc:
                     put(l, self._fwd(p, l, A_ptr, lda, K, C=row(self.ain, self.P1), ldc=lda_ain, elu=False))
                 elif p is es:
-                    put(l, self._fwd(p, l, A_ptr, lda, K, C32=self.pred.data_ptr(), ldc32=self.pred.shape[1],
-                                     elu=False))
+                    put(l + sh, self._fwd(p, l, A_ptr, lda, K, C32=self.pred.data_ptr(), ldc32=self.pred.shape[1],
+                                          elu=False))
                 else:
-                    put(l, self._fwd(p, l, A_ptr, lda, K, C32=self.value.data_ptr(), ldc32=1, elu=False))
+                    put(l + sh, self._fwd(p, l, A_ptr, lda, K, C32=self.value.data_ptr(), ldc32=1, elu=False))
         A_ptr, lda, K = row(self.ain), lda_ain, self.W8
         for l in range(a.n):
             lev = enc_depth + l
@@ -302,8 +309,9 @@ class S8Minibatch:
                               ld_add=0 if addend is None else addend.stride(0),
                               add_cols=0 if addend is None else addend.shape[1], colsum_ws=cs.data_ptr())
         for p in (a, cr, es):
+            sh = self.dx_shift.get(p.name, 0)
             for l in range(p.n - 1, 0, -1):
-                bput(p.n - 1 - l, dx(p, l, p.dy[l], p.dy[l - 1], p.cs[l - 1]))
+                bput(p.n - 1 - l + sh, dx(p, l, p.dy[l], p.dy[l - 1], p.cs[l - 1]))
         # the actor's first layer: gradient of its latent columns (+ the regulariser's)
         lev_lat = a.n - 1
         bput(lev_lat, dx(a, 0, a.dy[0], self.dlat.data_ptr(), self.cs_lat, N=self.P2 - self.P0,
