@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define LGX_MLP_ABI_VERSION 6
+#define LGX_MLP_ABI_VERSION 7
 
 enum {
   LGX_EPI_BIAS = 1,  /* + bias[n] */
@@ -210,6 +210,20 @@ int32_t lgx_aux_loss_backward(const lgx_aux_loss_args* args, void* stream);
  * equal aux->B. */
 int32_t lgx_loss_heads_forward(const lgx_ppo_head_args* head, const lgx_aux_loss_args* aux, void* stream);
 int32_t lgx_loss_heads_backward(const lgx_ppo_head_args* head, const lgx_aux_loss_args* aux, void* stream);
+/* ABI 7. Both heads' forward sums AND input gradients in ONE launch (the gradients need none
+ * of the forward's sums): the outputs of lgx_loss_heads_forward + lgx_loss_heads_backward on
+ * the same arguments (head->ws >= (3 + 16) * ceil(B/256) floats), where the narrow output
+ * gradients may ALSO (or instead: a NULL fp32 pointer) be written in S8 (include/lgx_s8.h:
+ * bf16 hi / lo per 8 columns, pitch in elements, a multiple of 8) with one column-sum partial
+ * per 256-row block ([ceil(B/256)][A], [..][1], [..][E]; E <= 8) — the S8 update's GEMM
+ * operands and last-layer bias-gradient partials (rsl_rl ppo.py:196-262 then the backward). */
+typedef struct lgx_heads_s8_args {
+  void* dmu_s8; int64_t ld_dmu; float* dmu_cs;
+  void* dvalue_s8; int64_t ld_dvalue; float* dvalue_cs;
+  void* de_s8; int64_t ld_de; float* de_cs;
+} lgx_heads_s8_args;
+int32_t lgx_loss_heads_fused(const lgx_ppo_head_args* head, const lgx_aux_loss_args* aux,
+                             const lgx_heads_s8_args* s8, void* stream);
 
 /* The optimizer tail of one PPO minibatch (rsl_rl ppo.py:264-291) in two launches, over
  * the flat gradient/parameter/moment buffers (one layout):

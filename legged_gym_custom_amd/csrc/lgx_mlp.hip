@@ -1350,6 +1350,209 @@ __global__ __launch_bounds__(HT) void loss_heads_bwd(lgx_ppo_head_args h, lgx_au
   else aux_loss_bwd_body(a);
 }
 
+// ---- both heads' forward sums AND input gradients in ONE launch (the S8 update): the
+// gradients need none of the forward's sums, so one pass over the rows serves both. The
+// narrow output gradients (dmu, dvalue, de) are also written in S8 (bf16 hi / lo interleaved
+// per 8 columns, lgx_s8.h) with one column-sum partial per block of HT = 256 rows — the
+// operands and bias-gradient partials of the update's GEMMs (replaces an lgx_s8_split launch).
+__device__ __forceinline__ unsigned pack_bf16x2(float a, float b) {
+  const __bf16 x = (__bf16)a, y = (__bf16)b;
+  return (unsigned)__builtin_bit_cast(unsigned short, x) | ((unsigned)__builtin_bit_cast(unsigned short, y) << 16);
+}
+// 8 fp32 -> one S8 group (32 B: the 8 bf16 hi values, then the 8 bf16 lo = bf16(x - hi))
+__device__ __forceinline__ void store_s8_group(char* dst, const float (&v)[8]) {
+  float lo[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) lo[e] = v[e] - (float)(__bf16)v[e];
+  typedef unsigned u32x4_ __attribute__((ext_vector_type(4)));
+  const u32x4_ H = {pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7])};
+  const u32x4_ L = {pack_bf16x2(lo[0], lo[1]), pack_bf16x2(lo[2], lo[3]), pack_bf16x2(lo[4], lo[5]),
+                    pack_bf16x2(lo[6], lo[7])};
+  reinterpret_cast<u32x4_*>(dst)[0] = H;
+  reinterpret_cast<u32x4_*>(dst)[1] = L;
+}
+
+template <int NA>
+__device__ __forceinline__ void ppo_head_fused_body(const lgx_ppo_head_args& p, const lgx_heads_s8_args& s) {
+  constexpr int NV = 3 + 2 * NA + 1;  // forward sums | dstd partial | dmu column sums | dvalue sum
+  __shared__ float red[4 * NV];
+  __shared__ float stdv[HMAXA], lstd[HMAXA];
+  if (threadIdx.x < HMAXA) {
+    const float sd = p.std[min((int)threadIdx.x, p.A - 1)];
+    stdv[threadIdx.x] = sd;
+    lstd[threadIdx.x] = logf(sd);
+  }
+  __syncthreads();
+  const float gs = p.g[0] / p.B, gv = p.g[1] / p.B, ge = p.g[2];
+  float v[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) v[k] = 0.f;
+  for (int i = blockIdx.x * HT + threadIdx.x; i < p.B; i += gridDim.x * HT) {
+    float act[NA], mu[NA], os[NA], om[NA];
+    load_cols(p.actions, i, p.A, act);
+    load_cols(p.mu, i, p.A, mu);
+    load_cols(p.old_sigma, i, p.A, os);
+    load_cols(p.old_mu, i, p.A, om);
+    const HeadRow h = head_row<NA>(p, i, stdv, lstd, act, mu);
+    const float a = p.adv[i];
+    const float lo = 1.f - p.clip, hi = 1.f + p.clip;
+    // forward (ppo_head_fwd_body)
+    const float s1 = -a * h.ratio, s2 = -a * fminf(fmaxf(h.ratio, lo), hi);
+    v[0] += fmaxf(s1, s2);
+    const float val = p.value[i], R = p.returns[i];
+    const float tv = (p.clipped_value ? p.target_values : p.value)[i];
+    float vc = 0.f;
+    if (p.clipped_value) {
+      vc = tv + fminf(fmaxf(val - tv, -p.clip), p.clip);
+      v[1] += fmaxf((val - R) * (val - R), (vc - R) * (vc - R));
+    } else {
+      v[1] += (R - val) * (R - val);
+    }
+    float kl = 0.f;
+#pragma unroll
+    for (int j = 0; j < NA; ++j) {
+      const float dm = om[j] - mu[j];
+      const float t = logf(stdv[j] / os[j] + 1.0e-5f) + (os[j] * os[j] + dm * dm) / (2.f * (stdv[j] * stdv[j])) - 0.5f;
+      kl = j < p.A ? kl + t : kl;
+    }
+    v[2] += kl;
+    // backward (ppo_head_bwd_body)
+    const float w1 = s1 > s2 ? 1.f : (s1 == s2 ? 0.5f : 0.f);
+    const float w2 = 1.f - w1;
+    const float in = (h.ratio >= lo && h.ratio <= hi) ? 1.f : 0.f;
+    const float dratio = gs * (w1 * -a + w2 * -a * in);
+    const float dlogp = dratio * h.ratio;
+    float dmu[NA];
+#pragma unroll
+    for (int j = 0; j < NA; ++j) {
+      const float d = act[j] - mu[j];
+      const float var = stdv[j] * stdv[j];
+      dmu[j] = j < p.A ? dlogp * d / var : 0.f;
+      if (j < p.A) {
+        if (p.dmu) p.dmu[(int64_t)i * p.A + j] = dmu[j];
+        v[3 + j] += dlogp * (d * d / (var * stdv[j]) - 1.f / stdv[j]);
+        v[3 + NA + j] += dmu[j];
+      }
+    }
+    float dv;
+    if (p.clipped_value) {
+      const float l1 = (val - R) * (val - R), l2 = (vc - R) * (vc - R);
+      const float u1 = l1 > l2 ? 1.f : (l1 == l2 ? 0.5f : 0.f);
+      const float inv = (val - tv >= -p.clip && val - tv <= p.clip) ? 1.f : 0.f;
+      dv = gv * (u1 * 2.f * (val - R) + (1.f - u1) * 2.f * (vc - R) * inv);
+    } else {
+      dv = gv * 2.f * (val - R);
+    }
+    if (p.dvalue) p.dvalue[i] = dv;
+    v[3 + 2 * NA] += dv;
+    if (s.dmu_s8) {
+#pragma unroll
+      for (int g0 = 0; g0 < NA; g0 += 8) {
+        if (g0 >= p.A) break;
+        float q[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) q[e] = g0 + e < NA ? dmu[g0 + e] : 0.f;
+        store_s8_group(static_cast<char*>(s.dmu_s8) + ((int64_t)i * s.ld_dmu + g0) * 4, q);
+      }
+    }
+    if (s.dvalue_s8) {
+      const float q[8] = {dv, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      store_s8_group(static_cast<char*>(s.dvalue_s8) + (int64_t)i * s.ld_dvalue * 4, q);
+    }
+  }
+  block_sum<NV>(v, red);
+  if (threadIdx.x == 0) {
+    for (int k = 0; k < 3; ++k) p.ws[blockIdx.x * (3 + HMAXA) + k] = v[k];
+    for (int j = 0; j < p.A; ++j) p.ws[blockIdx.x * (3 + HMAXA) + 3 + j] = v[3 + j];
+    if (s.dmu_cs)
+      for (int j = 0; j < p.A; ++j) s.dmu_cs[(int64_t)blockIdx.x * p.A + j] = v[3 + NA + j];
+    if (s.dvalue_cs) s.dvalue_cs[blockIdx.x] = v[3 + 2 * NA];
+  }
+  if (last_block(p.counter)) {
+    float t[3 + NA];
+    final_sum<3 + NA>(p.ws, 3 + HMAXA, gridDim.x, t, red);
+    if (threadIdx.x == 0) {
+      p.out[0] = t[0] / p.B;
+      p.out[1] = t[1] / p.B;
+      p.out[3] = t[2] / p.B;
+      if (p.kl_dst) *p.kl_dst = t[2] / p.B;
+      float ent = 0.f;
+      for (int j = 0; j < p.A; ++j) ent += 0.5f + 0.9189385332046727f + lstd[j];
+      p.out[2] = ent;
+      for (int j = 0; j < p.A; ++j) {
+        const float d = t[3 + j] + ge / stdv[j];
+        p.dstd[j] = p.accumulate_dstd ? p.dstd[j] + d : d;
+      }
+      *p.counter = 0u;
+    }
+  }
+}
+
+__device__ __forceinline__ void aux_loss_fused_body(const lgx_aux_loss_args& p, const lgx_heads_s8_args& s) {
+  constexpr int NV = 2 + 8;  // forward sums | de column sums (E <= 8 on the S8 path)
+  __shared__ float red[4 * NV];
+  __shared__ float st[HT * (AUX_CW + 1)];
+  const int i0 = blockIdx.x * HT, i = i0 + threadIdx.x;
+  const int64_t ic = min(i, p.B - 1);
+  const float gr = p.g[0] / p.B, ge = p.g[1] / p.B;
+  const int64_t ldp = p.ld_p > 0 ? p.ld_p : p.L;
+  float v[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) v[k] = 0.f;
+  const float n = sqrtf(aux_row_sq(p, ldp, i0, st));
+  const float q = aux_est_sq(p, ic);
+  if (i < p.B) {
+    v[0] = n;
+    const float nq = sqrtf(q);  // torch: norm(dim=1).pow(2)
+    v[1] = nq * nq;
+  }
+  const float k = n > 0.f ? gr / n : 0.f;
+  for (int j0 = 0; j0 < p.L; j0 += AUX_CW) {
+    const int w = min(AUX_CW, p.L - j0);
+    float a[AUX_CW];
+#pragma unroll
+    for (int j = 0; j < AUX_CW; ++j) a[j] = p.a[ic * p.L + j0 + min(j, w - 1)];
+    aux_stage_p(p, ldp, i0, j0, w, st);
+#pragma unroll
+    for (int j = 0; j < AUX_CW; ++j)
+      if (i < p.B && j < w) p.dp[ic * p.L + j0 + j] = k * (st[threadIdx.x * (AUX_CW + 1) + j] - a[j]);
+  }
+  float de[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int64_t c = ic * p.E + min(u, p.E - 1);
+    de[u] = u < p.E && i < p.B ? ge * 2.f * (p.e[c] - p.t[c]) : 0.f;
+    v[2 + u] = de[u];
+  }
+  if (i < p.B) {
+    if (p.de)
+      for (int u = 0; u < p.E; ++u) p.de[ic * p.E + u] = de[u];
+    if (s.de_s8) store_s8_group(static_cast<char*>(s.de_s8) + ic * s.ld_de * 4, de);
+  }
+  block_sum<NV>(v, red);
+  if (threadIdx.x == 0) {
+    p.ws[blockIdx.x * 2] = v[0];
+    p.ws[blockIdx.x * 2 + 1] = v[1];
+    if (s.de_cs)
+      for (int u = 0; u < p.E; ++u) s.de_cs[(int64_t)blockIdx.x * p.E + u] = v[2 + u];
+  }
+  if (last_block(p.counter)) {
+    float t[2];
+    final_sum<2>(p.ws, 2, gridDim.x, t, red);
+    if (threadIdx.x == 0) {
+      p.out[0] = t[0] / p.B;
+      p.out[1] = t[1] / p.B;
+      *p.counter = 0u;
+    }
+  }
+}
+
+template <int NA>
+__global__ __launch_bounds__(HT) void loss_heads_fused(lgx_ppo_head_args h, lgx_aux_loss_args a, lgx_heads_s8_args s) {
+  if (blockIdx.y == 0) ppo_head_fused_body<NA>(h, s);
+  else aux_loss_fused_body(a, s);
+}
+
 // ---------------------------------------------------------------- PPO minibatch optimizer tail
 #ifndef LGX_TAIL_BLOCKS
 #define LGX_TAIL_BLOCKS 128
@@ -1871,6 +2074,31 @@ int32_t lgx_loss_heads_backward(const lgx_ppo_head_args* h, const lgx_aux_loss_a
     return fail("lgx_loss_heads_backward: bad aux arguments");
   hipLaunchKernelGGL(h->A <= 12 ? lgxm::loss_heads_bwd<12> : lgxm::loss_heads_bwd<lgxm::HMAXA>, dim3(lgxm::head_grid(h->B), 2),
                      dim3(lgxm::HT), 0, static_cast<hipStream_t>(stream), *h, *a);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : fail(hipGetErrorString(e));
+}
+
+int32_t lgx_loss_heads_fused(const lgx_ppo_head_args* h, const lgx_aux_loss_args* a, const lgx_heads_s8_args* s,
+                             void* stream) {
+  if (head_check(h)) return -1;
+  if (!h->out || !h->old_mu || !h->old_sigma || !h->g || !h->dstd)
+    return fail("lgx_loss_heads_fused: null out/old_mu/old_sigma/g/dstd");
+  if (!a || a->B != h->B || a->L < 1 || a->E < 1 || !a->p || !a->a || !a->e || !a->t || !a->out || !a->ws ||
+      !a->counter || !a->g || !a->dp)
+    return fail("lgx_loss_heads_fused: bad aux arguments");
+  if (!s) return fail("lgx_loss_heads_fused: null S8 arguments");
+  if ((!h->dmu && !s->dmu_s8) || (!h->dvalue && !s->dvalue_s8) || (!a->de && !s->de_s8))
+    return fail("lgx_loss_heads_fused: dmu / dvalue / de need an fp32 or an S8 destination");
+  if (a->E > 8) return fail("lgx_loss_heads_fused: E <= 8");
+  if ((s->dmu_cs || s->dvalue_cs || s->de_cs) && lgxm::HT != 256)
+    return fail("lgx_loss_heads_fused: column-sum partials need 256-row blocks (LGX_HT 256)");
+  if ((s->dmu_s8 && (s->ld_dmu % 8 || s->ld_dmu < (h->A + 7) / 8 * 8)) || (s->dvalue_s8 && s->ld_dvalue % 8) ||
+      (s->de_s8 && s->ld_de % 8))
+    return fail("lgx_loss_heads_fused: S8 pitches are multiples of 8 covering the columns");
+  if ((((uintptr_t)s->dmu_s8) | ((uintptr_t)s->dvalue_s8) | ((uintptr_t)s->de_s8)) & 15)
+    return fail("lgx_loss_heads_fused: S8 destinations must be 16-B aligned");
+  hipLaunchKernelGGL(h->A <= 12 ? lgxm::loss_heads_fused<12> : lgxm::loss_heads_fused<lgxm::HMAXA>,
+                     dim3(lgxm::head_grid(h->B), 2), dim3(lgxm::HT), 0, static_cast<hipStream_t>(stream), *h, *a, *s);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : fail(hipGetErrorString(e));
 }

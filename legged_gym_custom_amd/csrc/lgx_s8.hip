@@ -5,10 +5,9 @@
 // inputs and the loss heads' gradients). So the K loop moves bytes and multiplies: no fp32 ->
 // bf16 split, no VGPR round trip.
 //
-// Block: output tile BM x 128 (BM 128: 4 waves, 2 LDS stages, 2 blocks per CU; BM 256: 8 waves,
-// 3 stages, 1 block per CU — lgxs::Cfg), each wave 64 x 64 = 4 x 4 tiles of
-// v_mfma_f32_16x16x32_bf16; per product lo*hi + hi*lo + hi*hi (3 x bf16, fp32 accumulation;
-// lgx_mlp.hip's order). K step 32.
+// Block: 256 threads = 4 waves as 2 x 2, output tile 128 x 128, each wave 64 x 64 = 4 x 4
+// tiles of v_mfma_f32_16x16x32_bf16; per product lo*hi + hi*lo + hi*hi (3 x bf16, fp32
+// accumulation; lgx_mlp.hip's order). K step 32, 2 LDS stages, 2 blocks per CU (lgxs::Cfg).
 // Staging: global_load_lds_dwordx4 (LDS-DMA; destination = wave base + 16 B x lane), 8 per wave
 // per K step, NS - 1 steps in flight across raw s_barriers with a counted vmcnt — no barrier
 // drains the DMA (cdna_hip_programming.md §5 "Pipelining across barriers"). Images:
@@ -42,30 +41,20 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 #ifndef LGX_S8_BK
 #define LGX_S8_BK 32
 #endif
-#ifndef LGX_S8_WIDE
-#define LGX_S8_WIDE 0  // bit (1 << kind): that kind's problems with M, N >= 256 run on the 256 x 256 kernel
-#endif
 
 namespace lgxs {
 
 constexpr int BK = LGX_S8_BK, BN = 128, NJ = 4, GMAX = LGX_S8_GROUP_MAX;
 static_assert(BK == 32 || BK == 64, "K step 32 or 64");
 constexpr int CP = BN + 4;  // fp32 epilogue image pitch (floats)
-// Two kernels. s8_gemm_kernel: output tile 128 x 128, 4 waves as 2 x 2 (each 64 x 64 = 4 x 4
-// MFMA tiles), 2 LDS stages of 32 KB, 2 blocks per CU. s8_gemm256_kernel: 256 x 256, 8 waves as
-// 2 x 4 (each 128 x 64), 2 stages of 64 KB, 1 block per CU, the two wave rows a barrier apart.
-// Measured and not kept: 256 x 128 and 128 x 128 tiles at 3-4 stages and 1
-// block per CU (a block's waves in lock step).
+// Output tile 128 x 128, 4 waves as 2 x 2 (each 64 x 64 = 4 x 4 MFMA tiles), 2 LDS stages of
+// 32 KB, 2 blocks per CU. Measured and not kept: 256 x 128 and 128 x 128 tiles
+// at 3-4 stages and 1 block per CU, and a 256 x 256 tile whose two wave rows run a barrier apart
+// (reads of one row beside the MFMAs of the other) — all slower on these shapes.
 struct Cfg {
   static constexpr int BM = 128, NS = 2, NW = 4, NT = 256, WR = 2;
   static constexpr int LDS_STAGES = NS * (BM + BN) * BK * 4, LDS_EPI = BM * CP * 4;
   static constexpr int LDS = LDS_STAGES > LDS_EPI ? LDS_STAGES : LDS_EPI;
-};
-struct Cfg256 {
-  static constexpr int BM = 256, BNW = 256, NW = 8, NT = 512, CPW = BNW + 4;
-  static constexpr int LDS_STAGES = 2 * (BM + BNW) * BK * 4, LDS_EPI = 128 * CPW * 4;
-  static constexpr int LDS = LDS_STAGES > LDS_EPI ? LDS_STAGES : LDS_EPI;
-  static_assert(LDS <= 160 * 1024, "LDS");
 };
 
 // slot swizzles (16-B slot index XOR), image row -> mask
@@ -439,135 +428,8 @@ __global__ __launch_bounds__(Cfg::NT, 2) __attribute__((amdgpu_waves_per_eu(1, 2
     epi_act<KIND, NT, BM, BN, CP>(P, img, m0, n0, tm * (BM / LGX_S8_TILE_M), tid);
 }
 
-// ---- 256 x 256 tile: 8 waves, wave (wr, wc) = (wave >> 2, wave & 3) owns rows 128 wr .. + 127,
-// columns 64 wc .. + 63 (8 x 4 MFMA tiles). Each 32-deep K step is 4 phases; a phase is a read
-// section R (this phase's fragments; phase 0 also the B fragments; phases 0 / 1 issue the next
-// step's LDS-DMA, A then B) and an MFMA section M (2 x 4 tiles x 3 products), each closed by a
-// raw s_barrier. The wave row wr = 1 runs one barrier behind wr = 0 (one extra barrier before
-// the loop, matched by one after it), so on every SIMD one wave's MFMAs overlap the other's
-// reads (cdna_hip_programming.md §5, the 256^2 8-phase template). Ordering (barrier counting,
-// one barrier of lag between the rows): every R ends with lgkmcnt(0), so a barrier retires the
-// reads before it (WAR: the next step's DMA overwrites the stage read one step earlier, issued
-// only after both rows passed their last read of it); phase 3's R waits vmcnt(0), two barriers
-// before the other row's first read of that stage (RAW).
-template <int KIND>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) void s8_gemm256_kernel(Group g) {
-  constexpr bool ATR = KIND == LGX_S8_DW, BTR = KIND != LGX_S8_FWD;
-  constexpr int T = 256, NW = 8, NT = 512, CPW = Cfg256::CPW;
-  using OA = Op<ATR, T, NW>;
-  using OB = Op<BTR, T, NW>;
-  constexpr int STAGE = OA::IMG + OB::IMG;
-  extern __shared__ __align__(16) char lds[];
-
-  const int x = blockIdx.x & 7, jb = blockIdx.x >> 3;
-  if (jb >= g.per_xcd) return;
-  int pi = 0;
-  while (pi + 1 < g.n && jb >= g.start[pi + 1]) ++pi;
-  const Prob P = g.p[pi];
-  const int l = x * (g.start[pi + 1] - g.start[pi]) + (jb - g.start[pi]);
-  if (l >= P.tiles) return;
-  const int tn = l % P.tiles_n, tm = (l / P.tiles_n) % P.tiles_m, z = l / (P.tiles_n * P.tiles_m);
-  const int m0 = tm * T, n0 = tn * T;
-  const int kbeg = z * P.kchunk;
-  const int kend = std::min(P.K, kbeg + P.kchunk);
-  const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = wave >> 2, wc = wave & 3;
-  const int wm = wr * 128, wn = wc * 64;
-  // a sub-tile entirely past M or N reads and multiplies nothing (wave-uniform)
-  const bool live = m0 + wm < P.M && n0 + wn < P.N;
-
-  uint32_t offA[OA::PW], offB[OB::PW];
-  OA::offsets(offA, wave, lane, m0, P.M, P.lda, kbeg);
-  OB::offsets(offB, wave, lane, n0, P.N, P.ldb, kbeg);
-  const int64_t sa = OA::step_bytes(P.lda), sb = OB::step_bytes(P.ldb);
-  const uint32_t lds0 = (uint32_t)(uintptr_t)((LDS_AS char*)lds);
-  const int wv = __builtin_amdgcn_readfirstlane(wave);
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bf16x8 bh[4], bl[4], ah[2], al[2];
-
-  if (nk > 0) {
-    OA::issue(P.A, offA, lds0, wv);
-    OB::issue(P.B, offB, lds0 + OA::IMG, wv);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  asm volatile("s_barrier" ::: "memory");
-  if (wr == 1) asm volatile("s_barrier" ::: "memory");
-  __builtin_amdgcn_sched_barrier(0);
-
-  for (int k = 0; k < nk; ++k) {
-    const char* st = lds + (k & 1) * STAGE;
-    const uint32_t nst = lds0 + (uint32_t)(((k + 1) & 1) * STAGE);
-    const bool next = k + 1 < nk;
-#pragma unroll
-    for (int ph = 0; ph < 4; ++ph) {
-      // R
-      if (live) {
-        if (ph == 0) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) OB::frag(st + OA::IMG, wn + 16 * j, 0, lane, bh[j], bl[j]);
-        }
-#pragma unroll
-        for (int i = 0; i < 2; ++i) OA::frag(st, wm + 32 * ph + 16 * i, 0, lane, ah[i], al[i]);
-      }
-      if (ph == 0 && next) OA::issue(P.A + (k + 1) * sa, offA, nst, wv);
-      if (ph == 1 && next) OB::issue(P.B + (k + 1) * sb, offB, nst + OA::IMG, wv);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if (ph == 3) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      asm volatile("s_barrier" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      // M
-      if (live) {
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            f32x4& c = acc[2 * ph + i][j];
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh[j], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl[j], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh[j], c, 0, 0, 0);
-          }
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      asm volatile("s_barrier" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-  if (wr == 0) asm volatile("s_barrier" ::: "memory");
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  __syncthreads();
-
-  // ---- epilogue, one wave row (128 x 256) at a time through the LDS image [128][CPW]
-  float* img = reinterpret_cast<float*>(lds);
-  const int ec = lane & 15, er = (lane >> 4) * 4;
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    if (wr == h) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) img[(16 * i + er + r) * CPW + wn + 16 * j + ec] = acc[i][j][r];
-    }
-    __syncthreads();
-    if constexpr (KIND == LGX_S8_DW)
-      epi_dw<NT, 128, T, CPW>(P, img, m0 + 128 * h, n0, z, tid);
-    else
-      epi_act<KIND, NT, 128, T, CPW>(P, img, m0 + 128 * h, n0, tm * 2 + h, tid);
-    __syncthreads();
-  }
-}
-
 // ---------------------------------------------------------------- fp32 -> S8 (+ column sums)
-#define LGX_S8_SPLIT_WIDE 1024  // (row, 8-column group) items per block of a wide split job
+#define LGX_S8_SPLIT_WIDE 512  // (row, 8-column group) items per block of a wide split job
 
 struct SplitJob {
   const float* src; int64_t ld_src;
@@ -701,22 +563,17 @@ static int launched(const char* what) {
 }
 static int cdiv(int a, int b) { return (a + b - 1) / b; }
 
-template <int KIND, bool WIDE>
+template <int KIND>
 static void launch_gemm(const lgxs::Group& g, hipStream_t s) {
-  constexpr int lds = WIDE ? lgxs::Cfg256::LDS : lgxs::Cfg::LDS;
-  const void* fn = WIDE ? (const void*)lgxs::s8_gemm256_kernel<KIND> : (const void*)lgxs::s8_gemm_kernel<KIND>;
+  constexpr int lds = lgxs::Cfg::LDS;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    (void)hipFuncSetAttribute((const void*)lgxs::s8_gemm_kernel<KIND>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              lds);
     attr = true;
   }
-  if constexpr (WIDE)
-    hipLaunchKernelGGL((lgxs::s8_gemm256_kernel<KIND>), dim3(8 * g.per_xcd), dim3(lgxs::Cfg256::NT), lds, s, g);
-  else
-    hipLaunchKernelGGL((lgxs::s8_gemm_kernel<KIND>), dim3(8 * g.per_xcd), dim3(lgxs::Cfg::NT), lds, s, g);
+  hipLaunchKernelGGL((lgxs::s8_gemm_kernel<KIND>), dim3(8 * g.per_xcd), dim3(lgxs::Cfg::NT), lds, s, g);
 }
-// problems of this kind with M, N >= 256 run on the 256 x 256 kernel
-static bool wide(int kind, int M, int N) { return ((LGX_S8_WIDE >> kind) & 1) && M >= 256 && N >= 256; }
 
 extern "C" {
 
@@ -726,35 +583,26 @@ const char* lgx_s8_last_error(void) { return g_err; }
 
 int32_t lgx_s8_pick_split(const int32_t* M, const int32_t* N, const int32_t* K, int32_t n, int32_t* out) {
   if (n < 0 || n > LGX_S8_GROUP_MAX) return fail("lgx_s8_pick_split: 0 <= n <= LGX_S8_GROUP_MAX");
-  for (int i = 0; i < n; ++i)
+  // one K chunk for every problem: the smallest that keeps the group within one residency
+  // round of 2 blocks per CU (256 CUs)
+  int64_t tiles = 0, kmax = 0;
+  for (int i = 0; i < n; ++i) {
     if (M[i] <= 0 || N[i] <= 0 || K[i] < 0) return fail("lgx_s8_pick_split: bad shape");
-  // per launch (the 256 x 256 problems, then the 128 x 128 ones: lgx_s8_gemm_group's split of
-  // the group) one K chunk for every problem: the smallest that keeps the launch within one
-  // residency round (256 CUs x 1 or 2 blocks)
-  for (int w = 0; w < 2; ++w) {
-    const int tile = w ? 256 : 128, slots = w ? 256 : 512;
-    int64_t tiles = 0, kmax = 0;
-    for (int i = 0; i < n; ++i) {
-      if (wide(LGX_S8_DW, M[i], N[i]) != (bool)w) continue;
-      tiles += (int64_t)cdiv(M[i], tile) * cdiv(N[i], tile);
-      kmax = std::max<int64_t>(kmax, K[i]);
-    }
-    const int64_t s = std::max<int64_t>(1, tiles ? slots / tiles : 1);
-    const int64_t chunk = ((kmax + s - 1) / s + lgxs::BK - 1) / lgxs::BK * lgxs::BK;
-    for (int i = 0; i < n; ++i)
-      if (wide(LGX_S8_DW, M[i], N[i]) == (bool)w)
-        out[i] = std::max(1, cdiv(K[i], (int)std::max<int64_t>(chunk, lgxs::BK)));
+    tiles += (int64_t)cdiv(M[i], lgxs::Cfg::BM) * cdiv(N[i], lgxs::BN);
+    kmax = std::max<int64_t>(kmax, K[i]);
   }
+  const int64_t s = std::max<int64_t>(1, tiles ? 512 / tiles : 1);
+  const int64_t chunk = ((kmax + s - 1) / s + lgxs::BK - 1) / lgxs::BK * lgxs::BK;
+  for (int i = 0; i < n; ++i) out[i] = std::max(1, cdiv(K[i], (int)std::max<int64_t>(chunk, lgxs::BK)));
   return 0;
 }
 
 int32_t lgx_s8_gemm_group(const lgx_s8_gemm_args* a, int32_t n, int32_t kind, void* stream) {
   if (n < 0 || n > LGX_S8_GROUP_MAX) return fail("lgx_s8_gemm_group: 0 <= n <= LGX_S8_GROUP_MAX");
   if (kind < LGX_S8_FWD || kind > LGX_S8_DW) return fail("lgx_s8_gemm_group: unknown kind");
-  // two launches at most: the problems on the 256 x 256 kernel (gw), the rest (g)
-  lgxs::Group gs[2];
-  memset(gs, 0, sizeof gs);
-  int nps[2] = {0, 0}, accs[2] = {0, 0};
+  lgxs::Group g;
+  memset(&g, 0, sizeof g);
+  int np = 0, acc = 0;
   for (int i = 0; i < n; ++i) {
     const lgx_s8_gemm_args& q = a[i];
     if (q.M < 0 || q.N < 0 || q.K < 0) return fail("lgx_s8_gemm_group: negative size");
@@ -771,9 +619,7 @@ int32_t lgx_s8_gemm_group(const lgx_s8_gemm_args* a, int32_t n, int32_t kind, vo
     if (!atr && q.lda < kp) return fail("lgx_s8_gemm_group: ROW operand A pitch < round_up(K, 32)");
     if (!btr && q.ldb < kp) return fail("lgx_s8_gemm_group: ROW operand B pitch < round_up(K, 32)");
     if (atr && q.lda < 8) return fail("lgx_s8_gemm_group: TR operand A pitch");
-    const int w = wide(kind, q.M, q.N);
-    const int tile = w ? 256 : 128;
-    lgxs::Prob& p = gs[w].p[nps[w]];
+    lgxs::Prob& p = g.p[np];
     p.A = (const char*)q.A;
     p.B = (const char*)q.B;
     p.lda = q.lda * 4;
@@ -781,8 +627,8 @@ int32_t lgx_s8_gemm_group(const lgx_s8_gemm_args* a, int32_t n, int32_t kind, vo
     p.M = q.M;
     p.N = q.N;
     p.K = q.K;
-    p.tiles_m = cdiv(q.M, tile);
-    p.tiles_n = cdiv(q.N, tile);
+    p.tiles_m = cdiv(q.M, lgxs::Cfg::BM);
+    p.tiles_n = cdiv(q.N, lgxs::BN);
     p.epi = q.epilogue;
     p.C = (char*)q.C;
     p.ldc = q.ldc * 4;
@@ -813,28 +659,17 @@ int32_t lgx_s8_gemm_group(const lgx_s8_gemm_args* a, int32_t n, int32_t kind, vo
     p.kchunk = per * lgxs::BK;
     split = std::max(1, cdiv(ksteps, per));
     p.tiles = p.tiles_m * p.tiles_n * split;
-    accs[w] += cdiv(p.tiles, 8);
-    gs[w].start[++nps[w]] = accs[w];
+    acc += cdiv(p.tiles, 8);
+    g.start[++np] = acc;
   }
+  g.n = np;
+  g.per_xcd = acc;
+  if (np == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
-  for (int w = 1; w >= 0; --w) {
-    lgxs::Group& g = gs[w];
-    g.n = nps[w];
-    g.per_xcd = accs[w];
-    if (g.n == 0) continue;
-    if (w) {
-      if (kind == LGX_S8_FWD) launch_gemm<LGX_S8_FWD, true>(g, s);
-      else if (kind == LGX_S8_DX) launch_gemm<LGX_S8_DX, true>(g, s);
-      else launch_gemm<LGX_S8_DW, true>(g, s);
-    } else {
-      if (kind == LGX_S8_FWD) launch_gemm<LGX_S8_FWD, false>(g, s);
-      else if (kind == LGX_S8_DX) launch_gemm<LGX_S8_DX, false>(g, s);
-      else launch_gemm<LGX_S8_DW, false>(g, s);
-    }
-    const int rc = launched("lgx_s8_gemm_group");
-    if (rc) return rc;
-  }
-  return 0;
+  if (kind == LGX_S8_FWD) launch_gemm<LGX_S8_FWD>(g, s);
+  else if (kind == LGX_S8_DX) launch_gemm<LGX_S8_DX>(g, s);
+  else launch_gemm<LGX_S8_DW>(g, s);
+  return launched("lgx_s8_gemm_group");
 }
 
 int32_t lgx_s8_split(const lgx_s8_split_args* a, int32_t n, void* stream) {

@@ -12,9 +12,10 @@ graph, no per-call allocation (the hipGraph captures exactly these launches):
        support_networks.py:25-80). Every epilogue writes its output in S8 (the next GEMMs'
        operand) — the encoders' last layers straight into their columns of the actor input —
        and in fp32 where a loss reads it (mu, V(s), the privileged latent, the estimate)
-    3  loss heads forward + backward (lgx_loss_heads_*: surrogate, clipped value loss, entropy,
-       KL, ROA regulariser, estimator loss; ppo.py:196-262); the narrow output gradients -> S8
-       with their column sums (the last layers' bias gradients)
+    3  loss heads forward + backward in one launch (lgx_loss_heads_fused: surrogate, clipped
+       value loss, entropy, KL, ROA regulariser, estimator loss; ppo.py:196-262), which also
+       writes the narrow output gradients in S8 with their column sums (the last layers' bias
+       gradients)
     4  input gradients, one grouped launch per level back through the chains; each epilogue
        applies ELU'(y) of the layer below (from its S8 output), writes S8, and sums its columns
        per 128-row tile (that layer's bias gradient). The actor's first layer forms the gradient
@@ -137,12 +138,9 @@ class S8Minibatch:
         self.dlat = S.empty(mb, self.W8 - self.P0, dev)
         self.priv.dy[-1] = None
         self.scan.dy[-1] = None
-        # fp32 loss-head gradients
-        A = self.mu.shape[1]
-        self.dmu = torch.empty(mb, A, device=dev)
-        self.dvalue = torch.empty(mb, device=dev)
+        # the regulariser's gradient of the privileged latent (fp32: the addend of the actor's
+        # latent-column input gradient) and the loss heads' partial-sum workspaces
         self.dp = torch.empty(mb, self.nlat, device=dev)
-        self.de = torch.empty(mb, self.pred.shape[1], device=dev)
         self.head_ws = torch.empty(16 * ((mb + 63) // 64), device=dev)
         self.aux_ws = torch.empty(2 * ((mb + 63) // 64), device=dev)
         # ---- weight-gradient split-K workspace and bias-gradient partials
@@ -256,40 +254,31 @@ class S8Minibatch:
                 put(lev, self._fwd(a, l, A_ptr, lda, K, C32=self.mu.data_ptr(), ldc32=self.mu.shape[1], elu=False))
         for lev in sorted(levels):
             S.gemm_group(levels[lev], S.FWD)
-        # 3. loss heads
+        # 3. loss heads: forward sums and input gradients in one launch; the narrow output
+        #    gradients straight into S8 with their per-256-row column sums (the last layers'
+        #    bias gradients)
         (obs_b, priv_b, critic_b, est_b, scan_b, actions_b, target_values_b, adv_b, returns_b, old_logp_b, old_mu_b,
          old_sigma_b) = shuf
         A = self.mu.shape[1]
         std = alg.actor_critic.std
         cnt, cnt_aux = H._counter(self.dev), H._counter(self.dev, "aux")
+        seeds = alg._seeds  # [1, c_value, -c_entropy, c_reg, 1]
         h = H.HeadArgs(mu=self.mu.data_ptr(), value=self.value.data_ptr(), std=std.data_ptr(),
                        actions=actions_b.data_ptr(), old_logp=old_logp_b.data_ptr(), adv=adv_b.data_ptr(),
                        target_values=target_values_b.data_ptr(), returns=returns_b.data_ptr(),
                        old_mu=old_mu_b.data_ptr(), old_sigma=old_sigma_b.data_ptr(), B=mb, A=A,
                        clip=float(alg.clip_param), clipped_value=int(bool(alg.use_clipped_value_loss)),
-                       out=head_out.data_ptr(), ws=self.head_ws.data_ptr(), counter=cnt.data_ptr(),
-                       kl_dst=None if kl_dst is None else kl_dst.data_ptr())
+                       out=head_out.data_ptr(), g=seeds.data_ptr(), dstd=std.grad.data_ptr(),
+                       ws=self.head_ws.data_ptr(), counter=cnt.data_ptr(),
+                       kl_dst=None if kl_dst is None else kl_dst.data_ptr(), accumulate_dstd=0)
         x = H.AuxArgs(p=self.lat.data_ptr(), a=adapt_latent.data_ptr(), L=self.nlat, e=self.pred.data_ptr(),
-                      t=est_b.data_ptr(), E=self.pred.shape[1], B=mb, out=aux_out.data_ptr(),
-                      ws=self.aux_ws.data_ptr(), counter=cnt_aux.data_ptr(), ld_p=self.nlat)
-        H._check(H.lib().lgx_loss_heads_forward(H.C.byref(h), H.C.byref(x), H._stream()), "lgx_loss_heads_forward")
-        seeds = alg._seeds  # [1, c_value, -c_entropy, c_reg, 1]
-        hb = H.HeadArgs(mu=self.mu.data_ptr(), value=self.value.data_ptr(), std=std.data_ptr(),
-                        actions=actions_b.data_ptr(), old_logp=old_logp_b.data_ptr(), adv=adv_b.data_ptr(),
-                        target_values=target_values_b.data_ptr(), returns=returns_b.data_ptr(), B=mb, A=A,
-                        clip=float(alg.clip_param), clipped_value=int(bool(alg.use_clipped_value_loss)),
-                        g=seeds.data_ptr(), dmu=self.dmu.data_ptr(), dvalue=self.dvalue.data_ptr(),
-                        dstd=std.grad.data_ptr(), ws=self.head_ws.data_ptr(), counter=cnt.data_ptr(),
-                        accumulate_dstd=0)
-        xb = H.AuxArgs(p=self.lat.data_ptr(), a=adapt_latent.data_ptr(), L=self.nlat, e=self.pred.data_ptr(),
-                       t=est_b.data_ptr(), E=self.pred.shape[1], B=mb, g=seeds.data_ptr() + 12,
-                       dp=self.dp.data_ptr(), de=self.de.data_ptr(), ld_p=self.nlat)
-        H._check(H.lib().lgx_loss_heads_backward(H.C.byref(hb), H.C.byref(xb), H._stream()),
-                 "lgx_loss_heads_backward")
-        # the narrow output gradients -> S8 + column sums (the last layers' bias gradients)
-        S.split([S.split_job(self.dmu, a.dy[-1].data_ptr(), a.dy[-1].shape[1], colsum_ws=a.cs[-1]),
-                 S.split_job(self.dvalue.view(mb, 1), cr.dy[-1].data_ptr(), cr.dy[-1].shape[1], colsum_ws=cr.cs[-1]),
-                 S.split_job(self.de, es.dy[-1].data_ptr(), es.dy[-1].shape[1], colsum_ws=es.cs[-1])])
+                      t=est_b.data_ptr(), E=self.pred.shape[1], B=mb, out=aux_out.data_ptr(), g=seeds.data_ptr() + 12,
+                      dp=self.dp.data_ptr(), ws=self.aux_ws.data_ptr(), counter=cnt_aux.data_ptr(), ld_p=self.nlat)
+        s8 = H.HeadsS8Args(dmu_s8=a.dy[-1].data_ptr(), ld_dmu=a.dy[-1].shape[1], dmu_cs=a.cs[-1].data_ptr(),
+                           dvalue_s8=cr.dy[-1].data_ptr(), ld_dvalue=cr.dy[-1].shape[1], dvalue_cs=cr.cs[-1].data_ptr(),
+                           de_s8=es.dy[-1].data_ptr(), ld_de=es.dy[-1].shape[1], de_cs=es.cs[-1].data_ptr())
+        H._check(H.lib().lgx_loss_heads_fused(H.C.byref(h), H.C.byref(x), H.C.byref(s8), H._stream()),
+                 "lgx_loss_heads_fused")
         # 4. input gradients
         blev = {}
 

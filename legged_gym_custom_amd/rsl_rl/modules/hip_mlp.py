@@ -20,7 +20,7 @@ import torch.nn as nn
 _LIB_PATH = os.environ.get("LGX_MLP_LIB") or os.path.join(
     os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))), "lib", "liblgx_mlp.so")
 _lib = None
-ABI_VERSION = 6
+ABI_VERSION = 7
 EPI_BIAS, EPI_ELU, EPI_DELU, EPI_ACCUM = 1, 2, 4, 8
 EXPORTED = ["lgx_mlp_abi_version", "lgx_mlp_sizeof_gemm_args", "lgx_mlp_pick_split", "lgx_gemm",
             "lgx_mlp_last_error", "lgx_adam_step", "lgx_ppo_head_forward", "lgx_ppo_head_backward",
@@ -28,7 +28,7 @@ EXPORTED = ["lgx_mlp_abi_version", "lgx_mlp_sizeof_gemm_args", "lgx_mlp_pick_spl
             "lgx_aux_loss_forward", "lgx_aux_loss_backward", "lgx_ppo_tail", "lgx_gemm_group",
             "lgx_mlp_pick_split_group", "lgx_gae", "lgx_normalize_advantages",
             "lgx_gather_rows", "lgx_transpose_batch", "lgx_loss_heads_forward", "lgx_loss_heads_backward",
-            "lgx_track_episodes", "lgx_chain", "lgx_adaptation_forward"]
+            "lgx_track_episodes", "lgx_chain", "lgx_adaptation_forward", "lgx_loss_heads_fused"]
 TAIL_MAX_LOSSES = 8
 COPY_MAX = 16
 SPLITK_MAX = 24
@@ -77,6 +77,13 @@ class AuxArgs(C.Structure):
     _fields_ = [("p", C.c_void_p), ("a", C.c_void_p), ("L", C.c_int32), ("e", C.c_void_p), ("t", C.c_void_p),
                 ("E", C.c_int32), ("B", C.c_int32), ("out", C.c_void_p), ("g", C.c_void_p), ("dp", C.c_void_p),
                 ("de", C.c_void_p), ("ws", C.c_void_p), ("counter", C.c_void_p), ("ld_p", C.c_int64)]
+
+
+class HeadsS8Args(C.Structure):
+    """Mirror of lgx_heads_s8_args (pitches in S8 elements)."""
+    _fields_ = [("dmu_s8", C.c_void_p), ("ld_dmu", C.c_int64), ("dmu_cs", C.c_void_p),
+                ("dvalue_s8", C.c_void_p), ("ld_dvalue", C.c_int64), ("dvalue_cs", C.c_void_p),
+                ("de_s8", C.c_void_p), ("ld_de", C.c_int64), ("de_cs", C.c_void_p)]
 
 
 class TailArgs(C.Structure):
@@ -187,6 +194,8 @@ def lib():
     for fn in ("lgx_loss_heads_forward", "lgx_loss_heads_backward"):
         getattr(L, fn).argtypes = [vp, vp, vp]
         getattr(L, fn).restype = C.c_int32
+    L.lgx_loss_heads_fused.argtypes = [vp, vp, vp, vp]
+    L.lgx_loss_heads_fused.restype = C.c_int32
     for fn in ("lgx_aux_loss_forward", "lgx_aux_loss_backward", "lgx_ppo_tail"):
         getattr(L, fn).argtypes = [vp, vp]
         getattr(L, fn).restype = C.c_int32

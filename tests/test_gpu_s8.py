@@ -180,3 +180,63 @@ def test_gather_split_and_span_reduce(S):
     ref = torch.full((20, 50), 7.0, device=dev)
     ref[:, 5:45] = ws[0, :, 10:50] + ws[1, :, 10:50] + ws[2, :, 10:50]
     assert torch.equal(out, ref)
+
+
+def test_loss_heads_fused_equals_forward_plus_backward(S):
+    """lgx_loss_heads_fused (one launch) == lgx_loss_heads_forward + lgx_loss_heads_backward on
+    the same arguments: the six losses, dstd, the latent gradient and the fp32 dmu / dvalue / de
+    bit for bit; its S8 outputs are the exact split of those fp32 gradients, and its column
+    sums are the 256-row block sums (fp32, fixed order: 1e-5)."""
+    from legged_gym_custom_amd.rsl_rl.modules import hip_mlp as H
+    g = torch.Generator(device=dev).manual_seed(43)
+    B, A, L, E = 3000, 12, 20, 3
+    r = lambda *s: torch.randn(*s, device=dev, generator=g)  # noqa: E731
+    mu, value, std = r(B, A), r(B, 1), r(A).abs() + 0.5
+    actions, old_logp, adv, tv, ret = r(B, A), r(B, 1), r(B, 1), r(B, 1), r(B, 1)
+    old_mu, old_sigma = r(B, A), r(B, A).abs() + 0.5
+    p_lat, a_lat, pred, t_est = r(B, L), r(B, L), r(B, E), r(B, E)
+    seeds = torch.tensor([1.0, 1.3, -0.01, 0.05, 1.0], device=dev)
+    nblk = (B + 255) // 256
+
+    def args(ws, wsa, out, out_aux, dmu, dvalue, dstd, dp, de, cnt, cnta):
+        h = H.HeadArgs(mu=mu.data_ptr(), value=value.data_ptr(), std=std.data_ptr(), actions=actions.data_ptr(),
+                       old_logp=old_logp.data_ptr(), adv=adv.data_ptr(), target_values=tv.data_ptr(),
+                       returns=ret.data_ptr(), old_mu=old_mu.data_ptr(), old_sigma=old_sigma.data_ptr(), B=B, A=A,
+                       clip=0.2, clipped_value=1, out=out.data_ptr(), g=seeds.data_ptr(),
+                       dmu=None if dmu is None else dmu.data_ptr(), dvalue=None if dvalue is None else dvalue.data_ptr(),
+                       dstd=dstd.data_ptr(), ws=ws.data_ptr(), counter=cnt.data_ptr(), accumulate_dstd=0)
+        x = H.AuxArgs(p=p_lat.data_ptr(), a=a_lat.data_ptr(), L=L, e=pred.data_ptr(), t=t_est.data_ptr(), E=E, B=B,
+                      out=out_aux.data_ptr(), g=seeds.data_ptr() + 12, dp=dp.data_ptr(),
+                      de=None if de is None else de.data_ptr(), ws=wsa.data_ptr(), counter=cnta.data_ptr(), ld_p=L)
+        return h, x
+
+    def bufs():
+        z = lambda *s: torch.full(s, float("nan"), device=dev)  # noqa: E731
+        return dict(ws=torch.zeros(19 * nblk, device=dev), wsa=torch.zeros(2 * nblk, device=dev), out=z(8),
+                    out_aux=z(2), dmu=z(B, A), dvalue=z(B), dstd=z(A), dp=z(B, L), de=z(B, E),
+                    cnt=torch.zeros(1, dtype=torch.int32, device=dev), cnta=torch.zeros(1, dtype=torch.int32, device=dev))
+    ref = bufs()
+    h, x = args(**ref)
+    H._check(H.lib().lgx_loss_heads_forward(H.C.byref(h), H.C.byref(x), H._stream()), "fwd")
+    H._check(H.lib().lgx_loss_heads_backward(H.C.byref(h), H.C.byref(x), H._stream()), "bwd")
+    got = bufs()
+    dmu8, dv8, de8 = S.empty(B, A, dev), S.empty(B, 1, dev), S.empty(B, E, dev)
+    cs_mu, cs_v, cs_e = (torch.full((nblk, n), float("nan"), device=dev) for n in (A, 1, E))
+    s8 = H.HeadsS8Args(dmu_s8=dmu8.data_ptr(), ld_dmu=dmu8.shape[1], dmu_cs=cs_mu.data_ptr(), dvalue_s8=dv8.data_ptr(),
+                       ld_dvalue=dv8.shape[1], dvalue_cs=cs_v.data_ptr(), de_s8=de8.data_ptr(), ld_de=de8.shape[1],
+                       de_cs=cs_e.data_ptr())
+    h, x = args(**got)
+    H._check(H.lib().lgx_loss_heads_fused(H.C.byref(h), H.C.byref(x), H.C.byref(s8), H._stream()), "fused")
+    torch.cuda.synchronize()
+    for k in ("out", "out_aux", "dmu", "dvalue", "dstd", "dp", "de"):
+        if k == "out":
+            idx = [0, 1, 2, 3]
+            assert torch.equal(got[k][idx], ref[k][idx]), k
+        else:
+            assert torch.equal(got[k], ref[k]), k
+    assert torch.equal(dmu8, S.to_s8_torch(ref["dmu"], ld=dmu8.shape[1], rows_pad=dmu8.shape[0]))
+    assert torch.equal(dv8, S.to_s8_torch(ref["dvalue"].view(B, 1), ld=dv8.shape[1], rows_pad=dv8.shape[0]))
+    assert torch.equal(de8, S.to_s8_torch(ref["de"], ld=de8.shape[1], rows_pad=de8.shape[0]))
+    for cs, full in ((cs_mu, ref["dmu"]), (cs_v, ref["dvalue"].view(B, 1)), (cs_e, ref["de"])):
+        blocks = torch.stack([full[i:i + 256].double().sum(0) for i in range(0, B, 256)])
+        torch.testing.assert_close(cs.double(), blocks, rtol=1e-5, atol=1e-6)

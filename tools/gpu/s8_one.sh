@@ -2,5 +2,5 @@
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 cd $R && mkdir -p gpurun_out
-PYTHONPATH=.:tools timeout -k 10 300 python -u tools/s8_one.py exp/*.so > gpurun_out/s8_one.log 2>&1
+PYTHONPATH=.:tools timeout -k 10 300 python -u tools/s8_one.py $(ls exp/*.so 2>/dev/null) > gpurun_out/s8_one.log 2>&1
 rc=$?; tail -1 gpurun_out/s8_one.log; exit $rc
