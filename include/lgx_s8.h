@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define LGX_S8_ABI_VERSION 1
+#define LGX_S8_ABI_VERSION 2
 
 enum { LGX_S8_FWD = 0, LGX_S8_DX = 1, LGX_S8_DW = 2 };  /* GEMM kinds (operand modes above) */
 
@@ -99,6 +99,43 @@ int32_t lgx_s8_gemm_group(const lgx_s8_gemm_args* args, int32_t n, int32_t kind,
 int32_t lgx_s8_pick_split(const int32_t* M, const int32_t* N, const int32_t* K, int32_t n, int32_t* out);
 int32_t lgx_s8_split(const lgx_s8_split_args* args, int32_t n, void* stream);
 int32_t lgx_s8_reduce(const lgx_s8_reduce_args* args, int32_t n, void* stream);
+
+/* ---- ABI v2: the rollout's act networks in ONE launch (PPO.act, ppo.py:129-153): the
+ * estimator, scan encoder and privileged encoder, the actor on [obs | priv latent | scan latent
+ * | est] (actor_critic.py:79-107) and the critic (:110-115), [Linear, ELU]* Linear chains whose
+ * weights are S8 ([N rows][ldw], ldw >= round_up(K, 32), pad zero) and biases fp32. The actor
+ * input is the S8 update's segmented layout: part p starts at column seg[p] (seg[0] = 0, a
+ * multiple of 4 each, zero gaps), width = its K (a multiple of 32); the actor's first-layer
+ * weights use the same layout. Writes mu [B, A] (row stride ld_mu) and value [B]. 32 rows per
+ * block, one block per CU; widths: actor input <= LGX_S8_ACT_MAXIN, hidden layers <=
+ * LGX_S8_ACT_MAXH (actor, critic) / LGX_S8_ACT_MAXENC (encoders), <= LGX_S8_ACT_MAXL layers. */
+#define LGX_S8_ACT_ROWS 32
+#define LGX_S8_ACT_MAXIN 640
+#define LGX_S8_ACT_MAXH 512
+#define LGX_S8_ACT_MAXENC 256
+#define LGX_S8_ACT_MAXL 6
+typedef struct lgx_s8_act_layer {
+  const void* W; int64_t ldw;   /* S8 weight rows (output columns), pitch in elements */
+  const float* b;
+  int32_t K, N, elu, pad0;
+} lgx_s8_act_layer;
+typedef struct lgx_s8_act_args {
+  int32_t B, width;
+  const float* obs; int64_t ld_obs; int32_t n_obs;                 /* actor / estimator input */
+  const float* priv_obs; int64_t ld_priv; int32_t n_priv_in;
+  const float* scan_obs; int64_t ld_scan; int32_t n_scan_in;
+  const float* critic_obs; int64_t ld_critic; int32_t n_critic_in;
+  int32_t est_c0;                                                   /* estimator input: obs columns [est_c0, est_c0 + K) */
+  int32_t seg[4];
+  lgx_s8_act_layer est[LGX_S8_ACT_MAXL], scan[LGX_S8_ACT_MAXL], priv[LGX_S8_ACT_MAXL];
+  lgx_s8_act_layer actor[LGX_S8_ACT_MAXL], critic[LGX_S8_ACT_MAXL];
+  int32_t n_est, n_scan, n_priv, n_actor, n_critic;
+  float* mu; int64_t ld_mu;
+  float* value;
+} lgx_s8_act_args;
+int32_t lgx_s8_act(const lgx_s8_act_args* args, void* stream);
+const char* lgx_s8_act_last_error(void);
+int32_t lgx_s8_sizeof_act_args(void);
 
 #ifdef __cplusplus
 }

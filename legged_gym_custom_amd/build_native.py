@@ -2,7 +2,8 @@
   lib/liblgx.so      env step (csrc/lgx_env.hip, include/lgx.h) + its host backend
                      (csrc/lgx_env_host.cpp, g++ -fopenmp, linked in: lgx_create(device=-1))
   lib/liblgx_mlp.so  learner MLP GEMMs (csrc/lgx_mlp.hip, include/lgx_mlp.h)
-  lib/liblgx_s8.so   the update's GEMM core on pre-split operands (csrc/lgx_s8.hip, include/lgx_s8.h)"""
+  lib/liblgx_s8.so   the update's GEMM core on pre-split operands (csrc/lgx_s8.hip) and the rollout's
+                     act networks in one launch (csrc/lgx_act.hip), include/lgx_s8.h"""
 import os
 import subprocess
 import sys
@@ -13,7 +14,7 @@ ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 LIBS = {
     "liblgx.so": (["lgx_env.hip"], ["lgx_device.h", "lgx_host.h", "lgx_env_host.cpp"], ["lgx.h"]),
     "liblgx_mlp.so": (["lgx_mlp.hip"], [], ["lgx_mlp.h"]),
-    "liblgx_s8.so": (["lgx_s8.hip"], [], ["lgx_s8.h"]),
+    "liblgx_s8.so": (["lgx_s8.hip", "lgx_act.hip"], [], ["lgx_s8.h"]),
 }
 OUT = os.path.join(HERE, "lib", "liblgx.so")
 OUT_MLP = os.path.join(HERE, "lib", "liblgx_mlp.so")

@@ -1,0 +1,335 @@
+// lgx_act.hip — the rollout's act networks in ONE launch (include/lgx_s8.h, lgx_s8_act):
+// PPO.act's estimator, scan encoder, privileged encoder, actor and critic (ppo.py:129-153,
+// actor_critic.py:79-107 / 190-226, support_networks.py:25-80) on S8 weights, gfx950.
+//
+// Block = 32 rows (envs) x 256 threads (4 waves); one block per CU (149 KB of LDS). Half of the
+// blocks ("actor blocks", on XCDs 0-3) run estimator -> scan encoder -> privileged encoder ->
+// actor for their rows, the other half ("critic blocks", XCDs 4-7) the critic, so each XCD's L2
+// holds one network's weights (≈2.4 MB). Activations stay in LDS (fp32, row pitch = 4 mod 64
+// floats: the 16 rows a fragment read touches fall on 16 distinct bank quads); the actor input
+// is assembled in place in the S8 update's segmented layout [obs | priv latent | scan latent |
+// est] (each part at a multiple of 8 columns, zero gaps), which is the layout of its S8 weights.
+//
+// A layer: out[32, N] = act(in[32, K] W^T + b), 3 x bf16 MFMAs (lo*hi + hi*lo + hi*hi, fp32
+// accumulation; lgx_s8.hip's order) per 16 x 16 x 32 tile. Wave w owns the 16-column tiles
+// w, w + 4, ...; each K step's weight fragments (hi 16 B + lo 16 B per lane, straight from the
+// S8 rows) are loaded two steps ahead into registers — with 32 rows per block the weights are
+// the streamed operand (each block reads all of its network's weights once), so this is the
+// weight-streaming pattern of a small-M GEMM, not a staged tile. The activation fragments are
+// read from LDS (or, for a first layer, from the input rows in global memory) and split into
+// hi / lo in registers; columns k >= K are zeroed by select (the S8 weights' pad columns are
+// zero too).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+
+#include "../../include/lgx_s8.h"
+
+namespace lgxa {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+#define GAS __attribute__((address_space(1)))  // global: the layers are separate functions, so
+                                               // their pointer arguments are cast back to it
+
+constexpr int R = LGX_S8_ACT_ROWS;          // rows per block (32)
+constexpr int NT = 256;                      // threads per block
+constexpr int XP = LGX_S8_ACT_MAXIN + 4;     // actor-input image pitch (floats, = 4 mod 64)
+constexpr int YP = LGX_S8_ACT_MAXH + 4;      // hidden-layer image pitch
+constexpr int SP = LGX_S8_ACT_MAXENC + 4;    // encoder scratch pitch (two images inside Y)
+static_assert(XP % 64 == 4 && YP % 64 == 4 && SP % 64 == 4, "pitches: 4 mod 64 floats");
+constexpr int XF = R * XP;                              // floats
+constexpr int YF = R * YP > 2 * R * SP ? R * YP : 2 * R * SP;
+constexpr int LDS_BYTES = (XF + YF) * 4;
+static_assert(LDS_BYTES <= 160 * 1024, "LDS");
+
+__device__ __forceinline__ float elu(float v) {  // lgx_mlp.hip's / lgx_s8.hip's ELU
+  float q = fmaf(v, 1.f / 40320.f, 1.f / 5040.f);
+  q = fmaf(v, q, 1.f / 720.f);
+  q = fmaf(v, q, 1.f / 120.f);
+  q = fmaf(v, q, 1.f / 24.f);
+  q = fmaf(v, q, 1.f / 6.f);
+  q = fmaf(v, q, 0.5f);
+  q = fmaf(v, q, 1.f);
+  const float small = v * q;
+  const float big = __expf(v) - 1.f;
+  return v > 0.f ? v : (v > -0.5f ? small : big);
+}
+
+// 8 fp32 (k >= K already zero) -> hi / lo bf16 fragments
+__device__ __forceinline__ void split8(const float (&v)[8], bf16x8& hi, bf16x8& lo) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const __bf16 h = (__bf16)v[e];
+    hi[e] = h;
+    lo[e] = (__bf16)(v[e] - (float)h);
+  }
+}
+
+// the dynamic LDS (the layers are separate functions: they address it by float offsets, so
+// their accesses stay LDS instructions)
+extern __shared__ __align__(16) float act_lds[];
+
+struct Src {  // a layer input: global rows (g, ld) or an LDS image (float offset of its first column, pitch ld)
+  const float* g;
+  int64_t ld;
+  int off;
+};
+struct Dst {  // a layer output: global rows (g, ld) or an LDS image
+  float* g;
+  int64_t ld;
+  int off;
+};
+
+// One layer for the block's 32 rows. TPW = 16-column tiles per wave (N <= 64 TPW). Not inlined:
+// the kernel calls each of the four instantiations from several chains.
+template <int TPW>
+__device__ __noinline__ void layer(const lgx_s8_act_layer L, Src in, Dst out, int rows) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, c = lane & 15;
+  const int K = L.K, N = L.N;
+  const int ns = (K + 31) / 32;
+  const int nt = (N + 15) / 16;
+  const GAS char* W = (const GAS char*)L.W;
+  const int64_t ldw = L.ldw * 4;  // bytes
+  // this lane's weight row (output column) per tile; tiles past N re-read the last row
+  int64_t wrow[TPW];
+  bool tv[TPW];
+#pragma unroll
+  for (int j = 0; j < TPW; ++j) {
+    const int t = wave + 4 * j;
+    tv[j] = t < nt;
+    wrow[j] = (int64_t)std::min(16 * t + c, N - 1) * ldw + g * 32;
+  }
+  u32x4 h0[TPW], l0[TPW], h1[TPW], l1[TPW], h2[TPW], l2[TPW];
+  auto loadw = [&](u32x4 (&h)[TPW], u32x4 (&l)[TPW], int s) {
+    const int64_t ko = (int64_t)std::min(s, ns - 1) * 128;  // 32 k x 4 B per step
+#pragma unroll
+    for (int j = 0; j < TPW; ++j) {
+      const GAS char* q = W + wrow[j] + ko;
+      h[j] = *(const GAS u32x4*)q;
+      l[j] = *(const GAS u32x4*)(q + 16);
+    }
+  };
+  f32x4 acc[2][TPW];
+#pragma unroll
+  for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+    for (int j = 0; j < TPW; ++j) acc[rt][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto step = [&](const u32x4 (&h)[TPW], const u32x4 (&l)[TPW], int s) {
+    bf16x8 ah[2], al[2];
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) {
+      const int row = std::min(16 * rt + c, rows - 1);
+      const int k0 = s * 32 + 8 * g;
+      float v[8];
+      if (in.g) {
+        const GAS float* q = (const GAS float*)in.g + (int64_t)row * in.ld;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = q[std::min(k0 + e, K - 1)];
+      } else {
+        const float* q = act_lds + in.off + row * (int)in.ld + k0;
+        const f32x4 a = *reinterpret_cast<const f32x4*>(q), b = *reinterpret_cast<const f32x4*>(q + 4);
+        v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3]; v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = k0 + e < K ? v[e] : 0.f;
+      split8(v, ah[rt], al[rt]);
+    }
+#pragma unroll
+    for (int j = 0; j < TPW; ++j) {
+      if (!tv[j]) continue;
+      const bf16x8 bh = __builtin_bit_cast(bf16x8, h[j]), bl = __builtin_bit_cast(bf16x8, l[j]);
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt) {
+        acc[rt][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[rt], bh, acc[rt][j], 0, 0, 0);
+        acc[rt][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[rt], bl, acc[rt][j], 0, 0, 0);
+        acc[rt][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[rt], bh, acc[rt][j], 0, 0, 0);
+      }
+    }
+  };
+
+  // weights two steps ahead (three register sets in rotation)
+  loadw(h0, l0, 0);
+  loadw(h1, l1, 1);
+  for (int s = 0; s < ns; s += 3) {
+    loadw(h2, l2, s + 2);
+    step(h0, l0, s);
+    if (s + 1 < ns) {
+      loadw(h0, l0, s + 3);
+      step(h1, l1, s + 1);
+    }
+    if (s + 2 < ns) {
+      loadw(h1, l1, s + 4);
+      step(h2, l2, s + 2);
+    }
+  }
+
+  // epilogue: bias (+ ELU); MFMA C map: col = lane & 15, row = 4 (lane >> 4) + r
+#pragma unroll
+  for (int j = 0; j < TPW; ++j) {
+    if (!tv[j]) continue;
+    const int col = 16 * (wave + 4 * j) + c;
+    if (col >= N) continue;
+    const float bias = ((const GAS float*)L.b)[col];
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * rt + 4 * g + r;
+        float v = acc[rt][j][r] + bias;
+        if (L.elu) v = elu(v);
+        if (out.g) {
+          if (row < rows) ((GAS float*)out.g)[(int64_t)row * out.ld + col] = v;
+        } else {
+          act_lds[out.off + row * (int)out.ld + col] = v;
+        }
+      }
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ void run_layer(const lgx_s8_act_layer L, Src in, Dst out, int rows) {
+  const int nt = (L.N + 15) / 16;
+  if (nt > 16) layer<8>(L, in, out, rows);
+  else if (nt > 8) layer<4>(L, in, out, rows);
+  else if (nt > 4) layer<2>(L, in, out, rows);
+  else layer<1>(L, in, out, rows);
+}
+
+// an encoder / estimator chain: first layer from `in`, hidden layers through the two scratch
+// images, the last layer into `last`
+__device__ __forceinline__ void run_chain(const lgx_s8_act_layer* Ls, int n, Src in, Dst last, int s1, int s2,
+                                          int rows) {
+  int cur = s1;
+  for (int i = 0; i < n; ++i) {
+    const bool fin = i == n - 1;
+    const Dst o = fin ? last : Dst{nullptr, SP, cur};
+    run_layer(Ls[i], in, o, rows);
+    if (!fin) {
+      in = Src{nullptr, SP, cur};
+      cur = cur == s1 ? s2 : s1;
+    }
+  }
+}
+
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 1))) void act_kernel(lgx_s8_act_args a) {
+  constexpr int X = 0, Y = XF;  // LDS images: X [R][XP], Y [R][YP] or two encoder scratch [R][SP]
+  const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+  const bool critic = xcd >= 4;
+  const int rb = slot * 4 + (xcd & 3);
+  const int nrb = (a.B + R - 1) / R;
+  if (rb >= nrb) return;
+  const int r0 = rb * R, rows = std::min(R, a.B - r0);
+  const int tid = threadIdx.x;
+  const int bufs[2] = {Y, X};
+  const int pit[2] = {YP, XP};
+
+  if (critic) {
+    Src in{a.critic_obs + (int64_t)r0 * a.ld_critic, a.ld_critic, 0};
+    for (int i = 0; i < a.n_critic; ++i) {
+      const bool fin = i == a.n_critic - 1;
+      const Dst o = fin ? Dst{a.value + r0, 1, 0} : Dst{nullptr, pit[i & 1], bufs[i & 1]};
+      run_layer(a.critic[i], in, o, rows);
+      in = Src{nullptr, pit[i & 1], bufs[i & 1]};
+    }
+    return;
+  }
+
+  // actor block: the actor-input image, zero (its gaps between parts stay zero), then obs
+  for (int i = tid; i < XF; i += NT) act_lds[X + i] = 0.f;
+  __syncthreads();
+  for (int i = tid; i < rows * a.n_obs; i += NT) {
+    const int r = i / a.n_obs, k = i - r * a.n_obs;
+    act_lds[X + r * XP + a.seg[0] + k] = a.obs[(int64_t)(r0 + r) * a.ld_obs + k];
+  }
+  __syncthreads();
+  const int s1 = Y, s2 = Y + R * SP;
+  // estimator (obs columns [est_c0, est_c0 + K) of the image) -> est part; scan encoder ->
+  // scan-latent part; privileged encoder -> latent part
+  run_chain(a.est, a.n_est, Src{nullptr, XP, X + a.seg[0] + a.est_c0}, Dst{nullptr, XP, X + a.seg[3]}, s1, s2, rows);
+  run_chain(a.scan, a.n_scan, Src{a.scan_obs + (int64_t)r0 * a.ld_scan, a.ld_scan, 0}, Dst{nullptr, XP, X + a.seg[2]},
+            s1, s2, rows);
+  run_chain(a.priv, a.n_priv, Src{a.priv_obs + (int64_t)r0 * a.ld_priv, a.ld_priv, 0}, Dst{nullptr, XP, X + a.seg[1]},
+            s1, s2, rows);
+  // actor: X -> Y -> X -> ... -> mu
+  Src in{nullptr, XP, X};
+  for (int i = 0; i < a.n_actor; ++i) {
+    const bool fin = i == a.n_actor - 1;
+    const Dst o = fin ? Dst{a.mu + (int64_t)r0 * a.ld_mu, a.ld_mu, 0} : Dst{nullptr, pit[i & 1], bufs[i & 1]};
+    run_layer(a.actor[i], in, o, rows);
+    in = Src{nullptr, pit[i & 1], bufs[i & 1]};
+  }
+}
+
+}  // namespace lgxa
+
+static thread_local char a_err[256] = "";
+static int afail(const char* m) {
+  snprintf(a_err, sizeof a_err, "%s", m);
+  return -1;
+}
+
+static int check_chain(const lgx_s8_act_layer* L, int n, int k_in, int maxh, const char* what) {
+  if (n < 1 || n > LGX_S8_ACT_MAXL) return afail(what);
+  int k = k_in;
+  for (int i = 0; i < n; ++i) {
+    if (!L[i].W || !L[i].b || L[i].K != k || L[i].N < 1 || L[i].ldw % 8 || L[i].ldw < (L[i].K + 31) / 32 * 32 ||
+        (((uintptr_t)L[i].W) & 15))
+      return afail(what);
+    if (i < n - 1 && L[i].N > maxh) return afail(what);
+    k = L[i].N;
+  }
+  return 0;
+}
+
+extern "C" {
+
+const char* lgx_s8_act_last_error(void) { return a_err; }
+int32_t lgx_s8_sizeof_act_args(void) { return (int32_t)sizeof(lgx_s8_act_args); }
+
+int32_t lgx_s8_act(const lgx_s8_act_args* a, void* stream) {
+  if (!a || a->B < 0) return afail("lgx_s8_act: bad arguments");
+  if (a->B == 0) return 0;
+  if (!a->obs || !a->scan_obs || !a->priv_obs || !a->critic_obs || !a->mu || !a->value)
+    return afail("lgx_s8_act: null input / output");
+  if (a->width > LGX_S8_ACT_MAXIN || a->width % 32 || a->seg[0] != 0 || a->n_obs + a->seg[0] > a->seg[1] ||
+      a->seg[1] > a->seg[2] || a->seg[2] > a->seg[3] || a->seg[3] > a->width || (a->seg[1] | a->seg[2] | a->seg[3]) % 4 ||
+      a->est_c0 % 4 || a->est_c0 < 0)
+    return afail("lgx_s8_act: actor-input layout (parts at multiples of 4 columns, width <= MAXIN, multiple of 32)");
+  if (check_chain(a->est, a->n_est, a->est->K, LGX_S8_ACT_MAXENC, "lgx_s8_act: estimator chain") ||
+      check_chain(a->scan, a->n_scan, a->scan->K, LGX_S8_ACT_MAXENC, "lgx_s8_act: scan-encoder chain") ||
+      check_chain(a->priv, a->n_priv, a->priv->K, LGX_S8_ACT_MAXENC, "lgx_s8_act: privileged-encoder chain") ||
+      check_chain(a->actor, a->n_actor, a->width, LGX_S8_ACT_MAXH, "lgx_s8_act: actor chain") ||
+      check_chain(a->critic, a->n_critic, a->critic->K, LGX_S8_ACT_MAXH, "lgx_s8_act: critic chain"))
+    return -1;
+  if (a->est_c0 + a->est->K > a->n_obs || a->scan->K != a->n_scan_in || a->priv->K != a->n_priv_in ||
+      a->critic->K != a->n_critic_in)
+    return afail("lgx_s8_act: first-layer widths do not match the inputs");
+  if (a->est[a->n_est - 1].N > a->width - a->seg[3] || a->scan[a->n_scan - 1].N > a->seg[3] - a->seg[2] ||
+      a->priv[a->n_priv - 1].N > a->seg[2] - a->seg[1] || a->critic[a->n_critic - 1].N != 1 ||
+      a->actor[a->n_actor - 1].N > a->ld_mu)
+    return afail("lgx_s8_act: output widths do not fit their parts");
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)lgxa::act_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              lgxa::LDS_BYTES);
+    attr = true;
+  }
+  const int nrb = (a->B + lgxa::R - 1) / lgxa::R;
+  hipLaunchKernelGGL(lgxa::act_kernel, dim3(8 * ((nrb + 3) / 4)), dim3(lgxa::NT), lgxa::LDS_BYTES,
+                     (hipStream_t)stream, *a);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    snprintf(a_err, sizeof a_err, "lgx_s8_act: %s", hipGetErrorString(e));
+    return -2;
+  }
+  return 0;
+}
+
+}  // extern "C"

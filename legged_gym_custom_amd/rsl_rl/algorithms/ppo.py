@@ -36,10 +36,13 @@ from legged_gym_custom_amd.rsl_rl.modules import ActorCritic, hip_mlp
 from legged_gym_custom_amd.rsl_rl.modules.support_networks import MlpEstimator
 from legged_gym_custom_amd.rsl_rl.storage import RolloutStorage
 
+from .s8_act import S8Act
 from .s8_update import S8Minibatch
 
 # the GPU minibatch on the pre-split GEMM core (s8_update.py); "0" selects the autograd path
 USE_S8 = os.environ.get("LGX_S8_UPDATE", "1") != "0"
+# the rollout's act networks in one launch (s8_act.py); "0" selects the grouped launches
+USE_FUSED_ACT = os.environ.get("LGX_FUSED_ACT", "1") != "0"
 # under RCCL ("nccl"), the per-minibatch gradient all-reduce is captured inside the one update
 # graph; "0" keeps the phased graphs (per-minibatch replays around host-issued all-reduces)
 GRAPH_ALLREDUCE = os.environ.get("LGX_GRAPH_ALLREDUCE", "1") != "0"
@@ -238,6 +241,8 @@ class PPO:
         # distributed path's graph capture on one GPU)
         self.allreduce_always = False
         self._s8 = None  # S8Minibatch, built at the first update (static buffers for the graphs)
+        self.use_fused_act = USE_FUSED_ACT and self.on_gpu
+        self._s8act = None  # S8Act, built at the first (eager) act
 
     # ------------------------------------------------------------------ flat Adam (HIP)
     def _flatten_params_and_moments(self):
@@ -316,15 +321,23 @@ class PPO:
             # samples a = mu + std * eps and writes actions, mu, sigma and the Normal
             # log-prob straight into this step's storage rows (lgx_act_head)
             s, k = self.storage, self.storage.step
+            fused = self._fused_act(adaptation_mode)
             with torch.no_grad():
-                items = [self.estimator.group_item(obs), ac.scan_encoder.group_item(scan_obs)]
-                if not adaptation_mode:
-                    items.append(ac.privileged_encoder_.group_item(privileged_obs))
-                outs = hip_mlp.forward_group(items)
-                estimated_obs, scan_latent = outs[:2]
-                latent = ac.adaptation_encoder(obs) if adaptation_mode else outs[2]
-                mean, t.values = hip_mlp.forward_group([(ac.actor, (obs, latent, scan_latent, estimated_obs)),
-                                                        (ac.critic, critic_obs)])
+                if fused is not None:
+                    # every act network in one launch (s8_act.py); its S8 weights are refreshed
+                    # at the rollout's first step (the update changed them)
+                    if k == 0:
+                        fused.refresh_weights()
+                    mean, t.values = fused.run(obs, privileged_obs, critic_obs, scan_obs)
+                else:
+                    items = [self.estimator.group_item(obs), ac.scan_encoder.group_item(scan_obs)]
+                    if not adaptation_mode:
+                        items.append(ac.privileged_encoder_.group_item(privileged_obs))
+                    outs = hip_mlp.forward_group(items)
+                    estimated_obs, scan_latent = outs[:2]
+                    latent = ac.adaptation_encoder(obs) if adaptation_mode else outs[2]
+                    mean, t.values = hip_mlp.forward_group([(ac.actor, (obs, latent, scan_latent, estimated_obs)),
+                                                            (ac.critic, critic_obs)])
                 noise = self.act_noise
                 eps = torch.randn_like(mean) if noise is None else None
                 dst = self.act_dst if self.act_dst is not None and self.act_dst.shape == mean.shape else None
@@ -343,6 +356,19 @@ class PPO:
         t.action_mean = ac.action_mean.detach()
         t.action_sigma = ac.action_std.detach()
         return t.actions
+
+    def _fused_act(self, adaptation_mode):
+        """The one-launch act networks (S8Act) for this rollout step, or None: adaptation mode
+        (DAgger iterations), shapes it does not cover, or disabled. Built outside graph capture."""
+        if adaptation_mode or not self.use_fused_act:
+            return None
+        n = self.storage.num_envs
+        if self._s8act is not None and self._s8act.B == n:
+            return self._s8act
+        if torch.cuda.is_current_stream_capturing() or not S8Act.supported(self):
+            return None
+        self._s8act = S8Act(self, n)
+        return self._s8act
 
     def _gpu_rollout(self):
         return str(self.device).startswith("cuda")
@@ -668,6 +694,7 @@ class PPO:
         self._eager_updates = 0
         self.graph_mode = None
         self._s8 = None  # its argument lists hold parameter / gradient addresses
+        self._s8act = None
 
     def _run_update(self):
         if not self.use_graphs:

@@ -1,0 +1,118 @@
+"""PPO.act's networks in ONE launch (include/lgx_s8.h lgx_s8_act; reference ppo.py:129-153,
+actor_critic.py:79-115 / 190-226, support_networks.py:25-80).
+
+The rollout step's estimator, scan encoder, privileged encoder, actor and critic run as one
+kernel over S8 copies of their weights (the update's operand format, s8_update.py): 32 envs per
+block, the activations in LDS, the actor input assembled in place as [obs | priv latent | scan
+latent | est] in the update's segmented layout. The weights are split once per rollout (at its
+first step, inside the rollout graph). The act head (sampling, log-prob, storage rows) stays
+`lgx_act_head`. Adaptation-mode rollouts (the DAgger iterations: the latent from the adaptation
+encoder) keep the grouped launches.
+
+Numerics: the same 3 x bf16 products as the grouped launches; the actor's first layer sums its
+input in the segmented order (the gaps are zeros), so mu differs from the grouped path by fp32
+rounding only (tests/test_gpu_s8_act.py: rtol 1e-5)."""
+import torch
+
+from legged_gym_custom_amd.rsl_rl.modules import hip_s8 as S
+from .s8_update import _chain
+
+
+def _r8(x):
+    return (x + 7) // 8 * 8
+
+
+class S8Act:
+    @staticmethod
+    def supported(alg):
+        if not alg.on_gpu:
+            return False
+        try:
+            S.lib()
+        except Exception:  # noqa: BLE001 — the grouped launches stay available
+            return False
+        ac, est = alg.actor_critic, alg.estimator
+        chains = [_chain(ac.actor), _chain(ac.critic), _chain(ac.privileged_encoder_.priv_encoder),
+                  _chain(ac.scan_encoder.scan_encoder), _chain(est.estimator)]
+        if any(c is None or len(c) > S.ACT_MAXL for c in chains):
+            return False
+        if ac.num_scan_obs <= 0 or ac.num_privileged_obs <= 0:
+            return False
+        actor, critic, priv, scan, estc = chains
+        nobs = ac.num_proprio * (1 + ac.history_buffer_length)
+        nlat, nscan, nest = priv[-1].out_features, scan[-1].out_features, ac.num_estimated_obs
+        width = (_r8(nobs) + _r8(nlat) + _r8(nscan) + _r8(nest) + 31) // 32 * 32
+        if width > S.ACT_MAXIN or actor[0].in_features != nobs + nlat + nscan + nest:
+            return False
+        if any(m.out_features > S.ACT_MAXH for m in actor[:-1] + critic[:-1]):
+            return False
+        if any(m.out_features > S.ACT_MAXENC for c in (priv, scan, estc) for m in c[:-1]):
+            return False
+        c0 = 0 if est.use_history else nobs - ac.num_proprio
+        return c0 % 4 == 0 and critic[-1].out_features == 1
+
+    def __init__(self, alg, num_envs):
+        ac, est = alg.actor_critic, alg.estimator
+        dev = alg.device
+        self.B = num_envs
+        actor, critic = _chain(ac.actor), _chain(ac.critic)
+        priv, scan = _chain(ac.privileged_encoder_.priv_encoder), _chain(ac.scan_encoder.scan_encoder)
+        estc = _chain(est.estimator)
+        nobs = ac.num_proprio * (1 + ac.history_buffer_length)
+        nlat, nscan, nest = priv[-1].out_features, scan[-1].out_features, ac.num_estimated_obs
+        P0 = _r8(nobs)
+        P1 = P0 + _r8(nlat)
+        P2 = P1 + _r8(nscan)
+        width = (P2 + _r8(nest) + 31) // 32 * 32
+        spans = [(0, 0, nobs), (nobs, P0, nlat), (nobs + nlat, P1, nscan), (nobs + nlat + nscan, P2, nest)]
+        self.nobs, self.width = nobs, width
+        self.est_c0 = 0 if est.use_history else nobs - ac.num_proprio
+        self._keep = []  # S8 weight buffers (their addresses are in the argument block)
+        self.wsplit = []
+        a = S.ActArgs()
+        a.B, a.width = num_envs, width
+        a.seg[0], a.seg[1], a.seg[2], a.seg[3] = 0, P0, P1, P2
+        a.est_c0 = self.est_c0
+
+        def fill(dst, layers, first_actor=False):
+            for i, m in enumerate(layers):
+                W = m.weight.detach()
+                if first_actor and i == 0:
+                    Ws = S.empty(W.shape[0], width, dev)
+                    for (c, s8, w) in spans:
+                        self.wsplit.append(S.split_job(W[:, c:c + w], S.group_ptr(Ws, s8), Ws.shape[1]))
+                    K = width
+                else:
+                    Ws = S.empty(W.shape[0], W.shape[1], dev)
+                    self.wsplit.append(S.split_job(W, Ws.data_ptr(), Ws.shape[1]))
+                    K = W.shape[1]
+                self._keep.append(Ws)
+                dst[i] = S.ActLayer(W=Ws.data_ptr(), ldw=Ws.shape[1], b=m.bias.data_ptr(), K=K, N=W.shape[0],
+                                    elu=int(i < len(layers) - 1))
+            return len(layers)
+        a.n_est = fill(a.est, estc)
+        a.n_scan = fill(a.scan, scan)
+        a.n_priv = fill(a.priv, priv)
+        a.n_actor = fill(a.actor, actor, first_actor=True)
+        a.n_critic = fill(a.critic, critic)
+        self.mu = torch.empty(num_envs, actor[-1].out_features, device=dev)
+        self.value = torch.empty(num_envs, 1, device=dev)
+        a.mu, a.ld_mu, a.value = self.mu.data_ptr(), self.mu.stride(0), self.value.data_ptr()
+        self.args = a
+
+    def refresh_weights(self):
+        """The weights -> S8 (one launch; the rollout's first step, after the update changed them)."""
+        S.split(self.wsplit)
+
+    def run(self, obs, priv, critic, scan):
+        """(mu [B, A], value [B, 1]) of this step's observations (static output buffers)."""
+        a = self.args
+        for t in (obs, priv, critic, scan):
+            if t.stride(1) != 1 or t.dtype != torch.float32 or t.shape[0] != self.B:
+                raise S.S8LibError("S8Act: fp32 [num_envs, cols] inputs with unit column stride")
+        a.obs, a.ld_obs, a.n_obs = obs.data_ptr(), obs.stride(0), obs.shape[1]
+        a.priv_obs, a.ld_priv, a.n_priv_in = priv.data_ptr(), priv.stride(0), priv.shape[1]
+        a.critic_obs, a.ld_critic, a.n_critic_in = critic.data_ptr(), critic.stride(0), critic.shape[1]
+        a.scan_obs, a.ld_scan, a.n_scan_in = scan.data_ptr(), scan.stride(0), scan.shape[1]
+        S.act(a)
+        return self.mu, self.value

@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "lib", "liblgx_s8.so")
 _lib = None
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 FWD, DX, DW = 0, 1, 2
 EPI_BIAS, EPI_ELU, EPI_DELU, EPI_ACCUM = 1, 2, 4, 8
 GROUP_MAX = 20
@@ -22,7 +22,9 @@ BATCH_MAX = 48
 TILE_M = 128
 SPLIT_ROWS = 256
 EXPORTED = ("lgx_s8_abi_version", "lgx_s8_sizeof_gemm_args", "lgx_s8_last_error", "lgx_s8_gemm_group",
-            "lgx_s8_pick_split", "lgx_s8_split", "lgx_s8_reduce")
+            "lgx_s8_pick_split", "lgx_s8_split", "lgx_s8_reduce", "lgx_s8_act", "lgx_s8_act_last_error",
+            "lgx_s8_sizeof_act_args")
+ACT_ROWS, ACT_MAXIN, ACT_MAXH, ACT_MAXENC, ACT_MAXL = 32, 640, 512, 256, 6
 
 vp, i32, i64 = C.c_void_p, C.c_int32, C.c_int64
 
@@ -42,6 +44,19 @@ class SplitArgs(C.Structure):
 class ReduceArgs(C.Structure):
     _fields_ = [("ws", vp), ("stride", i64), ("ld_ws", i64), ("out", vp), ("ld_out", i64), ("rows", i32),
                 ("cols", i32), ("nsplit", i32), ("accumulate", i32)]
+
+
+class ActLayer(C.Structure):
+    _fields_ = [("W", vp), ("ldw", i64), ("b", vp), ("K", i32), ("N", i32), ("elu", i32), ("pad0", i32)]
+
+
+class ActArgs(C.Structure):
+    _fields_ = [("B", i32), ("width", i32), ("obs", vp), ("ld_obs", i64), ("n_obs", i32), ("priv_obs", vp),
+                ("ld_priv", i64), ("n_priv_in", i32), ("scan_obs", vp), ("ld_scan", i64), ("n_scan_in", i32),
+                ("critic_obs", vp), ("ld_critic", i64), ("n_critic_in", i32), ("est_c0", i32), ("seg", i32 * 4),
+                ("est", ActLayer * 6), ("scan", ActLayer * 6), ("priv", ActLayer * 6), ("actor", ActLayer * 6),
+                ("critic", ActLayer * 6), ("n_est", i32), ("n_scan", i32), ("n_priv", i32), ("n_actor", i32),
+                ("n_critic", i32), ("mu", vp), ("ld_mu", i64), ("value", vp)]
 
 
 def flat_reduce(ws, stride, out, n, nsplit, accumulate=0):
@@ -69,11 +84,18 @@ def load(path=_LIB_PATH):
     for fn in ("lgx_s8_split", "lgx_s8_reduce"):
         getattr(L, fn).argtypes = [vp, i32, vp]
         getattr(L, fn).restype = i32
+    L.lgx_s8_act.argtypes = [vp, vp]
+    L.lgx_s8_act.restype = i32
+    L.lgx_s8_act_last_error.restype = C.c_char_p
+    L.lgx_s8_sizeof_act_args.restype = i32
     if L.lgx_s8_abi_version() != ABI_VERSION:
         raise S8LibError("liblgx_s8 ABI version mismatch; rebuild")
     if L.lgx_s8_sizeof_gemm_args() != C.sizeof(GemmArgs):
         raise S8LibError(f"lgx_s8_gemm_args layout mismatch: C {L.lgx_s8_sizeof_gemm_args()} vs ctypes "
                          f"{C.sizeof(GemmArgs)}")
+    if L.lgx_s8_sizeof_act_args() != C.sizeof(ActArgs):
+        raise S8LibError(f"lgx_s8_act_args layout mismatch: C {L.lgx_s8_sizeof_act_args()} vs ctypes "
+                         f"{C.sizeof(ActArgs)}")
     return L
 
 
@@ -177,6 +199,13 @@ def reduce(jobs, L=None):
         chunk = jobs[i:i + BATCH_MAX]
         arr = (ReduceArgs * len(chunk))(*chunk)
         _check(L.lgx_s8_reduce(arr, len(chunk), _stream()), "lgx_s8_reduce")
+
+
+def act(args):
+    """lgx_s8_act: the rollout's act networks in one launch (ActArgs)."""
+    L = lib()
+    if L.lgx_s8_act(C.byref(args), _stream()) != 0:
+        raise S8LibError("lgx_s8_act: " + L.lgx_s8_act_last_error().decode())
 
 
 def split_job(src, dst_ptr, ld_dst, colsum_ws=None, idx=None, rows=None):
