@@ -244,9 +244,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   // actor block: the actor-input image, zero (its gaps between parts stay zero), then obs
   for (int i = tid; i < XF; i += NT) act_lds[X + i] = 0.f;
   __syncthreads();
-  for (int i = tid; i < rows * a.n_obs; i += NT) {
-    const int r = i / a.n_obs, k = i - r * a.n_obs;
-    act_lds[X + r * XP + a.seg[0] + k] = a.obs[(int64_t)(r0 + r) * a.ld_obs + k];
+  for (int r = 0; r < rows; ++r) {
+    const float* src = a.obs + (int64_t)(r0 + r) * a.ld_obs;
+    for (int k = tid; k < a.n_obs; k += NT) act_lds[X + r * XP + a.seg[0] + k] = src[k];
   }
   __syncthreads();
   const int s1 = Y, s2 = Y + R * SP;
