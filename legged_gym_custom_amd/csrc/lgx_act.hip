@@ -85,10 +85,9 @@ struct Dst {  // a layer output: global rows (g, ld) or an LDS image
   int off;
 };
 
-// One layer for the block's 32 rows. TPW = 16-column tiles per wave (N <= 64 TPW). Not inlined:
-// the kernel calls each of the four instantiations from several chains.
+// One layer for the block's 32 rows. TPW = 16-column tiles per wave (N <= 64 TPW).
 template <int TPW>
-__device__ __noinline__ void layer(const lgx_s8_act_layer L, Src in, Dst out, int rows) {
+__device__ __forceinline__ void layer(const lgx_s8_act_layer& L, const Src& in, const Dst& out, int rows) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, c = lane & 15;
   const int K = L.K, N = L.N;
@@ -105,14 +104,34 @@ __device__ __noinline__ void layer(const lgx_s8_act_layer L, Src in, Dst out, in
     tv[j] = t < nt;
     wrow[j] = (int64_t)std::min(16 * t + c, N - 1) * ldw + g * 32;
   }
-  u32x4 h0[TPW], l0[TPW], h1[TPW], l1[TPW], h2[TPW], l2[TPW];
-  auto loadw = [&](u32x4 (&h)[TPW], u32x4 (&l)[TPW], int s) {
-    const int64_t ko = (int64_t)std::min(s, ns - 1) * 128;  // 32 k x 4 B per step
+  // a global input: this lane's two rows (row tiles 0, 1), clamped into the block
+  const bool gin = in.g != nullptr;
+  const GAS float* arow[2];
+#pragma unroll
+  for (int rt = 0; rt < 2; ++rt)
+    arow[rt] = (const GAS float*)in.g + (int64_t)std::min(16 * rt + c, rows - 1) * in.ld;
+
+  struct Set {
+    u32x4 h[TPW], l[TPW];
+    float a[2][8];  // a global input's values for this step
+  };
+  Set s0, s1, s2;
+  // weights (and a global input) two steps ahead, three register sets in rotation
+  auto load = [&](Set& S, int s) {
+    const int sc = std::min(s, ns - 1);
+    const int64_t ko = (int64_t)sc * 128;  // 32 k x 4 B per step
 #pragma unroll
     for (int j = 0; j < TPW; ++j) {
       const GAS char* q = W + wrow[j] + ko;
-      h[j] = *(const GAS u32x4*)q;
-      l[j] = *(const GAS u32x4*)(q + 16);
+      S.h[j] = *(const GAS u32x4*)q;
+      S.l[j] = *(const GAS u32x4*)(q + 16);
+    }
+    if (gin) {
+      const int k0 = sc * 32 + 8 * g;
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) S.a[rt][e] = arow[rt][std::min(k0 + e, K - 1)];
     }
   };
   f32x4 acc[2][TPW];
@@ -121,21 +140,19 @@ __device__ __noinline__ void layer(const lgx_s8_act_layer L, Src in, Dst out, in
 #pragma unroll
     for (int j = 0; j < TPW; ++j) acc[rt][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  auto step = [&](const u32x4 (&h)[TPW], const u32x4 (&l)[TPW], int s) {
+  auto step = [&](const Set& S, int s) {
     bf16x8 ah[2], al[2];
+    const int k0 = s * 32 + 8 * g;
 #pragma unroll
     for (int rt = 0; rt < 2; ++rt) {
-      const int row = std::min(16 * rt + c, rows - 1);
-      const int k0 = s * 32 + 8 * g;
       float v[8];
-      if (in.g) {
-        const GAS float* q = (const GAS float*)in.g + (int64_t)row * in.ld;
+      if (gin) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = q[std::min(k0 + e, K - 1)];
+        for (int e = 0; e < 8; ++e) v[e] = S.a[rt][e];
       } else {
-        const float* q = act_lds + in.off + row * (int)in.ld + k0;
-        const f32x4 a = *reinterpret_cast<const f32x4*>(q), b = *reinterpret_cast<const f32x4*>(q + 4);
-        v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3]; v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
+        const float* q = act_lds + in.off + (16 * rt + c) * (int)in.ld + k0;
+        const f32x4 x = *reinterpret_cast<const f32x4*>(q), y = *reinterpret_cast<const f32x4*>(q + 4);
+        v[0] = x[0]; v[1] = x[1]; v[2] = x[2]; v[3] = x[3]; v[4] = y[0]; v[5] = y[1]; v[6] = y[2]; v[7] = y[3];
       }
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = k0 + e < K ? v[e] : 0.f;
@@ -144,7 +161,7 @@ __device__ __noinline__ void layer(const lgx_s8_act_layer L, Src in, Dst out, in
 #pragma unroll
     for (int j = 0; j < TPW; ++j) {
       if (!tv[j]) continue;
-      const bf16x8 bh = __builtin_bit_cast(bf16x8, h[j]), bl = __builtin_bit_cast(bf16x8, l[j]);
+      const bf16x8 bh = __builtin_bit_cast(bf16x8, S.h[j]), bl = __builtin_bit_cast(bf16x8, S.l[j]);
 #pragma unroll
       for (int rt = 0; rt < 2; ++rt) {
         acc[rt][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[rt], bh, acc[rt][j], 0, 0, 0);
@@ -154,19 +171,18 @@ __device__ __noinline__ void layer(const lgx_s8_act_layer L, Src in, Dst out, in
     }
   };
 
-  // weights two steps ahead (three register sets in rotation)
-  loadw(h0, l0, 0);
-  loadw(h1, l1, 1);
+  load(s0, 0);
+  load(s1, 1);
   for (int s = 0; s < ns; s += 3) {
-    loadw(h2, l2, s + 2);
-    step(h0, l0, s);
+    load(s2, s + 2);
+    step(s0, s);
     if (s + 1 < ns) {
-      loadw(h0, l0, s + 3);
-      step(h1, l1, s + 1);
+      load(s0, s + 3);
+      step(s1, s + 1);
     }
     if (s + 2 < ns) {
-      loadw(h1, l1, s + 4);
-      step(h2, l2, s + 2);
+      load(s1, s + 4);
+      step(s2, s + 2);
     }
   }
 
@@ -194,32 +210,56 @@ __device__ __noinline__ void layer(const lgx_s8_act_layer L, Src in, Dst out, in
   __syncthreads();
 }
 
-__device__ __forceinline__ void run_layer(const lgx_s8_act_layer L, Src in, Dst out, int rows) {
-  const int nt = (L.N + 15) / 16;
-  if (nt > 16) layer<8>(L, in, out, rows);
-  else if (nt > 8) layer<4>(L, in, out, rows);
-  else if (nt > 4) layer<2>(L, in, out, rows);
-  else layer<1>(L, in, out, rows);
-}
-
-// an encoder / estimator chain: first layer from `in`, hidden layers through the two scratch
-// images, the last layer into `last`
-__device__ __forceinline__ void run_chain(const lgx_s8_act_layer* Ls, int n, Src in, Dst last, int s1, int s2,
-                                          int rows) {
-  int cur = s1;
-  for (int i = 0; i < n; ++i) {
-    const bool fin = i == n - 1;
-    const Dst o = fin ? last : Dst{nullptr, SP, cur};
-    run_layer(Ls[i], in, o, rows);
-    if (!fin) {
-      in = Src{nullptr, SP, cur};
-      cur = cur == s1 ? s2 : s1;
-    }
+// Layer i of this block's chain sequence — critic blocks: the critic; actor blocks: estimator,
+// scan encoder, privileged encoder, actor — with its input and output (LDS images: X the actor
+// input [R][XP], Y the hidden layers [R][YP] or two encoder scratch images [R][SP])
+__device__ __forceinline__ void job(const lgx_s8_act_args& a, bool critic, int i, int r0, lgx_s8_act_layer& L, Src& in,
+                                    Dst& out) {
+  constexpr int X = 0, Y = XF, S1 = XF, S2 = XF + R * SP;
+  auto hidden = [&](int pos, int& off, int64_t& ld) {  // the wide chains' images: Y, X, Y, ...
+    off = (pos & 1) ? X : Y;
+    ld = (pos & 1) ? XP : YP;
+  };
+  if (critic) {
+    L = a.critic[i];
+    if (i == 0) in = Src{a.critic_obs + (int64_t)r0 * a.ld_critic, a.ld_critic, 0};
+    else { in.g = nullptr; hidden(i - 1, in.off, in.ld); }
+    if (i == a.n_critic - 1) out = Dst{a.value + r0, 1, 0};
+    else { out.g = nullptr; hidden(i, out.off, out.ld); }
+    return;
   }
+  const lgx_s8_act_layer* ch;
+  int n, p;
+  Src first;
+  Dst last;
+  if (i < a.n_est) {
+    ch = a.est; n = a.n_est; p = i;
+    first = Src{nullptr, XP, X + a.seg[0] + a.est_c0};
+    last = Dst{nullptr, XP, X + a.seg[3]};
+  } else if (i < a.n_est + a.n_scan) {
+    ch = a.scan; n = a.n_scan; p = i - a.n_est;
+    first = Src{a.scan_obs + (int64_t)r0 * a.ld_scan, a.ld_scan, 0};
+    last = Dst{nullptr, XP, X + a.seg[2]};
+  } else if (i < a.n_est + a.n_scan + a.n_priv) {
+    ch = a.priv; n = a.n_priv; p = i - a.n_est - a.n_scan;
+    first = Src{a.priv_obs + (int64_t)r0 * a.ld_priv, a.ld_priv, 0};
+    last = Dst{nullptr, XP, X + a.seg[1]};
+  } else {
+    p = i - a.n_est - a.n_scan - a.n_priv;
+    L = a.actor[p];
+    if (p == 0) in = Src{nullptr, XP, X};
+    else { in.g = nullptr; hidden(p - 1, in.off, in.ld); }
+    if (p == a.n_actor - 1) out = Dst{a.mu + (int64_t)r0 * a.ld_mu, a.ld_mu, 0};
+    else { out.g = nullptr; hidden(p, out.off, out.ld); }
+    return;
+  }
+  // encoder chains: scratch images S1, S2, S1, ...
+  L = ch[p];
+  in = p == 0 ? first : Src{nullptr, SP, ((p - 1) & 1) ? S2 : S1};
+  out = p == n - 1 ? last : Dst{nullptr, SP, (p & 1) ? S2 : S1};
 }
 
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 1))) void act_kernel(lgx_s8_act_args a) {
-  constexpr int X = 0, Y = XF;  // LDS images: X [R][XP], Y [R][YP] or two encoder scratch [R][SP]
   const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
   const bool critic = xcd >= 4;
   const int rb = slot * 4 + (xcd & 3);
@@ -227,43 +267,27 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   if (rb >= nrb) return;
   const int r0 = rb * R, rows = std::min(R, a.B - r0);
   const int tid = threadIdx.x;
-  const int bufs[2] = {Y, X};
-  const int pit[2] = {YP, XP};
-
-  if (critic) {
-    Src in{a.critic_obs + (int64_t)r0 * a.ld_critic, a.ld_critic, 0};
-    for (int i = 0; i < a.n_critic; ++i) {
-      const bool fin = i == a.n_critic - 1;
-      const Dst o = fin ? Dst{a.value + r0, 1, 0} : Dst{nullptr, pit[i & 1], bufs[i & 1]};
-      run_layer(a.critic[i], in, o, rows);
-      in = Src{nullptr, pit[i & 1], bufs[i & 1]};
+  if (!critic) {
+    // the actor-input image: zero (its gaps between parts stay zero), then obs
+    for (int i = tid; i < XF; i += NT) act_lds[i] = 0.f;
+    __syncthreads();
+    for (int r = 0; r < rows; ++r) {
+      const float* src = a.obs + (int64_t)(r0 + r) * a.ld_obs;
+      for (int k = tid; k < a.n_obs; k += NT) act_lds[r * XP + a.seg[0] + k] = src[k];
     }
-    return;
+    __syncthreads();
   }
-
-  // actor block: the actor-input image, zero (its gaps between parts stay zero), then obs
-  for (int i = tid; i < XF; i += NT) act_lds[X + i] = 0.f;
-  __syncthreads();
-  for (int r = 0; r < rows; ++r) {
-    const float* src = a.obs + (int64_t)(r0 + r) * a.ld_obs;
-    for (int k = tid; k < a.n_obs; k += NT) act_lds[X + r * XP + a.seg[0] + k] = src[k];
-  }
-  __syncthreads();
-  const int s1 = Y, s2 = Y + R * SP;
-  // estimator (obs columns [est_c0, est_c0 + K) of the image) -> est part; scan encoder ->
-  // scan-latent part; privileged encoder -> latent part
-  run_chain(a.est, a.n_est, Src{nullptr, XP, X + a.seg[0] + a.est_c0}, Dst{nullptr, XP, X + a.seg[3]}, s1, s2, rows);
-  run_chain(a.scan, a.n_scan, Src{a.scan_obs + (int64_t)r0 * a.ld_scan, a.ld_scan, 0}, Dst{nullptr, XP, X + a.seg[2]},
-            s1, s2, rows);
-  run_chain(a.priv, a.n_priv, Src{a.priv_obs + (int64_t)r0 * a.ld_priv, a.ld_priv, 0}, Dst{nullptr, XP, X + a.seg[1]},
-            s1, s2, rows);
-  // actor: X -> Y -> X -> ... -> mu
-  Src in{nullptr, XP, X};
-  for (int i = 0; i < a.n_actor; ++i) {
-    const bool fin = i == a.n_actor - 1;
-    const Dst o = fin ? Dst{a.mu + (int64_t)r0 * a.ld_mu, a.ld_mu, 0} : Dst{nullptr, pit[i & 1], bufs[i & 1]};
-    run_layer(a.actor[i], in, o, rows);
-    in = Src{nullptr, pit[i & 1], bufs[i & 1]};
+  const int njobs = critic ? a.n_critic : a.n_est + a.n_scan + a.n_priv + a.n_actor;
+  for (int i = 0; i < njobs; ++i) {
+    lgx_s8_act_layer L;
+    Src in;
+    Dst out;
+    job(a, critic, i, r0, L, in, out);
+    const int nt = (L.N + 15) / 16;  // one call site per width class
+    if (nt > 16) layer<8>(L, in, out, rows);
+    else if (nt > 8) layer<4>(L, in, out, rows);
+    else if (nt > 4) layer<2>(L, in, out, rows);
+    else layer<1>(L, in, out, rows);
   }
 }
 
