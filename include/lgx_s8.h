@@ -132,6 +132,11 @@ typedef struct lgx_s8_act_args {
   int32_t n_est, n_scan, n_priv, n_actor, n_critic;
   float* mu; int64_t ld_mu;
   float* value;
+  /* optional (NULL: skipped): this step's storage rows (rollout_storage.py:87-105, written at
+   * act time), contiguous [B, width of the input]: the kernel copies obs, priv_obs, scan_obs,
+   * critic_obs and est_obs ([B, n_est_obs], read for this copy only) into them */
+  float* obs_st; float* priv_st; float* scan_st; float* critic_st; float* est_st;
+  const float* est_obs; int64_t ld_est; int32_t n_est_obs, pad1;
 } lgx_s8_act_args;
 int32_t lgx_s8_act(const lgx_s8_act_args* args, void* stream);
 const char* lgx_s8_act_last_error(void);

@@ -267,14 +267,30 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   if (rb >= nrb) return;
   const int r0 = rb * R, rows = std::min(R, a.B - r0);
   const int tid = threadIdx.x;
-  if (!critic) {
-    // the actor-input image: zero (its gaps between parts stay zero), then obs
+  // this step's storage rows (optional): a contiguous [rows, n] copy of an input
+  auto store_rows = [&](float* dst, const float* src, int64_t ld, int n) {
+    if (!dst) return;
+    for (int r = 0; r < rows; ++r)
+      for (int k = tid; k < n; k += NT) dst[(int64_t)(r0 + r) * n + k] = src[(int64_t)(r0 + r) * ld + k];
+  };
+  if (critic) {
+    store_rows(a.critic_st, a.critic_obs, a.ld_critic, a.n_critic_in);
+  } else {
+    // the actor-input image: zero (its gaps between parts stay zero), then obs (and its row)
     for (int i = tid; i < XF; i += NT) act_lds[i] = 0.f;
     __syncthreads();
     for (int r = 0; r < rows; ++r) {
       const float* src = a.obs + (int64_t)(r0 + r) * a.ld_obs;
-      for (int k = tid; k < a.n_obs; k += NT) act_lds[r * XP + a.seg[0] + k] = src[k];
+      float* st = a.obs_st ? a.obs_st + (int64_t)(r0 + r) * a.n_obs : nullptr;
+      for (int k = tid; k < a.n_obs; k += NT) {
+        const float v = src[k];
+        act_lds[r * XP + a.seg[0] + k] = v;
+        if (st) st[k] = v;
+      }
     }
+    store_rows(a.priv_st, a.priv_obs, a.ld_priv, a.n_priv_in);
+    store_rows(a.scan_st, a.scan_obs, a.ld_scan, a.n_scan_in);
+    store_rows(a.est_st, a.est_obs, a.ld_est, a.n_est_obs);
     __syncthreads();
   }
   const int njobs = critic ? a.n_critic : a.n_est + a.n_scan + a.n_priv + a.n_actor;
@@ -332,6 +348,8 @@ int32_t lgx_s8_act(const lgx_s8_act_args* a, void* stream) {
       check_chain(a->actor, a->n_actor, a->width, LGX_S8_ACT_MAXH, "lgx_s8_act: actor chain") ||
       check_chain(a->critic, a->n_critic, a->critic->K, LGX_S8_ACT_MAXH, "lgx_s8_act: critic chain"))
     return -1;
+  if (a->est_st && (!a->est_obs || a->n_est_obs < 1 || a->ld_est < a->n_est_obs))
+    return afail("lgx_s8_act: est storage row without its source");
   if (a->est_c0 + a->est->K > a->n_obs || a->scan->K != a->n_scan_in || a->priv->K != a->n_priv_in ||
       a->critic->K != a->n_critic_in)
     return afail("lgx_s8_act: first-layer widths do not match the inputs");

@@ -313,22 +313,29 @@ class PPO:
         t = self.transition
         ac = self.actor_critic
         if self._gpu_rollout():
-            (t.observations, t.privileged_observations, t.critic_observations, t.true_estimated_observations,
-             t.scan_observations) = self.storage.record_observations(obs, privileged_obs, critic_obs,
-                                                                     true_estimated_obs, scan_obs)
             # the estimator, privileged/scan encoders and critic read only observations: one
-            # grouped launch per depth (hip_mlp.forward_group), then the actor; one HIP kernel
-            # samples a = mu + std * eps and writes actions, mu, sigma and the Normal
+            # grouped launch per depth (hip_mlp.forward_group), then the actor — or all of them
+            # in one launch (s8_act.py), which also writes this step's observation rows; one HIP
+            # kernel samples a = mu + std * eps and writes actions, mu, sigma and the Normal
             # log-prob straight into this step's storage rows (lgx_act_head)
             s, k = self.storage, self.storage.step
             fused = self._fused_act(adaptation_mode)
+            if fused is None:
+                slots = self.storage.record_observations(obs, privileged_obs, critic_obs, true_estimated_obs,
+                                                         scan_obs)
+            else:
+                if k >= s.num_transitions_per_env:
+                    raise AssertionError("Rollout buffer overflow")
+                slots = self.storage.observation_slots()
+            (t.observations, t.privileged_observations, t.critic_observations, t.true_estimated_observations,
+             t.scan_observations) = slots
             with torch.no_grad():
                 if fused is not None:
-                    # every act network in one launch (s8_act.py); its S8 weights are refreshed
-                    # at the rollout's first step (the update changed them)
+                    # its S8 weights are refreshed at the rollout's first step (the update changed them)
                     if k == 0:
                         fused.refresh_weights()
-                    mean, t.values = fused.run(obs, privileged_obs, critic_obs, scan_obs)
+                    mean, t.values = fused.run(obs, privileged_obs, critic_obs, scan_obs, est=true_estimated_obs,
+                                               rows=slots)
                 else:
                     items = [self.estimator.group_item(obs), ac.scan_encoder.group_item(scan_obs)]
                     if not adaptation_mode:

@@ -5,8 +5,9 @@ The rollout step's estimator, scan encoder, privileged encoder, actor and critic
 kernel over S8 copies of their weights (the update's operand format, s8_update.py): 32 envs per
 block, the activations in LDS, the actor input assembled in place as [obs | priv latent | scan
 latent | est] in the update's segmented layout. The weights are split once per rollout (at its
-first step, inside the rollout graph). The act head (sampling, log-prob, storage rows) stays
-`lgx_act_head`. Adaptation-mode rollouts (the DAgger iterations: the latent from the adaptation
+first step, inside the rollout graph). The kernel also writes this step's observation rows of
+the storage (rollout_storage.py:87-105; no separate copy launch). The act head (sampling,
+log-prob, action rows) stays `lgx_act_head`. Adaptation-mode rollouts (the DAgger iterations: the latent from the adaptation
 encoder) keep the grouped launches.
 
 Numerics: the same 3 x bf16 products as the grouped launches; the actor's first layer sums its
@@ -104,15 +105,26 @@ class S8Act:
         """The weights -> S8 (one launch; the rollout's first step, after the update changed them)."""
         S.split(self.wsplit)
 
-    def run(self, obs, priv, critic, scan):
-        """(mu [B, A], value [B, 1]) of this step's observations (static output buffers)."""
+    def run(self, obs, priv, critic, scan, est=None, rows=None):
+        """(mu [B, A], value [B, 1]) of this step's observations (static output buffers).
+        rows (optional): this step's storage rows [obs, priv, critic, est, scan] (contiguous),
+        which the kernel fills from the inputs (est: the true estimated obs, copied only)."""
         a = self.args
-        for t in (obs, priv, critic, scan):
+        for t in (obs, priv, critic, scan) + (() if est is None else (est,)):
             if t.stride(1) != 1 or t.dtype != torch.float32 or t.shape[0] != self.B:
                 raise S.S8LibError("S8Act: fp32 [num_envs, cols] inputs with unit column stride")
         a.obs, a.ld_obs, a.n_obs = obs.data_ptr(), obs.stride(0), obs.shape[1]
         a.priv_obs, a.ld_priv, a.n_priv_in = priv.data_ptr(), priv.stride(0), priv.shape[1]
         a.critic_obs, a.ld_critic, a.n_critic_in = critic.data_ptr(), critic.stride(0), critic.shape[1]
         a.scan_obs, a.ld_scan, a.n_scan_in = scan.data_ptr(), scan.stride(0), scan.shape[1]
+        if rows is not None:
+            src = (obs, priv, critic, est, scan)
+            for d, x in zip(rows, src):
+                if not d.is_contiguous() or d.shape != x.shape:
+                    raise S.S8LibError("S8Act: storage rows must be contiguous and shaped as the inputs")
+            a.obs_st, a.priv_st, a.critic_st, a.est_st, a.scan_st = (d.data_ptr() for d in rows)
+            a.est_obs, a.ld_est, a.n_est_obs = est.data_ptr(), est.stride(0), est.shape[1]
+        else:
+            a.obs_st = a.priv_st = a.critic_st = a.est_st = a.scan_st = a.est_obs = None
         S.act(a)
         return self.mu, self.value

@@ -56,7 +56,9 @@ class ActArgs(C.Structure):
                 ("critic_obs", vp), ("ld_critic", i64), ("n_critic_in", i32), ("est_c0", i32), ("seg", i32 * 4),
                 ("est", ActLayer * 6), ("scan", ActLayer * 6), ("priv", ActLayer * 6), ("actor", ActLayer * 6),
                 ("critic", ActLayer * 6), ("n_est", i32), ("n_scan", i32), ("n_priv", i32), ("n_actor", i32),
-                ("n_critic", i32), ("mu", vp), ("ld_mu", i64), ("value", vp)]
+                ("n_critic", i32), ("mu", vp), ("ld_mu", i64), ("value", vp), ("obs_st", vp), ("priv_st", vp),
+                ("scan_st", vp), ("critic_st", vp), ("est_st", vp), ("est_obs", vp), ("ld_est", i64),
+                ("n_est_obs", i32), ("pad1", i32)]
 
 
 def flat_reduce(ws, stride, out, n, nsplit, accumulate=0):

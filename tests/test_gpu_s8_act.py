@@ -2,7 +2,7 @@
 the grouped launches (PPO.use_fused_act False), same parameters and injected noise, over a
 24-step rollout of every learner case: actions, mu, sigma, log-probs and values in the storage
 (fp32: the same 3 x bf16 products; the actor's first layer sums its segmented input in a
-different order, so rtol 1e-5). Plus: the weights are refreshed at each rollout's first step
+different order, so rtol 1e-5), and the observation rows it writes (bit for bit). Plus: the weights are refreshed at each rollout's first step
 (after an update the fused path follows the new weights), and the ABI rejects bad layouts."""
 import pytest
 import torch
@@ -13,6 +13,8 @@ import learner_replay as R
 pytestmark = pytest.mark.gpu
 dev = "cuda:0"
 FIELDS = ("actions", "mu", "sigma", "actions_log_prob", "values")
+OBS_FIELDS = ("observations", "privileged_observations", "critic_observations", "true_estimated_observations",
+              "scan_observations")
 
 
 def _rollout(case, fused, which=1):
@@ -20,7 +22,7 @@ def _rollout(case, fused, which=1):
     alg.use_fused_act = fused
     R.rollout(alg, case, which, {}, False, dev)
     assert (alg._s8act is not None) == fused
-    return alg, {f: getattr(alg.storage, f).clone() for f in FIELDS}
+    return alg, {f: getattr(alg.storage, f).clone() for f in FIELDS + OBS_FIELDS}
 
 
 @pytest.mark.parametrize("case", list(LC.CASES))
@@ -29,6 +31,8 @@ def test_fused_act_matches_grouped_launches(case):
     _b, got = _rollout(case, True)
     for f in FIELDS:
         torch.testing.assert_close(got[f], ref[f], rtol=1e-5, atol=1e-6, msg=f"{case}.{f}")
+    for f in OBS_FIELDS:  # the storage's observation rows: written by the fused kernel, copies
+        assert torch.equal(got[f], ref[f]), f"{case}.{f}"
 
 
 def test_fused_act_refreshes_weights_each_rollout():
