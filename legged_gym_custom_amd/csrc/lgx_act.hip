@@ -85,8 +85,11 @@ struct Dst {  // a layer output: global rows (g, ld) or an LDS image
   int off;
 };
 
-// One layer for the block's 32 rows. TPW = 16-column tiles per wave (N <= 64 TPW).
-template <int TPW>
+// One layer for the block's 32 rows. TPW = 16-column tiles per wave (N <= 64 TPW); GIN: the
+// input is global rows (else an LDS image). The K loop has no branches around its loads (steps
+// past the last one read clamped addresses and multiply zeros), so hipcc counts the loads in
+// flight instead of draining them every step.
+template <int TPW, bool GIN>
 __device__ __forceinline__ void layer(const lgx_s8_act_layer& L, const Src& in, const Dst& out, int rows) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, c = lane & 15;
@@ -105,7 +108,6 @@ __device__ __forceinline__ void layer(const lgx_s8_act_layer& L, const Src& in, 
     wrow[j] = (int64_t)std::min(16 * t + c, N - 1) * ldw + g * 32;
   }
   // a global input: this lane's two rows (row tiles 0, 1), clamped into the block
-  const bool gin = in.g != nullptr;
   const GAS float* arow[2];
 #pragma unroll
   for (int rt = 0; rt < 2; ++rt)
@@ -126,7 +128,7 @@ __device__ __forceinline__ void layer(const lgx_s8_act_layer& L, const Src& in, 
       S.h[j] = *(const GAS u32x4*)q;
       S.l[j] = *(const GAS u32x4*)(q + 16);
     }
-    if (gin) {
+    if constexpr (GIN) {
       const int k0 = sc * 32 + 8 * g;
 #pragma unroll
       for (int rt = 0; rt < 2; ++rt)
@@ -146,11 +148,12 @@ __device__ __forceinline__ void layer(const lgx_s8_act_layer& L, const Src& in, 
 #pragma unroll
     for (int rt = 0; rt < 2; ++rt) {
       float v[8];
-      if (gin) {
+      if constexpr (GIN) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] = S.a[rt][e];
       } else {
-        const float* q = act_lds + in.off + (16 * rt + c) * (int)in.ld + k0;
+        const int kc = std::min(s, ns - 1) * 32 + 8 * g;  // in the image (zeroed below past K)
+        const float* q = act_lds + in.off + (16 * rt + c) * (int)in.ld + kc;
         const f32x4 x = *reinterpret_cast<const f32x4*>(q), y = *reinterpret_cast<const f32x4*>(q + 4);
         v[0] = x[0]; v[1] = x[1]; v[2] = x[2]; v[3] = x[3]; v[4] = y[0]; v[5] = y[1]; v[6] = y[2]; v[7] = y[3];
       }
@@ -158,32 +161,32 @@ __device__ __forceinline__ void layer(const lgx_s8_act_layer& L, const Src& in, 
       for (int e = 0; e < 8; ++e) v[e] = k0 + e < K ? v[e] : 0.f;
       split8(v, ah[rt], al[rt]);
     }
+    // the three products of every tile in turn (lo*hi, hi*lo, hi*hi: each accumulator's chain
+    // in lgx_s8.hip's order), so dependent MFMAs are 2 TPW instructions apart
 #pragma unroll
-    for (int j = 0; j < TPW; ++j) {
-      if (!tv[j]) continue;
-      const bf16x8 bh = __builtin_bit_cast(bf16x8, S.h[j]), bl = __builtin_bit_cast(bf16x8, S.l[j]);
+    for (int pr = 0; pr < 3; ++pr)
 #pragma unroll
-      for (int rt = 0; rt < 2; ++rt) {
-        acc[rt][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[rt], bh, acc[rt][j], 0, 0, 0);
-        acc[rt][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[rt], bl, acc[rt][j], 0, 0, 0);
-        acc[rt][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[rt], bh, acc[rt][j], 0, 0, 0);
+      for (int j = 0; j < TPW; ++j) {
+        if (!tv[j]) continue;
+        const bf16x8 bh = __builtin_bit_cast(bf16x8, S.h[j]), bl = __builtin_bit_cast(bf16x8, S.l[j]);
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt) {
+          const bf16x8 x = pr == 0 ? al[rt] : ah[rt], y = pr == 1 ? bl : bh;
+          acc[rt][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x, y, acc[rt][j], 0, 0, 0);
+        }
       }
-    }
   };
 
   load(s0, 0);
   load(s1, 1);
-  for (int s = 0; s < ns; s += 3) {
+  const int nsp = (ns + 2) / 3 * 3;  // steps past ns multiply zeros (A is zero for k >= K)
+  for (int s = 0; s < nsp; s += 3) {
     load(s2, s + 2);
     step(s0, s);
-    if (s + 1 < ns) {
-      load(s0, s + 3);
-      step(s1, s + 1);
-    }
-    if (s + 2 < ns) {
-      load(s1, s + 4);
-      step(s2, s + 2);
-    }
+    load(s0, s + 3);
+    step(s1, s + 1);
+    load(s1, s + 4);
+    step(s2, s + 2);
   }
 
   // epilogue: bias (+ ELU); MFMA C map: col = lane & 15, row = 4 (lane >> 4) + r
@@ -299,11 +302,18 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     Src in;
     Dst out;
     job(a, critic, i, r0, L, in, out);
-    const int nt = (L.N + 15) / 16;  // one call site per width class
-    if (nt > 16) layer<8>(L, in, out, rows);
-    else if (nt > 8) layer<4>(L, in, out, rows);
-    else if (nt > 4) layer<2>(L, in, out, rows);
-    else layer<1>(L, in, out, rows);
+    const int nt = (L.N + 15) / 16;  // one call site per width class and input kind
+    if (in.g) {
+      if (nt > 16) layer<8, true>(L, in, out, rows);
+      else if (nt > 8) layer<4, true>(L, in, out, rows);
+      else if (nt > 4) layer<2, true>(L, in, out, rows);
+      else layer<1, true>(L, in, out, rows);
+    } else {
+      if (nt > 16) layer<8, false>(L, in, out, rows);
+      else if (nt > 8) layer<4, false>(L, in, out, rows);
+      else if (nt > 4) layer<2, false>(L, in, out, rows);
+      else layer<1, false>(L, in, out, rows);
+    }
   }
 }
 

@@ -12,7 +12,7 @@ encoder) keep the grouped launches.
 
 Numerics: the same 3 x bf16 products as the grouped launches; the actor's first layer sums its
 input in the segmented order (the gaps are zeros), so mu differs from the grouped path by fp32
-rounding only (tests/test_gpu_s8_act.py: rtol 1e-5)."""
+rounding only (tests/test_gpu_s8_act.py: within 1e-5)."""
 import torch
 
 from legged_gym_custom_amd.rsl_rl.modules import hip_s8 as S
