@@ -213,6 +213,35 @@ __device__ __forceinline__ void layer(const lgx_s8_act_layer& L, const Src& in, 
   __syncthreads();
 }
 
+// rows [r0, r0 + rows) x n columns of src (row stride ld) into the LDS image (lds_off >= 0,
+// pitch lds_ld) and / or a contiguous global [.., n] destination: 8 rows x 3 x 256 columns of
+// loads in flight per pass (a load per row and column loop would pay a round trip each)
+__device__ __forceinline__ void copy_rows(const float* src, int64_t ld, int n, int r0, int rows, int lds_off, int lds_ld,
+                                          float* st) {
+  const int tid = threadIdx.x;
+  for (int c0 = 0; c0 < n; c0 += 3 * NT)
+    for (int r = 0; r < rows; r += 8) {
+      float v[8][3];
+#pragma unroll
+      for (int rr = 0; rr < 8; ++rr)
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          const int k = c0 + tid + NT * q;
+          v[rr][q] = r + rr < rows && k < n ? src[(int64_t)(r0 + r + rr) * ld + k] : 0.f;
+        }
+#pragma unroll
+      for (int rr = 0; rr < 8; ++rr)
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          const int k = c0 + tid + NT * q;
+          if (r + rr < rows && k < n) {
+            if (lds_off >= 0) act_lds[lds_off + (r + rr) * lds_ld + k] = v[rr][q];
+            if (st) st[(int64_t)(r0 + r + rr) * n + k] = v[rr][q];
+          }
+        }
+    }
+}
+
 // Layer i of this block's chain sequence — critic blocks: the critic; actor blocks: estimator,
 // scan encoder, privileged encoder, actor — with its input and output (LDS images: X the actor
 // input [R][XP], Y the hidden layers [R][YP] or two encoder scratch images [R][SP])
@@ -270,30 +299,17 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   if (rb >= nrb) return;
   const int r0 = rb * R, rows = std::min(R, a.B - r0);
   const int tid = threadIdx.x;
-  // this step's storage rows (optional): a contiguous [rows, n] copy of an input
-  auto store_rows = [&](float* dst, const float* src, int64_t ld, int n) {
-    if (!dst) return;
-    for (int r = 0; r < rows; ++r)
-      for (int k = tid; k < n; k += NT) dst[(int64_t)(r0 + r) * n + k] = src[(int64_t)(r0 + r) * ld + k];
-  };
+  // this step's storage rows (optional): contiguous [rows, n] copies of the inputs
   if (critic) {
-    store_rows(a.critic_st, a.critic_obs, a.ld_critic, a.n_critic_in);
+    if (a.critic_st) copy_rows(a.critic_obs, a.ld_critic, a.n_critic_in, r0, rows, -1, 0, a.critic_st);
   } else {
     // the actor-input image: zero (its gaps between parts stay zero), then obs (and its row)
     for (int i = tid; i < XF; i += NT) act_lds[i] = 0.f;
     __syncthreads();
-    for (int r = 0; r < rows; ++r) {
-      const float* src = a.obs + (int64_t)(r0 + r) * a.ld_obs;
-      float* st = a.obs_st ? a.obs_st + (int64_t)(r0 + r) * a.n_obs : nullptr;
-      for (int k = tid; k < a.n_obs; k += NT) {
-        const float v = src[k];
-        act_lds[r * XP + a.seg[0] + k] = v;
-        if (st) st[k] = v;
-      }
-    }
-    store_rows(a.priv_st, a.priv_obs, a.ld_priv, a.n_priv_in);
-    store_rows(a.scan_st, a.scan_obs, a.ld_scan, a.n_scan_in);
-    store_rows(a.est_st, a.est_obs, a.ld_est, a.n_est_obs);
+    copy_rows(a.obs, a.ld_obs, a.n_obs, r0, rows, a.seg[0], XP, a.obs_st);
+    if (a.priv_st) copy_rows(a.priv_obs, a.ld_priv, a.n_priv_in, r0, rows, -1, 0, a.priv_st);
+    if (a.scan_st) copy_rows(a.scan_obs, a.ld_scan, a.n_scan_in, r0, rows, -1, 0, a.scan_st);
+    if (a.est_st) copy_rows(a.est_obs, a.ld_est, a.n_est_obs, r0, rows, -1, 0, a.est_st);
     __syncthreads();
   }
   const int njobs = critic ? a.n_critic : a.n_est + a.n_scan + a.n_priv + a.n_actor;
