@@ -103,7 +103,7 @@ int32_t lgx_s8_reduce(const lgx_s8_reduce_args* args, int32_t n, void* stream);
 /* ---- ABI v2: the rollout's act networks in ONE launch (PPO.act, ppo.py:129-153): the
  * estimator, scan encoder and privileged encoder, the actor on [obs | priv latent | scan latent
  * | est] (actor_critic.py:79-107) and the critic (:110-115), [Linear, ELU]* Linear chains whose
- * weights are S8 ([N rows][ldw], ldw >= round_up(K, 32), pad zero) and biases fp32. The actor
+ * weights are in the act-packed S8 format written by lgx_s8_act_pack and biases fp32. The actor
  * input is the S8 update's segmented layout: part p starts at column seg[p] (seg[0] = 0, a
  * multiple of 4 each, zero gaps), width = its K (a multiple of 32); the actor's first-layer
  * weights use the same layout. Writes mu [B, A] (row stride ld_mu) and value [B]. 32 rows per
@@ -115,7 +115,7 @@ int32_t lgx_s8_reduce(const lgx_s8_reduce_args* args, int32_t n, void* stream);
 #define LGX_S8_ACT_MAXENC 256
 #define LGX_S8_ACT_MAXL 6
 typedef struct lgx_s8_act_layer {
-  const void* W; int64_t ldw;   /* S8 weight rows (output columns), pitch in elements */
+  const void* W; int64_t ldw;   /* act-packed weights; ldw = K steps per tile (ceil(K / 32)) */
   const float* b;
   int32_t K, N, elu, pad0;
 } lgx_s8_act_layer;
@@ -139,8 +139,25 @@ typedef struct lgx_s8_act_args {
   const float* est_obs; int64_t ld_est; int32_t n_est_obs, pad1;
 } lgx_s8_act_args;
 int32_t lgx_s8_act(const lgx_s8_act_args* args, void* stream);
+/* The act-packed format: for each 16-row output tile t and 32-deep K step s, one 2 KB block
+ * [hi: 64 lanes x 16 B][lo: 64 lanes x 16 B] where lane (c, g) = (lane & 15, lane >> 4) holds
+ * the bf16 hi (lo = bf16(x - hi)) of W[16 t + c][32 s + 8 g .. + 7] — exactly the MFMA B
+ * fragment, so a wave loads it as 1 KB contiguous (whole cache lines); block (t, s) at byte
+ * ((t * steps + s) * 2048). Rows >= N and columns outside the spans are zero. Spans place
+ * logical input columns at packed columns (the actor's first layer: [obs | priv latent | scan
+ * latent | est] at seg[]); one span (0, 0, K) otherwise. One launch packs up to
+ * LGX_S8_BATCH_MAX layers (the rollout's first step: the update changed the weights). */
+typedef struct lgx_s8_act_pack_args {
+  const float* W; int64_t ld;   /* fp32 [N][ld] (nn.Linear.weight) */
+  void* dst;                    /* >= ceil(N / 16) * steps * 2048 bytes */
+  int32_t N, steps;             /* steps = ceil(packed K / 32) */
+  int32_t nspans;               /* 1..4 */
+  int32_t span_c0[4], span_p0[4], span_w[4];  /* logical column, packed column, width */
+} lgx_s8_act_pack_args;
+int32_t lgx_s8_act_pack(const lgx_s8_act_pack_args* args, int32_t n, void* stream);
 const char* lgx_s8_act_last_error(void);
 int32_t lgx_s8_sizeof_act_args(void);
+int32_t lgx_s8_sizeof_act_pack_args(void);
 
 #ifdef __cplusplus
 }

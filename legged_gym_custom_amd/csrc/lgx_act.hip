@@ -12,13 +12,14 @@
 //
 // A layer: out[32, N] = act(in[32, K] W^T + b), 3 x bf16 MFMAs (lo*hi + hi*lo + hi*hi, fp32
 // accumulation; lgx_s8.hip's order) per 16 x 16 x 32 tile. Wave w owns the 16-column tiles
-// w, w + 4, ...; each K step's weight fragments (hi 16 B + lo 16 B per lane, straight from the
-// S8 rows) are loaded two steps ahead into registers — with 32 rows per block the weights are
-// the streamed operand (each block reads all of its network's weights once), so this is the
-// weight-streaming pattern of a small-M GEMM, not a staged tile. The activation fragments are
-// read from LDS (or, for a first layer, from the input rows in global memory) and split into
-// hi / lo in registers; columns k >= K are zeroed by select (the S8 weights' pad columns are
-// zero too).
+// w, w + 4, ...; each K step's weight fragments are loaded two steps ahead into registers — with
+// 32 rows per block the weights are the streamed operand (each block reads all of its network's
+// weights once): the weight-streaming pattern of a small-M GEMM, not a staged tile. The weights
+// are act-packed (lgx_s8_act_pack): a fragment is 1 KB contiguous, so each load instruction
+// fetches 8 whole cache lines (row-major S8 rows would cost 16 half-used lines per instruction,
+// twice: measured 2.4 us per 512-wide K step, L1-miss bound). The activation fragments are read
+// from LDS (the critic's first layer: from the input rows, 32 B per lane) and split into hi / lo
+// in registers; columns k >= K are zeroed by select (the packed pad columns are zero too).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -96,16 +97,16 @@ __device__ __forceinline__ void layer(const lgx_s8_act_layer& L, const Src& in, 
   const int K = L.K, N = L.N;
   const int ns = (K + 31) / 32;
   const int nt = (N + 15) / 16;
-  const GAS char* W = (const GAS char*)L.W;
-  const int64_t ldw = L.ldw * 4;  // bytes
-  // this lane's weight row (output column) per tile; tiles past N re-read the last row
-  int64_t wrow[TPW];
+  const GAS char* W = (const GAS char*)L.W + lane * 16;
+  const int steps = (int)L.ldw;  // packed K steps per tile
+  // this wave's tiles' packed blocks; tiles past N re-read the last tile (discarded)
+  int64_t wtile[TPW];
   bool tv[TPW];
 #pragma unroll
   for (int j = 0; j < TPW; ++j) {
     const int t = wave + 4 * j;
     tv[j] = t < nt;
-    wrow[j] = (int64_t)std::min(16 * t + c, N - 1) * ldw + g * 32;
+    wtile[j] = (int64_t)std::min(t, nt - 1) * steps * 2048;
   }
   // a global input: this lane's two rows (row tiles 0, 1), clamped into the block
   const GAS float* arow[2];
@@ -121,19 +122,21 @@ __device__ __forceinline__ void layer(const lgx_s8_act_layer& L, const Src& in, 
   // weights (and a global input) two steps ahead, three register sets in rotation
   auto load = [&](Set& S, int s) {
     const int sc = std::min(s, ns - 1);
-    const int64_t ko = (int64_t)sc * 128;  // 32 k x 4 B per step
+    const int64_t ko = (int64_t)sc * 2048;
 #pragma unroll
     for (int j = 0; j < TPW; ++j) {
-      const GAS char* q = W + wrow[j] + ko;
+      const GAS char* q = W + wtile[j] + ko;
       S.h[j] = *(const GAS u32x4*)q;
-      S.l[j] = *(const GAS u32x4*)(q + 16);
+      S.l[j] = *(const GAS u32x4*)(q + 1024);
     }
-    if constexpr (GIN) {
+    if constexpr (GIN) {  // K % 32 == 0 and 16-B aligned rows (host-checked): 32 B per lane
       const int k0 = sc * 32 + 8 * g;
 #pragma unroll
-      for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) S.a[rt][e] = arow[rt][std::min(k0 + e, K - 1)];
+      for (int rt = 0; rt < 2; ++rt) {
+        const f32x4 x = *(const GAS f32x4*)(arow[rt] + k0), y = *(const GAS f32x4*)(arow[rt] + k0 + 4);
+        S.a[rt][0] = x[0]; S.a[rt][1] = x[1]; S.a[rt][2] = x[2]; S.a[rt][3] = x[3];
+        S.a[rt][4] = y[0]; S.a[rt][5] = y[1]; S.a[rt][6] = y[2]; S.a[rt][7] = y[3];
+      }
     }
   };
   f32x4 acc[2][TPW];
@@ -268,13 +271,13 @@ __device__ __forceinline__ void job(const lgx_s8_act_args& a, bool critic, int i
     ch = a.est; n = a.n_est; p = i;
     first = Src{nullptr, XP, X + a.seg[0] + a.est_c0};
     last = Dst{nullptr, XP, X + a.seg[3]};
-  } else if (i < a.n_est + a.n_scan) {
+  } else if (i < a.n_est + a.n_scan) {  // its input staged in S2 (act_kernel)
     ch = a.scan; n = a.n_scan; p = i - a.n_est;
-    first = Src{a.scan_obs + (int64_t)r0 * a.ld_scan, a.ld_scan, 0};
+    first = Src{nullptr, SP, S2};
     last = Dst{nullptr, XP, X + a.seg[2]};
   } else if (i < a.n_est + a.n_scan + a.n_priv) {
     ch = a.priv; n = a.n_priv; p = i - a.n_est - a.n_scan;
-    first = Src{a.priv_obs + (int64_t)r0 * a.ld_priv, a.ld_priv, 0};
+    first = Src{nullptr, SP, S2};
     last = Dst{nullptr, XP, X + a.seg[1]};
   } else {
     p = i - a.n_est - a.n_scan - a.n_priv;
@@ -318,6 +321,13 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     Src in;
     Dst out;
     job(a, critic, i, r0, L, in, out);
+    if (!critic && (i == a.n_est || i == a.n_est + a.n_scan)) {
+      // the scan / privileged encoder's input rows into S2 (free between chains)
+      const bool sc = i == a.n_est;
+      copy_rows(sc ? a.scan_obs : a.priv_obs, sc ? a.ld_scan : a.ld_priv, sc ? a.n_scan_in : a.n_priv_in, r0, rows,
+                XF + R * SP, SP, nullptr);
+      __syncthreads();
+    }
     const int nt = (L.N + 15) / 16;  // one call site per width class and input kind
     if (in.g) {
       if (nt > 16) layer<8, true>(L, in, out, rows);
@@ -333,6 +343,40 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   }
 }
 
+// the act-packed weights: thread = one (tile, step, lane) fragment (hi and lo, 32 B)
+struct PackBatch {
+  int n;
+  int64_t start[LGX_S8_BATCH_MAX + 1];  // prefix sums of fragments
+  lgx_s8_act_pack_args j[LGX_S8_BATCH_MAX];
+};
+
+__global__ __launch_bounds__(256) void pack_kernel(PackBatch b) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= b.start[b.n]) return;
+  int ji = 0;
+  while (ji + 1 < b.n && i >= b.start[ji + 1]) ++ji;
+  const lgx_s8_act_pack_args& J = b.j[ji];
+  const int64_t f = i - b.start[ji];
+  const int lane = (int)(f & 63);
+  const int64_t ts = f >> 6;  // t * steps + s
+  const int t = (int)(ts / J.steps), s = (int)(ts - (int64_t)t * J.steps);
+  const int n = 16 * t + (lane & 15), k0 = 32 * s + 8 * (lane >> 4);
+  float v[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int k = k0 + e;
+    float x = 0.f;
+    for (int q = 0; q < J.nspans; ++q)
+      if (n < J.N && k >= J.span_p0[q] && k < J.span_p0[q] + J.span_w[q]) x = J.W[(int64_t)n * J.ld + J.span_c0[q] + (k - J.span_p0[q])];
+    v[e] = x;
+  }
+  bf16x8 hi, lo;
+  split8(v, hi, lo);
+  char* d = static_cast<char*>(J.dst) + ts * 2048 + lane * 16;
+  *reinterpret_cast<bf16x8*>(d) = hi;
+  *reinterpret_cast<bf16x8*>(d + 1024) = lo;
+}
+
 }  // namespace lgxa
 
 static thread_local char a_err[256] = "";
@@ -345,7 +389,7 @@ static int check_chain(const lgx_s8_act_layer* L, int n, int k_in, int maxh, con
   if (n < 1 || n > LGX_S8_ACT_MAXL) return afail(what);
   int k = k_in;
   for (int i = 0; i < n; ++i) {
-    if (!L[i].W || !L[i].b || L[i].K != k || L[i].N < 1 || L[i].ldw % 8 || L[i].ldw < (L[i].K + 31) / 32 * 32 ||
+    if (!L[i].W || !L[i].b || L[i].K != k || L[i].N < 1 || L[i].ldw != (L[i].K + 31) / 32 ||
         (((uintptr_t)L[i].W) & 15))
       return afail(what);
     if (i < n - 1 && L[i].N > maxh) return afail(what);
@@ -358,6 +402,36 @@ extern "C" {
 
 const char* lgx_s8_act_last_error(void) { return a_err; }
 int32_t lgx_s8_sizeof_act_args(void) { return (int32_t)sizeof(lgx_s8_act_args); }
+int32_t lgx_s8_sizeof_act_pack_args(void) { return (int32_t)sizeof(lgx_s8_act_pack_args); }
+
+int32_t lgx_s8_act_pack(const lgx_s8_act_pack_args* args, int32_t n, void* stream) {
+  if (n < 0 || n > LGX_S8_BATCH_MAX || (n && !args)) return afail("lgx_s8_act_pack: 0 <= n <= LGX_S8_BATCH_MAX");
+  lgxa::PackBatch b;
+  memset(&b, 0, sizeof b);
+  int k = 0;
+  for (int i = 0; i < n; ++i) {
+    const lgx_s8_act_pack_args& q = args[i];
+    if (!q.W || !q.dst || q.N < 1 || q.steps < 1 || q.nspans < 1 || q.nspans > 4 || (((uintptr_t)q.dst) & 15))
+      return afail("lgx_s8_act_pack: bad layer");
+    for (int s = 0; s < q.nspans; ++s)
+      if (q.span_w[s] < 0 || q.span_p0[s] < 0 || q.span_p0[s] + q.span_w[s] > 32 * q.steps || q.span_c0[s] < 0 ||
+          q.span_c0[s] + q.span_w[s] > q.ld)
+        return afail("lgx_s8_act_pack: span outside the layer");
+    b.j[k] = q;
+    b.start[k + 1] = b.start[k] + (int64_t)((q.N + 15) / 16) * q.steps * 64;
+    ++k;
+  }
+  b.n = k;
+  if (!k) return 0;
+  hipLaunchKernelGGL(lgxa::pack_kernel, dim3((unsigned)((b.start[k] + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     b);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    snprintf(a_err, sizeof a_err, "lgx_s8_act_pack: %s", hipGetErrorString(e));
+    return -2;
+  }
+  return 0;
+}
 
 int32_t lgx_s8_act(const lgx_s8_act_args* a, void* stream) {
   if (!a || a->B < 0) return afail("lgx_s8_act: bad arguments");
@@ -376,6 +450,10 @@ int32_t lgx_s8_act(const lgx_s8_act_args* a, void* stream) {
     return -1;
   if (a->est_st && (!a->est_obs || a->n_est_obs < 1 || a->ld_est < a->n_est_obs))
     return afail("lgx_s8_act: est storage row without its source");
+  if (a->n_critic_in % 32 || a->ld_critic % 4 || (((uintptr_t)a->critic_obs) & 15))
+    return afail("lgx_s8_act: critic input: width a multiple of 32, 16-B aligned rows");
+  if (a->n_scan_in > LGX_S8_ACT_MAXENC || a->n_priv_in > LGX_S8_ACT_MAXENC)
+    return afail("lgx_s8_act: scan / privileged inputs wider than LGX_S8_ACT_MAXENC");
   if (a->est_c0 + a->est->K > a->n_obs || a->scan->K != a->n_scan_in || a->priv->K != a->n_priv_in ||
       a->critic->K != a->n_critic_in)
     return afail("lgx_s8_act: first-layer widths do not match the inputs");

@@ -2,9 +2,9 @@
 actor_critic.py:79-115 / 190-226, support_networks.py:25-80).
 
 The rollout step's estimator, scan encoder, privileged encoder, actor and critic run as one
-kernel over S8 copies of their weights (the update's operand format, s8_update.py): 32 envs per
-block, the activations in LDS, the actor input assembled in place as [obs | priv latent | scan
-latent | est] in the update's segmented layout. The weights are split once per rollout (at its
+kernel over S8 copies of their weights (bf16 hi / lo, packed as MFMA fragments: lgx_s8_act_pack):
+32 envs per block, the activations in LDS, the actor input assembled in place as [obs | priv latent | scan
+latent | est] in the update's segmented layout. The weights are packed once per rollout (at its
 first step, inside the rollout graph). The kernel also writes this step's observation rows of
 the storage (rollout_storage.py:87-105; no separate copy launch). The act head (sampling,
 log-prob, action rows) stays `lgx_act_head`. Adaptation-mode rollouts (the DAgger iterations: the latent from the adaptation
@@ -50,7 +50,8 @@ class S8Act:
         if any(m.out_features > S.ACT_MAXENC for c in (priv, scan, estc) for m in c[:-1]):
             return False
         c0 = 0 if est.use_history else nobs - ac.num_proprio
-        return c0 % 4 == 0 and critic[-1].out_features == 1
+        return (c0 % 4 == 0 and critic[-1].out_features == 1 and critic[0].in_features % 32 == 0
+                and scan[0].in_features <= S.ACT_MAXENC and priv[0].in_features <= S.ACT_MAXENC)
 
     def __init__(self, alg, num_envs):
         ac, est = alg.actor_critic, alg.estimator
@@ -68,8 +69,8 @@ class S8Act:
         spans = [(0, 0, nobs), (nobs, P0, nlat), (nobs + nlat, P1, nscan), (nobs + nlat + nscan, P2, nest)]
         self.nobs, self.width = nobs, width
         self.est_c0 = 0 if est.use_history else nobs - ac.num_proprio
-        self._keep = []  # S8 weight buffers (their addresses are in the argument block)
-        self.wsplit = []
+        self._keep = []  # packed weight buffers (their addresses are in the argument block)
+        self.wpack = []
         a = S.ActArgs()
         a.B, a.width = num_envs, width
         a.seg[0], a.seg[1], a.seg[2], a.seg[3] = 0, P0, P1, P2
@@ -78,17 +79,18 @@ class S8Act:
         def fill(dst, layers, first_actor=False):
             for i, m in enumerate(layers):
                 W = m.weight.detach()
+                N, K = W.shape
+                sp = spans if first_actor and i == 0 else [(0, 0, K)]
                 if first_actor and i == 0:
-                    Ws = S.empty(W.shape[0], width, dev)
-                    for (c, s8, w) in spans:
-                        self.wsplit.append(S.split_job(W[:, c:c + w], S.group_ptr(Ws, s8), Ws.shape[1]))
                     K = width
-                else:
-                    Ws = S.empty(W.shape[0], W.shape[1], dev)
-                    self.wsplit.append(S.split_job(W, Ws.data_ptr(), Ws.shape[1]))
-                    K = W.shape[1]
-                self._keep.append(Ws)
-                dst[i] = S.ActLayer(W=Ws.data_ptr(), ldw=Ws.shape[1], b=m.bias.data_ptr(), K=K, N=W.shape[0],
+                steps = (K + 31) // 32
+                Wp = torch.zeros(((N + 15) // 16) * steps * 2048 // 4, dtype=torch.int32, device=dev)
+                j = S.ActPackArgs(W=W.data_ptr(), ld=W.stride(0), dst=Wp.data_ptr(), N=N, steps=steps, nspans=len(sp))
+                for q, (c, p0, w) in enumerate(sp):
+                    j.span_c0[q], j.span_p0[q], j.span_w[q] = c, p0, w
+                self.wpack.append(j)
+                self._keep.append(Wp)
+                dst[i] = S.ActLayer(W=Wp.data_ptr(), ldw=steps, b=m.bias.data_ptr(), K=K, N=N,
                                     elu=int(i < len(layers) - 1))
             return len(layers)
         a.n_est = fill(a.est, estc)
@@ -102,8 +104,9 @@ class S8Act:
         self.args = a
 
     def refresh_weights(self):
-        """The weights -> S8 (one launch; the rollout's first step, after the update changed them)."""
-        S.split(self.wsplit)
+        """The weights -> the kernel's packed S8 fragments (one launch; the rollout's first step,
+        after the update changed them)."""
+        S.act_pack(self.wpack)
 
     def run(self, obs, priv, critic, scan, est=None, rows=None):
         """(mu [B, A], value [B, 1]) of this step's observations (static output buffers).

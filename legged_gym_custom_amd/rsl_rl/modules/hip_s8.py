@@ -23,7 +23,7 @@ TILE_M = 128
 SPLIT_ROWS = 256
 EXPORTED = ("lgx_s8_abi_version", "lgx_s8_sizeof_gemm_args", "lgx_s8_last_error", "lgx_s8_gemm_group",
             "lgx_s8_pick_split", "lgx_s8_split", "lgx_s8_reduce", "lgx_s8_act", "lgx_s8_act_last_error",
-            "lgx_s8_sizeof_act_args")
+            "lgx_s8_sizeof_act_args", "lgx_s8_act_pack", "lgx_s8_sizeof_act_pack_args")
 ACT_ROWS, ACT_MAXIN, ACT_MAXH, ACT_MAXENC, ACT_MAXL = 32, 640, 512, 256, 6
 
 vp, i32, i64 = C.c_void_p, C.c_int32, C.c_int64
@@ -48,6 +48,11 @@ class ReduceArgs(C.Structure):
 
 class ActLayer(C.Structure):
     _fields_ = [("W", vp), ("ldw", i64), ("b", vp), ("K", i32), ("N", i32), ("elu", i32), ("pad0", i32)]
+
+
+class ActPackArgs(C.Structure):
+    _fields_ = [("W", vp), ("ld", i64), ("dst", vp), ("N", i32), ("steps", i32), ("nspans", i32),
+                ("span_c0", i32 * 4), ("span_p0", i32 * 4), ("span_w", i32 * 4)]
 
 
 class ActArgs(C.Structure):
@@ -90,11 +95,16 @@ def load(path=_LIB_PATH):
     L.lgx_s8_act.restype = i32
     L.lgx_s8_act_last_error.restype = C.c_char_p
     L.lgx_s8_sizeof_act_args.restype = i32
+    L.lgx_s8_act_pack.argtypes = [vp, i32, vp]
+    L.lgx_s8_act_pack.restype = i32
+    L.lgx_s8_sizeof_act_pack_args.restype = i32
     if L.lgx_s8_abi_version() != ABI_VERSION:
         raise S8LibError("liblgx_s8 ABI version mismatch; rebuild")
     if L.lgx_s8_sizeof_gemm_args() != C.sizeof(GemmArgs):
         raise S8LibError(f"lgx_s8_gemm_args layout mismatch: C {L.lgx_s8_sizeof_gemm_args()} vs ctypes "
                          f"{C.sizeof(GemmArgs)}")
+    if L.lgx_s8_sizeof_act_pack_args() != C.sizeof(ActPackArgs):
+        raise S8LibError("lgx_s8_act_pack_args layout mismatch")
     if L.lgx_s8_sizeof_act_args() != C.sizeof(ActArgs):
         raise S8LibError(f"lgx_s8_act_args layout mismatch: C {L.lgx_s8_sizeof_act_args()} vs ctypes "
                          f"{C.sizeof(ActArgs)}")
@@ -203,11 +213,21 @@ def reduce(jobs, L=None):
         _check(L.lgx_s8_reduce(arr, len(chunk), _stream()), "lgx_s8_reduce")
 
 
-def act(args):
+def act(args, L=None):
     """lgx_s8_act: the rollout's act networks in one launch (ActArgs)."""
-    L = lib()
+    L = lib() if L is None else L
     if L.lgx_s8_act(C.byref(args), _stream()) != 0:
         raise S8LibError("lgx_s8_act: " + L.lgx_s8_act_last_error().decode())
+
+
+def act_pack(jobs, L=None):
+    """lgx_s8_act_pack: fp32 weights -> the act kernel's packed S8 fragments ([ActPackArgs])."""
+    L = lib() if L is None else L
+    for i in range(0, len(jobs), BATCH_MAX):
+        chunk = jobs[i:i + BATCH_MAX]
+        arr = (ActPackArgs * len(chunk))(*chunk)
+        if L.lgx_s8_act_pack(arr, len(chunk), _stream()) != 0:
+            raise S8LibError("lgx_s8_act_pack: " + L.lgx_s8_act_last_error().decode())
 
 
 def split_job(src, dst_ptr, ld_dst, colsum_ws=None, idx=None, rows=None):
