@@ -2,7 +2,8 @@
 // PPO.act's estimator, scan encoder, privileged encoder, actor and critic (ppo.py:129-153,
 // actor_critic.py:79-107 / 190-226, support_networks.py:25-80) on S8 weights, gfx950.
 //
-// Block = 32 rows (envs) x 256 threads (4 waves); one block per CU (149 KB of LDS). Half of the
+// Block = 32 rows (envs) x 512 threads (8 waves, 2 per SIMD: 10 % faster than 4); one block
+// per CU (149 KB of LDS). Half of the
 // blocks ("actor blocks", on XCDs 0-3) run estimator -> scan encoder -> privileged encoder ->
 // actor for their rows, the other half ("critic blocks", XCDs 4-7) the critic, so each XCD's L2
 // holds one network's weights (≈2.4 MB). Activations stay in LDS (fp32, row pitch = 4 mod 64
@@ -12,7 +13,7 @@
 //
 // A layer: out[32, N] = act(in[32, K] W^T + b), 3 x bf16 MFMAs (lo*hi + hi*lo + hi*hi, fp32
 // accumulation; lgx_s8.hip's order) per 16 x 16 x 32 tile. Wave w owns the 16-column tiles
-// w, w + 4, ...; each K step's weight fragments are loaded two steps ahead into registers — with
+// w, w + 8, ...; each K step's weight fragments are loaded two steps ahead into registers — with
 // 32 rows per block the weights are the streamed operand (each block reads all of its network's
 // weights once): the weight-streaming pattern of a small-M GEMM, not a staged tile. The weights
 // are act-packed (lgx_s8_act_pack): a fragment is 1 KB contiguous, so each load instruction
@@ -38,7 +39,8 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
                                                // their pointer arguments are cast back to it
 
 constexpr int R = LGX_S8_ACT_ROWS;          // rows per block (32)
-constexpr int NT = 256;                      // threads per block
+constexpr int NT = 512;                      // threads per block: 8 waves, 2 per SIMD
+constexpr int NWV = NT / 64;
 constexpr int XP = LGX_S8_ACT_MAXIN + 4;     // actor-input image pitch (floats, = 4 mod 64)
 constexpr int YP = LGX_S8_ACT_MAXH + 4;      // hidden-layer image pitch
 constexpr int SP = LGX_S8_ACT_MAXENC + 4;    // encoder scratch pitch (two images inside Y)
@@ -86,7 +88,7 @@ struct Dst {  // a layer output: global rows (g, ld) or an LDS image
   int off;
 };
 
-// One layer for the block's 32 rows. TPW = 16-column tiles per wave (N <= 64 TPW); GIN: the
+// One layer for the block's 32 rows. TPW = 16-column tiles per wave (N <= 128 TPW); GIN: the
 // input is global rows (else an LDS image). The K loop has no branches around its loads (steps
 // past the last one read clamped addresses and multiply zeros), so hipcc counts the loads in
 // flight instead of draining them every step.
@@ -104,7 +106,7 @@ __device__ __forceinline__ void layer(const lgx_s8_act_layer& L, const Src& in, 
   bool tv[TPW];
 #pragma unroll
   for (int j = 0; j < TPW; ++j) {
-    const int t = wave + 4 * j;
+    const int t = wave + NWV * j;
     tv[j] = t < nt;
     wtile[j] = (int64_t)std::min(t, nt - 1) * steps * 2048;
   }
@@ -196,7 +198,7 @@ __device__ __forceinline__ void layer(const lgx_s8_act_layer& L, const Src& in, 
 #pragma unroll
   for (int j = 0; j < TPW; ++j) {
     if (!tv[j]) continue;
-    const int col = 16 * (wave + 4 * j) + c;
+    const int col = 16 * (wave + NWV * j) + c;
     if (col >= N) continue;
     const float bias = ((const GAS float*)L.b)[col];
 #pragma unroll
@@ -294,7 +296,22 @@ __device__ __forceinline__ void job(const lgx_s8_act_args& a, bool critic, int i
   out = p == n - 1 ? last : Dst{nullptr, SP, (p & 1) ? S2 : S1};
 }
 
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 1))) void act_kernel(lgx_s8_act_args a) {
+// Every layer of this block type's chains, loaded once by all of the type's blocks on this XCD
+// together (wave gw of 256 takes every 256th KB): the weights come back from HBM / the
+// Infinity Cache in one round trip at the start instead of at each of the 13 layer starts
+// (the env step in between evicts them from L2). The values are summed into `sink`, which the
+// caller keeps alive.
+__device__ __forceinline__ void warm_l2(const lgx_s8_act_layer* Ls, int n, int gw, float& sink) {
+  const int lane = threadIdx.x & 63;
+  for (int i = 0; i < n; ++i) {
+    const int64_t bytes = (int64_t)((Ls[i].N + 15) / 16) * Ls[i].ldw * 2048;
+    const GAS char* W = (const GAS char*)Ls[i].W;
+    for (int64_t off = (int64_t)gw * 1024 + lane * 16; off < bytes; off += 32 * NWV * 1024)
+      sink += *(const GAS float*)(W + off);
+  }
+}
+
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void act_kernel(lgx_s8_act_args a) {
   const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
   const bool critic = xcd >= 4;
   const int rb = slot * 4 + (xcd & 3);
@@ -302,6 +319,18 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   if (rb >= nrb) return;
   const int r0 = rb * R, rows = std::min(R, a.B - r0);
   const int tid = threadIdx.x;
+  float sink = 0.f;
+  {
+    const int gw = slot * NWV + (tid >> 6);  // this XCD's 32 blocks x 8 waves
+    if (critic) {
+      warm_l2(a.critic, a.n_critic, gw, sink);
+    } else {
+      warm_l2(a.est, a.n_est, gw, sink);
+      warm_l2(a.scan, a.n_scan, gw, sink);
+      warm_l2(a.priv, a.n_priv, gw, sink);
+      warm_l2(a.actor, a.n_actor, gw, sink);
+    }
+  }
   // this step's storage rows (optional): contiguous [rows, n] copies of the inputs
   if (critic) {
     if (a.critic_st) copy_rows(a.critic_obs, a.ld_critic, a.n_critic_in, r0, rows, -1, 0, a.critic_st);
@@ -330,17 +359,16 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     }
     const int nt = (L.N + 15) / 16;  // one call site per width class and input kind
     if (in.g) {
-      if (nt > 16) layer<8, true>(L, in, out, rows);
-      else if (nt > 8) layer<4, true>(L, in, out, rows);
-      else if (nt > 4) layer<2, true>(L, in, out, rows);
+      if (nt > 2 * NWV) layer<4, true>(L, in, out, rows);
+      else if (nt > NWV) layer<2, true>(L, in, out, rows);
       else layer<1, true>(L, in, out, rows);
     } else {
-      if (nt > 16) layer<8, false>(L, in, out, rows);
-      else if (nt > 8) layer<4, false>(L, in, out, rows);
-      else if (nt > 4) layer<2, false>(L, in, out, rows);
+      if (nt > 2 * NWV) layer<4, false>(L, in, out, rows);
+      else if (nt > NWV) layer<2, false>(L, in, out, rows);
       else layer<1, false>(L, in, out, rows);
     }
   }
+  if (sink == 1.2345e-38f && a.B < 0) a.value[0] = sink;  // keeps the warm-up loads (never true)
 }
 
 // the act-packed weights: thread = one (tile, step, lane) fragment (hi and lo, 32 B)
