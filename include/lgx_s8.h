@@ -137,6 +137,9 @@ typedef struct lgx_s8_act_args {
    * critic_obs and est_obs ([B, n_est_obs], read for this copy only) into them */
   float* obs_st; float* priv_st; float* scan_st; float* critic_st; float* est_st;
   const float* est_obs; int64_t ld_est; int32_t n_est_obs, pad1;
+  /* n_est = n_scan = n_priv = 0: the encoders ran elsewhere; their outputs [B, w] (row stride
+   * ld) are copied into the actor-input parts 1..3 (priv latent, scan latent, est) instead */
+  const float* part_src[3]; int64_t part_ld[3]; int32_t part_w[3], pad2;
 } lgx_s8_act_args;
 int32_t lgx_s8_act(const lgx_s8_act_args* args, void* stream);
 /* The act-packed format: for each 16-row output tile t and 32-deep K step s, one 2 KB block

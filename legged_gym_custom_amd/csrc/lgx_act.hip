@@ -325,9 +325,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     if (critic) {
       warm_l2(a.critic, a.n_critic, gw, sink);
     } else {
-      warm_l2(a.est, a.n_est, gw, sink);
-      warm_l2(a.scan, a.n_scan, gw, sink);
-      warm_l2(a.priv, a.n_priv, gw, sink);
+      if (a.n_est) {
+        warm_l2(a.est, a.n_est, gw, sink);
+        warm_l2(a.scan, a.n_scan, gw, sink);
+        warm_l2(a.priv, a.n_priv, gw, sink);
+      }
       warm_l2(a.actor, a.n_actor, gw, sink);
     }
   }
@@ -339,6 +341,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     for (int i = tid; i < XF; i += NT) act_lds[i] = 0.f;
     __syncthreads();
     copy_rows(a.obs, a.ld_obs, a.n_obs, r0, rows, a.seg[0], XP, a.obs_st);
+    if (a.n_est == 0)  // the encoders ran elsewhere: their outputs into the actor-input parts
+      for (int q = 0; q < 3; ++q) copy_rows(a.part_src[q], a.part_ld[q], a.part_w[q], r0, rows, a.seg[q + 1], XP, nullptr);
     if (a.priv_st) copy_rows(a.priv_obs, a.ld_priv, a.n_priv_in, r0, rows, -1, 0, a.priv_st);
     if (a.scan_st) copy_rows(a.scan_obs, a.ld_scan, a.n_scan_in, r0, rows, -1, 0, a.scan_st);
     if (a.est_st) copy_rows(a.est_obs, a.ld_est, a.n_est_obs, r0, rows, -1, 0, a.est_st);
@@ -350,7 +354,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     Src in;
     Dst out;
     job(a, critic, i, r0, L, in, out);
-    if (!critic && (i == a.n_est || i == a.n_est + a.n_scan)) {
+    if (!critic && a.n_scan > 0 && (i == a.n_est || i == a.n_est + a.n_scan)) {
       // the scan / privileged encoder's input rows into S2 (free between chains)
       const bool sc = i == a.n_est;
       copy_rows(sc ? a.scan_obs : a.priv_obs, sc ? a.ld_scan : a.ld_priv, sc ? a.n_scan_in : a.n_priv_in, r0, rows,
@@ -470,9 +474,18 @@ int32_t lgx_s8_act(const lgx_s8_act_args* a, void* stream) {
       a->seg[1] > a->seg[2] || a->seg[2] > a->seg[3] || a->seg[3] > a->width || (a->seg[1] | a->seg[2] | a->seg[3]) % 4 ||
       a->est_c0 % 4 || a->est_c0 < 0)
     return afail("lgx_s8_act: actor-input layout (parts at multiples of 4 columns, width <= MAXIN, multiple of 32)");
-  if (check_chain(a->est, a->n_est, a->est->K, LGX_S8_ACT_MAXENC, "lgx_s8_act: estimator chain") ||
-      check_chain(a->scan, a->n_scan, a->scan->K, LGX_S8_ACT_MAXENC, "lgx_s8_act: scan-encoder chain") ||
-      check_chain(a->priv, a->n_priv, a->priv->K, LGX_S8_ACT_MAXENC, "lgx_s8_act: privileged-encoder chain") ||
+  const bool enc = a->n_est > 0;
+  if (!enc) {
+    if (a->n_scan || a->n_priv) return afail("lgx_s8_act: encoders all in the kernel or none");
+    const int pw[3] = {a->seg[2] - a->seg[1], a->seg[3] - a->seg[2], a->width - a->seg[3]};
+    for (int q = 0; q < 3; ++q)
+      if (!a->part_src[q] || a->part_w[q] < 1 || a->part_w[q] > pw[q] || a->part_ld[q] < a->part_w[q])
+        return afail("lgx_s8_act: actor-input part sources");
+  }
+  if ((enc && (check_chain(a->est, a->n_est, a->est->K, LGX_S8_ACT_MAXENC, "lgx_s8_act: estimator chain") ||
+               check_chain(a->scan, a->n_scan, a->scan->K, LGX_S8_ACT_MAXENC, "lgx_s8_act: scan-encoder chain") ||
+               check_chain(a->priv, a->n_priv, a->priv->K, LGX_S8_ACT_MAXENC,
+                           "lgx_s8_act: privileged-encoder chain"))) ||
       check_chain(a->actor, a->n_actor, a->width, LGX_S8_ACT_MAXH, "lgx_s8_act: actor chain") ||
       check_chain(a->critic, a->n_critic, a->critic->K, LGX_S8_ACT_MAXH, "lgx_s8_act: critic chain"))
     return -1;
@@ -480,14 +493,14 @@ int32_t lgx_s8_act(const lgx_s8_act_args* a, void* stream) {
     return afail("lgx_s8_act: est storage row without its source");
   if (a->n_critic_in % 32 || a->ld_critic % 4 || (((uintptr_t)a->critic_obs) & 15))
     return afail("lgx_s8_act: critic input: width a multiple of 32, 16-B aligned rows");
-  if (a->n_scan_in > LGX_S8_ACT_MAXENC || a->n_priv_in > LGX_S8_ACT_MAXENC)
+  if (enc && (a->n_scan_in > LGX_S8_ACT_MAXENC || a->n_priv_in > LGX_S8_ACT_MAXENC))
     return afail("lgx_s8_act: scan / privileged inputs wider than LGX_S8_ACT_MAXENC");
-  if (a->est_c0 + a->est->K > a->n_obs || a->scan->K != a->n_scan_in || a->priv->K != a->n_priv_in ||
+  if ((enc && (a->est_c0 + a->est->K > a->n_obs || a->scan->K != a->n_scan_in || a->priv->K != a->n_priv_in)) ||
       a->critic->K != a->n_critic_in)
     return afail("lgx_s8_act: first-layer widths do not match the inputs");
-  if (a->est[a->n_est - 1].N > a->width - a->seg[3] || a->scan[a->n_scan - 1].N > a->seg[3] - a->seg[2] ||
-      a->priv[a->n_priv - 1].N > a->seg[2] - a->seg[1] || a->critic[a->n_critic - 1].N != 1 ||
-      a->actor[a->n_actor - 1].N > a->ld_mu)
+  if ((enc && (a->est[a->n_est - 1].N > a->width - a->seg[3] || a->scan[a->n_scan - 1].N > a->seg[3] - a->seg[2] ||
+               a->priv[a->n_priv - 1].N > a->seg[2] - a->seg[1])) ||
+      a->critic[a->n_critic - 1].N != 1 || a->actor[a->n_actor - 1].N > a->ld_mu)
     return afail("lgx_s8_act: output widths do not fit their parts");
   static bool attr = false;
   if (!attr) {

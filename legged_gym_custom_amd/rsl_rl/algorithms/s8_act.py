@@ -15,6 +15,7 @@ input in the segmented order (the gaps are zeros), so mu differs from the groupe
 rounding only (tests/test_gpu_s8_act.py: within 1e-5)."""
 import torch
 
+from legged_gym_custom_amd.rsl_rl.modules import hip_mlp as H
 from legged_gym_custom_amd.rsl_rl.modules import hip_s8 as S
 from .s8_update import _chain
 
@@ -53,8 +54,13 @@ class S8Act:
         return (c0 % 4 == 0 and critic[-1].out_features == 1 and critic[0].in_features % 32 == 0
                 and scan[0].in_features <= S.ACT_MAXENC and priv[0].in_features <= S.ACT_MAXENC)
 
-    def __init__(self, alg, num_envs):
+    def __init__(self, alg, num_envs, encoders_in_kernel=False):
+        """encoders_in_kernel: the estimator / scan / privileged encoders inside the kernel too
+        (actor blocks run 13 dependent layers; measured slower than running the encoders as
+        the grouped launches first and the kernel on their outputs, the default)."""
         ac, est = alg.actor_critic, alg.estimator
+        self.alg = alg
+        self.enc_in_kernel = encoders_in_kernel
         dev = alg.device
         self.B = num_envs
         actor, critic = _chain(ac.actor), _chain(ac.critic)
@@ -93,9 +99,16 @@ class S8Act:
                 dst[i] = S.ActLayer(W=Wp.data_ptr(), ldw=steps, b=m.bias.data_ptr(), K=K, N=N,
                                     elu=int(i < len(layers) - 1))
             return len(layers)
-        a.n_est = fill(a.est, estc)
-        a.n_scan = fill(a.scan, scan)
-        a.n_priv = fill(a.priv, priv)
+        if encoders_in_kernel:
+            a.n_est = fill(a.est, estc)
+            a.n_scan = fill(a.scan, scan)
+            a.n_priv = fill(a.priv, priv)
+        else:
+            # the encoders' outputs: spans of one [B, latent | scan latent | est] buffer
+            self.parts = torch.empty(num_envs, nlat + nscan + nest, device=dev)
+            self.spans = [self.parts[:, :nlat], self.parts[:, nlat:nlat + nscan], self.parts[:, nlat + nscan:]]
+            for q, t in enumerate(self.spans):
+                a.part_src[q], a.part_ld[q], a.part_w[q] = t.data_ptr(), t.stride(0), t.shape[1]
         a.n_actor = fill(a.actor, actor, first_actor=True)
         a.n_critic = fill(a.critic, critic)
         self.mu = torch.empty(num_envs, actor[-1].out_features, device=dev)
@@ -120,6 +133,16 @@ class S8Act:
         a.priv_obs, a.ld_priv, a.n_priv_in = priv.data_ptr(), priv.stride(0), priv.shape[1]
         a.critic_obs, a.ld_critic, a.n_critic_in = critic.data_ptr(), critic.stride(0), critic.shape[1]
         a.scan_obs, a.ld_scan, a.n_scan_in = scan.data_ptr(), scan.stride(0), scan.shape[1]
+        if not self.enc_in_kernel:
+            # the estimator and the scan / privileged encoders: grouped launches writing their
+            # outputs into the spans the kernel reads
+            alg = self.alg
+            ac = alg.actor_critic
+            e_mod, e_in = alg.estimator.group_item(obs)
+            s_mod, s_in = ac.scan_encoder.group_item(scan)
+            p_mod, p_in = ac.privileged_encoder_.group_item(priv)
+            H.forward_group([(e_mod, e_in, None, self.spans[2]), (s_mod, s_in, None, self.spans[1]),
+                             (p_mod, p_in, None, self.spans[0])])
         if rows is not None:
             src = (obs, priv, critic, est, scan)
             for d, x in zip(rows, src):

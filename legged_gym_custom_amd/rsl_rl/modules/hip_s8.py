@@ -63,7 +63,8 @@ class ActArgs(C.Structure):
                 ("critic", ActLayer * 6), ("n_est", i32), ("n_scan", i32), ("n_priv", i32), ("n_actor", i32),
                 ("n_critic", i32), ("mu", vp), ("ld_mu", i64), ("value", vp), ("obs_st", vp), ("priv_st", vp),
                 ("scan_st", vp), ("critic_st", vp), ("est_st", vp), ("est_obs", vp), ("ld_est", i64),
-                ("n_est_obs", i32), ("pad1", i32)]
+                ("n_est_obs", i32), ("pad1", i32), ("part_src", vp * 3), ("part_ld", i64 * 3), ("part_w", i32 * 3),
+                ("pad2", i32)]
 
 
 def flat_reduce(ws, stride, out, n, nsplit, accumulate=0):
