@@ -219,32 +219,31 @@ __device__ __forceinline__ void layer(const lgx_s8_act_layer& L, const Src& in, 
 }
 
 // rows [r0, r0 + rows) x n columns of src (row stride ld) into the LDS image (lds_off >= 0,
-// pitch lds_ld) and / or a contiguous global [.., n] destination: 8 rows x 3 x 256 columns of
-// loads in flight per pass (a load per row and column loop would pay a round trip each)
+// pitch lds_ld) and / or a contiguous global [.., n] destination: the block's rows x columns as
+// one flat range, 16 loads per thread in flight per pass (a load per row would pay a round
+// trip each)
 __device__ __forceinline__ void copy_rows(const float* src, int64_t ld, int n, int r0, int rows, int lds_off, int lds_ld,
                                           float* st) {
+  constexpr int U = 16;
   const int tid = threadIdx.x;
-  for (int c0 = 0; c0 < n; c0 += 3 * NT)
-    for (int r = 0; r < rows; r += 8) {
-      float v[8][3];
+  const int total = rows * n;
+  for (int base = 0; base < total; base += NT * U) {
+    float v[U];
+    int rr[U], kk[U];
 #pragma unroll
-      for (int rr = 0; rr < 8; ++rr)
-#pragma unroll
-        for (int q = 0; q < 3; ++q) {
-          const int k = c0 + tid + NT * q;
-          v[rr][q] = r + rr < rows && k < n ? src[(int64_t)(r0 + r + rr) * ld + k] : 0.f;
-        }
-#pragma unroll
-      for (int rr = 0; rr < 8; ++rr)
-#pragma unroll
-        for (int q = 0; q < 3; ++q) {
-          const int k = c0 + tid + NT * q;
-          if (r + rr < rows && k < n) {
-            if (lds_off >= 0) act_lds[lds_off + (r + rr) * lds_ld + k] = v[rr][q];
-            if (st) st[(int64_t)(r0 + r + rr) * n + k] = v[rr][q];
-          }
-        }
+    for (int u = 0; u < U; ++u) {
+      const int idx = std::min(base + tid + NT * u, total - 1);
+      rr[u] = idx / n;
+      kk[u] = idx - rr[u] * n;
+      v[u] = src[(int64_t)(r0 + rr[u]) * ld + kk[u]];
     }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (base + tid + NT * u >= total) continue;
+      if (lds_off >= 0) act_lds[lds_off + rr[u] * lds_ld + kk[u]] = v[u];
+      if (st) st[(int64_t)(r0 + rr[u]) * n + kk[u]] = v[u];
+    }
+  }
 }
 
 // Layer i of this block's chain sequence — critic blocks: the critic; actor blocks: estimator,
@@ -302,12 +301,19 @@ __device__ __forceinline__ void job(const lgx_s8_act_args& a, bool critic, int i
 // (the env step in between evicts them from L2). The values are summed into `sink`, which the
 // caller keeps alive.
 __device__ __forceinline__ void warm_l2(const lgx_s8_act_layer* Ls, int n, int gw, float& sink) {
+  constexpr int U = 8;  // loads in flight per pass
   const int lane = threadIdx.x & 63;
   for (int i = 0; i < n; ++i) {
     const int64_t bytes = (int64_t)((Ls[i].N + 15) / 16) * Ls[i].ldw * 2048;
     const GAS char* W = (const GAS char*)Ls[i].W;
-    for (int64_t off = (int64_t)gw * 1024 + lane * 16; off < bytes; off += 32 * NWV * 1024)
-      sink += *(const GAS float*)(W + off);
+    constexpr int64_t stride = 32 * NWV * 1024;
+    for (int64_t off0 = (int64_t)gw * 1024 + lane * 16; off0 < bytes; off0 += U * stride) {
+      float v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = *(const GAS float*)(W + std::min(off0 + u * stride, bytes - 4));
+#pragma unroll
+      for (int u = 0; u < U; ++u) sink += v[u];
+    }
   }
 }
 
