@@ -164,6 +164,9 @@ class S8Minibatch:
         # (measured on go2 at 24,576-row minibatches, tools/s8_levels.py: 765 -> 734 us per minibatch)
         self.fwd_shift = {"critic": 3, "est": 3}
         self.dx_shift = {"critic": 0, "est": 2}
+        # the critic's first layer as column slices over levels 0..3, beside the privileged /
+        # scan encoders' narrow levels
+        self.l0_slices = {"critic": 4}
         self._build(shapes)
 
     # ------------------------------------------------------------------ argument lists
@@ -183,12 +186,20 @@ class S8Minibatch:
         self._fwd_levels = None  # built per minibatch offset (input row pointers)
         self._shapes = shapes
 
-    def _fwd(self, p, l, A_ptr, lda, K, C=None, ldc=0, C32=None, ldc32=0, elu=True):
+    def _fwd(self, p, l, A_ptr, lda, K, C=None, ldc=0, C32=None, ldc32=0, elu=True, n0=0, n1=None):
+        """Layer l's forward GemmArgs; n0, n1: only output columns [n0, n1) (C already offset)."""
         W = p.W[l]
         Ws = p.Ws[l]
-        return S.GemmArgs(A=A_ptr, lda=lda, B=Ws.data_ptr(), ldb=Ws.shape[1], M=self.mb, N=W.shape[0], K=K,
-                          epilogue=S.EPI_BIAS | (S.EPI_ELU if elu else 0), C=C, ldc=ldc, C32=C32, ldc32=ldc32,
-                          bias=p.b[l].data_ptr())
+        n1 = W.shape[0] if n1 is None else n1
+        return S.GemmArgs(A=A_ptr, lda=lda, B=Ws.data_ptr() + 4 * n0 * Ws.shape[1], ldb=Ws.shape[1], M=self.mb,
+                          N=n1 - n0, K=K, epilogue=S.EPI_BIAS | (S.EPI_ELU if elu else 0), C=C, ldc=ldc, C32=C32,
+                          ldc32=ldc32, bias=p.b[l].data_ptr() + 4 * n0)
+
+    @staticmethod
+    def _slices(N, ns):
+        """ns column ranges of [0, N), boundaries at multiples of 8 (S8 groups)."""
+        b = [min(N, (N * q // ns + 7) // 8 * 8) for q in range(ns)] + [N]
+        return [(b[q], b[q + 1]) for q in range(ns) if b[q] < b[q + 1]]
 
     def prepare(self, perm, flat):
         """Per update: the network inputs of every row, permuted, into S8 (one launch).
@@ -230,7 +241,15 @@ class S8Minibatch:
                 last = l == p.n - 1
                 if not last:
                     o = p.out[l]
-                    put(l + sh, self._fwd(p, l, A_ptr, lda, K, C=o.data_ptr(), ldc=o.shape[1]))
+                    ns = self.l0_slices.get(p.name, 1) if l == 0 else 1
+                    if ns > 1:
+                        # column slices of a first layer in the levels before its own (the
+                        # privileged / scan encoders' narrow levels), the last slice at l + sh
+                        for q, (n0, n1) in enumerate(self._slices(p.W[0].shape[0], ns)):
+                            put(l + sh - (ns - 1) + q, self._fwd(p, l, A_ptr, lda, K, C=S.group_ptr(o, n0),
+                                                                 ldc=o.shape[1], n0=n0, n1=n1))
+                    else:
+                        put(l + sh, self._fwd(p, l, A_ptr, lda, K, C=o.data_ptr(), ldc=o.shape[1]))
                     A_ptr, lda, K = o.data_ptr(), o.shape[1], p.W[l].shape[0]
                     continue
                 if p is pr:

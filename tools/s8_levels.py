@@ -25,7 +25,7 @@ def main():
     s8 = alg._s8
     assert s8 is not None
     mbs = list(alg._minibatches())
-    configs = [(fc, fe, bc, be) for fc, fe, bc, be in itertools.product((0, 3), (0, 3), (0, 1, 2), (0, 2))]
+    configs = [(3, 3, 0, 2, sl) for sl in (1, 2, 3, 4)] + [(3, 3, 0, 0, 4), (3, 3, 1, 2, 4)]
     res = {c: [] for c in configs}
 
     def run():
@@ -35,6 +35,7 @@ def main():
         for c in configs:
             s8.fwd_shift = {"critic": c[0], "est": c[1]}
             s8.dx_shift = {"critic": c[2], "est": c[3]}
+            s8.l0_slices = {"critic": c[4]}
             run()
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record()
@@ -45,7 +46,8 @@ def main():
             res[c].append(a.elapsed_time(b) * 1000 / (3 * len(mbs)))
     out = sorted(((round(statistics.median(v), 1), c) for c, v in res.items()))
     for t, c in out:
-        print(f"{t:8.1f} us/minibatch  fwd shift critic {c[0]} est {c[1]}  dx shift critic {c[2]} est {c[3]}")
+        print(f"{t:8.1f} us/minibatch  fwd shift critic {c[0]} est {c[1]}  dx shift critic {c[2]} est {c[3]}"
+              f"  critic L0 slices {c[4]}")
     print(json.dumps({str(c): t for t, c in out}))
 
 
