@@ -164,9 +164,10 @@ class S8Minibatch:
         # (measured on go2 at 24,576-row minibatches, tools/s8_levels.py: 765 -> 734 us per minibatch)
         self.fwd_shift = {"critic": 3, "est": 3}
         self.dx_shift = {"critic": 0, "est": 2}
-        # the critic's first layer as column slices over levels 0..3, beside the privileged /
-        # scan encoders' narrow levels
-        self.l0_slices = {"critic": 4}
+        # a first layer as column slices over the levels before its own (measured for the
+        # critic beside the privileged / scan encoders' narrow levels: 2 / 3 / 4 slices 720 / 746
+        # / 739 us per minibatch against 710 unsliced — not used)
+        self.l0_slices = {"critic": 1}
         self._build(shapes)
 
     # ------------------------------------------------------------------ argument lists
