@@ -15,6 +15,20 @@ env, _ = task_registry.make_env("go2", a)
 _, tcfg = task_registry.get_cfgs("go2")
 runner, _ = task_registry.make_alg_runner(env, args=a, train_cfg=tcfg, log_root=None)
 runner.learn(2, init_at_random_ep_len=True)
+dag = []
+_upd = runner.alg.update_dagger
+
+
+def timed_update_dagger(*a, **k):  # the DAgger update's own cost, synchronised around it
+    torch.cuda.synchronize()
+    t = time.time()
+    r = _upd(*a, **k)
+    torch.cuda.synchronize()
+    dag.append(time.time() - t)
+    return r
+
+
+runner.alg.update_dagger = timed_update_dagger
 times = []
 for i in range(22):
     it = runner.current_learning_iteration
@@ -26,5 +40,8 @@ for i in range(22):
 freq = runner.dagger_update_freq
 d = [t for it, t in times if it % freq == 0]
 n = [t for it, t in times if it % freq != 0]
+ppo = sum(n) / len(n)
 print("dagger every", freq, "| dagger iters ms:", [round(x * 1e3, 1) for x in d],
-      "| ppo iters mean ms: %.1f" % (1e3 * sum(n) / len(n)))
+      "| ppo iters mean ms: %.1f" % (1e3 * ppo), "| update_dagger ms:", [round(x * 1e3, 2) for x in dag])
+if d and dag:
+    print("dagger iteration / (ppo iteration + update_dagger) = %.3f" % (d[-1] / (ppo + dag[-1])))
