@@ -140,6 +140,13 @@ typedef struct lgx_s8_act_args {
   /* n_est = n_scan = n_priv = 0: the encoders ran elsewhere; their outputs [B, w] (row stride
    * ld) are copied into the actor-input parts 1..3 (priv latent, scan latent, est) instead */
   const float* part_src[3]; int64_t part_ld[3]; int32_t part_w[3], pad2;
+  /* optional act head (actions != NULL; lgx_act_head's semantics, lgx_mlp.h): from the actor's
+   * output mu, a = mu + std * eps and the Normal log-prob, into this step's storage rows
+   * actions / mu_st / sigma_st [B, A] and logp_st [B] (+ actions_copy); eps [B, A] given, or
+   * drawn from (seed, *step_dev, env_offset) as lgx_act_head does; mu is then not written */
+  const float* std; const float* eps;
+  float* actions; float* mu_st; float* sigma_st; float* logp_st; float* actions_copy;
+  const int64_t* step_dev; uint64_t seed; int64_t env_offset;
 } lgx_s8_act_args;
 int32_t lgx_s8_act(const lgx_s8_act_args* args, void* stream);
 /* The act-packed format: for each 16-row output tile t and 32-deep K step s, one 2 KB block

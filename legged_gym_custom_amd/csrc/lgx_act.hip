@@ -28,7 +28,9 @@
 
 #include <algorithm>
 
+#include "../../include/lgx_mlp.h"  // LGX_ACT_NOISE_STREAM
 #include "../../include/lgx_s8.h"
+#include "lgx_device.h"  // philox4x32_10 / u01: the env's counter RNG (the act head's noise)
 
 namespace lgxa {
 
@@ -285,8 +287,11 @@ __device__ __forceinline__ void job(const lgx_s8_act_args& a, bool critic, int i
     L = a.actor[p];
     if (p == 0) in = Src{nullptr, XP, X};
     else { in.g = nullptr; hidden(p - 1, in.off, in.ld); }
-    if (p == a.n_actor - 1) out = Dst{a.mu + (int64_t)r0 * a.ld_mu, a.ld_mu, 0};
-    else { out.g = nullptr; hidden(p, out.off, out.ld); }
+    if (p == a.n_actor - 1) {
+      // mu: to the act head's LDS image (the free half of the hidden images), or to global
+      if (a.actions) { out.g = nullptr; out.off = (p & 1) ? X : Y; out.ld = 16; }
+      else out = Dst{a.mu + (int64_t)r0 * a.ld_mu, a.ld_mu, 0};
+    } else { out.g = nullptr; hidden(p, out.off, out.ld); }
     return;
   }
   // encoder chains: scratch images S1, S2, S1, ...
@@ -314,6 +319,65 @@ __device__ __forceinline__ void warm_l2(const lgx_s8_act_layer* Ls, int n, int g
 #pragma unroll
       for (int u = 0; u < U; ++u) sink += v[u];
     }
+  }
+}
+
+// The act head for the block's rows (lgx_mlp.hip act_head_kernel, the same arithmetic): mu in
+// the LDS image at `mu_off` [R][16]; four lanes per row, lane q takes actions 4q..4q+3 (one
+// Philox call), the row's log-prob terms summed in action order by its lane 0.
+__device__ __forceinline__ void act_head(const lgx_s8_act_args& a, int mu_off, int r0, int rows, int A) {
+  const int t = threadIdx.x;
+  const int i = t >> 2, q = t & 3;
+  if (i >= R) return;
+  const bool row = i < rows, on = row && 4 * q < A;
+  const float cst = 0.91893853320467274178f;  // log(sqrt(2 pi))
+  float term[4] = {0.f, 0.f, 0.f, 0.f};
+  const int gi = r0 + i;
+  if (on) {
+    float e4[4];
+    if (a.eps == nullptr) {
+      const uint64_t step = (uint64_t)*a.step_dev;
+      const uint32_t gid = (uint32_t)(a.env_offset + gi);
+      uint32_t o[4];
+      philox4x32_10(gid, (uint32_t)step, (uint32_t)q | ((uint32_t)LGX_ACT_NOISE_STREAM << 16), (uint32_t)(step >> 32),
+                    (uint32_t)a.seed, (uint32_t)(a.seed >> 32), o);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const float u1 = 1.0f - u01(o[2 * h]);
+        const float u2 = u01(o[2 * h + 1]);
+        const float r = sqrtf(-2.0f * logf(u1));
+        const float th = 6.28318530717958647692f * u2;
+        e4[2 * h] = r * cosf(th);
+        e4[2 * h + 1] = r * sinf(th);
+      }
+    } else {
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) e4[jj] = 4 * q + jj < A ? a.eps[(size_t)gi * A + 4 * q + jj] : 0.f;
+    }
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int j = 4 * q + jj;
+      if (j >= A) break;
+      const size_t k = (size_t)gi * A + j;
+      const float m = act_lds[mu_off + i * 16 + j], sd = a.std[j];
+      const float x = m + sd * e4[jj];
+      const float d = x - m;
+      term[jj] = -(d * d) / (2.0f * (sd * sd)) - logf(sd) - cst;
+      a.actions[k] = x;
+      if (a.actions_copy) a.actions_copy[k] = x;
+      a.mu_st[k] = m;
+      a.sigma_st[k] = sd;
+    }
+  }
+  float all[16];
+#pragma unroll
+  for (int qq = 0; qq < 4; ++qq)
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) all[4 * qq + jj] = __shfl(term[jj], (threadIdx.x & ~3) + qq, 64);
+  if (row && q == 0) {
+    float lp = 0.0f;
+    for (int j = 0; j < A; ++j) lp += all[j];
+    a.logp_st[gi] = lp;
   }
 }
 
@@ -378,6 +442,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       else layer<1, false>(L, in, out, rows);
     }
   }
+  if (!critic && a.actions) act_head(a, ((a.n_actor - 1) & 1) ? 0 : XF, r0, rows, a.actor[a.n_actor - 1].N);
   if (sink == 1.2345e-38f && a.B < 0) a.value[0] = sink;  // keeps the warm-up loads (never true)
 }
 
@@ -497,6 +562,9 @@ int32_t lgx_s8_act(const lgx_s8_act_args* a, void* stream) {
     return -1;
   if (a->est_st && (!a->est_obs || a->n_est_obs < 1 || a->ld_est < a->n_est_obs))
     return afail("lgx_s8_act: est storage row without its source");
+  if (a->actions && (!a->std || !a->mu_st || !a->sigma_st || !a->logp_st || (!a->eps && !a->step_dev) ||
+                     a->actor[a->n_actor - 1].N > 16))
+    return afail("lgx_s8_act: act head arguments (A <= 16)");
   if (a->n_critic_in % 32 || a->ld_critic % 4 || (((uintptr_t)a->critic_obs) & 15))
     return afail("lgx_s8_act: critic input: width a multiple of 32, 16-B aligned rows");
   if (enc && (a->n_scan_in > LGX_S8_ACT_MAXENC || a->n_priv_in > LGX_S8_ACT_MAXENC))

@@ -315,8 +315,8 @@ class PPO:
         if self._gpu_rollout():
             # the estimator, privileged/scan encoders and critic read only observations: one
             # grouped launch per depth (hip_mlp.forward_group), then the actor — or all of them
-            # in one launch (s8_act.py), which also writes this step's observation rows; one HIP
-            # kernel samples a = mu + std * eps and writes actions, mu, sigma and the Normal
+            # in one launch (s8_act.py), which also writes this step's observation rows and runs
+            # the act head; otherwise one HIP kernel samples a = mu + std * eps and writes actions, mu, sigma and the Normal
             # log-prob straight into this step's storage rows (lgx_act_head)
             s, k = self.storage, self.storage.step
             fused = self._fused_act(adaptation_mode)
@@ -334,8 +334,13 @@ class PPO:
                     # its S8 weights are refreshed at the rollout's first step (the update changed them)
                     if k == 0:
                         fused.refresh_weights()
-                    mean, t.values = fused.run(obs, privileged_obs, critic_obs, scan_obs, est=true_estimated_obs,
-                                               rows=slots)
+                    noise = self.act_noise
+                    dst = self.act_dst if self.act_dst is not None and self.act_dst.shape == s.actions[k].shape else None
+                    head = dict(std=ac.std.detach(), eps=torch.randn_like(s.mu[k]) if noise is None else None,
+                                noise=noise, actions=s.actions[k], mu=s.mu[k], sigma=s.sigma[k],
+                                logp=s.actions_log_prob[k], actions_copy=dst)
+                    _, t.values = fused.run(obs, privileged_obs, critic_obs, scan_obs, est=true_estimated_obs,
+                                            rows=slots, head=head)
                 else:
                     items = [self.estimator.group_item(obs), ac.scan_encoder.group_item(scan_obs)]
                     if not adaptation_mode:
@@ -345,11 +350,12 @@ class PPO:
                     latent = ac.adaptation_encoder(obs) if adaptation_mode else outs[2]
                     mean, t.values = hip_mlp.forward_group([(ac.actor, (obs, latent, scan_latent, estimated_obs)),
                                                             (ac.critic, critic_obs)])
-                noise = self.act_noise
-                eps = torch.randn_like(mean) if noise is None else None
-                dst = self.act_dst if self.act_dst is not None and self.act_dst.shape == mean.shape else None
-                hip_mlp.act_head(mean, ac.std.detach(), eps, s.actions[k], s.mu[k], s.sigma[k], s.actions_log_prob[k],
-                                 actions_copy=dst, noise=noise)
+                if fused is None:
+                    noise = self.act_noise
+                    eps = torch.randn_like(mean) if noise is None else None
+                    dst = self.act_dst if self.act_dst is not None and self.act_dst.shape == mean.shape else None
+                    hip_mlp.act_head(mean, ac.std.detach(), eps, s.actions[k], s.mu[k], s.sigma[k],
+                                     s.actions_log_prob[k], actions_copy=dst, noise=noise)
             t.actions, t.action_mean, t.action_sigma = s.actions[k], s.mu[k], s.sigma[k]
             t.actions_log_prob = s.actions_log_prob[k].view(-1)
             return t.actions if dst is None else dst

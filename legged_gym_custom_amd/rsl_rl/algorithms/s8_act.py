@@ -6,8 +6,9 @@ kernel over S8 copies of their weights (bf16 hi / lo, packed as MFMA fragments: 
 32 envs per block, the activations in LDS, the actor input assembled in place as [obs | priv latent | scan
 latent | est] in the update's segmented layout. The weights are packed once per rollout (at its
 first step, inside the rollout graph). The kernel also writes this step's observation rows of
-the storage (rollout_storage.py:87-105; no separate copy launch). The act head (sampling,
-log-prob, action rows) stays `lgx_act_head`. Adaptation-mode rollouts (the DAgger iterations: the latent from the adaptation
+the storage (rollout_storage.py:87-105; no separate copy launch) and, given `head`, runs the act
+head in the actor blocks (a = mu + std * eps, the Normal log-prob, the action / mu / sigma rows:
+lgx_act_head's arithmetic, ppo.py:141-147), mu never leaving LDS. Adaptation-mode rollouts (the DAgger iterations: the latent from the adaptation
 encoder) keep the grouped launches.
 
 Numerics: the same 3 x bf16 products as the grouped launches; the actor's first layer sums its
@@ -121,11 +122,39 @@ class S8Act:
         after the update changed them)."""
         S.act_pack(self.wpack)
 
-    def run(self, obs, priv, critic, scan, est=None, rows=None):
+    def run(self, obs, priv, critic, scan, est=None, rows=None, head=None):
         """(mu [B, A], value [B, 1]) of this step's observations (static output buffers).
         rows (optional): this step's storage rows [obs, priv, critic, est, scan] (contiguous),
-        which the kernel fills from the inputs (est: the true estimated obs, copied only)."""
+        which the kernel fills from the inputs (est: the true estimated obs, copied only).
+        head (optional): dict(std, eps, actions, mu, sigma, logp, actions_copy, noise) as
+        hip_mlp.act_head takes them; the kernel then writes those rows and NOT the mu buffer
+        (mu is returned as None)."""
         a = self.args
+        if head is None:
+            a.actions = None
+        else:
+            A = self.mu.shape[1]
+            outs = [head[k] for k in ("actions", "mu", "sigma", "logp")]
+            cp = head.get("actions_copy")
+            for t in outs[:3] + ([cp] if cp is not None else []):
+                if t.shape != (self.B, A) or not t.is_contiguous() or t.dtype != torch.float32:
+                    raise S.S8LibError("S8Act: act-head rows must be contiguous fp32 [num_envs, A]")
+            if outs[3].numel() != self.B or not outs[3].is_contiguous():
+                raise S.S8LibError("S8Act: log-prob row must be contiguous [num_envs]")
+            eps = head.get("eps")
+            if eps is None:
+                seed, step_dev, off = head["noise"]
+                if step_dev.dtype != torch.int64 or step_dev.device != self.mu.device:
+                    raise S.S8LibError("S8Act: step_dev must be an int64 tensor on the device")
+                a.eps, a.step_dev, a.seed, a.env_offset = None, step_dev.data_ptr(), int(seed) & (2**64 - 1), int(off)
+            else:
+                if eps.shape != (self.B, A) or not eps.is_contiguous():
+                    raise S.S8LibError("S8Act: eps must be contiguous [num_envs, A]")
+                a.eps, a.step_dev, a.seed, a.env_offset = eps.data_ptr(), None, 0, 0
+            a.std = head["std"].data_ptr()
+            a.actions, a.mu_st, a.sigma_st, a.logp_st = (t.data_ptr() for t in outs)
+            a.actions_copy = None if cp is None else cp.data_ptr()
+            self._head_keep = head  # the argument block holds their addresses
         for t in (obs, priv, critic, scan) + (() if est is None else (est,)):
             if t.stride(1) != 1 or t.dtype != torch.float32 or t.shape[0] != self.B:
                 raise S.S8LibError("S8Act: fp32 [num_envs, cols] inputs with unit column stride")
@@ -153,4 +182,4 @@ class S8Act:
         else:
             a.obs_st = a.priv_st = a.critic_st = a.est_st = a.scan_st = a.est_obs = None
         S.act(a)
-        return self.mu, self.value
+        return (self.mu if head is None else None), self.value

@@ -64,7 +64,8 @@ class ActArgs(C.Structure):
                 ("n_critic", i32), ("mu", vp), ("ld_mu", i64), ("value", vp), ("obs_st", vp), ("priv_st", vp),
                 ("scan_st", vp), ("critic_st", vp), ("est_st", vp), ("est_obs", vp), ("ld_est", i64),
                 ("n_est_obs", i32), ("pad1", i32), ("part_src", vp * 3), ("part_ld", i64 * 3), ("part_w", i32 * 3),
-                ("pad2", i32)]
+                ("pad2", i32), ("std", vp), ("eps", vp), ("actions", vp), ("mu_st", vp), ("sigma_st", vp),
+                ("logp_st", vp), ("actions_copy", vp), ("step_dev", vp), ("seed", C.c_uint64), ("env_offset", i64)]
 
 
 def flat_reduce(ws, stride, out, n, nsplit, accumulate=0):

@@ -67,3 +67,35 @@ def test_act_abi_rejects_bad_layouts():
     with pytest.raises(S.S8LibError):
         S.act(a)
     a.actor[1].K = saved
+
+
+@pytest.mark.parametrize("drawn", [True, False])
+def test_fused_act_head_matches_act_head_kernel(drawn):
+    """The act head inside the fused kernel (mu from LDS) against lgx_act_head on the mu the
+    same kernel writes without it: actions (and their copy), mu, sigma and log-prob bit for bit,
+    with the Philox draw (the GPU rollout's) and with given eps."""
+    from legged_gym_custom_amd.rsl_rl.modules import hip_mlp as H
+    alg, _ = _rollout("go2", True)
+    f, s = alg._s8act, alg.storage
+    obs, priv, crit, est, scan = (getattr(s, n)[3].clone() for n in OBS_FIELDS)
+    mu, val = f.run(obs, priv, crit, scan)
+    mu, val = mu.clone(), val.clone()
+    B, A = mu.shape
+    std = alg.actor_critic.std.detach()
+    step = torch.tensor([7], dtype=torch.int64, device=dev)
+    noise = (0x9E3779B97F4A7C15, step, 5) if drawn else None
+    eps = None if drawn else torch.randn(B, A, device=dev)
+
+    def bufs():
+        return dict(actions=torch.full((B, A), 7.0, device=dev), mu=torch.full((B, A), 7.0, device=dev),
+                    sigma=torch.full((B, A), 7.0, device=dev), logp=torch.full((B, 1), 7.0, device=dev),
+                    actions_copy=torch.full((B, A), 7.0, device=dev))
+    ref = bufs()
+    H.act_head(mu, std, eps, ref["actions"], ref["mu"], ref["sigma"], ref["logp"], actions_copy=ref["actions_copy"],
+               noise=noise)
+    got = bufs()
+    m2, v2 = f.run(obs, priv, crit, scan, head=dict(std=std, eps=eps, noise=noise, **got))
+    assert m2 is None
+    assert torch.equal(v2, val)
+    for k in ref:
+        assert torch.equal(got[k], ref[k]), k
