@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define LGX_S8_ABI_VERSION 2
+#define LGX_S8_ABI_VERSION 3
 
 enum { LGX_S8_FWD = 0, LGX_S8_DX = 1, LGX_S8_DW = 2 };  /* GEMM kinds (operand modes above) */
 
@@ -74,6 +74,9 @@ typedef struct lgx_s8_split_args {
   int32_t rows, cols;
   float* colsum_ws;
   const int64_t* idx;           /* optional row gather (rollout_storage.py:141-147's permutation) */
+  int32_t packed_steps;         /* > 0: dst is fragment-packed (a chain's weights, below) with this
+                                   many 32-deep K steps per 16-row tile; ld_dst unused */
+  int32_t pad0;
 } lgx_s8_split_args;
 
 /* out[r * ld_out + c] (+)= sum_{s < nsplit} ws[s * stride + r * ld_ws + c], r < rows, c < cols
@@ -139,7 +142,8 @@ typedef struct lgx_s8_act_args {
   const float* est_obs; int64_t ld_est; int32_t n_est_obs, pad1;
   /* n_est = n_scan = n_priv = 0: the encoders ran elsewhere; their outputs [B, w] (row stride
    * ld) are copied into the actor-input parts 1..3 (priv latent, scan latent, est) instead */
-  const float* part_src[3]; int64_t part_ld[3]; int32_t part_w[3], pad2;
+  const float* part_src[3]; int64_t part_ld[3]; int32_t part_w[3];
+  int32_t nets;  // 0: actor and critic blocks; 1: the actor blocks only; 2: the critic blocks only
   /* optional act head (actions != NULL; lgx_act_head's semantics, lgx_mlp.h): from the actor's
    * output mu, a = mu + std * eps and the Normal log-prob, into this step's storage rows
    * actions / mu_st / sigma_st [B, A] and logp_st [B] (+ actions_copy); eps [B, A] given, or
@@ -168,6 +172,34 @@ int32_t lgx_s8_act_pack(const lgx_s8_act_pack_args* args, int32_t n, void* strea
 const char* lgx_s8_act_last_error(void);
 int32_t lgx_s8_sizeof_act_args(void);
 int32_t lgx_s8_sizeof_act_pack_args(void);
+
+/* Forward chains (lgx_s8chain.hip): the narrow encoders of the update's forward pass (the
+ * privileged and scan encoders, support_networks.py:25-80, as PPO.update runs them in
+ * ppo.py:201-233) as ONE launch instead of one grouped launch per depth. Per chain: A = the
+ * S8 input rows [rows][>= K_0] (pitch lda elements), then up to LGX_S8_CHAIN_MAXL layers
+ * y_l = act(y_{l-1} W_l^T + b_l) with W_l S8 [N_l][ldw_l], K_l = N_{l-1}; each layer's output
+ * goes to C_l (S8, pitch ldc_l, pads zero; may be null) and / or C32_l (fp32; may be null).
+ * Same operand contract and epilogue as lgx_s8_gemm_group FWD (bias, ELU, zero pad columns;
+ * the same 3 x bf16 products per 32-deep K step); widths <= LGX_S8_CHAIN_MAXW. */
+#define LGX_S8_CHAIN_MAX 4
+#define LGX_S8_CHAIN_MAXL 3
+#define LGX_S8_CHAIN_MAXW 256
+typedef struct lgx_s8_chain_layer {
+  const void* W; int64_t ldw;   /* S8 [N][ldw] */
+  const float* bias;
+  void* C; int64_t ldc;         /* S8 output (or null) */
+  float* C32; int64_t ldc32;    /* fp32 output (or null) */
+  int32_t K, N, elu;
+  int32_t packed;               /* W fragment-packed (lgx_s8_split packed_steps = ceil(K / 32)):
+                                   per (16-row tile, K step) 2 KB = 64 lanes x 16 B hi, then lo */
+} lgx_s8_chain_layer;
+typedef struct lgx_s8_chain_args {
+  const void* A; int64_t lda;   /* S8 input rows */
+  int32_t rows, nlayers;
+  lgx_s8_chain_layer layers[LGX_S8_CHAIN_MAXL];
+} lgx_s8_chain_args;
+int32_t lgx_s8_chain_fwd(const lgx_s8_chain_args* chains, int32_t n, void* stream);
+int32_t lgx_s8_sizeof_chain_args(void);
 
 #ifdef __cplusplus
 }

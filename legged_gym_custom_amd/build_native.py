@@ -14,7 +14,7 @@ ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 LIBS = {
     "liblgx.so": (["lgx_env.hip"], ["lgx_device.h", "lgx_host.h", "lgx_env_host.cpp"], ["lgx.h"]),
     "liblgx_mlp.so": (["lgx_mlp.hip"], [], ["lgx_mlp.h"]),
-    "liblgx_s8.so": (["lgx_s8.hip", "lgx_act.hip"], [], ["lgx_s8.h"]),
+    "liblgx_s8.so": (["lgx_s8.hip", "lgx_act.hip", "lgx_s8chain.hip"], [], ["lgx_s8.h"]),
 }
 OUT = os.path.join(HERE, "lib", "liblgx.so")
 OUT_MLP = os.path.join(HERE, "lib", "liblgx_mlp.so")

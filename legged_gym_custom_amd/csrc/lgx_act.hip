@@ -90,6 +90,19 @@ struct Dst {  // a layer output: global rows (g, ld) or an LDS image
   int off;
 };
 
+// Register sets in the weight pipeline per tile count: the narrower layers' sets are smaller,
+// so they keep more K steps in flight (a step's loads are L2 round trips)
+#ifndef ACT_D4
+#define ACT_D4 3
+#endif
+#ifndef ACT_D2
+#define ACT_D2 3
+#endif
+#ifndef ACT_D1
+#define ACT_D1 3
+#endif
+constexpr int act_depth(int tpw) { return tpw >= 4 ? ACT_D4 : tpw == 2 ? ACT_D2 : ACT_D1; }
+
 // One layer for the block's 32 rows. TPW = 16-column tiles per wave (N <= 128 TPW); GIN: the
 // input is global rows (else an LDS image). The K loop has no branches around its loads (steps
 // past the last one read clamped addresses and multiply zeros), so hipcc counts the loads in
@@ -122,8 +135,9 @@ __device__ __forceinline__ void layer(const lgx_s8_act_layer& L, const Src& in, 
     u32x4 h[TPW], l[TPW];
     float a[2][8];  // a global input's values for this step
   };
-  Set s0, s1, s2;
-  // weights (and a global input) two steps ahead, three register sets in rotation
+  constexpr int D = act_depth(TPW);
+  Set sets[D];
+  // weights (and a global input) D - 1 steps ahead, D register sets in rotation
   auto load = [&](Set& S, int s) {
     const int sc = std::min(s, ns - 1);
     const int64_t ko = (int64_t)sc * 2048;
@@ -184,16 +198,15 @@ __device__ __forceinline__ void layer(const lgx_s8_act_layer& L, const Src& in, 
       }
   };
 
-  load(s0, 0);
-  load(s1, 1);
-  const int nsp = (ns + 2) / 3 * 3;  // steps past ns multiply zeros (A is zero for k >= K)
-  for (int s = 0; s < nsp; s += 3) {
-    load(s2, s + 2);
-    step(s0, s);
-    load(s0, s + 3);
-    step(s1, s + 1);
-    load(s1, s + 4);
-    step(s2, s + 2);
+#pragma unroll
+  for (int d = 0; d < D - 1; ++d) load(sets[d], d);
+  const int nsp = (ns + D - 1) / D * D;  // steps past ns multiply zeros (A is zero for k >= K)
+  for (int s = 0; s < nsp; s += D) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      load(sets[(d + D - 1) % D], s + d + D - 1);
+      step(sets[d], s + d);
+    }
   }
 
   // epilogue: bias (+ ELU); MFMA C map: col = lane & 15, row = 4 (lane >> 4) + r
@@ -305,13 +318,13 @@ __device__ __forceinline__ void job(const lgx_s8_act_args& a, bool critic, int i
 // Infinity Cache in one round trip at the start instead of at each of the 13 layer starts
 // (the env step in between evicts them from L2). The values are summed into `sink`, which the
 // caller keeps alive.
-__device__ __forceinline__ void warm_l2(const lgx_s8_act_layer* Ls, int n, int gw, float& sink) {
+__device__ __forceinline__ void warm_l2(const lgx_s8_act_layer* Ls, int n, int gw, int nslot, float& sink) {
   constexpr int U = 8;  // loads in flight per pass
   const int lane = threadIdx.x & 63;
   for (int i = 0; i < n; ++i) {
     const int64_t bytes = (int64_t)((Ls[i].N + 15) / 16) * Ls[i].ldw * 2048;
     const GAS char* W = (const GAS char*)Ls[i].W;
-    constexpr int64_t stride = 32 * NWV * 1024;
+    const int64_t stride = (int64_t)nslot * NWV * 1024;
     for (int64_t off0 = (int64_t)gw * 1024 + lane * 16; off0 < bytes; off0 += U * stride) {
       float v[U];
 #pragma unroll
@@ -382,25 +395,26 @@ __device__ __forceinline__ void act_head(const lgx_s8_act_args& a, int mu_off, i
 }
 
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void act_kernel(lgx_s8_act_args a) {
-  const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
-  const bool critic = xcd >= 4;
-  const int rb = slot * 4 + (xcd & 3);
+  // both networks: actor blocks on XCDs 0-3, critic blocks on 4-7; one network: block = row block
+  const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3, nslot = (gridDim.x + 7) >> 3;
+  const bool critic = a.nets == 0 ? xcd >= 4 : a.nets == 2;
+  const int rb = a.nets == 0 ? slot * 4 + (xcd & 3) : blockIdx.x;
   const int nrb = (a.B + R - 1) / R;
   if (rb >= nrb) return;
   const int r0 = rb * R, rows = std::min(R, a.B - r0);
   const int tid = threadIdx.x;
   float sink = 0.f;
   {
-    const int gw = slot * NWV + (tid >> 6);  // this XCD's 32 blocks x 8 waves
+    const int gw = slot * NWV + (tid >> 6);  // this XCD's blocks x 8 waves
     if (critic) {
-      warm_l2(a.critic, a.n_critic, gw, sink);
+      warm_l2(a.critic, a.n_critic, gw, nslot, sink);
     } else {
       if (a.n_est) {
-        warm_l2(a.est, a.n_est, gw, sink);
-        warm_l2(a.scan, a.n_scan, gw, sink);
-        warm_l2(a.priv, a.n_priv, gw, sink);
+        warm_l2(a.est, a.n_est, gw, nslot, sink);
+        warm_l2(a.scan, a.n_scan, gw, nslot, sink);
+        warm_l2(a.priv, a.n_priv, gw, nslot, sink);
       }
-      warm_l2(a.actor, a.n_actor, gw, sink);
+      warm_l2(a.actor, a.n_actor, gw, nslot, sink);
     }
   }
   // this step's storage rows (optional): contiguous [rows, n] copies of the inputs
@@ -576,6 +590,7 @@ int32_t lgx_s8_act(const lgx_s8_act_args* a, void* stream) {
                a->priv[a->n_priv - 1].N > a->seg[2] - a->seg[1])) ||
       a->critic[a->n_critic - 1].N != 1 || a->actor[a->n_actor - 1].N > a->ld_mu)
     return afail("lgx_s8_act: output widths do not fit their parts");
+  if (a->nets < 0 || a->nets > 2) return afail("lgx_s8_act: nets must be 0, 1 or 2");
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)lgxa::act_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -583,7 +598,7 @@ int32_t lgx_s8_act(const lgx_s8_act_args* a, void* stream) {
     attr = true;
   }
   const int nrb = (a->B + lgxa::R - 1) / lgxa::R;
-  hipLaunchKernelGGL(lgxa::act_kernel, dim3(8 * ((nrb + 3) / 4)), dim3(lgxa::NT), lgxa::LDS_BYTES,
+  hipLaunchKernelGGL(lgxa::act_kernel, dim3(a->nets == 0 ? 8 * ((nrb + 3) / 4) : nrb), dim3(lgxa::NT), lgxa::LDS_BYTES,
                      (hipStream_t)stream, *a);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) {

@@ -187,8 +187,8 @@ __device__ __forceinline__ float elu(float v) {  // lgx_mlp.hip's ELU (same poly
 __device__ __forceinline__ unsigned pack2(__bf16 a, __bf16 b) {
   return (unsigned)__builtin_bit_cast(unsigned short, a) | ((unsigned)__builtin_bit_cast(unsigned short, b) << 16);
 }
-// 8 fp32 -> S8 group (32 B: hi x 8, lo x 8)
-__device__ __forceinline__ void store_s8(char* dst, const float (&v)[8]) {
+// 8 fp32 -> hi x 8 at h, lo x 8 at l
+__device__ __forceinline__ void store_s8x(char* hp, char* lp, const float (&v)[8]) {
   __bf16 h[8], l[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
@@ -197,9 +197,11 @@ __device__ __forceinline__ void store_s8(char* dst, const float (&v)[8]) {
   }
   const u32x4 H = {pack2(h[0], h[1]), pack2(h[2], h[3]), pack2(h[4], h[5]), pack2(h[6], h[7])};
   const u32x4 L = {pack2(l[0], l[1]), pack2(l[2], l[3]), pack2(l[4], l[5]), pack2(l[6], l[7])};
-  reinterpret_cast<u32x4*>(dst)[0] = H;
-  reinterpret_cast<u32x4*>(dst)[1] = L;
+  *reinterpret_cast<u32x4*>(hp) = H;
+  *reinterpret_cast<u32x4*>(lp) = L;
 }
+// 8 fp32 -> S8 group (32 B: hi x 8, lo x 8)
+__device__ __forceinline__ void store_s8(char* dst, const float (&v)[8]) { store_s8x(dst, dst + 16, v); }
 __device__ __forceinline__ void load_s8(const char* src, float (&v)[8]) {
   const u32x4 H = reinterpret_cast<const u32x4*>(src)[0];
   const u32x4 L = reinterpret_cast<const u32x4*>(src)[1];
@@ -437,7 +439,8 @@ struct SplitJob {
   int rows, cols;
   float* colsum_ws;
   const int64_t* idx;
-  int blk0;  // first block of this job
+  int blk0;     // first block of this job
+  int psteps;   // > 0: fragment-packed destination (lgx_s8_chain_layer.packed)
 };
 struct SplitBatch {
   int n;
@@ -467,9 +470,19 @@ __global__ __launch_bounds__(256) void s8_split_kernel(SplitBatch b) {
       for (int e = 0; e < 8; ++e) v[e] = 8 * gg + e < J.cols ? s[e] : 0.f;
     }
   };
+  // row r, group gg -> its 16 B of hi (lo: + 16 in rows; + 1024 packed: tile r / 16, step gg / 4,
+  // lane 16 (gg % 4) + r % 16 — the MFMA B fragment of that lane)
+  auto put = [&](int r, int gg, const float (&v)[8]) {
+    if (J.psteps) {
+      char* q = J.dst + ((int64_t)(r >> 4) * J.psteps + (gg >> 2)) * 2048 + (((gg & 3) << 4) | (r & 15)) * 16;
+      store_s8x(q, q + 1024, v);
+    } else {
+      store_s8(J.dst + (int64_t)r * J.ld_dst + gg * 32, v);
+    }
+  };
   auto one = [&](int r, int gg, float (&v)[8]) {
     load8(r, gg, v);
-    store_s8(J.dst + (int64_t)r * J.ld_dst + gg * 32, v);
+    put(r, gg, v);
   };
   if (G <= 8) {
     const int gg = tid & 7;
@@ -510,7 +523,7 @@ __global__ __launch_bounds__(256) void s8_split_kernel(SplitBatch b) {
   }
 #pragma unroll
   for (int k = 0; k < IT; ++k)
-    if (rr[k] < J.rows) store_s8(J.dst + (int64_t)rr[k] * J.ld_dst + gs[k] * 32, v[k]);
+    if (rr[k] < J.rows) put(rr[k], gs[k], v[k]);
 }
 
 struct ReduceBatch {
@@ -562,6 +575,8 @@ static int launched(const char* what) {
   return 0;
 }
 static int cdiv(int a, int b) { return (a + b - 1) / b; }
+int lgxs_fail(const char* msg) { return fail(msg); }  // for the library's other sources
+int lgxs_launched(const char* what) { return launched(what); }
 
 template <int KIND>
 static void launch_gemm(const lgxs::Group& g, hipStream_t s) {
@@ -682,10 +697,13 @@ int32_t lgx_s8_split(const lgx_s8_split_args* a, int32_t n, void* stream) {
     if (q.rows < 0 || q.cols < 0) return fail("lgx_s8_split: negative size");
     if (q.rows == 0 || q.cols == 0) continue;
     if (!q.src || !q.dst) return fail("lgx_s8_split: null pointer");
-    if (q.ld_dst % 8 || (((uintptr_t)q.dst) & 15) || q.ld_dst < cdiv(q.cols, 8) * 8)
+    if (q.packed_steps < 0 || (q.packed_steps && (q.packed_steps < cdiv(q.cols, 32) || q.colsum_ws || q.idx)))
+      return fail("lgx_s8_split: packed_steps >= ceil(cols / 32), no column sums or gather");
+    if ((((uintptr_t)q.dst) & 15) || (!q.packed_steps && (q.ld_dst % 8 || q.ld_dst < cdiv(q.cols, 8) * 8)))
       return fail("lgx_s8_split: S8 destination alignment / pitch");
     if (q.colsum_ws && q.cols > 64) return fail("lgx_s8_split: column sums for <= 64 columns only");
-    b.j[k] = lgxs::SplitJob{q.src, q.ld_src, (char*)q.dst, q.ld_dst * 4, q.rows, q.cols, q.colsum_ws, q.idx, blocks};
+    b.j[k] = lgxs::SplitJob{q.src, q.ld_src, (char*)q.dst, q.ld_dst * 4, q.rows, q.cols, q.colsum_ws, q.idx, blocks,
+                            q.packed_steps};
     const int64_t G = cdiv(q.cols, 8);
     blocks += G <= 8 ? cdiv(q.rows, LGX_S8_SPLIT_ROWS) : (int)((q.rows * G + LGX_S8_SPLIT_WIDE - 1) / LGX_S8_SPLIT_WIDE);
     ++k;

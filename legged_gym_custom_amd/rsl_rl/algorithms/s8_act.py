@@ -55,13 +55,18 @@ class S8Act:
         return (c0 % 4 == 0 and critic[-1].out_features == 1 and critic[0].in_features % 32 == 0
                 and scan[0].in_features <= S.ACT_MAXENC and priv[0].in_features <= S.ACT_MAXENC)
 
-    def __init__(self, alg, num_envs, encoders_in_kernel=False):
+    def __init__(self, alg, num_envs, encoders_in_kernel=False, split=False):
         """encoders_in_kernel: the estimator / scan / privileged encoders inside the kernel too
         (actor blocks run 13 dependent layers; measured slower than running the encoders as
-        the grouped launches first and the kernel on their outputs, the default)."""
+        the grouped launches first and the kernel on their outputs, the default).
+        split (encoders outside): the critic blocks as their own launch on a side stream, beside
+        the encoders' launches, and the actor blocks after the encoders (the critic reads
+        only the critic observations)."""
         ac, est = alg.actor_critic, alg.estimator
         self.alg = alg
         self.enc_in_kernel = encoders_in_kernel
+        self.split = split and not encoders_in_kernel
+        self.side = torch.cuda.Stream(device=alg.device) if self.split else None
         dev = alg.device
         self.B = num_envs
         actor, critic = _chain(ac.actor), _chain(ac.critic)
@@ -162,6 +167,25 @@ class S8Act:
         a.priv_obs, a.ld_priv, a.n_priv_in = priv.data_ptr(), priv.stride(0), priv.shape[1]
         a.critic_obs, a.ld_critic, a.n_critic_in = critic.data_ptr(), critic.stride(0), critic.shape[1]
         a.scan_obs, a.ld_scan, a.n_scan_in = scan.data_ptr(), scan.stride(0), scan.shape[1]
+        if rows is not None:
+            src = (obs, priv, critic, est, scan)
+            for d, x in zip(rows, src):
+                if not d.is_contiguous() or d.shape != x.shape:
+                    raise S.S8LibError("S8Act: storage rows must be contiguous and shaped as the inputs")
+            a.obs_st, a.priv_st, a.critic_st, a.est_st, a.scan_st = (d.data_ptr() for d in rows)
+            a.est_obs, a.ld_est, a.n_est_obs = est.data_ptr(), est.stride(0), est.shape[1]
+        else:
+            a.obs_st = a.priv_st = a.critic_st = a.est_st = a.scan_st = a.est_obs = None
+        main = torch.cuda.current_stream()
+        if self.split:
+            # the critic blocks first, on the side stream (they overlap the encoders)
+            self.side.wait_stream(main)
+            a.nets = 2
+            with torch.cuda.stream(self.side):
+                S.act(a)
+            a.nets = 1
+        else:
+            a.nets = 0
         if not self.enc_in_kernel:
             # the estimator and the scan / privileged encoders: grouped launches writing their
             # outputs into the spans the kernel reads
@@ -172,14 +196,7 @@ class S8Act:
             p_mod, p_in = ac.privileged_encoder_.group_item(priv)
             H.forward_group([(e_mod, e_in, None, self.spans[2]), (s_mod, s_in, None, self.spans[1]),
                              (p_mod, p_in, None, self.spans[0])])
-        if rows is not None:
-            src = (obs, priv, critic, est, scan)
-            for d, x in zip(rows, src):
-                if not d.is_contiguous() or d.shape != x.shape:
-                    raise S.S8LibError("S8Act: storage rows must be contiguous and shaped as the inputs")
-            a.obs_st, a.priv_st, a.critic_st, a.est_st, a.scan_st = (d.data_ptr() for d in rows)
-            a.est_obs, a.ld_est, a.n_est_obs = est.data_ptr(), est.stride(0), est.shape[1]
-        else:
-            a.obs_st = a.priv_st = a.critic_st = a.est_st = a.scan_st = a.est_obs = None
         S.act(a)
+        if self.split:
+            main.wait_stream(self.side)
         return (self.mu if head is None else None), self.value

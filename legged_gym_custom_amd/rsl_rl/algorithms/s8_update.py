@@ -33,11 +33,14 @@ fp32 values); ELU' reads y as hi + lo (~2^-17 relative of y), the bias gradients
 tile then over tiles (a different fixed order): within the stated fp32 tolerances of the update
 (tests/test_gpu_s8_update.py), not bit-identical to the autograd path.
 """
+import os
+
 import torch
 
 from legged_gym_custom_amd.rsl_rl.modules import hip_mlp as H
 from legged_gym_custom_amd.rsl_rl.modules import hip_s8 as S
 
+ENC_CHAIN = os.environ.get("LGX_S8_CHAIN", "1") != "0"  # the encoders' forward as one chain launch
 ROW_ALIGN = 64  # minibatch rows: whole K steps of every weight-gradient chunk
 
 
@@ -168,6 +171,10 @@ class S8Minibatch:
         # critic beside the privileged / scan encoders' narrow levels: 2 / 3 / 4 slices 720 / 746
         # / 739 us per minibatch against 710 unsliced — not used)
         self.l0_slices = {"critic": 1}
+        # the privileged and scan encoders' forward as one chain launch (lgx_s8_chain_fwd)
+        # instead of their own three grouped levels
+        self.enc_chain = ENC_CHAIN and all(p.n <= S.CHAIN_MAXL and max(max(W.shape) for W in p.W) <= S.CHAIN_MAXW
+                                           for p in (self.priv, self.scan))
         self._build(shapes)
 
     # ------------------------------------------------------------------ argument lists
@@ -184,6 +191,11 @@ class S8Minibatch:
                             self.wsplit.append(S.split_job(W.detach()[:, c:c + w], S.group_ptr(Ws, s8), Ws.shape[1]))
                 else:
                     self.wsplit.append(S.split_job(W.detach(), Ws.data_ptr(), Ws.shape[1]))
+        # the chained encoders' weights also fragment-packed (the chain kernel's B loads)
+        for p in ((pr, sc) if self.enc_chain else ()):
+            p.Wp = [S.packed_empty(W.shape[0], W.shape[1], self.dev) for W in p.W]
+            for W, Wp in zip(p.W, p.Wp):
+                self.wsplit.append(S.split_packed_job(W.detach(), Wp))
         self._fwd_levels = None  # built per minibatch offset (input row pointers)
         self._shapes = shapes
 
@@ -235,8 +247,24 @@ class S8Minibatch:
 
         def put(level, args):
             levels.setdefault(level, []).append(args)
+        chains = []
         for p in (pr, sc, es, cr):
             A_ptr, lda, K = ins[p.name]
+            if self.enc_chain and p in (pr, sc):
+                c = S.ChainArgs(A=A_ptr, lda=lda, rows=mb, nlayers=p.n)
+                for l in range(p.n):
+                    W = p.W[l]
+                    L = c.layers[l]
+                    L.W, L.packed, L.bias = p.Wp[l].data_ptr(), 1, p.b[l].data_ptr()
+                    L.K, L.N, L.elu = W.shape[1], W.shape[0], int(l < p.n - 1)
+                    if l < p.n - 1:
+                        L.C, L.ldc = p.out[l].data_ptr(), p.out[l].shape[1]
+                    elif p is pr:
+                        L.C, L.ldc, L.C32, L.ldc32 = row(self.ain, self.P0), lda_ain, self.lat.data_ptr(), self.nlat
+                    else:
+                        L.C, L.ldc = row(self.ain, self.P1), lda_ain
+                chains.append(c)
+                continue
             sh = self.fwd_shift.get(p.name, 0)
             for l in range(p.n):
                 last = l == p.n - 1
@@ -272,6 +300,8 @@ class S8Minibatch:
                 A_ptr, lda, K = o.data_ptr(), o.shape[1], a.W[l].shape[0]
             else:
                 put(lev, self._fwd(a, l, A_ptr, lda, K, C32=self.mu.data_ptr(), ldc32=self.mu.shape[1], elu=False))
+        if chains:
+            S.chain_fwd(chains)
         for lev in sorted(levels):
             S.gemm_group(levels[lev], S.FWD)
         # 3. loss heads: forward sums and input gradients in one launch; the narrow output

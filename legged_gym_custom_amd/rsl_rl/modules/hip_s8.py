@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "lib", "liblgx_s8.so")
 _lib = None
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 FWD, DX, DW = 0, 1, 2
 EPI_BIAS, EPI_ELU, EPI_DELU, EPI_ACCUM = 1, 2, 4, 8
 GROUP_MAX = 20
@@ -23,7 +23,9 @@ TILE_M = 128
 SPLIT_ROWS = 256
 EXPORTED = ("lgx_s8_abi_version", "lgx_s8_sizeof_gemm_args", "lgx_s8_last_error", "lgx_s8_gemm_group",
             "lgx_s8_pick_split", "lgx_s8_split", "lgx_s8_reduce", "lgx_s8_act", "lgx_s8_act_last_error",
-            "lgx_s8_sizeof_act_args", "lgx_s8_act_pack", "lgx_s8_sizeof_act_pack_args")
+            "lgx_s8_sizeof_act_args", "lgx_s8_act_pack", "lgx_s8_sizeof_act_pack_args", "lgx_s8_chain_fwd",
+            "lgx_s8_sizeof_chain_args")
+CHAIN_MAX, CHAIN_MAXL, CHAIN_MAXW = 4, 3, 256
 ACT_ROWS, ACT_MAXIN, ACT_MAXH, ACT_MAXENC, ACT_MAXL = 32, 640, 512, 256, 6
 
 vp, i32, i64 = C.c_void_p, C.c_int32, C.c_int64
@@ -38,7 +40,7 @@ class GemmArgs(C.Structure):
 
 class SplitArgs(C.Structure):
     _fields_ = [("src", vp), ("ld_src", i64), ("dst", vp), ("ld_dst", i64), ("rows", i32), ("cols", i32),
-                ("colsum_ws", vp), ("idx", vp)]
+                ("colsum_ws", vp), ("idx", vp), ("packed_steps", i32), ("pad0", i32)]
 
 
 class ReduceArgs(C.Structure):
@@ -64,8 +66,17 @@ class ActArgs(C.Structure):
                 ("n_critic", i32), ("mu", vp), ("ld_mu", i64), ("value", vp), ("obs_st", vp), ("priv_st", vp),
                 ("scan_st", vp), ("critic_st", vp), ("est_st", vp), ("est_obs", vp), ("ld_est", i64),
                 ("n_est_obs", i32), ("pad1", i32), ("part_src", vp * 3), ("part_ld", i64 * 3), ("part_w", i32 * 3),
-                ("pad2", i32), ("std", vp), ("eps", vp), ("actions", vp), ("mu_st", vp), ("sigma_st", vp),
+                ("nets", i32), ("std", vp), ("eps", vp), ("actions", vp), ("mu_st", vp), ("sigma_st", vp),
                 ("logp_st", vp), ("actions_copy", vp), ("step_dev", vp), ("seed", C.c_uint64), ("env_offset", i64)]
+
+
+class ChainLayer(C.Structure):
+    _fields_ = [("W", vp), ("ldw", i64), ("bias", vp), ("C", vp), ("ldc", i64), ("C32", vp), ("ldc32", i64),
+                ("K", i32), ("N", i32), ("elu", i32), ("packed", i32)]
+
+
+class ChainArgs(C.Structure):
+    _fields_ = [("A", vp), ("lda", i64), ("rows", i32), ("nlayers", i32), ("layers", ChainLayer * 3)]
 
 
 def flat_reduce(ws, stride, out, n, nsplit, accumulate=0):
@@ -100,6 +111,9 @@ def load(path=_LIB_PATH):
     L.lgx_s8_act_pack.argtypes = [vp, i32, vp]
     L.lgx_s8_act_pack.restype = i32
     L.lgx_s8_sizeof_act_pack_args.restype = i32
+    L.lgx_s8_chain_fwd.argtypes = [vp, i32, vp]
+    L.lgx_s8_chain_fwd.restype = i32
+    L.lgx_s8_sizeof_chain_args.restype = i32
     if L.lgx_s8_abi_version() != ABI_VERSION:
         raise S8LibError("liblgx_s8 ABI version mismatch; rebuild")
     if L.lgx_s8_sizeof_gemm_args() != C.sizeof(GemmArgs):
@@ -107,6 +121,8 @@ def load(path=_LIB_PATH):
                          f"{C.sizeof(GemmArgs)}")
     if L.lgx_s8_sizeof_act_pack_args() != C.sizeof(ActPackArgs):
         raise S8LibError("lgx_s8_act_pack_args layout mismatch")
+    if L.lgx_s8_sizeof_chain_args() != C.sizeof(ChainArgs):
+        raise S8LibError("lgx_s8_chain_args layout mismatch")
     if L.lgx_s8_sizeof_act_args() != C.sizeof(ActArgs):
         raise S8LibError(f"lgx_s8_act_args layout mismatch: C {L.lgx_s8_sizeof_act_args()} vs ctypes "
                          f"{C.sizeof(ActArgs)}")
@@ -215,6 +231,13 @@ def reduce(jobs, L=None):
         _check(L.lgx_s8_reduce(arr, len(chunk), _stream()), "lgx_s8_reduce")
 
 
+def chain_fwd(chains, L=None):
+    """lgx_s8_chain_fwd: up to CHAIN_MAX narrow forward chains in one launch ([ChainArgs])."""
+    L = lib() if L is None else L
+    arr = (ChainArgs * len(chains))(*chains)
+    _check(L.lgx_s8_chain_fwd(arr, len(chains), _stream()), "lgx_s8_chain_fwd")
+
+
 def act(args, L=None):
     """lgx_s8_act: the rollout's act networks in one launch (ActArgs)."""
     L = lib() if L is None else L
@@ -230,6 +253,19 @@ def act_pack(jobs, L=None):
         arr = (ActPackArgs * len(chunk))(*chunk)
         if L.lgx_s8_act_pack(arr, len(chunk), _stream()) != 0:
             raise S8LibError("lgx_s8_act_pack: " + L.lgx_s8_act_last_error().decode())
+
+
+def packed_empty(N, K, device):
+    """A zeroed fragment-packed S8 weight buffer for [N, K] (lgx_s8_chain_layer.packed)."""
+    return torch.zeros((N + 15) // 16 * ((K + 31) // 32) * 512, dtype=torch.int32, device=device)
+
+
+def split_packed_job(W, dst):
+    """SplitArgs: fp32 weight [N, K] -> its fragment-packed S8 copy (packed_empty)."""
+    if W.stride(1) != 1 or W.dtype != torch.float32:
+        raise S8LibError("split: fp32 with unit column stride")
+    return SplitArgs(src=W.data_ptr(), ld_src=W.stride(0), dst=dst.data_ptr(), ld_dst=0, rows=W.shape[0],
+                     cols=W.shape[1], packed_steps=(W.shape[1] + 31) // 32)
 
 
 def split_job(src, dst_ptr, ld_dst, colsum_ws=None, idx=None, rows=None):

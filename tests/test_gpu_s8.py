@@ -240,3 +240,92 @@ def test_loss_heads_fused_equals_forward_plus_backward(S):
     for cs, full in ((cs_mu, ref["dmu"]), (cs_v, ref["dvalue"].view(B, 1)), (cs_e, ref["de"])):
         blocks = torch.stack([full[i:i + 256].double().sum(0) for i in range(0, B, 256)])
         torch.testing.assert_close(cs.double(), blocks, rtol=1e-5, atol=1e-6)
+
+
+def _pack_ref(Ws, N, K):
+    """Fragment packing of an S8 weight buffer in torch (lgx_s8_chain_layer.packed)."""
+    T, st = (N + 15) // 16, (K + 31) // 32
+    r, ld = Ws.shape
+    b = torch.zeros(T * 16, st * 32 // 8, 2, 8, dtype=torch.bfloat16, device=Ws.device)
+    src = Ws.view(torch.bfloat16).view(r, ld // 8, 2, 8)
+    g = min(st * 4, ld // 8)
+    b[:N, :g] = src[:N, :g]
+    # [tile, fr, step, fc, 2, 8] -> [tile, step, 2, fc, fr, 8]
+    b = b.view(T, 16, st, 4, 2, 8).permute(0, 2, 4, 3, 1, 5).contiguous()
+    return b.view(-1).view(torch.int32)
+
+
+def test_split_packed_matches_reference(S):
+    g = torch.Generator(device="cpu").manual_seed(5)
+    for N, K in ((128, 132), (20, 64), (64, 29), (33, 200)):
+        W = torch.randn(N, K, generator=g).to(dev)
+        Wp = S.packed_empty(N, K, dev)
+        S.split([S.split_packed_job(W, Wp)])
+        torch.cuda.synchronize()
+        assert torch.equal(Wp, _pack_ref(S.to_s8_torch(W), N, K)), (N, K)
+
+
+@pytest.mark.parametrize("rows,packed", [(1000, 0), (1000, 1), (24576, 1)])
+def test_chain_fwd_equals_grouped_levels(S, rows, packed):
+    """lgx_s8_chain_fwd (the privileged / scan encoders' forward in one launch) against the same
+    layers as one grouped FWD launch each: S8 outputs (hidden layers, the last one at a column
+    offset of a wider buffer, pads zero), the fp32 copy, bit for bit."""
+    g = torch.Generator(device="cpu").manual_seed(rows)
+    shapes = {"scan": [132, 128, 64, 32], "priv": [29, 64, 20]}
+    wide = S.empty(rows, 96, dev)  # the last layers' outputs: columns 0 (scan) and 40 (priv)
+    wide_ref = S.empty(rows, 96, dev)
+    chains, outs = [], {}
+    for name, col in (("scan", 0), ("priv", 40)):
+        w = shapes[name]
+        x = S.to_s8_torch(torch.randn(rows, w[0], generator=g).to(dev))
+        W32 = [(torch.randn(n, k, generator=g) * 0.2).to(dev) for k, n in zip(w[:-1], w[1:])]
+        Ws = [S.to_s8_torch(W) for W in W32]
+        Wp = [S.packed_empty(W.shape[0], W.shape[1], dev) for W in W32]
+        S.split([S.split_packed_job(W, P) for W, P in zip(W32, Wp)])
+        bs = [torch.randn(n, generator=g).to(dev) for n in w[1:]]
+        hid = [S.empty(rows, n, dev) for n in w[1:-1]]
+        hid_ref = [S.empty(rows, n, dev) for n in w[1:-1]]
+        y32, y32_ref = torch.full((rows, w[-1]), float("nan"), device=dev), torch.full((rows, w[-1]), 7.0, device=dev)
+        c = S.ChainArgs(A=x.data_ptr(), lda=x.shape[1], rows=rows, nlayers=len(w) - 1)
+        A, lda = x, x.shape[1]
+        for l, (k, n) in enumerate(zip(w[:-1], w[1:])):
+            last = l == len(w) - 2
+            L = c.layers[l]
+            L.W, L.ldw, L.bias, L.K, L.N, L.elu = Ws[l].data_ptr(), Ws[l].shape[1], bs[l].data_ptr(), k, n, int(not last)
+            if packed:
+                L.W, L.packed = Wp[l].data_ptr(), 1
+            if last:
+                L.C, L.ldc, L.C32, L.ldc32 = S.group_ptr(wide, col), wide.shape[1], y32.data_ptr(), n
+                ref_c, ref_ldc = S.group_ptr(wide_ref, col), wide_ref.shape[1]
+            else:
+                L.C, L.ldc = hid[l].data_ptr(), hid[l].shape[1]
+                ref_c, ref_ldc = hid_ref[l].data_ptr(), hid_ref[l].shape[1]
+            S.gemm_group([S.GemmArgs(A=A.data_ptr(), lda=lda, B=Ws[l].data_ptr(), ldb=Ws[l].shape[1], M=rows, N=n, K=k,
+                                     epilogue=S.EPI_BIAS | (0 if last else S.EPI_ELU), C=ref_c, ldc=ref_ldc,
+                                     C32=y32_ref.data_ptr() if last else None, ldc32=n if last else 0,
+                                     bias=bs[l].data_ptr())], S.FWD)
+            if not last:
+                A, lda = hid_ref[l], hid_ref[l].shape[1]
+        chains.append(c)
+        outs[name] = (hid, hid_ref, y32, y32_ref, x, Ws, Wp, bs)  # (the chain reads x, Ws, bs at launch)
+    S.chain_fwd(chains)
+    torch.cuda.synchronize()
+    for name, (hid, hid_ref, y32, y32_ref, *_keep) in outs.items():
+        for h, hr in zip(hid, hid_ref):
+            assert torch.equal(h, hr), name
+        assert torch.equal(y32, y32_ref), name
+    assert torch.equal(wide, wide_ref)
+
+
+def test_chain_fwd_rejects_bad_arguments(S):
+    x = S.empty(64, 40, dev)
+    W = S.empty(16, 40, dev)
+    c = S.ChainArgs(A=x.data_ptr(), lda=x.shape[1], rows=64, nlayers=2)
+    c.layers[0] = S.ChainLayer(W=W.data_ptr(), ldw=W.shape[1], K=40, N=16)
+    c.layers[1] = S.ChainLayer(W=W.data_ptr(), ldw=W.shape[1], K=40, N=16)  # K != previous N
+    with pytest.raises(S.S8LibError, match="K_l"):
+        S.chain_fwd([c])
+    c.nlayers = 1
+    c.layers[0].K = 300  # wider than the chain's image
+    with pytest.raises(S.S8LibError):
+        S.chain_fwd([c])

@@ -31,6 +31,11 @@ def main():
         libs[v.split("/")[-1]] = S.load(v)
     res = timeit_many({k: (lambda L=L: S.act(fa.args, L)) for k, L in libs.items()}, n=20, rounds=5)
     print(json.dumps(res))
+    # fewer blocks per XCD (the first rows only): per-CU vs per-XCD bound
+    for b in (2048, 1024, 256, 32):
+        fa.args.B = b
+        print(b, json.dumps(timeit_many({"product": lambda: S.act(fa.args)}, n=20, rounds=3)))
+    fa.args.B = N
 
 
 if __name__ == "__main__":
