@@ -43,6 +43,7 @@ from .s8_update import S8Minibatch
 USE_S8 = os.environ.get("LGX_S8_UPDATE", "1") != "0"
 # the rollout's act networks in one launch (s8_act.py); "0" selects the grouped launches
 USE_FUSED_ACT = os.environ.get("LGX_FUSED_ACT", "1") != "0"
+ACT_ENC = os.environ.get("LGX_ACT_ENC_IN_KERNEL", "0") != "0"  # s8_act.py: encoders inside the act kernel
 ACT_SPLIT = os.environ.get("LGX_ACT_SPLIT", "0") != "0"  # s8_act.py: critic launch beside the encoders (measured slower)
 # under RCCL ("nccl"), the per-minibatch gradient all-reduce is captured inside the one update
 # graph; "0" keeps the phased graphs (per-minibatch replays around host-issued all-reduces)
@@ -381,7 +382,7 @@ class PPO:
             return self._s8act
         if torch.cuda.is_current_stream_capturing() or not S8Act.supported(self):
             return None
-        self._s8act = S8Act(self, n, split=ACT_SPLIT)
+        self._s8act = S8Act(self, n, encoders_in_kernel=ACT_ENC, split=ACT_SPLIT)
         return self._s8act
 
     def _gpu_rollout(self):
