@@ -76,7 +76,8 @@ typedef struct lgx_s8_split_args {
   const int64_t* idx;           /* optional row gather (rollout_storage.py:141-147's permutation) */
   int32_t packed_steps;         /* > 0: dst is fragment-packed (a chain's weights, below) with this
                                    many 32-deep K steps per 16-row tile; ld_dst unused */
-  int32_t pad0;
+  int32_t transpose;            /* packed only: dst = src^T (src [cols][rows]: an input-gradient
+                                   chain's W^T) */
 } lgx_s8_split_args;
 
 /* out[r * ld_out + c] (+)= sum_{s < nsplit} ws[s * stride + r * ld_ws + c], r < rows, c < cols
@@ -173,14 +174,18 @@ const char* lgx_s8_act_last_error(void);
 int32_t lgx_s8_sizeof_act_args(void);
 int32_t lgx_s8_sizeof_act_pack_args(void);
 
-/* Forward chains (lgx_s8chain.hip): the narrow encoders of the update's forward pass (the
- * privileged and scan encoders, support_networks.py:25-80, as PPO.update runs them in
- * ppo.py:201-233) as ONE launch instead of one grouped launch per depth. Per chain: A = the
- * S8 input rows [rows][>= K_0] (pitch lda elements), then up to LGX_S8_CHAIN_MAXL layers
- * y_l = act(y_{l-1} W_l^T + b_l) with W_l S8 [N_l][ldw_l], K_l = N_{l-1}; each layer's output
- * goes to C_l (S8, pitch ldc_l, pads zero; may be null) and / or C32_l (fp32; may be null).
- * Same operand contract and epilogue as lgx_s8_gemm_group FWD (bias, ELU, zero pad columns;
- * the same 3 x bf16 products per 32-deep K step); widths <= LGX_S8_CHAIN_MAXW. */
+/* Chains (lgx_s8chain.hip): the narrow encoders of the update (the privileged and scan
+ * encoders, support_networks.py:25-80, as PPO.update runs them in ppo.py:201-233) as ONE launch
+ * instead of one grouped launch per depth — their forward, and their input gradients. Per
+ * chain: A = the S8 input rows [rows][>= K_0] (pitch lda elements; columns past K_0 are read as
+ * zero), then up to LGX_S8_CHAIN_MAXL layers y_l = epi(y_{l-1} W_l^T + b_l) with W_l S8
+ * [N_l][ldw_l] (or fragment-packed), K_l = N_{l-1}. epi (`elu`): 0 none, 1 ELU (forward), 2
+ * times ELU'(act) with act the S8 ELU output at the same rows (input gradient: W_l = the
+ * forward weight transposed, bias null). Each layer's output goes to C_l (S8, pitch ldc_l,
+ * pads zero; may be null) and / or C32_l (fp32; may be null); colsum_ws (optional, every
+ * layer of the launch or none): the column sums of each 128-row tile, colsum_ws[tile * N + n]
+ * (lgx_s8_gemm_group's tile partials). Same operand contract, products and epilogues as
+ * lgx_s8_gemm_group; widths <= LGX_S8_CHAIN_MAXW (<= 128 with column sums). */
 #define LGX_S8_CHAIN_MAX 4
 #define LGX_S8_CHAIN_MAXL 3
 #define LGX_S8_CHAIN_MAXW 256
@@ -189,6 +194,8 @@ typedef struct lgx_s8_chain_layer {
   const float* bias;
   void* C; int64_t ldc;         /* S8 output (or null) */
   float* C32; int64_t ldc32;    /* fp32 output (or null) */
+  const void* act; int64_t ld_act;  /* S8 ELU output for elu = 2 */
+  float* colsum_ws;
   int32_t K, N, elu;
   int32_t packed;               /* W fragment-packed (lgx_s8_split packed_steps = ceil(K / 32)):
                                    per (16-row tile, K step) 2 KB = 64 lanes x 16 B hi, then lo */
@@ -198,7 +205,7 @@ typedef struct lgx_s8_chain_args {
   int32_t rows, nlayers;
   lgx_s8_chain_layer layers[LGX_S8_CHAIN_MAXL];
 } lgx_s8_chain_args;
-int32_t lgx_s8_chain_fwd(const lgx_s8_chain_args* chains, int32_t n, void* stream);
+int32_t lgx_s8_chain(const lgx_s8_chain_args* chains, int32_t n, void* stream);
 int32_t lgx_s8_sizeof_chain_args(void);
 
 #ifdef __cplusplus

@@ -441,6 +441,7 @@ struct SplitJob {
   const int64_t* idx;
   int blk0;     // first block of this job
   int psteps;   // > 0: fragment-packed destination (lgx_s8_chain_layer.packed)
+  int tr;       // packed only: src is [cols][rows] (the destination is its transpose)
 };
 struct SplitBatch {
   int n;
@@ -460,6 +461,11 @@ __global__ __launch_bounds__(256) void s8_split_kernel(SplitBatch b) {
   const int G = (J.cols + 7) / 8;
   const int tid = threadIdx.x;
   auto load8 = [&](int r, int gg, float (&v)[8]) {
+    if (J.tr) {  // element (r, c) = src[c][r]
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = 8 * gg + e < J.cols ? J.src[(int64_t)(8 * gg + e) * J.ld_src + r] : 0.f;
+      return;
+    }
     const int64_t sr = J.idx ? J.idx[r] : r;
     const float* s = J.src + sr * J.ld_src + 8 * gg;
     if (8 * gg + 8 <= J.cols) {
@@ -697,13 +703,14 @@ int32_t lgx_s8_split(const lgx_s8_split_args* a, int32_t n, void* stream) {
     if (q.rows < 0 || q.cols < 0) return fail("lgx_s8_split: negative size");
     if (q.rows == 0 || q.cols == 0) continue;
     if (!q.src || !q.dst) return fail("lgx_s8_split: null pointer");
-    if (q.packed_steps < 0 || (q.packed_steps && (q.packed_steps < cdiv(q.cols, 32) || q.colsum_ws || q.idx)))
-      return fail("lgx_s8_split: packed_steps >= ceil(cols / 32), no column sums or gather");
+    if (q.packed_steps < 0 || (q.packed_steps && (q.packed_steps < cdiv(q.cols, 32) || q.colsum_ws || q.idx)) ||
+        (q.transpose && !q.packed_steps))
+      return fail("lgx_s8_split: packed_steps >= ceil(cols / 32), no column sums or gather; transpose packed only");
     if ((((uintptr_t)q.dst) & 15) || (!q.packed_steps && (q.ld_dst % 8 || q.ld_dst < cdiv(q.cols, 8) * 8)))
       return fail("lgx_s8_split: S8 destination alignment / pitch");
     if (q.colsum_ws && q.cols > 64) return fail("lgx_s8_split: column sums for <= 64 columns only");
     b.j[k] = lgxs::SplitJob{q.src, q.ld_src, (char*)q.dst, q.ld_dst * 4, q.rows, q.cols, q.colsum_ws, q.idx, blocks,
-                            q.packed_steps};
+                            q.packed_steps, q.transpose != 0};
     const int64_t G = cdiv(q.cols, 8);
     blocks += G <= 8 ? cdiv(q.rows, LGX_S8_SPLIT_ROWS) : (int)((q.rows * G + LGX_S8_SPLIT_WIDE - 1) / LGX_S8_SPLIT_WIDE);
     ++k;

@@ -1,5 +1,5 @@
 // lgx_s8chain.hip — the update's narrow forward chains in one launch, gfx950 (include/lgx_s8.h
-// lgx_s8_chain_fwd).
+// lgx_s8_chain).
 //
 // The privileged and scan encoders (support_networks.py:25-80) are 2-3 layers of <= 132 inputs:
 // as grouped launches (one per depth, lgx_s8.hip) every level is a few-microsecond kernel bound
@@ -30,13 +30,7 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 namespace lgxc {
 
-#ifndef LGX_S8_CHAIN_BR
-#define LGX_S8_CHAIN_BR 32
-#endif
-constexpr int BR = LGX_S8_CHAIN_BR;            // rows per block
-constexpr int MI = BR / 16;                    // 16-row MFMA tiles
 constexpr int NT = 256;                        // 4 waves
-constexpr int IP = LGX_S8_CHAIN_MAXW + 8;      // image pitch (bf16): fragment reads conflict-free
 constexpr int CMAX = LGX_S8_CHAIN_MAX;
 #ifndef LGX_S8_CHAIN_D
 #define LGX_S8_CHAIN_D 2
@@ -69,11 +63,17 @@ struct BSet {
 };
 
 // NJW = output tiles per wave (16 columns each): the launch's widest layer / 64, rounded up to
-// 1, 2 or 4 (the registers of the narrow chains' launches stay few: 4 waves per SIMD)
-template <int NJW>
-__global__ __launch_bounds__(NT) void chain_fwd_kernel(Params P) {
+// 1, 2 or 4 (the registers of the narrow chains' launches stay few: 4 waves per SIMD). BR = rows
+// per block: 32, or 128 when the launch writes column sums (one block per 128-row tile: the
+// partials are lgx_s8_gemm_group's). IPW = the image's width (its pitch IPW + 8 bf16: fragment
+// reads conflict-free).
+template <int NJW, int BR, int IPW>
+__global__ __launch_bounds__(NT) void chain_kernel(Params P) {
+  constexpr int MI = BR / 16, IP = IPW + 8;
+  constexpr bool DX = BR == 128;  // the input-gradient launches: ELU' epilogue, column sums
   __shared__ __align__(16) __bf16 ih[BR * IP];
   __shared__ __align__(16) __bf16 il[BR * IP];
+  __shared__ float red[DX ? 4 : 1][DX ? IPW : 1];  // column-sum partials of the 4 lane groups
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, fc = lane >> 4;
   const int blk = blockIdx.x;
@@ -83,13 +83,15 @@ __global__ __launch_bounds__(NT) void chain_fwd_kernel(Params P) {
   const lgx_s8_chain_args& c = P.c[ci];
   const int rows = c.rows, r0 = (blk - P.start[ci]) * BR;
 
-  {  // the input rows' S8 groups -> the image (clamped rows; past K the operand's zero pads)
-    const int G = (c.layers[0].K + 31) / 32 * 4;
+  {  // the input rows' S8 groups -> the image (clamped rows; zero past K: the input may be a
+     // column span of a wider buffer)
+    const int G = (c.layers[0].K + 31) / 32 * 4, GK = (c.layers[0].K + 7) / 8;
     const char* A = (const char*)c.A;
     for (int idx = tid; idx < BR * G; idx += NT) {
       const int r = idx / G, g = idx % G;
-      const char* q = A + (int64_t)std::min(r0 + r, rows - 1) * c.lda * 4 + g * 32;
-      const u32x4 h = reinterpret_cast<const u32x4*>(q)[0], l = reinterpret_cast<const u32x4*>(q)[1];
+      const char* q = A + (int64_t)std::min(r0 + r, rows - 1) * c.lda * 4 + std::min(g, GK - 1) * 32;
+      u32x4 h = reinterpret_cast<const u32x4*>(q)[0], l = reinterpret_cast<const u32x4*>(q)[1];
+      if (g >= GK) h = l = u32x4{0u, 0u, 0u, 0u};
       *reinterpret_cast<u32x4*>(ih + r * IP + 8 * g) = h;
       *reinterpret_cast<u32x4*>(il + r * IP + 8 * g) = l;
     }
@@ -164,27 +166,43 @@ __global__ __launch_bounds__(NT) void chain_fwd_kernel(Params P) {
     }
     __syncthreads();  // every wave is done reading the image
 
-    // epilogue: bias (+ ELU), zero pad columns; fp32 rows out, the split back into the image
+    // epilogue: bias (+ ELU) or times ELU'(act), zero pad columns; fp32 rows out, the split back
+    // into the image, the column sums of the block's valid rows
+    const char* act = (const char*)L.act;
 #pragma unroll
     for (int j = 0; j < NJW; ++j) {
       if (!tv[j]) continue;
       const int col = 16 * (wave + 4 * j) + fr;
       const float bias = col < N && L.bias != nullptr ? L.bias[col] : 0.f;
+      float cs = 0.f;
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int row = 16 * i + 4 * fc + r;
           float v = acc[i][j][r] + bias;
-          if (L.elu) v = elu(v);
+          if (!DX && L.elu == 1) {
+            v = elu(v);
+          } else if (DX && L.elu == 2) {  // y = hi + lo of the S8 ELU output (lgx_s8.hip load_s8)
+            const unsigned short* q = reinterpret_cast<const unsigned short*>(
+                act + (int64_t)std::min(r0 + row, rows - 1) * L.ld_act * 4 + (std::min(col, N - 1) >> 3) * 32 +
+                (std::min(col, N - 1) & 7) * 2);
+            const float y = __uint_as_float((unsigned)q[0] << 16) + __uint_as_float((unsigned)q[8] << 16);
+            v *= y > 0.f ? 1.f : y + 1.f;
+          }
           v = col < N ? v : 0.f;
+          if (DX && r0 + row < rows) cs += v;
           if (L.C32 != nullptr && col < N && r0 + row < rows) L.C32[(int64_t)(r0 + row) * L.ldc32 + col] = v;
           const __bf16 h = (__bf16)v;
           ih[row * IP + col] = h;
           il[row * IP + col] = (__bf16)(v - (float)h);
         }
+      if constexpr (DX) red[fc][col] = cs;
     }
     __syncthreads();
+    if (DX && L.colsum_ws != nullptr)  // the 4 lane groups' partials in order: one 128-row tile's sums
+      for (int n = tid; n < N; n += NT)
+        L.colsum_ws[(int64_t)(r0 / BR) * N + n] = ((red[0][n] + red[1][n]) + red[2][n]) + red[3][n];
     if (L.C != nullptr) {  // the image's groups -> S8 rows (hi 16 B | lo 16 B)
       const int G = (N + 7) / 8;
       char* C = (char*)L.C;
@@ -205,39 +223,57 @@ extern "C" {
 
 int32_t lgx_s8_sizeof_chain_args(void) { return (int32_t)sizeof(lgx_s8_chain_args); }
 
-int32_t lgx_s8_chain_fwd(const lgx_s8_chain_args* chains, int32_t n, void* stream) {
-  if (n < 1 || n > LGX_S8_CHAIN_MAX || chains == nullptr) return lgxs_fail("lgx_s8_chain_fwd: 1 <= n <= LGX_S8_CHAIN_MAX");
+int32_t lgx_s8_chain(const lgx_s8_chain_args* chains, int32_t n, void* stream) {
+  if (n < 1 || n > LGX_S8_CHAIN_MAX || chains == nullptr) return lgxs_fail("lgx_s8_chain: 1 <= n <= LGX_S8_CHAIN_MAX");
   lgxc::Params P{};
   P.n = n;
-  int tot = 0, wmax = 0;
+  int tot = 0, wmax = 0, nmax = 0, ncs = 0, nl = 0;
   for (int i = 0; i < n; ++i) {
     const lgx_s8_chain_args& c = chains[i];
     if (c.A == nullptr || c.rows < 1 || c.nlayers < 1 || c.nlayers > LGX_S8_CHAIN_MAXL)
-      return lgxs_fail("lgx_s8_chain_fwd: input, rows >= 1, 1 <= nlayers <= LGX_S8_CHAIN_MAXL");
+      return lgxs_fail("lgx_s8_chain: input, rows >= 1, 1 <= nlayers <= LGX_S8_CHAIN_MAXL");
     if ((reinterpret_cast<uintptr_t>(c.A) & 15) || c.lda < (c.layers[0].K + 31) / 32 * 32)
-      return lgxs_fail("lgx_s8_chain_fwd: input pitch >= K rounded up to 32, 16-B aligned");
+      return lgxs_fail("lgx_s8_chain: input pitch >= K rounded up to 32, 16-B aligned");
     for (int l = 0; l < c.nlayers; ++l) {
       const lgx_s8_chain_layer& L = c.layers[l];
       if (L.K < 1 || L.N < 1 || L.K > LGX_S8_CHAIN_MAXW || L.N > LGX_S8_CHAIN_MAXW)
-        return lgxs_fail("lgx_s8_chain_fwd: 1 <= K, N <= LGX_S8_CHAIN_MAXW");
-      if (l > 0 && L.K != c.layers[l - 1].N) return lgxs_fail("lgx_s8_chain_fwd: K_l must equal N_{l-1}");
+        return lgxs_fail("lgx_s8_chain: 1 <= K, N <= LGX_S8_CHAIN_MAXW");
+      if (l > 0 && L.K != c.layers[l - 1].N) return lgxs_fail("lgx_s8_chain: K_l must equal N_{l-1}");
       if (L.W == nullptr || (reinterpret_cast<uintptr_t>(L.W) & 15) || (!L.packed && L.ldw < (L.K + 31) / 32 * 32))
-        return lgxs_fail("lgx_s8_chain_fwd: weight pitch >= K rounded up to 32, 16-B aligned");
+        return lgxs_fail("lgx_s8_chain: weight pitch >= K rounded up to 32, 16-B aligned");
       if (L.C != nullptr && ((reinterpret_cast<uintptr_t>(L.C) & 15) || L.ldc % 8 || L.ldc < (L.N + 7) / 8 * 8))
-        return lgxs_fail("lgx_s8_chain_fwd: S8 output pitch a multiple of 8, >= N, 16-B aligned");
-      if (L.C32 != nullptr && L.ldc32 < L.N) return lgxs_fail("lgx_s8_chain_fwd: fp32 output pitch >= N");
-      wmax = std::max(wmax, (L.N + 31) / 32 * 32);
+        return lgxs_fail("lgx_s8_chain: S8 output pitch a multiple of 8, >= N, 16-B aligned");
+      if (L.C32 != nullptr && L.ldc32 < L.N) return lgxs_fail("lgx_s8_chain: fp32 output pitch >= N");
+      if (L.elu < 0 || L.elu > 2 || (L.elu == 2 && (L.act == nullptr || L.ld_act < (L.N + 7) / 8 * 8)))
+        return lgxs_fail("lgx_s8_chain: elu 0 / 1 / 2 (2: the S8 activation, pitch >= N)");
+      if ((L.elu == 2) != (L.colsum_ws != nullptr))
+        return lgxs_fail("lgx_s8_chain: column sums exactly on the ELU' (input-gradient) layers");
+      nmax = std::max(nmax, (L.N + 31) / 32 * 32);  // output tiles per wave
+      wmax = std::max(wmax, std::max((L.N + 31) / 32 * 32, (L.K + 31) / 32 * 32));  // the image
+      ncs += L.colsum_ws != nullptr;
+      ++nl;
     }
     P.c[i] = c;
+  }
+  if (ncs && (ncs != nl || wmax > 128 || nmax > 128))
+    return lgxs_fail("lgx_s8_chain: column sums on every layer or none, widths <= 128 with them");
+  const int br = ncs ? 128 : 32;
+  for (int i = 0; i < n; ++i) {
     P.start[i] = tot;
-    tot += (c.rows + lgxc::BR - 1) / lgxc::BR;
+    tot += (chains[i].rows + br - 1) / br;
   }
   P.start[n] = tot;
   const hipStream_t s = (hipStream_t)stream;
-  if (wmax <= 64) hipLaunchKernelGGL(lgxc::chain_fwd_kernel<1>, dim3(tot), dim3(lgxc::NT), 0, s, P);
-  else if (wmax <= 128) hipLaunchKernelGGL(lgxc::chain_fwd_kernel<2>, dim3(tot), dim3(lgxc::NT), 0, s, P);
-  else hipLaunchKernelGGL(lgxc::chain_fwd_kernel<4>, dim3(tot), dim3(lgxc::NT), 0, s, P);
-  return lgxs_launched("lgx_s8_chain_fwd");
+  const dim3 g(tot), b(lgxc::NT);
+  if (ncs) {
+    if (nmax <= 64) hipLaunchKernelGGL((lgxc::chain_kernel<1, 128, 128>), g, b, 0, s, P);
+    else hipLaunchKernelGGL((lgxc::chain_kernel<2, 128, 128>), g, b, 0, s, P);
+  } else {
+    if (nmax <= 64) hipLaunchKernelGGL((lgxc::chain_kernel<1, 32, 256>), g, b, 0, s, P);
+    else if (nmax <= 128) hipLaunchKernelGGL((lgxc::chain_kernel<2, 32, 256>), g, b, 0, s, P);
+    else hipLaunchKernelGGL((lgxc::chain_kernel<4, 32, 256>), g, b, 0, s, P);
+  }
+  return lgxs_launched("lgx_s8_chain");
 }
 
 }  // extern "C"

@@ -41,6 +41,9 @@ from legged_gym_custom_amd.rsl_rl.modules import hip_mlp as H
 from legged_gym_custom_amd.rsl_rl.modules import hip_s8 as S
 
 ENC_CHAIN = os.environ.get("LGX_S8_CHAIN", "1") != "0"  # the encoders' forward as one chain launch
+# their input gradients as one chain launch too (128-row blocks for the column sums: measured
+# 104 us against 31 us for the two grouped levels — one wave per SIMD waits on the ELU' loads)
+ENC_CHAIN_DX = os.environ.get("LGX_S8_CHAIN_DX", "0") != "0"
 ROW_ALIGN = 64  # minibatch rows: whole K steps of every weight-gradient chunk
 
 
@@ -171,10 +174,12 @@ class S8Minibatch:
         # critic beside the privileged / scan encoders' narrow levels: 2 / 3 / 4 slices 720 / 746
         # / 739 us per minibatch against 710 unsliced — not used)
         self.l0_slices = {"critic": 1}
-        # the privileged and scan encoders' forward as one chain launch (lgx_s8_chain_fwd)
+        # the privileged and scan encoders' forward as one chain launch (lgx_s8_chain)
         # instead of their own three grouped levels
         self.enc_chain = ENC_CHAIN and all(p.n <= S.CHAIN_MAXL and max(max(W.shape) for W in p.W) <= S.CHAIN_MAXW
                                            for p in (self.priv, self.scan))
+        self.enc_chain_dx = self.enc_chain and ENC_CHAIN_DX and all(
+            max(max(W.shape) for W in p.W[1:]) <= 128 for p in (self.priv, self.scan))
         self._build(shapes)
 
     # ------------------------------------------------------------------ argument lists
@@ -192,10 +197,15 @@ class S8Minibatch:
                 else:
                     self.wsplit.append(S.split_job(W.detach(), Ws.data_ptr(), Ws.shape[1]))
         # the chained encoders' weights also fragment-packed (the chain kernel's B loads)
+        # (forward), and their transposes (input gradients of the layers past the first)
         for p in ((pr, sc) if self.enc_chain else ()):
             p.Wp = [S.packed_empty(W.shape[0], W.shape[1], self.dev) for W in p.W]
             for W, Wp in zip(p.W, p.Wp):
                 self.wsplit.append(S.split_packed_job(W.detach(), Wp))
+        for p in ((pr, sc) if self.enc_chain_dx else ()):
+            p.WpT = [None] + [S.packed_empty(W.shape[1], W.shape[0], self.dev) for W in p.W[1:]]
+            for W, WpT in zip(p.W[1:], p.WpT[1:]):
+                self.wsplit.append(S.split_packed_job(W.detach(), WpT, transpose=True))
         self._fwd_levels = None  # built per minibatch offset (input row pointers)
         self._shapes = shapes
 
@@ -301,7 +311,7 @@ class S8Minibatch:
             else:
                 put(lev, self._fwd(a, l, A_ptr, lda, K, C32=self.mu.data_ptr(), ldc32=self.mu.shape[1], elu=False))
         if chains:
-            S.chain_fwd(chains)
+            S.chain(chains)
         for lev in sorted(levels):
             S.gemm_group(levels[lev], S.FWD)
         # 3. loss heads: forward sums and input gradients in one launch; the narrow output
@@ -355,7 +365,19 @@ class S8Minibatch:
         lev_lat = a.n - 1
         bput(lev_lat, dx(a, 0, a.dy[0], self.dlat.data_ptr(), self.cs_lat, N=self.P2 - self.P0,
                          Bptr=S.group_ptr(a.Ws[0], self.P0), elu=False, addend=self.dp))
+        dchains = []
         for p, c0 in ((pr, 0), (sc, self.P1 - self.P0)):
+            if self.enc_chain_dx:
+                # the encoder's input gradients, all layers in one chain launch (after the
+                # levels): dy_{l-1} = (dy_l W_l) * ELU'(y_{l-1}), the 128-row column sums
+                c = S.ChainArgs(A=S.group_ptr(self.dlat, c0), lda=self.dlat.shape[1], rows=mb, nlayers=p.n - 1)
+                for q, l in enumerate(range(p.n - 1, 0, -1)):
+                    L = c.layers[q]
+                    L.W, L.packed, L.K, L.N, L.elu = p.WpT[l].data_ptr(), 1, p.W[l].shape[0], p.W[l].shape[1], 2
+                    L.act, L.ld_act = p.out[l - 1].data_ptr(), p.out[l - 1].shape[1]
+                    L.C, L.ldc, L.colsum_ws = p.dy[l - 1].data_ptr(), p.dy[l - 1].shape[1], p.cs[l - 1].data_ptr()
+                dchains.append(c)
+                continue
             for l in range(p.n - 1, 0, -1):
                 dy = self.dlat if l == p.n - 1 else p.dy[l]
                 if l == p.n - 1:
@@ -369,6 +391,8 @@ class S8Minibatch:
                 bput(lev_lat + 1 + (p.n - 1 - l), args)
         for lev in sorted(blev):
             S.gemm_group(blev[lev], S.DX)
+        if dchains:
+            S.chain(dchains)
         # 5. weight gradients (one launch) and the reductions into the flat gradient buffer
         g_args, red = [], []
         off = 0

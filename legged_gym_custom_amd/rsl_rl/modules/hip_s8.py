@@ -23,7 +23,7 @@ TILE_M = 128
 SPLIT_ROWS = 256
 EXPORTED = ("lgx_s8_abi_version", "lgx_s8_sizeof_gemm_args", "lgx_s8_last_error", "lgx_s8_gemm_group",
             "lgx_s8_pick_split", "lgx_s8_split", "lgx_s8_reduce", "lgx_s8_act", "lgx_s8_act_last_error",
-            "lgx_s8_sizeof_act_args", "lgx_s8_act_pack", "lgx_s8_sizeof_act_pack_args", "lgx_s8_chain_fwd",
+            "lgx_s8_sizeof_act_args", "lgx_s8_act_pack", "lgx_s8_sizeof_act_pack_args", "lgx_s8_chain",
             "lgx_s8_sizeof_chain_args")
 CHAIN_MAX, CHAIN_MAXL, CHAIN_MAXW = 4, 3, 256
 ACT_ROWS, ACT_MAXIN, ACT_MAXH, ACT_MAXENC, ACT_MAXL = 32, 640, 512, 256, 6
@@ -40,7 +40,7 @@ class GemmArgs(C.Structure):
 
 class SplitArgs(C.Structure):
     _fields_ = [("src", vp), ("ld_src", i64), ("dst", vp), ("ld_dst", i64), ("rows", i32), ("cols", i32),
-                ("colsum_ws", vp), ("idx", vp), ("packed_steps", i32), ("pad0", i32)]
+                ("colsum_ws", vp), ("idx", vp), ("packed_steps", i32), ("transpose", i32)]
 
 
 class ReduceArgs(C.Structure):
@@ -72,7 +72,7 @@ class ActArgs(C.Structure):
 
 class ChainLayer(C.Structure):
     _fields_ = [("W", vp), ("ldw", i64), ("bias", vp), ("C", vp), ("ldc", i64), ("C32", vp), ("ldc32", i64),
-                ("K", i32), ("N", i32), ("elu", i32), ("packed", i32)]
+                ("act", vp), ("ld_act", i64), ("colsum_ws", vp), ("K", i32), ("N", i32), ("elu", i32), ("packed", i32)]
 
 
 class ChainArgs(C.Structure):
@@ -111,8 +111,8 @@ def load(path=_LIB_PATH):
     L.lgx_s8_act_pack.argtypes = [vp, i32, vp]
     L.lgx_s8_act_pack.restype = i32
     L.lgx_s8_sizeof_act_pack_args.restype = i32
-    L.lgx_s8_chain_fwd.argtypes = [vp, i32, vp]
-    L.lgx_s8_chain_fwd.restype = i32
+    L.lgx_s8_chain.argtypes = [vp, i32, vp]
+    L.lgx_s8_chain.restype = i32
     L.lgx_s8_sizeof_chain_args.restype = i32
     if L.lgx_s8_abi_version() != ABI_VERSION:
         raise S8LibError("liblgx_s8 ABI version mismatch; rebuild")
@@ -231,11 +231,11 @@ def reduce(jobs, L=None):
         _check(L.lgx_s8_reduce(arr, len(chunk), _stream()), "lgx_s8_reduce")
 
 
-def chain_fwd(chains, L=None):
-    """lgx_s8_chain_fwd: up to CHAIN_MAX narrow forward chains in one launch ([ChainArgs])."""
+def chain(chains, L=None):
+    """lgx_s8_chain: up to CHAIN_MAX narrow forward chains in one launch ([ChainArgs])."""
     L = lib() if L is None else L
     arr = (ChainArgs * len(chains))(*chains)
-    _check(L.lgx_s8_chain_fwd(arr, len(chains), _stream()), "lgx_s8_chain_fwd")
+    _check(L.lgx_s8_chain(arr, len(chains), _stream()), "lgx_s8_chain")
 
 
 def act(args, L=None):
@@ -260,12 +260,14 @@ def packed_empty(N, K, device):
     return torch.zeros((N + 15) // 16 * ((K + 31) // 32) * 512, dtype=torch.int32, device=device)
 
 
-def split_packed_job(W, dst):
-    """SplitArgs: fp32 weight [N, K] -> its fragment-packed S8 copy (packed_empty)."""
+def split_packed_job(W, dst, transpose=False):
+    """SplitArgs: fp32 weight [N, K] -> its fragment-packed S8 copy (packed_empty(N, K)), or with
+    transpose its transpose's (packed_empty(K, N): an input-gradient chain's B operand)."""
     if W.stride(1) != 1 or W.dtype != torch.float32:
         raise S8LibError("split: fp32 with unit column stride")
-    return SplitArgs(src=W.data_ptr(), ld_src=W.stride(0), dst=dst.data_ptr(), ld_dst=0, rows=W.shape[0],
-                     cols=W.shape[1], packed_steps=(W.shape[1] + 31) // 32)
+    rows, cols = (W.shape[1], W.shape[0]) if transpose else W.shape
+    return SplitArgs(src=W.data_ptr(), ld_src=W.stride(0), dst=dst.data_ptr(), ld_dst=0, rows=rows, cols=cols,
+                     packed_steps=(cols + 31) // 32, transpose=int(transpose))
 
 
 def split_job(src, dst_ptr, ld_dst, colsum_ws=None, idx=None, rows=None):

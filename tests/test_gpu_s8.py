@@ -267,7 +267,7 @@ def test_split_packed_matches_reference(S):
 
 @pytest.mark.parametrize("rows,packed", [(1000, 0), (1000, 1), (24576, 1)])
 def test_chain_fwd_equals_grouped_levels(S, rows, packed):
-    """lgx_s8_chain_fwd (the privileged / scan encoders' forward in one launch) against the same
+    """lgx_s8_chain (the privileged / scan encoders' forward in one launch) against the same
     layers as one grouped FWD launch each: S8 outputs (hidden layers, the last one at a column
     offset of a wider buffer, pads zero), the fp32 copy, bit for bit."""
     g = torch.Generator(device="cpu").manual_seed(rows)
@@ -308,7 +308,7 @@ def test_chain_fwd_equals_grouped_levels(S, rows, packed):
                 A, lda = hid_ref[l], hid_ref[l].shape[1]
         chains.append(c)
         outs[name] = (hid, hid_ref, y32, y32_ref, x, Ws, Wp, bs)  # (the chain reads x, Ws, bs at launch)
-    S.chain_fwd(chains)
+    S.chain(chains)
     torch.cuda.synchronize()
     for name, (hid, hid_ref, y32, y32_ref, *_keep) in outs.items():
         for h, hr in zip(hid, hid_ref):
@@ -324,8 +324,61 @@ def test_chain_fwd_rejects_bad_arguments(S):
     c.layers[0] = S.ChainLayer(W=W.data_ptr(), ldw=W.shape[1], K=40, N=16)
     c.layers[1] = S.ChainLayer(W=W.data_ptr(), ldw=W.shape[1], K=40, N=16)  # K != previous N
     with pytest.raises(S.S8LibError, match="K_l"):
-        S.chain_fwd([c])
+        S.chain([c])
     c.nlayers = 1
     c.layers[0].K = 300  # wider than the chain's image
     with pytest.raises(S.S8LibError):
-        S.chain_fwd([c])
+        S.chain([c])
+
+
+@pytest.mark.parametrize("rows", [1000, 24576])
+def test_chain_input_grads_equal_grouped_levels(S, rows):
+    """The encoders' input gradients as one chain launch (elu = 2: times ELU'(y), W^T
+    fragment-packed by a transposed split, column sums per 128-row tile) against one grouped DX
+    launch per layer: S8 outputs bit for bit; the column sums (a different summation order
+    inside the tile) to fp32 rounding. The inputs are column spans of one wider buffer (the
+    update's dlat: privileged latent at 0, scan latent at 24): the chain reads zeros past K."""
+    g = torch.Generator(device="cpu").manual_seed(rows + 1)
+    dlat32 = torch.zeros(rows, 64, device=dev)
+    dlat32[:, :20] = torch.randn(rows, 20, generator=g).to(dev)
+    dlat32[:, 24:56] = torch.randn(rows, 32, generator=g).to(dev)
+    dlat = S.to_s8_torch(dlat32)
+    chains, checks, keep = [], [], []
+    for c0, widths in ((24, [32, 64, 128]), (0, [20, 64])):  # scan (layers 2, 1), privileged (layer 1)
+        c = S.ChainArgs(A=S.group_ptr(dlat, c0), lda=dlat.shape[1], rows=rows, nlayers=len(widths) - 1)
+        A, lda = S.group_ptr(dlat, c0), dlat.shape[1]
+        for q, (k, n) in enumerate(zip(widths[:-1], widths[1:])):
+            W = (torch.randn(k, n, generator=g) * 0.2).to(dev)  # the forward weight [out k][in n]
+            y = S.to_s8_torch(torch.nn.functional.elu(torch.randn(rows, n, generator=g)).to(dev))
+            WpT = S.packed_empty(n, k, dev)
+            S.split([S.split_packed_job(W, WpT, transpose=True)])
+            Ws = S.to_s8_torch(W)
+            out, out_ref = S.empty(rows, n, dev), S.empty(rows, n, dev)
+            tiles = (rows + 127) // 128
+            cs, cs_ref = torch.full((tiles, n), float("nan"), device=dev), torch.zeros(tiles, n, device=dev)
+            L = c.layers[q]
+            L.W, L.packed, L.K, L.N, L.elu = WpT.data_ptr(), 1, k, n, 2
+            L.act, L.ld_act, L.C, L.ldc, L.colsum_ws = y.data_ptr(), y.shape[1], out.data_ptr(), out.shape[1], cs.data_ptr()
+            S.gemm_group([S.GemmArgs(A=A, lda=lda, B=Ws.data_ptr(), ldb=Ws.shape[1], M=rows, N=n, K=k,
+                                     epilogue=S.EPI_DELU, C=out_ref.data_ptr(), ldc=out_ref.shape[1], act=y.data_ptr(),
+                                     ld_act=y.shape[1], colsum_ws=cs_ref.data_ptr())], S.DX)
+            A, lda = out_ref.data_ptr(), out_ref.shape[1]
+            keep += [W, y, WpT, Ws]
+            checks.append((out, out_ref, cs, cs_ref))
+        chains.append(c)
+    S.chain(chains)
+    torch.cuda.synchronize()
+    for out, out_ref, cs, cs_ref in checks:
+        assert torch.equal(out, out_ref)
+        torch.testing.assert_close(cs, cs_ref, rtol=1e-5, atol=1e-5)
+
+
+def test_chain_rejects_partial_column_sums(S):
+    x = S.empty(256, 64, dev)
+    W = S.packed_empty(64, 64, dev)
+    cs = torch.zeros(2, 64, device=dev)
+    c = S.ChainArgs(A=x.data_ptr(), lda=x.shape[1], rows=256, nlayers=2)
+    c.layers[0] = S.ChainLayer(W=W.data_ptr(), packed=1, K=64, N=64, colsum_ws=cs.data_ptr())
+    c.layers[1] = S.ChainLayer(W=W.data_ptr(), packed=1, K=64, N=64)  # no column sums here
+    with pytest.raises(S.S8LibError, match="column sums"):
+        S.chain([c])

@@ -1,4 +1,4 @@
-"""lgx_s8_chain_fwd on the go2 update's encoder chains (scan 132-128-64-32, privileged 29-64-20,
+"""lgx_s8_chain on the go2 update's encoder chains (scan 132-128-64-32, privileged 29-64-20,
 24,576 rows): HIP-event time per launch, the product library and build variants interleaved,
 against the same layers as three grouped levels (dev tool).
 Usage: PYTHONPATH=.:tests:tools python tools/chain_bench.py [variant.so ...]"""
@@ -43,12 +43,12 @@ def main(rows=24576):
     libs = {"product": S.lib()}
     for v in sys.argv[1:]:
         libs[v.split("/")[-1]] = S.load(v)
-    fns = {k: (lambda L=L: S.chain_fwd(chains, L)) for k, L in libs.items()}
+    fns = {k: (lambda L=L: S.chain(chains, L)) for k, L in libs.items()}
     fns["levels"] = lambda: [S.gemm_group(lv, S.FWD) for lv in levels if lv]
     print(json.dumps(timeit_many(fns, n=20, rounds=5)))
     for L, w in rowW:  # the same chains on row-layout weights
         L.W, L.packed = w, 0
-    print("row-layout weights", json.dumps(timeit_many({"product": lambda: S.chain_fwd(chains)}, n=20, rounds=3)))
+    print("row-layout weights", json.dumps(timeit_many({"product": lambda: S.chain(chains)}, n=20, rounds=3)))
 
 
 if __name__ == "__main__":
