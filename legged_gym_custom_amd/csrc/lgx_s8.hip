@@ -534,8 +534,9 @@ __global__ __launch_bounds__(256) void s8_split_kernel(SplitBatch b) {
 
 struct ReduceBatch {
   int n;
-  int64_t start[LGX_S8_BATCH_MAX + 1];  // prefix sums of rows * cols
+  int64_t start[LGX_S8_BATCH_MAX + 1];  // first thread of each job (wave jobs: 64-aligned)
   lgx_s8_reduce_args j[LGX_S8_BATCH_MAX];
+  unsigned char wave[LGX_S8_BATCH_MAX];  // one wave per output (long sums: the bias partials)
 };
 static_assert(sizeof(ReduceBatch) <= 4096, "kernel argument segment");
 
@@ -545,7 +546,33 @@ __global__ __launch_bounds__(256) void s8_reduce_kernel(ReduceBatch b) {
   int ji = 0;
   while (ji + 1 < b.n && i >= b.start[ji + 1]) ++ji;
   const lgx_s8_reduce_args& J = b.j[ji];
+  if (b.wave[ji]) {
+    // a long sum (one partial per 128-row tile): lane l takes partials l, l + 64, ... in order,
+    // then a fixed butterfly over the wave — a few loads per lane instead of one thread's
+    // nsplit / 16 dependent rounds (deterministic; the job's threads are whole waves)
+    const int64_t e = (i - b.start[ji]) >> 6;
+    const int lane = (int)(i & 63);
+    if (e >= (int64_t)J.rows * J.cols) return;  // (never splits a wave: 64-aligned, whole waves)
+    const int64_t r = e / J.cols, c = e - r * J.cols;
+    const float* w = J.ws + r * J.ld_ws + c;
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    int q = lane;
+    for (; q + 192 < J.nsplit; q += 256) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] += w[(int64_t)(q + 64 * u) * J.stride];
+    }
+    for (; q < J.nsplit; q += 64) v[0] += w[(int64_t)q * J.stride];
+    float s = (v[0] + v[1]) + (v[2] + v[3]);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
+    if (lane == 0) {
+      float* o = J.out + r * J.ld_out + c;
+      *o = J.accumulate ? *o + s : s;
+    }
+    return;
+  }
   const int64_t e = i - b.start[ji];
+  if (e >= (int64_t)J.rows * J.cols) return;  // the alignment gap before a wave job
   const int64_t r = e / J.cols, c = e - r * J.cols;
   const float* w = J.ws + r * J.ld_ws + c;
   // partials summed in split order; loaded 16 at a time so the bias jobs' long (one partial per
@@ -733,7 +760,9 @@ int32_t lgx_s8_reduce(const lgx_s8_reduce_args* a, int32_t n, void* stream) {
     if (!a[i].ws || !a[i].out) return fail("lgx_s8_reduce: null pointer");
     if (a[i].rows > 1 && (a[i].ld_ws < a[i].cols || a[i].ld_out < a[i].cols)) return fail("lgx_s8_reduce: pitch < cols");
     b.j[k] = a[i];
-    b.start[k + 1] = b.start[k] + (int64_t)a[i].rows * a[i].cols;
+    b.wave[k] = a[i].nsplit >= 64 && (int64_t)a[i].rows * a[i].cols <= 4096;
+    if (b.wave[k]) b.start[k] = (b.start[k] + 63) / 64 * 64;
+    b.start[k + 1] = b.start[k] + (int64_t)a[i].rows * a[i].cols * (b.wave[k] ? 64 : 1);
     ++k;
   }
   b.n = k;

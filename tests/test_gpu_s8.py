@@ -382,3 +382,23 @@ def test_chain_rejects_partial_column_sums(S):
     c.layers[1] = S.ChainLayer(W=W.data_ptr(), packed=1, K=64, N=64)  # no column sums here
     with pytest.raises(S.S8LibError, match="column sums"):
         S.chain([c])
+
+
+def test_reduce_long_sums_one_wave_per_output(S):
+    """Reduce jobs with many partials (the bias gradients: one per 128-row tile) run one wave per
+    output; mixed in one launch with per-thread jobs, against fp64 sums; deterministic."""
+    g = torch.Generator(device="cpu").manual_seed(9)
+    jobs, refs = [], []
+    for nsplit, n in ((192, 128), (768, 64), (3, 1000), (65, 20), (96, 1)):
+        ws = torch.randn(nsplit, n, generator=g).to(dev)
+        out = torch.full((n,), 5.0, device=dev)
+        jobs.append(S.flat_reduce(ws.data_ptr(), n, out.data_ptr(), n, nsplit))
+        refs.append((ws, out))
+    S.reduce(jobs)
+    torch.cuda.synchronize()
+    first = [o.clone() for _, o in refs]
+    for ws, out in refs:
+        torch.testing.assert_close(out.double(), ws.double().sum(0), rtol=1e-5, atol=1e-5)
+    S.reduce(jobs)
+    torch.cuda.synchronize()
+    assert all(torch.equal(a, o) for a, (_, o) in zip(first, refs))
