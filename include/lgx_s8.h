@@ -182,10 +182,10 @@ int32_t lgx_s8_sizeof_act_pack_args(void);
  * [N_l][ldw_l] (or fragment-packed), K_l = N_{l-1}. epi (`elu`): 0 none, 1 ELU (forward), 2
  * times ELU'(act) with act the S8 ELU output at the same rows (input gradient: W_l = the
  * forward weight transposed, bias null). Each layer's output goes to C_l (S8, pitch ldc_l,
- * pads zero; may be null) and / or C32_l (fp32; may be null); colsum_ws (optional, every
- * layer of the launch or none): the column sums of each 128-row tile, colsum_ws[tile * N + n]
- * (lgx_s8_gemm_group's tile partials). Same operand contract, products and epilogues as
- * lgx_s8_gemm_group; widths <= LGX_S8_CHAIN_MAXW (<= 128 with column sums). */
+ * pads zero; may be null) and / or C32_l (fp32; may be null); colsum_ws (exactly on the elu = 2
+ * layers): the column sums of each 32-row block, colsum_ws[block * N + n] (a bias gradient is
+ * their lgx_s8_reduce). Same operand contract, products and epilogues as lgx_s8_gemm_group;
+ * widths <= LGX_S8_CHAIN_MAXW. */
 #define LGX_S8_CHAIN_MAX 4
 #define LGX_S8_CHAIN_MAXL 3
 #define LGX_S8_CHAIN_MAXW 256

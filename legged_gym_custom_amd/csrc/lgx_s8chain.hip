@@ -64,13 +64,10 @@ struct BSet {
 
 // NJW = output tiles per wave (16 columns each): the launch's widest layer / 64, rounded up to
 // 1, 2 or 4 (the registers of the narrow chains' launches stay few: 4 waves per SIMD). BR = rows
-// per block: 32, or 128 when the launch writes column sums (one block per 128-row tile: the
-// partials are lgx_s8_gemm_group's). IPW = the image's width (its pitch IPW + 8 bf16: fragment
-// reads conflict-free).
-template <int NJW, int BR, int IPW>
+// per block. IPW = the image's width (its pitch IPW + 8 bf16: fragment reads conflict-free).
+template <int NJW, int BR, int IPW, bool DX>  // DX: the input-gradient launches (ELU', column sums)
 __global__ __launch_bounds__(NT) void chain_kernel(Params P) {
   constexpr int MI = BR / 16, IP = IPW + 8;
-  constexpr bool DX = BR == 128;  // the input-gradient launches: ELU' epilogue, column sums
   __shared__ __align__(16) __bf16 ih[BR * IP];
   __shared__ __align__(16) __bf16 il[BR * IP];
   __shared__ float red[DX ? 4 : 1][DX ? IPW : 1];  // column-sum partials of the 4 lane groups
@@ -200,7 +197,7 @@ __global__ __launch_bounds__(NT) void chain_kernel(Params P) {
       if constexpr (DX) red[fc][col] = cs;
     }
     __syncthreads();
-    if (DX && L.colsum_ws != nullptr)  // the 4 lane groups' partials in order: one 128-row tile's sums
+    if (DX && L.colsum_ws != nullptr)  // the 4 lane groups' partials in order: the block's sums
       for (int n = tid; n < N; n += NT)
         L.colsum_ws[(int64_t)(r0 / BR) * N + n] = ((red[0][n] + red[1][n]) + red[2][n]) + red[3][n];
     if (L.C != nullptr) {  // the image's groups -> S8 rows (hi 16 B | lo 16 B)
@@ -255,9 +252,8 @@ int32_t lgx_s8_chain(const lgx_s8_chain_args* chains, int32_t n, void* stream) {
     }
     P.c[i] = c;
   }
-  if (ncs && (ncs != nl || wmax > 128 || nmax > 128))
-    return lgxs_fail("lgx_s8_chain: column sums on every layer or none, widths <= 128 with them");
-  const int br = ncs ? 128 : 32;
+  if (ncs && ncs != nl) return lgxs_fail("lgx_s8_chain: column sums on every layer or none");
+  const int br = 32;
   for (int i = 0; i < n; ++i) {
     P.start[i] = tot;
     tot += (chains[i].rows + br - 1) / br;
@@ -266,12 +262,13 @@ int32_t lgx_s8_chain(const lgx_s8_chain_args* chains, int32_t n, void* stream) {
   const hipStream_t s = (hipStream_t)stream;
   const dim3 g(tot), b(lgxc::NT);
   if (ncs) {
-    if (nmax <= 64) hipLaunchKernelGGL((lgxc::chain_kernel<1, 128, 128>), g, b, 0, s, P);
-    else hipLaunchKernelGGL((lgxc::chain_kernel<2, 128, 128>), g, b, 0, s, P);
+    if (nmax <= 64) hipLaunchKernelGGL((lgxc::chain_kernel<1, 32, 256, true>), g, b, 0, s, P);
+    else if (nmax <= 128) hipLaunchKernelGGL((lgxc::chain_kernel<2, 32, 256, true>), g, b, 0, s, P);
+    else hipLaunchKernelGGL((lgxc::chain_kernel<4, 32, 256, true>), g, b, 0, s, P);
   } else {
-    if (nmax <= 64) hipLaunchKernelGGL((lgxc::chain_kernel<1, 32, 256>), g, b, 0, s, P);
-    else if (nmax <= 128) hipLaunchKernelGGL((lgxc::chain_kernel<2, 32, 256>), g, b, 0, s, P);
-    else hipLaunchKernelGGL((lgxc::chain_kernel<4, 32, 256>), g, b, 0, s, P);
+    if (nmax <= 64) hipLaunchKernelGGL((lgxc::chain_kernel<1, 32, 256, false>), g, b, 0, s, P);
+    else if (nmax <= 128) hipLaunchKernelGGL((lgxc::chain_kernel<2, 32, 256, false>), g, b, 0, s, P);
+    else hipLaunchKernelGGL((lgxc::chain_kernel<4, 32, 256, false>), g, b, 0, s, P);
   }
   return lgxs_launched("lgx_s8_chain");
 }

@@ -41,8 +41,7 @@ from legged_gym_custom_amd.rsl_rl.modules import hip_mlp as H
 from legged_gym_custom_amd.rsl_rl.modules import hip_s8 as S
 
 ENC_CHAIN = os.environ.get("LGX_S8_CHAIN", "1") != "0"  # the encoders' forward as one chain launch
-# their input gradients as one chain launch too (128-row blocks for the column sums: measured
-# 104 us against 31 us for the two grouped levels — one wave per SIMD waits on the ELU' loads)
+# their input gradients as one chain launch too (column sums per 32-row block)
 ENC_CHAIN_DX = os.environ.get("LGX_S8_CHAIN_DX", "0") != "0"
 ROW_ALIGN = 64  # minibatch rows: whole K steps of every weight-gradient chunk
 
@@ -160,9 +159,11 @@ class S8Minibatch:
         self.dw_ws = torch.empty(tot, device=dev)
         self.tiles_m = (mb + 127) // 128
         self.nsb = (mb + S.SPLIT_ROWS - 1) // S.SPLIT_ROWS
+        self.nsb32 = (mb + 31) // 32
         for p in self.parts:
             # colsum partials of dy[l] (the bias gradient of layer l): [tiles][out_l]
-            p.cs = [torch.empty(max(self.tiles_m, self.nsb), W.shape[0], device=dev) for W in p.W]
+            # (the encoders' input-gradient chain writes one partial per 32 rows: nsb32)
+            p.cs = [torch.empty(max(self.tiles_m, self.nsb, self.nsb32), W.shape[0], device=dev) for W in p.W]
         self.cs_lat = torch.empty(self.tiles_m, self.P2 - self.P0, device=dev)
         # launch schedule: the level (grouped launch) of each chain's layer is its depth plus this
         # shift — the critic and the estimator do not feed the actor, so they can share the
@@ -178,8 +179,7 @@ class S8Minibatch:
         # instead of their own three grouped levels
         self.enc_chain = ENC_CHAIN and all(p.n <= S.CHAIN_MAXL and max(max(W.shape) for W in p.W) <= S.CHAIN_MAXW
                                            for p in (self.priv, self.scan))
-        self.enc_chain_dx = self.enc_chain and ENC_CHAIN_DX and all(
-            max(max(W.shape) for W in p.W[1:]) <= 128 for p in (self.priv, self.scan))
+        self.enc_chain_dx = self.enc_chain and ENC_CHAIN_DX
         self._build(shapes)
 
     # ------------------------------------------------------------------ argument lists
@@ -435,6 +435,8 @@ class S8Minibatch:
                                              tm))
                     continue
                 from_split = l == p.n - 1  # the loss heads' gradients: lgx_s8_split partials (256 rows)
-                red.append(S.flat_reduce(p.cs[l].data_ptr(), n, bg.data_ptr(), n, nsb if from_split else tm))
+                chained = self.enc_chain_dx and p in (pr, sc)  # the chain's 32-row partials
+                red.append(S.flat_reduce(p.cs[l].data_ptr(), n, bg.data_ptr(), n,
+                                         nsb if from_split else self.nsb32 if chained else tm))
         S.gemm_group(g_args, S.DW)
         S.reduce(red)

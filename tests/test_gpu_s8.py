@@ -334,9 +334,9 @@ def test_chain_fwd_rejects_bad_arguments(S):
 @pytest.mark.parametrize("rows", [1000, 24576])
 def test_chain_input_grads_equal_grouped_levels(S, rows):
     """The encoders' input gradients as one chain launch (elu = 2: times ELU'(y), W^T
-    fragment-packed by a transposed split, column sums per 128-row tile) against one grouped DX
-    launch per layer: S8 outputs bit for bit; the column sums (a different summation order
-    inside the tile) to fp32 rounding. The inputs are column spans of one wider buffer (the
+    fragment-packed by a transposed split, column sums per 32-row block) against one grouped DX
+    launch per layer: S8 outputs bit for bit; the column totals (the bias gradients, summed in
+    another order) to fp32 rounding. The inputs are column spans of one wider buffer (the
     update's dlat: privileged latent at 0, scan latent at 24): the chain reads zeros past K."""
     g = torch.Generator(device="cpu").manual_seed(rows + 1)
     dlat32 = torch.zeros(rows, 64, device=dev)
@@ -354,8 +354,8 @@ def test_chain_input_grads_equal_grouped_levels(S, rows):
             S.split([S.split_packed_job(W, WpT, transpose=True)])
             Ws = S.to_s8_torch(W)
             out, out_ref = S.empty(rows, n, dev), S.empty(rows, n, dev)
-            tiles = (rows + 127) // 128
-            cs, cs_ref = torch.full((tiles, n), float("nan"), device=dev), torch.zeros(tiles, n, device=dev)
+            cs = torch.full(((rows + 31) // 32, n), float("nan"), device=dev)
+            cs_ref = torch.zeros((rows + 127) // 128, n, device=dev)
             L = c.layers[q]
             L.W, L.packed, L.K, L.N, L.elu = WpT.data_ptr(), 1, k, n, 2
             L.act, L.ld_act, L.C, L.ldc, L.colsum_ws = y.data_ptr(), y.shape[1], out.data_ptr(), out.shape[1], cs.data_ptr()
@@ -370,7 +370,7 @@ def test_chain_input_grads_equal_grouped_levels(S, rows):
     torch.cuda.synchronize()
     for out, out_ref, cs, cs_ref in checks:
         assert torch.equal(out, out_ref)
-        torch.testing.assert_close(cs, cs_ref, rtol=1e-5, atol=1e-5)
+        torch.testing.assert_close(cs.double().sum(0), cs_ref.double().sum(0), rtol=1e-5, atol=1e-4)
 
 
 def test_chain_rejects_partial_column_sums(S):
