@@ -124,6 +124,23 @@ __global__ __launch_bounds__(NT) void chain_kernel(Params P) {
         S.l[j] = *reinterpret_cast<const u32x4*>(q + lo);
       }
     };
+    // the ELU' epilogue's y values, requested before the K loop (their latency overlaps it)
+    float yv[DX ? MI : 1][DX ? NJW : 1][4];
+    if constexpr (DX) {
+      const char* act = (const char*)L.act;
+#pragma unroll
+      for (int j = 0; j < NJW; ++j) {
+        const int cc = std::min(16 * (wave + 4 * j) + fr, N - 1);
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const unsigned short* q = reinterpret_cast<const unsigned short*>(
+                act + (int64_t)std::min(r0 + 16 * i + 4 * fc + r, rows - 1) * L.ld_act * 4 + (cc >> 3) * 32 + (cc & 7) * 2);
+            yv[i][j][r] = tv[j] ? __uint_as_float((unsigned)q[0] << 16) + __uint_as_float((unsigned)q[8] << 16) : 0.f;
+          }
+      }
+    }
     f32x4 acc[MI][NJW];
 #pragma unroll
     for (int i = 0; i < MI; ++i)
@@ -165,7 +182,6 @@ __global__ __launch_bounds__(NT) void chain_kernel(Params P) {
 
     // epilogue: bias (+ ELU) or times ELU'(act), zero pad columns; fp32 rows out, the split back
     // into the image, the column sums of the block's valid rows
-    const char* act = (const char*)L.act;
 #pragma unroll
     for (int j = 0; j < NJW; ++j) {
       if (!tv[j]) continue;
@@ -181,10 +197,7 @@ __global__ __launch_bounds__(NT) void chain_kernel(Params P) {
           if (!DX && L.elu == 1) {
             v = elu(v);
           } else if (DX && L.elu == 2) {  // y = hi + lo of the S8 ELU output (lgx_s8.hip load_s8)
-            const unsigned short* q = reinterpret_cast<const unsigned short*>(
-                act + (int64_t)std::min(r0 + row, rows - 1) * L.ld_act * 4 + (std::min(col, N - 1) >> 3) * 32 +
-                (std::min(col, N - 1) & 7) * 2);
-            const float y = __uint_as_float((unsigned)q[0] << 16) + __uint_as_float((unsigned)q[8] << 16);
+            const float y = yv[DX ? i : 0][DX ? j : 0][r];
             v *= y > 0.f ? 1.f : y + 1.f;
           }
           v = col < N ? v : 0.f;
