@@ -43,6 +43,8 @@ from legged_gym_custom_amd.rsl_rl.modules import hip_s8 as S
 ENC_CHAIN = os.environ.get("LGX_S8_CHAIN", "1") != "0"  # the encoders' forward as one chain launch
 # their input gradients as one chain launch too (column sums per 32-row block)
 ENC_CHAIN_DX = os.environ.get("LGX_S8_CHAIN_DX", "0") != "0"
+# the actor's and critic's last layers (mu, value) as 1-layer chains instead of their own level
+TAIL_CHAIN = os.environ.get("LGX_S8_TAIL_CHAIN", "0") != "0"
 ROW_ALIGN = 64  # minibatch rows: whole K steps of every weight-gradient chunk
 
 
@@ -180,6 +182,7 @@ class S8Minibatch:
         self.enc_chain = ENC_CHAIN and all(p.n <= S.CHAIN_MAXL and max(max(W.shape) for W in p.W) <= S.CHAIN_MAXW
                                            for p in (self.priv, self.scan))
         self.enc_chain_dx = self.enc_chain and ENC_CHAIN_DX
+        self.tail_chain = TAIL_CHAIN and all(max(p.W[-1].shape) <= S.CHAIN_MAXW for p in (self.actor, self.critic))
         self._build(shapes)
 
     # ------------------------------------------------------------------ argument lists
@@ -202,6 +205,9 @@ class S8Minibatch:
             p.Wp = [S.packed_empty(W.shape[0], W.shape[1], self.dev) for W in p.W]
             for W, Wp in zip(p.W, p.Wp):
                 self.wsplit.append(S.split_packed_job(W.detach(), Wp))
+        for p in ((a, cr) if self.tail_chain else ()):
+            p.Wp_last = S.packed_empty(p.W[-1].shape[0], p.W[-1].shape[1], self.dev)
+            self.wsplit.append(S.split_packed_job(p.W[-1].detach(), p.Wp_last))
         for p in ((pr, sc) if self.enc_chain_dx else ()):
             p.WpT = [None] + [S.packed_empty(W.shape[1], W.shape[0], self.dev) for W in p.W[1:]]
             for W, WpT in zip(p.W[1:], p.WpT[1:]):
@@ -257,7 +263,15 @@ class S8Minibatch:
 
         def put(level, args):
             levels.setdefault(level, []).append(args)
-        chains = []
+        chains, tails = [], []
+
+        def tail(p, A_ptr, lda, K, C32, ldc32):
+            """p's last layer as a 1-layer chain (fp32 output only)."""
+            c = S.ChainArgs(A=A_ptr, lda=lda, rows=mb, nlayers=1)
+            L = c.layers[0]
+            L.W, L.packed, L.bias, L.K, L.N = p.Wp_last.data_ptr(), 1, p.b[-1].data_ptr(), K, p.W[-1].shape[0]
+            L.C32, L.ldc32 = C32, ldc32
+            tails.append(c)
         for p in (pr, sc, es, cr):
             A_ptr, lda, K = ins[p.name]
             if self.enc_chain and p in (pr, sc):
@@ -299,6 +313,8 @@ class S8Minibatch:
                 elif p is es:
                     put(l + sh, self._fwd(p, l, A_ptr, lda, K, C32=self.pred.data_ptr(), ldc32=self.pred.shape[1],
                                           elu=False))
+                elif self.tail_chain:
+                    tail(p, A_ptr, lda, K, self.value.data_ptr(), 1)
                 else:
                     put(l + sh, self._fwd(p, l, A_ptr, lda, K, C32=self.value.data_ptr(), ldc32=1, elu=False))
         A_ptr, lda, K = row(self.ain), lda_ain, self.W8
@@ -308,12 +324,16 @@ class S8Minibatch:
                 o = a.out[l]
                 put(lev, self._fwd(a, l, A_ptr, lda, K, C=o.data_ptr(), ldc=o.shape[1]))
                 A_ptr, lda, K = o.data_ptr(), o.shape[1], a.W[l].shape[0]
+            elif self.tail_chain:
+                tail(a, A_ptr, lda, K, self.mu.data_ptr(), self.mu.shape[1])
             else:
                 put(lev, self._fwd(a, l, A_ptr, lda, K, C32=self.mu.data_ptr(), ldc32=self.mu.shape[1], elu=False))
         if chains:
             S.chain(chains)
         for lev in sorted(levels):
             S.gemm_group(levels[lev], S.FWD)
+        if tails:
+            S.chain(tails)
         # 3. loss heads: forward sums and input gradients in one launch; the narrow output
         #    gradients straight into S8 with their per-256-row column sums (the last layers'
         #    bias gradients)
