@@ -417,6 +417,12 @@ def main():
             "windows": [{"value": round(total_env_steps / el, 1), "ms_per_step": round(el / args.steps * 1e3, 3),
                          "sclk_mhz": clk} for el, _p, clk in windows],
             "window_spread": round((max(w[0] for w in windows) - min(w[0] for w in windows)) / elapsed, 4),
+            # which code paths the timed iterations ran (no silent fallback: ppo.py / s8_*.py raise
+            # on a missing library; these say which of the built paths were selected)
+            "paths": {"learner": "s8" if runner.alg._s8 is not None else "autograd",
+                      "act": "fused" if runner.alg._s8act is not None else "grouped",
+                      "graph_mode": runner.alg.graph_mode,
+                      "rollout_graphs": sorted(str(k) for k in runner._graphs)},
             "collection_s": round(perf.get("collection_time", 0.0), 4),
             "learn_s": round(perf.get("learn_time", 0.0), 4),
             "env_kernel": {"avg_us": round(kern_avg_ms * 1e3, 2), "min_us": round(kern_ms[0] * 1e3, 2),

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define LGX_MLP_ABI_VERSION 7
+#define LGX_MLP_ABI_VERSION 8
 
 enum {
   LGX_EPI_BIAS = 1,  /* + bias[n] */
@@ -221,6 +221,16 @@ typedef struct lgx_heads_s8_args {
   void* dmu_s8; int64_t ld_dmu; float* dmu_cs;
   void* dvalue_s8; int64_t ld_dvalue; float* dvalue_cs;
   void* de_s8; int64_t ld_de; float* de_cs;
+  /* ABI 8, optional (NULL: unused). The per-sample discrete decisions of the PPO head, one byte
+   * per row: bits 0-1 the surrogate max (ppo.py:254) weight of the unclipped term times 2 (0, 1:
+   * a tie, 2), bit 2 the ratio inside [1-clip, 1+clip] (the clamp's gradient, :252), bits 3-4 the
+   * value-loss max (:261) weight of the unclipped term times 2, bit 5 v - target inside
+   * [-clip, clip] (:258). decisions_out: this launch writes its own decisions. decisions_in: the
+   * launch takes its decisions from here instead (forward maxima and gradients; the continuous
+   * quantities stay its own), so a test can replay a reference run's decisions and its
+   * trajectory cannot leave the reference's at a sample sitting within rounding of a clip
+   * boundary (tests/test_gpu_learner_golden.py). */
+  const uint8_t* decisions_in; uint8_t* decisions_out;
 } lgx_heads_s8_args;
 int32_t lgx_loss_heads_fused(const lgx_ppo_head_args* head, const lgx_aux_loss_args* aux,
                              const lgx_heads_s8_args* s8, void* stream);

@@ -1398,15 +1398,32 @@ __device__ __forceinline__ void ppo_head_fused_body(const lgx_ppo_head_args& p, 
     const float lo = 1.f - p.clip, hi = 1.f + p.clip;
     // forward (ppo_head_fwd_body)
     const float s1 = -a * h.ratio, s2 = -a * fminf(fmaxf(h.ratio, lo), hi);
-    v[0] += fmaxf(s1, s2);
     const float val = p.value[i], R = p.returns[i];
     const float tv = (p.clipped_value ? p.target_values : p.value)[i];
-    float vc = 0.f;
-    if (p.clipped_value) {
-      vc = tv + fminf(fmaxf(val - tv, -p.clip), p.clip);
-      v[1] += fmaxf((val - R) * (val - R), (vc - R) * (vc - R));
-    } else {
-      v[1] += (R - val) * (R - val);
+    const float vc = p.clipped_value ? tv + fminf(fmaxf(val - tv, -p.clip), p.clip) : 0.f;
+    const float l1 = (val - R) * (val - R), l2 = (vc - R) * (vc - R);
+    // the discrete decisions (torch's gradient rules: max splits ties, clamp passes on [lo, hi])
+    float w1 = s1 > s2 ? 1.f : (s1 == s2 ? 0.5f : 0.f);
+    float in = (h.ratio >= lo && h.ratio <= hi) ? 1.f : 0.f;
+    float u1 = l1 > l2 ? 1.f : (l1 == l2 ? 0.5f : 0.f);
+    float inv = (val - tv >= -p.clip && val - tv <= p.clip) ? 1.f : 0.f;
+    if (s.decisions_out)
+      s.decisions_out[i] = (uint8_t)((unsigned)(2.f * w1) | ((unsigned)in << 2) | ((unsigned)(2.f * u1) << 3) |
+                                     ((unsigned)inv << 5));
+    const bool forced = s.decisions_in != nullptr;
+    if (forced) {
+      const unsigned d = s.decisions_in[i];
+      w1 = 0.5f * (float)(d & 3u);
+      in = (float)((d >> 2) & 1u);
+      u1 = 0.5f * (float)((d >> 3) & 3u);
+      inv = (float)((d >> 5) & 1u);
+    }
+    if (!forced) {
+      v[0] += fmaxf(s1, s2);
+      v[1] += p.clipped_value ? fmaxf(l1, l2) : (R - val) * (R - val);
+    } else {  // the forced branch's value (a tie: either)
+      v[0] += w1 > 0.75f ? s1 : (w1 < 0.25f ? s2 : fmaxf(s1, s2));
+      v[1] += p.clipped_value ? (u1 > 0.75f ? l1 : (u1 < 0.25f ? l2 : fmaxf(l1, l2))) : (R - val) * (R - val);
     }
     float kl = 0.f;
 #pragma unroll
@@ -1417,9 +1434,7 @@ __device__ __forceinline__ void ppo_head_fused_body(const lgx_ppo_head_args& p, 
     }
     v[2] += kl;
     // backward (ppo_head_bwd_body)
-    const float w1 = s1 > s2 ? 1.f : (s1 == s2 ? 0.5f : 0.f);
     const float w2 = 1.f - w1;
-    const float in = (h.ratio >= lo && h.ratio <= hi) ? 1.f : 0.f;
     const float dratio = gs * (w1 * -a + w2 * -a * in);
     const float dlogp = dratio * h.ratio;
     float dmu[NA];
@@ -1436,9 +1451,6 @@ __device__ __forceinline__ void ppo_head_fused_body(const lgx_ppo_head_args& p, 
     }
     float dv;
     if (p.clipped_value) {
-      const float l1 = (val - R) * (val - R), l2 = (vc - R) * (vc - R);
-      const float u1 = l1 > l2 ? 1.f : (l1 == l2 ? 0.5f : 0.f);
-      const float inv = (val - tv >= -p.clip && val - tv <= p.clip) ? 1.f : 0.f;
       dv = gv * (u1 * 2.f * (val - R) + (1.f - u1) * 2.f * (vc - R) * inv);
     } else {
       dv = gv * 2.f * (val - R);

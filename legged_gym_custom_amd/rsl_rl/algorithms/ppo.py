@@ -43,11 +43,11 @@ from .s8_update import S8Minibatch
 USE_S8 = os.environ.get("LGX_S8_UPDATE", "1") != "0"
 # the rollout's act networks in one launch (s8_act.py); "0" selects the grouped launches
 USE_FUSED_ACT = os.environ.get("LGX_FUSED_ACT", "1") != "0"
-ACT_ENC = os.environ.get("LGX_ACT_ENC_IN_KERNEL", "0") != "0"  # s8_act.py: encoders inside the act kernel
-ACT_SPLIT = os.environ.get("LGX_ACT_SPLIT", "0") != "0"  # s8_act.py: critic launch beside the encoders (measured slower)
-# under RCCL ("nccl"), the per-minibatch gradient all-reduce is captured inside the one update
-# graph; "0" keeps the phased graphs (per-minibatch replays around host-issued all-reduces)
-GRAPH_ALLREDUCE = os.environ.get("LGX_GRAPH_ALLREDUCE", "1") != "0"
+# under RCCL ("nccl"), "1" captures the per-minibatch gradient all-reduce inside the one update
+# graph. Default "0": the phased graphs (per-minibatch replays around host-issued all-reduces),
+# the mode the 2-rank tests exercise, until a multi-GPU run has shown the captured collective
+# equal to eager (tests/test_gpu_graph_allreduce.py covers it on a 1-rank group only)
+GRAPH_ALLREDUCE = os.environ.get("LGX_GRAPH_ALLREDUCE", "0") != "0"
 
 
 def _distributed():
@@ -236,6 +236,9 @@ class PPO:
         self._perm = None
         self._graphs = None
         self._eager_updates = 0
+        # bumped whenever captured state is dropped (invalidate_graphs): the runner's rollout
+        # graphs record the act kernel's buffers (S8Act) and drop themselves when it changes
+        self.graph_generation = 0
         self.graph_mode = None  # "whole" | "phased" once captured
         self.phased_graphs = None  # None: phased iff world_size > 1 (tests force it on one GPU)
         self.use_s8 = USE_S8 and self.on_gpu
@@ -382,7 +385,7 @@ class PPO:
             return self._s8act
         if torch.cuda.is_current_stream_capturing() or not S8Act.supported(self):
             return None
-        self._s8act = S8Act(self, n, encoders_in_kernel=ACT_ENC, split=ACT_SPLIT)
+        self._s8act = S8Act(self, n)
         return self._s8act
 
     def _gpu_rollout(self):
@@ -705,11 +708,15 @@ class PPO:
             self.graph_mode = "phased"
 
     def invalidate_graphs(self):
+        """Drop every captured graph and the executors whose argument lists hold parameter /
+        gradient addresses (S8Minibatch, S8Act). The runner's rollout graphs replay S8Act's
+        buffers: they check `graph_generation` before every replay and re-capture."""
         self._graphs = None
         self._eager_updates = 0
         self.graph_mode = None
-        self._s8 = None  # its argument lists hold parameter / gradient addresses
+        self._s8 = None
         self._s8act = None
+        self.graph_generation += 1
 
     def _run_update(self):
         if not self.use_graphs:

@@ -30,10 +30,7 @@ class S8Act:
     def supported(alg):
         if not alg.on_gpu:
             return False
-        try:
-            S.lib()
-        except Exception:  # noqa: BLE001 — the grouped launches stay available
-            return False
+        S.lib()  # a broken build raises (LGX_FUSED_ACT on): no silent fallback to the grouped launches
         ac, est = alg.actor_critic, alg.estimator
         chains = [_chain(ac.actor), _chain(ac.critic), _chain(ac.privileged_encoder_.priv_encoder),
                   _chain(ac.scan_encoder.scan_encoder), _chain(est.estimator)]
@@ -55,18 +52,11 @@ class S8Act:
         return (c0 % 4 == 0 and critic[-1].out_features == 1 and critic[0].in_features % 32 == 0
                 and scan[0].in_features <= S.ACT_MAXENC and priv[0].in_features <= S.ACT_MAXENC)
 
-    def __init__(self, alg, num_envs, encoders_in_kernel=False, split=False):
-        """encoders_in_kernel: the estimator / scan / privileged encoders inside the kernel too
-        (actor blocks run 13 dependent layers; measured slower than running the encoders as
-        the grouped launches first and the kernel on their outputs, the default).
-        split (encoders outside): the critic blocks as their own launch on a side stream, beside
-        the encoders' launches, and the actor blocks after the encoders (the critic reads
-        only the critic observations)."""
+    def __init__(self, alg, num_envs):
+        """The estimator and the scan / privileged encoders run as grouped launches before the
+        kernel (inside it, the actor blocks' 13 dependent layers measured slower)."""
         ac, est = alg.actor_critic, alg.estimator
         self.alg = alg
-        self.enc_in_kernel = encoders_in_kernel
-        self.split = split and not encoders_in_kernel
-        self.side = torch.cuda.Stream(device=alg.device) if self.split else None
         dev = alg.device
         self.B = num_envs
         actor, critic = _chain(ac.actor), _chain(ac.critic)
@@ -105,16 +95,11 @@ class S8Act:
                 dst[i] = S.ActLayer(W=Wp.data_ptr(), ldw=steps, b=m.bias.data_ptr(), K=K, N=N,
                                     elu=int(i < len(layers) - 1))
             return len(layers)
-        if encoders_in_kernel:
-            a.n_est = fill(a.est, estc)
-            a.n_scan = fill(a.scan, scan)
-            a.n_priv = fill(a.priv, priv)
-        else:
-            # the encoders' outputs: spans of one [B, latent | scan latent | est] buffer
-            self.parts = torch.empty(num_envs, nlat + nscan + nest, device=dev)
-            self.spans = [self.parts[:, :nlat], self.parts[:, nlat:nlat + nscan], self.parts[:, nlat + nscan:]]
-            for q, t in enumerate(self.spans):
-                a.part_src[q], a.part_ld[q], a.part_w[q] = t.data_ptr(), t.stride(0), t.shape[1]
+        # the encoders' outputs: spans of one [B, latent | scan latent | est] buffer
+        self.parts = torch.empty(num_envs, nlat + nscan + nest, device=dev)
+        self.spans = [self.parts[:, :nlat], self.parts[:, nlat:nlat + nscan], self.parts[:, nlat + nscan:]]
+        for q, t in enumerate(self.spans):
+            a.part_src[q], a.part_ld[q], a.part_w[q] = t.data_ptr(), t.stride(0), t.shape[1]
         a.n_actor = fill(a.actor, actor, first_actor=True)
         a.n_critic = fill(a.critic, critic)
         self.mu = torch.empty(num_envs, actor[-1].out_features, device=dev)
@@ -176,27 +161,15 @@ class S8Act:
             a.est_obs, a.ld_est, a.n_est_obs = est.data_ptr(), est.stride(0), est.shape[1]
         else:
             a.obs_st = a.priv_st = a.critic_st = a.est_st = a.scan_st = a.est_obs = None
-        main = torch.cuda.current_stream()
-        if self.split:
-            # the critic blocks first, on the side stream (they overlap the encoders)
-            self.side.wait_stream(main)
-            a.nets = 2
-            with torch.cuda.stream(self.side):
-                S.act(a)
-            a.nets = 1
-        else:
-            a.nets = 0
-        if not self.enc_in_kernel:
-            # the estimator and the scan / privileged encoders: grouped launches writing their
-            # outputs into the spans the kernel reads
-            alg = self.alg
-            ac = alg.actor_critic
-            e_mod, e_in = alg.estimator.group_item(obs)
-            s_mod, s_in = ac.scan_encoder.group_item(scan)
-            p_mod, p_in = ac.privileged_encoder_.group_item(priv)
-            H.forward_group([(e_mod, e_in, None, self.spans[2]), (s_mod, s_in, None, self.spans[1]),
-                             (p_mod, p_in, None, self.spans[0])])
+        a.nets = 0
+        # the estimator and the scan / privileged encoders: grouped launches writing their
+        # outputs into the spans the kernel reads
+        alg = self.alg
+        ac = alg.actor_critic
+        e_mod, e_in = alg.estimator.group_item(obs)
+        s_mod, s_in = ac.scan_encoder.group_item(scan)
+        p_mod, p_in = ac.privileged_encoder_.group_item(priv)
+        H.forward_group([(e_mod, e_in, None, self.spans[2]), (s_mod, s_in, None, self.spans[1]),
+                         (p_mod, p_in, None, self.spans[0])])
         S.act(a)
-        if self.split:
-            main.wait_stream(self.side)
         return (self.mu if head is None else None), self.value

@@ -41,10 +41,6 @@ from legged_gym_custom_amd.rsl_rl.modules import hip_mlp as H
 from legged_gym_custom_amd.rsl_rl.modules import hip_s8 as S
 
 ENC_CHAIN = os.environ.get("LGX_S8_CHAIN", "1") != "0"  # the encoders' forward as one chain launch
-# their input gradients as one chain launch too (column sums per 32-row block)
-ENC_CHAIN_DX = os.environ.get("LGX_S8_CHAIN_DX", "0") != "0"
-# the actor's and critic's last layers (mu, value) as 1-layer chains instead of their own level
-TAIL_CHAIN = os.environ.get("LGX_S8_TAIL_CHAIN", "0") != "0"
 ROW_ALIGN = 64  # minibatch rows: whole K steps of every weight-gradient chunk
 
 
@@ -74,14 +70,16 @@ class S8Minibatch:
     def supported(alg, mb):
         if not alg.on_gpu or mb % ROW_ALIGN or mb <= 0:
             return False
+        # no fallback for a broken build: with the S8 update selected (LGX_S8_UPDATE, default on)
+        # a missing or stale liblgx_s8.so raises here (S.lib), it never silently selects the
+        # autograd path; only shapes the S8 layout does not cover return False
+        S.lib()
         ac = alg.actor_critic
-        try:
-            S.lib()
-        except Exception:  # noqa: BLE001 — the legacy path stays available
-            return False
         chains = [_chain(ac.actor), _chain(ac.critic), _chain(ac.privileged_encoder_.priv_encoder),
                   _chain(ac.scan_encoder.scan_encoder), _chain(alg.estimator.estimator)]
         if any(c is None for c in chains):
+            return False
+        if sum(len(c) for c in chains) > S.GROUP_MAX:  # one weight-gradient group (lgx_s8_pick_split)
             return False
         if ac.num_scan_obs <= 0 or ac.num_privileged_obs <= 0:
             return False
@@ -161,11 +159,9 @@ class S8Minibatch:
         self.dw_ws = torch.empty(tot, device=dev)
         self.tiles_m = (mb + 127) // 128
         self.nsb = (mb + S.SPLIT_ROWS - 1) // S.SPLIT_ROWS
-        self.nsb32 = (mb + 31) // 32
         for p in self.parts:
             # colsum partials of dy[l] (the bias gradient of layer l): [tiles][out_l]
-            # (the encoders' input-gradient chain writes one partial per 32 rows: nsb32)
-            p.cs = [torch.empty(max(self.tiles_m, self.nsb, self.nsb32), W.shape[0], device=dev) for W in p.W]
+            p.cs = [torch.empty(max(self.tiles_m, self.nsb), W.shape[0], device=dev) for W in p.W]
         self.cs_lat = torch.empty(self.tiles_m, self.P2 - self.P0, device=dev)
         # launch schedule: the level (grouped launch) of each chain's layer is its depth plus this
         # shift — the critic and the estimator do not feed the actor, so they can share the
@@ -181,8 +177,6 @@ class S8Minibatch:
         # instead of their own three grouped levels
         self.enc_chain = ENC_CHAIN and all(p.n <= S.CHAIN_MAXL and max(max(W.shape) for W in p.W) <= S.CHAIN_MAXW
                                            for p in (self.priv, self.scan))
-        self.enc_chain_dx = self.enc_chain and ENC_CHAIN_DX
-        self.tail_chain = TAIL_CHAIN and all(max(p.W[-1].shape) <= S.CHAIN_MAXW for p in (self.actor, self.critic))
         self._build(shapes)
 
     # ------------------------------------------------------------------ argument lists
@@ -205,13 +199,6 @@ class S8Minibatch:
             p.Wp = [S.packed_empty(W.shape[0], W.shape[1], self.dev) for W in p.W]
             for W, Wp in zip(p.W, p.Wp):
                 self.wsplit.append(S.split_packed_job(W.detach(), Wp))
-        for p in ((a, cr) if self.tail_chain else ()):
-            p.Wp_last = S.packed_empty(p.W[-1].shape[0], p.W[-1].shape[1], self.dev)
-            self.wsplit.append(S.split_packed_job(p.W[-1].detach(), p.Wp_last))
-        for p in ((pr, sc) if self.enc_chain_dx else ()):
-            p.WpT = [None] + [S.packed_empty(W.shape[1], W.shape[0], self.dev) for W in p.W[1:]]
-            for W, WpT in zip(p.W[1:], p.WpT[1:]):
-                self.wsplit.append(S.split_packed_job(W.detach(), WpT, transpose=True))
         self._fwd_levels = None  # built per minibatch offset (input row pointers)
         self._shapes = shapes
 
@@ -263,15 +250,7 @@ class S8Minibatch:
 
         def put(level, args):
             levels.setdefault(level, []).append(args)
-        chains, tails = [], []
-
-        def tail(p, A_ptr, lda, K, C32, ldc32):
-            """p's last layer as a 1-layer chain (fp32 output only)."""
-            c = S.ChainArgs(A=A_ptr, lda=lda, rows=mb, nlayers=1)
-            L = c.layers[0]
-            L.W, L.packed, L.bias, L.K, L.N = p.Wp_last.data_ptr(), 1, p.b[-1].data_ptr(), K, p.W[-1].shape[0]
-            L.C32, L.ldc32 = C32, ldc32
-            tails.append(c)
+        chains = []
         for p in (pr, sc, es, cr):
             A_ptr, lda, K = ins[p.name]
             if self.enc_chain and p in (pr, sc):
@@ -313,8 +292,6 @@ class S8Minibatch:
                 elif p is es:
                     put(l + sh, self._fwd(p, l, A_ptr, lda, K, C32=self.pred.data_ptr(), ldc32=self.pred.shape[1],
                                           elu=False))
-                elif self.tail_chain:
-                    tail(p, A_ptr, lda, K, self.value.data_ptr(), 1)
                 else:
                     put(l + sh, self._fwd(p, l, A_ptr, lda, K, C32=self.value.data_ptr(), ldc32=1, elu=False))
         A_ptr, lda, K = row(self.ain), lda_ain, self.W8
@@ -324,16 +301,12 @@ class S8Minibatch:
                 o = a.out[l]
                 put(lev, self._fwd(a, l, A_ptr, lda, K, C=o.data_ptr(), ldc=o.shape[1]))
                 A_ptr, lda, K = o.data_ptr(), o.shape[1], a.W[l].shape[0]
-            elif self.tail_chain:
-                tail(a, A_ptr, lda, K, self.mu.data_ptr(), self.mu.shape[1])
             else:
                 put(lev, self._fwd(a, l, A_ptr, lda, K, C32=self.mu.data_ptr(), ldc32=self.mu.shape[1], elu=False))
         if chains:
             S.chain(chains)
         for lev in sorted(levels):
             S.gemm_group(levels[lev], S.FWD)
-        if tails:
-            S.chain(tails)
         # 3. loss heads: forward sums and input gradients in one launch; the narrow output
         #    gradients straight into S8 with their per-256-row column sums (the last layers'
         #    bias gradients)
@@ -357,6 +330,15 @@ class S8Minibatch:
         s8 = H.HeadsS8Args(dmu_s8=a.dy[-1].data_ptr(), ld_dmu=a.dy[-1].shape[1], dmu_cs=a.cs[-1].data_ptr(),
                            dvalue_s8=cr.dy[-1].data_ptr(), ld_dvalue=cr.dy[-1].shape[1], dvalue_cs=cr.cs[-1].data_ptr(),
                            de_s8=es.dy[-1].data_ptr(), ld_de=es.dy[-1].shape[1], de_cs=es.cs[-1].data_ptr())
+        dec = getattr(alg, "_decisions", None)
+        if dec is not None:
+            # test hook (tests/learner_replay.py, eager updates only): the k-th minibatch's
+            # per-sample clip / max decisions replayed from a reference run ("in") and / or
+            # recorded ("out"), include/lgx_mlp.h lgx_heads_s8_args
+            k = dec["k"]
+            dec["k"] = k + 1
+            s8.decisions_in = dec["in"][k].data_ptr() if dec.get("in") is not None else None
+            s8.decisions_out = dec["out"][k].data_ptr() if dec.get("out") is not None else None
         H._check(H.lib().lgx_loss_heads_fused(H.C.byref(h), H.C.byref(x), H.C.byref(s8), H._stream()),
                  "lgx_loss_heads_fused")
         # 4. input gradients
@@ -385,19 +367,7 @@ class S8Minibatch:
         lev_lat = a.n - 1
         bput(lev_lat, dx(a, 0, a.dy[0], self.dlat.data_ptr(), self.cs_lat, N=self.P2 - self.P0,
                          Bptr=S.group_ptr(a.Ws[0], self.P0), elu=False, addend=self.dp))
-        dchains = []
         for p, c0 in ((pr, 0), (sc, self.P1 - self.P0)):
-            if self.enc_chain_dx:
-                # the encoder's input gradients, all layers in one chain launch (after the
-                # levels): dy_{l-1} = (dy_l W_l) * ELU'(y_{l-1}), the 128-row column sums
-                c = S.ChainArgs(A=S.group_ptr(self.dlat, c0), lda=self.dlat.shape[1], rows=mb, nlayers=p.n - 1)
-                for q, l in enumerate(range(p.n - 1, 0, -1)):
-                    L = c.layers[q]
-                    L.W, L.packed, L.K, L.N, L.elu = p.WpT[l].data_ptr(), 1, p.W[l].shape[0], p.W[l].shape[1], 2
-                    L.act, L.ld_act = p.out[l - 1].data_ptr(), p.out[l - 1].shape[1]
-                    L.C, L.ldc, L.colsum_ws = p.dy[l - 1].data_ptr(), p.dy[l - 1].shape[1], p.cs[l - 1].data_ptr()
-                dchains.append(c)
-                continue
             for l in range(p.n - 1, 0, -1):
                 dy = self.dlat if l == p.n - 1 else p.dy[l]
                 if l == p.n - 1:
@@ -411,8 +381,6 @@ class S8Minibatch:
                 bput(lev_lat + 1 + (p.n - 1 - l), args)
         for lev in sorted(blev):
             S.gemm_group(blev[lev], S.DX)
-        if dchains:
-            S.chain(dchains)
         # 5. weight gradients (one launch) and the reductions into the flat gradient buffer
         g_args, red = [], []
         off = 0
@@ -455,8 +423,6 @@ class S8Minibatch:
                                              tm))
                     continue
                 from_split = l == p.n - 1  # the loss heads' gradients: lgx_s8_split partials (256 rows)
-                chained = self.enc_chain_dx and p in (pr, sc)  # the chain's 32-row partials
-                red.append(S.flat_reduce(p.cs[l].data_ptr(), n, bg.data_ptr(), n,
-                                         nsb if from_split else self.nsb32 if chained else tm))
+                red.append(S.flat_reduce(p.cs[l].data_ptr(), n, bg.data_ptr(), n, nsb if from_split else tm))
         S.gemm_group(g_args, S.DW)
         S.reduce(red)

@@ -20,7 +20,7 @@ import torch.nn as nn
 _LIB_PATH = os.environ.get("LGX_MLP_LIB") or os.path.join(
     os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))), "lib", "liblgx_mlp.so")
 _lib = None
-ABI_VERSION = 7
+ABI_VERSION = 8
 EPI_BIAS, EPI_ELU, EPI_DELU, EPI_ACCUM = 1, 2, 4, 8
 EXPORTED = ["lgx_mlp_abi_version", "lgx_mlp_sizeof_gemm_args", "lgx_mlp_pick_split", "lgx_gemm",
             "lgx_mlp_last_error", "lgx_adam_step", "lgx_ppo_head_forward", "lgx_ppo_head_backward",
@@ -83,7 +83,8 @@ class HeadsS8Args(C.Structure):
     """Mirror of lgx_heads_s8_args (pitches in S8 elements)."""
     _fields_ = [("dmu_s8", C.c_void_p), ("ld_dmu", C.c_int64), ("dmu_cs", C.c_void_p),
                 ("dvalue_s8", C.c_void_p), ("ld_dvalue", C.c_int64), ("dvalue_cs", C.c_void_p),
-                ("de_s8", C.c_void_p), ("ld_de", C.c_int64), ("de_cs", C.c_void_p)]
+                ("de_s8", C.c_void_p), ("ld_de", C.c_int64), ("de_cs", C.c_void_p),
+                ("decisions_in", C.c_void_p), ("decisions_out", C.c_void_p)]
 
 
 class TailArgs(C.Structure):

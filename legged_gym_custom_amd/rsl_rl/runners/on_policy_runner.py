@@ -122,6 +122,7 @@ class OnPolicyRunner:
         self.use_graphs = str(device).startswith("cuda")
         self._graphs = {}
         self._eager_rollouts = {}  # per adaptation mode
+        self._graphs_gen = getattr(self.alg, "graph_generation", 0)
         self._stats = None
         self._obs = None
         _ = self.env.reset()
@@ -224,7 +225,18 @@ class OnPolicyRunner:
         # one graph per (DAgger iteration's adaptation-mode rollout, PPO rollout) x tracking
         return ("rollout", track) if not adaptation_mode else ("rollout", track, "adaptation")
 
+    def _check_generation(self):
+        """Drop the rollout graphs when the algorithm has dropped the state they replay
+        (PPO.invalidate_graphs frees the act kernel's buffers: a stale replay would read and
+        write freed memory)."""
+        gen = getattr(self.alg, "graph_generation", 0)
+        if gen != self._graphs_gen:
+            self._graphs = {}
+            self._eager_rollouts = {}
+            self._graphs_gen = gen
+
     def _rollout(self, adaptation_mode, track):
+        self._check_generation()
         key = self._rollout_key(adaptation_mode, track)
         if self._graphable(adaptation_mode) and key in self._graphs:
             self._graphs[key].replay()
@@ -241,6 +253,7 @@ class OnPolicyRunner:
         warmed every kernel and the storage is empty). Capture does not execute anything. The
         DAgger iterations' rollout (adaptation mode: the latent from the adaptation encoder over
         the observation history, ppo.py:135-141) gets its own graph."""
+        self._check_generation()
         key = self._rollout_key(adaptation_mode, track)
         if (key in self._graphs or not self._graphable(adaptation_mode)
                 or self._eager_rollouts.get(bool(adaptation_mode), 0) < 1):

@@ -32,6 +32,14 @@ import numpy as np
 N, T = 64, 24            # default envs per case (CASES[...]["N"] overrides), steps per rollout
 TOTAL_UPDATES = 10000.0  # ppo.py:218-220: stage 0.5 of 5000..15000 -> coefficient 0.025
 SAMPLE = 2048            # entries kept per large tensor (plus its fp64 sum / sum of squares)
+SAMPLE_MB = 256          # per-minibatch gradients: entries kept per tensor
+# a per-sample decision of the PPO head (ratio clip, surrogate / value max) whose two sides are
+# within this relative margin: fp32 rounding of the log-prob (~1e-5 on a 3 x bf16 GEMM path) can
+# put the sample on the other side (tools/ref_minibatch_ties.py)
+NEAR_TIE = 3e-5
+# decision byte (include/lgx_mlp.h lgx_heads_s8_args.decisions): surrogate max weight of the
+# unclipped term x2 (bits 0-1), ratio in band (bit 2), value max weight x2 (bits 3-4), v - target
+# in band (bit 5)
 
 CASES = {
     # go2 network shapes (go2_config.py:180-200; estimator defaults support_networks.py:45) with
@@ -124,17 +132,17 @@ def permutation(case, which):
     return _rng(case, 4, which).permutation(n_envs(case) * T).astype(np.int64)
 
 
-def sample_index(name, size):
+def sample_index(name, size, sample=SAMPLE):
     """Fixed entry subset of a flattened tensor (all of it when small)."""
-    if size <= SAMPLE:
+    if size <= sample:
         return np.arange(size, dtype=np.int64)
-    return np.sort(np.random.default_rng([7, _key(name)]).choice(size, SAMPLE, replace=False)).astype(np.int64)
+    return np.sort(np.random.default_rng([7, _key(name)]).choice(size, sample, replace=False)).astype(np.int64)
 
 
-def record(out, prefix, name, arr):
+def record(out, prefix, name, arr, sample=SAMPLE):
     """Store a tensor's sampled entries and its full fp64 sum / sum of squares."""
     flat = np.asarray(arr, dtype=np.float32).reshape(-1)
-    idx = sample_index(name, flat.size)
+    idx = sample_index(name, flat.size, sample)
     out[f"{prefix}.{name}.v"] = flat[idx]
     out[f"{prefix}.{name}.sum"] = np.float64(flat.astype(np.float64).sum())
     out[f"{prefix}.{name}.sumsq"] = np.float64((flat.astype(np.float64) ** 2).sum())

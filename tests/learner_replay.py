@@ -147,3 +147,79 @@ def run(case, device, use_graphs=None):
 
 def meta(d):
     return json.loads(str(d["meta_json"]))
+
+
+DEC_SURR = 0x07   # decision byte: surrogate max weight (bits 0-1) + ratio in band (bit 2)
+DEC_VALUE = 0x18  # value-loss max weight (bits 3-4)
+DEC_VBAND = 0x20  # v - target inside the value clip band (bit 5)
+
+
+def effective_mismatch(ref, got):
+    """Per-sample disagreement of two decision byte arrays: every bit except the value-loss max
+    weight of samples inside the value clip band, where both terms of that max are the same
+    number up to rounding and give the same gradient (ppo.py:258-261)."""
+    ref, got = ref.astype(np.int32), got.astype(np.int32)
+    mask = np.where((ref & DEC_VBAND) != 0, DEC_SURR | DEC_VBAND, DEC_SURR | DEC_VALUE | DEC_VBAND)
+    return np.flatnonzero((ref & mask) != (got & mask))
+
+
+def run_per_minibatch(case, device, d, force=True):
+    """The fixture's sequence with the update run eagerly minibatch by minibatch: with `force`, the
+    PPO head takes every per-sample discrete decision (ratio clip, surrogate / value max) from
+    the reference run's record (d["mb<k>.decisions"]), so the trajectory follows the reference's
+    branch at every sample; the launch also records its OWN decisions. Returns per minibatch the
+    sampled pre-clip gradients (+ fp64 sums), both pre-clip norms and the own decisions, and the
+    end state (parameters, Adam moments)."""
+    alg = build(case, device, use_graphs=False)
+    res = {}
+    rollout(alg, case, 0, res, True, device)
+    perm0 = torch.from_numpy(LC.permutation(case, 0)).to(device)
+    alg._next_perm = lambda n: perm0
+    alg.update_dagger()
+    rollout(alg, case, 1, res, False, device)
+    alg.total_updates = LC.TOTAL_UPDATES
+    perm1 = torch.from_numpy(LC.permutation(case, 1)).to(device)
+    alg._next_perm = lambda n: perm1
+    n_mb = alg.num_learning_epochs * alg.num_mini_batches
+    mb = perm1.numel() // alg.num_mini_batches
+    dec_in = None
+    if force:
+        dec_in = torch.stack([torch.from_numpy(d[f"mb{k}.decisions"]) for k in range(n_mb)]).to(device)
+    dec_out = torch.zeros(n_mb, mb, dtype=torch.uint8, device=device)
+    alg._decisions = {"k": 0, "in": dec_in, "out": dec_out}
+    grads, norms = [], []
+    inner = alg._minibatch_grads
+
+    def wrapped(idx):
+        inner(idx)
+        g = alg.grads
+        rec = {}
+        for n, p in named_params(alg):
+            if n.startswith("adaptation"):
+                continue
+            flat = p.grad.detach().reshape(-1)
+            sel = torch.from_numpy(LC.sample_index(n, flat.numel(), LC.SAMPLE_MB)).to(device)
+            f64 = flat.double()
+            rec[n] = (_np(flat[sel]), float(f64.sum()), float((f64 * f64).sum()))
+        grads.append(rec)
+        est = g.segment("estimator").double().norm()
+        main = torch.cat([g.segment("main"), g.segment("adaptation")]).double().norm()
+        norms.append((float(est), float(main)))
+
+    alg._minibatch_grads = wrapped
+    alg.update()
+    del alg._minibatch_grads
+    assert alg._s8 is not None and alg._decisions["k"] == n_mb, "every minibatch ran on the S8 path"
+    alg._decisions = None
+    res["mbg"], res["norms"], res["dec_out"] = grads, norms, dec_out.cpu().numpy()
+    res["after"] = {n: _np(p) for n, p in named_params(alg)}
+    names_of = {id(p): n for n, p in named_params(alg)}
+    res["exp_avg"], res["exp_avg_sq"] = {}, {}
+    for oname in ("optimizer", "estimator_optimizer"):
+        opt = getattr(alg, oname)
+        for grp in opt.param_groups:
+            for p in grp["params"]:
+                st = opt.state[p]
+                res["exp_avg"][names_of[id(p)]] = _np(st["exp_avg"])
+                res["exp_avg_sq"][names_of[id(p)]] = _np(st["exp_avg_sq"])
+    return res, alg

@@ -61,6 +61,27 @@ def test_graph_rollout_equals_eager():
     assert int(env_b._step_dev) == env_b.common_step_counter + 1  # the next step's number
 
 
+def test_rollout_graph_dropped_when_algorithm_invalidates():
+    """PPO.invalidate_graphs (e.g. after grads.rebind() in update()) frees the act kernel's
+    buffers (S8Act) that the captured rollout replays; the runner must re-capture instead of
+    replaying into freed memory. The freed blocks are refilled with garbage before
+    the next rollout: the results still equal the eager loop bit for bit."""
+    env_a, run_a = _setup(False)
+    eager = _run(env_a, run_a, 3) + _run(env_a, run_a, 3)
+    env_b, run_b = _setup(True)
+    graph = _run(env_b, run_b, 3)
+    assert ("rollout", True) in run_b._graphs
+    gen = run_b.alg.graph_generation
+    run_b.alg.invalidate_graphs()
+    assert run_b.alg.graph_generation == gen + 1
+    junk = [torch.full((1 << 20,), float("nan"), device="cuda:0") for _ in range(64)]  # noqa: F841
+    graph += _run(env_b, run_b, 3)
+    assert ("rollout", True) in run_b._graphs  # re-captured after one eager rollout
+    for i, (a, b) in enumerate(zip(eager, graph)):
+        for k in ("obs", "rew", "dones", "root"):
+            torch.testing.assert_close(b[k], a[k], rtol=0, atol=0, msg=f"iteration {i} {k}")
+
+
 def test_graph_adaptation_rollout_equals_eager():
     """The DAgger iterations' rollout (adaptation mode: the adaptation encoder's latent over the
     observation history drives the actor, ppo.py:135-141) replayed from its own hipGraph equals

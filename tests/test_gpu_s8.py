@@ -129,6 +129,68 @@ def test_weight_grad_split_k(S, rows, M, N, split):
     assert ((out.double() - 0.25) - ref).abs().le(bound + 1e-6).all(), float(((out.double() - 0.25) - ref).abs().max())
 
 
+def _tail_buffer(rows, ld):
+    """An S8 buffer [rows, ld] ending exactly at the end of its own 2 MiB allocation (the caching
+    allocator gives a 2 MiB request its own segment): a read past its last row leaves the segment."""
+    n = 1 << 19  # int32 words = 2 MiB
+    assert rows * ld <= n
+    flat = torch.zeros(n, dtype=torch.int32, device=dev)
+    return flat, flat[n - rows * ld:].view(rows, ld)
+
+
+def test_column_span_operands_at_allocation_end(S):
+    """Regression test for the round-4 fault (gpurun_out/s8_update_tests.log:70, "illegal memory
+    access" under test_gpu_learner.py): TR-mode operand offsets were clamped to the row PITCH, so
+    an operand that is a column span of a wider row (the actor's latent columns, the encoders'
+    last-layer gradients) read up to its column offset past the buffer's last row. Every operand
+    here is a column span (offset 64, width 40, pitch 128) of a buffer flush against the end of
+    its allocation; FWD, DX and DW against fp64 (lgx_s8.hip Op::offsets clamps to the span)."""
+    g = torch.Generator(device="cpu").manual_seed(11)
+    c0, w, ld = 64, 40, 128
+    rows, K = 1024, 512
+    # DX: dX = dY W[:, span] with W [K, ld] read TR (k = source row), span at column c0
+    W = (torch.randn(K, ld, generator=g) * 0.1).to(dev)
+    _keep_w, Wb = _tail_buffer(K, ld)
+    Wb.copy_(_s8(S, W, ld=ld))
+    dy = torch.randn(rows, K, generator=g).to(dev)
+    dys = _s8(S, dy)
+    out = S.empty(rows, w, dev)
+    S.gemm_group([S.GemmArgs(A=dys.data_ptr(), lda=dys.shape[1], B=S.group_ptr(Wb, c0), ldb=ld, M=rows, N=w, K=K,
+                             C=out.data_ptr(), ldc=out.shape[1])], S.DX)
+    # DW: dW = dY[:, span]^T X[:, span], both TR column spans of tail buffers (K = rows)
+    A = torch.randn(rows, ld, generator=g).to(dev)
+    X = torch.randn(rows, ld, generator=g).to(dev)
+    _keep_a, Ab = _tail_buffer(rows, ld)
+    _keep_x, Xb = _tail_buffer(rows, ld)
+    Ab.copy_(_s8(S, A, ld=ld))
+    Xb.copy_(_s8(S, X, ld=ld))
+    dw = torch.zeros(w, w, device=dev)
+    S.gemm_group([S.GemmArgs(A=S.group_ptr(Ab, c0), lda=ld, B=S.group_ptr(Xb, c0), ldb=ld, M=w, N=w, K=rows,
+                             epilogue=S.EPI_ACCUM, C32=dw.data_ptr(), ldc32=w, split=1)], S.DW)
+    # FWD: Y = X[:, c0:] V^T with the input a ROW-mode column span (the last 64 columns: whole
+    # K steps) of a tail buffer
+    kf = ld - c0
+    V = (torch.randn(24, kf, generator=g) * 0.1).to(dev)
+    Vs = _s8(S, V)
+    y = torch.full((rows, 24), float("nan"), device=dev)
+    S.gemm_group([S.GemmArgs(A=S.group_ptr(Xb, c0), lda=ld, B=Vs.data_ptr(), ldb=Vs.shape[1], M=rows, N=24, K=kf,
+                             C32=y.data_ptr(), ldc32=24)], S.FWD)
+    torch.cuda.synchronize()
+    Wv = S.from_s8(Wb, K, ld).double()[:, c0:c0 + w]
+    dyv = S.from_s8(dys, rows, K).double()
+    ref = dyv @ Wv
+    got = S.from_s8(out, rows, w).double()
+    assert (got - ref).abs().le(_bound(dyv, Wv) + 1e-5 * ref.abs() + 1e-6).all(), float((got - ref).abs().max())
+    Av = S.from_s8(Ab, rows, ld).double()[:, c0:c0 + w]
+    Xv = S.from_s8(Xb, rows, ld).double()[:, c0:c0 + w]
+    ref = Av.t() @ Xv
+    assert (dw.double() - ref).abs().le(_bound(Av.t(), Xv) + 1e-6).all(), float((dw.double() - ref).abs().max())
+    Vv = S.from_s8(Vs, 24, kf).double()
+    Xf = S.from_s8(Xb, rows, ld).double()[:, c0:]
+    ref = Xf @ Vv.t()
+    assert (y.double() - ref).abs().le(_bound(Xf, Vv.t()) + 1e-6).all(), float((y.double() - ref).abs().max())
+
+
 def test_grouped_launch_equals_single_launches(S):
     """Several problems in one launch give the single launches' results bit for bit."""
     g = torch.Generator(device="cpu").manual_seed(3)

@@ -152,6 +152,87 @@ def adam_state(opt, names_of):
     return res
 
 
+class PerMinibatch:
+    """Hooks on the reference update (ppo.py:182-293) recording every minibatch: torch.clamp
+    (the ratio clamp, :252) and Tensor.clamp (v - target, :258) for the in-band bits, torch.max
+    (:254 surrogate, :261 value loss) for the max weights, clip_grad_norm_ for the gradients and
+    norms. Decisions are torch's gradient rules: max(x, y) gives x weight 1 / 0.5 / 0 for x > y,
+    x == y, x < y; clamp passes the gradient on [min, max]."""
+
+    def __init__(self, alg, names_of):
+        self.alg, self.names_of = alg, names_of
+        self.cur, self.mbs = {}, []
+
+    def install(self):
+        self._clip, self._max, self._clamp, self._tclamp = (nn.utils.clip_grad_norm_, torch.max, torch.clamp,
+                                                            torch.Tensor.clamp)
+        me = self
+
+        def clip_hook(params, max_norm, *a, **k):
+            params = list(params)
+            est = all(me.names_of[id(p)].startswith("estimator.") for p in params)
+            grads = {me.names_of[id(p)]: p.grad.detach().numpy().copy() for p in params if p.grad is not None}
+            total = me._clip(params, max_norm, *a, **k)
+            me.cur.setdefault("grads", {}).update(grads)
+            me.cur["norm_est" if est else "norm_main"] = float(total)
+            if not est:  # the minibatch's last hook call (ppo.py:275)
+                me.mbs.append(me.cur)
+                me.cur = {}
+            return total
+
+        def max_hook(*a, **k):
+            if len(a) == 2 and isinstance(a[1], torch.Tensor) and a[0].dim() >= 1:
+                x, y = a[0].detach(), a[1].detach()
+                w = (x > y).to(torch.uint8) * 2 + (x == y).to(torch.uint8)
+                rel = (x - y).abs() / torch.maximum(x.abs(), y.abs()).clamp_min(1e-30)
+                key = "surr" if "surr_w" not in me.cur else "value"
+                me.cur[key + "_w"] = w.reshape(-1).numpy().copy()
+                me.cur[key + "_margin"] = torch.where(x == y, torch.ones_like(rel), rel).reshape(-1).numpy().copy()
+            return me._max(*a, **k)
+
+        def band(x, lo, hi):
+            x = x.detach()
+            inb = ((x >= lo) & (x <= hi)).reshape(-1).numpy().copy()
+            scale = max(abs(lo), abs(hi))
+            margin = (torch.minimum((x - lo).abs(), (x - hi).abs()) / scale).reshape(-1).numpy().copy()
+            return inb, margin
+
+        def clamp_hook(*a, **k):  # torch.clamp(ratio, 1 - clip, 1 + clip)
+            if len(a) == 3 and not k and isinstance(a[1], float) and isinstance(a[2], float):
+                me.cur["ratio_in"], me.cur["ratio_band"] = band(a[0], a[1], a[2])
+            return me._clamp(*a, **k)
+
+        def tclamp_hook(*a, **k):  # (value - target).clamp(-clip, clip)
+            if len(a) == 3 and not k and isinstance(a[1], float) and isinstance(a[2], float):
+                me.cur["value_in"], me.cur["value_band"] = band(a[0], a[1], a[2])
+            return me._tclamp(*a, **k)
+
+        nn.utils.clip_grad_norm_ = clip_hook
+        torch.max = max_hook
+        torch.clamp = clamp_hook
+        torch.Tensor.clamp = tclamp_hook
+
+    def remove(self):
+        nn.utils.clip_grad_norm_, torch.max, torch.clamp, torch.Tensor.clamp = (self._clip, self._max, self._clamp,
+                                                                                self._tclamp)
+
+    def store(self, out):
+        for k, m in enumerate(self.mbs):
+            for n, g in m["grads"].items():
+                if not n.startswith("adaptation"):
+                    LC.record(out, f"mbg{k}", n, g, sample=LC.SAMPLE_MB)
+            out[f"mb{k}.norms"] = np.array([m["norm_est"], m["norm_main"]], dtype=np.float64)
+            dec = (m["surr_w"].astype(np.uint8) | (m["ratio_in"].astype(np.uint8) << 2) |
+                   (m["value_w"].astype(np.uint8) << 3) | (m["value_in"].astype(np.uint8) << 5))
+            out[f"mb{k}.decisions"] = dec
+            # inside the value clip band both terms of the value max are the same number up to
+            # rounding (v vs target + (v - target)) and give the same gradient: not a decision
+            near = ((m["surr_margin"] < LC.NEAR_TIE) | (m["ratio_band"] < LC.NEAR_TIE) |
+                    (m["value_band"] < LC.NEAR_TIE) | (~m["value_in"].astype(bool) &
+                                                       (m["value_margin"] < LC.NEAR_TIE)))
+            out[f"mb{k}.near"] = np.flatnonzero(near).astype(np.int32)
+
+
 def main(cases):
     for case in cases:
         alg = build(case)
@@ -221,11 +302,18 @@ def main(cases):
 
         once(alg.optimizer, "main", "optimizer")
         once(alg.estimator_optimizer, "est", "estimator_optimizer")
+        # every minibatch (round 5): the pre-clip gradients (sampled + fp64 sums), both norms, the
+        # surrogate / value losses and the per-sample discrete decisions (LC.DEC_* bits), with the
+        # samples whose decision sits within LC.NEAR_TIE of its boundary
+        per_mb = PerMinibatch(alg, names_of)
+        per_mb.install()
         _Inject.perm = torch.from_numpy(LC.permutation(case, 1))
         mv, ms, mr, coef, me = alg.update()
         _Inject.perm = None
+        per_mb.remove()
         nn.utils.clip_grad_norm_ = orig_clip
         del alg.optimizer.step, alg.estimator_optimizer.step
+        per_mb.store(out)
         for key in ("main", "est"):
             for n, p in mb0[key].items():
                 LC.record(out, "mb0", n, p)
