@@ -248,6 +248,8 @@ class PPO:
         self._s8 = None  # S8Minibatch, built at the first update (static buffers for the graphs)
         self.use_fused_act = USE_FUSED_ACT and self.on_gpu
         self._s8act = None  # S8Act, built at the first (eager) act
+        self._dagger_graph = None  # update_dagger's hipGraph (GPU, world size 1)
+        self._dagger_sum = torch.zeros((), device=device)
 
     # ------------------------------------------------------------------ flat Adam (HIP)
     def _flatten_params_and_moments(self):
@@ -345,7 +347,7 @@ class PPO:
                                 noise=noise, actions=s.actions[k], mu=s.mu[k], sigma=s.sigma[k],
                                 logp=s.actions_log_prob[k], actions_copy=dst)
                     _, t.values = fused.run(obs, privileged_obs, critic_obs, scan_obs, est=true_estimated_obs,
-                                            rows=slots, head=head)
+                                            rows=slots, head=head, adaptation_mode=adaptation_mode)
                 else:
                     items = [self.estimator.group_item(obs), ac.scan_encoder.group_item(scan_obs)]
                     if not adaptation_mode:
@@ -376,9 +378,9 @@ class PPO:
         return t.actions
 
     def _fused_act(self, adaptation_mode):
-        """The one-launch act networks (S8Act) for this rollout step, or None: adaptation mode
-        (DAgger iterations), shapes it does not cover, or disabled. Built outside graph capture."""
-        if adaptation_mode or not self.use_fused_act:
+        """The one-launch act networks (S8Act) for this rollout step (PPO and DAgger iterations),
+        or None: shapes it does not cover, or disabled. Built outside graph capture."""
+        if not self.use_fused_act:
             return None
         n = self.storage.num_envs
         if self._s8act is not None and self._s8act.B == n:
@@ -716,6 +718,7 @@ class PPO:
         self.graph_mode = None
         self._s8 = None
         self._s8act = None
+        self._dagger_graph = None
         self.graph_generation += 1
 
     def _run_update(self):
@@ -784,17 +787,79 @@ class PPO:
 
     def update_dagger(self):
         """ppo.py:309-349: adaptation-encoder-only imitation of the privileged latent
-        (same epoch-shared permutation and minibatch slices as update())."""
+        (same epoch-shared permutation and minibatch slices as update()).
+
+        GPU: the privileged latents and the observation rows of every sample are formed once per
+        update in the epoch-shared permutation (the privileged encoder does not train here, and
+        minibatch i is the same rows every epoch), and the 20 minibatches (adaptation encoder
+        forward + backward, L2 loss, clip, Adam) are one hipGraph: the first call runs eagerly on
+        a side stream and records the graph, later calls replay it. The loss sum stays on the
+        device until the one .item() of the return value (ppo.py:347)."""
         if not self.grads.check():
             self.grads.rebind()
             self.invalidate_graphs()
+        self._perm.copy_(self._next_perm(self._perm.numel()))
+        n = self.num_learning_epochs * self.num_mini_batches
+        if not self.on_gpu:
+            total = self._dagger_body_cpu()
+        elif not self.use_graphs or _distributed():
+            self._dagger_body()
+            total = self._dagger_sum
+        else:
+            if self._dagger_graph is None:
+                cur = torch.cuda.current_stream(self.device)
+                side = torch.cuda.Stream(self.device)
+                side.wait_stream(cur)
+                with torch.cuda.stream(side):
+                    self._dagger_body()
+                cur.wait_stream(side)
+                torch.cuda.synchronize(self.device)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=torch.cuda.graph_pool_handle(), capture_error_mode=self.capture_mode()):
+                    self._dagger_body()
+                self._dagger_graph = g
+            else:
+                self._dagger_graph.replay()
+            total = self._dagger_sum
+        mean_adaptation_loss = (total / n).item()
+        self.storage.clear()
+        self.increase_update_count()
+        return mean_adaptation_loss
+
+    def _dagger_body(self):
+        """The GPU DAgger update's kernels (fixed addresses: captured by the graph)."""
+        ac = self.actor_critic
+        adapt = self.grads.segment("adaptation")
+        s = self.storage
+        rows = self._perm.numel()
+        mb = rows // self.num_mini_batches
+        with torch.no_grad():
+            obs = s.observations.flatten(0, 1)
+            obs_p, priv_p = hip_mlp.gather_rows([obs, s.privileged_observations.flatten(0, 1)], self._perm)
+            priv_lat = ac.privileged_encoder(priv_p)
+        self._dagger_sum.zero_()
+        for _ in range(self.num_learning_epochs):
+            for i in range(self.num_mini_batches):
+                adapt_latent = ac.adaptation_encoder(obs_p[i * mb:(i + 1) * mb])
+                adaptation_loss = (priv_lat[i * mb:(i + 1) * mb] - adapt_latent).norm(p=2, dim=1).mean()
+                adapt.zero_()
+                adaptation_loss.backward()
+                if _distributed():
+                    dist.all_reduce(adapt)
+                    adapt.div_(dist.get_world_size())
+                with torch.no_grad():
+                    _clip_([adapt], self.max_grad_norm)
+                    self._adam("adaptation_optimizer", self._adapt_lr)
+                    self._dagger_sum.add_(adaptation_loss.detach())
+
+    def _dagger_body_cpu(self):
+        """The CPU learner's DAgger update (the reference's statement order, per-minibatch
+        gathers)."""
         total = torch.zeros((), device=self.device)
         ac = self.actor_critic
         adapt = self.grads.segment("adaptation")
-        self._perm.copy_(self._next_perm(self._perm.numel()))
-        slices = self._perm_slices()
         for _ in range(self.num_learning_epochs):
-            for idx in slices:
+            for idx in self._perm_slices():
                 obs_b, priv_b = self.storage.gather_fields(idx, ("observations", "privileged_observations"))
                 with torch.no_grad():
                     priv_latent = ac.privileged_encoder(priv_b)
@@ -807,15 +872,9 @@ class PPO:
                     adapt.div_(dist.get_world_size())
                 with torch.no_grad():
                     _clip_([adapt], self.max_grad_norm)
-                    if self.on_gpu:
-                        self._adam("adaptation_optimizer", self._adapt_lr)
-                if not self.on_gpu:
-                    self.adaptation_optimizer.step()
+                self.adaptation_optimizer.step()
                 total += adaptation_loss.detach()
-        mean_adaptation_loss = (total / (self.num_learning_epochs * self.num_mini_batches)).item()
-        self.storage.clear()
-        self.increase_update_count()
-        return mean_adaptation_loss
+        return total
 
     # ------------------------------------------------------------------ checkpoints
     def optimizer_state_dicts(self):

@@ -8,8 +8,8 @@ latent | est] in the update's segmented layout. The weights are packed once per 
 first step, inside the rollout graph). The kernel also writes this step's observation rows of
 the storage (rollout_storage.py:87-105; no separate copy launch) and, given `head`, runs the act
 head in the actor blocks (a = mu + std * eps, the Normal log-prob, the action / mu / sigma rows:
-lgx_act_head's arithmetic, ppo.py:141-147), mu never leaving LDS. Adaptation-mode rollouts (the DAgger iterations: the latent from the adaptation
-encoder) keep the grouped launches.
+lgx_act_head's arithmetic, ppo.py:141-147), mu never leaving LDS. Adaptation-mode rollouts (the DAgger
+iterations) run the same kernel with the latent from the adaptation encoder (one fused launch).
 
 Numerics: the same 3 x bf16 products as the grouped launches; the actor's first layer sums its
 input in the segmented order (the gaps are zeros), so mu differs from the grouped path by fp32
@@ -112,13 +112,15 @@ class S8Act:
         after the update changed them)."""
         S.act_pack(self.wpack)
 
-    def run(self, obs, priv, critic, scan, est=None, rows=None, head=None):
+    def run(self, obs, priv, critic, scan, est=None, rows=None, head=None, adaptation_mode=False):
         """(mu [B, A], value [B, 1]) of this step's observations (static output buffers).
         rows (optional): this step's storage rows [obs, priv, critic, est, scan] (contiguous),
         which the kernel fills from the inputs (est: the true estimated obs, copied only).
         head (optional): dict(std, eps, actions, mu, sigma, logp, actions_copy, noise) as
         hip_mlp.act_head takes them; the kernel then writes those rows and NOT the mu buffer
-        (mu is returned as None)."""
+        (mu is returned as None). adaptation_mode: the actor's latent from the adaptation encoder
+        over the observation history (the DAgger iterations' rollout, actor_critic.py:75-76, one
+        lgx_adaptation_forward launch into the latent span) instead of the privileged encoder."""
         a = self.args
         if head is None:
             a.actions = None
@@ -168,8 +170,14 @@ class S8Act:
         ac = alg.actor_critic
         e_mod, e_in = alg.estimator.group_item(obs)
         s_mod, s_in = ac.scan_encoder.group_item(scan)
-        p_mod, p_in = ac.privileged_encoder_.group_item(priv)
-        H.forward_group([(e_mod, e_in, None, self.spans[2]), (s_mod, s_in, None, self.spans[1]),
-                         (p_mod, p_in, None, self.spans[0])])
+        items = [(e_mod, e_in, None, self.spans[2]), (s_mod, s_in, None, self.spans[1])]
+        if not adaptation_mode:
+            p_mod, p_in = ac.privileged_encoder_.group_item(priv)
+            items.append((p_mod, p_in, None, self.spans[0]))
+        H.forward_group(items)
+        if adaptation_mode:
+            P = ac.num_proprio
+            hist = obs[:, :obs.shape[1] - P].reshape(self.B, ac.history_buffer_length, P)
+            H.adaptation_forward_into(ac.adaptation_encoder_, hist, self.spans[0])
         S.act(a)
         return (self.mu if head is None else None), self.value

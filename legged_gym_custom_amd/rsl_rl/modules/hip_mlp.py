@@ -1183,6 +1183,31 @@ def adaptation_forward(mod, hist):
     return _AdaptationFn.apply(hist, dims, want_grad, *ps)
 
 
+def adaptation_forward_into(mod, hist, out):
+    """AdaptationEncoder.forward without gradient in ONE launch (lgx_adaptation_forward), writing
+    into `out` ([B, output_dim] fp32, unit column stride, any row stride: e.g. the latent span of
+    the fused act kernel's encoder-output buffer). hist [B, H, P] with unit column stride and row
+    pitch P (the history inside the obs rows, read in place). Same numbers as adaptation_forward."""
+    Bn, H, P = hist.shape
+    C1, C2, C3, k1, s1, k2, s2, L1, L2 = dims = _conv_dims(mod, H)
+    f_w = mod.fc_final[0].weight
+    if dims[8] * dims[2] != f_w.shape[1]:
+        raise ValueError("adaptation encoder: flatten size does not match fc_final (history 10, Q17)")
+    if (hist.stride(2) != 1 or hist.stride(1) != P or hist.stride(0) < H * P or Bn * hist.stride(0) > 2 ** 31 - 1
+            or 16 * (H * C1 + L1 * C2 + L2 * C3) * 4 > 64 * 1024):
+        raise MlpLibError("adaptation_forward_into: history layout / sizes outside the fused kernel's limits")
+    if out.shape != (Bn, f_w.shape[0]) or out.stride(1) != 1 or out.dtype != torch.float32:
+        raise MlpLibError("adaptation_forward_into: out must be fp32 [B, output_dim] with unit column stride")
+    fc_w, fc_b = mod.fc_encoder[0].weight, mod.fc_encoder[0].bias
+    W1, W2, Wf = _conv_w(mod.conv_layers[0].weight), _conv_w(mod.conv_layers[2].weight), _final_w(f_w, C3, L2)
+    args = AdaptArgs(x=hist.data_ptr(), ldx=hist.stride(0), B=Bn, H=H, P=P, w0=_ptr(fc_w), b0=_ptr(fc_b), C1=C1,
+                     w1=_ptr(W1), b1=_ptr(mod.conv_layers[0].bias), C2=C2, k1=k1, s1=s1, w2=_ptr(W2),
+                     b2=_ptr(mod.conv_layers[2].bias), C3=C3, k2=k2, s2=s2, wf=_ptr(Wf), bf=_ptr(mod.fc_final[0].bias),
+                     NO=f_w.shape[0], out=_ptr(out), ldo=out.stride(0))
+    _check(lib().lgx_adaptation_forward(C.byref(args), _stream()), "lgx_adaptation_forward")
+    return out
+
+
 # ---------------------------------------------------------------------------------------
 # PPO loss head (ppo.py:196-262 over actor_critic.py's Normal(mu, std)): surrogate, clipped
 # value loss, entropy and KL as one forward and one backward kernel (lgx_ppo_head_*).

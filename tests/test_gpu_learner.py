@@ -45,6 +45,26 @@ def test_graph_update_matches_eager(phased):
     assert graph.grads.check()
 
 
+def test_graph_update_dagger_matches_eager():
+    """update_dagger (ppo.py:309-349) replayed from its hipGraph (calls 2..) == eager, bit for
+    bit: the adaptation encoder, its Adam moments and the returned mean loss."""
+    base = _make("adaptive")
+    eager = _to_gpu(base, use_graphs=False)
+    graph = _to_gpu(base, use_graphs=True)
+    for it in range(4):
+        for alg in (eager, graph):
+            _fill(alg, 20 + it)
+        torch.manual_seed(200 + it)
+        le = eager.update_dagger()
+        torch.manual_seed(200 + it)
+        lg = graph.update_dagger()
+        assert lg == le, (it, lg, le)
+    assert graph._dagger_graph is not None
+    for a, b in zip(graph.actor_critic.adaptation_encoder_.parameters(), eager.actor_critic.adaptation_encoder_.parameters()):
+        assert torch.equal(a.detach(), b.detach())
+    assert torch.equal(graph.exp_avg, eager.exp_avg) and torch.equal(graph.exp_avg_sq, eager.exp_avg_sq)
+
+
 def test_gpu_update_tracks_cpu_torch_update():
     """HIP GEMMs (3xbf16) + flat HIP Adam + hipGraph vs the CPU torch update (fp32 GEMMs,
     torch Adam) on the same data and minibatches. Per-element Adam steps are bounded by
