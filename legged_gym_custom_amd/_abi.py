@@ -5,7 +5,7 @@ sizeof against the values the native library (and the oracle) report.
 """
 import ctypes as C
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 MAX_DOF = 12
 MAX_LINKS = 16
 MAX_BODIES = 24

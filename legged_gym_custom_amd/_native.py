@@ -34,6 +34,7 @@ def lib():
     L.lgx_reset_envs.argtypes = [vp, vp, u64, u64, vp]
     L.lgx_episode_extras.argtypes = [vp, vp, vp, vp, vp, vp]
     L.lgx_command_curriculum.argtypes = [vp, u64, u64, vp, vp, vp]
+    L.lgx_set_envs_per_wave.argtypes = [vp, i32]
     L.lgx_last_error.argtypes = [vp]
     L.lgx_last_error.restype = C.c_char_p
     L.lgx_destroy.argtypes = [vp]
@@ -47,7 +48,7 @@ def lib():
 
 EXPORTED = ["lgx_abi_version", "lgx_sizeof_model", "lgx_sizeof_task_params", "lgx_sizeof_buffers", "lgx_create",
             "lgx_bind", "lgx_step", "lgx_step_dev", "lgx_post_physics", "lgx_physics", "lgx_reset_envs", "lgx_last_error",
-            "lgx_destroy", "lgx_episode_extras", "lgx_command_curriculum"]
+            "lgx_destroy", "lgx_episode_extras", "lgx_command_curriculum", "lgx_set_envs_per_wave"]
 
 
 class NativeEnv:
@@ -86,6 +87,10 @@ class NativeEnv:
             setattr(self.buffers, name, t.data_ptr())
             self._keep[name] = t
         self._check(self._L.lgx_bind(self.handle, C.byref(self.buffers)), "lgx_bind")
+
+    def set_envs_per_wave(self, n):
+        """lgx_set_envs_per_wave: 2 (default where it applies), 1, or 0 (default)."""
+        self._check(self._L.lgx_set_envs_per_wave(self.handle, int(n)), "lgx_set_envs_per_wave")
 
     def step(self, seed, step_counter, stream):
         self._check(self._L.lgx_step(self.handle, seed, step_counter, C.c_void_p(stream)), "lgx_step")

@@ -77,9 +77,11 @@ struct DynTemps {
   float Sp[21];                // Σ_j X_j B_jᵀ, packed lower
 };
 static_assert(sizeof(DynTemps) <= ROWS_FLOATS * sizeof(float), "dynamics temporaries fit the arena");
-LGX_DEV DynTemps& dtmp() { return *reinterpret_cast<DynTemps*>(lgx_dyn); }
-LGX_DEV float* stg_U() { return lgx_dyn; }
-LGX_DEV float* stg_cur(const lgx_task_params* Pm) { return lgx_dyn + 4 * rng_blocks(Pm); }
+// Each env owns one arena (A below: lgx_dyn, or lgx_dyn + arena_floats for the second env of a
+// paired wave, see env_step_kernel)
+LGX_DEV DynTemps& dtmp(float* A) { return *reinterpret_cast<DynTemps*>(A); }
+LGX_DEV float* stg_U(float* A) { return A; }
+LGX_DEV float* stg_cur(float* A, const lgx_task_params* Pm) { return A + 4 * rng_blocks(Pm); }
 // The old observation history is staged in LDS when it is short (Go2: 10 x 52 = 520); a long
 // one (ANYmal: 5 x 235 = 1175, 4.7 KB) is shifted in place in HBM instead (post-physics below),
 // which keeps ANYmal's arena at the Go2 size: 9.9 KB of LDS per env, 16 envs per CU.
@@ -87,11 +89,11 @@ constexpr int HIST_LDS_MAX = 640;
 __host__ __device__ inline bool hist_in_lds(const lgx_task_params* Pm) {
   return Pm->history_len * Pm->num_proprio <= HIST_LDS_MAX || Pm->num_proprio < 64;
 }
-LGX_DEV float* stg_hist(const lgx_task_params* Pm) { return stg_cur(Pm) + Pm->num_proprio; }
-LGX_DEV float* stg_heights(const lgx_task_params* Pm) {
-  return stg_hist(Pm) + (hist_in_lds(Pm) ? Pm->history_len * Pm->num_proprio : 0);
+LGX_DEV float* stg_hist(float* A, const lgx_task_params* Pm) { return stg_cur(A, Pm) + Pm->num_proprio; }
+LGX_DEV float* stg_heights(float* A, const lgx_task_params* Pm) {
+  return stg_hist(A, Pm) + (hist_in_lds(Pm) ? Pm->history_len * Pm->num_proprio : 0);
 }
-static inline int64_t arena_floats(const lgx_task_params& p) {
+__host__ __device__ inline int64_t arena_floats(const lgx_task_params& p) {
   const int64_t post = 4 * (9 + (p.num_proprio + 3) / 4) + p.num_proprio +
                        (hist_in_lds(&p) ? (int64_t)p.history_len * p.num_proprio : 0) + p.num_height_points;
   return post > ROWS_FLOATS ? post : ROWS_FLOATS;
@@ -140,7 +142,7 @@ struct Sh {
 // Lane 0 accumulates s_memtime deltas per phase in LDS; the kernel's end writes them to
 // g_phase_out[env][phase]. Compiled out of the product library.
 #ifdef LGX_PHASE_CLOCK
-constexpr int NPH = 20;  // 16 phases + [16] max constraint rows, [17] wide-path substeps
+constexpr int NPH = 20;  // 16 phases + [16] max constraint rows, [17] wide-path substeps, [18] HW_ID, [19] XCC_ID
 __device__ uint32_t* g_phase_out = nullptr;
 #define PH(k)                                              \
   do {                                                     \
@@ -185,6 +187,68 @@ LGX_DEV int opaque_lane(int v) {
   return v;
 }
 
+// ---- lane groups. An env owns WL consecutive lanes of its wave: WL = 64 (one env per wave) or
+// WL = 32 (two envs per wave, lanes 0..31 and 32..63: the phases that use a dozen to thirty
+// lanes of an env then do two envs' work per instruction). The physics and post-physics
+// functions below take `lane` = the lane within the group and the group's own Sh / arena; the
+// helpers here are the cross-lane operations made group-local. (DPP row operations act on
+// 16-lane rows and are group-local as they are.)
+template <int WL>
+LGX_DEV int grp_of_lane() {
+  if constexpr (WL == 64) return 0;
+  else return (int)(__lane_id() >> 5);
+}
+// this group's ballot, bit i = group lane i
+template <int WL>
+LGX_DEV uint64_t gballot(bool p) {
+  const uint64_t m = __ballot(p);
+  if constexpr (WL == 64) return m;
+  else return (__lane_id() >> 5) ? (m >> 32) : (m & 0xffffffffull);
+}
+LGX_DEV float rdl(float v, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); }
+LGX_DEV int rdl(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+// v of group lane r0 (group 0) / r1 (group 1), in every lane of the group (r0, r1 wave-uniform)
+template <int WL>
+LGX_DEV float gbcast(float v, int r0, int r1) {
+  if constexpr (WL == 64) {
+    return rdl(v, r0);
+  } else {
+    const float a = rdl(v, r0), b = rdl(v, 32 + r1);
+    return (__lane_id() >> 5) ? b : a;
+  }
+}
+template <int WL>
+LGX_DEV float gbcast(float v, int r) { return gbcast<WL>(v, r, r); }
+// a * b for a, b < 2^24 as one full-rate v_mul_u32_u24 (the compiler otherwise folds small
+// index products into 64-bit multiply-adds)
+LGX_DEV int mul24(int a, int b) {
+  int r;
+  __asm__("v_mul_u32_u24 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+// a group-uniform int of group 0 / group 1 as wave-uniform scalars
+template <int WL>
+LGX_DEV int gval(int v, int g) {
+  if constexpr (WL == 64) return __builtin_amdgcn_readfirstlane(v);
+  else return rdl(v, 32 * g);
+}
+// the largest of the groups' values of a group-uniform int (a wave-uniform loop bound)
+template <int WL>
+LGX_DEV int gmax(int v) {
+  if constexpr (WL == 64) return __builtin_amdgcn_readfirstlane(v);
+  else return max(rdl(v, 0), rdl(v, 32));
+}
+// sum over group lanes 0..15 (the group's first DPP row), returned to every lane of the group;
+// lanes 0..15 of the group must be active
+template <int WL>
+LGX_DEV float grow_sum16(float x) {
+  x += dpp_shr_t<0x111>(x);
+  x += dpp_shr_t<0x112>(x);
+  x += dpp_shr_t<0x114>(x);
+  x += dpp_shr_t<0x118>(x);
+  return gbcast<WL>(x, 15);
+}
+
 // symmetric 3x3 (xx yy zz xy xz yz) inverse
 LGX_DEV void sym3_inv(const float* D, float* O) {
   float a = D[0], b = D[1], c = D[2], d = D[3], e = D[4], f = D[5];
@@ -217,7 +281,7 @@ LGX_DEV float from_prev_lane(float x) { return dpp_shr_t<0x111>(x); }
 // also form the per-link COM wrench (Fw, Nw) and return the 16 base sums about p0 (mass,
 // first moment, inertia, wrench), reduced across lanes 0..15 by DPP (see dynamics).
 template <bool BIAS>
-LGX_DEV void kinematics(Sh& s, const lgx_model* M, const lgx_task_params* Pm, int lane) {
+LGX_DEV void kinematics(Sh& s, float* A, const lgx_model* M, const lgx_task_params* Pm, int lane) {
   const int j = lane < NJ ? lane : NJ - 1;
   const bool base = lane == NJ;  // the base rides the chain as a fixed joint at the root
   const int a = base ? 0 : j % 3;
@@ -325,8 +389,8 @@ LGX_DEV void kinematics(Sh& s, const lgx_model* M, const lgx_task_params* Pm, in
 #pragma unroll
       for (int q = 0; q < 6; ++q) s.I[k][q] = Iw[q];
       s.m[k] = m;
-      st3(dtmp().Fw[k], F);
-      st3(dtmp().Nw[k], N);
+      st3(dtmp(A).Fw[k], F);
+      st3(dtmp(A).Nw[k], N);
     }
     // the 16 base sums about p0, reduced over lanes 0..15 (row 0) by a DPP scan whose
     // total lands on lane 15
@@ -345,7 +409,7 @@ LGX_DEV void kinematics(Sh& s, const lgx_model* M, const lgx_task_params* Pm, in
       x += dpp_shr_t<0x112>(x);
       x += dpp_shr_t<0x114>(x);
       x += dpp_shr_t<0x118>(x);
-      if (lane == 15) dtmp().tot[q] = x;
+      if (lane == 15) dtmp(A).tot[q] = x;
     }
   }
   __syncthreads();
@@ -359,7 +423,7 @@ LGX_DEV void kinematics(Sh& s, const lgx_model* M, const lgx_task_params* Pm, in
 //   J M⁻¹ Jᵀ = y_rᵀ S⁻¹ y_s + [leg_r = leg_s] J_r,Jᵀ D_l⁻¹ J_s,J  with  y = J_B − X J_J
 // Lanes:
 //   D1 (in kinematics<true>) per-link COM wrench; the 16 base sums about p0 by DPP
-//   D2 lanes 0..11  joint bias h_j and coupling column B_j;  lanes 16..39 leg block D_l
+//   D2 lanes 0..11  joint bias h_j and coupling column B_j;  lanes 8..31 leg block D_l
 //   D3 lanes 0..11  D_l⁻¹ (row a), X_j; the 21 Schur sums by DPP; every lane factors S in
 //                   registers (Cholesky); lanes 0..5 write column `lane` of S⁻¹
 struct DynOut {
@@ -369,9 +433,9 @@ struct DynOut {
   float dinv[3];  // lane j < 12: row a of D_l⁻¹
 };
 
-LGX_DEV void dynamics(Sh& s, int lane, DynOut& o) {
+LGX_DEV void dynamics(Sh& s, float* A, int lane, DynOut& o) {
   const f3 p0 = ld3(s.P[0]);
-  const float* tot = dtmp().tot;
+  const float* tot = dtmp(A).tot;
   const int j = lane < NJ ? lane : NJ - 1, l = j / 3, a = j % 3;
   if (lane < NJ) {  // ---- D2a: joint j (leg l, chain position a)
     const int kj = 1 + j;
@@ -384,7 +448,7 @@ LGX_DEV void dynamics(Sh& s, int lane, DynOut& o) {
       const f3 c = ld3(s.C[k]);
       const f3 d = c - pj;
       const float m = s.m[k];
-      acc = acc + cross(d, ld3(dtmp().Fw[k])) + ld3(dtmp().Nw[k]);
+      acc = acc + cross(d, ld3(dtmp(A).Fw[k])) + ld3(dtmp(A).Nw[k]);
       hl = hl + d * m;
       bang = bang + cross(c - p0, cross(ax, d)) * m + symv(s.I[k], ax);
     }
@@ -392,8 +456,11 @@ LGX_DEV void dynamics(Sh& s, int lane, DynOut& o) {
     const f3 blin = cross(ax, hl);
     float* Bj = s.Bc[j];
     Bj[0] = blin.x; Bj[1] = blin.y; Bj[2] = blin.z; Bj[3] = bang.x; Bj[4] = bang.y; Bj[5] = bang.z;
-  } else if (lane >= 16 && lane < 40) {  // ---- D2b: leg block entry (xx yy zz xy xz yz)
-    const int q = lane - 16, lq = q / 6, e = q % 6;
+  }
+  // (the two branches run one after the other in the wave either way; lanes 8..31 keep both
+  // parts within one 32-lane group)
+  if (lane >= 8 && lane < 32) {  // ---- D2b: leg block entry (xx yy zz xy xz yz)
+    const int q = lane - 8, lq = q / 6, e = q % 6;
     const int j1 = e < 3 ? e : (e == 5 ? 1 : 0);
     const int j2 = e < 3 ? e : (e == 3 ? 1 : 2);
     const int k1 = 1 + 3 * lq + j1, k2 = 1 + 3 * lq + j2;
@@ -406,12 +473,12 @@ LGX_DEV void dynamics(Sh& s, int lane, DynOut& o) {
       const f3 c = ld3(s.C[k]);
       acc += s.m[k] * dot(cross(a1, c - p1), cross(a2, c - p2)) + dot(a1, symv(s.I[k], a2));
     }
-    dtmp().Dl[lq][e] = acc;
+    dtmp(A).Dl[lq][e] = acc;
   }
   __syncthreads();
   // ---- D3
   float Di[6];
-  sym3_inv(dtmp().Dl[l], Di);
+  sym3_inv(dtmp(A).Dl[l], Di);
 #pragma unroll
   for (int c = 0; c < 3; ++c) o.dinv[c] = sym3(Di, a, c);
   if (lane < NJ && a == 0) {
@@ -442,7 +509,7 @@ LGX_DEV void dynamics(Sh& s, int lane, DynOut& o) {
     float acc = 0.f;
 #pragma unroll
     for (int jj = 0; jj < NJ; ++jj) acc += s.X[jj][r] * s.Bc[jj][c];
-    dtmp().Sp[q] = acc;
+    dtmp(A).Sp[q] = acc;
   }
   __syncthreads();
   // S = A_bb − Σ_j X_j B_jᵀ; A_bb = [[M I, −[H]x], [[H]x, Ip]] (base origin velocity, ω),
@@ -452,7 +519,7 @@ LGX_DEV void dynamics(Sh& s, int lane, DynOut& o) {
                         -Hy, Hx, 0.f, tot[8], tot[9], tot[6]};
   float L[21];
 #pragma unroll
-  for (int q = 0; q < 21; ++q) L[q] = Ab[q] - dtmp().Sp[q];
+  for (int q = 0; q < 21; ++q) L[q] = Ab[q] - dtmp(A).Sp[q];
   float inv[6];
 #pragma unroll
   for (int c = 0; c < 6; ++c) {
@@ -567,8 +634,9 @@ constexpr int MESH_BLOCK = 8;  // vertices per block side of the packed block ma
 LGX_DEV float mesh_block_bound(uint32_t w) {  // block max height (raw units), or +inf if absent
   return (w >> 31) ? (float)((int)((w >> 20) & 0x7ffu) * 32 - 32768) : 3.0e38f;
 }
-LGX_DEV TerrainHit terrain_contact_wave(const lgx_task_params* Pm, const lgx_buffers& B, f3 x, float r, bool cand,
-                                        int lane) {
+template <int WL>
+LGX_DEV TerrainHit terrain_contact_wave(const lgx_task_params* Pm, const lgx_buffers& B, float* A, f3 x, float r,
+                                        bool cand, int lane) {
   const float hs = Pm->horizontal_scale, vs = Pm->vertical_scale;
   const int rows = Pm->hf_rows, cols = Pm->hf_cols;
   const uint32_t* mesh = B.terrain_mesh;
@@ -595,34 +663,35 @@ LGX_DEV TerrainHit terrain_contact_wave(const lgx_task_params* Pm, const lgx_buf
       }
     }
   }
-  // inclusive prefix of the task counts over lanes
+  // inclusive prefix of the task counts over the group's lanes
   int endp = cnt;
 #pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const int v = __shfl_up(endp, d, 64);
+  for (int d = 1; d < WL; d <<= 1) {
+    const int v = __shfl_up(endp, d, WL);
     if (lane >= d) endp += v;
   }
-  const int total = __shfl(endp, 63, 64);
-  int* const T_end = reinterpret_cast<int*>(lgx_dyn);
+  const int total = __shfl(endp, WL - 1, WL);
+  const int total_max = gmax<WL>(total);  // the groups' task lists run side by side
+  int* const T_end = reinterpret_cast<int*>(A);
   int* const T_ci = T_end + 64;
   int* const T_cj = T_end + 128;
   int* const T_i0 = T_end + 192;
   int* const T_j0 = T_end + 256;
   int* const T_w = T_end + 320;
-  float* const T_p = lgx_dyn + 384;        // [3][64]
-  float* const R_ = lgx_dyn + 576;         // results [8][64]: d2, q(3), fn(3), zs
+  float* const T_p = A + 384;        // [3][64]
+  float* const R_ = A + 576;         // results [8][64]: d2, q(3), fn(3), zs
   T_end[lane] = endp; T_ci[lane] = ci; T_cj[lane] = cj; T_i0[lane] = i0; T_j0[lane] = j0; T_w[lane] = w;
   T_p[lane] = p.x; T_p[64 + lane] = p.y; T_p[128 + lane] = p.z;
   float best = 3.0e38f, zs = -3.0e38f;
   f3 q = mk(0.f, 0.f, -3.0e38f), fn = mk(0.f, 0.f, 1.f);
   const int mystart = endp - cnt;
-  for (int base = 0; base < total; base += 64) {
+  for (int base = 0; base < total_max; base += WL) {
     __syncthreads();  // the tables (first round) / the previous round's results are read
     const int t = base + lane;
     float td2 = 3.0e38f, tz = -3.0e38f;
     f3 tq = mk(0.f, 0.f, -3.0e38f), tfn = mk(0.f, 0.f, 1.f);
     if (t < total) {
-      int lo = 0, hi = 63;  // owner: the first lane whose inclusive end exceeds t
+      int lo = 0, hi = WL - 1;  // owner: the first lane whose inclusive end exceeds t
       while (lo < hi) {
         const int mid = (lo + hi) >> 1;
         if (T_end[mid] > t) hi = mid; else lo = mid + 1;
@@ -654,7 +723,7 @@ LGX_DEV TerrainHit terrain_contact_wave(const lgx_task_params* Pm, const lgx_buf
     R_[448 + lane] = tz;
     __syncthreads();
     if (cnt > 0) {  // this candidate's tasks of the round, in order
-      const int a0 = max(mystart, base) - base, a1 = min(endp, base + 64) - base;
+      const int a0 = max(mystart, base) - base, a1 = min(endp, base + WL) - base;
       for (int sl = a0; sl < a1; ++sl) {
         const float d2 = R_[sl];
         if (d2 < best) {
@@ -777,7 +846,7 @@ LGX_DEV void sea_unit_k(const float* __restrict__ w_ih, const float* __restrict_
 // with 33-38 spilled VGPRs: not kept, profiles/r03_sea_spill_fix.txt.)
 // inlined (54 VGPRs spill at the 4-waves-per-SIMD budget, yet C3's kernel is 589 us against 611
 // as a call and 642 one joint per lane: profiles/r03_bench_anymal_c_rough_sea_waves.txt)
-LGX_DEV void sea_torques_lanes(Sh& s, const lgx_task_params* Pm_, const lgx_buffers& B, int e, int lane) {
+LGX_DEV void sea_torques_lanes(Sh& s, float* A, const lgx_task_params* Pm_, const lgx_buffers& B, int e, int lane) {
   const size_t NT = (size_t)Pm_->num_envs * Pm_->num_dof;
   const int u = lane & 7;
   // The net's 972 floats (sea_in_scale .. sea_lin_w, contiguous in lgx_task_params) are copied
@@ -786,7 +855,7 @@ LGX_DEV void sea_torques_lanes(Sh& s, const lgx_task_params* Pm_, const lgx_buff
   // LDS reads instead of vector-memory loads (8 distinct addresses per wave instruction).
   {
     const float* src = &Pm_->sea_in_scale[0];
-    for (int i = lane; i < SEA_WN; i += 64) lgx_dyn[i] = src[i];
+    for (int i = lane; i < SEA_WN; i += 64) A[i] = src[i];
     __syncthreads();
   }
 #pragma unroll 1
@@ -796,7 +865,7 @@ LGX_DEV void sea_torques_lanes(Sh& s, const lgx_task_params* Pm_, const lgx_buff
     const lgx_task_params* Pm = opaque(Pm_);
     int wb = 0;  // opaque per pass, as Pm
     __asm__ volatile("" : "+s"(wb));
-    const SeaW W{lgx_dyn + wb};
+    const SeaW W{A + wb};
     const int j = pass * 8 + (lane >> 3);
     const bool on = j < NJ;  // pass 1: lanes 0..31 (joints 8..11); lanes 32..63 follow along
     const int jj = on ? j : NJ - 1;
@@ -829,189 +898,17 @@ LGX_DEV void sea_torques_lanes(Sh& s, const lgx_task_params* Pm_, const lgx_buff
   }
 }
 
-// one physics substep (legged_robot.py:80-85 loop body)
-template <bool TERRAIN, bool ACTNET>
-LGX_DEV void substep(Sh& s, const lgx_model* M_, const lgx_task_params* Pm_, const lgx_buffers& B, int lane_,
-                     bool last) {
-  // The model and task tables are re-read each substep (L1 / scalar-cache hits) rather than
-  // hoisted out of the decimation loop, where ~40 lane-indexed constants would otherwise stay
-  // live in VGPRs across the whole step. Likewise the lane index, so that per-lane index and
-  // LDS-address arithmetic is recomputed each substep instead of being hoisted and spilled.
-  const lgx_model* M = opaque(M_);
-  const lgx_task_params* Pm = opaque(Pm_);
-  const int lane = opaque_lane(lane_);
-  const float dt = Pm->sim_dt;
-  // ---- PD torques: LeggedRobot._compute_torques legged_robot.py:440-478
-  {
-#pragma clang fp contract(off)
-    if (ACTNET) {
-      sea_torques_lanes(s, Pm, B, env_of_block(blockIdx.x, gridDim.x), lane);
-    } else if (lane < NJ) {
-      const int j = lane;
-      float as = s.act[j] * Pm->action_scale;
-      float t;
-      if (Pm->control_type == LGX_CONTROL_P) {
-        float err = (as + Pm->default_dof_pos[j]) - s.th[j];
-        if (Pm->randomize_kp_kd)
-          t = (s.kpm[j] * Pm->p_gains[j]) * err - (s.kdm[j] * Pm->d_gains[j]) * s.thd[j];
-        else
-          t = Pm->p_gains[j] * err - Pm->d_gains[j] * s.thd[j];
-      } else if (Pm->control_type == LGX_CONTROL_V) {
-        t = Pm->p_gains[j] * (as - s.thd[j]) - Pm->d_gains[j] * ((s.thd[j] - s.ldv[j]) / Pm->sim_dt);
-      } else {
-        t = as;
-      }
-      s.tau[j] = fminf(fmaxf(t, -Pm->torque_limits[j]), Pm->torque_limits[j]);
-    }
-  }
-  PH(1);
-  kinematics<true>(s, M, Pm, lane);
-  PH(2);
-  DynOut dy;
-  dynamics(s, lane, dy);
-  const int jl_ = lane < NJ ? lane : NJ - 1, leg_ = jl_ / 3, pos_ = jl_ % 3;  // joint lanes' leg / chain position
-  // ---- free velocity u* = u + dt M⁻¹ f, f = [−h_B ; τ − h_J] (factored form, see dynamics)
-  const float fj = lane < NJ ? s.tau[lane] - dy.hj : 0.f;
-  if (lane < NJ) s.up[lane] = fj;  // scratch: f_J, read by the leg's lanes below
-  float vb[6];
-#pragma unroll
-  for (int r = 0; r < 6; ++r) vb[r] = -dy.hb[r] - row0_sum16(dy.xj[r] * fj);
-  __syncthreads();  // S⁻¹ (dynamics) and f_J visible
-  PH(3);
-  {
-    float zb[6];
-#pragma unroll
-    for (int r = 0; r < 6; ++r) {
-      const float* Si = s.Sinv[r];
-      zb[r] = Si[0] * vb[0] + Si[1] * vb[1] + Si[2] * vb[2] + Si[3] * vb[3] + Si[4] * vb[4] + Si[5] * vb[5];
-    }
-    if (lane < 6) {
-      const float* Si = s.Sinv[lane];
-      const float zl = Si[0] * vb[0] + Si[1] * vb[1] + Si[2] * vb[2] + Si[3] * vb[3] + Si[4] * vb[4] + Si[5] * vb[5];
-      const float u0 = lane < 3 ? s.vo[lane] : s.wb[lane - 3];
-      s.us[lane] = u0 + dt * zl;
-    }
-    if (lane < NJ) {
-      const float* fl = s.up + 3 * leg_;
-      float bot = dy.dinv[0] * fl[0] + dy.dinv[1] * fl[1] + dy.dinv[2] * fl[2];
-#pragma unroll
-      for (int r = 0; r < 6; ++r) bot -= dy.xj[r] * zb[r];
-      s.us[6 + lane] = s.thd[lane] + dt * bot;
-    }
-  }
-  PH(4);
-  // ---- constraint detection: joint limits (lanes 0..11), contacts (one candidate per lane)
-  bool lim_lo = false, lim_hi = false;
-  if (lane < NJ && M->joint_has_limits[lane + 1]) {
-    lim_lo = s.th[lane] < M->joint_lower[lane + 1] + Pm->limit_margin;
-    lim_hi = !lim_lo && s.th[lane] > M->joint_upper[lane + 1] - Pm->limit_margin;
-  }
-  uint64_t lmask = __ballot(lim_lo || lim_hi);
-  int nlim = __popcll(lmask);
-  bool act = false;
-  f3 xc = mk(0, 0, 0), nrm = mk(0.f, 0.f, 1.f);
-  float depth = 0.f;
-  int ck = 0;
-  constexpr bool plane = !TERRAIN;  // the launch picks the variant from mesh_type
-  if constexpr (plane) {
-    if (lane < M->num_candidates) {
-      ck = M->cand_link[lane];
-      xc = ld3(s.P[ck]) + mv(s.R[ck], ld3(M->cand_pos[lane]));
-      const float r = M->cand_radius[lane];
-      depth = r - xc.z;
-      xc.z -= r;
-      act = depth > -Pm->contact_margin;
-    }
-  } else {
-    const bool cand = lane < M->num_candidates;
-    float r = 0.f;
-    if (cand) {
-      ck = M->cand_link[lane];
-      xc = ld3(s.P[ck]) + mv(s.R[ck], ld3(M->cand_pos[lane]));
-      r = M->cand_radius[lane];
-    }
-    const TerrainHit th = terrain_contact_wave(Pm, B, xc, r, cand, lane);
-    if (cand) {
-      depth = th.depth;
-      nrm = th.n;
-      xc = xc - nrm * r;  // deepest sphere point
-      act = depth > -Pm->contact_margin;
-    }
-  }
-  uint64_t cmask = __ballot(act);
-  uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  int crank = __popcll(cmask & below);
-  int ncon = min(__popcll(cmask), MAXC);
-  const int nrows = nlim + 3 * ncon;
-#if LGX_ROW_PRIO > 0
-  // Issue priority by constraint-system size (s_setprio 0..3 above 0 / t / 2t / 3t rows): a
-  // launch lasts as long as its slowest wave, and the waves with the largest systems are the
-  // slow ones; the SIMD's other waves have the slack (profiles/r03_wave_priority.txt).
-  if (nrows > LGX_ROW_PRIO * 3) __builtin_amdgcn_s_setprio(3);
-  else if (nrows > LGX_ROW_PRIO * 2) __builtin_amdgcn_s_setprio(2);
-  else if (nrows > LGX_ROW_PRIO) __builtin_amdgcn_s_setprio(1);
-  else __builtin_amdgcn_s_setprio(0);
-#endif
-  auto target = [&](float d) {
-    float tv;
-    if (d > Pm->slop) tv = fminf(Pm->baumgarte * (d - Pm->slop) / dt, Pm->max_depenetration_vel);
-    else if (d >= 0.f) tv = 0.f;
-    else tv = d / dt;
-    return tv;
-  };
-  float* const ZG = lgx_dyn;                // [nrows][RW]: z_r (6) | g_r (3)
-  float* const J9 = lgx_dyn + MAXR * RW;    // [nrows][RW]: J_B (6) | J of leg rleg (3)
-  float* const Am = J9;                     // A [nrows][nrows] (A path, after J9 is consumed)
-  if (lim_lo || lim_hi) {
-    const int r = __popcll(lmask & below);
-    float* jr = J9 + r * RW;
-#pragma unroll
-    for (int q = 0; q < RW; ++q) jr[q] = 0.f;
-    jr[6 + pos_] = lim_lo ? 1.f : -1.f;
-    const float d = lim_lo ? (M->joint_lower[lane + 1] - s.th[lane]) : (s.th[lane] - M->joint_upper[lane + 1]);
-    s.tgt[r] = target(d);
-    s.rleg[r] = leg_;
-  }
-  if (act && crank < MAXC) {
-    const int r0 = nlim + 3 * crank;
-    const f3 p0 = ld3(s.P[0]);
-    f3 dn = mk(0, 0, 1), dt1 = mk(1, 0, 0), dt2 = mk(0, 1, 0);
-    if constexpr (!plane) {
-      dn = nrm;
-      contact_tangents(nrm, dt1, dt2);
-    }
-    st3(s.cn[crank], dn);
-    const int leg = ck > 0 ? (ck - 1) / 3 : -1;
-    const int pos = ck > 0 ? (ck - 1) % 3 : -1;
-    const int kl = ck > 0 ? 1 + 3 * leg : 1;
-    const f3 ax0 = ld3(s.Ax[kl]), ax1 = ld3(s.Ax[kl + 1]), ax2 = ld3(s.Ax[kl + 2]);
-    const f3 r0p = xc - ld3(s.P[kl]), r1p = xc - ld3(s.P[kl + 1]), r2p = xc - ld3(s.P[kl + 2]);
-    const f3 rb = xc - p0;
-#pragma unroll
-    for (int t = 0; t < 3; ++t) {
-      const int r = r0 + t;
-      const f3 d = t == 0 ? dn : (t == 1 ? dt1 : dt2);
-      const f3 ang = cross(rb, d);
-      float* jr = J9 + r * RW;
-      jr[0] = d.x; jr[1] = d.y; jr[2] = d.z;
-      jr[3] = ang.x; jr[4] = ang.y; jr[5] = ang.z;
-      jr[6] = pos >= 0 ? dot(ax0, cross(r0p, d)) : 0.f;
-      jr[7] = pos >= 1 ? dot(ax1, cross(r1p, d)) : 0.f;
-      jr[8] = pos >= 2 ? dot(ax2, cross(r2p, d)) : 0.f;
-      s.rleg[r] = leg;
-      s.tgt[r] = t == 0 ? target(depth) : 0.f;
-    }
-    s.cbody[crank] = M->cand_body[lane];
-  }
-  if (lane == 0) { s.nrows = nrows; s.nlim = nlim; s.ncon = ncon; }
-#ifdef LGX_PHASE_CLOCK
-  if (lane == 0) {
-    s.phacc[16] = max(s.phacc[16], (uint32_t)nrows);
-    s.phacc[17] += nrows > AMAX ? 1u : 0u;
-  }
-#endif
-  __syncthreads();
-  PH(5);
+// ---- the constraint solve of one substep for one env (oracle_physics.c steps 3-4): per row
+//      (one lane each) the Schur solves, A = J M⁻¹ Jᵀ, projected Gauss-Seidel -> s.lam; z_r, g_r
+//      stay in the arena (ZG) for the velocity update. Input: the rows the detection wrote (J9,
+//      s.rleg, s.tgt, s.nrows / nlim / ncon). WL = the env's lanes: 64, or 32 with both envs of
+//      the wave at <= 32 rows (the groups' loops then run side by side to the larger count, each
+//      group predicated on its own; the broadcasts read each group's own row lane).
+template <int WL>
+LGX_DEV void solve_rows(Sh& s, float* A, const lgx_task_params* Pm, int lane, int nrows, int nlim, int ncon) {
+  float* const ZG = A;                // [nrows][RW]: z_r (6) | g_r (3)
+  float* const J9 = A + MAXR * RW;    // [nrows][RW]: J_B (6) | J of leg rleg (3)
+  float* const Am = J9;               // A [nrows][nrows] (A path, after J9 is consumed)
   // ---- per row (one lane each): y = J_B − X_l J_l, z = S⁻¹ y, g = D_l⁻¹ J_l,
   //      A_rr = y·z + J_l·g, w_r = J_r u*
   const bool row_lane = lane < nrows;
@@ -1061,16 +958,21 @@ LGX_DEV void substep(Sh& s, const lgx_model* M_, const lgx_task_params* Pm_, con
   //      up to AMAX the lower triangle q >= r packed at q (q + 1) / 2 + r; beyond (a fallen
   //      robot: up to 12 + 3 * MAXC rows) the PGS forms A[r][lane] from z_r, g_r (LDS) and the
   //      lane's own y, J_l (registers) each time it needs it — the same numbers, nothing stored.
+  //      Two envs per wave (both <= 32 rows): each group its own form, read through a
+  //      branch-free per-lane index (arow_mix below).
+  const int NRm = gmax<WL>(nrows);
   const bool tri = nrows > ASQ, stored = nrows <= AMAX;
   if (stored && row_lane) {
 #pragma unroll 4
-    for (int q = 0; q < nrows; ++q) {
-      const float* zg = ZG + q * RW;
-      const float v = yr[0] * zg[0] + yr[1] * zg[1] + yr[2] * zg[2] + yr[3] * zg[3] + yr[4] * zg[4] + yr[5] * zg[5];
-      const float vl = jlr[0] * zg[6] + jlr[1] * zg[7] + jlr[2] * zg[8];
-      const float a = v + (s.rleg[q] == lr ? vl : 0.f);
-      if (!tri) Am[q * nrows + lane] = a;
-      else if (q >= lane) Am[q * (q + 1) / 2 + lane] = a;
+    for (int q = 0; q < NRm; ++q) {
+      if (q < nrows) {
+        const float* zg = ZG + q * RW;
+        const float v = yr[0] * zg[0] + yr[1] * zg[1] + yr[2] * zg[2] + yr[3] * zg[3] + yr[4] * zg[4] + yr[5] * zg[5];
+        const float vl = jlr[0] * zg[6] + jlr[1] * zg[7] + jlr[2] * zg[8];
+        const float a = v + (s.rleg[q] == lr ? vl : 0.f);
+        if (!tri) Am[q * nrows + lane] = a;
+        else if (q >= lane) Am[q * (q + 1) / 2 + lane] = a;
+      }
     }
   }
   __syncthreads();
@@ -1085,7 +987,6 @@ LGX_DEV void substep(Sh& s, const lgx_model* M_, const lgx_task_params* Pm_, con
   {
     float w = w0, lam = 0.f;
     const float mu = s.mu;
-    auto rd = [](float v, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); };
     auto wave_shl1 = [](float v) {  // lane x receives lane x + 1 (wave-wide shift)
       return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xf, 0xf, false));
     };
@@ -1094,47 +995,69 @@ LGX_DEV void substep(Sh& s, const lgx_model* M_, const lgx_task_params* Pm_, con
     };
     const float tg = row_lane ? s.tgt[lane] : 0.f;
     const float ia = row_lane ? 1.0f / s.Arr[lane] : 0.f;
-    const int rlast = nrows - 3;  // first row of the last contact
-    const int lc = min(lane, nrows - 1);  // lanes past the rows read a valid (unused) entry
+    const int rlast = max(nrows - 3, 0);      // first row of the last contact
+    const int lc = max(min(lane, nrows - 1), 0);  // lanes past the rows read a valid (unused) entry
     // A[r][lane]: square, from the packed triangle (row r up to the diagonal, then column r),
     // or formed on the fly (lanes past the rows have y = J_l = 0 and read 0)
     const int tl = lc * (lc + 1) / 2;
     auto arow_sq = [&](int r) { return Am[r * nrows + lc]; };
     auto arow_tri = [&](int r) { return Am[lc <= r ? r * (r + 1) / 2 + lc : tl + r]; };
+    // either form per lane, without a branch: the triangle index of (max, min) (24-bit products)
+    auto arow_mix = [&](int r) {
+      const int hi = max(r, lc), lo = min(r, lc);
+      const int it = (mul24(hi, hi + 1) >> 1) + lo;
+      const int is = mul24(r, nrows) + lc;
+      return Am[tri ? it : is];
+    };
+    // keep a or take b where m, as a bitwise select (no branch)
+    auto sel = [](bool m, float a, float b) {
+      const int k = -(int)m;
+      return __int_as_float((__float_as_int(b) & k) | (__float_as_int(a) & ~k));
+    };
     auto arow_otf = [&](int r) {
       const float* zg = ZG + r * RW;
       const float v = yr[0] * zg[0] + yr[1] * zg[1] + yr[2] * zg[2] + yr[3] * zg[3] + yr[4] * zg[4] + yr[5] * zg[5];
       const float vl = jlr[0] * zg[6] + jlr[1] * zg[7] + jlr[2] * zg[8];
       return v + (s.rleg[r] == lr ? vl : 0.f);
     };
+    // the groups' row counts as wave-uniform scalars (the loops run to the larger; a group past
+    // its own count changes nothing)
+    const int NLm = gmax<WL>(nlim), NCm = gmax<WL>(ncon);
+    const int nl0 = gval<WL>(nlim, 0), nl1 = WL == 64 ? nl0 : gval<WL>(nlim, 1);
     // the sweeps, instantiated for each form of A (the square one carries no index selects)
     auto sweeps = [&](auto arow) {
       for (int it = 0; it < Pm->solver_iterations; ++it) {
-        for (int r = 0; r < nlim; ++r) {
-          const float a0 = arow(r);
+        for (int r = 0; r < NLm; ++r) {
+          const bool on = WL == 64 || r < nlim;
+          const float a0 = on ? arow(r) : 0.f;
           const float cand = fmaxf(0.f, lam + (tg - w) * ia);
-          const float d = rd(cand - lam, r);
-          lam = lane == r ? cand : lam;
-          w += a0 * d;
+          const float d = gbcast<WL>(cand - lam, min(r, 31), min(r, 31));
+          lam = sel(lane == r && on, lam, cand);
+          w += on ? a0 * d : 0.f;
         }
-        if (ncon == 0) continue;
-        float n0 = arow(nlim), n1 = arow(nlim + 1), n2 = arow(nlim + 2);
-        for (int r = nlim; r < nrows; r += 3) {
-          const float a0 = n0, a1 = n1, a2 = n2;
+        if (NCm == 0) continue;
+        float n0 = arow(min(nlim, rlast)), n1 = arow(min(nlim + 1, rlast + 1)), n2 = arow(min(nlim + 2, rlast + 2));
+        for (int c = 0; c < NCm; ++c) {
+          const bool on = WL == 64 || c < ncon;
+          const int r = nlim + 3 * c;                               // this group's row
+          const int ra = nl0 + 3 * c, rb = nl1 + 3 * c;             // each group's, uniform
+          const int ra_ = WL == 64 ? ra : min(ra, WL - 3), rb_ = WL == 64 ? rb : min(rb, WL - 3);
+          const float a0 = on ? n0 : 0.f, a1 = on ? n1 : 0.f, a2 = on ? n2 : 0.f;
           const int rn = min(r + 3, rlast);
           n0 = arow(rn);
           n1 = arow(rn + 1);
           n2 = arow(rn + 2);
           // normal row
           const float cand = fmaxf(0.f, lam + (tg - w) * ia);
-          const float d = rd(cand - lam, r);
-          lam = lane == r ? cand : lam;
+          const float d = gbcast<WL>(cand - lam, ra_, rb_);
+          lam = sel(lane == r && on, lam, cand);
           w += a0 * d;
           // tangent pair, projected onto the friction disk |λ_t| <= μ λ_n
-          const float lim = mu * rd(lam, r);
+          const float lim = mu * gbcast<WL>(lam, ra_, rb_);
           const float l = lam - w * ia;
           // both shifts with every lane active (a DPP source lane outside EXEC reads 0), then
-          // the select: lane r + 1 takes r + 2's candidate, lane r + 2 takes r + 1's
+          // the select: lane r + 1 takes r + 2's candidate, lane r + 2 takes r + 1's (the pair
+          // never straddles the two groups: r + 2 < WL)
           float from_next = wave_shl1(l), from_prev = wave_shr1(l);
           __asm__ volatile("" : "+v"(from_next), "+v"(from_prev));
           const float other = lane == r + 1 ? from_next : from_prev;
@@ -1142,31 +1065,260 @@ LGX_DEV void substep(Sh& s, const lgx_model* M_, const lgx_task_params* Pm_, con
           const float sc = nn > lim * lim ? lim * __builtin_amdgcn_rsqf(nn) : 1.0f;
           const float lt = l * sc;
           const float dl = lt - lam;
-          const float d1 = rd(dl, r + 1), d2 = rd(dl, r + 2);
-          lam = (lane == r + 1 || lane == r + 2) ? lt : lam;
+          const float d1 = gbcast<WL>(dl, ra_ + 1, rb_ + 1), d2 = gbcast<WL>(dl, ra_ + 2, rb_ + 2);
+          lam = sel((unsigned)(lane - r - 1) < 2u && on, lam, lt);
           w += a1 * d1 + a2 * d2;
         }
       }
     };
-    if (!stored) sweeps(arow_otf);
-    else if (tri) sweeps(arow_tri);
-    else sweeps(arow_sq);
+    if constexpr (WL == 64) {
+      if (!stored) sweeps(arow_otf);
+      else if (tri) sweeps(arow_tri);
+      else sweeps(arow_sq);
+    } else {
+      sweeps(arow_mix);
+    }
     if (row_lane) s.lam[lane] = lam;
   }
   __syncthreads();
   PH(8);
+}
+
+// one physics substep (legged_robot.py:80-85 loop body) of the group's env. WL = the env's lanes
+// (see grp_of_lane); with two envs per wave, S0 / A0 / astride locate both envs' Sh and arenas
+// for the wide constraint solve (an env with more than 32 rows: each env in turn on all 64 lanes).
+template <bool TERRAIN, bool ACTNET, int WL>
+LGX_DEV void substep(Sh& s, float* A, Sh* S0, float* A0, int astride, const lgx_model* M_,
+                     const lgx_task_params* Pm_, const lgx_buffers& B, int lane_, int e, bool last) {
+  // The model and task tables are re-read each substep (L1 / scalar-cache hits) rather than
+  // hoisted out of the decimation loop, where ~40 lane-indexed constants would otherwise stay
+  // live in VGPRs across the whole step. Likewise the lane index, so that per-lane index and
+  // LDS-address arithmetic is recomputed each substep instead of being hoisted and spilled.
+  const lgx_model* M = opaque(M_);
+  const lgx_task_params* Pm = opaque(Pm_);
+  const int lane = opaque_lane(lane_);
+  const float dt = Pm->sim_dt;
+  // ---- PD torques: LeggedRobot._compute_torques legged_robot.py:440-478
+  {
+#pragma clang fp contract(off)
+    if (ACTNET) {
+      sea_torques_lanes(s, A, Pm, B, e, lane);
+    } else if (lane < NJ) {
+      const int j = lane;
+      float as = s.act[j] * Pm->action_scale;
+      float t;
+      if (Pm->control_type == LGX_CONTROL_P) {
+        float err = (as + Pm->default_dof_pos[j]) - s.th[j];
+        if (Pm->randomize_kp_kd)
+          t = (s.kpm[j] * Pm->p_gains[j]) * err - (s.kdm[j] * Pm->d_gains[j]) * s.thd[j];
+        else
+          t = Pm->p_gains[j] * err - Pm->d_gains[j] * s.thd[j];
+      } else if (Pm->control_type == LGX_CONTROL_V) {
+        t = Pm->p_gains[j] * (as - s.thd[j]) - Pm->d_gains[j] * ((s.thd[j] - s.ldv[j]) / Pm->sim_dt);
+      } else {
+        t = as;
+      }
+      s.tau[j] = fminf(fmaxf(t, -Pm->torque_limits[j]), Pm->torque_limits[j]);
+    }
+  }
+  PH(1);
+  kinematics<true>(s, A, M, Pm, lane);
+  PH(2);
+  DynOut dy;
+  dynamics(s, A, lane, dy);
+  const int jl_ = lane < NJ ? lane : NJ - 1, leg_ = jl_ / 3, pos_ = jl_ % 3;  // joint lanes' leg / chain position
+  // ---- free velocity u* = u + dt M⁻¹ f, f = [−h_B ; τ − h_J] (factored form, see dynamics)
+  const float fj = lane < NJ ? s.tau[lane] - dy.hj : 0.f;
+  if (lane < NJ) s.up[lane] = fj;  // scratch: f_J, read by the leg's lanes below
+  float vb[6];
+#pragma unroll
+  for (int r = 0; r < 6; ++r) vb[r] = -dy.hb[r] - grow_sum16<WL>(dy.xj[r] * fj);
+  __syncthreads();  // S⁻¹ (dynamics) and f_J visible
+  PH(3);
+  {
+    float zb[6];
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+      const float* Si = s.Sinv[r];
+      zb[r] = Si[0] * vb[0] + Si[1] * vb[1] + Si[2] * vb[2] + Si[3] * vb[3] + Si[4] * vb[4] + Si[5] * vb[5];
+    }
+    if (lane < 6) {
+      const float* Si = s.Sinv[lane];
+      const float zl = Si[0] * vb[0] + Si[1] * vb[1] + Si[2] * vb[2] + Si[3] * vb[3] + Si[4] * vb[4] + Si[5] * vb[5];
+      const float u0 = lane < 3 ? s.vo[lane] : s.wb[lane - 3];
+      s.us[lane] = u0 + dt * zl;
+    }
+    if (lane < NJ) {
+      const float* fl = s.up + 3 * leg_;
+      float bot = dy.dinv[0] * fl[0] + dy.dinv[1] * fl[1] + dy.dinv[2] * fl[2];
+#pragma unroll
+      for (int r = 0; r < 6; ++r) bot -= dy.xj[r] * zb[r];
+      s.us[6 + lane] = s.thd[lane] + dt * bot;
+    }
+  }
+  PH(4);
+  // ---- constraint detection: joint limits (lanes 0..11), contacts (one candidate per lane, in
+  //      rounds of WL candidates: the rows keep the candidates' order)
+  bool lim_lo = false, lim_hi = false;
+  if (lane < NJ && M->joint_has_limits[lane + 1]) {
+    lim_lo = s.th[lane] < M->joint_lower[lane + 1] + Pm->limit_margin;
+    lim_hi = !lim_lo && s.th[lane] > M->joint_upper[lane + 1] - Pm->limit_margin;
+  }
+  const uint64_t lmask = gballot<WL>(lim_lo || lim_hi);
+  const int nlim = __popcll(lmask);
+  const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  auto target = [&](float d) {
+    float tv;
+    if (d > Pm->slop) tv = fminf(Pm->baumgarte * (d - Pm->slop) / dt, Pm->max_depenetration_vel);
+    else if (d >= 0.f) tv = 0.f;
+    else tv = d / dt;
+    return tv;
+  };
+  float* const J9 = A + MAXR * RW;    // [nrows][RW]: J_B (6) | J of leg rleg (3)
+  constexpr bool plane = !TERRAIN;  // the launch picks the variant from mesh_type
+  // every candidate's contact query first (the trimesh query uses the arena the rows go to),
+  // then the rows: limits, then contacts in candidate order
+  constexpr int CR = (LGX_MAX_CANDIDATES + WL - 1) / WL;
+  bool act[CR];
+  f3 xc[CR], nrm[CR];
+  float depth[CR];
+  int ck[CR];
+#pragma unroll
+  for (int cr = 0; cr < CR; ++cr) {
+    act[cr] = false;
+    xc[cr] = mk(0, 0, 0);
+    nrm[cr] = mk(0.f, 0.f, 1.f);
+    depth[cr] = 0.f;
+    ck[cr] = 0;
+    if (cr * WL >= M->num_candidates) continue;  // uniform
+    const int ci = cr * WL + lane;
+    const bool cand = ci < M->num_candidates;
+    if constexpr (plane) {
+      if (cand) {
+        ck[cr] = M->cand_link[ci];
+        xc[cr] = ld3(s.P[ck[cr]]) + mv(s.R[ck[cr]], ld3(M->cand_pos[ci]));
+        const float r = M->cand_radius[ci];
+        depth[cr] = r - xc[cr].z;
+        xc[cr].z -= r;
+        act[cr] = depth[cr] > -Pm->contact_margin;
+      }
+    } else {
+      float r = 0.f;
+      if (cand) {
+        ck[cr] = M->cand_link[ci];
+        xc[cr] = ld3(s.P[ck[cr]]) + mv(s.R[ck[cr]], ld3(M->cand_pos[ci]));
+        r = M->cand_radius[ci];
+      }
+      const TerrainHit th = terrain_contact_wave<WL>(Pm, B, A, xc[cr], r, cand, lane);
+      if (cand) {
+        depth[cr] = th.depth;
+        nrm[cr] = th.n;
+        xc[cr] = xc[cr] - nrm[cr] * r;  // deepest sphere point
+        act[cr] = depth[cr] > -Pm->contact_margin;
+      }
+    }
+  }
+  if (lim_lo || lim_hi) {
+    const int r = __popcll(lmask & below);
+    float* jr = J9 + r * RW;
+#pragma unroll
+    for (int q = 0; q < RW; ++q) jr[q] = 0.f;
+    jr[6 + pos_] = lim_lo ? 1.f : -1.f;
+    const float d = lim_lo ? (M->joint_lower[lane + 1] - s.th[lane]) : (s.th[lane] - M->joint_upper[lane + 1]);
+    s.tgt[r] = target(d);
+    s.rleg[r] = leg_;
+  }
+  int nfound = 0;  // contacts of the earlier rounds (group-uniform)
+#pragma unroll
+  for (int cr = 0; cr < CR; ++cr) {
+    if (cr * WL >= M->num_candidates) continue;  // uniform
+    const int ci = cr * WL + lane;
+    const uint64_t cmask = gballot<WL>(act[cr]);
+    const int crank = nfound + __popcll(cmask & below);
+    nfound += __popcll(cmask);
+    if (act[cr] && crank < MAXC) {
+      const int r0 = nlim + 3 * crank;
+      const f3 p0 = ld3(s.P[0]);
+      f3 dn = mk(0, 0, 1), dt1 = mk(1, 0, 0), dt2 = mk(0, 1, 0);
+      if constexpr (!plane) {
+        dn = nrm[cr];
+        contact_tangents(nrm[cr], dt1, dt2);
+      }
+      st3(s.cn[crank], dn);
+      const int leg = ck[cr] > 0 ? (ck[cr] - 1) / 3 : -1;
+      const int pos = ck[cr] > 0 ? (ck[cr] - 1) % 3 : -1;
+      const int kl = ck[cr] > 0 ? 1 + 3 * leg : 1;
+      const f3 ax0 = ld3(s.Ax[kl]), ax1 = ld3(s.Ax[kl + 1]), ax2 = ld3(s.Ax[kl + 2]);
+      const f3 r0p = xc[cr] - ld3(s.P[kl]), r1p = xc[cr] - ld3(s.P[kl + 1]), r2p = xc[cr] - ld3(s.P[kl + 2]);
+      const f3 rb = xc[cr] - p0;
+#pragma unroll
+      for (int t = 0; t < 3; ++t) {
+        const int r = r0 + t;
+        const f3 d = t == 0 ? dn : (t == 1 ? dt1 : dt2);
+        const f3 ang = cross(rb, d);
+        float* jr = J9 + r * RW;
+        jr[0] = d.x; jr[1] = d.y; jr[2] = d.z;
+        jr[3] = ang.x; jr[4] = ang.y; jr[5] = ang.z;
+        jr[6] = pos >= 0 ? dot(ax0, cross(r0p, d)) : 0.f;
+        jr[7] = pos >= 1 ? dot(ax1, cross(r1p, d)) : 0.f;
+        jr[8] = pos >= 2 ? dot(ax2, cross(r2p, d)) : 0.f;
+        s.rleg[r] = leg;
+        s.tgt[r] = t == 0 ? target(depth[cr]) : 0.f;
+      }
+      s.cbody[crank] = M->cand_body[ci];
+    }
+  }
+  const int ncon = min(nfound, MAXC);
+  const int nrows = nlim + 3 * ncon;
+  const int nrw = gmax<WL>(nrows);  // the wave's largest system
+#if LGX_ROW_PRIO > 0
+  // Issue priority by constraint-system size (s_setprio 0..3 above 0 / t / 2t / 3t rows): a
+  // launch lasts as long as its slowest wave, and the waves with the largest systems are the
+  // slow ones; the SIMD's other waves have the slack (profiles/r03_wave_priority.txt).
+  if (nrw > LGX_ROW_PRIO * 3) __builtin_amdgcn_s_setprio(3);
+  else if (nrw > LGX_ROW_PRIO * 2) __builtin_amdgcn_s_setprio(2);
+  else if (nrw > LGX_ROW_PRIO) __builtin_amdgcn_s_setprio(1);
+  else __builtin_amdgcn_s_setprio(0);
+#endif
+  if (lane == 0) { s.nrows = nrows; s.nlim = nlim; s.ncon = ncon; }
+#ifdef LGX_PHASE_CLOCK
+  if (lane == 0) {
+    s.phacc[16] = max(s.phacc[16], (uint32_t)nrows);
+    s.phacc[17] += nrows > AMAX ? 1u : 0u;
+  }
+#endif
+  __syncthreads();
+  PH(5);
+  if constexpr (WL == 64) {
+    solve_rows<64>(s, A, Pm, lane, nrows, nlim, ncon);
+  } else if (nrw <= WL) {
+    solve_rows<WL>(s, A, Pm, lane, nrows, nlim, ncon);
+  } else {
+    // an env of this wave has more rows than its group has lanes (a fallen robot): each env's
+    // solve in turn on the whole wave (its rows from LDS; the same numbers)
+    const int wl = (int)__lane_id();
+#pragma unroll 1
+    for (int g = 0; g < 64 / WL; ++g) {
+      Sh& sg = S0[g];
+      const int nr = gval<WL>(nrows, g), nli = gval<WL>(nlim, g), nco = gval<WL>(ncon, g);
+      solve_rows<64>(sg, A0 + (size_t)g * astride, Pm, wl, nr, nli, nco);
+    }
+  }
   // ---- u+ = u* + M⁻¹ Jᵀ λ = u* + [Z ; G_J − Xᵀ Z]:  Z = Σ_r λ_r z_r,
   //      G_j = Σ_{r on leg(j)} λ_r g_r[pos(j)]
   {
+    const float* const ZG = A;
     float Z[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, G = 0.f;
 #pragma unroll 4
-    for (int r = 0; r < nrows; ++r) {
-      const float lr_ = s.lam[r];
-      const float* zg = ZG + r * RW;
+    for (int r = 0; r < nrw; ++r) {
+      if (WL == 64 || r < nrows) {
+        const float lr_ = s.lam[r];
+        const float* zg = ZG + r * RW;
 #pragma unroll
-      for (int q = 0; q < 6; ++q) Z[q] += lr_ * zg[q];
-      const float gq = pos_ == 0 ? zg[6] : (pos_ == 1 ? zg[7] : zg[8]);
-      G += s.rleg[r] == leg_ ? lr_ * gq : 0.f;
+        for (int q = 0; q < 6; ++q) Z[q] += lr_ * zg[q];
+        const float gq = pos_ == 0 ? zg[6] : (pos_ == 1 ? zg[7] : zg[8]);
+        G += s.rleg[r] == leg_ ? lr_ * gq : 0.f;
+      }
     }
     if (lane < 6) {
       float zl = 0.f;
@@ -1187,8 +1339,9 @@ LGX_DEV void substep(Sh& s, const lgx_model* M_, const lgx_task_params* Pm_, con
   // ---- contact forces of the last substep, per reported body (world frame)
   if (last && lane < LGX_MAX_BODIES) {
     float f[3] = {0.f, 0.f, 0.f};
-    for (int c = 0; c < ncon; ++c) {
-      if (s.cbody[c] != lane) continue;
+    const int ncm = gmax<WL>(ncon);
+    for (int c = 0; c < ncm; ++c) {
+      if (c >= ncon || s.cbody[c] != lane) continue;
       const int r = nlim + 3 * c;
       if constexpr (!TERRAIN) {
         f[2] += s.lam[r]; f[0] += s.lam[r + 1]; f[1] += s.lam[r + 2];
@@ -1327,10 +1480,11 @@ LGX_DEV void resample_commands(const lgx_task_params* Pm, const double* R, float
 // reset_idx for one env (go2.py:207-263 / legged_robot.py:157-213). The env's root/dof/
 // command state is in LDS (s.root, s.th, s.thd, s.cmd, s.ep): lane 0 does the scalar part,
 // lanes write the per-env buffer rows. Called under a uniform branch.
-LGX_DEV void reset_env(const lgx_task_params* Pm, const lgx_buffers& B, Sh& s, int e, int lane, bool after_init,
-                       bool zero_carried, bool sums_in_lds) {
+template <int WL>
+LGX_DEV void reset_env(const lgx_task_params* Pm, const lgx_buffers& B, Sh& s, float* A, int e, int lane,
+                       bool after_init, bool zero_carried, bool sums_in_lds) {
   const int D = Pm->num_dof;
-  const float* U = stg_U();
+  const float* U = stg_U(A);
   if (lane == 0) {
     float* root = s.root;
     float* cmd = s.cmd;
@@ -1377,7 +1531,7 @@ LGX_DEV void reset_env(const lgx_task_params* Pm, const lgx_buffers& B, Sh& s, i
     if (lane < D) { B.last_dof_vel[(size_t)e * D + lane] = 0.f; B.last_torques[(size_t)e * D + lane] = 0.f; }
     if (lane < 6) B.last_root_vel[e * 6 + lane] = 0.f;
     if (lane < 3) B.last_base_lin_vel[e * 3 + lane] = 0.f;
-    for (int i = lane; i < H; i += 64) B.obs_history[(size_t)e * H + i] = 0.f;
+    for (int i = lane; i < H; i += WL) B.obs_history[(size_t)e * H + i] = 0.f;
   }
   if (Pm->actuator_net && lane < 2 * D) {  // Anymal.reset_idx anymal.py:56-60: zero h, c
     const size_t NT = (size_t)Pm->num_envs * D;
@@ -1392,24 +1546,25 @@ LGX_DEV void reset_env(const lgx_task_params* Pm, const lgx_buffers& B, Sh& s, i
     B.last_contact_heights[e * Pm->num_feet + lane] = 0.f;
   }
   const int K = Pm->num_reward_terms + (Pm->has_termination_reward ? 1 : 0);
-  if (lane < K) {
-    float* es = B.episode_sums + (size_t)e * K + lane;
-    const float sum = sums_in_lds ? s.es[lane] : *es;  // in a step: this step's updated row, staged in LDS
-    if (B.episode_stats) atomicAdd(B.episode_stats + lane, sum);
+  for (int k = lane; k < K; k += WL) {
+    float* es = B.episode_sums + (size_t)e * K + k;
+    const float sum = sums_in_lds ? s.es[k] : *es;  // in a step: this step's updated row, staged in LDS
+    if (B.episode_stats) atomicAdd(B.episode_stats + k, sum);
     // the command curriculum's input (go2.py:87): this env's tracking_lin_vel sum at its reset
-    if (sums_in_lds && B.curriculum_vals && lane == Pm->curriculum_term) B.curriculum_vals[e] = sum;
+    if (sums_in_lds && B.curriculum_vals && k == Pm->curriculum_term) B.curriculum_vals[e] = sum;
     *es = 0.f;
   }
   if (lane == 0 && B.episode_stats) atomicAdd(B.episode_stats + K, 1.0f);
   __syncthreads();
 }
 
-LGX_DEV void fill_uniforms(Sh& s, uint64_t seed, uint32_t gid, uint64_t step, uint32_t stream, int lane, int nblk) {
-  for (int b = lane; b < nblk; b += 64) {
+template <int WL>
+LGX_DEV void fill_uniforms(float* A, uint64_t seed, uint32_t gid, uint64_t step, uint32_t stream, int lane, int nblk) {
+  for (int b = lane; b < nblk; b += WL) {
     uint32_t o[4];
     philox4x32_10(gid, (uint32_t)step, (uint32_t)b | (stream << 16), (uint32_t)(step >> 32), (uint32_t)seed,
                   (uint32_t)(seed >> 32), o);
-    float* U = stg_U();
+    float* U = stg_U(A);
     U[4 * b + 0] = u01(o[0]); U[4 * b + 1] = u01(o[1]);
     U[4 * b + 2] = u01(o[2]); U[4 * b + 3] = u01(o[3]);
   }
@@ -1422,12 +1577,11 @@ LGX_DEV void fill_uniforms(Sh& s, uint64_t seed, uint32_t gid, uint64_t step, ui
 // dim by ~1 ulp of the sum (golden tests: 1e-5).
 enum JSum { J_ACTION_RATE, J_DELTA_TORQUES, J_DOF_ACC, J_DOF_ERROR, J_DOF_POS_LIMITS, J_DOF_VEL, J_DOF_VEL_LIMITS,
             J_STAND_ABS, J_TORQUE_LIMITS, J_TORQUES, J_HIP_POS, J_THIGH_POS, J_CALF_POS, J_HEIGHT, J_N };
-LGX_DEV void joint_sums(const lgx_task_params* Pm, const lgx_buffers& B, Sh& s, int e, int lane) {
-  const int D = Pm->num_dof, A = Pm->num_actions;
+LGX_DEV void joint_sums(const lgx_task_params* Pm, const lgx_buffers& B, Sh& s, float* A, int e, int lane) {
+  const int D = Pm->num_dof;
   const int j = lane < D ? lane : 0;
   const float on = lane < D ? 1.0f : 0.0f;
   const float la = s.la_prev[j], lt = s.lt_prev[j];  // prefetched at kernel start
-  (void)A;
   const float q = s.th[j], qd = s.thd[j], tau = s.tau[j], q0 = Pm->default_dof_pos[j];
   const float dq = q - q0;
   float v[J_N];
@@ -1461,7 +1615,7 @@ LGX_DEV void joint_sums(const lgx_task_params* Pm, const lgx_buffers& B, Sh& s, 
   // height points: lane i < 16 sums points i, i + 16, ...
   float hsum = 0.f;
   if (lane < 16) {
-    const float* hts = stg_heights(Pm);
+    const float* hts = stg_heights(A, Pm);
     for (int i = lane; i < Pm->num_height_points; i += 16) hsum += s.root[2] - hts[i];
   }
 #pragma unroll
@@ -1616,18 +1770,19 @@ LGX_DEV float reward_term(const lgx_task_params* Pm, const lgx_buffers& B, Sh& s
   }
 }
 
-LGX_DEV void get_heights(const lgx_task_params* Pm, const lgx_buffers& B, Sh& s, int lane) {
+template <int WL>
+LGX_DEV void get_heights(const lgx_task_params* Pm, const lgx_buffers& B, Sh& s, float* A, int lane) {
   const int NP = Pm->num_height_points;
   const float* root = s.root;
   if (Pm->mesh_type == LGX_MESH_PLANE || B.height_samples == nullptr) {
-    for (int i = lane; i < NP; i += 64) stg_heights(Pm)[i] = 0.0f;
+    for (int i = lane; i < NP; i += WL) stg_heights(A, Pm)[i] = 0.0f;
     return;
   }
   float qz = root[5], qw = root[6];
   float n = sqrtf(qz * qz + qw * qw);
   n = n < 1e-9f ? 1e-9f : n;
   float qy[4] = {0.f, 0.f, qz / n, qw / n};
-  for (int i = lane; i < NP; i += 64) {
+  for (int i = lane; i < NP; i += WL) {
     float p[3] = {Pm->height_points[i][0], Pm->height_points[i][1], 0.f}, w[3];
     quat_apply(qy, p, w);
     float px = (w[0] + root[0]) + Pm->border_size, py = (w[1] + root[1]) + Pm->border_size;
@@ -1639,7 +1794,7 @@ LGX_DEV void get_heights(const lgx_task_params* Pm, const lgx_buffers& B, Sh& s,
     int16_t h3 = B.height_samples[ix * Pm->hf_cols + iy + 1];
     int16_t h = h1 < h2 ? h1 : h2;
     h = h < h3 ? h : h3;
-    stg_heights(Pm)[i] = (float)h * Pm->vertical_scale;
+    stg_heights(A, Pm)[i] = (float)h * Pm->vertical_scale;
   }
 }
 
@@ -1650,18 +1805,27 @@ LGX_DEV void get_heights(const lgx_task_params* Pm, const lgx_buffers& B, Sh& s,
 #ifndef LGX_SEA_WAVES
 #define LGX_SEA_WAVES 4
 #endif
-template <bool PHYSICS, bool TERRAIN, bool ACTNET>
-__global__ __launch_bounds__(64, ACTNET ? LGX_SEA_WAVES : 4) void env_step_kernel(const lgx_model* __restrict__ M,
+// EPW envs per wave (1, or 2: each env on a 32-lane group, grp_of_lane; blocks = N / 2, envs 2b'
+// and 2b' + 1 of the XCD-aware pair order b' = env_of_block). Each env has its own Sh and LDS arena.
+// Two envs per wave: LDS holds 2 x (Sh + arena) per block, so 8 blocks per CU (2 waves per
+// SIMD) are resident — the register budget is that of 2 waves per SIMD.
+template <bool PHYSICS, bool TERRAIN, bool ACTNET, int EPW>
+__global__ __launch_bounds__(64, ACTNET ? LGX_SEA_WAVES : (EPW == 2 ? 2 : 4)) void env_step_kernel(const lgx_model* __restrict__ M,
                                                       const lgx_task_params* __restrict__ Pm,
                                                       const lgx_buffers* __restrict__ Bp, uint64_t seed,
                                                       uint64_t step_arg, const uint64_t* __restrict__ step_dev) {
-  __shared__ Sh s;
+  constexpr int WL = 64 / EPW;  // lanes per env
+  __shared__ Sh S_[EPW];
+  const int grp = grp_of_lane<WL>();
+  Sh& s = S_[grp];
+  const int astride = (int)arena_floats(*Pm);
+  float* const AR = lgx_dyn + (EPW == 1 ? 0 : grp * astride);  // this env's arena
   // buffer pointers are read from device memory (scalar loads) when used, not held in SGPRs
   const lgx_buffers& B = *Bp;
   // graph-replayable form: the step counter is read from device memory (lgx_step_dev)
   const uint64_t step = step_dev ? *step_dev : step_arg;
-  const int e = env_of_block(blockIdx.x, gridDim.x);
-  const int lane = threadIdx.x;
+  const int e = EPW * env_of_block(blockIdx.x, gridDim.x) + grp;
+  const int lane = EPW == 1 ? (int)threadIdx.x : (int)(threadIdx.x & (WL - 1));
   const int D = Pm->num_dof, A = Pm->num_actions, NB = Pm->num_bodies;
   const uint32_t gid = (uint32_t)(Pm->env_id_offset + e);
 
@@ -1698,7 +1862,7 @@ __global__ __launch_bounds__(64, ACTNET ? LGX_SEA_WAVES : 4) void env_step_kerne
   if (lane < D) s.lt_prev[lane] = B.last_torques[(size_t)e * D + lane];
   {
     const int KS0 = Pm->num_reward_terms + (Pm->has_termination_reward ? 1 : 0);
-    if (lane < KS0) s.es[lane] = B.episode_sums[(size_t)e * KS0 + lane];
+    for (int k = lane; k < KS0; k += WL) s.es[k] = B.episode_sums[(size_t)e * KS0 + k];
   }
   if (Pm->task_kind == LGX_TASK_GO2 && lane < Pm->num_feet) {
     s.lc_prev[lane] = B.last_contacts[e * Pm->num_feet + lane];
@@ -1725,7 +1889,8 @@ __global__ __launch_bounds__(64, ACTNET ? LGX_SEA_WAVES : 4) void env_step_kerne
     }
     __syncthreads();
     PH(0);
-    for (int sub = 0; sub < Pm->decimation; ++sub) substep<TERRAIN, ACTNET>(s, M, Pm, B, lane, sub == Pm->decimation - 1);
+    for (int sub = 0; sub < Pm->decimation; ++sub)
+      substep<TERRAIN, ACTNET, WL>(s, AR, S_, lgx_dyn, astride, M, Pm, B, lane, e, sub == Pm->decimation - 1);
     __syncthreads();
     // NaN/Inf guard (SURVEY.md §5 "Failure detection"; the reference has none): a state that
     // went non-finite in any substep stays non-finite, so one check after the substeps sees it.
@@ -1740,7 +1905,7 @@ __global__ __launch_bounds__(64, ACTNET ? LGX_SEA_WAVES : 4) void env_step_kerne
       if (lane < 3) bad = bad || !(isfinite(s.pb[lane]) && isfinite(s.vo[lane]) && isfinite(s.wb[lane]));
       if (lane < 4) bad = bad || !isfinite(s.qb[lane]);
       if (lane < NB) bad = bad || !(isfinite(s.cf[lane][0]) && isfinite(s.cf[lane][1]) && isfinite(s.cf[lane][2]));
-      if (__ballot(bad) != 0ull) {
+      if (gballot<WL>(bad) != 0ull) {
         if (lane < D) { s.th[lane] = Pm->default_dof_pos[lane]; s.thd[lane] = 0.f; s.tau[lane] = 0.f; }
         if (lane < A) { s.act[lane] = 0.f; B.actions[(size_t)e * A + lane] = 0.f; }
         if (lane < 3) { s.pb[lane] = isfinite(s.root[lane]) ? s.root[lane] : 0.f; s.vo[lane] = 0.f; s.wb[lane] = 0.f; }
@@ -1754,7 +1919,7 @@ __global__ __launch_bounds__(64, ACTNET ? LGX_SEA_WAVES : 4) void env_step_kerne
       __syncthreads();
     }
     // final kinematics for the rigid-body state tensor
-    kinematics<false>(s, M, Pm, lane);
+    kinematics<false>(s, AR, M, Pm, lane);
     float root[13];
     {
       float R[9];
@@ -1822,18 +1987,18 @@ __global__ __launch_bounds__(64, ACTNET ? LGX_SEA_WAVES : 4) void env_step_kerne
   // Per-env scalars: lane 0, into LDS. Vectors: lane-parallel from LDS.
   // the old observation history (read back at the end of the step) in flight from here on:
   // the first HV x 64 entries into registers (all of Go2's 5 x 52)
-  constexpr int HV = 5;
+  constexpr int HV = 320 / WL;
   float hv[HV];
   {
     const int HPn = Pm->history_len * Pm->num_proprio;
     const float* hsrc = B.obs_history + (size_t)e * HPn;
 #pragma unroll
     for (int t = 0; t < HV; ++t) {
-      const int i = lane + 64 * t;
+      const int i = lane + WL * t;
       hv[t] = i < HPn ? hsrc[i] : 0.f;
     }
   }
-  fill_uniforms(s, seed, gid, step, 0, lane, rng_blocks(Pm));
+  fill_uniforms<WL>(AR, seed, gid, step, 0, lane, rng_blocks(Pm));
   PH(12);
   const bool go2 = Pm->task_kind == LGX_TASK_GO2;
   if (lane == 0) {
@@ -1873,7 +2038,7 @@ __global__ __launch_bounds__(64, ACTNET ? LGX_SEA_WAVES : 4) void env_step_kerne
       x.yaw = atan2f(2.0f * (qw * qz + qx * qy), 1.0f - 2.0f * (qy * qy + qz * qz));
     }
     // _post_physics_step_callback go2.py:390-410
-    if (ep % Pm->resample_interval == 0) resample_commands(Pm, B.command_ranges, cmd, stg_U(), S_CMD, root + 3);
+    if (ep % Pm->resample_interval == 0) resample_commands(Pm, B.command_ranges, cmd, stg_U(AR), S_CMD, root + 3);
     if (Pm->heading_command) {
       const float fwd[3] = {1.f, 0.f, 0.f};
       float f[3];
@@ -1883,8 +2048,8 @@ __global__ __launch_bounds__(64, ACTNET ? LGX_SEA_WAVES : 4) void env_step_kerne
       cmd[2] = clipf(wrap_to_pi(cmd[3] - heading) * gain, -1.0f, 1.0f);
     }
     if (Pm->push_robots && (step % (uint64_t)Pm->push_interval == 0)) {
-      root[7] = rand_range(-Pm->max_push_vel_xy, Pm->max_push_vel_xy, stg_U()[S_PUSH + 0]);
-      root[8] = rand_range(-Pm->max_push_vel_xy, Pm->max_push_vel_xy, stg_U()[S_PUSH + 1]);
+      root[7] = rand_range(-Pm->max_push_vel_xy, Pm->max_push_vel_xy, stg_U(AR)[S_PUSH + 0]);
+      root[8] = rand_range(-Pm->max_push_vel_xy, Pm->max_push_vel_xy, stg_U(AR)[S_PUSH + 1]);
     }
     // check_termination go2.py:186-204
     int reset = 0;
@@ -1905,14 +2070,15 @@ __global__ __launch_bounds__(64, ACTNET ? LGX_SEA_WAVES : 4) void env_step_kerne
   }
   __syncthreads();
   PH(13);
-  get_heights(Pm, B, s, lane);
+  get_heights<WL>(Pm, B, s, AR, lane);
   __syncthreads();
-  joint_sums(Pm, B, s, e, lane);
+  joint_sums(Pm, B, s, AR, e, lane);
   __syncthreads();
   // compute_reward legged_robot.py:216-237: lane k evaluates term k (alphabetical order)
   const int K = Pm->num_reward_terms;
   const int KS = K + (Pm->has_termination_reward ? 1 : 0);
-  if (lane < K) s.rterm[lane] = s.blew ? 0.0f : reward_term(Pm, B, s, e, Pm->reward_ids[lane]) * Pm->reward_scales[lane];
+  for (int k = lane; k < K; k += WL)
+    s.rterm[k] = s.blew ? 0.0f : reward_term(Pm, B, s, e, Pm->reward_ids[k]) * Pm->reward_scales[k];
   __syncthreads();
   const int reset = s.reset;
   if (lane == 0) {
@@ -1930,25 +2096,25 @@ __global__ __launch_bounds__(64, ACTNET ? LGX_SEA_WAVES : 4) void env_step_kerne
     if (B.blew_up) B.blew_up[e] = (uint8_t)s.blew;
   }
   __syncthreads();
-  if (lane < KS) {
-    const float v = s.es[lane] + s.rterm[lane];
-    s.es[lane] = v;
-    B.episode_sums[(size_t)e * KS + lane] = v;
+  for (int k = lane; k < KS; k += WL) {
+    const float v = s.es[k] + s.rterm[k];
+    s.es[k] = v;
+    B.episode_sums[(size_t)e * KS + k] = v;
   }
   __syncthreads();
   PH(14);
   // reset_idx (go2.py:207-263)
-  if (reset) reset_env(Pm, B, s, e, lane, true, false, true);
+  if (reset) reset_env<WL>(Pm, B, s, AR, e, lane, true, false, true);
 
   // compute_observations go2.py:467-574 / legged_robot.py:240-273
   const int Pp = Pm->num_proprio, H = Pm->history_len;
   const Scratch& x = s.x;
   if (go2 && Pm->parkour && lane == 0) {
     int outl = 0;
-    for (int i = 0; i < Pm->num_height_points; ++i) outl += fabsf(stg_heights(Pm)[i]) > 0.1f;
+    for (int i = 0; i < Pm->num_height_points; ++i) outl += fabsf(stg_heights(AR, Pm)[i]) > 0.1f;
     s.x.jump = (float)(outl >= 8);
   }
-  for (int i = lane; i < Pp; i += 64) {
+  for (int i = lane; i < Pp; i += WL) {
     float v;
     if (go2) {
       if (i < 3) v = x.bav[i] * Pm->obs_scale_ang_vel;
@@ -1972,15 +2138,15 @@ __global__ __launch_bounds__(64, ACTNET ? LGX_SEA_WAVES : 4) void env_step_kerne
       else if (i < 12 + D) v = (s.th[i - 12] - Pm->default_dof_pos[i - 12]) * Pm->obs_scale_dof_pos;
       else if (i < 12 + 2 * D) v = s.thd[i - 12 - D] * Pm->obs_scale_dof_vel;
       else if (i < 12 + 2 * D + A) v = s.act[i - 12 - 2 * D];
-      else v = clipf(s.root[2] - 0.5f - stg_heights(Pm)[i - (12 + 2 * D + A)], -1.0f, 1.0f) * Pm->obs_scale_height;
+      else v = clipf(s.root[2] - 0.5f - stg_heights(AR, Pm)[i - (12 + 2 * D + A)], -1.0f, 1.0f) * Pm->obs_scale_height;
     }
-    if (Pm->add_noise) v = v + (2.0f * stg_U()[S_NOISE + i] - 1.0f) * Pm->noise_vec[i];
-    stg_cur(Pm)[i] = v;
+    if (Pm->add_noise) v = v + (2.0f * stg_U(AR)[S_NOISE + i] - 1.0f) * Pm->noise_vec[i];
+    stg_cur(AR, Pm)[i] = v;
   }
   // stage the old history (obs[0:H*P]) in LDS; a reset env's history was zeroed (go2.py:238)
   float* hist_g = B.obs_history + (size_t)e * H * Pp;
-  float* const hist = stg_hist(Pm);
-  const float* const cur = stg_cur(Pm);
+  float* const hist = stg_hist(AR, Pm);
+  const float* const cur = stg_cur(AR, Pm);
   const bool hl = hist_in_lds(Pm);
   const long long ep = s.ep;
   const float co = Pm->clip_obs;
@@ -1989,14 +2155,14 @@ __global__ __launch_bounds__(64, ACTNET ? LGX_SEA_WAVES : 4) void env_step_kerne
   if (hl) {
 #pragma unroll
     for (int t = 0; t < HV; ++t) {
-      const int i = lane + 64 * t;
+      const int i = lane + WL * t;
       if (i < H * Pp) hist[i] = reset ? 0.f : hv[t];
     }
-    for (int i = lane + 64 * HV; i < H * Pp; i += 64) hist[i] = reset ? 0.f : hist_g[i];
+    for (int i = lane + WL * HV; i < H * Pp; i += WL) hist[i] = reset ? 0.f : hist_g[i];
   }
   __syncthreads();
   if (hl) {
-    for (int i = lane; i < H * Pp; i += 64) {
+    for (int i = lane; i < H * Pp; i += WL) {
       float v = clipf(hist[i], -co, co);
       obs[i] = v;
       if (go2 && cr) cr[i] = v;
@@ -2009,9 +2175,9 @@ __global__ __launch_bounds__(64, ACTNET ? LGX_SEA_WAVES : 4) void env_step_kerne
     // before it is read.
     const int HP = H * Pp, HP1 = (H - 1) * Pp;
 #pragma unroll
-    for (int t = 0; t < (MAXHIST + 63) / 64; ++t) {
-      const int i = lane + 64 * t;
-      if (64 * t >= HP) break;
+    for (int t = 0; t < (MAXHIST + WL - 1) / WL; ++t) {
+      const int i = lane + WL * t;
+      if (WL * t >= HP) break;
       if (i < HP) {
         const float old = reset ? 0.f : (t < HV ? hv[t < HV ? t : 0] : hist_g[i]);
         const float v = clipf(old, -co, co);
@@ -2022,7 +2188,7 @@ __global__ __launch_bounds__(64, ACTNET ? LGX_SEA_WAVES : 4) void env_step_kerne
       }
     }
   }
-  for (int i = lane; i < Pp; i += 64) {
+  for (int i = lane; i < Pp; i += WL) {
     float v = clipf(cur[i], -co, co);
     obs[H * Pp + i] = v;
     if (go2 && cr) cr[H * Pp + i] = v;
@@ -2030,7 +2196,7 @@ __global__ __launch_bounds__(64, ACTNET ? LGX_SEA_WAVES : 4) void env_step_kerne
   if (go2) {
     const int NO = Pm->num_obs;
     // priv = [mass params (4), friction, kp-1 (D), kd-1 (D)]
-    for (int i = lane; i < Pm->num_priv; i += 64) {
+    for (int i = lane; i < Pm->num_priv; i += WL) {
       float v;
       if (i < 4) v = i == 0 ? s.madd : s.cadd[i - 1];  // mass_params row, staged at kernel start
       else if (i == 4) v = s.fric;
@@ -2045,15 +2211,15 @@ __global__ __launch_bounds__(64, ACTNET ? LGX_SEA_WAVES : 4) void env_step_kerne
       B.est[(size_t)e * Pm->num_est + lane] = v;
       if (cr) cr[NO + Pm->num_priv + lane] = v;
     }
-    for (int i = lane; i < Pm->num_scan; i += 64) {
-      float v = clipf(s.root[2] - 0.3f - stg_heights(Pm)[i], -1.0f, 1.0f);
+    for (int i = lane; i < Pm->num_scan; i += WL) {
+      float v = clipf(s.root[2] - 0.3f - stg_heights(AR, Pm)[i], -1.0f, 1.0f);
       B.scan[(size_t)e * Pm->num_scan + i] = v;
       if (cr) cr[NO + Pm->num_priv + 3 + i] = clipf(v, -co, co);
     }
   }
   // history update go2.py:570-574 (the long-history path wrote it above)
   if (hl)
-    for (int i = lane; i < H * Pp; i += 64) {
+    for (int i = lane; i < H * Pp; i += WL) {
       float v = (ep <= 1) ? cur[i % Pp] : (i < (H - 1) * Pp ? hist[i + Pp] : cur[i - (H - 1) * Pp]);
       hist_g[i] = v;
     }
@@ -2085,10 +2251,16 @@ __global__ __launch_bounds__(64, ACTNET ? LGX_SEA_WAVES : 4) void env_step_kerne
     B.rpy_phase[e * 8 + lane] = v;
   }
   if (B.measured_heights)
-    for (int i = lane; i < Pm->num_height_points; i += 64) B.measured_heights[(size_t)e * Pm->num_height_points + i] = stg_heights(Pm)[i];
+    for (int i = lane; i < Pm->num_height_points; i += WL)
+      B.measured_heights[(size_t)e * Pm->num_height_points + i] = stg_heights(AR, Pm)[i];
 #ifdef LGX_PHASE_CLOCK
   __syncthreads();
   PH(15);
+  __syncthreads();
+  if (lane == 0) {  // where the wave ran: HW_ID (wave, SIMD, CU, SE fields) and XCC_ID
+    s.phacc[18] = __builtin_amdgcn_s_getreg(4 | (31 << 11));
+    s.phacc[19] = __builtin_amdgcn_s_getreg(20 | (31 << 11));
+  }
   __syncthreads();
   if (g_phase_out && lane < NPH) g_phase_out[(size_t)e * NPH + lane] = s.phacc[lane];
 #endif
@@ -2104,13 +2276,13 @@ __global__ __launch_bounds__(64) void reset_kernel(const lgx_task_params* __rest
   const int lane = threadIdx.x;
   if (!mask[e]) return;
   const int D = Pm->num_dof;
-  fill_uniforms(s, seed, (uint32_t)(Pm->env_id_offset + e), call, 1, lane, rng_blocks(Pm));
+  fill_uniforms<64>(lgx_dyn, seed, (uint32_t)(Pm->env_id_offset + e), call, 1, lane, rng_blocks(Pm));
   if (lane < 13) s.root[lane] = B.root_states[(size_t)e * 13 + lane];
   if (lane < 4) s.cmd[lane] = B.commands[e * 4 + lane];
   __syncthreads();
   // an external reset (BaseTask.reset -> reset_idx) only exists once the env is built,
   // i.e. with init_done set: the terrain curriculum applies (legged_robot.py:551-552)
-  reset_env(Pm, B, s, e, lane, true, true, false);
+  reset_env<64>(Pm, B, s, lgx_dyn, e, lane, true, true, false);
   if (lane < 13) B.root_states[(size_t)e * 13 + lane] = s.root[lane];
   if (lane < D) {
     B.dof_state[((size_t)e * D + lane) * 2] = s.th[lane];
@@ -2138,6 +2310,7 @@ struct lgx_env {
   bool host = false;         // device < 0: the host backend (lgx_env_host.cpp), host buffers
   bool bound = false;
   bool stats_clean = false;  // episode_stats zeroed by lgx_episode_extras and not written since
+  int epw = 0;               // envs per wave (lgx_set_envs_per_wave; 0: default)
   std::string err;
 };
 
@@ -2279,15 +2452,33 @@ static int launch_step(lgx_env* env, uint64_t seed, uint64_t step, const uint64_
   if (env->buffers.episode_stats && !env->stats_clean)
     HIP_OK(hipMemsetAsync(env->buffers.episode_stats, 0, sizeof(float) * (KS + 1), st));
   env->stats_clean = false;
-  // compiled variants: the plane/PD path (the benchmark) carries no terrain or LSTM code
+  // compiled variants: the plane/PD path (the benchmark) carries no terrain or LSTM code. Two
+  // envs per wave (EPW 2: 32 lanes each, lgx_env.hip grp_of_lane) for an even env count without
+  // the actuator net (its LSTM lanes need the whole wave); LGX_ENVS_PER_WAVE=1 selects one env
+  // per wave (A/B, tests)
   const bool terrain = env->params.mesh_type != LGX_MESH_PLANE, actnet = env->params.actuator_net != 0;
-  auto kern = !physics ? lgx::env_step_kernel<false, false, false>
-              : actnet ? (terrain ? lgx::env_step_kernel<true, true, true> : lgx::env_step_kernel<true, false, true>)
-                       : (terrain ? lgx::env_step_kernel<true, true, false> : lgx::env_step_kernel<true, false, false>);
-  const size_t dyn = sizeof(float) * (size_t)lgx::arena_floats(env->params);
-  hipLaunchKernelGGL(kern, dim3(N), dim3(64), dyn, st, env->d_model, env->d_params, env->d_buffers, seed, step,
+  static const int epw_env = [] {
+    const char* v = getenv("LGX_ENVS_PER_WAVE");
+    return v && atoi(v) == 1 ? 1 : 2;
+  }();
+  const int epw = (!actnet && N % 2 == 0 && (env->epw ? env->epw : epw_env) == 2) ? 2 : 1;
+  auto kern = epw == 2 ? (!physics ? lgx::env_step_kernel<false, false, false, 2>
+                                   : (terrain ? lgx::env_step_kernel<true, true, false, 2>
+                                              : lgx::env_step_kernel<true, false, false, 2>))
+            : !physics ? lgx::env_step_kernel<false, false, false, 1>
+            : actnet   ? (terrain ? lgx::env_step_kernel<true, true, true, 1> : lgx::env_step_kernel<true, false, true, 1>)
+                       : (terrain ? lgx::env_step_kernel<true, true, false, 1> : lgx::env_step_kernel<true, false, false, 1>);
+  const size_t dyn = sizeof(float) * (size_t)lgx::arena_floats(env->params) * epw;
+  hipLaunchKernelGGL(kern, dim3(N / epw), dim3(64), dyn, st, env->d_model, env->d_params, env->d_buffers, seed, step,
                      step_dev);
   HIP_OK(hipGetLastError());
+  return 0;
+}
+
+int lgx_set_envs_per_wave(lgx_env* env, int32_t envs_per_wave) {
+  if (!env) return -2;
+  if (envs_per_wave < 0 || envs_per_wave > 2) return fail(env, "lgx_set_envs_per_wave: 0, 1 or 2");
+  env->epw = envs_per_wave;
   return 0;
 }
 

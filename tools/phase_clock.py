@@ -78,12 +78,32 @@ def run():
             torch.cuda.synchronize()
             ms += s.elapsed_time(e)
             cyc = buf.double().remainder(2 ** 32)
-            acc += cyc
+            acc[:, :18] += cyc[:, :18]
             rows.append(buf[:, 16].clone())
             wt = cyc[:, :16].sum(dim=1)
             j = int(wt.argmax())
             per_step.append((s.elapsed_time(e) * 1e3, float(wt.median()), float(wt.max()), int(buf[j, 16]),
                              int(buf[j, 17]), float(torch.quantile(wt, 0.999))))
+    # the last step's slowest waves against the median: phases and where they ran
+    last = buf.double().remainder(2 ** 32)
+    wt = last[:, :16].sum(dim=1)
+    order = torch.argsort(wt)
+    med = order[n // 2]
+    hw = buf[:, 18].long() & 0xffffffff
+    xcc = buf[:, 19].long() & 0xf
+
+    def where(i):
+        h = int(hw[i])
+        return f"xcc {int(xcc[i])} se {(h >> 13) & 7} cu {(h >> 8) & 15} simd {(h >> 4) & 3} wave {h & 15}"
+    print("last step, slowest envs vs the median env (cycles per phase):")
+    print("  median env", int(med), where(int(med)), " ".join(f"{PHASES[j]}={int(last[med, j])}" for j in range(16)))
+    for i in order[-6:].tolist():
+        print("  env", i, where(i), f"total {int(wt[i])}:", " ".join(f"{PHASES[j]}={int(last[i, j])}" for j in range(16)))
+    import collections
+    slow = order[-max(1, n // 100):].tolist()
+    print("  slowest 1 % by xcc:", dict(collections.Counter(int(xcc[i]) for i in slow)),
+          "by simd:", dict(collections.Counter((int(hw[i]) >> 4) & 3 for i in slow)),
+          "by wave slot:", dict(collections.Counter(int(hw[i]) & 15 for i in slow)))
     acc /= k
     tot = acc[:, :16].sum(dim=1)
     r = torch.stack(rows).float()
