@@ -181,6 +181,19 @@ LGX_DEV int env_of_block(int b, int n) {
 #ifndef LGX_ROW_PRIO
 #define LGX_ROW_PRIO 9  // 0: no priority
 #endif
+#ifndef LGX_SLOT_PRIO
+#define LGX_SLOT_PRIO 0  // 1: issue priority by the wave's slot on its SIMD (see env_step_kernel)
+#endif
+
+// the wave's slot on its SIMD (HW_ID wave_id field)
+LGX_DEV int wave_slot() { return __builtin_amdgcn_s_getreg(4 | (3 << 11)) & 15; }
+// s_setprio(p) for a runtime p in 0..3
+LGX_DEV void set_prio(int p) {
+  if (p >= 3) __builtin_amdgcn_s_setprio(3);
+  else if (p == 2) __builtin_amdgcn_s_setprio(2);
+  else if (p == 1) __builtin_amdgcn_s_setprio(1);
+  else __builtin_amdgcn_s_setprio(0);
+}
 
 LGX_DEV int opaque_lane(int v) {
   __asm__ volatile("" : "+v"(v));
@@ -1275,10 +1288,10 @@ LGX_DEV void substep(Sh& s, float* A, Sh* S0, float* A0, int astride, const lgx_
   // Issue priority by constraint-system size (s_setprio 0..3 above 0 / t / 2t / 3t rows): a
   // launch lasts as long as its slowest wave, and the waves with the largest systems are the
   // slow ones; the SIMD's other waves have the slack (profiles/r03_wave_priority.txt).
-  if (nrw > LGX_ROW_PRIO * 3) __builtin_amdgcn_s_setprio(3);
-  else if (nrw > LGX_ROW_PRIO * 2) __builtin_amdgcn_s_setprio(2);
-  else if (nrw > LGX_ROW_PRIO) __builtin_amdgcn_s_setprio(1);
-  else __builtin_amdgcn_s_setprio(0);
+  {
+    const int rp = nrw > LGX_ROW_PRIO * 3 ? 3 : nrw > LGX_ROW_PRIO * 2 ? 2 : nrw > LGX_ROW_PRIO ? 1 : 0;
+    set_prio(LGX_SLOT_PRIO ? max(rp, min(wave_slot(), 3)) : rp);
+  }
 #endif
   if (lane == 0) { s.nrows = nrows; s.nlim = nlim; s.ncon = ncon; }
 #ifdef LGX_PHASE_CLOCK
@@ -1826,6 +1839,11 @@ __global__ __launch_bounds__(64, ACTNET ? LGX_SEA_WAVES : (EPW == 2 ? 2 : 4)) vo
   const uint64_t step = step_dev ? *step_dev : step_arg;
   const int e = EPW * env_of_block(blockIdx.x, gridDim.x) + grp;
   const int lane = EPW == 1 ? (int)threadIdx.x : (int)(threadIdx.x & (WL - 1));
+#if LGX_SLOT_PRIO
+  // the SIMD's arbiter favours its older waves; a launch ends with its slowest wave, so the
+  // younger slots get the higher issue priority
+  set_prio(min(wave_slot(), 3));
+#endif
   const int D = Pm->num_dof, A = Pm->num_actions, NB = Pm->num_bodies;
   const uint32_t gid = (uint32_t)(Pm->env_id_offset + e);
 

@@ -8,6 +8,6 @@ for r in 1 2; do
   for v in "$@"; do
     i=$((i+1))
     env $v timeout -k 10 300 python bench.py --no_cpu_baseline > $O/bench_$i.log 2>&1 || { tail -20 $O/bench_$i.log; exit 1; }
-    echo "[$v] $(tail -n 1 $O/bench_$i.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["collection_s"], d["learn_s"], d["roofline_learner"]["us_per_launch"])')"
+    echo "[$v] $(tail -n 1 $O/bench_$i.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["collection_s"], d["learn_s"], d["env_kernel"]["avg_us"], d["roofline_learner"]["us_per_launch"])')"
   done
 done
