@@ -57,6 +57,13 @@ struct Cfg {
   static constexpr int LDS = LDS_STAGES > LDS_EPI ? LDS_STAGES : LDS_EPI;
 };
 
+// ---- per-block cycle accounts (dev builds only: -DLGX_S8_CLOCK, tools/s8_clock.py): waves 0 and
+// NW - 1 of every block sum clock64 deltas of the K loop's DMA wait, barrier and issue + compute
+// sections and of the epilogue, into g_s8clk[block][wave slot][12]. Compiled out of the product.
+#ifdef LGX_S8_CLOCK
+__device__ uint32_t* g_s8clk = nullptr;
+#endif
+
 // slot swizzles (16-B slot index XOR), image row -> mask
 __device__ __forceinline__ int fsw_row(int r) {
   if constexpr (BK == 32) return ((r >> 1) & 1) | (((r >> 3) & 1) << 2);  // 8 slots per 128-B row
@@ -79,10 +86,18 @@ struct Prob {
   float* colsum_ws;
 };
 
+// XCD units (weight gradients): whole K-chunk slices of a problem (all its output tiles of one
+// K chunk) dealt to one XCD each, so that every operand byte of a chunk is fetched into one L2
+// only (the tiles of a slice share its dY and X rows). units[ustart[x] .. ustart[x + 1]) are XCD
+// slot x's slices in order, each pi | z << 5, covering tiles_m * tiles_n consecutive jb.
+constexpr int UMAX = 256;
 struct Group {
   int n, per_xcd;
   int start[GMAX + 1];
   Prob p[GMAX];
+  int nunits;
+  uint16_t ustart[9];
+  uint16_t units[UMAX];
 };
 static_assert(sizeof(Group) <= 4096, "kernel argument segment");
 
@@ -331,10 +346,24 @@ __global__ __launch_bounds__(Cfg::NT, 2) __attribute__((amdgpu_waves_per_eu(1, 2
 
   const int x = blockIdx.x & 7, jb = blockIdx.x >> 3;
   if (jb >= g.per_xcd) return;
-  int pi = 0;
-  while (pi + 1 < g.n && jb >= g.start[pi + 1]) ++pi;
+  int pi = 0, l = -1;
+  if (g.nunits > 0) {
+    int j = jb;
+    for (int u = g.ustart[x]; u < g.ustart[x + 1]; ++u) {
+      const int e = g.units[u], q = e & 31, sz = g.p[q].tiles_m * g.p[q].tiles_n;
+      if (j < sz) {
+        pi = q;
+        l = (e >> 5) * sz + j;
+        break;
+      }
+      j -= sz;
+    }
+    if (l < 0) return;
+  } else {
+    while (pi + 1 < g.n && jb >= g.start[pi + 1]) ++pi;
+    l = x * (g.start[pi + 1] - g.start[pi]) + (jb - g.start[pi]);
+  }
   const Prob P = g.p[pi];
-  const int l = x * (g.start[pi + 1] - g.start[pi]) + (jb - g.start[pi]);
   if (l >= P.tiles) return;
   const int tn = l % P.tiles_n, tm = (l / P.tiles_n) % P.tiles_m, z = l / (P.tiles_n * P.tiles_m);
   const int m0 = tm * BM, n0 = tn * BN;
@@ -397,7 +426,15 @@ __global__ __launch_bounds__(Cfg::NT, 2) __attribute__((amdgpu_waves_per_eu(1, 2
 #pragma unroll
   for (int s = 0; s < NS - 1; ++s)
     if (s < nk) issue(s, s);
+#ifdef LGX_S8_CLOCK
+  uint64_t ck0 = clock64(), ckl = ck0;
+  uint32_t ckw = 0, ckb = 0, ckc = 0;
+#define S8CK(acc_) do { const uint64_t t_ = clock64(); acc_ += (uint32_t)(t_ - ckl); ckl = t_; } while (0)
+#else
+#define S8CK(acc_) do { } while (0)
+#endif
   for (int k = 0; k < nk; ++k) {
+    S8CK(ckc);
     if (k + NS - 2 < nk) {
       if constexpr (NS == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       else if constexpr (NS == 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW) : "memory");
@@ -405,12 +442,15 @@ __global__ __launch_bounds__(Cfg::NT, 2) __attribute__((amdgpu_waves_per_eu(1, 2
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
+    S8CK(ckw);
     asm volatile("s_barrier" ::: "memory");
+    S8CK(ckb);
     if (k + NS - 1 < nk) issue((k + NS - 1) % NS, k + NS - 1);
     compute(k % NS);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  S8CK(ckc);
 
   // ---- epilogue: the fp32 tile into LDS (MFMA C/D map: col = lane & 15, row = (lane >> 4) * 4 + r)
   float* img = reinterpret_cast<float*>(lds);
@@ -428,6 +468,14 @@ __global__ __launch_bounds__(Cfg::NT, 2) __attribute__((amdgpu_waves_per_eu(1, 2
     epi_dw<NT, BM, BN, CP>(P, img, m0, n0, z, tid);
   else
     epi_act<KIND, NT, BM, BN, CP>(P, img, m0, n0, tm * (BM / LGX_S8_TILE_M), tid);
+#ifdef LGX_S8_CLOCK
+  if (lane == 0 && (wave == 0 || wave == NW - 1) && g_s8clk != nullptr) {
+    const uint64_t t = clock64();
+    uint32_t* o = g_s8clk + ((size_t)blockIdx.x * 2 + (wave != 0)) * 12;
+    o[0] = ckw; o[1] = ckb; o[2] = ckc; o[3] = (uint32_t)(t - ckl); o[4] = (uint32_t)(t - ck0);
+    o[5] = (uint32_t)nk; o[6] = __builtin_amdgcn_s_getreg(20 | (31 << 11)) & 15;  // XCC_ID
+  }
+#endif
 }
 
 // ---------------------------------------------------------------- fp32 -> S8 (+ column sums)
@@ -611,6 +659,51 @@ static int cdiv(int a, int b) { return (a + b - 1) / b; }
 int lgxs_fail(const char* msg) { return fail(msg); }  // for the library's other sources
 int lgxs_launched(const char* what) { return launched(what); }
 
+static bool dw_xcd_units() {
+  static int on = -1;
+  if (on < 0) {
+    const char* e = getenv("LGX_S8_DW_XCD");  // dev knob: 0 = tiles dealt per problem
+    on = e ? atoi(e) != 0 : 1;
+  }
+  return on != 0;
+}
+
+// Deal the weight-gradient slices (problem, K chunk) to the 8 XCD slots, largest first onto the
+// least-loaded slot (LPT); kept only if it needs no more block slots per XCD than one residency
+// round (2 blocks x 32 CUs) or than the per-problem deal. Measured (tools/dw_probe.py, the go2
+// minibatch's group alone): fabric reads 958 -> 687 MB per launch (FETCH_SIZE x 2; the operands
+// are 661 MB), 196.6 -> 193.7 us — the group is not bound by its HBM traffic.
+static void deal_units(lgxs::Group& g) {
+  struct U { int pi, z, sz; };
+  U u[lgxs::UMAX];
+  int nu = 0;
+  for (int pi = 0; pi < g.n; ++pi) {
+    const lgxs::Prob& p = g.p[pi];
+    const int sz = p.tiles_m * p.tiles_n, split = p.tiles / sz;
+    if (split > 2047 || nu + split > lgxs::UMAX) return;
+    for (int z = 0; z < split; ++z) u[nu++] = U{pi, z, sz};
+  }
+  std::stable_sort(u, u + nu, [](const U& a, const U& b) { return a.sz > b.sz; });
+  int load[8] = {0}, cnt[8] = {0}, slot[lgxs::UMAX];
+  for (int i = 0; i < nu; ++i) {
+    int x = 0;
+    for (int y = 1; y < 8; ++y)
+      if (load[y] < load[x]) x = y;
+    slot[i] = x;
+    load[x] += u[i].sz;
+    ++cnt[x];
+  }
+  const int mx = *std::max_element(load, load + 8);
+  if (mx > std::max(g.per_xcd, 64)) return;
+  g.ustart[0] = 0;
+  for (int x = 0; x < 8; ++x) g.ustart[x + 1] = (uint16_t)(g.ustart[x] + cnt[x]);
+  int fill[8];
+  for (int x = 0; x < 8; ++x) fill[x] = g.ustart[x];
+  for (int i = 0; i < nu; ++i) g.units[fill[slot[i]]++] = (uint16_t)(u[i].pi | (u[i].z << 5));
+  g.nunits = nu;
+  g.per_xcd = mx;
+}
+
 template <int KIND>
 static void launch_gemm(const lgxs::Group& g, hipStream_t s) {
   constexpr int lds = lgxs::Cfg::LDS;
@@ -626,6 +719,11 @@ static void launch_gemm(const lgxs::Group& g, hipStream_t s) {
 extern "C" {
 
 int32_t lgx_s8_abi_version(void) { return LGX_S8_ABI_VERSION; }
+#ifdef LGX_S8_CLOCK
+int32_t lgx_s8_set_clock(void* dev_buf) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(lgxs::g_s8clk), &dev_buf, sizeof(void*)) == hipSuccess ? 0 : -1;
+}
+#endif
 int32_t lgx_s8_sizeof_gemm_args(void) { return (int32_t)sizeof(lgx_s8_gemm_args); }
 const char* lgx_s8_last_error(void) { return g_err; }
 
@@ -713,6 +811,7 @@ int32_t lgx_s8_gemm_group(const lgx_s8_gemm_args* a, int32_t n, int32_t kind, vo
   g.n = np;
   g.per_xcd = acc;
   if (np == 0) return 0;
+  if (kind == LGX_S8_DW && dw_xcd_units()) deal_units(g);
   hipStream_t s = (hipStream_t)stream;
   if (kind == LGX_S8_FWD) launch_gemm<LGX_S8_FWD>(g, s);
   else if (kind == LGX_S8_DX) launch_gemm<LGX_S8_DX>(g, s);
