@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define LGX_MLP_ABI_VERSION 8
+#define LGX_MLP_ABI_VERSION 9
 
 enum {
   LGX_EPI_BIAS = 1,  /* + bias[n] */
@@ -229,11 +229,44 @@ typedef struct lgx_heads_s8_args {
    * launch takes its decisions from here instead (forward maxima and gradients; the continuous
    * quantities stay its own), so a test can replay a reference run's decisions and its
    * trajectory cannot leave the reference's at a sample sitting within rounding of a clip
-   * boundary (tests/test_gpu_learner_golden.py). */
+   * boundary (tests/test_gpu_learner_golden.py). ABI 9: a decisions_in byte with bit 6 (0x40)
+   * set leaves that row its own decisions (replaying only the near-tie samples). */
   const uint8_t* decisions_in; uint8_t* decisions_out;
 } lgx_heads_s8_args;
 int32_t lgx_loss_heads_fused(const lgx_ppo_head_args* head, const lgx_aux_loss_args* aux,
                              const lgx_heads_s8_args* s8, void* stream);
+
+/* ABI 9. lgx_loss_heads_fused with the actor's and the critic's LAST layers fused around the
+ * PPO head (the S8 update; rsl_rl actor_critic.py:82-107, ppo.py:196-262 and the backward of
+ * those two layers), per block of LGX_HEADS_TAIL_ROWS rows:
+ *   mu = y W^T + b, value = y_c W_c^T + b_c   fp32 FMAs over k in order; y, y_c: the last hidden
+ *                                             layers' S8 outputs [B][H] read as hi + lo; W [A][H],
+ *                                             W_c [1][H_c] fp32 (nn.Linear layout)
+ *   the PPO head of lgx_loss_heads_fused on them (head->mu / head->value are IGNORED as inputs);
+ *   the aux head as there (blockIdx.y = 1)
+ *   dy = (dmu W) * ELU'(y), dy_c = (dvalue W_c) * ELU'(y_c) -> S8 [B][H] with one column-sum
+ *                                             partial per block ([ceil(B/32)][H]: the hidden
+ *                                             layers' bias-gradient partials)
+ * It replaces the last layers' forward launch, lgx_loss_heads_fused and the last layers' input-
+ * gradient launch. Here s8->dmu_cs / dvalue_cs are per 32-row block ([ceil(B/32)][A], [..][1]),
+ * head->ws >= (3 + 16) * ceil(B/32) floats; mu_out / value_out (optional): fp32 copies of mu
+ * [B][A] and value [B]. H, H_c multiples of 8 in [8, 256]; A <= 16.
+ * The PPO head's totals are NOT formed in this launch (no last-block pass; head->counter is not
+ * used): head->ws holds one row of 3 + 16 floats per block, {surrogate / B, value loss / B,
+ * KL / B, dstd partial [A]} (block 0's dstd partial includes the entropy term), and the caller
+ * sums the rows (out[0..1], out[3] / kl_dst, dstd: lgx_s8_reduce jobs); out[2] (the entropy) is
+ * written here. The aux head forms its totals as in lgx_loss_heads_fused. */
+#define LGX_HEADS_TAIL_ROWS 32
+typedef struct lgx_heads_tail_args {
+  const void* y; int64_t ld_y; const float* W; const float* b;
+  void* dy; int64_t ld_dy; float* dy_cs;
+  const void* yc; int64_t ld_yc; const float* Wc; const float* bc;
+  void* dyc; int64_t ld_dyc; float* dyc_cs;
+  float* mu_out; float* value_out;
+  int32_t H, Hc;
+} lgx_heads_tail_args;
+int32_t lgx_loss_heads_tail(const lgx_ppo_head_args* head, const lgx_aux_loss_args* aux,
+                            const lgx_heads_s8_args* s8, const lgx_heads_tail_args* tail, void* stream);
 
 /* The optimizer tail of one PPO minibatch (rsl_rl ppo.py:264-291) in two launches, over
  * the flat gradient/parameter/moment buffers (one layout):

@@ -992,7 +992,7 @@ constexpr int HT = LGX_HT;  // threads per block (rows per block and grid-stride
 // the loss heads' cross-wave scratch (red[4 * ...]) holds at most 4 waves
 static_assert(HT % 64 == 0 && HT >= 64 && HT <= 256, "LGX_HT: 64..256 threads, whole waves");
 // one row per thread (grid-stride loops, so any grid is correct; fewer blocks measured slower)
-static unsigned head_grid(int B) { return (unsigned)((B + HT - 1) / HT); }
+__host__ __device__ inline unsigned head_grid(int B) { return (unsigned)((B + HT - 1) / HT); }
 constexpr int HMAXA = 16;   // max actions
 
 // block-wide sum of NV values per thread into red[NV] (thread 0 holds the result)
@@ -1022,12 +1022,12 @@ __device__ void block_sum(float (&v)[NV], float* red) {
 // partials: it alone releases them (agent scope) before the counter — an agent-scope fence
 // by every thread of every block costs microseconds per block — and the last block's
 // threads acquire before they read the other blocks' partials.
-__device__ bool last_block(uint32_t* counter) {
+__device__ bool last_block(uint32_t* counter, unsigned nblk = 0) {
   __shared__ bool last;
   __syncthreads();
   if (threadIdx.x == 0) {
     __threadfence();
-    last = atomicAdd(counter, 1u) == gridDim.x - 1;
+    last = atomicAdd(counter, 1u) == (nblk ? nblk : gridDim.x) - 1;
   }
   __syncthreads();
   if (last) __threadfence();
@@ -1372,106 +1372,131 @@ __device__ __forceinline__ void store_s8_group(char* dst, const float (&v)[8]) {
   reinterpret_cast<u32x4_*>(dst)[1] = L;
 }
 
+// One row of the fused PPO head (forward sums into v, input gradients dmu / dv, the S8 / fp32
+// gradient rows and the decisions): mu and the value come from the caller (global rows, or the
+// fused last layers of lgx_loss_heads_tail).
+// A row's inputs of the PPO head besides mu and the value (columns past A repeat the last one)
 template <int NA>
-__device__ __forceinline__ void ppo_head_fused_body(const lgx_ppo_head_args& p, const lgx_heads_s8_args& s) {
-  constexpr int NV = 3 + 2 * NA + 1;  // forward sums | dstd partial | dmu column sums | dvalue sum
-  __shared__ float red[4 * NV];
-  __shared__ float stdv[HMAXA], lstd[HMAXA];
-  if (threadIdx.x < HMAXA) {
-    const float sd = p.std[min((int)threadIdx.x, p.A - 1)];
-    stdv[threadIdx.x] = sd;
-    lstd[threadIdx.x] = logf(sd);
-  }
-  __syncthreads();
-  const float gs = p.g[0] / p.B, gv = p.g[1] / p.B, ge = p.g[2];
-  float v[NV];
-#pragma unroll
-  for (int k = 0; k < NV; ++k) v[k] = 0.f;
-  for (int i = blockIdx.x * HT + threadIdx.x; i < p.B; i += gridDim.x * HT) {
-    float act[NA], mu[NA], os[NA], om[NA];
+struct HeadIn {
+  float act[NA], os[NA], om[NA];
+  float old_logp, adv, tv, R;
+  __device__ __forceinline__ void load(const lgx_ppo_head_args& p, int i) {
     load_cols(p.actions, i, p.A, act);
-    load_cols(p.mu, i, p.A, mu);
     load_cols(p.old_sigma, i, p.A, os);
     load_cols(p.old_mu, i, p.A, om);
-    const HeadRow h = head_row<NA>(p, i, stdv, lstd, act, mu);
-    const float a = p.adv[i];
-    const float lo = 1.f - p.clip, hi = 1.f + p.clip;
-    // forward (ppo_head_fwd_body)
-    const float s1 = -a * h.ratio, s2 = -a * fminf(fmaxf(h.ratio, lo), hi);
-    const float val = p.value[i], R = p.returns[i];
-    const float tv = (p.clipped_value ? p.target_values : p.value)[i];
-    const float vc = p.clipped_value ? tv + fminf(fmaxf(val - tv, -p.clip), p.clip) : 0.f;
-    const float l1 = (val - R) * (val - R), l2 = (vc - R) * (vc - R);
-    // the discrete decisions (torch's gradient rules: max splits ties, clamp passes on [lo, hi])
-    float w1 = s1 > s2 ? 1.f : (s1 == s2 ? 0.5f : 0.f);
-    float in = (h.ratio >= lo && h.ratio <= hi) ? 1.f : 0.f;
-    float u1 = l1 > l2 ? 1.f : (l1 == l2 ? 0.5f : 0.f);
-    float inv = (val - tv >= -p.clip && val - tv <= p.clip) ? 1.f : 0.f;
-    if (s.decisions_out)
-      s.decisions_out[i] = (uint8_t)((unsigned)(2.f * w1) | ((unsigned)in << 2) | ((unsigned)(2.f * u1) << 3) |
-                                     ((unsigned)inv << 5));
-    const bool forced = s.decisions_in != nullptr;
-    if (forced) {
-      const unsigned d = s.decisions_in[i];
-      w1 = 0.5f * (float)(d & 3u);
-      in = (float)((d >> 2) & 1u);
-      u1 = 0.5f * (float)((d >> 3) & 3u);
-      inv = (float)((d >> 5) & 1u);
-    }
-    if (!forced) {
-      v[0] += fmaxf(s1, s2);
-      v[1] += p.clipped_value ? fmaxf(l1, l2) : (R - val) * (R - val);
-    } else {  // the forced branch's value (a tie: either)
-      v[0] += w1 > 0.75f ? s1 : (w1 < 0.25f ? s2 : fmaxf(s1, s2));
-      v[1] += p.clipped_value ? (u1 > 0.75f ? l1 : (u1 < 0.25f ? l2 : fmaxf(l1, l2))) : (R - val) * (R - val);
-    }
-    float kl = 0.f;
-#pragma unroll
-    for (int j = 0; j < NA; ++j) {
-      const float dm = om[j] - mu[j];
-      const float t = logf(stdv[j] / os[j] + 1.0e-5f) + (os[j] * os[j] + dm * dm) / (2.f * (stdv[j] * stdv[j])) - 0.5f;
-      kl = j < p.A ? kl + t : kl;
-    }
-    v[2] += kl;
-    // backward (ppo_head_bwd_body)
-    const float w2 = 1.f - w1;
-    const float dratio = gs * (w1 * -a + w2 * -a * in);
-    const float dlogp = dratio * h.ratio;
-    float dmu[NA];
+    old_logp = p.old_logp[i];
+    adv = p.adv[i];
+    tv = p.clipped_value ? p.target_values[i] : 0.f;
+    R = p.returns[i];
+  }
+};
+
+template <int NA>
+__device__ __forceinline__ void head_fused_row(const lgx_ppo_head_args& p, const lgx_heads_s8_args& s, int i,
+                                               const float* stdv, const float* lstd, const float (&mu)[NA], float val,
+                                               const HeadIn<NA>& x, float gs, float gv, float (&v)[3 + 2 * NA + 1],
+                                               float (&dmu)[NA], float& dv) {
+  const float(&act)[NA] = x.act;
+  const float(&os)[NA] = x.os;
+  const float(&om)[NA] = x.om;
+  HeadRow h;
+  {
+    const float l2pi = 0.9189385332046727f;  // log(sqrt(2 pi)); head_row's arithmetic
+    float lp = 0.f;
 #pragma unroll
     for (int j = 0; j < NA; ++j) {
       const float d = act[j] - mu[j];
-      const float var = stdv[j] * stdv[j];
-      dmu[j] = j < p.A ? dlogp * d / var : 0.f;
-      if (j < p.A) {
-        if (p.dmu) p.dmu[(int64_t)i * p.A + j] = dmu[j];
-        v[3 + j] += dlogp * (d * d / (var * stdv[j]) - 1.f / stdv[j]);
-        v[3 + NA + j] += dmu[j];
-      }
+      const float t = -(d * d) / (2.f * stdv[j] * stdv[j]) - lstd[j] - l2pi;
+      lp = j < p.A ? lp + t : lp;
     }
-    float dv;
-    if (p.clipped_value) {
-      dv = gv * (u1 * 2.f * (val - R) + (1.f - u1) * 2.f * (vc - R) * inv);
-    } else {
-      dv = gv * 2.f * (val - R);
-    }
-    if (p.dvalue) p.dvalue[i] = dv;
-    v[3 + 2 * NA] += dv;
-    if (s.dmu_s8) {
+    h.logp = lp;
+    h.ratio = expf(lp - x.old_logp);
+  }
+  const float a = x.adv;
+  const float lo = 1.f - p.clip, hi = 1.f + p.clip;
+  // forward (ppo_head_fwd_body)
+  const float s1 = -a * h.ratio, s2 = -a * fminf(fmaxf(h.ratio, lo), hi);
+  const float R = x.R;
+  const float tv = p.clipped_value ? x.tv : val;
+  const float vc = p.clipped_value ? tv + fminf(fmaxf(val - tv, -p.clip), p.clip) : 0.f;
+  const float l1 = (val - R) * (val - R), l2 = (vc - R) * (vc - R);
+  // the discrete decisions (torch's gradient rules: max splits ties, clamp passes on [lo, hi])
+  float w1 = s1 > s2 ? 1.f : (s1 == s2 ? 0.5f : 0.f);
+  float in = (h.ratio >= lo && h.ratio <= hi) ? 1.f : 0.f;
+  float u1 = l1 > l2 ? 1.f : (l1 == l2 ? 0.5f : 0.f);
+  float inv = (val - tv >= -p.clip && val - tv <= p.clip) ? 1.f : 0.f;
+  if (s.decisions_out)
+    s.decisions_out[i] = (uint8_t)((unsigned)(2.f * w1) | ((unsigned)in << 2) | ((unsigned)(2.f * u1) << 3) |
+                                   ((unsigned)inv << 5));
+  // a decisions_in byte with bit 6 set leaves the row its own decisions (near-tie-only replays)
+  const bool forced = s.decisions_in != nullptr && !(s.decisions_in[i] & 0x40u);
+  if (forced) {
+    const unsigned d = s.decisions_in[i];
+    w1 = 0.5f * (float)(d & 3u);
+    in = (float)((d >> 2) & 1u);
+    u1 = 0.5f * (float)((d >> 3) & 3u);
+    inv = (float)((d >> 5) & 1u);
+  }
+  if (!forced) {
+    v[0] += fmaxf(s1, s2);
+    v[1] += p.clipped_value ? fmaxf(l1, l2) : (R - val) * (R - val);
+  } else {  // the forced branch's value (a tie: either)
+    v[0] += w1 > 0.75f ? s1 : (w1 < 0.25f ? s2 : fmaxf(s1, s2));
+    v[1] += p.clipped_value ? (u1 > 0.75f ? l1 : (u1 < 0.25f ? l2 : fmaxf(l1, l2))) : (R - val) * (R - val);
+  }
+  float kl = 0.f;
 #pragma unroll
-      for (int g0 = 0; g0 < NA; g0 += 8) {
-        if (g0 >= p.A) break;
-        float q[8];
+  for (int j = 0; j < NA; ++j) {
+    const float dm = om[j] - mu[j];
+    const float t = logf(stdv[j] / os[j] + 1.0e-5f) + (os[j] * os[j] + dm * dm) / (2.f * (stdv[j] * stdv[j])) - 0.5f;
+    kl = j < p.A ? kl + t : kl;
+  }
+  v[2] += kl;
+  // backward (ppo_head_bwd_body)
+  const float w2 = 1.f - w1;
+  const float dratio = gs * (w1 * -a + w2 * -a * in);
+  const float dlogp = dratio * h.ratio;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) q[e] = g0 + e < NA ? dmu[g0 + e] : 0.f;
-        store_s8_group(static_cast<char*>(s.dmu_s8) + ((int64_t)i * s.ld_dmu + g0) * 4, q);
-      }
-    }
-    if (s.dvalue_s8) {
-      const float q[8] = {dv, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      store_s8_group(static_cast<char*>(s.dvalue_s8) + (int64_t)i * s.ld_dvalue * 4, q);
+  for (int j = 0; j < NA; ++j) {
+    const float d = act[j] - mu[j];
+    const float var = stdv[j] * stdv[j];
+    dmu[j] = j < p.A ? dlogp * d / var : 0.f;
+    if (j < p.A) {
+      if (p.dmu) p.dmu[(int64_t)i * p.A + j] = dmu[j];
+      v[3 + j] += dlogp * (d * d / (var * stdv[j]) - 1.f / stdv[j]);
+      v[3 + NA + j] += dmu[j];
     }
   }
+  if (p.clipped_value) {
+    dv = gv * (u1 * 2.f * (val - R) + (1.f - u1) * 2.f * (vc - R) * inv);
+  } else {
+    dv = gv * 2.f * (val - R);
+  }
+  if (p.dvalue) p.dvalue[i] = dv;
+  v[3 + 2 * NA] += dv;
+  if (s.dmu_s8) {
+#pragma unroll
+    for (int g0 = 0; g0 < NA; g0 += 8) {
+      if (g0 >= p.A) break;
+      float q[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) q[e] = g0 + e < NA ? dmu[g0 + e] : 0.f;
+      store_s8_group(static_cast<char*>(s.dmu_s8) + ((int64_t)i * s.ld_dmu + g0) * 4, q);
+    }
+  }
+  if (s.dvalue_s8) {
+    const float q[8] = {dv, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    store_s8_group(static_cast<char*>(s.dvalue_s8) + (int64_t)i * s.ld_dvalue * 4, q);
+  }
+}
+
+// The fused PPO head's block partials (ws, the gradient column sums) and the last block's
+// totals: the losses, the KL, the entropy, dstd (one block per grid x-index)
+template <int NA>
+__device__ __forceinline__ void head_block_finish(const lgx_ppo_head_args& p, const lgx_heads_s8_args& s,
+                                                  float (&v)[3 + 2 * NA + 1], float* red, const float* stdv,
+                                                  const float* lstd, float ge) {
+  constexpr int NV = 3 + 2 * NA + 1;
   block_sum<NV>(v, red);
   if (threadIdx.x == 0) {
     for (int k = 0; k < 3; ++k) p.ws[blockIdx.x * (3 + HMAXA) + k] = v[k];
@@ -1500,10 +1525,39 @@ __device__ __forceinline__ void ppo_head_fused_body(const lgx_ppo_head_args& p, 
   }
 }
 
-__device__ __forceinline__ void aux_loss_fused_body(const lgx_aux_loss_args& p, const lgx_heads_s8_args& s) {
+template <int NA>
+__device__ __forceinline__ void ppo_head_fused_body(const lgx_ppo_head_args& p, const lgx_heads_s8_args& s) {
+  constexpr int NV = 3 + 2 * NA + 1;  // forward sums | dstd partial | dmu column sums | dvalue sum
+  __shared__ float red[4 * NV];
+  __shared__ float stdv[HMAXA], lstd[HMAXA];
+  if (threadIdx.x < HMAXA) {
+    const float sd = p.std[min((int)threadIdx.x, p.A - 1)];
+    stdv[threadIdx.x] = sd;
+    lstd[threadIdx.x] = logf(sd);
+  }
+  __syncthreads();
+  const float gs = p.g[0] / p.B, gv = p.g[1] / p.B, ge = p.g[2];
+  float v[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) v[k] = 0.f;
+  for (int i = blockIdx.x * HT + threadIdx.x; i < p.B; i += gridDim.x * HT) {
+    float mu[NA], dmu[NA], dv;
+    load_cols(p.mu, i, p.A, mu);
+    HeadIn<NA> x;
+    x.load(p, i);
+    head_fused_row<NA>(p, s, i, stdv, lstd, mu, p.value[i], x, gs, gv, v, dmu, dv);
+  }
+  head_block_finish<NA>(p, s, v, red, stdv, lstd, ge);
+}
+
+// nblk: the blocks that take part (blockIdx.x < nblk; 0: the grid's)
+// st: the row staging ([HT][AUX_CW + 1] floats of LDS)
+__device__ __forceinline__ void aux_loss_fused_core(const lgx_aux_loss_args& p, const lgx_heads_s8_args& s,
+                                                    unsigned nblk, float* st) {
+  const unsigned nb = nblk ? nblk : gridDim.x;
+  if (blockIdx.x >= nb) return;
   constexpr int NV = 2 + 8;  // forward sums | de column sums (E <= 8 on the S8 path)
   __shared__ float red[4 * NV];
-  __shared__ float st[HT * (AUX_CW + 1)];
   const int i0 = blockIdx.x * HT, i = i0 + threadIdx.x;
   const int64_t ic = min(i, p.B - 1);
   const float gr = p.g[0] / p.B, ge = p.g[1] / p.B;
@@ -1548,9 +1602,9 @@ __device__ __forceinline__ void aux_loss_fused_body(const lgx_aux_loss_args& p, 
     if (s.de_cs)
       for (int u = 0; u < p.E; ++u) s.de_cs[(int64_t)blockIdx.x * p.E + u] = v[2 + u];
   }
-  if (last_block(p.counter)) {
+  if (last_block(p.counter, nb)) {
     float t[2];
-    final_sum<2>(p.ws, 2, gridDim.x, t, red);
+    final_sum<2>(p.ws, 2, nb, t, red);
     if (threadIdx.x == 0) {
       p.out[0] = t[0] / p.B;
       p.out[1] = t[1] / p.B;
@@ -1559,10 +1613,318 @@ __device__ __forceinline__ void aux_loss_fused_body(const lgx_aux_loss_args& p, 
   }
 }
 
+__device__ __forceinline__ void aux_loss_fused_body(const lgx_aux_loss_args& p, const lgx_heads_s8_args& s) {
+  __shared__ float st[HT * (AUX_CW + 1)];
+  aux_loss_fused_core(p, s, 0, st);
+}
+
 template <int NA>
 __global__ __launch_bounds__(HT) void loss_heads_fused(lgx_ppo_head_args h, lgx_aux_loss_args a, lgx_heads_s8_args s) {
   if (blockIdx.y == 0) ppo_head_fused_body<NA>(h, s);
   else aux_loss_fused_body(a, s);
+}
+
+// ---- the PPO head with the actor's / critic's last layers around it (lgx_loss_heads_tail):
+// block = TR rows, 256 threads. LDS (dynamic, floats): the rows' hidden activations y, y_c
+// [TR][H + 4] (then, in place, the input gradients dy, dy_c), W [NA][H + 4], W_c [H_c + 4],
+// mu [TR][NA], value [TR], dmu [TR][NA], dvalue [TR].
+constexpr int TR = LGX_HEADS_TAIL_ROWS;
+// per-block phase clocks (dev builds only: -DLGX_TAIL_CLOCK, tools/tail_clock.py): thread 0 of
+// every PPO block writes clock64 deltas of its phases to g_tailclk[block][8]
+#ifdef LGX_TAIL_CLOCK
+__device__ uint32_t* g_tailclk = nullptr;
+#define TCK(q) do { if (tid == 0) { const uint64_t t_ = clock64(); ck[q] = (uint32_t)(t_ - ckl); ckl = t_; } } while (0)
+#else
+#define TCK(q) do { } while (0)
+#endif
+__host__ __device__ constexpr int tail_pitch(int h) { return h + 4; }
+__host__ __device__ inline size_t tail_lds_floats(int NA, int H, int Hc) {
+  return (size_t)TR * tail_pitch(H) + (size_t)TR * tail_pitch(Hc) + (size_t)NA * tail_pitch(H) + tail_pitch(Hc) +
+         2 * (size_t)TR * NA + 2 * TR;
+}
+
+// dot over k < n of two LDS rows (16-B aligned), k in order
+__device__ __forceinline__ float lds_dot(const float* x, const float* w, int n) {
+  float acc = 0.f;
+#pragma unroll 8
+  for (int k = 0; k < n; k += 4) {
+    const float4 a = *reinterpret_cast<const float4*>(x + k);
+    const float4 b = *reinterpret_cast<const float4*>(w + k);
+    acc = fmaf(a.x, b.x, acc);
+    acc = fmaf(a.y, b.y, acc);
+    acc = fmaf(a.z, b.z, acc);
+    acc = fmaf(a.w, b.w, acc);
+  }
+  return acc;
+}
+
+template <int NA>
+__device__ __forceinline__ void ppo_tail_body(const lgx_ppo_head_args& p, const lgx_heads_s8_args& s,
+                                              const lgx_heads_tail_args& t, int bx) {
+  constexpr int NV = 3 + 2 * NA + 1;
+  extern __shared__ __align__(16) float tl[];
+  __shared__ float stdv[HMAXA], lstd[HMAXA];
+  // the head rows' inputs (act | old_sigma | old_mu | old_logp adv tv R), later their sums
+  __shared__ float hin_[TR * (3 * NA + 4 > NV + 1 ? 3 * NA + 4 : NV + 1)];
+  float(*hin)[3 * NA + 4] = reinterpret_cast<float(*)[3 * NA + 4]>(hin_);
+  float(*vred)[NV + 1] = reinterpret_cast<float(*)[NV + 1]>(hin_);
+  const int H = t.H, Hc = t.Hc, PH = tail_pitch(H), PC = tail_pitch(Hc), A = p.A;
+  float* ys = tl;                   // [TR][PH]
+  float* yc = ys + TR * PH;         // [TR][PC]
+  float* Ws = yc + TR * PC;         // [NA][PH] (rows past A zero)
+  float* Wc = Ws + NA * PH;         // [PC]
+  float* mus = Wc + PC;             // [TR][NA]
+  float* vals = mus + TR * NA;      // [TR]
+  float* dmus = vals + TR;          // [TR][NA] (columns past A zero)
+  float* dvs = dmus + TR * NA;      // [TR]
+  const int r0 = bx * TR, tid = threadIdx.x;
+#ifdef LGX_TAIL_CLOCK
+  uint64_t ckl = clock64(), ck0 = ckl;
+  uint32_t ck[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
+  if (tid < HMAXA) {
+    const float sd = p.std[min(tid, A - 1)];
+    stdv[tid] = sd;
+    lstd[tid] = logf(sd);
+  }
+  // every global input of the block, by all threads: all requests first (registers), then the
+  // LDS writes — one memory round trip instead of one per loop
+  typedef unsigned u4 __attribute__((ext_vector_type(4)));
+  constexpr int YS = TR * 32 / 256;     // S8 groups per thread and network (H <= 256)
+  constexpr int WS = HMAXA * 256 / 256;  // weight elements per thread (A <= 16, H <= 256)
+  constexpr int IS = TR * (3 * NA + 4) / 256 + 1;
+  u4 yh[2][YS], yl[2][YS];
+  float wv[WS], wcv, iv[IS];
+#pragma unroll
+  for (int n = 0; n < 2; ++n) {
+    const int G = (n ? Hc : H) / 8;
+    const char* src = static_cast<const char*>(n ? t.yc : t.y);
+    const int64_t ld = n ? t.ld_yc : t.ld_y;
+#pragma unroll
+    for (int q = 0; q < YS; ++q) {
+      const int it = tid + 256 * q, r = it / G, g = it % G;
+      const bool ok = it < TR * G && r0 + r < p.B;
+      const u4* gp = reinterpret_cast<const u4*>(src + ((int64_t)min(r0 + r, p.B - 1) * ld + 8 * g) * 4);
+      yh[n][q] = ok ? gp[0] : u4{0u, 0u, 0u, 0u};
+      yl[n][q] = ok ? gp[1] : u4{0u, 0u, 0u, 0u};
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < WS; ++q) {
+    const int it = tid + 256 * q, a = it / H;
+    wv[q] = a < A ? t.W[min(it, A * H - 1)] : 0.f;
+  }
+  wcv = t.Wc[min(tid, Hc - 1)];
+#pragma unroll
+  for (int q = 0; q < IS; ++q) {
+    const int it = tid + 256 * q, r = it / (3 * NA + 4), c = it % (3 * NA + 4);
+    const int i = min(r0 + min(r, TR - 1), p.B - 1);
+    float x;
+    if (c < 3 * NA) {
+      const int qq = c / NA, j = c % NA;
+      const float* src = qq == 0 ? p.actions : (qq == 1 ? p.old_sigma : p.old_mu);
+      x = src[(int64_t)i * A + min(j, A - 1)];
+    } else if (c == 3 * NA) {
+      x = p.old_logp[i];
+    } else if (c == 3 * NA + 1) {
+      x = p.adv[i];
+    } else if (c == 3 * NA + 2) {
+      x = p.clipped_value ? p.target_values[i] : 0.f;
+    } else {
+      x = p.returns[i];
+    }
+    iv[q] = x;
+  }
+#pragma unroll
+  for (int n = 0; n < 2; ++n) {
+    const int G = (n ? Hc : H) / 8, P = n ? PC : PH;
+    float* dst = n ? yc : ys;
+#pragma unroll
+    for (int q = 0; q < YS; ++q) {
+      const int it = tid + 256 * q, r = it / G, g = it % G;
+      if (it >= TR * G) continue;
+      const u4 Hh = yh[n][q], Ll = yl[n][q];
+      *reinterpret_cast<float4*>(dst + r * P + 8 * g) =
+          float4{__uint_as_float(Hh[0] << 16) + __uint_as_float(Ll[0] << 16),
+                 __uint_as_float(Hh[0] & 0xffff0000u) + __uint_as_float(Ll[0] & 0xffff0000u),
+                 __uint_as_float(Hh[1] << 16) + __uint_as_float(Ll[1] << 16),
+                 __uint_as_float(Hh[1] & 0xffff0000u) + __uint_as_float(Ll[1] & 0xffff0000u)};
+      *reinterpret_cast<float4*>(dst + r * P + 8 * g + 4) =
+          float4{__uint_as_float(Hh[2] << 16) + __uint_as_float(Ll[2] << 16),
+                 __uint_as_float(Hh[2] & 0xffff0000u) + __uint_as_float(Ll[2] & 0xffff0000u),
+                 __uint_as_float(Hh[3] << 16) + __uint_as_float(Ll[3] << 16),
+                 __uint_as_float(Hh[3] & 0xffff0000u) + __uint_as_float(Ll[3] & 0xffff0000u)};
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < WS; ++q) {
+    const int it = tid + 256 * q, a = it / H, k = it % H;
+    if (a < NA) Ws[a * PH + k] = wv[q];
+  }
+  if (tid < Hc) Wc[tid] = wcv;
+#pragma unroll
+  for (int q = 0; q < IS; ++q) {
+    const int it = tid + 256 * q, r = it / (3 * NA + 4), c = it % (3 * NA + 4);
+    if (r < TR) hin[r][c] = iv[q];
+  }
+  __syncthreads();
+  TCK(0);
+  // the last layers' forward: TR x A actor outputs, then TR values (k in order)
+  for (int o = tid; o < TR * A + TR; o += blockDim.x) {
+    if (o < TR * A) {
+      const int r = o / A, a = o % A;
+      const float m = lds_dot(ys + r * PH, Ws + a * PH, H) + t.b[a];
+      mus[r * NA + a] = m;
+      if (t.mu_out && r0 + r < p.B) t.mu_out[(int64_t)(r0 + r) * A + a] = m;
+    } else {
+      const int r = o - TR * A;
+      const float v = lds_dot(yc + r * PC, Wc, Hc) + t.bc[0];
+      vals[r] = v;
+      if (t.value_out && r0 + r < p.B) t.value_out[r0 + r] = v;
+    }
+  }
+  __syncthreads();
+  TCK(1);
+  const float gs = p.g[0] / p.B, gv = p.g[1] / p.B, ge = p.g[2];
+  float v[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) v[k] = 0.f;
+  if (tid < TR) {
+    float dmu[NA], dv = 0.f;
+#pragma unroll
+    for (int j = 0; j < NA; ++j) dmu[j] = 0.f;
+    const int i = r0 + tid;
+    if (i < p.B) {
+      float mu[NA];
+      HeadIn<NA> x;
+#pragma unroll
+      for (int j = 0; j < NA; ++j) {
+        mu[j] = mus[tid * NA + min(j, A - 1)];  // load_cols' clamped columns
+        x.act[j] = hin[tid][j];
+        x.os[j] = hin[tid][NA + j];
+        x.om[j] = hin[tid][2 * NA + j];
+      }
+      x.old_logp = hin[tid][3 * NA];
+      x.adv = hin[tid][3 * NA + 1];
+      x.tv = hin[tid][3 * NA + 2];
+      x.R = hin[tid][3 * NA + 3];
+      head_fused_row<NA>(p, s, i, stdv, lstd, mu, vals[tid], x, gs, gv, v, dmu, dv);
+    }
+#pragma unroll
+    for (int j = 0; j < NA; ++j) dmus[tid * NA + j] = j < A ? dmu[j] : 0.f;
+    dvs[tid] = dv;
+  }
+  __syncthreads();
+  TCK(2);
+  // the last layers' input gradients, in place of y / y_c: (dmu W) * ELU'(y), (dvalue W_c) * ELU'(y_c)
+  {
+    const int G = H / 8, Gc = Hc / 8;
+    for (int it = tid; it < TR * (G + Gc); it += blockDim.x) {
+      const bool critic = it >= TR * G;
+      const int jt = critic ? it - TR * G : it;
+      const int gg = critic ? Gc : G;
+      const int r = jt / gg, q = jt % gg;
+      float* y = critic ? yc + r * PC + 8 * q : ys + r * PH + 8 * q;
+      float x[8];
+      if (critic) {
+        const float d = dvs[r];
+        const float4 w0 = *reinterpret_cast<const float4*>(Wc + 8 * q);
+        const float4 w1 = *reinterpret_cast<const float4*>(Wc + 8 * q + 4);
+        x[0] = d * w0.x; x[1] = d * w0.y; x[2] = d * w0.z; x[3] = d * w0.w;
+        x[4] = d * w1.x; x[5] = d * w1.y; x[6] = d * w1.z; x[7] = d * w1.w;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) x[e] = 0.f;
+#pragma unroll
+        for (int a = 0; a < NA; ++a) {  // a in order; rows past A are zero
+          const float d = dmus[r * NA + a];
+          const float4 w0 = *reinterpret_cast<const float4*>(Ws + a * PH + 8 * q);
+          const float4 w1 = *reinterpret_cast<const float4*>(Ws + a * PH + 8 * q + 4);
+          x[0] = fmaf(d, w0.x, x[0]); x[1] = fmaf(d, w0.y, x[1]); x[2] = fmaf(d, w0.z, x[2]);
+          x[3] = fmaf(d, w0.w, x[3]); x[4] = fmaf(d, w1.x, x[4]); x[5] = fmaf(d, w1.y, x[5]);
+          x[6] = fmaf(d, w1.z, x[6]); x[7] = fmaf(d, w1.w, x[7]);
+        }
+      }
+      const float4 y0 = *reinterpret_cast<const float4*>(y);
+      const float4 y1 = *reinterpret_cast<const float4*>(y + 4);
+      const float yy[8] = {y0.x, y0.y, y0.z, y0.w, y1.x, y1.y, y1.z, y1.w};
+      float d[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) d[e] = x[e] * (yy[e] > 0.f ? 1.f : yy[e] + 1.f);
+      *reinterpret_cast<float4*>(y) = {d[0], d[1], d[2], d[3]};
+      *reinterpret_cast<float4*>(y + 4) = {d[4], d[5], d[6], d[7]};
+      if (r0 + r < p.B) {
+        if (critic) store_s8_group(static_cast<char*>(t.dyc) + ((int64_t)(r0 + r) * t.ld_dyc + 8 * q) * 4, d);
+        else store_s8_group(static_cast<char*>(t.dy) + ((int64_t)(r0 + r) * t.ld_dy + 8 * q) * 4, d);
+      }
+    }
+  }
+  __syncthreads();
+  TCK(3);
+  // their column sums over the block's rows (rows past B hold zeros), rows in order
+  for (int o = tid; o < H + Hc; o += blockDim.x) {
+    const bool critic = o >= H;
+    const int k = critic ? o - H : o;
+    float* cs = critic ? t.dyc_cs : t.dy_cs;
+    if (!cs) continue;
+    const float* y = critic ? yc : ys;
+    const int P = critic ? PC : PH;
+    float sum = 0.f;
+#pragma unroll 8
+    for (int r = 0; r < TR; ++r) sum += y[r * P + k];
+    cs[(int64_t)bx * (critic ? Hc : H) + k] = sum;
+  }
+  // the block's partials only — no last-block pass (an agent-scope fence per block costs the L2's
+  // write-back: ~1 us each): ws[b] = {surr / B, vloss / B, kl / B, dstd partial [A]}, block 0's
+  // dstd partial with the entropy term ge / std; the launch's totals are flat sums of these
+  // (lgx_s8_reduce jobs of the caller). Block 0 writes the entropy (a constant) into out[2].
+  TCK(4);
+  // the block's sums: only the TR head threads hold values; rows through LDS, summed in row order
+  if (tid < TR)
+#pragma unroll
+    for (int k = 0; k < NV; ++k) vred[tid][k] = v[k];
+  __syncthreads();
+  if (tid < NV) {
+    float sum = 0.f;
+    for (int q = 0; q < TR; ++q) sum += vred[q][tid];
+    const float inv = 1.f / p.B;
+    float* w = p.ws + (int64_t)bx * (3 + HMAXA);
+    if (tid < 3) w[tid] = sum * inv;
+    else if (tid < 3 + NA) {
+      const int j = tid - 3;
+      if (j < A) w[3 + j] = sum + (bx == 0 ? ge / stdv[j] : 0.f);
+    } else if (tid < 3 + 2 * NA) {
+      const int j = tid - 3 - NA;
+      if (s.dmu_cs && j < A) s.dmu_cs[(int64_t)bx * A + j] = sum;
+    } else if (s.dvalue_cs) {
+      s.dvalue_cs[bx] = sum;
+    }
+  }
+  TCK(5);
+  if (tid == 0) {
+    if (bx == 0) {
+      float ent = 0.f;
+      for (int j = 0; j < A; ++j) ent += 0.5f + 0.9189385332046727f + lstd[j];
+      p.out[2] = ent;
+    }
+  }
+#ifdef LGX_TAIL_CLOCK
+  if (tid == 0 && g_tailclk) {
+    ck[6] = (uint32_t)(clock64() - ck0);
+    for (int q = 0; q < 7; ++q) g_tailclk[(size_t)bx * 8 + q] = ck[q];
+  }
+#endif
+}
+
+// one grid: blocks [0, naux) the aux head's 256-row blocks (first, so that they run beside the
+// PPO head's blocks rather than after them), then the PPO head's TR-row blocks
+template <int NA>
+__global__ __launch_bounds__(256) void loss_heads_tail(lgx_ppo_head_args h, lgx_aux_loss_args a, lgx_heads_s8_args s,
+                                                       lgx_heads_tail_args t) {
+  const int naux = (int)head_grid(a.B);
+  extern __shared__ __align__(16) float tl[];
+  if ((int)blockIdx.x < naux) aux_loss_fused_core(a, s, naux, tl);  // staging in the dynamic LDS
+  else ppo_tail_body<NA>(h, s, t, (int)blockIdx.x - naux);
 }
 
 // ---------------------------------------------------------------- PPO minibatch optimizer tail
@@ -2111,6 +2473,56 @@ int32_t lgx_loss_heads_fused(const lgx_ppo_head_args* h, const lgx_aux_loss_args
     return fail("lgx_loss_heads_fused: S8 destinations must be 16-B aligned");
   hipLaunchKernelGGL(h->A <= 12 ? lgxm::loss_heads_fused<12> : lgxm::loss_heads_fused<lgxm::HMAXA>,
                      dim3(lgxm::head_grid(h->B), 2), dim3(lgxm::HT), 0, static_cast<hipStream_t>(stream), *h, *a, *s);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : fail(hipGetErrorString(e));
+}
+
+#ifdef LGX_TAIL_CLOCK
+int32_t lgx_tail_set_clock(void* buf) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(lgxm::g_tailclk), &buf, sizeof(void*)) == hipSuccess ? 0 : -1;
+}
+#endif
+int32_t lgx_loss_heads_tail(const lgx_ppo_head_args* h, const lgx_aux_loss_args* a, const lgx_heads_s8_args* s,
+                            const lgx_heads_tail_args* t, void* stream) {
+  if (!h || !t || !s) return fail("lgx_loss_heads_tail: null arguments");
+  if (h->B < 1 || h->A < 1 || h->A > lgxm::HMAXA || !h->std || !h->actions || !h->old_logp || !h->adv ||
+      !h->returns || (h->clipped_value && !h->target_values) || !h->ws || !h->counter)
+    return fail("lgx_loss_heads_tail: bad head arguments");
+  if (!h->out || !h->old_mu || !h->old_sigma || !h->g || !h->dstd)
+    return fail("lgx_loss_heads_tail: null out/old_mu/old_sigma/g/dstd");
+  if (!a || a->B != h->B || a->L < 1 || a->E < 1 || !a->p || !a->a || !a->e || !a->t || !a->out || !a->ws ||
+      !a->counter || !a->g || !a->dp)
+    return fail("lgx_loss_heads_tail: bad aux arguments");
+  if ((!h->dmu && !s->dmu_s8) || (!h->dvalue && !s->dvalue_s8) || (!a->de && !s->de_s8))
+    return fail("lgx_loss_heads_tail: dmu / dvalue / de need an fp32 or an S8 destination");
+  if (a->E > 8) return fail("lgx_loss_heads_tail: E <= 8");
+  if (s->de_cs && lgxm::HT != 256) return fail("lgx_loss_heads_tail: de column sums need LGX_HT 256");
+  if ((s->dmu_s8 && (s->ld_dmu % 8 || s->ld_dmu < (h->A + 7) / 8 * 8)) || (s->dvalue_s8 && s->ld_dvalue % 8) ||
+      (s->de_s8 && s->ld_de % 8))
+    return fail("lgx_loss_heads_tail: S8 pitches are multiples of 8 covering the columns");
+  if (t->H < 8 || t->H > 256 || t->H % 8 || t->Hc < 8 || t->Hc > 256 || t->Hc % 8 || !t->y || !t->W || !t->b ||
+      !t->dy || !t->yc || !t->Wc || !t->bc || !t->dyc || t->ld_y % 8 || t->ld_y < t->H || t->ld_yc % 8 ||
+      t->ld_yc < t->Hc || t->ld_dy % 8 || t->ld_dy < t->H || t->ld_dyc % 8 || t->ld_dyc < t->Hc)
+    return fail("lgx_loss_heads_tail: bad tail arguments (H, H_c multiples of 8 in [8, 256]; S8 pitches)");
+  if ((((uintptr_t)s->dmu_s8) | ((uintptr_t)s->dvalue_s8) | ((uintptr_t)s->de_s8) | ((uintptr_t)t->y) |
+       ((uintptr_t)t->yc) | ((uintptr_t)t->dy) | ((uintptr_t)t->dyc)) & 15)
+    return fail("lgx_loss_heads_tail: S8 operands must be 16-B aligned");
+  const int na = h->A <= 12 ? 12 : lgxm::HMAXA;
+  const size_t lds = std::max(lgxm::tail_lds_floats(na, t->H, t->Hc), (size_t)lgxm::HT * (lgxm::AUX_CW + 1)) *
+                     sizeof(float);
+  const unsigned nb = (unsigned)((h->B + lgxm::TR - 1) / lgxm::TR);
+  auto* k = h->A <= 12 ? lgxm::loss_heads_tail<12> : lgxm::loss_heads_tail<lgxm::HMAXA>;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)lgxm::loss_heads_tail<12>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lgxm::tail_lds_floats(12, 256, 256) * 4);
+    (void)hipFuncSetAttribute((const void*)lgxm::loss_heads_tail<lgxm::HMAXA>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lgxm::tail_lds_floats(lgxm::HMAXA, 256, 256) * 4);
+    attr = true;
+  }
+  hipLaunchKernelGGL(k, dim3(nb + lgxm::head_grid(h->B)), dim3(256), lds, static_cast<hipStream_t>(stream), *h, *a, *s,
+                     *t);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : fail(hipGetErrorString(e));
 }

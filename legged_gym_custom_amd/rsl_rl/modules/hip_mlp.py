@@ -20,7 +20,7 @@ import torch.nn as nn
 _LIB_PATH = os.environ.get("LGX_MLP_LIB") or os.path.join(
     os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))), "lib", "liblgx_mlp.so")
 _lib = None
-ABI_VERSION = 8
+ABI_VERSION = 9
 EPI_BIAS, EPI_ELU, EPI_DELU, EPI_ACCUM = 1, 2, 4, 8
 EXPORTED = ["lgx_mlp_abi_version", "lgx_mlp_sizeof_gemm_args", "lgx_mlp_pick_split", "lgx_gemm",
             "lgx_mlp_last_error", "lgx_adam_step", "lgx_ppo_head_forward", "lgx_ppo_head_backward",
@@ -28,7 +28,8 @@ EXPORTED = ["lgx_mlp_abi_version", "lgx_mlp_sizeof_gemm_args", "lgx_mlp_pick_spl
             "lgx_aux_loss_forward", "lgx_aux_loss_backward", "lgx_ppo_tail", "lgx_gemm_group",
             "lgx_mlp_pick_split_group", "lgx_gae", "lgx_normalize_advantages",
             "lgx_gather_rows", "lgx_transpose_batch", "lgx_loss_heads_forward", "lgx_loss_heads_backward",
-            "lgx_track_episodes", "lgx_chain", "lgx_adaptation_forward", "lgx_loss_heads_fused"]
+            "lgx_track_episodes", "lgx_chain", "lgx_adaptation_forward", "lgx_loss_heads_fused",
+            "lgx_loss_heads_tail"]
 TAIL_MAX_LOSSES = 8
 COPY_MAX = 16
 SPLITK_MAX = 24
@@ -85,6 +86,19 @@ class HeadsS8Args(C.Structure):
                 ("dvalue_s8", C.c_void_p), ("ld_dvalue", C.c_int64), ("dvalue_cs", C.c_void_p),
                 ("de_s8", C.c_void_p), ("ld_de", C.c_int64), ("de_cs", C.c_void_p),
                 ("decisions_in", C.c_void_p), ("decisions_out", C.c_void_p)]
+
+
+class HeadsTailArgs(C.Structure):
+    """Mirror of lgx_heads_tail_args (ABI 9: the actor's / critic's last layers fused around the
+    PPO head; pitches in S8 elements)."""
+    _fields_ = [("y", C.c_void_p), ("ld_y", C.c_int64), ("W", C.c_void_p), ("b", C.c_void_p),
+                ("dy", C.c_void_p), ("ld_dy", C.c_int64), ("dy_cs", C.c_void_p),
+                ("yc", C.c_void_p), ("ld_yc", C.c_int64), ("Wc", C.c_void_p), ("bc", C.c_void_p),
+                ("dyc", C.c_void_p), ("ld_dyc", C.c_int64), ("dyc_cs", C.c_void_p),
+                ("mu_out", C.c_void_p), ("value_out", C.c_void_p), ("H", C.c_int32), ("Hc", C.c_int32)]
+
+
+HEADS_TAIL_ROWS = 32  # LGX_HEADS_TAIL_ROWS: rows of one column-sum partial of lgx_loss_heads_tail
 
 
 class TailArgs(C.Structure):
@@ -197,6 +211,8 @@ def lib():
         getattr(L, fn).restype = C.c_int32
     L.lgx_loss_heads_fused.argtypes = [vp, vp, vp, vp]
     L.lgx_loss_heads_fused.restype = C.c_int32
+    L.lgx_loss_heads_tail.argtypes = [vp, vp, vp, vp, vp]
+    L.lgx_loss_heads_tail.restype = C.c_int32
     for fn in ("lgx_aux_loss_forward", "lgx_aux_loss_backward", "lgx_ppo_tail"):
         getattr(L, fn).argtypes = [vp, vp]
         getattr(L, fn).restype = C.c_int32

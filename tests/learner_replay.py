@@ -163,11 +163,13 @@ def effective_mismatch(ref, got):
     return np.flatnonzero((ref & mask) != (got & mask))
 
 
-def run_per_minibatch(case, device, d, force=True):
+def run_per_minibatch(case, device, d, force=True, near_only=False):
     """The fixture's sequence with the update run eagerly minibatch by minibatch: with `force`, the
     PPO head takes every per-sample discrete decision (ratio clip, surrogate / value max) from
     the reference run's record (d["mb<k>.decisions"]), so the trajectory follows the reference's
-    branch at every sample; the launch also records its OWN decisions. Returns per minibatch the
+    branch at every sample — with `near_only`, only at the samples the reference records within
+    LC.NEAR_TIE of a boundary (all others are the head's own); the launch also records its OWN
+    decisions. Returns per minibatch the
     sampled pre-clip gradients (+ fp64 sums), both pre-clip norms and the own decisions, and the
     end state (parameters, Adam moments)."""
     alg = build(case, device, use_graphs=False)
@@ -184,7 +186,15 @@ def run_per_minibatch(case, device, d, force=True):
     mb = perm1.numel() // alg.num_mini_batches
     dec_in = None
     if force:
-        dec_in = torch.stack([torch.from_numpy(d[f"mb{k}.decisions"]) for k in range(n_mb)]).to(device)
+        rows = []
+        for k in range(n_mb):
+            dk = d[f"mb{k}.decisions"].copy()
+            if near_only:  # replay only the samples within NEAR_TIE of a boundary; the rest decide freely
+                keep = np.zeros(dk.size, bool)
+                keep[d[f"mb{k}.near"]] = True
+                dk[~keep] = 0x40
+            rows.append(torch.from_numpy(dk))
+        dec_in = torch.stack(rows).to(device)
     dec_out = torch.zeros(n_mb, mb, dtype=torch.uint8, device=device)
     alg._decisions = {"k": 0, "in": dec_in, "out": dec_out}
     grads, norms = [], []

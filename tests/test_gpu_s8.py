@@ -464,3 +464,90 @@ def test_reduce_long_sums_one_wave_per_output(S):
     S.reduce(jobs)
     torch.cuda.synchronize()
     assert all(torch.equal(a, o) for a, (_, o) in zip(first, refs))
+
+
+@pytest.mark.parametrize("B,H,Hc", [(3000, 128, 128), (777, 64, 256)])
+def test_loss_heads_tail_equals_last_layers_and_fused_heads(S, B, H, Hc):
+    """lgx_loss_heads_tail (the actor's / critic's last layers fused around the PPO head, lgx_mlp
+    ABI 9) against its parts: mu = y W^T + b and value = y_c W_c^T + b_c against fp64 on the
+    same S8 values (|err| <= 1e-5 sum|y w| + 1e-6); lgx_loss_heads_fused fed those mu / value
+    gives the same per-row gradients (dmu, dvalue, their S8 splits, the latent and estimator
+    gradients) bit for bit, and the per-block rows it leaves in ws sum to the same losses and dstd
+    to fp32 rounding (another block partition);
+    the hidden layers' input gradients (dmu W) * ELU'(y) and (dvalue W_c) * ELU'(y_c) against
+    fp64 and their 32-row column sums."""
+    from legged_gym_custom_amd.rsl_rl.modules import hip_mlp as H_
+    g = torch.Generator(device=dev).manual_seed(B + H)
+    A, L, E = 12, 20, 3
+    r = lambda *s: torch.randn(*s, device=dev, generator=g)  # noqa: E731
+    y8 = S.to_s8_torch(torch.nn.functional.elu(r(B, H)))
+    yc8 = S.to_s8_torch(torch.nn.functional.elu(r(B, Hc)))
+    yv, ycv = S.from_s8(y8, B, H).double(), S.from_s8(yc8, B, Hc).double()
+    W, b, Wc, bc = 0.1 * r(A, H), r(A), 0.1 * r(1, Hc), r(1)
+    std = r(A).abs() + 0.5
+    actions, old_logp, adv, tv, ret = r(B, A), r(B, 1), r(B, 1), r(B, 1), r(B, 1)
+    old_mu, old_sigma = r(B, A), r(B, A).abs() + 0.5
+    p_lat, a_lat, pred, t_est = r(B, L), r(B, L), r(B, E), r(B, E)
+    seeds = torch.tensor([1.0, 1.3, -0.01, 0.05, 1.0], device=dev)
+    nt, nblk = (B + 31) // 32, (B + 255) // 256
+    z = lambda *s: torch.full(s, float("nan"), device=dev)  # noqa: E731
+
+    def run(tail, mu=None, value=None):
+        o = dict(ws=torch.zeros(19 * nt, device=dev), wsa=torch.zeros(2 * nt, device=dev), out=z(8), out_aux=z(2),
+                 dmu=z(B, A), dvalue=z(B), dstd=z(A), dp=z(B, L), de=z(B, E),
+                 cnt=torch.zeros(1, dtype=torch.int32, device=dev), cnta=torch.zeros(1, dtype=torch.int32, device=dev),
+                 dmu8=S.empty(B, A, dev), dv8=S.empty(B, 1, dev), de8=S.empty(B, E, dev),
+                 cs_mu=z(nt if tail else nblk, A), cs_v=z(nt if tail else nblk, 1), cs_e=z(nblk, E),
+                 mu=z(B, A) if mu is None else mu, value=z(B, 1) if value is None else value)
+        h = H_.HeadArgs(mu=o["mu"].data_ptr(), value=o["value"].data_ptr(), std=std.data_ptr(),
+                        actions=actions.data_ptr(), old_logp=old_logp.data_ptr(), adv=adv.data_ptr(),
+                        target_values=tv.data_ptr(), returns=ret.data_ptr(), old_mu=old_mu.data_ptr(),
+                        old_sigma=old_sigma.data_ptr(), B=B, A=A, clip=0.2, clipped_value=1, out=o["out"].data_ptr(),
+                        g=seeds.data_ptr(), dmu=o["dmu"].data_ptr(), dvalue=o["dvalue"].data_ptr(),
+                        dstd=o["dstd"].data_ptr(), ws=o["ws"].data_ptr(), counter=o["cnt"].data_ptr(),
+                        accumulate_dstd=0)
+        x = H_.AuxArgs(p=p_lat.data_ptr(), a=a_lat.data_ptr(), L=L, e=pred.data_ptr(), t=t_est.data_ptr(), E=E, B=B,
+                       out=o["out_aux"].data_ptr(), g=seeds.data_ptr() + 12, dp=o["dp"].data_ptr(),
+                       de=o["de"].data_ptr(), ws=o["wsa"].data_ptr(), counter=o["cnta"].data_ptr(), ld_p=L)
+        s8 = H_.HeadsS8Args(dmu_s8=o["dmu8"].data_ptr(), ld_dmu=o["dmu8"].shape[1], dmu_cs=o["cs_mu"].data_ptr(),
+                            dvalue_s8=o["dv8"].data_ptr(), ld_dvalue=o["dv8"].shape[1], dvalue_cs=o["cs_v"].data_ptr(),
+                            de_s8=o["de8"].data_ptr(), ld_de=o["de8"].shape[1], de_cs=o["cs_e"].data_ptr())
+        if tail:
+            o.update(dy8=S.empty(B, H, dev), dyc8=S.empty(B, Hc, dev), cs_y=z(nt, H), cs_yc=z(nt, Hc))
+            t = H_.HeadsTailArgs(y=y8.data_ptr(), ld_y=y8.shape[1], W=W.data_ptr(), b=b.data_ptr(),
+                                 dy=o["dy8"].data_ptr(), ld_dy=o["dy8"].shape[1], dy_cs=o["cs_y"].data_ptr(),
+                                 yc=yc8.data_ptr(), ld_yc=yc8.shape[1], Wc=Wc.data_ptr(), bc=bc.data_ptr(),
+                                 dyc=o["dyc8"].data_ptr(), ld_dyc=o["dyc8"].shape[1], dyc_cs=o["cs_yc"].data_ptr(),
+                                 mu_out=o["mu"].data_ptr(), value_out=o["value"].data_ptr(), H=H, Hc=Hc)
+            H_._check(H_.lib().lgx_loss_heads_tail(H_.C.byref(h), H_.C.byref(x), H_.C.byref(s8), H_.C.byref(t),
+                                                   H_._stream()), "tail")
+        else:
+            H_._check(H_.lib().lgx_loss_heads_fused(H_.C.byref(h), H_.C.byref(x), H_.C.byref(s8), H_._stream()),
+                      "fused")
+        torch.cuda.synchronize()
+        return o
+
+    got = run(True)
+    mu_ref = yv @ W.double().t() + b.double()
+    v_ref = ycv @ Wc.double().t() + bc.double()
+    assert (got["mu"].double() - mu_ref).abs().le(1e-5 * (yv.abs() @ W.double().abs().t()) + 1e-6).all()
+    assert (got["value"].double() - v_ref).abs().le(1e-5 * (ycv.abs() @ Wc.double().abs().t()) + 1e-6).all()
+    ref = run(False, mu=got["mu"].clone(), value=got["value"].clone())
+    for k in ("dmu", "dvalue", "dp", "de", "dmu8", "dv8", "de8", "cs_e", "out_aux"):
+        assert torch.equal(got[k], ref[k]), k
+    # the head's totals are the caller's flat sums of the per-block rows (no last-block pass)
+    rows = got["ws"].view(-1, 19)[:nt].double()
+    assert torch.equal(got["out"][2], ref["out"][2])  # the entropy, written by block 0
+    torch.testing.assert_close(rows[:, :3].sum(0), ref["out"][[0, 1, 3]].double(), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(rows[:, 3:3 + A].sum(0), ref["dstd"].double(), rtol=1e-5, atol=1e-6)
+    dmu, dv = got["dmu"].double(), got["dvalue"].double().view(B, 1)
+    for dy8, yy, WW, dd, cs, n in ((got["dy8"], yv, W, dmu, got["cs_y"], H), (got["dyc8"], ycv, Wc, dv, got["cs_yc"], Hc)):
+        ref_dy = (dd @ WW.double()) * torch.where(yy > 0, torch.ones_like(yy), yy + 1.0)
+        got_dy = S.from_s8(dy8, B, n).double()
+        bound = 1e-5 * ((dd.abs() @ WW.double().abs()) * (yy.abs() + 1)) + 1e-6
+        assert (got_dy - ref_dy).abs().le(bound).all(), float((got_dy - ref_dy).abs().max())
+        blocks = torch.stack([ref_dy[i:i + 32].sum(0) for i in range(0, B, 32)])
+        torch.testing.assert_close(cs.double(), blocks, rtol=1e-4, atol=1e-5)
+    for cs, full in ((got["cs_mu"], dmu), (got["cs_v"], dv)):
+        blocks = torch.stack([full[i:i + 32].sum(0) for i in range(0, B, 32)])
+        torch.testing.assert_close(cs.double(), blocks, rtol=1e-5, atol=1e-6)
