@@ -279,8 +279,9 @@ int32_t lgx_loss_heads_tail(const lgx_ppo_head_args* head, const lgx_aux_loss_ar
  *   Adam(main segment, (float) lr, coef_m)                      optimizer.step()
  *   sums[i] += *loss_ptrs[i] (i < nloss)                        loss bookkeeping
  * Adam arithmetic as lgx_adam_step; step_main / step_est are incremented here. Norms are
- * block partials summed in block order (deterministic). ws >= 2 * 512 floats + 8; counter:
- * one zero-initialised uint32 (left at zero). */
+ * block partials summed in block order (deterministic): the first launch writes them, every
+ * block of the second sums them (no last-block pass). ws >= 2 * 512 floats + 8; counter:
+ * unused (kept for the layout). */
 #define LGX_TAIL_MAX_LOSSES 8
 typedef struct lgx_ppo_tail_args {
   float* grads; float* params; float* exp_avg; float* exp_avg_sq;

@@ -1966,8 +1966,10 @@ __device__ __forceinline__ float sumsq_range(const float* __restrict__ g, int64_
   return (s0 + s1) + (s2 + s3);
 }
 
-// grid TAIL_BLOCKS: squared norms (estimator; main + adaptation) -> the last block turns
-// them into clip coefficients, runs the KL schedule, bumps the Adam steps and the loss sums
+// grid TAIL_BLOCKS: squared norms (estimator; main + adaptation) as block partials; block 0 also
+// runs the KL schedule, bumps the Adam steps and the loss sums (none of which needs the norms).
+// No last-block pass (an agent-scope fence per block costs an L2 write-back, ~1 us each): every
+// tail_adam block sums the partials itself, in one fixed order, after the launch boundary.
 __global__ __launch_bounds__(256) void tail_norms(lgx_ppo_tail_args p) {
   __shared__ float red[4 * 2];
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -1977,26 +1979,19 @@ __global__ __launch_bounds__(256) void tail_norms(lgx_ppo_tail_args p) {
   v[1] = sumsq_range(p.grads, p.main_lo, p.main_hi, i0, stride) + sumsq_range(p.grads, p.adapt_lo, p.adapt_hi, i0, stride);
   block_sum<2>(v, red);
   if (threadIdx.x == 0) { p.ws[blockIdx.x * 2] = v[0]; p.ws[blockIdx.x * 2 + 1] = v[1]; }
-  if (last_block(p.counter)) {
-    float t[2];
-    final_sum<2>(p.ws, 2, gridDim.x, t, red);
+  if (blockIdx.x == 0) {
     // the scalar bookkeeping on separate threads (each one dependent memory round trip,
     // not one thread's serial chain of loads behind possibly-aliasing stores)
     const int tid = threadIdx.x;
     if (tid == 0) {
-      const float se = t[0], sm = t[1];
-      const double kl = p.kl_index >= 0 ? (double)p.grads[p.kl_index] : 0.0;
-      double lr = p.kl_index >= 0 ? *p.lr64 : 0.0;
-      float* sc = p.ws + 2 * TAIL_BLOCKS;  // [coef_e, coef_m]
-      sc[0] = fminf(p.max_norm / (sqrtf(se) + 1e-6f), 1.f);
-      sc[1] = fminf(p.max_norm / (sqrtf(sm) + 1e-6f), 1.f);
       if (p.kl_index >= 0) {
+        const double kl = (double)p.grads[p.kl_index];
+        double lr = *p.lr64;
         if (kl > p.desired_kl * 2.0) lr = fmax(lr / 1.5, 1e-5);
         else if (kl < p.desired_kl / 2.0 && kl > 0.0) lr = fmin(lr * 1.5, 1e-2);
         *p.lr64 = lr;
         *p.lr32 = (float)lr;
       }
-      *p.counter = 0u;
     } else if (tid == 1) {
       *p.step_main += 1.f;
     } else if (tid == 2) {
@@ -2038,7 +2033,17 @@ __device__ __forceinline__ void adam_range(const lgx_ppo_tail_args& p, int64_t l
 }
 
 __global__ __launch_bounds__(256) void tail_adam(lgx_ppo_tail_args p) {
-  const float* sc = p.ws + 2 * TAIL_BLOCKS;
+  __shared__ float red[4 * 2];
+  __shared__ float sc[2];
+  {  // the clip coefficients from tail_norms' partials (the same fixed order in every block)
+    float t[2];
+    final_sum<2>(p.ws, 2, TAIL_BLOCKS, t, red);
+    if (threadIdx.x == 0) {
+      sc[0] = fminf(p.max_norm / (sqrtf(t[0]) + 1e-6f), 1.f);
+      sc[1] = fminf(p.max_norm / (sqrtf(t[1]) + 1e-6f), 1.f);
+    }
+    __syncthreads();
+  }
   const float ce = sc[0], cm = sc[1];
   const float tm = *p.step_main, te = *p.step_est;
   const float lrm = *p.lr32;
