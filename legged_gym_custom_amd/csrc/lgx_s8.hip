@@ -585,6 +585,7 @@ struct ReduceBatch {
   int64_t start[LGX_S8_BATCH_MAX + 1];  // first thread of each job (wave jobs: 64-aligned)
   lgx_s8_reduce_args j[LGX_S8_BATCH_MAX];
   unsigned char wave[LGX_S8_BATCH_MAX];  // one wave per output (long sums: the bias partials)
+  unsigned char vec[LGX_S8_BATCH_MAX];   // 4 consecutive outputs per thread (flat, 16-B aligned jobs)
 };
 static_assert(sizeof(ReduceBatch) <= 4096, "kernel argument segment");
 
@@ -617,6 +618,25 @@ __global__ __launch_bounds__(256) void s8_reduce_kernel(ReduceBatch b) {
       float* o = J.out + r * J.ld_out + c;
       *o = J.accumulate ? *o + s : s;
     }
+    return;
+  }
+  if (b.vec[ji]) {
+    // a flat job (the split-K weight partials): float4 per thread, the partials requested 8 at a
+    // time (clamped indices, no load under a condition), summed in split order per component
+    const int64_t e = (i - b.start[ji]) * 4;
+    if (e >= J.cols) return;
+    const float* w = J.ws + e;
+    f32x4 s = {0.f, 0.f, 0.f, 0.f};
+    for (int q = 0; q < J.nsplit; q += 8) {
+      f32x4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const f32x4*>(w + (int64_t)min(q + u, J.nsplit - 1) * J.stride);
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (q + u < J.nsplit) s += v[u];
+    }
+    f32x4* o = reinterpret_cast<f32x4*>(J.out + e);
+    *o = J.accumulate ? *o + s : s;
     return;
   }
   const int64_t e = i - b.start[ji];
@@ -860,8 +880,10 @@ int32_t lgx_s8_reduce(const lgx_s8_reduce_args* a, int32_t n, void* stream) {
     if (a[i].rows > 1 && (a[i].ld_ws < a[i].cols || a[i].ld_out < a[i].cols)) return fail("lgx_s8_reduce: pitch < cols");
     b.j[k] = a[i];
     b.wave[k] = a[i].nsplit >= 64 && (int64_t)a[i].rows * a[i].cols <= 4096;
+    b.vec[k] = !b.wave[k] && a[i].rows == 1 && a[i].cols % 4 == 0 && a[i].stride % 4 == 0 &&
+               ((((uintptr_t)a[i].ws) | ((uintptr_t)a[i].out)) & 15) == 0;
     if (b.wave[k]) b.start[k] = (b.start[k] + 63) / 64 * 64;
-    b.start[k + 1] = b.start[k] + (int64_t)a[i].rows * a[i].cols * (b.wave[k] ? 64 : 1);
+    b.start[k + 1] = b.start[k] + (b.vec[k] ? a[i].cols / 4 : (int64_t)a[i].rows * a[i].cols * (b.wave[k] ? 64 : 1));
     ++k;
   }
   b.n = k;
