@@ -534,20 +534,22 @@ __global__ __launch_bounds__(256) void s8_split_kernel(SplitBatch b) {
       store_s8(J.dst + (int64_t)r * J.ld_dst + gg * 32, v);
     }
   };
-  auto one = [&](int r, int gg, float (&v)[8]) {
-    load8(r, gg, v);
-    put(r, gg, v);
-  };
   if (G <= 8) {
-    const int gg = tid & 7;
+    // every row's loads first (clamped rows, no load under a condition), then the stores: one
+    // memory round trip per thread instead of one per row (src and dst never alias)
+    constexpr int NI = LGX_S8_SPLIT_ROWS / 32;
+    const int gg = tid & 7, ggc = min(gg, G - 1);
     float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int it = 0; it < LGX_S8_SPLIT_ROWS / 32; ++it) {
+    float v[NI][8];
+#pragma unroll
+    for (int it = 0; it < NI; ++it) load8(min(rbase + (tid >> 3) + 32 * it, J.rows - 1), ggc, v[it]);
+#pragma unroll
+    for (int it = 0; it < NI; ++it) {
       const int r = rbase + (tid >> 3) + 32 * it;
       if (gg >= G || r >= J.rows) continue;
-      float v[8];
-      one(r, gg, v);
+      put(r, gg, v[it]);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) cs[e] += v[e];
+      for (int e = 0; e < 8; ++e) cs[e] += v[it][e];
     }
     if (J.colsum_ws != nullptr) {
       __shared__ float red[32][64];
