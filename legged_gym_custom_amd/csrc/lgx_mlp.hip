@@ -828,6 +828,260 @@ __global__ __launch_bounds__(NT) void adapt_fwd_kernel(AdaptParams P) {
               });
 }
 
+// ---- the adaptation encoder's DAgger minibatch (lgx_adaptation_train): forward (the stages
+// above, latent kept in LDS), the loss rows ||target - latent||_2 / B, and the backward of every
+// layer, per 16-row chunk; a block walks `chunks` chunks and keeps the weight gradients of its
+// entries (thread t: entries t, t + NT, ...), summed over the chunks' virtual rows
+// in order (in LDS), then writes one partial row per block (flat parameter layout, torch's order).
+// Backward arithmetic is fp32 FMA; ELU' from the stored ELU outputs (y > 0 ? 1 : y + 1).
+constexpr int ATR = 8;  // rows per chunk of lgx_adaptation_train (small LDS: 3 blocks per CU)
+struct AdaptTrainParams {
+  lgx_adapt_train_args t;
+  int L1, L2, NP, chunks;
+  int off[9];  // entry ranges in the flat layout: w0 b0 w1 b1 w2 b2 wf bf | NP
+};
+
+__device__ __forceinline__ float elu_d(float y) { return y > 0.f ? 1.f : y + 1.f; }
+
+#ifdef LGX_ADAPT_CLOCK
+__device__ uint32_t* g_adclk = nullptr;
+#endif
+__global__ __launch_bounds__(NT) void adapt_train_kernel(AdaptTrainParams Q) {
+  const lgx_adapt_args& a = Q.t.f;
+  extern __shared__ __align__(16) float alds[];
+  const int H = a.H, P = a.P, C1 = a.C1, C2 = a.C2, C3 = a.C3, NO = a.NO, L1 = Q.L1, L2 = Q.L2;
+  const int k1 = a.k1, s1 = a.s1, k2 = a.k2, s2 = a.s2;
+  float* xs = alds;                   // [ATR][H*P]
+  float* y0 = xs + ATR * H * P;        // [ATR][H*C1]   (then dpre0)
+  float* y1 = y0 + ATR * H * C1;       // [ATR][L1*C2]  (then dpre1)
+  float* y2 = y1 + ATR * L1 * C2;      // [ATR][L2*C3]  (then dpre2)
+  float* y3 = y2 + ATR * L2 * C3;      // [ATR][NO]     (then dpre3)
+  float* gacc = y3 + ATR * NO;         // [NP]: the block's gradient entries (entry e: thread e % NT)
+  // the layers' weights the backward reads (our layouts), staged once per block: no global load
+  // inside the backward loops (each would hold every later LDS read behind a vmcnt wait)
+  float* w1l = gacc + Q.NP;            // [C2][k1*C1]
+  float* w2l = w1l + C2 * k1 * C1;     // [C3][k2*C2]
+  float* wfl = w2l + C3 * k2 * C2;     // [NO][L2*C3]
+  __shared__ float lrow[ATR];
+  const int tid = threadIdx.x;
+  const float invB = 1.f / (float)a.B;
+#ifdef LGX_ADAPT_CLOCK
+  uint64_t ckl = clock64();
+  uint32_t ck[16] = {0};
+#define ACK(q) do { if (tid == 0) { const uint64_t t_ = clock64(); ck[q] += (uint32_t)(t_ - ckl); ckl = t_; } } while (0)
+#else
+#define ACK(q) do { } while (0)
+#endif
+  for (int e = tid; e < Q.NP; e += NT) gacc[e] = 0.f;
+  for (int i = tid; i < C2 * k1 * C1; i += NT) w1l[i] = a.w1[i];
+  for (int i = tid; i < C3 * k2 * C2; i += NT) w2l[i] = a.w2[i];
+  for (int i = tid; i < NO * L2 * C3; i += NT) wfl[i] = a.wf[i];
+  float lsum = 0.f;  // thread r < ATR: its rows' loss terms, chunks in order
+  const int* off = Q.off;
+  for (int ch = 0; ch < Q.chunks; ++ch) {
+    const int r0 = (blockIdx.x * Q.chunks + ch) * ATR;
+    if (r0 >= a.B) break;  // uniform
+    const int last = a.B - 1 - r0;
+    // inputs: the chunk's history rows
+    for (int i = tid; i < ATR * H * P; i += NT) {
+      const int r = i / (H * P), k = i % (H * P);
+      xs[i] = a.x[(int64_t)(r0 + min(r, last)) * a.ldx + k];
+    }
+    __syncthreads(); ACK(0);
+    adapt_stage(ATR * H, P, C1, a.w0, a.b0, [&](int v) { return (const float*)xs + (v / H) * (H * P) + (v % H) * P; },
+                [&](int v, int n, float y) { y0[(v / H) * (H * C1) + (v % H) * C1 + n] = y; });
+    __syncthreads(); ACK(1);
+    adapt_stage(ATR * L1, k1 * C1, C2, a.w1, a.b1,
+                [&](int v) { return (const float*)y0 + (v / L1) * (H * C1) + (v % L1) * s1 * C1; },
+                [&](int v, int n, float y) { y1[(v / L1) * (L1 * C2) + (v % L1) * C2 + n] = y; });
+    __syncthreads(); ACK(2);
+    adapt_stage(ATR * L2, k2 * C2, C3, a.w2, a.b2,
+                [&](int v) { return (const float*)y1 + (v / L2) * (L1 * C2) + (v % L2) * s2 * C2; },
+                [&](int v, int n, float y) { y2[(v / L2) * (L2 * C3) + (v % L2) * C3 + n] = y; });
+    __syncthreads(); ACK(3);
+    adapt_stage(ATR, L2 * C3, NO, a.wf, a.bf, [&](int v) { return (const float*)y2 + v * (L2 * C3); },
+                [&](int v, int n, float y) {
+                  y3[v * NO + n] = y;
+                  if (a.out && v <= last) a.out[(int64_t)(r0 + v) * a.ldo + n] = y;
+                });
+    __syncthreads(); ACK(4);
+    // loss rows and d(latent pre-activation): (y3 - t) / (B ||y3 - t||) * ELU'(y3); rows past B: 0
+    if (tid < ATR) {
+      const int r = tid;
+      float ss = 0.f;
+      for (int j = 0; j < NO; ++j) {
+        const float d = y3[r * NO + j] - Q.t.target[(int64_t)(r0 + min(r, last)) * Q.t.ldt + j];
+        ss = fmaf(d, d, ss);
+      }
+      const float n = sqrtf(ss);
+      const bool ok = r <= last;
+      if (ok) lsum += n * invB;
+      const float k = ok && n > 0.f ? invB / n : 0.f;
+      for (int j = 0; j < NO; ++j) {
+        const float y = y3[r * NO + j];
+        const float d = y - Q.t.target[(int64_t)(r0 + min(r, last)) * Q.t.ldt + j];
+        y3[r * NO + j] = k * d * elu_d(y);
+      }
+    }
+    __syncthreads(); ACK(5);
+    // fc_final: dW[j][c*L2 + t] += sum_r dpre3[r][j] y2[r][t*C3 + c]; db[j] += sum_r dpre3[r][j]
+#pragma unroll 1
+    for (int e = tid; e < Q.NP; e += NT) {
+      if (e >= off[6] && e < off[8]) {
+        float sum = 0.f;
+        if (e < off[7]) {
+          const int j = (e - off[6]) / (C3 * L2), i = (e - off[6]) % (C3 * L2), c = i / L2, t = i % L2;
+          for (int r = 0; r < ATR; ++r) sum = fmaf(y3[r * NO + j], y2[r * (L2 * C3) + t * C3 + c], sum);
+        } else {
+          const int j = e - off[7];
+          for (int r = 0; r < ATR; ++r) sum += y3[r * NO + j];
+        }
+        gacc[e] += sum;
+      }
+    }
+    __syncthreads(); ACK(6);
+    // dpre2[r][t*C3 + c] = (sum_j dpre3[r][j] Wf[j][t*C3 + c]) * ELU'(y2)   (a.wf in our order)
+    for (int i = tid; i < ATR * L2 * C3; i += NT) {
+      const int r = i / (L2 * C3), f = i % (L2 * C3);
+      float d = 0.f;
+      for (int j = 0; j < NO; ++j) d = fmaf(y3[r * NO + j], wfl[j * (L2 * C3) + f], d);
+      y2[i] = d * elu_d(y2[i]);
+    }
+    __syncthreads(); ACK(7);
+    // conv2: dW[o][c][k] += sum_{r,l} dpre2[r][l][o] y1[r][(l s2 + k) C2 + c]; db[o]
+#pragma unroll 1
+    for (int e = tid; e < Q.NP; e += NT) {
+      if (e >= off[4] && e < off[6]) {
+        float sum = 0.f;
+        if (e < off[5]) {
+          const int o = (e - off[4]) / (C2 * k2), c = ((e - off[4]) / k2) % C2, k = (e - off[4]) % k2;
+          for (int r = 0; r < ATR; ++r)
+            for (int l = 0; l < L2; ++l)
+              sum = fmaf(y2[r * (L2 * C3) + l * C3 + o], y1[r * (L1 * C2) + (l * s2 + k) * C2 + c], sum);
+        } else {
+          const int o = e - off[5];
+          for (int r = 0; r < ATR; ++r)
+            for (int l = 0; l < L2; ++l) sum += y2[r * (L2 * C3) + l * C3 + o];
+        }
+        gacc[e] += sum;
+      }
+    }
+    __syncthreads(); ACK(8);
+    // dpre1[r][p][c] = (sum_{l,k: l s2 + k = p} sum_o dpre2[r][l][o] W2[o][k C2 + c]) * ELU'(y1)
+    for (int i = tid; i < ATR * L1 * C2; i += NT) {
+      const int r = i / (L1 * C2), pc = i % (L1 * C2), pp = pc / C2, c = pc % C2;
+      float d = 0.f;
+      for (int l = 0; l < L2; ++l) {
+        const int k = pp - l * s2;
+        if (k < 0 || k >= k2) continue;
+        for (int o = 0; o < C3; ++o) d = fmaf(y2[r * (L2 * C3) + l * C3 + o], w2l[o * (k2 * C2) + k * C2 + c], d);
+      }
+      y1[i] = d * elu_d(y1[i]);
+    }
+    __syncthreads(); ACK(9);
+    // conv1: dW[o][c][k] += sum_{r,l} dpre1[r][l][o] y0[r][(l s1 + k) C1 + c]; db[o]. Item (o, c)
+    // carries its k1 <= 4 taps (independent sums, one dpre1 load per (r, l)); then the biases
+#pragma unroll 1
+    for (int it = tid; it < C2 * C1 + C2; it += NT) {
+      if (it < C2 * C1) {
+        const int o = it / C1, c = it % C1;
+        // taps past k1 read a clamped tap and are discarded (no branch around a load)
+        const int t1 = min(1, k1 - 1) * C1, t2 = min(2, k1 - 1) * C1, t3 = min(3, k1 - 1) * C1;
+        float s4[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int r = 0; r < ATR; ++r) {
+          const float* g = y1 + r * (L1 * C2) + o;
+          const float* yr = y0 + r * (H * C1) + c;
+#pragma unroll 4
+          for (int l = 0; l < L1; ++l) {
+            const float d = g[l * C2];
+            const float* yb = yr + (l * s1) * C1;
+            const float v0 = yb[0], v1 = yb[t1], v2 = yb[t2], v3 = yb[t3];
+            s4[0] = fmaf(d, v0, s4[0]);
+            s4[1] = fmaf(d, v1, s4[1]);
+            s4[2] = fmaf(d, v2, s4[2]);
+            s4[3] = fmaf(d, v3, s4[3]);
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (k < k1) gacc[off[2] + o * (C1 * k1) + c * k1 + k] += s4[k];
+      } else {
+        const int o = it - C2 * C1;
+        float sum = 0.f;
+        for (int r = 0; r < ATR; ++r)
+          for (int l = 0; l < L1; ++l) sum += y1[r * (L1 * C2) + l * C2 + o];
+        gacc[off[3] + o] += sum;
+      }
+    }
+    __syncthreads(); ACK(10);
+    // dpre0[r][t][c] = (sum_{l,k: l s1 + k = t} sum_o dpre1[r][l][o] W1[o][k C1 + c]) * ELU'(y0),
+    // two channels per item (C1 even)
+    for (int i = tid; i < ATR * H * (C1 / 2); i += NT) {
+      const int r = i / (H * (C1 / 2)), tc = i % (H * (C1 / 2)), t = tc / (C1 / 2), c = 2 * (tc % (C1 / 2));
+      float d0 = 0.f, d1 = 0.f;
+      for (int l = 0; l < L1; ++l) {
+        const int k = t - l * s1;
+        if (k < 0 || k >= k1) continue;
+        const float* w = w1l + k * C1 + c;
+        const float* g = y1 + r * (L1 * C2) + l * C2;
+#pragma unroll 4
+        for (int o = 0; o < C2; ++o) {
+          const float gv = g[o];
+          d0 = fmaf(gv, w[o * (k1 * C1)], d0);
+          d1 = fmaf(gv, w[o * (k1 * C1) + 1], d1);
+        }
+      }
+      float* y = y0 + r * (H * C1) + t * C1 + c;
+      y[0] = d0 * elu_d(y[0]);
+      y[1] = d1 * elu_d(y[1]);
+    }
+    __syncthreads(); ACK(11);
+    // fc_encoder: dW[c][p] += sum_{r,t} dpre0[r][t][c] x[r][t][p]; db[c]. Item (c, 4 p's): one
+    // dpre0 load and one float4 of x per (r, t), four independent sums
+#pragma unroll 1
+    for (int it = tid; it < C1 * (P / 4) + C1; it += NT) {
+      if (it < C1 * (P / 4)) {
+        const int c = it / (P / 4), pp = 4 * (it % (P / 4));
+        float4 s4 = {0.f, 0.f, 0.f, 0.f};
+        for (int r = 0; r < ATR; ++r)
+#pragma unroll 5
+          for (int t = 0; t < H; ++t) {
+            const float d = y0[r * (H * C1) + t * C1 + c];
+            const float4 x4 = *reinterpret_cast<const float4*>(xs + r * (H * P) + t * P + pp);
+            s4.x = fmaf(d, x4.x, s4.x);
+            s4.y = fmaf(d, x4.y, s4.y);
+            s4.z = fmaf(d, x4.z, s4.z);
+            s4.w = fmaf(d, x4.w, s4.w);
+          }
+        float* g = gacc + c * P + pp;
+        g[0] += s4.x;
+        g[1] += s4.y;
+        g[2] += s4.z;
+        g[3] += s4.w;
+      } else {
+        const int c = it - C1 * (P / 4);
+        float sum = 0.f;
+        for (int r = 0; r < ATR; ++r)
+          for (int t = 0; t < H; ++t) sum += y0[r * (H * C1) + t * C1 + c];
+        gacc[off[1] + c] += sum;
+      }
+    }
+    __syncthreads(); ACK(12);
+  }
+  for (int e = tid; e < Q.NP; e += NT) Q.t.gws[(int64_t)blockIdx.x * Q.NP + e] = gacc[e];
+#ifdef LGX_ADAPT_CLOCK
+  if (tid == 0 && g_adclk)
+    for (int q = 0; q < 16; ++q) g_adclk[(size_t)blockIdx.x * 16 + q] = ck[q];
+#endif
+  if (tid < ATR) lrow[tid] = lsum;
+  __syncthreads(); ACK(13);
+  if (tid == 0) {
+    float l = 0.f;
+    for (int r = 0; r < ATR; ++r) l += lrow[r];
+    Q.t.loss_ws[blockIdx.x] = l;
+  }
+}
+
 // C (=|+=) epilogue(sum_z ws[z]) and colsum[m] (=|+=) sum_z colsum_ws[z][m]. Each thread owns
 // 4 consecutive outputs (float4 when N % 4 == 0) and walks the splits with 4 independent
 // accumulators (z mod 4) combined in a fixed order: deterministic, memory-level parallel.
@@ -2764,6 +3018,50 @@ int32_t lgx_adaptation_forward(const lgx_adapt_args* a, void* stream) {
     return fail("lgx_adaptation_forward: sizes beyond the fused kernel's LDS / 32-bit offsets");
   hipLaunchKernelGGL(adapt_fwd_kernel, dim3((unsigned)((a->B + AR - 1) / AR)), dim3(NT), (size_t)floats * 4,
                      static_cast<hipStream_t>(stream), P);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : fail(hipGetErrorString(e));
+}
+
+#ifdef LGX_ADAPT_CLOCK
+int32_t lgx_adapt_set_clock(void* buf) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(lgxm::g_adclk), &buf, sizeof(void*)) == hipSuccess ? 0 : -1;
+}
+#endif
+int32_t lgx_adaptation_train(const lgx_adapt_train_args* t, void* stream) {
+  using namespace lgxm;
+  if (!t) return fail("lgx_adaptation_train: null args");
+  const lgx_adapt_args* a = &t->f;
+  if (a->B < 1 || a->H < 1 || a->P < 1 || a->C1 < 1 || a->C2 < 1 || a->C3 < 1 || a->NO < 1 || a->k1 < 1 ||
+      a->s1 < 1 || a->k2 < 1 || a->s2 < 1 || t->blocks < 1)
+    return fail("lgx_adaptation_train: dimensions must be positive");
+  AdaptTrainParams Q;
+  Q.t = *t;
+  Q.L1 = (a->H - a->k1) / a->s1 + 1;
+  Q.L2 = (Q.L1 - a->k2) / a->s2 + 1;
+  if (a->H < a->k1 || Q.L1 < a->k2) return fail("lgx_adaptation_train: history shorter than a kernel");
+  if (a->P % 4 || a->C1 % 2 || a->k1 > 4) return fail("lgx_adaptation_train: P % 4 == 0, C1 even, k1 <= 4");
+  if (!a->x || a->ldx < (int64_t)a->H * a->P || !a->w0 || !a->b0 || !a->w1 || !a->b1 || !a->w2 || !a->b2 || !a->wf ||
+      !a->bf || (a->out && a->ldo < a->NO) || !t->target || t->ldt < a->NO || !t->gws || !t->loss_ws)
+    return fail("lgx_adaptation_train: bad operands");
+  const int sizes[8] = {a->C1 * a->P, a->C1, a->C2 * a->C1 * a->k1, a->C2, a->C3 * a->C2 * a->k2, a->C3,
+                        a->NO * a->C3 * Q.L2, a->NO};
+  Q.off[0] = 0;
+  for (int i = 0; i < 8; ++i) Q.off[i + 1] = Q.off[i] + sizes[i];
+  Q.NP = Q.off[8];
+  const int nchunk = (a->B + ATR - 1) / ATR;
+  Q.chunks = (nchunk + t->blocks - 1) / t->blocks;
+  const unsigned grid = (unsigned)((nchunk + Q.chunks - 1) / Q.chunks);
+  const int64_t floats = (int64_t)ATR * ((int64_t)a->H * a->P + (int64_t)a->H * a->C1 + (int64_t)Q.L1 * a->C2 +
+                                        (int64_t)Q.L2 * a->C3 + a->NO) + Q.NP +
+                         (int64_t)a->C2 * a->k1 * a->C1 + (int64_t)a->C3 * a->k2 * a->C2 + (int64_t)a->NO * Q.L2 * a->C3;
+  if (floats * 4 > 96 * 1024 || (int64_t)a->B * a->ldx > INT32_MAX)
+    return fail("lgx_adaptation_train: sizes beyond the fused kernel's LDS / 32-bit offsets");
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)adapt_train_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+    attr = true;
+  }
+  hipLaunchKernelGGL(adapt_train_kernel, dim3(grid), dim3(NT), (size_t)floats * 4, static_cast<hipStream_t>(stream), Q);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : fail(hipGetErrorString(e));
 }

@@ -48,6 +48,10 @@ USE_FUSED_ACT = os.environ.get("LGX_FUSED_ACT", "1") != "0"
 # the mode the 2-rank tests exercise, until a multi-GPU run has shown the captured collective
 # equal to eager (tests/test_gpu_graph_allreduce.py covers it on a 1-rank group only)
 GRAPH_ALLREDUCE = os.environ.get("LGX_GRAPH_ALLREDUCE", "0") != "0"
+# the DAgger minibatch as one fused launch (lgx_adaptation_train) + one reduce, instead of the
+# adaptation encoder's autograd graph
+DAGGER_FUSED = os.environ.get("LGX_DAGGER_FUSED", "1") != "0"
+DAGGER_BLOCKS = 512  # lgx_adaptation_train's block budget (two per CU: 64 KB of LDS each)
 
 
 def _distributed():
@@ -838,6 +842,9 @@ class PPO:
             obs_p, priv_p = hip_mlp.gather_rows([obs, s.privileged_observations.flatten(0, 1)], self._perm)
             priv_lat = ac.privileged_encoder(priv_p)
         self._dagger_sum.zero_()
+        if DAGGER_FUSED and self._dagger_fused_ok(adapt):
+            self._dagger_fused(obs_p, priv_lat, mb, adapt)
+            return
         for _ in range(self.num_learning_epochs):
             for i in range(self.num_mini_batches):
                 adapt_latent = ac.adaptation_encoder(obs_p[i * mb:(i + 1) * mb])
@@ -851,6 +858,52 @@ class PPO:
                     _clip_([adapt], self.max_grad_norm)
                     self._adam("adaptation_optimizer", self._adapt_lr)
                     self._dagger_sum.add_(adaptation_loss.detach())
+
+    def _dagger_fused_ok(self, adapt):
+        """lgx_adaptation_train writes the gradient in the flat order of hip_mlp.adaptation_param_order:
+        the adaptation segment must hold exactly those parameters' gradients, in that order."""
+        ac = self.actor_critic
+        mod = ac.adaptation_encoder_
+        conv1 = mod.conv_layers[0]
+        if ac.num_proprio % 4 or mod.fc_encoder[0].out_features % 2 or conv1.kernel_size[0] > 4:
+            return False  # outside lgx_adaptation_train's shapes
+        ps = hip_mlp.adaptation_param_order(mod)
+        off = adapt.data_ptr()
+        for p in ps:
+            if p.grad is None or p.grad.data_ptr() != off or not p.grad.is_contiguous():
+                return False
+            off += 4 * p.numel()
+        return off == adapt.data_ptr() + 4 * adapt.numel()
+
+    def _dagger_fused(self, obs_p, priv_lat, mb, adapt):
+        """The DAgger minibatches with the adaptation encoder's forward, loss and backward in ONE
+        launch each (lgx_adaptation_train: per-block gradient rows), the rows summed into the flat
+        gradient segment and the loss into the running sum by one reduce launch, then the clip and
+        Adam of _dagger_body (ppo.py:336-345)."""
+        from legged_gym_custom_amd.rsl_rl.modules import hip_s8 as S
+        ac = self.actor_critic
+        hist_cols = ac.num_proprio * ac.history_buffer_length
+        grid = hip_mlp.adapt_train_grid(mb, DAGGER_BLOCKS)
+        NP = adapt.numel()
+        ws = getattr(self, "_dagger_ws", None)
+        if ws is None or ws[0].numel() != grid * NP:
+            ws = (torch.empty(grid * NP, device=self.device), torch.empty(grid, device=self.device))
+            self._dagger_ws = ws
+        gws, lws = ws
+        jobs = [S.flat_reduce(gws.data_ptr(), NP, adapt.data_ptr(), NP, grid),
+                S.flat_reduce(lws.data_ptr(), 1, self._dagger_sum.data_ptr(), 1, grid, accumulate=1)]
+        for _ in range(self.num_learning_epochs):
+            for i in range(self.num_mini_batches):
+                keep = hip_mlp.adaptation_train(ac.adaptation_encoder_, obs_p[i * mb:(i + 1) * mb], hist_cols,
+                                                priv_lat[i * mb:(i + 1) * mb], gws, lws, DAGGER_BLOCKS)
+                S.reduce(jobs)
+                del keep
+                if _distributed():
+                    dist.all_reduce(adapt)
+                    adapt.div_(dist.get_world_size())
+                with torch.no_grad():
+                    _clip_([adapt], self.max_grad_norm)
+                    self._adam("adaptation_optimizer", self._adapt_lr)
 
     def _dagger_body_cpu(self):
         """The CPU learner's DAgger update (the reference's statement order, per-minibatch

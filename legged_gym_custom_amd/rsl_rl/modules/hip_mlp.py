@@ -29,7 +29,7 @@ EXPORTED = ["lgx_mlp_abi_version", "lgx_mlp_sizeof_gemm_args", "lgx_mlp_pick_spl
             "lgx_mlp_pick_split_group", "lgx_gae", "lgx_normalize_advantages",
             "lgx_gather_rows", "lgx_transpose_batch", "lgx_loss_heads_forward", "lgx_loss_heads_backward",
             "lgx_track_episodes", "lgx_chain", "lgx_adaptation_forward", "lgx_loss_heads_fused",
-            "lgx_loss_heads_tail"]
+            "lgx_loss_heads_tail", "lgx_adaptation_train"]
 TAIL_MAX_LOSSES = 8
 COPY_MAX = 16
 SPLITK_MAX = 24
@@ -167,6 +167,52 @@ class AdaptArgs(C.Structure):
                 ("out", C.c_void_p), ("ldo", C.c_int64)]
 
 
+class AdaptTrainArgs(C.Structure):
+    """Mirror of lgx_adapt_train_args (ABI 9)."""
+    _fields_ = [("f", AdaptArgs), ("target", C.c_void_p), ("ldt", C.c_int64), ("gws", C.c_void_p),
+                ("loss_ws", C.c_void_p), ("blocks", C.c_int32)]
+
+
+ADAPT_TRAIN_ROWS = 8  # rows per chunk of lgx_adaptation_train (lgx_mlp.hip ATR)
+
+
+def adapt_train_grid(rows, blocks):
+    """lgx_adaptation_train's grid for `rows` rows and a `blocks` budget (its partial rows)."""
+    nchunk = (rows + ADAPT_TRAIN_ROWS - 1) // ADAPT_TRAIN_ROWS
+    chunks = (nchunk + blocks - 1) // blocks
+    return (nchunk + chunks - 1) // chunks
+
+
+def adaptation_param_order(mod):
+    """The adaptation encoder's parameters in lgx_adaptation_train's flat gradient order."""
+    return [mod.fc_encoder[0].weight, mod.fc_encoder[0].bias, mod.conv_layers[0].weight, mod.conv_layers[0].bias,
+            mod.conv_layers[2].weight, mod.conv_layers[2].bias, mod.fc_final[0].weight, mod.fc_final[0].bias]
+
+
+def adaptation_train(mod, obs_rows, hist_cols, target, gws, loss_ws, blocks):
+    """One DAgger minibatch's forward + loss + backward of the adaptation encoder in ONE launch
+    (lgx_adaptation_train): obs_rows [B, >= hist_cols] fp32 (the history = its first hist_cols
+    columns, read in place), target [B, NO] (the privileged latent). Writes the per-block gradient
+    rows gws [grid, NP] and loss rows loss_ws [grid] (adapt_train_grid)."""
+    Bn = obs_rows.shape[0]
+    H = mod.history_buffer_length
+    P = hist_cols // H
+    C1, C2, C3, k1, s1, k2, s2, L1, L2 = _conv_dims(mod, H)
+    f_w = mod.fc_final[0].weight
+    if L2 * C3 != f_w.shape[1] or obs_rows.stride(1) != 1 or target.stride(1) != 1:
+        raise MlpLibError("adaptation_train: layout outside the fused kernel's limits")
+    fc_w, fc_b = mod.fc_encoder[0].weight, mod.fc_encoder[0].bias
+    W1, W2, Wf = _conv_w(mod.conv_layers[0].weight), _conv_w(mod.conv_layers[2].weight), _final_w(f_w, C3, L2)
+    f = AdaptArgs(x=obs_rows.data_ptr(), ldx=obs_rows.stride(0), B=Bn, H=H, P=P, w0=_ptr(fc_w), b0=_ptr(fc_b), C1=C1,
+                  w1=_ptr(W1), b1=_ptr(mod.conv_layers[0].bias), C2=C2, k1=k1, s1=s1, w2=_ptr(W2),
+                  b2=_ptr(mod.conv_layers[2].bias), C3=C3, k2=k2, s2=s2, wf=_ptr(Wf), bf=_ptr(mod.fc_final[0].bias),
+                  NO=f_w.shape[0], out=None, ldo=0)
+    t = AdaptTrainArgs(f=f, target=target.data_ptr(), ldt=target.stride(0), gws=gws.data_ptr(),
+                       loss_ws=loss_ws.data_ptr(), blocks=blocks)
+    _check(lib().lgx_adaptation_train(C.byref(t), _stream()), "lgx_adaptation_train")
+    return (W1, W2, Wf)  # keep the re-laid weights alive until the launch has run (stream order)
+
+
 class GaeArgs(C.Structure):
     """Mirror of lgx_gae_args."""
     _fields_ = [(n, C.c_void_p) for n in ("rewards", "dones", "values", "last_values", "returns", "advantages")] + \
@@ -213,6 +259,8 @@ def lib():
     L.lgx_loss_heads_fused.restype = C.c_int32
     L.lgx_loss_heads_tail.argtypes = [vp, vp, vp, vp, vp]
     L.lgx_loss_heads_tail.restype = C.c_int32
+    L.lgx_adaptation_train.argtypes = [vp, vp]
+    L.lgx_adaptation_train.restype = C.c_int32
     for fn in ("lgx_aux_loss_forward", "lgx_aux_loss_backward", "lgx_ppo_tail"):
         getattr(L, fn).argtypes = [vp, vp]
         getattr(L, fn).restype = C.c_int32

@@ -123,3 +123,45 @@ def test_gae_kernel_matches_torch_statement():
     a = (a - a.mean()) / (a.std() + 1e-8)
     assert torch.equal(ret, s.returns)
     torch.testing.assert_close(s.advantages, a, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("B", [16 * 300 + 5, 24576])
+def test_adaptation_train_matches_autograd_fp64(B):
+    """lgx_adaptation_train (one DAgger minibatch of the adaptation encoder in one launch, lgx_mlp
+    ABI 9) against torch autograd in fp64 on the same weights and rows: the summed per-block
+    gradient rows of every parameter within 2e-4 * max|g| + 1e-7 (the forward is the 3 x bf16
+    fused forward, the backward fp32) and the loss within 1e-5 relative; fixed-order sums: two
+    launches give identical rows."""
+    from legged_gym_custom_amd.rsl_rl.modules import hip_mlp as H
+    from legged_gym_custom_amd.rsl_rl.modules.support_networks import AdaptationEncoder, AdaptationEncoderTS
+    torch.manual_seed(5)
+    P, Hh = 52, 10
+    mod = AdaptationEncoder(num_proprio=P, history_buffer_length=Hh).to("cuda:0")
+    obs = torch.randn(B, P * (Hh + 1), device="cuda:0")
+    target = torch.randn(B, 20, device="cuda:0") * 0.5
+    ps = H.adaptation_param_order(mod)
+    NP = sum(p.numel() for p in ps)
+    grid = H.adapt_train_grid(B, 768)
+    gws, lws = torch.empty(grid * NP, device="cuda:0"), torch.empty(grid, device="cuda:0")
+    keep = H.adaptation_train(mod, obs, P * Hh, target, gws, lws, 768)
+    torch.cuda.synchronize()
+    got = gws.view(grid, NP).double().sum(0)
+    rows1 = gws.clone()
+    keep = H.adaptation_train(mod, obs, P * Hh, target, gws, lws, 768)
+    torch.cuda.synchronize()
+    del keep
+    assert torch.equal(gws, rows1)
+    ref = AdaptationEncoderTS(num_proprio=P, history_buffer_length=Hh).double()
+    ref.load_state_dict({k: v.double().cpu() for k, v in mod.state_dict().items()})
+    hist = obs[:, :P * Hh].double().cpu().reshape(B, Hh, P)
+    lat = ref(hist)
+    loss = (target.double().cpu() - lat).norm(p=2, dim=1).mean()
+    loss.backward()
+    ref_ps = H.adaptation_param_order(ref)
+    o = 0
+    for p, rp in zip(ps, ref_ps):
+        g, rg = got[o:o + p.numel()].cpu().view_as(rp), rp.grad
+        o += p.numel()
+        err = float((g - rg).abs().max())
+        assert err <= 2e-4 * float(rg.abs().max()) + 1e-7, (tuple(p.shape), err, float(rg.abs().max()))
+    assert abs(float(lws.double().sum()) - float(loss.detach())) <= 1e-5 * float(loss.detach())
