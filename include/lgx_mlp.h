@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define LGX_MLP_ABI_VERSION 9
+#define LGX_MLP_ABI_VERSION 10
 
 enum {
   LGX_EPI_BIAS = 1,  /* + bias[n] */
@@ -171,6 +171,16 @@ const char* lgx_mlp_last_error(void);
 int32_t lgx_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
                       const float* lr_dev, float lr, float beta1, float beta2, float eps, const float* step,
                       const float* grad_scale, void* stream);
+/* ABI 10. clip_grad_norm_ + one Adam step over a small segment in ONE launch (one block; the
+ * DAgger step, rsl_rl ppo.py:336-345 — clip_grad_norm_(adaptation_encoder.parameters()), then
+ * adaptation_optimizer.step()):
+ *   coef = min(max_norm / (||grad||_2 + 1e-6), 1);  grad *= coef (in place, as torch leaves it)
+ *   *step += 1;  Adam as lgx_adam_step with the clipped gradient;  *coef_out = coef (optional)
+ * ||grad|| is summed in a fixed order (deterministic). n <= LGX_CLIP_ADAM_MAX. */
+#define LGX_CLIP_ADAM_MAX 65536
+int32_t lgx_clip_adam(float* param, float* grad, float* exp_avg, float* exp_avg_sq, int64_t n, const float* lr_dev,
+                      float lr, float beta1, float beta2, float eps, float* step, float max_norm, float* coef_out,
+                      void* stream);
 
 /* PPO loss head (rsl_rl ppo.py:196-262 with the Gaussian policy of actor_critic.py:
  * Normal(mu, std) log_prob / entropy), forward and backward in one kernel each.

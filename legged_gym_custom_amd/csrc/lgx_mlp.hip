@@ -828,42 +828,167 @@ __global__ __launch_bounds__(NT) void adapt_fwd_kernel(AdaptParams P) {
               });
 }
 
-// ---- the adaptation encoder's DAgger minibatch (lgx_adaptation_train): forward (the stages
-// above, latent kept in LDS), the loss rows ||target - latent||_2 / B, and the backward of every
-// layer, per 16-row chunk; a block walks `chunks` chunks and keeps the weight gradients of its
-// entries (thread t: entries t, t + NT, ...), summed over the chunks' virtual rows
-// in order (in LDS), then writes one partial row per block (flat parameter layout, torch's order).
-// Backward arithmetic is fp32 FMA; ELU' from the stored ELU outputs (y > 0 ? 1 : y + 1).
-constexpr int ATR = 8;  // rows per chunk of lgx_adaptation_train (small LDS: 3 blocks per CU)
+// ---- the adaptation encoder's DAgger minibatch (lgx_adaptation_train) on f32-input MFMA
+// (v_mfma_f32_16x16x4_f32: exact f32, each output a k-ordered fmaf chain). A block walks `chunks`
+// chunks of ATR = 16 rows with everything in LDS: the forward (4 GEMM stages over virtual rows
+// (row, position), each A row a window of the previous stage), the loss rows, and the backward:
+// each input gradient as a GEMM per output position over the (position, tap) pairs that reach
+// it, times ELU'; each weight gradient as a GEMM over the chunk's virtual rows, accumulated in
+// registers across the chunks (each wave owns fixed 16 x 16 tiles; a bias gradient is the tile
+// column whose B operand is 1). One partial row per block (flat layout, torch's order) and one
+// loss partial. The next chunk's rows are loaded into registers while this one computes.
+constexpr int ATR = 16;                                     // rows per chunk (one 16-row tile)
+constexpr int AT_W0 = 2, AT_W1 = 4, AT_W2 = 1, AT_WF = 1;  // weight-gradient tiles per wave
+constexpr int AT_XPT = 36, AT_TPT = 2, AT_K0 = 16;          // prefetch floats per thread; W0 steps
+enum { AL_XS, AL_Y0, AL_Y1, AL_Y2, AL_Y3, AL_TG, AL_W1, AL_W2, AL_WF, AL_BIAS, AL_ONE, AL_END };
 struct AdaptTrainParams {
   lgx_adapt_train_args t;
   int L1, L2, NP, chunks;
-  int off[9];  // entry ranges in the flat layout: w0 b0 w1 b1 w2 b2 wf bf | NP
+  int off[9];                     // entry ranges in the flat layout: w0 b0 w1 b1 w2 b2 wf bf | NP
+  int Y0P, W1P, W2P, Y2P, C2P, C3P, NOP;  // LDS pitches / padded K extents (floats)
+  int lds[AL_END + 1];            // LDS region offsets (floats)
 };
 
 __device__ __forceinline__ float elu_d(float y) { return y > 0.f ? 1.f : y + 1.f; }
 
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+// acc += sum_{s < n} A_s B_s: this lane's operands of step s are a[s * as], b[s * bs] (LDS); the
+// loads of 8 (then 4) steps are issued before their MFMAs
+__device__ __forceinline__ f32x4 mma_run(f32x4 acc, const float* a, int as, const float* b, int bs, int n) {
+  int s = 0;
+  for (; s + 8 <= n; s += 8) {
+    float av[8], bv[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { av[j] = a[j * as]; bv[j] = b[j * bs]; }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc = mfma4(av[j], bv[j], acc);
+    a += 8 * as; b += 8 * bs;
+  }
+  if (s + 4 <= n) {
+    float av[4], bv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { av[j] = a[j * as]; bv[j] = b[j * bs]; }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc = mfma4(av[j], bv[j], acc);
+    a += 4 * as; b += 4 * bs; s += 4;
+  }
+  for (; s < n; ++s, a += as, b += bs) acc = mfma4(*a, *b, acc);
+  return acc;
+}
+
+// forward stage: st(v, n, ELU(sum_k A(v, k) w[n * wp + k] + bias[n])) for v < M, n < N; A(v, k) =
+// arow(v)[k], K = 4 * K4 (the weight rows zero past the layer's K)
+template <class ARow, class St>
+__device__ __forceinline__ void at_fwd(int lane, int wave, int M, int N, int K4, ARow arow, const float* w, int wp,
+                                       const float* bias, St st) {
+  const int i = lane & 15, g = lane >> 4;
+  const int ntn = (N + 15) >> 4, ntiles = ((M + 15) >> 4) * ntn;
+  for (int tile = wave; tile < ntiles; tile += NT / 64) {
+    const int mt = tile / ntn, nt = tile - mt * ntn;
+    const int v = min(mt * 16 + i, M - 1), n = min(nt * 16 + i, N - 1);
+    const f32x4 acc = mma_run(f32x4{0.f, 0.f, 0.f, 0.f}, arow(v) + g, 4, w + n * wp + g, 4, K4);
+    const int nn = nt * 16 + i;  // C/D map: column i, rows 4 g + q
+    if (nn < N) {
+      const float bn = bias[nn];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int vv = mt * 16 + 4 * g + q;
+        if (vv < M) st(vv, nn, elu(acc[q] + bn));
+      }
+    }
+  }
+}
+
+// input-gradient stage, per output position p < npos and column n < N of the 16 rows:
+// out(r, p, n) *= ... := (sum_{l < Ls, k = p - l s in [0, ktaps)} sum_c src[r srs + l sps + c]
+// w[c wp + k tw + n]) * ELU'(out(r, p, n)), c over 4 * K4 (the weight rows zero past the channels)
+template <class Out>
+__device__ __forceinline__ void at_dx(int lane, int wave, int npos, int N, int Ls, int s, int ktaps, const float* src,
+                                      int srs, int sps, int K4, const float* w, int wp, int tw, Out outp) {
+  const int i = lane & 15, g = lane >> 4;
+  const int ntn = (N + 15) >> 4;
+  for (int tile = wave; tile < npos * ntn; tile += NT / 64) {
+    const int p = tile / ntn, nt = tile - p * ntn;
+    const int n = min(nt * 16 + i, N - 1);
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int l = 0; l < Ls; ++l) {
+      const int k = p - l * s;
+      if (k < 0 || k >= ktaps) continue;
+      acc = mma_run(acc, src + i * srs + l * sps + g, 4, w + g * wp + k * tw + n, 4 * wp, K4);
+    }
+    const int nn = nt * 16 + i;
+    if (nn < N) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float* o = outp(4 * g + q, p, nn);
+        *o = acc[q] * elu_d(*o);
+      }
+    }
+  }
+}
+
+// weight-gradient stage: tiles wave + 4 j (j < J) of the M x (nvalid + 1) gradient; column nvalid
+// is the bias (B = 1). A(m, step s) = a0[m + s as] with a0 = abase (this lane's k slot) or the
+// zero word when the slot is invalid; B(step s, n) = bbase[n + s bs], 1 at n == nvalid, else 0.
+template <int J>
+__device__ __forceinline__ void at_dw(int lane, int wave, f32x4 (&acc)[J], int M, int nvalid, int nsteps, bool kval,
+                                      const float* abase, int as, const float* bbase, int bs, const float* one) {
+  const int i = lane & 15;
+  const int ntn = (nvalid + 16) >> 4, ntiles = ((M + 15) >> 4) * ntn;
+  const float* zero = one + 4;
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int tile = wave + (NT / 64) * j;
+    if (tile >= ntiles) break;
+    const int mt = tile / ntn, nt = tile - mt * ntn;
+    const int m = min(mt * 16 + i, M - 1), n = nt * 16 + i;
+    const float* a = kval ? abase + m : zero;
+    const float* b = kval && n < nvalid ? bbase + n : (n == nvalid ? one : zero);
+    acc[j] = mma_run(acc[j], a, kval ? as : 0, b, kval && n < nvalid ? bs : 0, nsteps);
+  }
+}
+
+// the tiles of at_dw to the block's gradient row: idx(m, n) = flat entry or -1
+template <int J, class Idx>
+__device__ __forceinline__ void at_dw_store(int lane, int wave, const f32x4 (&acc)[J], int M, int nvalid, float* row,
+                                            Idx idx) {
+  const int i = lane & 15, g = lane >> 4;
+  const int ntn = (nvalid + 16) >> 4, ntiles = ((M + 15) >> 4) * ntn;
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int tile = wave + (NT / 64) * j;
+    if (tile >= ntiles) break;
+    const int mt = tile / ntn, nt = tile - mt * ntn, n = nt * 16 + i;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int m = mt * 16 + 4 * g + q;
+      if (m < M && n <= nvalid) {
+        const int e = idx(m, n);
+        if (e >= 0) row[e] = acc[j][q];
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ int at_opq_s(int v) {  // a uniform value the compiler must treat as changed here
+  __asm__ volatile("" : "+s"(v));
+  return v;
+}
+__device__ __forceinline__ int at_opq_v(int v) {
+  __asm__ volatile("" : "+v"(v));
+  return v;
+}
+
 #ifdef LGX_ADAPT_CLOCK
 __device__ uint32_t* g_adclk = nullptr;
 #endif
-__global__ __launch_bounds__(NT) void adapt_train_kernel(AdaptTrainParams Q) {
+__global__ __launch_bounds__(NT, 2) void adapt_train_kernel(AdaptTrainParams Q) {
   const lgx_adapt_args& a = Q.t.f;
   extern __shared__ __align__(16) float alds[];
-  const int H = a.H, P = a.P, C1 = a.C1, C2 = a.C2, C3 = a.C3, NO = a.NO, L1 = Q.L1, L2 = Q.L2;
-  const int k1 = a.k1, s1 = a.s1, k2 = a.k2, s2 = a.s2;
-  float* xs = alds;                   // [ATR][H*P]
-  float* y0 = xs + ATR * H * P;        // [ATR][H*C1]   (then dpre0)
-  float* y1 = y0 + ATR * H * C1;       // [ATR][L1*C2]  (then dpre1)
-  float* y2 = y1 + ATR * L1 * C2;      // [ATR][L2*C3]  (then dpre2)
-  float* y3 = y2 + ATR * L2 * C3;      // [ATR][NO]     (then dpre3)
-  float* gacc = y3 + ATR * NO;         // [NP]: the block's gradient entries (entry e: thread e % NT)
-  // the layers' weights the backward reads (our layouts), staged once per block: no global load
-  // inside the backward loops (each would hold every later LDS read behind a vmcnt wait)
-  float* w1l = gacc + Q.NP;            // [C2][k1*C1]
-  float* w2l = w1l + C2 * k1 * C1;     // [C3][k2*C2]
-  float* wfl = w2l + C3 * k2 * C2;     // [NO][L2*C3]
   __shared__ float lrow[ATR];
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, wave0 = __builtin_amdgcn_readfirstlane(tid >> 6);
   const float invB = 1.f / (float)a.B;
 #ifdef LGX_ADAPT_CLOCK
   uint64_t ckl = clock64();
@@ -872,209 +997,201 @@ __global__ __launch_bounds__(NT) void adapt_train_kernel(AdaptTrainParams Q) {
 #else
 #define ACK(q) do { } while (0)
 #endif
-  for (int e = tid; e < Q.NP; e += NT) gacc[e] = 0.f;
-  for (int i = tid; i < C2 * k1 * C1; i += NT) w1l[i] = a.w1[i];
-  for (int i = tid; i < C3 * k2 * C2; i += NT) w2l[i] = a.w2[i];
-  for (int i = tid; i < NO * L2 * C3; i += NT) wfl[i] = a.wf[i];
-  float lsum = 0.f;  // thread r < ATR: its rows' loss terms, chunks in order
-  const int* off = Q.off;
+  // prologue: LDS zeroed (pads and K tails read zeros), the weights staged in the LDS layouts
+  {
+    const int C1 = a.C1, C2 = a.C2, C3 = a.C3, NO = a.NO, k1 = a.k1, k2 = a.k2, L2 = Q.L2;
+    for (int e = 4 * tid; e < Q.lds[AL_END]; e += 4 * NT)
+      *reinterpret_cast<float4*>(alds + e) = float4{0.f, 0.f, 0.f, 0.f};
+    __syncthreads();
+    float* w1l = alds + Q.lds[AL_W1];  // [C2P][W1P]: w1[o][k C1 + c] at k Y0P + c, zero pads
+    float* w2l = alds + Q.lds[AL_W2];  // [C3P][W2P]
+    float* wfl = alds + Q.lds[AL_WF];  // [NOP][Y2P]
+    float* bl = alds + Q.lds[AL_BIAS];  // b0 | b1 | b2 | bf
+    for (int e = tid; e < C2 * k1 * C1; e += NT) {
+      const int o = e / (k1 * C1), j = e - o * (k1 * C1), k = j / C1, c = j - k * C1;
+      w1l[o * Q.W1P + k * Q.Y0P + c] = a.w1[e];
+    }
+    for (int e = tid; e < C3 * k2 * C2; e += NT) w2l[(e / (k2 * C2)) * Q.W2P + e % (k2 * C2)] = a.w2[e];
+    for (int e = tid; e < NO * L2 * C3; e += NT) wfl[(e / (L2 * C3)) * Q.Y2P + e % (L2 * C3)] = a.wf[e];
+    for (int e = tid; e < C1 + C2 + C3 + NO; e += NT)
+      bl[e] = e < C1 ? a.b0[e] : e < C1 + C2 ? a.b1[e - C1] : e < C1 + C2 + C3 ? a.b2[e - C1 - C2] : a.bf[e - C1 - C2 - C3];
+    if (tid < 4) alds[Q.lds[AL_ONE] + tid] = 1.f;  // then 4 zero words
+  }
+  // W0 fragment of the wave's fc_encoder column tile (wave % ntn0; ntn0 divides 4): k = 4 s + g
+  float w0r[AT_K0];
+  {
+    const int ntn0 = (a.C1 + 15) >> 4, K40 = (a.P + 3) >> 2, lane = tid & 63, g = lane >> 4;
+    const int n = min((wave0 % ntn0) * 16 + (lane & 15), a.C1 - 1);
+#pragma unroll
+    for (int s = 0; s < AT_K0; ++s) w0r[s] = s < K40 && 4 * s + g < a.P ? a.w0[n * a.P + 4 * s + g] : 0.f;
+  }
+  f32x4 g0[AT_W0], g1[AT_W1], g2[AT_W2], gf[AT_WF];
+#pragma unroll
+  for (int j = 0; j < AT_W0; ++j) g0[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < AT_W1; ++j) g1[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < AT_W2; ++j) g2[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < AT_WF; ++j) gf[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // a chunk's rows in registers: element e = tid + k NT of its [ATR][H P] block
+  float xr[AT_XPT], tr[AT_TPT];
+  auto fetch = [&](int r0) {
+    const int last = a.B - 1 - r0, HP = a.H * a.P, NO = a.NO;
+    int r = tid / HP, c = tid - r * HP;
+#pragma unroll
+    for (int k = 0; k < AT_XPT; ++k) {
+      if (r < ATR) xr[k] = a.x[(int64_t)(r0 + min(r, last)) * a.ldx + c];
+      c += NT;
+      while (c >= HP) { c -= HP; ++r; }
+    }
+#pragma unroll
+    for (int k = 0; k < AT_TPT; ++k) {
+      const int e = tid + k * NT, rr = e / NO;
+      if (rr < ATR) tr[k] = Q.t.target[(int64_t)(r0 + min(rr, last)) * Q.t.ldt + (e - rr * NO)];
+    }
+  };
+  float lsum = 0.f;  // wave 0, lanes 4 r: row slot r's loss terms, chunks in order
+  if (blockIdx.x * Q.chunks * ATR < a.B) fetch(blockIdx.x * Q.chunks * ATR);
   for (int ch = 0; ch < Q.chunks; ++ch) {
     const int r0 = (blockIdx.x * Q.chunks + ch) * ATR;
     if (r0 >= a.B) break;  // uniform
+    // per-chunk opaque copies of the shape and the lane: every stage's addresses are derived
+    // here, not hoisted out of the chunk loop (which spilled them)
+    const int H = at_opq_s(a.H), P = at_opq_s(a.P), C1 = at_opq_s(a.C1), C2 = at_opq_s(a.C2), C3 = at_opq_s(a.C3);
+    const int NO = at_opq_s(a.NO), L1 = at_opq_s(Q.L1), L2 = at_opq_s(Q.L2), k1 = at_opq_s(a.k1);
+    const int s1 = at_opq_s(a.s1), k2 = at_opq_s(a.k2), s2 = at_opq_s(a.s2);
+    const int Y0P = at_opq_s(Q.Y0P), W1P = at_opq_s(Q.W1P), W2P = at_opq_s(Q.W2P), Y2P = at_opq_s(Q.Y2P);
+    const int lane = at_opq_v(tid & 63), wave = at_opq_s(wave0), i = lane & 15, g = lane >> 4, HP = H * P;
+    float* xs = alds + at_opq_s(Q.lds[AL_XS]);   // [ATR][H][P]
+    float* y0 = alds + at_opq_s(Q.lds[AL_Y0]);   // [ATR][H][Y0P]  (then dpre0)
+    float* y1 = alds + at_opq_s(Q.lds[AL_Y1]);   // [ATR][L1][C2]  (then dpre1)
+    float* y2 = alds + at_opq_s(Q.lds[AL_Y2]);   // [ATR][Y2P]: (t, c) flatten + zero pad (then dpre2)
+    float* y3 = alds + at_opq_s(Q.lds[AL_Y3]);   // [ATR][NO]      (then dpre3)
+    float* tg = alds + at_opq_s(Q.lds[AL_TG]);   // [ATR][NO] target rows
+    const float* w1l = alds + at_opq_s(Q.lds[AL_W1]);
+    const float* w2l = alds + at_opq_s(Q.lds[AL_W2]);
+    const float* wfl = alds + at_opq_s(Q.lds[AL_WF]);
+    const float* bl = alds + at_opq_s(Q.lds[AL_BIAS]);
+    const float* one = alds + at_opq_s(Q.lds[AL_ONE]);
     const int last = a.B - 1 - r0;
-    // inputs: the chunk's history rows
-    for (int i = tid; i < ATR * H * P; i += NT) {
-      const int r = i / (H * P), k = i % (H * P);
-      xs[i] = a.x[(int64_t)(r0 + min(r, last)) * a.ldx + k];
-    }
+    __syncthreads();  // the previous chunk's last readers of xs / y0 are done (and the weights staged)
+#pragma unroll
+    for (int k = 0; k < AT_XPT; ++k)
+      if (tid + k * NT < ATR * HP) xs[tid + k * NT] = xr[k];
+#pragma unroll
+    for (int k = 0; k < AT_TPT; ++k)
+      if (tid + k * NT < ATR * NO) tg[tid + k * NT] = tr[k];
+    if (ch + 1 < Q.chunks && r0 + ATR < a.B) fetch(r0 + ATR);
     __syncthreads(); ACK(0);
-    adapt_stage(ATR * H, P, C1, a.w0, a.b0, [&](int v) { return (const float*)xs + (v / H) * (H * P) + (v % H) * P; },
-                [&](int v, int n, float y) { y0[(v / H) * (H * C1) + (v % H) * C1 + n] = y; });
+    // fc_encoder per position: y0[v][c], v = (r, t) = r H + t, K = P (W0 from registers)
+    {
+      const int ntn0 = (C1 + 15) >> 4, K40 = (P + 3) >> 2;
+      for (int tile = wave; tile < (ATR * H / 16) * ntn0; tile += NT / 64) {
+        const int mt = tile / ntn0, nt = tile - mt * ntn0;
+        const float* ap = xs + (mt * 16 + i) * P + g;
+        float av[AT_K0];
+#pragma unroll
+        for (int s = 0; s < AT_K0; ++s)
+          if (s < K40) av[s] = ap[4 * s];
+        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < AT_K0; ++s)
+          if (s < K40) acc = mfma4(av[s], w0r[s], acc);
+        const int nn = nt * 16 + i;
+        if (nn < C1) {
+          const float bn = bl[nn];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) y0[(mt * 16 + 4 * g + q) * Y0P + nn] = elu(acc[q] + bn);
+        }
+      }
+    }
     __syncthreads(); ACK(1);
-    adapt_stage(ATR * L1, k1 * C1, C2, a.w1, a.b1,
-                [&](int v) { return (const float*)y0 + (v / L1) * (H * C1) + (v % L1) * s1 * C1; },
-                [&](int v, int n, float y) { y1[(v / L1) * (L1 * C2) + (v % L1) * C2 + n] = y; });
+    // conv1: y1[(r, l)][o], window of y0 at row r, position l s1 (K = k1 Y0P, pads zero)
+    at_fwd(lane, wave, ATR * L1, C2, W1P / 4,
+           [&](int v) { return (const float*)y0 + ((v / L1) * H + (v % L1) * s1) * Y0P; }, w1l, W1P, bl + C1,
+           [&](int v, int n, float y) { y1[v * C2 + n] = y; });
     __syncthreads(); ACK(2);
-    adapt_stage(ATR * L2, k2 * C2, C3, a.w2, a.b2,
-                [&](int v) { return (const float*)y1 + (v / L2) * (L1 * C2) + (v % L2) * s2 * C2; },
-                [&](int v, int n, float y) { y2[(v / L2) * (L2 * C3) + (v % L2) * C3 + n] = y; });
+    at_fwd(lane, wave, ATR * L2, C3, W2P / 4,
+           [&](int v) { return (const float*)y1 + ((v / L2) * L1 + (v % L2) * s2) * C2; }, w2l, W2P, bl + C1 + C2,
+           [&](int v, int n, float y) { y2[(v / L2) * Y2P + (v % L2) * C3 + n] = y; });
     __syncthreads(); ACK(3);
-    adapt_stage(ATR, L2 * C3, NO, a.wf, a.bf, [&](int v) { return (const float*)y2 + v * (L2 * C3); },
-                [&](int v, int n, float y) {
-                  y3[v * NO + n] = y;
-                  if (a.out && v <= last) a.out[(int64_t)(r0 + v) * a.ldo + n] = y;
-                });
+    at_fwd(lane, wave, ATR, NO, Y2P / 4, [&](int v) { return (const float*)y2 + v * Y2P; }, wfl, Y2P,
+           bl + C1 + C2 + C3, [&](int v, int n, float y) {
+             y3[v * NO + n] = y;
+             if (a.out && v <= last) a.out[(int64_t)(r0 + v) * a.ldo + n] = y;
+           });
     __syncthreads(); ACK(4);
-    // loss rows and d(latent pre-activation): (y3 - t) / (B ||y3 - t||) * ELU'(y3); rows past B: 0
-    if (tid < ATR) {
-      const int r = tid;
+    // loss rows and dpre3 = (y3 - t) / (B ||y3 - t||) * ELU'(y3) (wave 0: 4 lanes per row; rows past B: 0)
+    if (wave == 0) {
+      const int r = lane >> 2, sub = lane & 3;
       float ss = 0.f;
-      for (int j = 0; j < NO; ++j) {
-        const float d = y3[r * NO + j] - Q.t.target[(int64_t)(r0 + min(r, last)) * Q.t.ldt + j];
+      for (int j = sub; j < NO; j += 4) {
+        const float d = y3[r * NO + j] - tg[r * NO + j];
         ss = fmaf(d, d, ss);
       }
-      const float n = sqrtf(ss);
+      ss += __shfl_xor(ss, 1);
+      ss += __shfl_xor(ss, 2);
+      const float nrm = sqrtf(ss);
       const bool ok = r <= last;
-      if (ok) lsum += n * invB;
-      const float k = ok && n > 0.f ? invB / n : 0.f;
-      for (int j = 0; j < NO; ++j) {
+      if (ok) lsum += nrm * invB;
+      const float kk = ok && nrm > 0.f ? invB / nrm : 0.f;
+      for (int j = sub; j < NO; j += 4) {
         const float y = y3[r * NO + j];
-        const float d = y - Q.t.target[(int64_t)(r0 + min(r, last)) * Q.t.ldt + j];
-        y3[r * NO + j] = k * d * elu_d(y);
+        y3[r * NO + j] = kk * (y - tg[r * NO + j]) * elu_d(y);
       }
     }
     __syncthreads(); ACK(5);
-    // fc_final: dW[j][c*L2 + t] += sum_r dpre3[r][j] y2[r][t*C3 + c]; db[j] += sum_r dpre3[r][j]
-#pragma unroll 1
-    for (int e = tid; e < Q.NP; e += NT) {
-      if (e >= off[6] && e < off[8]) {
-        float sum = 0.f;
-        if (e < off[7]) {
-          const int j = (e - off[6]) / (C3 * L2), i = (e - off[6]) % (C3 * L2), c = i / L2, t = i % L2;
-          for (int r = 0; r < ATR; ++r) sum = fmaf(y3[r * NO + j], y2[r * (L2 * C3) + t * C3 + c], sum);
-        } else {
-          const int j = e - off[7];
-          for (int r = 0; r < ATR; ++r) sum += y3[r * NO + j];
-        }
-        gacc[e] += sum;
-      }
-    }
+    // fc_final: dW[j][f] += sum_r dpre3[r][j] y2[r][f], K = rows
+    at_dw(lane, wave, gf, NO, L2 * C3, ATR / 4, true, y3 + g * NO, 4 * NO, y2 + g * Y2P, 4 * Y2P, one);
     __syncthreads(); ACK(6);
-    // dpre2[r][t*C3 + c] = (sum_j dpre3[r][j] Wf[j][t*C3 + c]) * ELU'(y2)   (a.wf in our order)
-    for (int i = tid; i < ATR * L2 * C3; i += NT) {
-      const int r = i / (L2 * C3), f = i % (L2 * C3);
-      float d = 0.f;
-      for (int j = 0; j < NO; ++j) d = fmaf(y3[r * NO + j], wfl[j * (L2 * C3) + f], d);
-      y2[i] = d * elu_d(y2[i]);
-    }
+    at_dx(lane, wave, 1, L2 * C3, 1, 1, 1, y3, NO, 0, at_opq_s(Q.NOP) / 4, wfl, Y2P, 0,
+          [&](int r, int, int n) { return y2 + r * Y2P + n; });
     __syncthreads(); ACK(7);
-    // conv2: dW[o][c][k] += sum_{r,l} dpre2[r][l][o] y1[r][(l s2 + k) C2 + c]; db[o]
-#pragma unroll 1
-    for (int e = tid; e < Q.NP; e += NT) {
-      if (e >= off[4] && e < off[6]) {
-        float sum = 0.f;
-        if (e < off[5]) {
-          const int o = (e - off[4]) / (C2 * k2), c = ((e - off[4]) / k2) % C2, k = (e - off[4]) % k2;
-          for (int r = 0; r < ATR; ++r)
-            for (int l = 0; l < L2; ++l)
-              sum = fmaf(y2[r * (L2 * C3) + l * C3 + o], y1[r * (L1 * C2) + (l * s2 + k) * C2 + c], sum);
-        } else {
-          const int o = e - off[5];
-          for (int r = 0; r < ATR; ++r)
-            for (int l = 0; l < L2; ++l) sum += y2[r * (L2 * C3) + l * C3 + o];
-        }
-        gacc[e] += sum;
-      }
-    }
+    // conv2: dW[o][k C2 + c] += sum_{r, l} dpre2[r][l][o] y1[r][l s2 + k][c]; K = (row, l = k slot)
+    at_dw(lane, wave, g2, C3, k2 * C2, ATR, g < L2, y2 + g * C3, Y2P, y1 + g * s2 * C2, L1 * C2, one);
     __syncthreads(); ACK(8);
-    // dpre1[r][p][c] = (sum_{l,k: l s2 + k = p} sum_o dpre2[r][l][o] W2[o][k C2 + c]) * ELU'(y1)
-    for (int i = tid; i < ATR * L1 * C2; i += NT) {
-      const int r = i / (L1 * C2), pc = i % (L1 * C2), pp = pc / C2, c = pc % C2;
-      float d = 0.f;
-      for (int l = 0; l < L2; ++l) {
-        const int k = pp - l * s2;
-        if (k < 0 || k >= k2) continue;
-        for (int o = 0; o < C3; ++o) d = fmaf(y2[r * (L2 * C3) + l * C3 + o], w2l[o * (k2 * C2) + k * C2 + c], d);
-      }
-      y1[i] = d * elu_d(y1[i]);
-    }
+    at_dx(lane, wave, L1, C2, L2, s2, k2, y2, Y2P, C3, at_opq_s(Q.C3P) / 4, w2l, W2P, C2,
+          [&](int r, int p, int n) { return y1 + (r * L1 + p) * C2 + n; });
     __syncthreads(); ACK(9);
-    // conv1: dW[o][c][k] += sum_{r,l} dpre1[r][l][o] y0[r][(l s1 + k) C1 + c]; db[o]. Item (o, c)
-    // carries its k1 <= 4 taps (independent sums, one dpre1 load per (r, l)); then the biases
-#pragma unroll 1
-    for (int it = tid; it < C2 * C1 + C2; it += NT) {
-      if (it < C2 * C1) {
-        const int o = it / C1, c = it % C1;
-        // taps past k1 read a clamped tap and are discarded (no branch around a load)
-        const int t1 = min(1, k1 - 1) * C1, t2 = min(2, k1 - 1) * C1, t3 = min(3, k1 - 1) * C1;
-        float s4[4] = {0.f, 0.f, 0.f, 0.f};
-        for (int r = 0; r < ATR; ++r) {
-          const float* g = y1 + r * (L1 * C2) + o;
-          const float* yr = y0 + r * (H * C1) + c;
-#pragma unroll 4
-          for (int l = 0; l < L1; ++l) {
-            const float d = g[l * C2];
-            const float* yb = yr + (l * s1) * C1;
-            const float v0 = yb[0], v1 = yb[t1], v2 = yb[t2], v3 = yb[t3];
-            s4[0] = fmaf(d, v0, s4[0]);
-            s4[1] = fmaf(d, v1, s4[1]);
-            s4[2] = fmaf(d, v2, s4[2]);
-            s4[3] = fmaf(d, v3, s4[3]);
-          }
-        }
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-          if (k < k1) gacc[off[2] + o * (C1 * k1) + c * k1 + k] += s4[k];
-      } else {
-        const int o = it - C2 * C1;
-        float sum = 0.f;
-        for (int r = 0; r < ATR; ++r)
-          for (int l = 0; l < L1; ++l) sum += y1[r * (L1 * C2) + l * C2 + o];
-        gacc[off[3] + o] += sum;
-      }
-    }
+    // conv1: dW[o][k Y0P + c] += sum_{r, l} dpre1[r][l][o] y0[r][l s1 + k][c]
+    at_dw(lane, wave, g1, C2, k1 * Y0P, ATR, g < L1, y1 + g * C2, L1 * C2, y0 + g * s1 * Y0P, H * Y0P, one);
     __syncthreads(); ACK(10);
-    // dpre0[r][t][c] = (sum_{l,k: l s1 + k = t} sum_o dpre1[r][l][o] W1[o][k C1 + c]) * ELU'(y0),
-    // two channels per item (C1 even)
-    for (int i = tid; i < ATR * H * (C1 / 2); i += NT) {
-      const int r = i / (H * (C1 / 2)), tc = i % (H * (C1 / 2)), t = tc / (C1 / 2), c = 2 * (tc % (C1 / 2));
-      float d0 = 0.f, d1 = 0.f;
-      for (int l = 0; l < L1; ++l) {
-        const int k = t - l * s1;
-        if (k < 0 || k >= k1) continue;
-        const float* w = w1l + k * C1 + c;
-        const float* g = y1 + r * (L1 * C2) + l * C2;
-#pragma unroll 4
-        for (int o = 0; o < C2; ++o) {
-          const float gv = g[o];
-          d0 = fmaf(gv, w[o * (k1 * C1)], d0);
-          d1 = fmaf(gv, w[o * (k1 * C1) + 1], d1);
-        }
-      }
-      float* y = y0 + r * (H * C1) + t * C1 + c;
-      y[0] = d0 * elu_d(y[0]);
-      y[1] = d1 * elu_d(y[1]);
-    }
+    at_dx(lane, wave, H, C1, L1, s1, k1, y1, L1 * C2, C2, at_opq_s(Q.C2P) / 4, w1l, W1P, Y0P,
+          [&](int r, int p, int n) { return y0 + (r * H + p) * Y0P + n; });
     __syncthreads(); ACK(11);
-    // fc_encoder: dW[c][p] += sum_{r,t} dpre0[r][t][c] x[r][t][p]; db[c]. Item (c, 4 p's): one
-    // dpre0 load and one float4 of x per (r, t), four independent sums
-#pragma unroll 1
-    for (int it = tid; it < C1 * (P / 4) + C1; it += NT) {
-      if (it < C1 * (P / 4)) {
-        const int c = it / (P / 4), pp = 4 * (it % (P / 4));
-        float4 s4 = {0.f, 0.f, 0.f, 0.f};
-        for (int r = 0; r < ATR; ++r)
-#pragma unroll 5
-          for (int t = 0; t < H; ++t) {
-            const float d = y0[r * (H * C1) + t * C1 + c];
-            const float4 x4 = *reinterpret_cast<const float4*>(xs + r * (H * P) + t * P + pp);
-            s4.x = fmaf(d, x4.x, s4.x);
-            s4.y = fmaf(d, x4.y, s4.y);
-            s4.z = fmaf(d, x4.z, s4.z);
-            s4.w = fmaf(d, x4.w, s4.w);
-          }
-        float* g = gacc + c * P + pp;
-        g[0] += s4.x;
-        g[1] += s4.y;
-        g[2] += s4.z;
-        g[3] += s4.w;
-      } else {
-        const int c = it - C1 * (P / 4);
-        float sum = 0.f;
-        for (int r = 0; r < ATR; ++r)
-          for (int t = 0; t < H; ++t) sum += y0[r * (H * C1) + t * C1 + c];
-        gacc[off[1] + c] += sum;
-      }
-    }
-    __syncthreads(); ACK(12);
+    // fc_encoder: dW[c][p] += sum_v dpre0[v][c] x[v][p], K = virtual rows
+    at_dw(lane, wave, g0, C1, P, ATR * H / 4, true, y0 + g * Y0P, 4 * Y0P, xs + g * P, 4 * P, one);
+    ACK(12);
   }
-  for (int e = tid; e < Q.NP; e += NT) Q.t.gws[(int64_t)blockIdx.x * Q.NP + e] = gacc[e];
+  {
+    const int C1 = a.C1, C2 = a.C2, C3 = a.C3, NO = a.NO, P = a.P, k1 = a.k1, k2 = a.k2, L2 = Q.L2, Y0P = Q.Y0P;
+    const int lane = tid & 63;
+    float* row = Q.t.gws + (int64_t)blockIdx.x * Q.NP;
+    const int* off = Q.off;
+    at_dw_store(lane, wave0, g0, C1, P, row, [&](int m, int n) { return n < P ? off[0] + m * P + n : off[1] + m; });
+    at_dw_store(lane, wave0, g1, C2, k1 * Y0P, row, [&](int m, int n) {
+      if (n == k1 * Y0P) return off[3] + m;
+      const int k = n / Y0P, c = n - k * Y0P;
+      return c < C1 ? off[2] + m * (C1 * k1) + c * k1 + k : -1;
+    });
+    at_dw_store(lane, wave0, g2, C3, k2 * C2, row, [&](int m, int n) {
+      if (n == k2 * C2) return off[5] + m;
+      const int k = n / C2, c = n - k * C2;
+      return off[4] + m * (C2 * k2) + c * k2 + k;
+    });
+    at_dw_store(lane, wave0, gf, NO, L2 * C3, row, [&](int m, int n) {
+      if (n == L2 * C3) return off[7] + m;
+      const int t = n / C3, c = n - t * C3;
+      return off[6] + m * (C3 * L2) + c * L2 + t;
+    });
+    if (wave0 == 0 && (lane & 3) == 0) lrow[lane >> 2] = lsum;
+  }
 #ifdef LGX_ADAPT_CLOCK
   if (tid == 0 && g_adclk)
     for (int q = 0; q < 16; ++q) g_adclk[(size_t)blockIdx.x * 16 + q] = ck[q];
 #endif
-  if (tid < ATR) lrow[tid] = lsum;
-  __syncthreads(); ACK(13);
+  __syncthreads();
   if (tid == 0) {
     float l = 0.f;
     for (int r = 0; r < ATR; ++r) l += lrow[r];
@@ -1203,6 +1320,45 @@ __global__ __launch_bounds__(256) void transpose_batch_kernel(TransposeBatch b) 
       if (c < d.cols && r < d.rows) d.dst[(int64_t)c * d.rows + r] = tile[tx][ty + k];
     }
     __syncthreads();
+  }
+}
+
+// clip_grad_norm_ + Adam over one small flat segment in ONE block (the DAgger step of the
+// adaptation encoder, rsl_rl ppo.py:336-345): ||g||_2 in a fixed order (thread partials over a
+// stride, then a tree), coef = min(max_norm / (||g|| + 1e-6), 1), g *= coef in place (torch keeps
+// the clipped gradient), step += 1, and lgx_adam_step's arithmetic with the clipped gradient.
+constexpr int CLIP_ADAM_NT = 1024;
+__global__ __launch_bounds__(CLIP_ADAM_NT) void clip_adam_kernel(float* __restrict__ p, float* __restrict__ g,
+                                                                  float* __restrict__ m, float* __restrict__ v, int n,
+                                                                  const float* __restrict__ lr_dev, float lr, float b1,
+                                                                  float b2, float eps, float* __restrict__ step,
+                                                                  float max_norm, float* __restrict__ coef_out) {
+  __shared__ float red[CLIP_ADAM_NT];
+  const int tid = threadIdx.x;
+  float ss = 0.f;
+  for (int i = tid; i < n; i += CLIP_ADAM_NT) ss = fmaf(g[i], g[i], ss);
+  red[tid] = ss;
+  __syncthreads();
+  for (int w = CLIP_ADAM_NT / 2; w > 0; w >>= 1) {
+    if (tid < w) red[tid] += red[tid + w];
+    __syncthreads();
+  }
+  const float coef = fminf(max_norm / (sqrtf(red[0]) + 1e-6f), 1.f);
+  const float t = *step + 1.f;
+  const float lr_ = lr_dev ? *lr_dev : lr;
+  const float step_size = lr_ / (1.f - powf(b1, t)), bc2s = sqrtf(1.f - powf(b2, t));
+  for (int i = tid; i < n; i += CLIP_ADAM_NT) {
+    const float gc = g[i] * coef;
+    g[i] = gc;
+    float P = p[i], M = m[i], V = v[i];
+    adam1(P, gc, M, V, b1, b2, eps, step_size, bc2s);
+    p[i] = P;
+    m[i] = M;
+    v[i] = V;
+  }
+  if (tid == 0) {
+    *step = t;
+    if (coef_out) *coef_out = coef;
   }
 }
 
@@ -2642,6 +2798,17 @@ int32_t lgx_adam_step(float* param, const float* grad, float* exp_avg, float* ex
   return e == hipSuccess ? 0 : fail(hipGetErrorString(e));
 }
 
+int32_t lgx_clip_adam(float* param, float* grad, float* exp_avg, float* exp_avg_sq, int64_t n, const float* lr_dev,
+                      float lr, float beta1, float beta2, float eps, float* step, float max_norm, float* coef_out,
+                      void* stream) {
+  if (n < 1 || n > LGX_CLIP_ADAM_MAX) return fail("lgx_clip_adam: 1 <= n <= LGX_CLIP_ADAM_MAX");
+  if (!param || !grad || !exp_avg || !exp_avg_sq || !step) return fail("lgx_clip_adam: null pointer");
+  hipLaunchKernelGGL(lgxm::clip_adam_kernel, dim3(1), dim3(lgxm::CLIP_ADAM_NT), 0, static_cast<hipStream_t>(stream),
+                     param, grad, exp_avg, exp_avg_sq, (int)n, lr_dev, lr, beta1, beta2, eps, step, max_norm, coef_out);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : fail(hipGetErrorString(e));
+}
+
 static int head_check(const lgx_ppo_head_args* a) {
   if (!a) return fail("lgx_ppo_head: null args");
   if (a->A < 1 || a->A > lgxm::HMAXA) return fail("lgx_ppo_head: 1 <= A <= 16");
@@ -3039,29 +3206,45 @@ int32_t lgx_adaptation_train(const lgx_adapt_train_args* t, void* stream) {
   Q.L1 = (a->H - a->k1) / a->s1 + 1;
   Q.L2 = (Q.L1 - a->k2) / a->s2 + 1;
   if (a->H < a->k1 || Q.L1 < a->k2) return fail("lgx_adaptation_train: history shorter than a kernel");
-  if (a->P % 4 || a->C1 % 2 || a->k1 > 4) return fail("lgx_adaptation_train: P % 4 == 0, C1 even, k1 <= 4");
   if (!a->x || a->ldx < (int64_t)a->H * a->P || !a->w0 || !a->b0 || !a->w1 || !a->b1 || !a->w2 || !a->b2 || !a->wf ||
       !a->bf || (a->out && a->ldo < a->NO) || !t->target || t->ldt < a->NO || !t->gws || !t->loss_ws)
     return fail("lgx_adaptation_train: bad operands");
+  auto r4 = [](int v) { return (v + 3) / 4 * 4; };
+  auto tiles = [](int m, int n) { return ((m + 15) / 16) * ((n + 15) / 16); };
+  Q.Y0P = a->C1 | 1;  // odd pitch: the conv1 windows of a 16-row tile spread over the banks
+  Q.W1P = r4(a->k1 * Q.Y0P);
+  Q.W2P = r4(a->k2 * a->C2);
+  Q.Y2P = r4(Q.L2 * a->C3);
+  Q.C2P = r4(a->C2);
+  Q.C3P = r4(a->C3);
+  Q.NOP = r4(a->NO);
+  const int ntn0 = (a->C1 + 15) / 16;
+  if (Q.L1 > 4 || Q.L2 > 4 || 4 % ntn0 || (a->P + 3) / 4 > AT_K0 || ATR * a->H * a->P > AT_XPT * NT ||
+      ATR * a->NO > AT_TPT * NT || tiles(a->C1, a->P + 1) > 4 * AT_W0 || tiles(a->C2, a->k1 * Q.Y0P + 1) > 4 * AT_W1 ||
+      tiles(a->C3, a->k2 * a->C2 + 1) > 4 * AT_W2 || tiles(a->NO, Q.L2 * a->C3 + 1) > 4 * AT_WF)
+    return fail("lgx_adaptation_train: encoder shape outside the fused kernel's tiling");
   const int sizes[8] = {a->C1 * a->P, a->C1, a->C2 * a->C1 * a->k1, a->C2, a->C3 * a->C2 * a->k2, a->C3,
                         a->NO * a->C3 * Q.L2, a->NO};
   Q.off[0] = 0;
   for (int i = 0; i < 8; ++i) Q.off[i + 1] = Q.off[i] + sizes[i];
   Q.NP = Q.off[8];
+  const int region[AL_END] = {ATR * a->H * a->P, ATR * a->H * Q.Y0P, ATR * Q.L1 * a->C2, ATR * Q.Y2P, ATR * a->NO,
+                              ATR * a->NO, Q.C2P * Q.W1P, Q.C3P * Q.W2P, Q.NOP * Q.Y2P,
+                              a->C1 + a->C2 + a->C3 + a->NO, 8};
+  Q.lds[0] = 0;
+  for (int i = 0; i < AL_END; ++i) Q.lds[i + 1] = Q.lds[i] + r4(region[i]);
+  const int64_t bytes = (int64_t)Q.lds[AL_END] * 4;
+  if (bytes > 80 * 1024 || (int64_t)a->B * a->ldx > INT32_MAX)
+    return fail("lgx_adaptation_train: sizes beyond the fused kernel's LDS / 32-bit offsets");
   const int nchunk = (a->B + ATR - 1) / ATR;
   Q.chunks = (nchunk + t->blocks - 1) / t->blocks;
   const unsigned grid = (unsigned)((nchunk + Q.chunks - 1) / Q.chunks);
-  const int64_t floats = (int64_t)ATR * ((int64_t)a->H * a->P + (int64_t)a->H * a->C1 + (int64_t)Q.L1 * a->C2 +
-                                        (int64_t)Q.L2 * a->C3 + a->NO) + Q.NP +
-                         (int64_t)a->C2 * a->k1 * a->C1 + (int64_t)a->C3 * a->k2 * a->C2 + (int64_t)a->NO * Q.L2 * a->C3;
-  if (floats * 4 > 96 * 1024 || (int64_t)a->B * a->ldx > INT32_MAX)
-    return fail("lgx_adaptation_train: sizes beyond the fused kernel's LDS / 32-bit offsets");
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)adapt_train_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+    (void)hipFuncSetAttribute((const void*)adapt_train_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
     attr = true;
   }
-  hipLaunchKernelGGL(adapt_train_kernel, dim3(grid), dim3(NT), (size_t)floats * 4, static_cast<hipStream_t>(stream), Q);
+  hipLaunchKernelGGL(adapt_train_kernel, dim3(grid), dim3(NT), (size_t)bytes, static_cast<hipStream_t>(stream), Q);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : fail(hipGetErrorString(e));
 }

@@ -51,7 +51,7 @@ GRAPH_ALLREDUCE = os.environ.get("LGX_GRAPH_ALLREDUCE", "0") != "0"
 # the DAgger minibatch as one fused launch (lgx_adaptation_train) + one reduce, instead of the
 # adaptation encoder's autograd graph
 DAGGER_FUSED = os.environ.get("LGX_DAGGER_FUSED", "1") != "0"
-DAGGER_BLOCKS = 512  # lgx_adaptation_train's block budget (two per CU: 64 KB of LDS each)
+DAGGER_BLOCKS = 512  # lgx_adaptation_train's block budget (two per CU: <= 80 KB of LDS each)
 
 
 def _distributed():
@@ -864,9 +864,10 @@ class PPO:
         the adaptation segment must hold exactly those parameters' gradients, in that order."""
         ac = self.actor_critic
         mod = ac.adaptation_encoder_
-        conv1 = mod.conv_layers[0]
-        if ac.num_proprio % 4 or mod.fc_encoder[0].out_features % 2 or conv1.kernel_size[0] > 4:
-            return False  # outside lgx_adaptation_train's shapes
+        if not hip_mlp.adaptation_train_supported(mod, ac.num_proprio):
+            return False  # outside lgx_adaptation_train's tiling
+        if adapt.numel() > 65536:
+            return False  # lgx_clip_adam's one-block segment
         ps = hip_mlp.adaptation_param_order(mod)
         off = adapt.data_ptr()
         for p in ps:
@@ -879,7 +880,7 @@ class PPO:
         """The DAgger minibatches with the adaptation encoder's forward, loss and backward in ONE
         launch each (lgx_adaptation_train: per-block gradient rows), the rows summed into the flat
         gradient segment and the loss into the running sum by one reduce launch, then the clip and
-        Adam of _dagger_body (ppo.py:336-345)."""
+        Adam of _dagger_body (ppo.py:336-345) as one lgx_clip_adam launch: 3 launches per minibatch."""
         from legged_gym_custom_amd.rsl_rl.modules import hip_s8 as S
         ac = self.actor_critic
         hist_cols = ac.num_proprio * ac.history_buffer_length
@@ -901,9 +902,16 @@ class PPO:
                 if _distributed():
                     dist.all_reduce(adapt)
                     adapt.div_(dist.get_world_size())
-                with torch.no_grad():
-                    _clip_([adapt], self.max_grad_norm)
-                    self._adam("adaptation_optimizer", self._adapt_lr)
+                self._clip_adam("adaptation_optimizer", self._adapt_lr)
+
+    def _clip_adam(self, name, lr):
+        """clip_grad_norm_ of this optimizer's segment (in place) + its Adam step in one launch
+        (lgx_clip_adam; the segment is small: the adaptation encoder)."""
+        opt = getattr(self, name)
+        b1, b2 = opt.param_groups[0]["betas"]
+        a, b = self.grads.slices[self._segment_of[name]]
+        hip_mlp.clip_adam(self.params_buf[a:b], self.grads.buf[a:b], self.exp_avg[a:b], self.exp_avg_sq[a:b],
+                          self._opt_step[name], lr, b1, b2, opt.param_groups[0]["eps"], self.max_grad_norm)
 
     def _dagger_body_cpu(self):
         """The CPU learner's DAgger update (the reference's statement order, per-minibatch

@@ -20,7 +20,7 @@ import torch.nn as nn
 _LIB_PATH = os.environ.get("LGX_MLP_LIB") or os.path.join(
     os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))), "lib", "liblgx_mlp.so")
 _lib = None
-ABI_VERSION = 9
+ABI_VERSION = 10
 EPI_BIAS, EPI_ELU, EPI_DELU, EPI_ACCUM = 1, 2, 4, 8
 EXPORTED = ["lgx_mlp_abi_version", "lgx_mlp_sizeof_gemm_args", "lgx_mlp_pick_split", "lgx_gemm",
             "lgx_mlp_last_error", "lgx_adam_step", "lgx_ppo_head_forward", "lgx_ppo_head_backward",
@@ -29,7 +29,7 @@ EXPORTED = ["lgx_mlp_abi_version", "lgx_mlp_sizeof_gemm_args", "lgx_mlp_pick_spl
             "lgx_mlp_pick_split_group", "lgx_gae", "lgx_normalize_advantages",
             "lgx_gather_rows", "lgx_transpose_batch", "lgx_loss_heads_forward", "lgx_loss_heads_backward",
             "lgx_track_episodes", "lgx_chain", "lgx_adaptation_forward", "lgx_loss_heads_fused",
-            "lgx_loss_heads_tail", "lgx_adaptation_train"]
+            "lgx_loss_heads_tail", "lgx_adaptation_train", "lgx_clip_adam"]
 TAIL_MAX_LOSSES = 8
 COPY_MAX = 16
 SPLITK_MAX = 24
@@ -173,7 +173,7 @@ class AdaptTrainArgs(C.Structure):
                 ("loss_ws", C.c_void_p), ("blocks", C.c_int32)]
 
 
-ADAPT_TRAIN_ROWS = 8  # rows per chunk of lgx_adaptation_train (lgx_mlp.hip ATR)
+ADAPT_TRAIN_ROWS = 16  # rows per chunk of lgx_adaptation_train (lgx_mlp.hip ATR)
 
 
 def adapt_train_grid(rows, blocks):
@@ -181,6 +181,28 @@ def adapt_train_grid(rows, blocks):
     nchunk = (rows + ADAPT_TRAIN_ROWS - 1) // ADAPT_TRAIN_ROWS
     chunks = (nchunk + blocks - 1) // blocks
     return (nchunk + chunks - 1) // chunks
+
+
+def adaptation_train_supported(mod, P):
+    """Whether lgx_adaptation_train's tiling covers this encoder (the checks of its C entry point:
+    16-row chunks, <= 4 positions after each convolution, the per-wave weight-gradient tiles, the
+    fc_encoder fragment in registers, 80 KB of LDS)."""
+    H = mod.history_buffer_length
+    C1, C2, C3, k1, s1, k2, s2, L1, L2 = _conv_dims(mod, H)
+    NO = mod.fc_final[0].weight.shape[0]
+    r4 = lambda v: (v + 3) // 4 * 4
+    tiles = lambda m, n: ((m + 15) // 16) * ((n + 15) // 16)
+    Y0P = C1 | 1
+    if L1 < 1 or L2 < 1 or L1 > 4 or L2 > 4 or 4 % ((C1 + 15) // 16) or (P + 3) // 4 > 16:
+        return False
+    if ADAPT_TRAIN_ROWS * H * P > 36 * 256 or ADAPT_TRAIN_ROWS * NO > 2 * 256:
+        return False
+    if tiles(C1, P + 1) > 8 or tiles(C2, k1 * Y0P + 1) > 16 or tiles(C3, k2 * C2 + 1) > 4 or \
+            tiles(NO, L2 * C3 + 1) > 4:
+        return False
+    regions = [16 * H * P, 16 * H * Y0P, 16 * L1 * C2, 16 * r4(L2 * C3), 16 * NO, 16 * NO,
+               r4(C2) * r4(k1 * Y0P), r4(C3) * r4(k2 * C2), r4(NO) * r4(L2 * C3), C1 + C2 + C3 + NO, 8]
+    return 4 * sum(r4(r) for r in regions) <= 80 * 1024
 
 
 def adaptation_param_order(mod):
@@ -244,6 +266,8 @@ def lib():
     L.lgx_ppo_head_backward.restype = C.c_int32
     L.lgx_adam_step.argtypes = [vp, vp, vp, vp, C.c_int64, vp, f32, f32, f32, f32, vp, vp, vp]
     L.lgx_adam_step.restype = C.c_int32
+    L.lgx_clip_adam.argtypes = [vp, vp, vp, vp, C.c_int64, vp, f32, f32, f32, f32, vp, f32, vp, vp]
+    L.lgx_clip_adam.restype = C.c_int32
     L.lgx_copy_batch.argtypes = [vp, C.c_int32, vp]
     L.lgx_copy_batch.restype = C.c_int32
     L.lgx_act_head.argtypes = [vp, vp]
@@ -417,6 +441,16 @@ def gae(rewards, dones, values, last_values, returns, advantages, gamma, lam, mo
 def normalize_advantages(advantages, moments, count):
     _check(lib().lgx_normalize_advantages(advantages.data_ptr(), advantages.numel(), moments.data_ptr(), float(count),
                                           _stream()), "lgx_normalize_advantages")
+
+
+def clip_adam(p, g, m, v, step, lr, beta1, beta2, eps, max_norm, coef_out=None):
+    """lgx_clip_adam: clip_grad_norm_(g, max_norm) in place, step += 1 and one Adam step over one
+    small flat segment (<= 65536 entries), in one launch; lr: float or 0-dim device tensor."""
+    lr_dev = lr.data_ptr() if isinstance(lr, torch.Tensor) else None
+    lr_f = 0.0 if isinstance(lr, torch.Tensor) else float(lr)
+    _check(lib().lgx_clip_adam(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), g.numel(), lr_dev, lr_f,
+                               float(beta1), float(beta2), float(eps), step.data_ptr(), float(max_norm),
+                               None if coef_out is None else coef_out.data_ptr(), _stream()), "lgx_clip_adam")
 
 
 def adam_step(p, g, m, v, step, lr, beta1, beta2, eps, grad_scale=None):
