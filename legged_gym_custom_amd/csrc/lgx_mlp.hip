@@ -981,6 +981,10 @@ __device__ __forceinline__ int at_opq_v(int v) {
   return v;
 }
 
+// a workgroup barrier over LDS only: the chunk's global prefetch stays in flight across it
+// (__syncthreads() waits vmcnt(0) first, which exposed the prefetch at the next barrier)
+__device__ __forceinline__ void at_bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 #ifdef LGX_ADAPT_CLOCK
 __device__ uint32_t* g_adclk = nullptr;
 #endif
@@ -1075,7 +1079,7 @@ __global__ __launch_bounds__(NT, 2) void adapt_train_kernel(AdaptTrainParams Q) 
     const float* bl = alds + at_opq_s(Q.lds[AL_BIAS]);
     const float* one = alds + at_opq_s(Q.lds[AL_ONE]);
     const int last = a.B - 1 - r0;
-    __syncthreads();  // the previous chunk's last readers of xs / y0 are done (and the weights staged)
+    at_bar();  // the previous chunk's last readers of xs / y0 are done (and the weights staged)
 #pragma unroll
     for (int k = 0; k < AT_XPT; ++k)
       if (tid + k * NT < ATR * HP) xs[tid + k * NT] = xr[k];
@@ -1083,7 +1087,7 @@ __global__ __launch_bounds__(NT, 2) void adapt_train_kernel(AdaptTrainParams Q) 
     for (int k = 0; k < AT_TPT; ++k)
       if (tid + k * NT < ATR * NO) tg[tid + k * NT] = tr[k];
     if (ch + 1 < Q.chunks && r0 + ATR < a.B) fetch(r0 + ATR);
-    __syncthreads(); ACK(0);
+    at_bar(); ACK(0);
     // fc_encoder per position: y0[v][c], v = (r, t) = r H + t, K = P (W0 from registers)
     {
       const int ntn0 = (C1 + 15) >> 4, K40 = (P + 3) >> 2;
@@ -1106,22 +1110,22 @@ __global__ __launch_bounds__(NT, 2) void adapt_train_kernel(AdaptTrainParams Q) 
         }
       }
     }
-    __syncthreads(); ACK(1);
+    at_bar(); ACK(1);
     // conv1: y1[(r, l)][o], window of y0 at row r, position l s1 (K = k1 Y0P, pads zero)
     at_fwd(lane, wave, ATR * L1, C2, W1P / 4,
            [&](int v) { return (const float*)y0 + ((v / L1) * H + (v % L1) * s1) * Y0P; }, w1l, W1P, bl + C1,
            [&](int v, int n, float y) { y1[v * C2 + n] = y; });
-    __syncthreads(); ACK(2);
+    at_bar(); ACK(2);
     at_fwd(lane, wave, ATR * L2, C3, W2P / 4,
            [&](int v) { return (const float*)y1 + ((v / L2) * L1 + (v % L2) * s2) * C2; }, w2l, W2P, bl + C1 + C2,
            [&](int v, int n, float y) { y2[(v / L2) * Y2P + (v % L2) * C3 + n] = y; });
-    __syncthreads(); ACK(3);
+    at_bar(); ACK(3);
     at_fwd(lane, wave, ATR, NO, Y2P / 4, [&](int v) { return (const float*)y2 + v * Y2P; }, wfl, Y2P,
            bl + C1 + C2 + C3, [&](int v, int n, float y) {
              y3[v * NO + n] = y;
              if (a.out && v <= last) a.out[(int64_t)(r0 + v) * a.ldo + n] = y;
            });
-    __syncthreads(); ACK(4);
+    at_bar(); ACK(4);
     // loss rows and dpre3 = (y3 - t) / (B ||y3 - t||) * ELU'(y3) (wave 0: 4 lanes per row; rows past B: 0)
     if (wave == 0) {
       const int r = lane >> 2, sub = lane & 3;
@@ -1141,25 +1145,25 @@ __global__ __launch_bounds__(NT, 2) void adapt_train_kernel(AdaptTrainParams Q) 
         y3[r * NO + j] = kk * (y - tg[r * NO + j]) * elu_d(y);
       }
     }
-    __syncthreads(); ACK(5);
+    at_bar(); ACK(5);
     // fc_final: dW[j][f] += sum_r dpre3[r][j] y2[r][f], K = rows
     at_dw(lane, wave, gf, NO, L2 * C3, ATR / 4, true, y3 + g * NO, 4 * NO, y2 + g * Y2P, 4 * Y2P, one);
-    __syncthreads(); ACK(6);
+    at_bar(); ACK(6);
     at_dx(lane, wave, 1, L2 * C3, 1, 1, 1, y3, NO, 0, at_opq_s(Q.NOP) / 4, wfl, Y2P, 0,
           [&](int r, int, int n) { return y2 + r * Y2P + n; });
-    __syncthreads(); ACK(7);
+    at_bar(); ACK(7);
     // conv2: dW[o][k C2 + c] += sum_{r, l} dpre2[r][l][o] y1[r][l s2 + k][c]; K = (row, l = k slot)
     at_dw(lane, wave, g2, C3, k2 * C2, ATR, g < L2, y2 + g * C3, Y2P, y1 + g * s2 * C2, L1 * C2, one);
-    __syncthreads(); ACK(8);
+    at_bar(); ACK(8);
     at_dx(lane, wave, L1, C2, L2, s2, k2, y2, Y2P, C3, at_opq_s(Q.C3P) / 4, w2l, W2P, C2,
           [&](int r, int p, int n) { return y1 + (r * L1 + p) * C2 + n; });
-    __syncthreads(); ACK(9);
+    at_bar(); ACK(9);
     // conv1: dW[o][k Y0P + c] += sum_{r, l} dpre1[r][l][o] y0[r][l s1 + k][c]
     at_dw(lane, wave, g1, C2, k1 * Y0P, ATR, g < L1, y1 + g * C2, L1 * C2, y0 + g * s1 * Y0P, H * Y0P, one);
-    __syncthreads(); ACK(10);
+    at_bar(); ACK(10);
     at_dx(lane, wave, H, C1, L1, s1, k1, y1, L1 * C2, C2, at_opq_s(Q.C2P) / 4, w1l, W1P, Y0P,
           [&](int r, int p, int n) { return y0 + (r * H + p) * Y0P + n; });
-    __syncthreads(); ACK(11);
+    at_bar(); ACK(11);
     // fc_encoder: dW[c][p] += sum_v dpre0[v][c] x[v][p], K = virtual rows
     at_dw(lane, wave, g0, C1, P, ATR * H / 4, true, y0 + g * Y0P, 4 * Y0P, xs + g * P, 4 * P, one);
     ACK(12);

@@ -2,8 +2,9 @@
 (RCCL: the "nccl" backend), on ONE GPU: a world-size-1 RCCL group with the distributed path
 forced on (PPO.allreduce_always), so every minibatch runs the all-reduce of [main | estimator |
 kl] between its backward and its optimizer tail (ppo.py:273-276) — eagerly in one run, inside the
-captured graph in the other. Graph == eager, bit for bit, over three updates; the graph mode is
-"whole" (no per-minibatch replays around host-issued collectives)."""
+captured graph in the other. Graph == eager, bit for bit, over three updates; with
+LGX_GRAPH_ALLREDUCE=1 the graph mode is "whole" (no per-minibatch replays around host-issued
+collectives; without it, the default, "phased")."""
 import os
 import queue
 import socket
@@ -27,7 +28,10 @@ def _port():
 
 def _worker(rank, port, out):
     sys.path.insert(0, HERE)
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
+    # the in-graph collective is opt-in (LGX_GRAPH_ALLREDUCE; phased graphs are the default at
+    # world size > 1): set before the learner is imported in this spawned process
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1",
+                      LGX_GRAPH_ALLREDUCE="1")
     import torch.distributed as dist
     import learner_case as LC
     import learner_replay as R
