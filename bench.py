@@ -168,7 +168,10 @@ def committed_valu(num_envs):
     if not files:
         return None
     vals = {}
+    kname = "lgx::env_step_kernel"
     for line in open(files[-1]):
+        if "kernel void " in line:  # the header names the profiled instance
+            kname = line.split("kernel void ", 1)[1].split("(", 1)[0].strip()
         f = line.split()
         if len(f) == 2 and f[0].isupper():
             try:
@@ -180,7 +183,7 @@ def committed_valu(num_envs):
     cyc = vals["GRBM_GUI_ACTIVE"] / 8
     used = 2 * vals["SQ_INSTS_VALU"]
     cap = 1024 * cyc
-    out = {"bound": "valu", "kernel": "lgx::env_step_kernel<true, false, false>",
+    out = {"bound": "valu", "kernel": kname,
            "achieved": round(used / 1e6, 1), "peak": round(cap / 1e6, 1), "unit": "M VALU issue cycles per launch",
            "frac": round(used / cap, 4), "valu_instructions_per_env_step": round(vals["SQ_INSTS_VALU"] / num_envs),
            "source": os.path.relpath(files[-1], ROOT)}
@@ -189,7 +192,8 @@ def committed_valu(num_envs):
     if "SQ_INSTS_LDS" in vals:
         out["lds_instructions_per_env_step"] = round(vals["SQ_INSTS_LDS"] / num_envs)
     out["note"] = ("VALU pipe partly busy; the waves wait on LDS / memory (wait_fraction) and on dependent "
-                   "DPP / readlane chains: latency-bound at 4 waves per SIMD (DESIGN.md 4.1)")
+                   "DPP / readlane chains: latency-bound (4096 envs fill one wave slot each: 2 waves per SIMD "
+                   "at two envs per wavefront, DESIGN.md 4.1)")
     return out
 
 
