@@ -406,9 +406,10 @@ def main():
 
     if rank == 0:
         terrain = env.cfg.terrain.mesh_type in ("heightfield", "trimesh")
-        # two envs per wavefront (EPW 2) for an even env count without the actuator net (lgx_env.hip launch_step)
+        # two envs per wavefront (EPW 2) by default on the plane with an even env count (lgx_env.hip launch_step)
         actnet = bool(getattr(env.cfg.control, "use_actuator_network", False))
-        epw = 2 if (env.num_envs % 2 == 0 and not actnet and os.environ.get("LGX_ENVS_PER_WAVE") != "1") else 1
+        epw = 2 if (env.num_envs % 2 == 0 and not actnet and not terrain and
+                    os.environ.get("LGX_ENVS_PER_WAVE") != "1") else 1
         kname = f"lgx::env_step_kernel<true, {'true' if terrain else 'false'}, {'true' if actnet else 'false'}, {epw}>"
         data = ("synthetic (Go2 flat terrain, random-init ActorCritic/estimator, seed 1)" if args.task == "go2" else
                 f"synthetic ({args.task}: generated terrain, random-init ActorCritic/estimator, seed 1)")

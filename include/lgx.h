@@ -351,11 +351,12 @@ int lgx_episode_extras(lgx_env* env, float* means, float* level_mean, uint8_t* t
  * happens on other steps. Needs params.command_curriculum and the three buffers bound. */
 int lgx_command_curriculum(lgx_env* env, uint64_t seed, uint64_t step_counter, const uint64_t* d_step_counter,
                            const double* global_sum_count, void* hip_stream);
-/* ABI 6. Envs per wavefront of the step kernel: 2 (the default, for an even env count without
- * the actuator net: each env on 32 lanes, two envs' work per instruction in the phases that use
- * a few dozen lanes; an env with more than 32 constraint rows is solved on the whole wave), or 1
- * (one env per 64-lane wave). The numbers are the same either way; 0 restores the default
- * (environment variable LGX_ENVS_PER_WAVE=1 changes the default). */
+/* ABI 6. Envs per wavefront of the step kernel: 2 (each env on 32 lanes, two envs' work per
+ * instruction in the phases that use a few dozen lanes; an env with more than 32 constraint rows
+ * is solved on the whole wave; even env counts without the actuator net only) or 1 (one env per
+ * 64-lane wave). The numbers are the same either way. 0 restores the default: 2 on the plane, 1
+ * on heightfield / trimesh terrain (faster there) and with the actuator net (environment
+ * variable LGX_ENVS_PER_WAVE=1 makes 1 the default everywhere). */
 int lgx_set_envs_per_wave(lgx_env* env, int32_t envs_per_wave);
 const char* lgx_last_error(const lgx_env* env);
 void lgx_destroy(lgx_env* env);

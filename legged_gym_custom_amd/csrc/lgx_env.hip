@@ -2471,15 +2471,18 @@ static int launch_step(lgx_env* env, uint64_t seed, uint64_t step, const uint64_
     HIP_OK(hipMemsetAsync(env->buffers.episode_stats, 0, sizeof(float) * (KS + 1), st));
   env->stats_clean = false;
   // compiled variants: the plane/PD path (the benchmark) carries no terrain or LSTM code. Two
-  // envs per wave (EPW 2: 32 lanes each, lgx_env.hip grp_of_lane) for an even env count without
-  // the actuator net (its LSTM lanes need the whole wave); LGX_ENVS_PER_WAVE=1 selects one env
-  // per wave (A/B, tests)
+  // envs per wave (EPW 2: 32 lanes each, lgx_env.hip grp_of_lane) by default on the plane with an
+  // even env count (measured: Go2 4096 envs 184 -> 177 us); on a trimesh the one-env kernel is
+  // faster (go2_parkour 8192 envs: 423 vs 491 us), so there EPW 2 only when asked for
+  // (lgx_set_envs_per_wave); never with the actuator net (its LSTM lanes need the whole wave).
+  // LGX_ENVS_PER_WAVE=1 selects one env per wave (A/B, tests)
   const bool terrain = env->params.mesh_type != LGX_MESH_PLANE, actnet = env->params.actuator_net != 0;
   static const int epw_env = [] {
     const char* v = getenv("LGX_ENVS_PER_WAVE");
     return v && atoi(v) == 1 ? 1 : 2;
   }();
-  const int epw = (!actnet && N % 2 == 0 && (env->epw ? env->epw : epw_env) == 2) ? 2 : 1;
+  const int want = env->epw ? env->epw : (terrain ? 1 : epw_env);
+  const int epw = (!actnet && N % 2 == 0 && want == 2) ? 2 : 1;
   auto kern = epw == 2 ? (!physics ? lgx::env_step_kernel<false, false, false, 2>
                                    : (terrain ? lgx::env_step_kernel<true, true, false, 2>
                                               : lgx::env_step_kernel<true, false, false, 2>))

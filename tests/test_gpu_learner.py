@@ -128,10 +128,10 @@ def test_gae_kernel_matches_torch_statement():
 @pytest.mark.parametrize("B", [16 * 300 + 5, 24576])
 def test_adaptation_train_matches_autograd_fp64(B):
     """lgx_adaptation_train (one DAgger minibatch of the adaptation encoder in one launch, lgx_mlp
-    ABI 9) against torch autograd in fp64 on the same weights and rows: the summed per-block
-    gradient rows of every parameter within 2e-4 * max|g| + 1e-7 (the forward is the 3 x bf16
-    fused forward, the backward fp32) and the loss within 1e-5 relative; fixed-order sums: two
-    launches give identical rows."""
+    ABI 9/10) against torch autograd in fp64 on the same weights and rows: the summed per-block
+    gradient rows of every parameter within 2e-4 * max|g| + 1e-7 (every stage on f32-input MFMA:
+    exact f32 products, fp32 sums) and the loss within 1e-5 relative; B = 4805 ends in a partial
+    16-row chunk; fixed-order sums: two launches give identical rows."""
     from legged_gym_custom_amd.rsl_rl.modules import hip_mlp as H
     from legged_gym_custom_amd.rsl_rl.modules.support_networks import AdaptationEncoder, AdaptationEncoderTS
     torch.manual_seed(5)
@@ -158,10 +158,42 @@ def test_adaptation_train_matches_autograd_fp64(B):
     loss = (target.double().cpu() - lat).norm(p=2, dim=1).mean()
     loss.backward()
     ref_ps = H.adaptation_param_order(ref)
-    o = 0
+    o, worst = 0, 0.0
     for p, rp in zip(ps, ref_ps):
         g, rg = got[o:o + p.numel()].cpu().view_as(rp), rp.grad
         o += p.numel()
         err = float((g - rg).abs().max())
+        worst = max(worst, err / float(rg.abs().max()))
         assert err <= 2e-4 * float(rg.abs().max()) + 1e-7, (tuple(p.shape), err, float(rg.abs().max()))
+    print(f"B={B}: worst gradient |err| / max|g| = {worst:.2e}")
     assert abs(float(lws.double().sum()) - float(loss.detach())) <= 1e-5 * float(loss.detach())
+
+
+@pytest.mark.parametrize("n,scale", [(5040, 0.01), (5040, 10.0), (40001, 1.0)])
+def test_clip_adam_matches_clip_grad_norm_and_adam(n, scale):
+    """lgx_clip_adam (ABI 10: the DAgger step's clip_grad_norm_ + Adam in one block) against the
+    torch statement it replaces (ppo.py:336-345): g *= min(max_norm / (||g|| + 1e-6), 1) in place,
+    then Adam (torch's arithmetic, as lgx_adam_step) — with the clip inactive (small gradient) and
+    active; the step counter advanced on the device."""
+    from legged_gym_custom_amd.rsl_rl.modules import hip_mlp as H
+    torch.manual_seed(n)
+    dev = "cuda:0"
+    p, g = torch.randn(n, device=dev), torch.randn(n, device=dev) * scale
+    m, v = torch.randn(n, device=dev) * 0.01, torch.rand(n, device=dev) * 1e-4
+    step = torch.full((), 3.0, device=dev)
+    p0, g0, m0, v0 = (t.double().cpu() for t in (p, g, m, v))
+    lr, b1, b2, eps, max_norm = 1e-3, 0.9, 0.999, 1e-8, 1.0
+    H.clip_adam(p, g, m, v, step, lr, b1, b2, eps, max_norm)
+    torch.cuda.synchronize()
+    coef = min(max_norm / (float(g0.norm()) + 1e-6), 1.0)
+    gc = g0 * coef
+    t = 4.0
+    b1, b2 = (float(torch.tensor(b, dtype=torch.float32)) for b in (b1, b2))  # the kernel's fp32 betas (torch's fused Adam)
+    m1 = b1 * m0 + (1 - b1) * gc
+    v1 = b2 * v0 + (1 - b2) * gc * gc
+    p1 = p0 - (lr / (1 - b1 ** t)) * m1 / (v1.sqrt() / (1 - b2 ** t) ** 0.5 + eps)
+    assert float(step) == t
+    torch.testing.assert_close(g.double().cpu(), gc, rtol=2e-6, atol=1e-12)
+    torch.testing.assert_close(m.double().cpu(), m1, rtol=2e-6, atol=1e-8)  # (0.9 m + 0.1 g) cancels
+    torch.testing.assert_close(v.double().cpu(), v1, rtol=2e-6, atol=1e-14)
+    torch.testing.assert_close(p.double().cpu(), p1, rtol=1e-6, atol=2e-7)

@@ -1,5 +1,5 @@
-"""Two envs per wavefront (lgx_set_envs_per_wave, the default for an even env count without the
-actuator net) against one env per wavefront: from the same state, one step of each kernel gives
+"""Two envs per wavefront (lgx_set_envs_per_wave; the default on the plane for an even env count,
+selectable on a trimesh) against one env per wavefront: from the same state, one step of each kernel gives
 the same discrete outcome (resets, time-outs, episode lengths, contact flags) and the same
 continuous state within fp32 rounding — the two instantiations contract multiply-adds into FMAs
 in different places (the physics is compiled with fp contract(fast)), so the last bits of a few
