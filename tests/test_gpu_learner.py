@@ -129,8 +129,8 @@ def test_gae_kernel_matches_torch_statement():
 def test_adaptation_train_matches_autograd_fp64(B):
     """lgx_adaptation_train (one DAgger minibatch of the adaptation encoder in one launch, lgx_mlp
     ABI 9/10) against torch autograd in fp64 on the same weights and rows: the summed per-block
-    gradient rows of every parameter within 2e-4 * max|g| + 1e-7 (every stage on f32-input MFMA:
-    exact f32 products, fp32 sums) and the loss within 1e-5 relative; B = 4805 ends in a partial
+    gradient rows of every parameter within 5e-6 * max|g| (every stage on f32-input MFMA: exact
+    f32 products, fp32 sums; measured 1e-7) and the loss within 1e-5 relative; B = 4805 ends in a partial
     16-row chunk; fixed-order sums: two launches give identical rows."""
     from legged_gym_custom_amd.rsl_rl.modules import hip_mlp as H
     from legged_gym_custom_amd.rsl_rl.modules.support_networks import AdaptationEncoder, AdaptationEncoderTS
@@ -164,7 +164,7 @@ def test_adaptation_train_matches_autograd_fp64(B):
         o += p.numel()
         err = float((g - rg).abs().max())
         worst = max(worst, err / float(rg.abs().max()))
-        assert err <= 2e-4 * float(rg.abs().max()) + 1e-7, (tuple(p.shape), err, float(rg.abs().max()))
+        assert err <= 5e-6 * float(rg.abs().max()) + 1e-9, (tuple(p.shape), err, float(rg.abs().max()))
     print(f"B={B}: worst gradient |err| / max|g| = {worst:.2e}")
     assert abs(float(lws.double().sum()) - float(loss.detach())) <= 1e-5 * float(loss.detach())
 
