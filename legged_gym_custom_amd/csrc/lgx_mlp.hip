@@ -3452,8 +3452,29 @@ __global__ __launch_bounds__(1024) void track_kernel(lgx_track_args a) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int chunk = (a.N + 1023) / 1024;
   const int i0 = min(tid * chunk, a.N), i1 = min(i0 + chunk, a.N);
+  const int64_t ptr = *a.ptr;  // every thread reads it before thread 0 moves it (barriers below)
+  // 4 or 8 envs per thread with aligned rows (N = 4096 / 8192): the thread's rows as float4 /
+  // 4-byte loads, all issued before any use — one memory round trip instead of one per env
+  const bool vec = (chunk == 4 || chunk == 8) && a.N % chunk == 0 &&
+                   ((reinterpret_cast<uintptr_t>(a.cur_rew) | reinterpret_cast<uintptr_t>(a.cur_len) |
+                     reinterpret_cast<uintptr_t>(a.rewards)) & 15) == 0 && (reinterpret_cast<uintptr_t>(a.dones) & 3) == 0;
+  float4 cr[2], rw[2], cl[2];
+  uint32_t dn[2] = {0u, 0u};
   int cnt = 0;
-  for (int i = i0; i < i1; ++i) cnt += a.dones[i] != 0;
+  if (vec) {
+    const int nv = chunk / 4, q0 = tid * nv;
+    for (int v = 0; v < 2; ++v) {
+      if (v >= nv || i0 >= i1) continue;
+      cr[v] = reinterpret_cast<const float4*>(a.cur_rew)[q0 + v];
+      cl[v] = reinterpret_cast<const float4*>(a.cur_len)[q0 + v];
+      rw[v] = reinterpret_cast<const float4*>(a.rewards)[q0 + v];
+      dn[v] = reinterpret_cast<const uint32_t*>(a.dones)[q0 + v];
+    }
+    for (int v = 0; v < 2; ++v)
+      for (int e = 0; e < 4; ++e) cnt += ((dn[v] >> (8 * e)) & 0xffu) != 0u;
+  } else {
+    for (int i = i0; i < i1; ++i) cnt += a.dones[i] != 0;
+  }
   // inclusive scan over the block: within the wave by shuffles, then over the 16 waves
   int x = cnt;
   for (int o = 1; o < 64; o <<= 1) {
@@ -3474,22 +3495,42 @@ __global__ __launch_bounds__(1024) void track_kernel(lgx_track_args a) {
   __syncthreads();
   const int k = k_all;
   int rank = wsum[wv] + x - cnt;  // exclusive prefix of this thread's chunk
-  const int64_t ptr = *a.ptr;
-  for (int i = i0; i < i1; ++i) {
-    const float r = a.cur_rew[i] + a.rewards[i];
-    const float l = a.cur_len[i] + 1.0f;
-    if (a.dones[i]) {
+  // env i's update; returns its new (cur_rew, cur_len)
+  auto one = [&](float cur_r, float rew, float cur_l, bool done, float& nr, float& nl) {
+    const float r = cur_r + rew;
+    const float l = cur_l + 1.0f;
+    if (done) {
       if (rank >= k - 100) {
         const int slot = (int)((ptr + rank) % 100);
         a.rew_ring[slot] = r;
         a.len_ring[slot] = l;
       }
       ++rank;
-      a.cur_rew[i] = 0.f;
-      a.cur_len[i] = 0.f;
+      nr = 0.f;
+      nl = 0.f;
     } else {
-      a.cur_rew[i] = r;
-      a.cur_len[i] = l;
+      nr = r;
+      nl = l;
+    }
+  };
+  if (vec) {
+    const int nv = chunk / 4, q0 = tid * nv;
+    for (int v = 0; v < 2; ++v) {
+      if (v >= nv || i0 >= i1) continue;
+      float4 R, L;
+      one(cr[v].x, rw[v].x, cl[v].x, (dn[v] & 0xffu) != 0u, R.x, L.x);
+      one(cr[v].y, rw[v].y, cl[v].y, ((dn[v] >> 8) & 0xffu) != 0u, R.y, L.y);
+      one(cr[v].z, rw[v].z, cl[v].z, ((dn[v] >> 16) & 0xffu) != 0u, R.z, L.z);
+      one(cr[v].w, rw[v].w, cl[v].w, ((dn[v] >> 24) & 0xffu) != 0u, R.w, L.w);
+      reinterpret_cast<float4*>(a.cur_rew)[q0 + v] = R;
+      reinterpret_cast<float4*>(a.cur_len)[q0 + v] = L;
+    }
+  } else {
+    for (int i = i0; i < i1; ++i) {
+      float nr, nl;
+      one(a.cur_rew[i], a.rewards[i], a.cur_len[i], a.dones[i] != 0, nr, nl);
+      a.cur_rew[i] = nr;
+      a.cur_len[i] = nl;
     }
   }
   __syncthreads();  // every thread read *ptr before it moves

@@ -501,8 +501,12 @@ static_assert(sizeof(SplitBatch) <= 4096, "kernel argument segment");
 // group t & 7 of rows (t >> 3) + 32 it (fixed order). Wide jobs: block = SPLIT_WIDE (row, group)
 // items, so a few-row job (a weight matrix) still spreads over many blocks.
 __global__ __launch_bounds__(256) void s8_split_kernel(SplitBatch b) {
-  int ji = 0;
-  while (ji + 1 < b.n && (int)blockIdx.x >= b.j[ji + 1].blk0) ++ji;
+  int ji = 0, hi = b.n - 1;  // the block's job: binary search on the jobs' first blocks
+  while (ji < hi) {
+    const int mid = (ji + hi + 1) >> 1;
+    if ((int)blockIdx.x >= b.j[mid].blk0) ji = mid;
+    else hi = mid - 1;
+  }
   const SplitJob J = b.j[ji];
   const int blk = blockIdx.x - J.blk0;
   const int rbase = blk * LGX_S8_SPLIT_ROWS;
@@ -584,7 +588,7 @@ __global__ __launch_bounds__(256) void s8_split_kernel(SplitBatch b) {
 
 struct ReduceBatch {
   int n;
-  int64_t start[LGX_S8_BATCH_MAX + 1];  // first thread of each job (wave jobs: 64-aligned)
+  int64_t start[LGX_S8_BATCH_MAX + 1];  // first thread of each job (256-aligned: one job per block)
   lgx_s8_reduce_args j[LGX_S8_BATCH_MAX];
   unsigned char wave[LGX_S8_BATCH_MAX];  // one wave per output (long sums: the bias partials)
   unsigned char vec[LGX_S8_BATCH_MAX];   // 4 consecutive outputs per thread (flat, 16-B aligned jobs)
@@ -592,10 +596,18 @@ struct ReduceBatch {
 static_assert(sizeof(ReduceBatch) <= 4096, "kernel argument segment");
 
 __global__ __launch_bounds__(256) void s8_reduce_kernel(ReduceBatch b) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  // jobs start at multiples of 256 threads: a block belongs to one job, found by a binary search
+  // on the block's first thread (wave-uniform: scalar loads of the job, no per-lane job fetch)
+  const int64_t b0 = (int64_t)blockIdx.x * 256;
+  int lo = 0, hi = b.n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (b.start[mid] <= b0) lo = mid;
+    else hi = mid - 1;
+  }
+  const int ji = __builtin_amdgcn_readfirstlane(lo);
+  const int64_t i = b0 + threadIdx.x;
   if (i >= b.start[b.n]) return;
-  int ji = 0;
-  while (ji + 1 < b.n && i >= b.start[ji + 1]) ++ji;
   const lgx_s8_reduce_args& J = b.j[ji];
   if (b.wave[ji]) {
     // a long sum (one partial per 128-row tile): lane l takes partials l, l + 64, ... in order,
@@ -884,7 +896,7 @@ int32_t lgx_s8_reduce(const lgx_s8_reduce_args* a, int32_t n, void* stream) {
     b.wave[k] = a[i].nsplit >= 64 && (int64_t)a[i].rows * a[i].cols <= 4096;
     b.vec[k] = !b.wave[k] && a[i].rows == 1 && a[i].cols % 4 == 0 && a[i].stride % 4 == 0 &&
                ((((uintptr_t)a[i].ws) | ((uintptr_t)a[i].out)) & 15) == 0;
-    if (b.wave[k]) b.start[k] = (b.start[k] + 63) / 64 * 64;
+    b.start[k] = (b.start[k] + 255) / 256 * 256;  // one job per block (s8_reduce_kernel)
     b.start[k + 1] = b.start[k] + (b.vec[k] ? a[i].cols / 4 : (int64_t)a[i].rows * a[i].cols * (b.wave[k] ? 64 : 1));
     ++k;
   }

@@ -158,14 +158,16 @@ def test_act_head_feeds_env_the_stored_actions():
         assert stored.std() > 0.3  # really sampled
 
 
-def test_native_episode_tracking_matches_torch_statement():
+@pytest.mark.parametrize("n", [4096, 8192, 100, 12289])
+def test_native_episode_tracking_matches_torch_statement(n):
     """lgx_track_episodes == the runner's torch statement of on_policy_runner.py:160-170,
     bitwise, over steps with many (> 100, exercising keep-the-last-100) and few dones, with
-    infos['episode'] as the env lays it out (episode means + a separate terrain-level mean)."""
+    infos['episode'] as the env lays it out (episode means + a separate terrain-level mean).
+    n = 4096 / 8192: each thread's 4 / 8 envs as vector loads; 100 / 12289: the per-env loop."""
     import types
     import torch
     from legged_gym_custom_amd.rsl_rl.runners.on_policy_runner import OnPolicyRunner
-    dev, n = "cuda", 4096
+    dev = "cuda"
 
     def stats():
         z = lambda *sh: torch.zeros(*sh, device=dev)  # noqa: E731
