@@ -275,6 +275,25 @@ __device__ __forceinline__ void epi_act(const Prob& P, float* img, int m_base, i
 #pragma unroll
     for (int e = 0; e < 8; ++e) bias[e] = (P.epi & LGX_S8_EPI_BIAS) && n + e < P.N ? P.bias[n + e] : 0.f;
   }
+  // DX: the ELU' operand y (the layer below's S8 output) of every row slot requested before the
+  // first use — one memory round trip for the tile instead of one per row slot (a load after a
+  // store of the previous slot cannot be hoisted: the compiler cannot rule out aliasing).
+  // Clamped rows / groups: no load under a condition.
+  constexpr int NIT = KIND == LGX_S8_FWD ? 1 : ROWS / RS;
+  u32x4 yh[NIT], yl[NIT];
+  const bool delu = KIND != LGX_S8_FWD && (P.epi & LGX_S8_EPI_DELU);
+  if constexpr (KIND != LGX_S8_FWD) {
+    if (delu) {
+      const int64_t gofs = (int64_t)(std::min(n, P.N - 1) >> 3) * 32;
+#pragma unroll
+      for (int it = 0; it < NIT; ++it) {
+        const int m = std::min(m_base + r0 + RS * it, P.M - 1);
+        const char* src = P.act + (int64_t)m * P.ld_act + gofs;
+        yh[it] = reinterpret_cast<const u32x4*>(src)[0];
+        yl[it] = reinterpret_cast<const u32x4*>(src)[1];
+      }
+    }
+  }
 #pragma unroll
   for (int it = 0; it < ROWS / RS; ++it) {
     const int h = RS * it / LGX_S8_TILE_M;  // compile-time: r0 < RS and RS divides 128
@@ -291,9 +310,14 @@ __device__ __forceinline__ void epi_act(const Prob& P, float* img, int m_base, i
         for (int e = 0; e < 8; ++e) v[e] = elu(v[e]);
       }
     } else {
-      if (P.epi & LGX_S8_EPI_DELU) {
+      if (delu) {  // y = hi + lo, as load_s8
+        const int q = KIND == LGX_S8_FWD ? 0 : it;
         float y[8];
-        load_s8(P.act + (int64_t)m * P.ld_act + (n >> 3) * 32, y);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          y[2 * e] = __uint_as_float(yh[q][e] << 16) + __uint_as_float(yl[q][e] << 16);
+          y[2 * e + 1] = __uint_as_float(yh[q][e] & 0xffff0000u) + __uint_as_float(yl[q][e] & 0xffff0000u);
+        }
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] *= y[e] > 0.f ? 1.f : y[e] + 1.f;
       }

@@ -11,7 +11,7 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "lib", "liblgx_s8.so")
+_LIB_PATH = os.environ.get("LGX_S8_LIB") or os.path.join(os.path.dirname(os.path.dirname(_HERE)), "lib", "liblgx_s8.so")  # env: A/B builds
 _lib = None
 
 ABI_VERSION = 3
