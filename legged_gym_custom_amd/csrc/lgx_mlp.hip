@@ -2715,9 +2715,10 @@ __global__ __launch_bounds__(256) void transition_kernel(lgx_transition_args p) 
   if (i >= p.B) return;
   const float v = p.values[i];
   float r = p.rewards[i];
+  const bool d = p.dones[i] != 0;  // every load before the first store (no aliasing stall)
   if (p.time_outs) r = r + p.gamma * (v * (float)p.time_outs[i]);
   p.rewards_out[i] = r;
-  p.dones_out[i] = p.dones[i] ? 1 : 0;
+  p.dones_out[i] = d ? 1 : 0;
   p.values_out[i] = v;
 }
 
@@ -2731,19 +2732,52 @@ __global__ __launch_bounds__(256) void gae_kernel(lgx_gae_args p) {
     const int64_t N = p.N;
     const float g = p.gamma, lam = p.lam;
     float adv = 0.f;
-    for (int t = p.T - 1; t >= 0; --t) {
-      const int64_t i = (int64_t)t * N + n;
-      const float v = p.values[i];
-      const float next = t == p.T - 1 ? p.last_values[n] : p.values[i + N];
-      const float nt = 1.0f - (float)p.dones[i];
-      const float delta = (p.rewards[i] + (nt * g) * next) - v;
-      adv = delta + ((nt * g) * lam) * adv;
-      const float ret = adv + v;
-      const float a = ret - v;
-      p.returns[i] = ret;
-      p.advantages[i] = a;
-      s1 += (double)a;
-      s2 += (double)a * (double)a;
+    // the env's rows of up to GT steps requested before the recursion (the stores of returns /
+    // advantages would otherwise hold each step's loads behind the previous step's stores: one
+    // memory round trip per step); clamped steps, no load under a condition
+    constexpr int GT = 32;
+    const int T = p.T;
+    if (T <= GT) {
+      float vv[GT], rr[GT], dd[GT];
+#pragma unroll
+      for (int t = 0; t < GT; ++t) {
+        const int64_t i = (int64_t)min(t, T - 1) * N + n;
+        vv[t] = p.values[i];
+        rr[t] = p.rewards[i];
+        dd[t] = (float)p.dones[i];
+      }
+      const float last = p.last_values[n];
+#pragma unroll
+      for (int t = GT - 1; t >= 0; --t) {
+        if (t >= T) continue;
+        const int64_t i = (int64_t)t * N + n;
+        const float v = vv[t];
+        const float next = t == T - 1 ? last : vv[t + 1 < GT ? t + 1 : t];
+        const float nt = 1.0f - dd[t];
+        const float delta = (rr[t] + (nt * g) * next) - v;
+        adv = delta + ((nt * g) * lam) * adv;
+        const float ret = adv + v;
+        const float a = ret - v;
+        p.returns[i] = ret;
+        p.advantages[i] = a;
+        s1 += (double)a;
+        s2 += (double)a * (double)a;
+      }
+    } else {
+      for (int t = T - 1; t >= 0; --t) {
+        const int64_t i = (int64_t)t * N + n;
+        const float v = p.values[i];
+        const float next = t == T - 1 ? p.last_values[n] : p.values[i + N];
+        const float nt = 1.0f - (float)p.dones[i];
+        const float delta = (p.rewards[i] + (nt * g) * next) - v;
+        adv = delta + ((nt * g) * lam) * adv;
+        const float ret = adv + v;
+        const float a = ret - v;
+        p.returns[i] = ret;
+        p.advantages[i] = a;
+        s1 += (double)a;
+        s2 += (double)a * (double)a;
+      }
     }
   }
   for (int o = 32; o > 0; o >>= 1) {
