@@ -2356,8 +2356,8 @@ __device__ __forceinline__ void body4(int64_t lo, int64_t hi, int64_t& a, int64_
   b = max(a, hi & ~(int64_t)3);
 }
 
-// squared norm partial of one thread: float4 body, two loads in flight per pass, four
-// accumulators (one per lane of the float4) combined in a fixed order
+// squared norm partial of one thread: float4 body, four loads in flight per pass, four
+// accumulators (one per lane of the float4) combined in a fixed order (the float4s in index order)
 __device__ __forceinline__ float sumsq_range(const float* __restrict__ g, int64_t lo, int64_t hi, int64_t i0,
                                              int64_t stride) {
   int64_t a, b;
@@ -2366,12 +2366,16 @@ __device__ __forceinline__ float sumsq_range(const float* __restrict__ g, int64_
   const float4* g4 = reinterpret_cast<const float4*>(g + a);
   const int64_t n4 = (b - a) >> 2;
   int64_t j = i0;
-  for (; j + stride < n4; j += 2 * stride) {
-    const float4 x = g4[j], y = g4[j + stride];
-    s0 += x.x * x.x; s1 += x.y * x.y; s2 += x.z * x.z; s3 += x.w * x.w;
-    s0 += y.x * y.x; s1 += y.y * y.y; s2 += y.z * y.z; s3 += y.w * y.w;
+  for (; j + 3 * stride < n4; j += 4 * stride) {
+    float4 x[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) x[u] = g4[j + u * stride];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      s0 += x[u].x * x[u].x; s1 += x[u].y * x[u].y; s2 += x[u].z * x[u].z; s3 += x[u].w * x[u].w;
+    }
   }
-  if (j < n4) {
+  for (; j < n4; j += stride) {
     const float4 x = g4[j];
     s0 += x.x * x.x; s1 += x.y * x.y; s2 += x.z * x.z; s3 += x.w * x.w;
   }
@@ -2427,7 +2431,11 @@ __device__ __forceinline__ void adam_range(const lgx_ppo_tail_args& p, int64_t l
   const float4* G = reinterpret_cast<const float4*>(p.grads + a);
   float4* M = reinterpret_cast<float4*>(p.exp_avg + a);
   float4* V = reinterpret_cast<float4*>(p.exp_avg_sq + a);
-  for (int64_t j = i0; j < (b - a) >> 2; j += stride) {
+  // one float4 item per pass (4 items per pass with every load before the first store measured
+  // slower: 13.1 -> 15.5 us per launch)
+  const int64_t n4 = (b - a) >> 2;
+  int64_t j = i0;
+  for (; j < n4; j += stride) {
     float4 x = P[j], m = M[j], v = V[j];
     const float4 g = G[j];
     adam1(x.x, g.x * c, m.x, v.x, b1, b2, eps, ss, sq);
