@@ -281,6 +281,7 @@ __device__ __forceinline__ void epi_act(const Prob& P, float* img, int m_base, i
   // Clamped rows / groups: no load under a condition.
   constexpr int NIT = KIND == LGX_S8_FWD ? 1 : ROWS / RS;
   u32x4 yh[NIT], yl[NIT];
+  float adv[NIT][8];  // the addend (the regulariser's latent gradient), requested the same way
   const bool delu = KIND != LGX_S8_FWD && (P.epi & LGX_S8_EPI_DELU);
   if constexpr (KIND != LGX_S8_FWD) {
     if (delu) {
@@ -291,6 +292,14 @@ __device__ __forceinline__ void epi_act(const Prob& P, float* img, int m_base, i
         const char* src = P.act + (int64_t)m * P.ld_act + gofs;
         yh[it] = reinterpret_cast<const u32x4*>(src)[0];
         yl[it] = reinterpret_cast<const u32x4*>(src)[1];
+      }
+    }
+    if (P.addend != nullptr && P.add_cols > 0) {
+#pragma unroll
+      for (int it = 0; it < NIT; ++it) {
+        const int m = std::min(m_base + r0 + RS * it, P.M - 1);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) adv[it][e] = P.addend[(int64_t)m * P.ld_add + std::min(n + e, P.add_cols - 1)];
       }
     }
   }
@@ -321,10 +330,11 @@ __device__ __forceinline__ void epi_act(const Prob& P, float* img, int m_base, i
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] *= y[e] > 0.f ? 1.f : y[e] + 1.f;
       }
-      if (P.addend != nullptr) {
+      if (P.addend != nullptr && P.add_cols > 0) {
+        const int q = KIND == LGX_S8_FWD ? 0 : it;
 #pragma unroll
         for (int e = 0; e < 8; ++e)
-          if (n + e < P.add_cols) v[e] += P.addend[(int64_t)m * P.ld_add + n + e];
+          if (n + e < P.add_cols) v[e] += adv[q][e];
       }
     }
 #pragma unroll

@@ -7,5 +7,4 @@ timeout -k 10 500 python -u -m pytest -x -q --timeout 200 --timeout-method threa
 for v in new old new old; do
   if [ $v = old ]; then export LGX_S8_LIB=$R/exp/s8_old.so; else unset LGX_S8_LIB; fi
   echo "== $v"; bash tools/gpu/prof_bench.sh 2>&1 | grep -E "s8_gemm_kernel" || exit 1
-  python -c "import json; b=json.loads(open('$R/gpurun_out/prof_bench/b.log').read().strip().splitlines()[-1]); print('value', b['value'], 'learn_s', b['learn_s'])"
 done
