@@ -116,16 +116,19 @@ typedef struct lgx_adapt_args {
   float* out; int64_t ldo;
 } lgx_adapt_args;
 int32_t lgx_adaptation_forward(const lgx_adapt_args* a, void* stream);
-/* ABI 9. One DAgger minibatch of the adaptation encoder (rsl_rl ppo.py:309-349: adaptation
- * forward, loss = mean_i ||target_i - latent_i||_2, backward) in ONE launch: the forward as
- * lgx_adaptation_forward (f.out optional), then per row the loss term and the backward of every
- * layer (fp32), the weight / bias gradients of the block's rows summed in row order into one
- * partial row per block: gws[block][NP] in the flat parameter layout (fc_encoder w, b, conv1 w
- * [out][in][k], b, conv2 w, b, fc_final w [out][c * L2 + t], b; NP their total) and
- * loss_ws[block] = sum of the block's ||.|| / B. The grid is min(blocks, ceil(B/8)) blocks over
- * 8-row chunks; the caller sums the partial rows (the gradient and the loss). P % 4 == 0, C1
- * even, k1 <= 4. f.w1 / f.w2 /
- * f.wf in lgx_adaptation_forward's layouts (tap-major, (t, c) flatten). */
+/* ABI 9 (f32-MFMA form: ABI 10). One DAgger minibatch of the adaptation encoder (rsl_rl
+ * ppo.py:309-349: adaptation forward, loss = mean_i ||target_i - latent_i||_2, backward) in ONE
+ * launch. A block walks 16-row chunks with everything in LDS; every stage (the four forward
+ * layers, each input gradient, each weight gradient) is a GEMM on v_mfma_f32_16x16x4_f32 (exact
+ * f32 products, fp32 sums; f.out, the latent, optional). The weight / bias gradients of the
+ * block's rows are summed in a fixed order into one partial row per block: gws[block][NP] in the
+ * flat parameter layout (fc_encoder w, b, conv1 w [out][in][k], b, conv2 w, b, fc_final w
+ * [out][c * L2 + t], b; NP their total), and loss_ws[block] = sum of the block's ||.|| / B. The
+ * grid is min(blocks, ceil(B/16)) blocks; the caller sums the partial rows (the gradient and the
+ * loss). Shapes outside the kernel's tiling return an error (hip_mlp.adaptation_train_supported
+ * states them: <= 4 positions after each convolution, P <= 64, C1 <= 32 or 64, the per-wave
+ * weight-gradient tiles, <= 80 KB of LDS). f.w1 / f.w2 / f.wf in lgx_adaptation_forward's
+ * layouts (tap-major, (t, c) flatten). */
 typedef struct lgx_adapt_train_args {
   lgx_adapt_args f;
   const float* target; int64_t ldt;
