@@ -6,5 +6,5 @@ cd $R
 timeout -k 10 500 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_s8.py tests/test_gpu_s8_update.py tests/test_gpu_learner_golden.py 2>&1 | tail -1
 for v in new old new old; do
   if [ $v = old ]; then export LGX_S8_LIB=$R/exp/s8_old.so; else unset LGX_S8_LIB; fi
-  echo "== $v"; bash tools/gpu/prof_bench.sh 2>&1 | grep -E "s8_gemm_kernel" || exit 1
+  echo "== $v"; bash tools/gpu/prof_bench.sh 2>&1 | grep -E "s8_gemm_kernel|chain_kernel<2" || exit 1
 done
