@@ -197,6 +197,41 @@ def committed_valu(num_envs):
     return out
 
 
+LIB_OVERRIDES = ("LGX_LIB", "LGX_MLP_LIB", "LGX_S8_LIB")
+
+
+def refuse_overrides():
+    """The bench measures the in-tree product libraries only: a library-path override (dev builds)
+    is refused, not recorded."""
+    bad = [k for k in LIB_OVERRIDES if os.environ.get(k)]
+    if bad:
+        sys.exit(f"bench.py: refusing to run with library override(s) {bad}: the bench measures the in-tree "
+                 f"legged_gym_custom_amd/lib/*.so only")
+
+
+def loaded_binaries():
+    """The native libraries this process actually mapped (from /proc/self/maps), each with its
+    path and sha256: which binaries produced the line."""
+    import hashlib
+    paths = set()
+    try:
+        for line in open("/proc/self/maps"):
+            f = line.split()
+            if len(f) >= 6 and f[-1].endswith(".so") and "liblgx" in os.path.basename(f[-1]):
+                paths.add(f[-1])
+    except OSError:
+        return None
+    out = {}
+    for pth in sorted(paths):
+        h = hashlib.sha256()
+        with open(pth, "rb") as fh:
+            for chunk in iter(lambda: fh.read(1 << 20), b""):
+                h.update(chunk)
+        out[os.path.basename(pth)] = {"path": os.path.relpath(pth, ROOT) if pth.startswith(ROOT) else pth,
+                                      "sha256": h.hexdigest()}
+    return out
+
+
 def cpu_baseline(num_envs=4096, iters=3, steps_per_env=24):
     """The same framework on the host: `--sim_device=cpu --rl_device=cpu` (helpers.py:174-177)
     — liblgx.so's host backend (OpenMP over envs) for the env step and the torch-CPU rsl_rl
@@ -304,6 +339,7 @@ def main():
     ap.add_argument("--task", default="go2", help="go2 (the BASELINE metric) | go2_parkour (C4) | anymal_c_rough "
                                                   "(C3: rollout only)")
     args = ap.parse_args()
+    refuse_overrides()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -408,8 +444,7 @@ def main():
         terrain = env.cfg.terrain.mesh_type in ("heightfield", "trimesh")
         # two envs per wavefront (EPW 2) by default on the plane with an even env count (lgx_env.hip launch_step)
         actnet = bool(getattr(env.cfg.control, "use_actuator_network", False))
-        epw = 2 if (env.num_envs % 2 == 0 and not actnet and not terrain and
-                    os.environ.get("LGX_ENVS_PER_WAVE") != "1") else 1
+        epw = 2 if (env.num_envs % 2 == 0 and not actnet and not terrain) else 1
         kname = f"lgx::env_step_kernel<true, {'true' if terrain else 'false'}, {'true' if actnet else 'false'}, {epw}>"
         data = ("synthetic (Go2 flat terrain, random-init ActorCritic/estimator, seed 1)" if args.task == "go2" else
                 f"synthetic ({args.task}: generated terrain, random-init ActorCritic/estimator, seed 1)")
@@ -430,7 +465,11 @@ def main():
             "paths": {"learner": "s8" if runner.alg._s8 is not None else "autograd",
                       "act": "fused" if runner.alg._s8act is not None else "grouped",
                       "graph_mode": runner.alg.graph_mode,
+                      "dagger": runner.alg.dagger_path, "dagger_graph_mode": runner.alg.dagger_graph_mode,
                       "rollout_graphs": sorted(str(k) for k in runner._graphs)},
+            # the native libraries that ran (mapped by this process) and any LGX_* variables set
+            "binaries": loaded_binaries(),
+            "env_overrides": {k: v for k, v in sorted(os.environ.items()) if k.startswith("LGX_")},
             "collection_s": round(perf.get("collection_time", 0.0), 4),
             "learn_s": round(perf.get("learn_time", 0.0), 4),
             "env_kernel": {"avg_us": round(kern_avg_ms * 1e3, 2), "min_us": round(kern_ms[0] * 1e3, 2),

@@ -12,9 +12,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 INC = os.path.join(os.path.dirname(HERE), "include")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 LIBS = {
-    "liblgx.so": (["lgx_env.hip"], ["lgx_device.h", "lgx_host.h", "lgx_env_host.cpp"], ["lgx.h"]),
-    "liblgx_mlp.so": (["lgx_mlp.hip"], [], ["lgx_mlp.h"]),
-    "liblgx_s8.so": (["lgx_s8.hip", "lgx_act.hip", "lgx_s8chain.hip"], [], ["lgx_s8.h"]),
+    "liblgx.so": (["lgx_env.hip"], ["lgx_device.h", "lgx_host.h", "lgx_env_host.cpp", "lgx_knobs.h"], ["lgx.h"]),
+    "liblgx_mlp.so": (["lgx_mlp.hip"], ["lgx_knobs.h"], ["lgx_mlp.h"]),
+    "liblgx_s8.so": (["lgx_s8.hip", "lgx_act.hip", "lgx_s8chain.hip"], ["lgx_knobs.h"], ["lgx_s8.h"]),
 }
 OUT = os.path.join(HERE, "lib", "liblgx.so")
 OUT_MLP = os.path.join(HERE, "lib", "liblgx_mlp.so")
@@ -52,9 +52,10 @@ def _host_objects(name, verbose):
 
 
 def build_one(name, force=False, verbose=False):
+    """Compile one library if a source is newer than it (or force). Returns (path, compiled?)."""
     src, _, out = _paths(name)
     if not force and not needs_build(name):
-        return out
+        return out, False
     os.makedirs(os.path.dirname(out), exist_ok=True)
     hip = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off"]
     extra = _host_objects(name, verbose)
@@ -68,6 +69,20 @@ def build_one(name, force=False, verbose=False):
             print(" ".join(cmd))
         subprocess.run(cmd, check=True)
     os.replace(out + ".tmp", out)
+    return out, True
+
+
+def build_variant(name, out, flags, verbose=True):
+    """A dev build of one library (e.g. liblgx_s8.so with -DLGX_DEV_KNOBS or -DLGX_S8_CLOCK) at `out`;
+    the product path never loads it (bench.py refuses LGX_*_LIB overrides)."""
+    src, _, _ = _paths(name)
+    hip = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off"] + list(flags)
+    if name == "liblgx.so":
+        return build_env_variant(out, flags, verbose)
+    cmd = hip + ["-shared", "-o", out] + src
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
     return out
 
 
@@ -85,7 +100,9 @@ def build_env_variant(out, flags, verbose=True):
 
 def build(force=False, verbose=False):
     for name in LIBS:
-        build_one(name, force=force, verbose=verbose)
+        out, compiled = build_one(name, force=force, verbose=verbose)
+        if verbose:
+            print(f"build_native: {name}: {'compiled' if compiled else 'reused (up to date)'} -> {out}")
     return OUT
 
 

@@ -17,6 +17,7 @@
 // Post-physics (Go2Robot.post_physics_step go2.py:345-387, LeggedRobot legged_robot.py:
 //   103-138): uniform scalar control flow per env; vector outputs written lane-parallel.
 #include <hip/hip_runtime.h>
+#include "lgx_knobs.h"
 #include <math.h>
 #include <stddef.h>
 #include <stdint.h>
@@ -2478,7 +2479,7 @@ static int launch_step(lgx_env* env, uint64_t seed, uint64_t step, const uint64_
   // LGX_ENVS_PER_WAVE=1 selects one env per wave (A/B, tests)
   const bool terrain = env->params.mesh_type != LGX_MESH_PLANE, actnet = env->params.actuator_net != 0;
   static const int epw_env = [] {
-    const char* v = getenv("LGX_ENVS_PER_WAVE");
+    const char* v = LGX_DEV_KNOB("LGX_ENVS_PER_WAVE");
     return v && atoi(v) == 1 ? 1 : 2;
   }();
   const int want = env->epw ? env->epw : (terrain ? 1 : epw_env);

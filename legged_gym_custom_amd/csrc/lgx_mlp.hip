@@ -23,6 +23,7 @@
 //   weight grad split-K partials to a workspace + the bias gradient (column sums of dY,
 //   taken from the unsplit fp32 values), reduced in fixed order by splitk_reduce.
 #include <hip/hip_runtime.h>
+#include "lgx_knobs.h"
 #include <algorithm>
 #include <limits.h>
 #include <stdint.h>
@@ -1339,6 +1340,10 @@ __global__ __launch_bounds__(CLIP_ADAM_NT) void clip_adam_kernel(float* __restri
                                                                   float max_norm, float* __restrict__ coef_out) {
   __shared__ float red[CLIP_ADAM_NT];
   const int tid = threadIdx.x;
+  // the step counter and the learning rate are read before the reduction's barriers: thread 0
+  // writes *step after its own Adam loop, which a late wave could otherwise already see
+  const float t = *step + 1.f;
+  const float lr_ = lr_dev ? *lr_dev : lr;
   float ss = 0.f;
   for (int i = tid; i < n; i += CLIP_ADAM_NT) ss = fmaf(g[i], g[i], ss);
   red[tid] = ss;
@@ -1348,8 +1353,6 @@ __global__ __launch_bounds__(CLIP_ADAM_NT) void clip_adam_kernel(float* __restri
     __syncthreads();
   }
   const float coef = fminf(max_norm / (sqrtf(red[0]) + 1e-6f), 1.f);
-  const float t = *step + 1.f;
-  const float lr_ = lr_dev ? *lr_dev : lr;
   const float step_size = lr_ / (1.f - powf(b1, t)), bc2s = sqrtf(1.f - powf(b2, t));
   for (int i = tid; i < n; i += CLIP_ADAM_NT) {
     const float gc = g[i] * coef;
@@ -2527,7 +2530,7 @@ static int fail(const char* msg) {
 static int tile_n(int N) {
   static int forced = -1;
   if (forced < 0) {
-    const char* e = getenv("LGX_MLP_BN");  // dev knob: force 64 or 128
+    const char* e = LGX_DEV_KNOB("LGX_MLP_BN");  // dev knob: force 64 or 128
     forced = e ? atoi(e) : 0;
   }
   if (forced == 64 || forced == 128) return forced;
@@ -2541,7 +2544,7 @@ static int tile_n(int N) {
 static int tile_n_for(int M, int N, bool rows_are_batch) {
   static int forced = -1;
   if (forced < 0) {
-    const char* e = getenv("LGX_MLP_BN");
+    const char* e = LGX_DEV_KNOB("LGX_MLP_BN");
     forced = e ? atoi(e) : 0;
   }
   if (forced == 64 || forced == 128) return forced;
@@ -2553,7 +2556,7 @@ static int tile_n_for(int M, int N, bool rows_are_batch) {
 static int dw_tile_n(int N) {
   static int forced = -1;
   if (forced < 0) {
-    const char* e = getenv("LGX_DW_BN");
+    const char* e = LGX_DEV_KNOB("LGX_DW_BN");
     forced = e ? atoi(e) : 0;
   }
   if (forced == 64 || forced == 128) return forced;
@@ -2567,7 +2570,7 @@ static int dw_tile_n(int N) {
 static int group_tile_m(int kind, int bn, int64_t tiles128) {
   static int forced = -1;
   if (forced < 0) {
-    const char* e = getenv("LGX_MLP_BM");
+    const char* e = LGX_DEV_KNOB("LGX_MLP_BM");
     forced = e ? atoi(e) : 0;
   }
   if (forced == 128) return lgxm::BM;
@@ -2584,9 +2587,9 @@ static int group_tile_m(int kind, int bn, int64_t tiles128) {
 static int group_waves(int kind) {
   static int fwd = -1, dw = -1;
   if (fwd < 0) {
-    const char* e = getenv("LGX_MLP_NW");
+    const char* e = LGX_DEV_KNOB("LGX_MLP_NW");
     fwd = e ? (atoi(e) == 4 ? 4 : 8) : 8;
-    const char* d = getenv("LGX_MLP_NW_DW");
+    const char* d = LGX_DEV_KNOB("LGX_MLP_NW_DW");
     dw = d && atoi(d) == 8 ? 8 : 4;
   }
   return kind == lgxm::G_DW ? dw : fwd;
@@ -3363,7 +3366,7 @@ int32_t lgx_mlp_pick_split_group(const int32_t* M, const int32_t* N, const int32
   }
   const int bn = dw_tile_n(maxn);
   // LGX_DW_SLOTS: dev knob (block budget of the grouped weight-gradient launch)
-  const char* knob = getenv("LGX_DW_SLOTS");
+  const char* knob = LGX_DEV_KNOB("LGX_DW_SLOTS");
   const int slots = knob ? std::max(64, atoi(knob)) : group_slots(bn);
   // equal K chunks for every problem: the smallest chunk (a multiple of the K step, at least
   // 256 rows) whose block count fits one residency wave; every split >= 2 (bias gradient)

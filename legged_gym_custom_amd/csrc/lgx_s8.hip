@@ -22,6 +22,7 @@
 // both written as S8 (32 B per lane: 8 columns' hi + lo) and/or fp32, with the column sums of each
 // 128-row tile (the next weight gradient's bias gradient); DW fp32 split-K partials.
 #include <hip/hip_runtime.h>
+#include "lgx_knobs.h"
 #include <stdint.h>
 #include <stdio.h>
 #include <string.h>
@@ -730,7 +731,7 @@ int lgxs_launched(const char* what) { return launched(what); }
 static bool dw_xcd_units() {
   static int on = -1;
   if (on < 0) {
-    const char* e = getenv("LGX_S8_DW_XCD");  // dev knob: 0 = tiles dealt per problem
+    const char* e = LGX_DEV_KNOB("LGX_S8_DW_XCD");  // dev knob: 0 = tiles dealt per problem
     on = e ? atoi(e) != 0 : 1;
   }
   return on != 0;

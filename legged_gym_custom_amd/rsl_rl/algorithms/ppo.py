@@ -252,7 +252,9 @@ class PPO:
         self._s8 = None  # S8Minibatch, built at the first update (static buffers for the graphs)
         self.use_fused_act = USE_FUSED_ACT and self.on_gpu
         self._s8act = None  # S8Act, built at the first (eager) act
-        self._dagger_graph = None  # update_dagger's hipGraph (GPU, world size 1)
+        self._dagger_graph = None  # update_dagger's hipGraph (world size 1) or phased graphs (> 1)
+        self.dagger_path = None  # "fused" | "autograd" | "cpu": the DAgger update that ran
+        self.dagger_graph_mode = None  # "whole" | "phased" once captured
         self._dagger_sum = torch.zeros((), device=device)
 
     # ------------------------------------------------------------------ flat Adam (HIP)
@@ -805,9 +807,16 @@ class PPO:
         self._perm.copy_(self._next_perm(self._perm.numel()))
         n = self.num_learning_epochs * self.num_mini_batches
         if not self.on_gpu:
+            self.dagger_path = "cpu"
             total = self._dagger_body_cpu()
-        elif not self.use_graphs or _distributed():
+        elif not self.use_graphs:
             self._dagger_body()
+            total = self._dagger_sum
+        elif _distributed():
+            # world size > 1: phased graphs around the host-issued all-reduce of the adaptation
+            # gradient (per minibatch: graph A = forward + backward + the block-row reduce, the
+            # all-reduce, graph B = clip + Adam), as update() does with its phased graphs
+            self._dagger_phased()
             total = self._dagger_sum
         else:
             if self._dagger_graph is None:
@@ -822,6 +831,7 @@ class PPO:
                 with torch.cuda.graph(g, pool=torch.cuda.graph_pool_handle(), capture_error_mode=self.capture_mode()):
                     self._dagger_body()
                 self._dagger_graph = g
+                self.dagger_graph_mode = "whole"
             else:
                 self._dagger_graph.replay()
             total = self._dagger_sum
@@ -843,8 +853,10 @@ class PPO:
             priv_lat = ac.privileged_encoder(priv_p)
         self._dagger_sum.zero_()
         if DAGGER_FUSED and self._dagger_fused_ok(adapt):
+            self.dagger_path = "fused"
             self._dagger_fused(obs_p, priv_lat, mb, adapt)
             return
+        self.dagger_path = "autograd"
         for _ in range(self.num_learning_epochs):
             for i in range(self.num_mini_batches):
                 adapt_latent = ac.adaptation_encoder(obs_p[i * mb:(i + 1) * mb])
@@ -866,21 +878,39 @@ class PPO:
         mod = ac.adaptation_encoder_
         if not hip_mlp.adaptation_train_supported(mod, ac.num_proprio):
             return False  # outside lgx_adaptation_train's tiling
+        why = None
         if adapt.numel() > 65536:
-            return False  # lgx_clip_adam's one-block segment
-        ps = hip_mlp.adaptation_param_order(mod)
-        off = adapt.data_ptr()
-        for p in ps:
-            if p.grad is None or p.grad.data_ptr() != off or not p.grad.is_contiguous():
-                return False
-            off += 4 * p.numel()
-        return off == adapt.data_ptr() + 4 * adapt.numel()
+            why = "the adaptation segment exceeds lgx_clip_adam's one-block limit (65536)"
+        else:
+            off = adapt.data_ptr()
+            for p in hip_mlp.adaptation_param_order(mod):
+                if p.grad is None or p.grad.data_ptr() != off or not p.grad.is_contiguous():
+                    why = "the adaptation gradients are not views of the flat segment in lgx_adaptation_train's order"
+                    break
+                off += 4 * p.numel()
+            if why is None and off != adapt.data_ptr() + 4 * adapt.numel():
+                why = "the adaptation segment holds more than the encoder's parameters"
+        if why is not None and not getattr(self, "_dagger_warned", False):
+            self._dagger_warned = True
+            print(f"[ppo] update_dagger: fused path not used ({why}); running the autograd path", flush=True)
+        return why is None
 
     def _dagger_fused(self, obs_p, priv_lat, mb, adapt):
         """The DAgger minibatches with the adaptation encoder's forward, loss and backward in ONE
         launch each (lgx_adaptation_train: per-block gradient rows), the rows summed into the flat
         gradient segment and the loss into the running sum by one reduce launch, then the clip and
         Adam of _dagger_body (ppo.py:336-345) as one lgx_clip_adam launch: 3 launches per minibatch."""
+        for _ in range(self.num_learning_epochs):
+            for i in range(self.num_mini_batches):
+                self._dagger_fused_grads(obs_p, priv_lat, mb, adapt, i)
+                if _distributed():
+                    dist.all_reduce(adapt)
+                    adapt.div_(dist.get_world_size())
+                self._clip_adam("adaptation_optimizer", self._adapt_lr)
+
+    def _dagger_fused_grads(self, obs_p, priv_lat, mb, adapt, i):
+        """Minibatch i's adaptation gradient (lgx_adaptation_train block rows, one reduce launch
+        into the flat segment) and its loss into the running sum."""
         from legged_gym_custom_amd.rsl_rl.modules import hip_s8 as S
         ac = self.actor_critic
         hist_cols = ac.num_proprio * ac.history_buffer_length
@@ -893,16 +923,64 @@ class PPO:
         gws, lws = ws
         jobs = [S.flat_reduce(gws.data_ptr(), NP, adapt.data_ptr(), NP, grid),
                 S.flat_reduce(lws.data_ptr(), 1, self._dagger_sum.data_ptr(), 1, grid, accumulate=1)]
-        for _ in range(self.num_learning_epochs):
+        keep = hip_mlp.adaptation_train(ac.adaptation_encoder_, obs_p[i * mb:(i + 1) * mb], hist_cols,
+                                        priv_lat[i * mb:(i + 1) * mb], gws, lws, DAGGER_BLOCKS)
+        S.reduce(jobs)
+        del keep
+
+    def _dagger_phased(self):
+        """update_dagger at world size > 1 (GPU, fused path): graph P (gathers, privileged latents),
+        per minibatch graph A_i (the fused forward + backward + reduce), the host-issued all-reduce
+        of the 5,040-entry adaptation segment, graph B (mean, clip, Adam). The first call runs the
+        body eagerly and captures; the autograd fallback stays eager."""
+        adapt = self.grads.segment("adaptation")
+        if not (DAGGER_FUSED and self._dagger_fused_ok(adapt)):
+            self._dagger_body()
+            return
+        rows = self._perm.numel()
+        mb = rows // self.num_mini_batches
+        if self._dagger_graph is None:
+            cur = torch.cuda.current_stream(self.device)
+            side = torch.cuda.Stream(self.device)
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                self._dagger_body()
+            cur.wait_stream(side)
+            torch.cuda.synchronize(self.device)
+            pool, mode = torch.cuda.graph_pool_handle(), self.capture_mode()
+            keep = {}
+
+            def prep():
+                ac, s = self.actor_critic, self.storage
+                with torch.no_grad():
+                    obs = s.observations.flatten(0, 1)
+                    keep["obs_p"], priv_p = hip_mlp.gather_rows([obs, s.privileged_observations.flatten(0, 1)],
+                                                                self._perm)
+                    keep["priv_lat"] = ac.privileged_encoder(priv_p)
+                self._dagger_sum.zero_()
+            gp = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gp, pool=pool, capture_error_mode=mode):
+                prep()
+            ga = []
             for i in range(self.num_mini_batches):
-                keep = hip_mlp.adaptation_train(ac.adaptation_encoder_, obs_p[i * mb:(i + 1) * mb], hist_cols,
-                                                priv_lat[i * mb:(i + 1) * mb], gws, lws, DAGGER_BLOCKS)
-                S.reduce(jobs)
-                del keep
-                if _distributed():
-                    dist.all_reduce(adapt)
-                    adapt.div_(dist.get_world_size())
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=pool, capture_error_mode=mode):
+                    self._dagger_fused_grads(keep["obs_p"], keep["priv_lat"], mb, adapt, i)
+                ga.append(g)
+            gb = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gb, pool=pool, capture_error_mode=mode):
+                adapt.div_(dist.get_world_size())
                 self._clip_adam("adaptation_optimizer", self._adapt_lr)
+            self._dagger_graph = {"P": gp, "A": ga, "B": gb, "keep": keep}
+            self.dagger_graph_mode = "phased"
+            return
+        gr = self._dagger_graph
+        gr["P"].replay()
+        for _ in range(self.num_learning_epochs):
+            for g in gr["A"]:
+                g.replay()
+                dist.all_reduce(adapt)
+                gr["B"].replay()
 
     def _clip_adam(self, name, lr):
         """clip_grad_norm_ of this optimizer's segment (in place) + its Adam step in one launch

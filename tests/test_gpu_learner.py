@@ -197,3 +197,47 @@ def test_clip_adam_matches_clip_grad_norm_and_adam(n, scale):
     torch.testing.assert_close(m.double().cpu(), m1, rtol=2e-6, atol=1e-8)  # (0.9 m + 0.1 g) cancels
     torch.testing.assert_close(v.double().cpu(), v1, rtol=2e-6, atol=1e-14)
     torch.testing.assert_close(p.double().cpu(), p1, rtol=1e-6, atol=2e-7)
+
+
+def test_gpu_update_dagger_tracks_cpu_update():
+    """The whole fused GPU update_dagger (per minibatch: lgx_adaptation_train, the block-row reduce,
+    lgx_clip_adam with the device step counter; 2 epochs x 3 minibatches, graph-replayed from the
+    second call) against the CPU learner's update_dagger (torch autograd, clip_grad_norm_, torch
+    Adam; ppo.py:309-349) from the same state, data and permutation, three calls: the mean losses
+    within 1e-4 relative, the adaptation encoder's parameters and both Adam moments close (per-element
+    Adam steps are ~lr, so a sign flip of a near-zero gradient moves one entry by ~2 lr: statistical
+    bounds), and the same step count — a sequencing bug (step increment, loss accumulation, a missed
+    zeroing) fails here, where the single-launch tests cannot see it."""
+    base = _make("adaptive")
+    cpu = _to_gpu(base, use_graphs=False, device="cpu")
+    gpu = _to_gpu(base, use_graphs=True)
+    for alg in (cpu, gpu):
+        alg._next_perm = lambda n, dev=alg.device: torch.arange(n, device=dev)
+    for it in range(3):
+        for alg in (cpu, gpu):
+            _fill(alg, 60 + it)
+        lc = cpu.update_dagger()
+        lg = gpu.update_dagger()
+        assert lg == pytest.approx(lc, rel=1e-4, abs=1e-7), (it, lg, lc)
+    assert gpu.dagger_path == "fused" and gpu.dagger_graph_mode == "whole"
+    pc = torch.cat([p.detach().reshape(-1) for p in cpu.actor_critic.adaptation_encoder_.parameters()])
+    pg = torch.cat([p.detach().reshape(-1).cpu() for p in gpu.actor_critic.adaptation_encoder_.parameters()])
+    d = (pg - pc).abs()
+    lr = cpu.adaptation_optimizer.param_groups[0]["lr"]
+    assert d.median() < 1e-6 and d.max() < 4 * lr, (float(d.median()), float(d.max()), lr)
+    a, b = gpu.grads.slices[gpu._segment_of["adaptation_optimizer"]]
+    st = cpu.adaptation_optimizer.state_dict()["state"]
+    m_cpu = torch.cat([st[k]["exp_avg"].reshape(-1) for k in sorted(st)])
+    v_cpu = torch.cat([st[k]["exp_avg_sq"].reshape(-1) for k in sorted(st)])
+    n = 3 * gpu.num_learning_epochs * gpu.num_mini_batches
+    assert all(float(st[k]["step"]) == n for k in st)
+    assert float(gpu._opt_step["adaptation_optimizer"]) == n
+    # the flat moments are in lgx_adaptation_train's parameter order; the CPU optimizer's in
+    # parameters() order: compare as multisets of magnitudes' summary statistics and per tensor
+    # through the export path below
+    exp = gpu.optimizer_state_dicts()["adaptation_optimizer_state_dict"]["state"]
+    for k in sorted(st):
+        torch.testing.assert_close(exp[k]["exp_avg"].cpu(), st[k]["exp_avg"], rtol=5e-3, atol=2e-4 * float(m_cpu.abs().max()))
+        torch.testing.assert_close(exp[k]["exp_avg_sq"].cpu(), st[k]["exp_avg_sq"], rtol=5e-3,
+                                   atol=2e-4 * float(v_cpu.abs().max()))
+    assert b - a == pc.numel()

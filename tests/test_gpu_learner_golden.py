@@ -169,11 +169,13 @@ def test_gpu_adam_moments_after_epoch0(replay):
 def test_gpu_adam_moments_after_update(replay):
     """After all 20 minibatches, free-running. The 384-row cases within 5e-3 / 1e-2; at the
     production minibatch sizes (24,576 / 49,152 rows) near-tie clip flips (module docstring) put
-    the free-running end state on another branch, so there the end state is reported and finite,
-    and test_gpu_near_tie_forced_update_end_state is the tight check."""
+    the free-running end state on another branch: there a gross-divergence guard holds it (measured
+    round 5: exp_avg 0.067 / 0.111, exp_avg_sq ≈0.02 of max|ref| at go2_c2 / go2_parkour_c4; bound
+    0.25 / 0.1, so a 3-10x regression of the product's own free-running path fails), and
+    test_gpu_near_tie_forced_update_end_state is the tight check."""
     case, d, res, _ = replay
     large = LC.n_envs(case) >= 4096
-    tols = (float("inf"), float("inf")) if large else (5e-3, 1e-2)
+    tols = (0.25, 0.1) if large else (5e-3, 1e-2)
     w = _moments(case, d, res, ("exp_avg", "exp_avg_sq"), tols)
     assert np.isfinite(w).all()
     print(f"{case}: free-running Adam moments, worst |err| / max|ref| per tensor: exp_avg {w[0]:.3g}, "
