@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define LGX_S8_ABI_VERSION 3
+#define LGX_S8_ABI_VERSION 4
 
 enum { LGX_S8_FWD = 0, LGX_S8_DX = 1, LGX_S8_DW = 2 };  /* GEMM kinds (operand modes above) */
 
@@ -57,9 +57,9 @@ typedef struct lgx_s8_gemm_args {
   const void* act; int64_t ld_act;      /* DX, LGX_S8_EPI_DELU: Y_prev (S8) */
   const float* addend; int64_t ld_add;  /* DX (optional): + addend[m][n] for n < add_cols, after ELU' */
   int32_t add_cols;
-  float* colsum_ws;             /* FWD / DX (optional): [tiles_m][N] fp32 column sums of the
-                                   output over each 128-row tile (the next weight gradient's
-                                   bias gradient, reduced with lgx_s8_reduce) */
+  float* colsum_ws;             /* FWD / DX (optional): [ceil(M / LGX_S8_TILE_M)][N] fp32 column
+                                   sums of the output over each 64-row half tile (the next weight
+                                   gradient's bias gradient, reduced with lgx_s8_reduce) */
   int32_t split;                /* DW: K split (>= 1); kchunk = round_up(ceil(K / split), 32) */
   int32_t pad0;
 } lgx_s8_gemm_args;
@@ -91,7 +91,7 @@ typedef struct lgx_s8_reduce_args {
 
 #define LGX_S8_GROUP_MAX 20
 #define LGX_S8_BATCH_MAX 48
-#define LGX_S8_TILE_M 128        /* rows of one colsum_ws partial (FWD / DX) */
+#define LGX_S8_TILE_M 64         /* rows of one colsum_ws partial (FWD / DX; ABI 4: was 128) */
 #define LGX_S8_SPLIT_ROWS 256    /* rows of one lgx_s8_split colsum partial */
 
 int32_t lgx_s8_abi_version(void);

@@ -513,6 +513,192 @@ __global__ __launch_bounds__(Cfg::NT, 2) __attribute__((amdgpu_waves_per_eu(1, 2
 #endif
 }
 
+// ---------------------------------------------------------------- FWD with a register epilogue (round 6)
+// The forward kind's tile with its epilogue run from the accumulator registers (no fp32 LDS image,
+// no barrier): one tile per block, the blocks dispatched by the hardware as slots free up (a
+// static persistent tile list measured slower: it loses that dynamic balance).
+// The MFMA operands are swapped (weights as the MFMA's A operand, activations as its B operand):
+// the same three products per K step in the same accumulation order (lo*hi, hi*lo, hi*hi; bit-
+// identical outputs, tests/test_gpu_s8.py), but each lane then holds 4 CONSECUTIVE output columns
+// of one row (C/D map: column = 4 (lane >> 4) + r, row = lane & 15). Lanes l and l + 16 hold the
+// two halves of one 8-column S8 group: after the bf16 hi / lo split one v_permlane16_swap per
+// dword gives lane l the group's 8 hi values and lane l + 16 its 8 lo values — one 16-B store
+// each, the 32-B group written whole. Column sums (optional for FWD) per 64-row half tile: the
+// wave's 4 row tiles summed in registers, then the 16 lanes of a row by DPP (fixed order).
+// The input-gradient kind keeps lgxs::s8_gemm_kernel: its ELU' operand loads coalesce better
+// through the LDS image's row-slot map (measured, §4.2b).
+struct FGroup {
+  int n, per_xcd;
+  int start[GMAX + 1];   // first tile of each problem in the launch's tile list
+  int xstart[9];         // XCD slot x: tiles [xstart[x], xstart[x + 1]); its block s runs tile xstart[x] + s
+  Prob p[GMAX];
+};
+static_assert(sizeof(FGroup) <= 4096, "kernel argument segment");
+
+__device__ __forceinline__ float dpp_row_sum(float v) {
+  // sum over the 16 lanes of each DPP row (every lane of the row gets it): quad swaps, then
+  // rotations by 4 and 8 within the row — a fixed order, so the result is deterministic
+  int x = __float_as_int(v);
+  v += __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0xB1, 0xf, 0xf, false));  // quad_perm [1,0,3,2]
+  x = __float_as_int(v);
+  v += __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0x4E, 0xf, 0xf, false));  // quad_perm [2,3,0,1]
+  x = __float_as_int(v);
+  v += __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0x124, 0xf, 0xf, false));  // row_ror:4
+  x = __float_as_int(v);
+  v += __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0x128, 0xf, 0xf, false));  // row_ror:8
+  return v;
+}
+
+__global__ __launch_bounds__(Cfg::NT, 2) __attribute__((amdgpu_waves_per_eu(1, 2))) void s8f_kernel(FGroup g) {
+  constexpr int BM = Cfg::BM, NW = Cfg::NW;
+  using OA = Op<false, BM, NW>;
+  using OB = Op<false, BN, NW>;
+  constexpr int STAGE = OA::IMG + OB::IMG;
+  static_assert(2 * STAGE <= Cfg::LDS_STAGES, "two stages");
+  extern __shared__ __align__(16) char lds[];
+
+  const int x = blockIdx.x & 7, slot = blockIdx.x >> 3;
+  const int t = g.xstart[x] + slot;
+  if (t >= g.xstart[x + 1]) return;
+  int pi = 0;
+  while (pi + 1 < g.n && t >= g.start[pi + 1]) ++pi;
+  const Prob& P = g.p[pi];
+  const int M = P.M, N = P.N, epi = P.epi;
+  const int l = t - g.start[pi];
+  const int n0 = (l % P.tiles_n) * BN, m0 = (l / P.tiles_n) * BM;
+  const int nk = (P.K + BK - 1) / BK;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = (wave % Cfg::WR) * 64, wn = (wave / Cfg::WR) * 64;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)((LDS_AS char*)lds);
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  uint32_t offA[OA::PW], offB[OB::PW];
+  OA::offsets(offA, wave, lane, m0, M, P.lda, 0);
+  OB::offsets(offB, wave, lane, n0, N, P.ldb, 0);
+  auto issue = [&](int stage, int step) {
+    const uint32_t st = lds0 + (uint32_t)(stage * STAGE);
+    OA::issue(P.A + step * OA::step_bytes(P.lda), offA, st, wv);
+    OB::issue(P.B + step * OB::step_bytes(P.ldb), offB, st + OA::IMG, wv);
+  };
+  f32x4 acc[NJ][4];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto compute = [&](int stage) {
+    const char* st = lds + stage * STAGE;
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      bf16x8 ah[4], al[4], bh[NJ], bl[NJ];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) OB::frag(st + OA::IMG, wn + 16 * j, kk, lane, bh[j], bl[j]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) OA::frag(st, wm + 16 * i, kk, lane, ah[i], al[i]);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh[j], al[i], acc[j][i], 0, 0, 0);
+          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl[j], ah[i], acc[j][i], 0, 0, 0);
+          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh[j], ah[i], acc[j][i], 0, 0, 0);
+        }
+    }
+  };
+  // pipeline as lgxs::s8_gemm_kernel (2 stages, counted waits, raw barriers); the bias is
+  // requested before the last step's MFMAs, so its latency runs beside them
+  if (nk > 0) issue(0, 0);
+  const int q4 = lane >> 4, lr = lane & 15, odd = q4 & 1;
+  float bv[NJ][4];
+  for (int k = 0; k < nk; ++k) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_barrier" ::: "memory");
+    if (k + 1 < nk) issue((k + 1) & 1, k + 1);
+    compute(k & 1);
+  }
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int nq = n0 + wn + 16 * j + 4 * q4;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bv[j][r] = (epi & LGX_S8_EPI_BIAS) ? P.bias[min(nq + r, N - 1)] : 0.f;
+  }
+
+  // ---- epilogue from the accumulators: lane (lr, q4) holds rows m0 + wm + 16 i + lr, columns
+  // n0 + wn + 16 j + 4 q4 + r of acc[j][i][r]
+  char* const Cp = P.C;
+  float* const C32p = P.C32;
+  const int64_t ldc = P.ldc, ldc32 = P.ldc32;
+  const bool full = m0 + BM <= M && n0 + BN <= N;  // no row / column checks
+  float cs[NJ][4];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) cs[j][r] = 0.f;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int nq = n0 + wn + 16 * j + 4 * q4;  // this lane's first column
+    const int grp = (n0 + wn + 16 * j) / 8 + (q4 >> 1);
+    bool colok[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) colok[r] = full || nq + r < N;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = m0 + wm + 16 * i + lr;
+      const bool rowok = full || m < M;
+      float v[4] = {acc[j][i][0], acc[j][i][1], acc[j][i][2], acc[j][i][3]};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] += bv[j][r];
+      if (epi & LGX_S8_EPI_ELU) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = elu(v[r]);
+      }
+      if (!full) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = colok[r] ? v[r] : 0.f;  // zero pad columns
+      }
+      if (Cp != nullptr) {
+        __bf16 h[4], lo[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          h[r] = (__bf16)v[r];
+          lo[r] = (__bf16)(v[r] - (float)h[r]);
+        }
+        const auto s0 = __builtin_amdgcn_permlane16_swap(pack2(h[0], h[1]), pack2(lo[0], lo[1]), false, false);
+        const auto s1 = __builtin_amdgcn_permlane16_swap(pack2(h[2], h[3]), pack2(lo[2], lo[3]), false, false);
+        // even-row lanes: {own hi, partner hi} = the group's 8 hi; odd-row: its 8 lo
+        const u32x4 out = {s0[0], s1[0], s0[1], s1[1]};
+        if (rowok && (full || grp * 8 < N))
+          *reinterpret_cast<u32x4*>(Cp + (int64_t)m * ldc + grp * 32 + odd * 16) = out;
+      }
+      if (C32p != nullptr && rowok) {
+        float* d = C32p + (int64_t)m * ldc32 + nq;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (colok[r]) d[r] = v[r];
+      }
+      if (rowok) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) cs[j][r] += v[r];
+      }
+    }
+  }
+  if (P.colsum_ws != nullptr) {
+    // per 64-row half tile: partial index (m0 + wm) / 64, columns n of this wave
+    const int part = (m0 + wm) / LGX_S8_TILE_M;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int nq = n0 + wn + 16 * j + 4 * q4;
+      float sv[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sv[r] = dpp_row_sum(cs[j][r]);
+      if (lr == 0 && m0 + wm < M) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (nq + r < N) P.colsum_ws[(int64_t)part * N + nq + r] = sv[r];
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------- fp32 -> S8 (+ column sums)
 #define LGX_S8_SPLIT_WIDE 512  // (row, 8-column group) items per block of a wide split job
 
@@ -773,6 +959,61 @@ static void deal_units(lgxs::Group& g) {
   g.per_xcd = mx;
 }
 
+// The FWD launch: problems ordered by K (longest first: the dispatcher then starts the longest
+// tiles first); the tile list cut into 8 contiguous XCD ranges of equal cost (an XCD's blocks
+// share its L2: a row tile's column tiles stay together); block s of XCD slot x runs tile
+// xstart[x] + s, one tile per block.
+static bool fwd_register_epilogue() {
+  static int on = -1;
+  if (on < 0) {
+    const char* e = LGX_DEV_KNOB("LGX_S8_FWD_REG");  // dev knob: 0 = the LDS-image epilogue kernel for FWD
+#ifndef LGX_S8_FWD_REG_DEFAULT
+#define LGX_S8_FWD_REG_DEFAULT 1  // (dev builds: -DLGX_S8_FWD_REG_DEFAULT=0 for the A/B variant)
+#endif
+    on = e ? atoi(e) != 0 : LGX_S8_FWD_REG_DEFAULT;
+  }
+  return on != 0;
+}
+
+static void launch_fwd(const lgxs::Group& g0, hipStream_t s) {
+  lgxs::FGroup g;
+  memset(&g, 0, sizeof g);
+  int order[lgxs::GMAX];
+  for (int i = 0; i < g0.n; ++i) order[i] = i;
+  constexpr int EPI = 4;  // epilogue allowance in K steps
+  auto nk = [&](int i) { return (g0.p[i].K + lgxs::BK - 1) / lgxs::BK; };
+  std::stable_sort(order, order + g0.n, [&](int a, int b) { return nk(a) > nk(b); });
+  int64_t total = 0;
+  int ntiles = 0;
+  for (int k = 0; k < g0.n; ++k) {
+    g.p[k] = g0.p[order[k]];
+    g.start[k] = ntiles;
+    ntiles += g.p[k].tiles;
+    total += (int64_t)g.p[k].tiles * (nk(order[k]) + EPI);
+  }
+  g.n = g0.n;
+  g.start[g.n] = ntiles;
+  g.xstart[0] = 0;
+  int x = 1, pi = 0;
+  int64_t acc = 0;
+  for (int tt = 0; tt < ntiles && x < 8; ++tt) {
+    while (tt >= g.start[pi + 1]) ++pi;
+    acc += nk(order[pi]) + EPI;
+    if (acc * 8 >= total * x) g.xstart[x++] = tt + 1;
+  }
+  while (x <= 8) g.xstart[x++] = ntiles;
+  int mx = 0;
+  for (int k = 0; k < 8; ++k) mx = std::max(mx, g.xstart[k + 1] - g.xstart[k]);
+  g.per_xcd = mx;
+  constexpr int lds = lgxs::Cfg::LDS_STAGES;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)lgxs::s8f_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    attr = true;
+  }
+  if (g.per_xcd > 0) hipLaunchKernelGGL(lgxs::s8f_kernel, dim3(8 * g.per_xcd), dim3(lgxs::Cfg::NT), lds, s, g);
+}
+
 template <int KIND>
 static void launch_gemm(const lgxs::Group& g, hipStream_t s) {
   constexpr int lds = lgxs::Cfg::LDS;
@@ -882,7 +1123,8 @@ int32_t lgx_s8_gemm_group(const lgx_s8_gemm_args* a, int32_t n, int32_t kind, vo
   if (np == 0) return 0;
   if (kind == LGX_S8_DW && dw_xcd_units()) deal_units(g);
   hipStream_t s = (hipStream_t)stream;
-  if (kind == LGX_S8_FWD) launch_gemm<LGX_S8_FWD>(g, s);
+  if (kind == LGX_S8_FWD && fwd_register_epilogue()) launch_fwd(g, s);
+  else if (kind == LGX_S8_FWD) launch_gemm<LGX_S8_FWD>(g, s);
   else if (kind == LGX_S8_DX) launch_gemm<LGX_S8_DX>(g, s);
   else launch_gemm<LGX_S8_DW>(g, s);
   return launched("lgx_s8_gemm_group");

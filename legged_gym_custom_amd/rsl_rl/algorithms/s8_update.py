@@ -166,7 +166,7 @@ class S8Minibatch:
         self.splits = S.pick_split(shapes)
         tot = sum(s * m * n for s, (m, n, _k) in zip(self.splits, shapes))
         self.dw_ws = torch.empty(tot, device=dev)
-        self.tiles_m = (mb + 127) // 128
+        self.tiles_m = (mb + S.TILE_M - 1) // S.TILE_M  # column-sum partials of the FWD / DX epilogues
         self.nsb = (mb + S.SPLIT_ROWS - 1) // S.SPLIT_ROWS
         for p in self.parts:
             # colsum partials of dy[l] (the bias gradient of layer l): [tiles][out_l] (the

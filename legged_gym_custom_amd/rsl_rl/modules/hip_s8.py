@@ -14,12 +14,12 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.environ.get("LGX_S8_LIB") or os.path.join(os.path.dirname(os.path.dirname(_HERE)), "lib", "liblgx_s8.so")  # env: A/B builds
 _lib = None
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 FWD, DX, DW = 0, 1, 2
 EPI_BIAS, EPI_ELU, EPI_DELU, EPI_ACCUM = 1, 2, 4, 8
 GROUP_MAX = 20
 BATCH_MAX = 48
-TILE_M = 128
+TILE_M = 64  # rows of one FWD / DX column-sum partial (lgx_s8.h LGX_S8_TILE_M)
 SPLIT_ROWS = 256
 EXPORTED = ("lgx_s8_abi_version", "lgx_s8_sizeof_gemm_args", "lgx_s8_last_error", "lgx_s8_gemm_group",
             "lgx_s8_pick_split", "lgx_s8_split", "lgx_s8_reduce", "lgx_s8_act", "lgx_s8_act_last_error",

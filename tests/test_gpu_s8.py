@@ -55,7 +55,7 @@ def test_forward_bias_elu(S, M, N, K):
     xv, Wv = S.from_s8(xs, M, K).double(), S.from_s8(Ws, N, K).double()
     out = S.empty(M, N, dev)
     y32 = torch.full((M, N + 3), float("nan"), device=dev)
-    cs = torch.zeros((M + 127) // 128, N, device=dev)
+    cs = torch.zeros((M + S.TILE_M - 1) // S.TILE_M, N, device=dev)
     S.gemm_group([S.GemmArgs(A=xs.data_ptr(), lda=xs.shape[1], B=Ws.data_ptr(), ldb=Ws.shape[1], M=M, N=N, K=K,
                              epilogue=S.EPI_BIAS | S.EPI_ELU, C=out.data_ptr(), ldc=out.shape[1], C32=y32.data_ptr(),
                              ldc32=y32.stride(0), bias=b.data_ptr(), colsum_ws=cs.data_ptr())], S.FWD)
@@ -68,7 +68,7 @@ def test_forward_bias_elu(S, M, N, K):
     assert torch.isnan(y32[:, N:]).all()  # nothing past N in the fp32 copy
     # the S8 output is the split of the fp32 output, pads zero
     assert torch.equal(out, S.to_s8_torch(y32[:, :N].contiguous(), ld=out.shape[1], rows_pad=out.shape[0]))
-    blocks = torch.stack([y32[i:i + 128, :N].double().sum(0) for i in range(0, M, 128)])
+    blocks = torch.stack([y32[i:i + S.TILE_M, :N].double().sum(0) for i in range(0, M, S.TILE_M)])
     torch.testing.assert_close(cs.double(), blocks, rtol=1e-5, atol=1e-5)
 
 
@@ -83,7 +83,7 @@ def test_input_grad_delu_addend(S, M, N, K):
     dys, Ws, yps = _s8(S, dy), _s8(S, W), _s8(S, yp)
     dyv, Wv, ypv = S.from_s8(dys, M, K).double(), S.from_s8(Ws, K, N).double(), S.from_s8(yps, M, N).double()
     out = S.empty(M, N, dev)
-    cs = torch.zeros((M + 127) // 128, N, device=dev)
+    cs = torch.zeros((M + S.TILE_M - 1) // S.TILE_M, N, device=dev)
     S.gemm_group([S.GemmArgs(A=dys.data_ptr(), lda=dys.shape[1], B=Ws.data_ptr(), ldb=Ws.shape[1], M=M, N=N, K=K,
                              epilogue=S.EPI_DELU, C=out.data_ptr(), ldc=out.shape[1], act=yps.data_ptr(),
                              ld_act=yps.shape[1], addend=add.data_ptr(), ld_add=add.stride(0), add_cols=17,
@@ -98,7 +98,7 @@ def test_input_grad_delu_addend(S, M, N, K):
     # the pad columns of the output's last group stay zero
     hi, lo = S.planes(out, M, out.shape[1])
     assert (hi[:, N:] == 0).all() and (lo[:, N:] == 0).all()
-    blocks = torch.stack([got[i:i + 128].sum(0) for i in range(0, M, 128)])
+    blocks = torch.stack([got[i:i + S.TILE_M].sum(0) for i in range(0, M, S.TILE_M)])
     torch.testing.assert_close(cs.double(), blocks, rtol=1e-4, atol=1e-4)
 
 
@@ -417,7 +417,7 @@ def test_chain_input_grads_equal_grouped_levels(S, rows):
             Ws = S.to_s8_torch(W)
             out, out_ref = S.empty(rows, n, dev), S.empty(rows, n, dev)
             cs = torch.full(((rows + 31) // 32, n), float("nan"), device=dev)
-            cs_ref = torch.zeros((rows + 127) // 128, n, device=dev)
+            cs_ref = torch.zeros((rows + S.TILE_M - 1) // S.TILE_M, n, device=dev)
             L = c.layers[q]
             L.W, L.packed, L.K, L.N, L.elu = WpT.data_ptr(), 1, k, n, 2
             L.act, L.ld_act, L.C, L.ldc, L.colsum_ws = y.data_ptr(), y.shape[1], out.data_ptr(), out.shape[1], cs.data_ptr()

@@ -14,8 +14,8 @@ from legged_gym_custom_amd.rsl_rl.modules import hip_s8 as S
 
 dev = "cuda:0"
 R = 24576
-PROBS = [("fwd", R, 512, 736), ("fwd-noelu", R, 512, 736), ("dx", R, 512, 256), ("dx-nodelu", R, 512, 256),
-         ("dw", 512, 736, R), ("fwd-solo", 16384, 128, 736), ("fwd-solo-noelu", 16384, 128, 736),
+PROBS = [("fwd", R, 512, 736), ("fwd-noelu", R, 512, 736), ("fwd", R, 1024, 1024), ("dx", R, 512, 256),
+         ("dx-nodelu", R, 512, 256), ("fwd-solo", 16384, 128, 736), ("fwd-solo-noelu", 16384, 128, 736),
          ("dx-solo", 16384, 128, 256)]
 
 
@@ -79,7 +79,8 @@ def main():
             for w, name in ((0, "wave 0"), (1, "last wave")):
                 per = lambda c: d[:, w, c].astype(np.float64) / nk  # noqa: E731
                 print(f"  {name}: per K step  wait {per(0).mean():7.0f}  barrier {per(1).mean():7.0f}  "
-                      f"issue+compute {per(2).mean():7.0f}   epilogue {d[:, w, 3].mean():6.0f}  "
+                      f"issue+compute {per(2).mean():7.0f}   epilogue/tile "
+                      f"{(d[:, w, 3] / np.maximum(d[:, w, 7], 1)).mean():6.0f}  tiles/block {np.maximum(d[:, w, 7], 1).mean():4.2f}  "
                       f"block total {tot[:, w].mean():9.0f} (p10 {np.percentile(tot[:, w], 10):9.0f}, "
                       f"max {tot[:, w].max():9.0f})")
             del keep
