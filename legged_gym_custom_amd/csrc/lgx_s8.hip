@@ -37,6 +37,22 @@ typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4u __attribute__((ext_vector_type(4), aligned(4)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+// MFMA issue order of a K step: each accumulator's three products back to back (lo*hi, hi*lo,
+// hi*hi), then the next accumulator. Left to itself the scheduler groups the MFMAs by a shared
+// operand register (one fragment held over 4 consecutive MFMAs, the accumulators rotating); the
+// per-accumulator chain draws less power at the same per-clock MFMA issue rate, so the chip holds
+// a higher clock under the K loop (measured: tools/exp/mfma_power.hip). A
+// scheduling barrier after each MFMA pins the source order; the products and their accumulation
+// order are the same either way (bit-identical results).
+#ifndef LGX_S8_MFMA_CHAIN
+#define LGX_S8_MFMA_CHAIN 1
+#endif
+#if LGX_S8_MFMA_CHAIN
+#define S8_MFMA_ORDER() __builtin_amdgcn_sched_barrier(0)
+#else
+#define S8_MFMA_ORDER() do { } while (0)
+#endif
 #define LDS_AS __attribute__((address_space(3)))
 
 #ifndef LGX_S8_BK
@@ -447,8 +463,11 @@ __global__ __launch_bounds__(Cfg::NT, 2) __attribute__((amdgpu_waves_per_eu(1, 2
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+          S8_MFMA_ORDER();
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+          S8_MFMA_ORDER();
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+          S8_MFMA_ORDER();
         }
     }
   };
@@ -599,8 +618,11 @@ __global__ __launch_bounds__(Cfg::NT, 2) __attribute__((amdgpu_waves_per_eu(1, 2
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh[j], al[i], acc[j][i], 0, 0, 0);
+          S8_MFMA_ORDER();
           acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl[j], ah[i], acc[j][i], 0, 0, 0);
+          S8_MFMA_ORDER();
           acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh[j], ah[i], acc[j][i], 0, 0, 0);
+          S8_MFMA_ORDER();
         }
     }
   };
