@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define LGX_MLP_ABI_VERSION 10
+#define LGX_MLP_ABI_VERSION 11
 
 enum {
   LGX_EPI_BIAS = 1,  /* + bias[n] */
@@ -311,8 +311,29 @@ int32_t lgx_loss_heads_tail(const lgx_ppo_head_args* head, const lgx_aux_loss_ar
  * Adam arithmetic as lgx_adam_step; step_main / step_est are incremented here. Norms are
  * block partials summed in block order (deterministic): the first launch writes them, every
  * block of the second sums them (no last-block pass). ws >= 2 * 512 floats + 8; counter:
- * unused (kept for the layout). */
+ * unused (kept for the layout).
+ * ABI 11, optional (n_s8 = 0: none): the updated weights also written in S8 (the update's GEMM
+ * operands, include/lgx_s8.h) by the Adam launch itself, so the next minibatch needs no weight
+ * split launch. Each lgx_tail_s8_seg maps the logical columns [c0, c0 + w) of one weight W [N][K]
+ * (row-major in params from index p0) to S8 destination columns 0.. of dst: S8 rows of pitch ld
+ * elements (32 B per 8-column group: 8 hi then 8 lo bf16), or, packed != 0, the fragment-packed
+ * copy (lgx_s8_split packed_steps = ld: per 16-row tile and 32-deep K step 64 lanes x 16 B of hi,
+ * then of lo). The conversion is lgx_s8_split's (hi = RN bf16(x), lo = RN bf16(x - hi)), so the
+ * copies equal a split of the updated weights bit for bit; pad columns are not written (a split
+ * zeroed them). The table (host memory, n_s8 <= LGX_TAIL_S8_MAX entries sorted by p0, a weight's
+ * entries consecutive, at most 4 per weight; every weight inside the main or the estimator
+ * segment) is read at the
+ * call: a captured graph keeps the table of its capture. */
 #define LGX_TAIL_MAX_LOSSES 8
+#define LGX_TAIL_S8_MAX 32
+typedef struct lgx_tail_s8_seg {
+  int64_t p0;         /* params index of W[0][0] */
+  int32_t N, K;       /* W rows, columns */
+  int32_t c0, w;      /* the logical columns this entry covers */
+  char* dst;          /* S8 column 0 of this entry (row 0) */
+  int32_t ld;         /* S8 row pitch in elements; packed: K steps per 16-row tile */
+  int32_t packed;
+} lgx_tail_s8_seg;
 typedef struct lgx_ppo_tail_args {
   float* grads; float* params; float* exp_avg; float* exp_avg_sq;
   int64_t main_lo, main_hi, est_lo, est_hi, adapt_lo, adapt_hi, kl_index;
@@ -323,6 +344,7 @@ typedef struct lgx_ppo_tail_args {
   float* step_main; float* step_est;
   const float* loss_ptrs[LGX_TAIL_MAX_LOSSES]; float* sums; int32_t nloss;
   float* ws; uint32_t* counter;
+  const lgx_tail_s8_seg* s8; int32_t n_s8;  /* ABI 11 */
 } lgx_ppo_tail_args;
 int32_t lgx_ppo_tail(const lgx_ppo_tail_args* args, void* stream);
 
@@ -395,6 +417,10 @@ typedef struct lgx_track_args {
   int32_t N, na, nb;
 } lgx_track_args;
 int32_t lgx_track_episodes(const lgx_track_args* args, void* stream);
+/* ABI 11. lgx_store_transition and lgx_track_episodes of one rollout step in ONE launch (both
+ * read the env's rewards / dones and write disjoint buffers; the same arithmetic as the two
+ * launches, bit for bit). track NULL: lgx_store_transition alone. */
+int32_t lgx_post_step(const lgx_transition_args* transition, const lgx_track_args* track, void* stream);
 
 /* RolloutStorage.compute_returns (rollout_storage.py:110-124) over [T, N] rows, one thread
  * per env walking the steps backwards in torch's operation order:

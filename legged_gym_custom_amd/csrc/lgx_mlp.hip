@@ -2491,6 +2491,181 @@ __global__ __launch_bounds__(256) void tail_adam(lgx_ppo_tail_args p) {
   if (i0 < p.adapt_hi - b) p.grads[b + i0] *= cm;
 }
 
+// The tail's Adam launch with the S8 copies (lgx_ppo_tail_args.n_s8 > 0): the host cuts the
+// three segments at the weights' boundaries into ranges, each with its own blocks (a block's
+// range is uniform: no per-element table lookup), and a weight's range writes every updated
+// value's S8 copies (lgx_s8_split's conversion and layouts) right after its Adam update.
+constexpr int TAIL_RMAX = 48;
+struct TailRange {
+  int64_t lo, hi;   // flat elements
+  int32_t opt;      // 0: main Adam, 1: estimator Adam, 2: the adaptation gradients' clip scaling
+  int32_t seg0, nseg;  // this weight's S8 entries (nseg 0: not a weight)
+  int32_t blk0;     // first block
+};
+struct TailK {
+  lgx_ppo_tail_args p;
+  int32_t nr;
+  TailRange r[TAIL_RMAX + 1];  // r[nr].blk0 = the grid
+  lgx_tail_s8_seg s[LGX_TAIL_S8_MAX];
+};
+static_assert(sizeof(TailK) <= 4096, "kernel argument segment");
+
+__device__ __forceinline__ void s8_put(const lgx_tail_s8_seg& S, int r, int c, float x) {
+  const __bf16 h = (__bf16)x;
+  const __bf16 l = (__bf16)(x - (float)h);
+  char* q;
+  int lo;
+  if (S.packed) {
+    q = S.dst + ((int64_t)(r >> 4) * S.ld + (c >> 5)) * 2048 + ((((c >> 3) & 3) << 4) | (r & 15)) * 16 + (c & 7) * 2;
+    lo = 1024;
+  } else {
+    q = S.dst + (int64_t)r * S.ld * 4 + (c >> 3) * 32 + (c & 7) * 2;
+    lo = 16;
+  }
+  *reinterpret_cast<__bf16*>(q) = h;
+  *reinterpret_cast<__bf16*>(q + lo) = l;
+}
+
+// 4 consecutive columns c..c+3 (c % 4 == 0) of row r: 8 B of hi, 8 B of lo (same group half)
+__device__ __forceinline__ void s8_put4(const lgx_tail_s8_seg& S, int r, int c, const float (&x)[4]) {
+  uint32_t h[2], l[2];
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const __bf16 h0 = (__bf16)x[2 * e], h1 = (__bf16)x[2 * e + 1];
+    const __bf16 l0 = (__bf16)(x[2 * e] - (float)h0), l1 = (__bf16)(x[2 * e + 1] - (float)h1);
+    h[e] = (uint32_t)__builtin_bit_cast(uint16_t, h0) | ((uint32_t)__builtin_bit_cast(uint16_t, h1) << 16);
+    l[e] = (uint32_t)__builtin_bit_cast(uint16_t, l0) | ((uint32_t)__builtin_bit_cast(uint16_t, l1) << 16);
+  }
+  char* q;
+  int lo;
+  if (S.packed) {
+    q = S.dst + ((int64_t)(r >> 4) * S.ld + (c >> 5)) * 2048 + ((((c >> 3) & 3) << 4) | (r & 15)) * 16 + (c & 7) * 2;
+    lo = 1024;
+  } else {
+    q = S.dst + (int64_t)r * S.ld * 4 + (c >> 3) * 32 + (c & 7) * 2;
+    lo = 16;
+  }
+  *reinterpret_cast<uint2*>(q) = make_uint2(h[0], h[1]);
+  *reinterpret_cast<uint2*>(q + lo) = make_uint2(l[0], l[1]);
+}
+
+__global__ __launch_bounds__(256) void tail_adam_ranges(TailK k) {
+  __shared__ float red[4 * 2];
+  __shared__ float sc[2];
+  const lgx_ppo_tail_args& p = k.p;
+  {  // the clip coefficients from tail_norms' partials (as tail_adam)
+    float t[2];
+    final_sum<2>(p.ws, 2, TAIL_BLOCKS, t, red);
+    if (threadIdx.x == 0) {
+      sc[0] = fminf(p.max_norm / (sqrtf(t[0]) + 1e-6f), 1.f);
+      sc[1] = fminf(p.max_norm / (sqrtf(t[1]) + 1e-6f), 1.f);
+    }
+    __syncthreads();
+  }
+  int ri = 0, hi_ = k.nr - 1;  // this block's range (binary search on the first blocks)
+  while (ri < hi_) {
+    const int mid = (ri + hi_ + 1) >> 1;
+    if ((int)blockIdx.x >= k.r[mid].blk0) ri = mid;
+    else hi_ = mid - 1;
+  }
+  TailRange R = k.r[ri];
+  const float c = R.opt == 1 ? sc[0] : sc[1];
+  const int64_t nb = k.r[ri + 1].blk0 - R.blk0;
+  const int64_t stride = nb * blockDim.x;
+  const int64_t i0 = (int64_t)(blockIdx.x - R.blk0) * blockDim.x + threadIdx.x;
+  int64_t a, b;
+  body4(R.lo, R.hi, a, b);
+  if (R.opt == 2) {  // g[adapt] *= coef_m
+    float4* g4 = reinterpret_cast<float4*>(p.grads + a);
+    for (int64_t j = i0; j < (b - a) >> 2; j += stride) {
+      float4 x = g4[j];
+      x.x *= c; x.y *= c; x.z *= c; x.w *= c;
+      g4[j] = x;
+    }
+    if (i0 < a - R.lo) p.grads[R.lo + i0] *= c;
+    if (i0 < R.hi - b) p.grads[b + i0] *= c;
+    return;
+  }
+  const bool est = R.opt == 1;
+  const float t = est ? *p.step_est : *p.step_main;
+  const float b1 = est ? p.b1_est : p.b1_main, b2 = est ? p.b2_est : p.b2_main, eps = est ? p.eps_est : p.eps_main;
+  const float lr = est ? p.est_lr : *p.lr32;
+  const float ss = lr / (1.f - powf(b1, t)), sq = sqrtf(1.f - powf(b2, t));
+  // the weight's S8 entries (all share p0, N, K)
+#ifdef LGX_TAIL_NOEMIT  // dev builds: the ranges kernel without its S8 stores (timing only)
+  R.nseg = 0;
+#endif
+  const int64_t p0 = R.nseg > 0 ? k.s[R.seg0].p0 : 0;
+  const int K = R.nseg > 0 ? k.s[R.seg0].K : 1;
+  // the weight's entries (<= 4 used here: the segmented first layer's spans, or a row-major and
+  // a packed copy), hoisted out of the element loop
+  constexpr int NSEG = 4;
+  lgx_tail_s8_seg sg[NSEG];
+  const int ns = min(R.nseg, NSEG);
+#pragma unroll
+  for (int e = 0; e < NSEG; ++e) sg[e] = k.s[R.seg0 + min(e, max(ns - 1, 0))];
+  auto emit_rc = [&](int r, int col, float x) {
+#pragma unroll
+    for (int e = 0; e < NSEG; ++e) {
+      const int cc = col - sg[e].c0;
+      if (e < ns && cc >= 0 && cc < sg[e].w) s8_put(sg[e], r, cc, x);
+    }
+  };
+  auto emit = [&](int64_t i, float x) {
+    const int d = (int)(i - p0);
+    const int r = d / K;
+    emit_rc(r, d - r * K, x);
+  };
+  float4* P = reinterpret_cast<float4*>(p.params + a);
+  const float4* G = reinterpret_cast<const float4*>(p.grads + a);
+  float4* M = reinterpret_cast<float4*>(p.exp_avg + a);
+  float4* V = reinterpret_cast<float4*>(p.exp_avg_sq + a);
+  for (int64_t j = i0; j < (b - a) >> 2; j += stride) {
+    float4 x = P[j], m = M[j], v = V[j];
+    const float4 g = G[j];
+    adam1(x.x, g.x * c, m.x, v.x, b1, b2, eps, ss, sq);
+    adam1(x.y, g.y * c, m.y, v.y, b1, b2, eps, ss, sq);
+    adam1(x.z, g.z * c, m.z, v.z, b1, b2, eps, ss, sq);
+    adam1(x.w, g.w * c, m.w, v.w, b1, b2, eps, ss, sq);
+    P[j] = x; M[j] = m; V[j] = v;
+    if (R.nseg > 0) {  // one division per float4: the next three elements by carry
+      const int d = (int)(a + 4 * j - p0);
+      int r = d / K, col = d - r * K;
+      const float xs[4] = {x.x, x.y, x.z, x.w};
+      if ((col & 3) == 0 && col + 4 <= K) {  // one row: whole 4-column pieces where they fit
+#pragma unroll
+        for (int e = 0; e < NSEG; ++e) {
+          const int cc = col - sg[e].c0;
+          if (e >= ns || cc + 4 <= 0 || cc >= sg[e].w) continue;
+          if ((cc & 3) == 0 && cc >= 0 && cc + 4 <= sg[e].w) {
+            s8_put4(sg[e], r, cc, xs);
+          } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              if (cc + q >= 0 && cc + q < sg[e].w) s8_put(sg[e], r, cc + q, xs[q]);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          emit_rc(r, col, xs[e]);
+          if (++col == K) { col = 0; ++r; }
+        }
+      }
+    }
+  }
+  if (i0 < a - R.lo) {
+    const int64_t i = R.lo + i0;
+    adam1(p.params[i], p.grads[i] * c, p.exp_avg[i], p.exp_avg_sq[i], b1, b2, eps, ss, sq);
+    if (R.nseg > 0) emit(i, p.params[i]);
+  }
+  if (i0 < R.hi - b) {
+    const int64_t i = b + i0;
+    adam1(p.params[i], p.grads[i] * c, p.exp_avg[i], p.exp_avg_sq[i], b1, b2, eps, ss, sq);
+    if (R.nseg > 0) emit(i, p.params[i]);
+  }
+}
+
 // dynamic LDS: two K-step stages of hi/lo A and B images, or the fp32 C image (reused)
 constexpr size_t lds_bytes(int bn, int bm = BM) {
   const size_t stages = 2 * (2 * bm * PITCH + 2 * bn * PITCH) * sizeof(__bf16);
@@ -3011,7 +3186,67 @@ int32_t lgx_ppo_tail(const lgx_ppo_tail_args* a, void* stream) {
     return fail("lgx_ppo_tail: bad ranges");
   for (int k = 0; k < a->nloss; ++k)
     if (!a->loss_ptrs[k]) return fail("lgx_ppo_tail: null loss pointer");
+  if (a->n_s8 < 0 || a->n_s8 > LGX_TAIL_S8_MAX || (a->n_s8 > 0 && !a->s8))
+    return fail("lgx_ppo_tail: bad S8 segment table");
   hipStream_t s = static_cast<hipStream_t>(stream);
+  if (a->n_s8 > 0) {
+    // ranges: the main / estimator segments cut at every S8 weight's [p0, p0 + N K), then the
+    // adaptation scaling; a weight's entries are consecutive in the table (same p0)
+#ifndef LGX_TAIL_ELEMS
+#define LGX_TAIL_ELEMS 1024
+#endif
+    constexpr int64_t TAIL_ELEMS = LGX_TAIL_ELEMS;  // elements per block (one float4 per thread)
+    static lgxm::TailK k;
+    k = lgxm::TailK{};
+    k.p = *a;
+    for (int i = 0; i < a->n_s8; ++i) {
+      const lgx_tail_s8_seg& q = a->s8[i];
+      if (q.N <= 0 || q.K <= 0 || q.w <= 0 || q.c0 < 0 || q.c0 + q.w > q.K || !q.dst || q.ld <= 0 ||
+          (int64_t)q.N * q.K >= (1ll << 31))
+        return fail("lgx_ppo_tail: bad S8 entry");
+      if (i > 0 && q.p0 < a->s8[i - 1].p0) return fail("lgx_ppo_tail: S8 entries must be sorted by p0");
+      if (i > 0 && q.p0 == a->s8[i - 1].p0 && (q.N != a->s8[i - 1].N || q.K != a->s8[i - 1].K))
+        return fail("lgx_ppo_tail: S8 entries of one weight disagree on its shape");
+      k.s[i] = q;
+    }
+    int nr = 0, blk = 0;
+    auto add = [&](int64_t lo, int64_t hi, int opt, int seg0, int nseg) -> bool {
+      if (hi <= lo) return true;
+      if (nr >= lgxm::TAIL_RMAX) return false;
+      lgxm::TailRange& r = k.r[nr++];
+      r.lo = lo; r.hi = hi; r.opt = opt; r.seg0 = seg0; r.nseg = nseg; r.blk0 = blk;
+      blk += (int)std::max<int64_t>(1, (hi - lo + TAIL_ELEMS - 1) / TAIL_ELEMS);
+      return true;
+    };
+    const int64_t segs[2][2] = {{a->main_lo, a->main_hi}, {a->est_lo, a->est_hi}};
+    bool ok = true;
+    for (int o = 0; o < 2 && ok; ++o) {
+      int64_t cur = segs[o][0];
+      for (int i = 0; i < a->n_s8 && ok;) {
+        int j = i;
+        while (j < a->n_s8 && a->s8[j].p0 == a->s8[i].p0) ++j;
+        if (j - i > 4) return fail("lgx_ppo_tail: more than 4 S8 entries for one weight");
+        const int64_t w0 = a->s8[i].p0, w1 = w0 + (int64_t)a->s8[i].N * a->s8[i].K;
+        if (w0 >= segs[o][0] && w1 <= segs[o][1]) {
+          if (w0 < cur) return fail("lgx_ppo_tail: overlapping S8 weights");
+          ok = add(cur, w0, o, 0, 0) && add(w0, w1, o, i, j - i);
+          cur = w1;
+        } else if (w0 < segs[o][1] && w1 > segs[o][0]) {
+          return fail("lgx_ppo_tail: an S8 weight straddles a segment boundary");
+        }
+        i = j;
+      }
+      ok = ok && add(cur, segs[o][1], o, 0, 0);
+    }
+    ok = ok && add(a->adapt_lo, a->adapt_hi, 2, 0, 0);
+    if (!ok) return fail("lgx_ppo_tail: too many ranges");
+    k.nr = nr;
+    k.r[nr].blk0 = blk;
+    hipLaunchKernelGGL(lgxm::tail_norms, dim3(lgxm::TAIL_BLOCKS), dim3(256), 0, s, *a);
+    if (blk > 0) hipLaunchKernelGGL(lgxm::tail_adam_ranges, dim3(blk), dim3(256), 0, s, k);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : fail(hipGetErrorString(e));
+  }
   hipLaunchKernelGGL(lgxm::tail_norms, dim3(lgxm::TAIL_BLOCKS), dim3(256), 0, s, *a);
   hipLaunchKernelGGL(lgxm::tail_adam, dim3(1024), dim3(256), 0, s, *a);
   hipError_t e = hipGetLastError();
@@ -3491,7 +3726,29 @@ namespace lgxm {
 // on_policy_runner.py:160-170 bookkeeping: one workgroup of 1024 threads, each owning a
 // contiguous chunk of envs; the done count per chunk is scanned across the block so every
 // done env knows its rank among all done envs (env order, as torch.cumsum gives).
-__global__ __launch_bounds__(1024) void track_kernel(lgx_track_args a) {
+__device__ __forceinline__ void track_block(const lgx_track_args& a);
+__global__ __launch_bounds__(1024) void track_kernel(lgx_track_args a) { track_block(a); }
+
+// The rollout step's transition row and episode bookkeeping in ONE launch (lgx_post_step):
+// blocks 0 .. nt-1 (1024 threads) store the transition, block nt runs track_block. The two read
+// the same env outputs and write disjoint buffers, so their blocks need no ordering.
+__global__ __launch_bounds__(1024) void post_step_kernel(lgx_transition_args p, lgx_track_args a, int nt) {
+  if ((int)blockIdx.x < nt) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= p.B) return;
+    const float v = p.values[i];
+    float r = p.rewards[i];
+    const bool d = p.dones[i] != 0;
+    if (p.time_outs) r = r + p.gamma * (v * (float)p.time_outs[i]);
+    p.rewards_out[i] = r;
+    p.dones_out[i] = d ? 1 : 0;
+    p.values_out[i] = v;
+    return;
+  }
+  track_block(a);
+}
+
+__device__ __forceinline__ void track_block(const lgx_track_args& a) {
   __shared__ int wsum[16];
   __shared__ int k_all;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -3604,6 +3861,19 @@ int32_t lgx_track_episodes(const lgx_track_args* a, void* stream) {
   return e == hipSuccess ? 0 : fail(hipGetErrorString(e));
 }
 
+int32_t lgx_post_step(const lgx_transition_args* t, const lgx_track_args* a, void* stream) {
+  if (!a) return lgx_store_transition(t, stream);
+  if (!t || !t->rewards || !t->dones || !t->values || !t->rewards_out || !t->dones_out || !t->values_out || t->B < 0)
+    return fail("lgx_post_step: bad transition arguments");
+  if (!a->rewards || !a->dones || !a->cur_rew || !a->cur_len || !a->rew_ring || !a->len_ring || !a->ptr ||
+      !a->n || a->N < 0 || a->na < 0 || a->nb < 0 || a->na + a->nb > 1024 ||
+      (a->ep_sum && (!a->ep_cnt || (a->na && !a->ep_a) || (a->nb && !a->ep_b))))
+    return fail("lgx_post_step: bad tracking arguments");
+  const int nt = (t->B + 1023) / 1024;
+  hipLaunchKernelGGL(lgxm::post_step_kernel, dim3(nt + 1), dim3(1024), 0, static_cast<hipStream_t>(stream), *t, *a, nt);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : fail(hipGetErrorString(e));
+}
 int32_t lgx_store_transition(const lgx_transition_args* a, void* stream) {
   if (!a || !a->rewards || !a->dones || !a->values || !a->rewards_out || !a->dones_out || !a->values_out || a->B < 0)
     return fail("lgx_store_transition: bad arguments");

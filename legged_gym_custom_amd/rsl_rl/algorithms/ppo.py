@@ -51,6 +51,8 @@ GRAPH_ALLREDUCE = os.environ.get("LGX_GRAPH_ALLREDUCE", "0") != "0"
 # the DAgger minibatch as one fused launch (lgx_adaptation_train) + one reduce, instead of the
 # adaptation encoder's autograd graph
 DAGGER_FUSED = os.environ.get("LGX_DAGGER_FUSED", "1") != "0"
+# dev knob: LGX_POST_STEP=0 launches the transition row and the episode bookkeeping separately
+POST_STEP_FUSED = os.environ.get("LGX_POST_STEP", "1") != "0"
 DAGGER_BLOCKS = 512  # lgx_adaptation_train's block budget (two per CU: <= 80 KB of LDS each)
 
 
@@ -399,9 +401,16 @@ class PPO:
     def _gpu_rollout(self):
         return str(self.device).startswith("cuda")
 
-    def process_env_step(self, rewards, dones, infos):
-        """ppo.py:156-171: time-out bootstrap r += γ V(s) on timed-out envs."""
+    def post_step_fusable(self):
+        """process_env_step takes the runner's episode-tracking arguments (one launch for both)."""
+        return self._gpu_rollout() and POST_STEP_FUSED
+
+    def process_env_step(self, rewards, dones, infos, track=None):
+        """ppo.py:156-171: time-out bootstrap r += γ V(s) on timed-out envs. track: the runner's
+        lgx_track_episodes arguments (GPU), launched with the transition row as one kernel."""
         t = self.transition
+        if track is not None and not self._gpu_rollout():
+            raise ValueError("process_env_step: fused tracking needs the GPU rollout")
         if self._gpu_rollout():
             # bootstrap + rewards/dones/values rows in one HIP kernel (lgx_store_transition)
             s, k = self.storage, self.storage.step
@@ -411,7 +420,7 @@ class PPO:
             b = lambda x: x.view(torch.uint8) if x.dtype == torch.bool else x.to(torch.uint8)  # noqa: E731
             hip_mlp.store_transition(rewards.contiguous(), b(dones), None if to is None else b(to),
                                      t.values.reshape(-1), s.rewards[k].view(-1), s.dones[k].view(-1),
-                                     s.values[k].view(-1), self.gamma)
+                                     s.values[k].view(-1), self.gamma, track=track)
             s.step += 1
             t.clear()
             self.actor_critic.reset(dones)
@@ -557,7 +566,8 @@ class PPO:
                              self.desired_kl if adaptive else 0.0, self._lr64, self._lr32,
                              self._opt_step["optimizer"], self._opt_step["estimator_optimizer"],
                              [self._head_out[1], self._head_out[0], self._aux_out[0], self._aux_out[1]], self._sums,
-                             self._tail_ws, self._tail_counter)
+                             self._tail_ws, self._tail_counter,
+                             s8=self._s8.tail_table() if self._s8 is not None else None)
             return
         with torch.no_grad():
             _clip_([g.segment("estimator")], self.max_grad_norm)

@@ -6,7 +6,9 @@ graph, no per-call allocation (the hipGraph captures exactly these launches):
   per update   the network inputs of every row, gathered in the epoch-shared permutation
                (rollout_storage.py:141-147) and split into S8 (bf16 hi/lo planes) in one launch
   per minibatch
-    1  the 17 weight matrices -> S8 (one launch; they change after every Adam step)
+    1  the 17 weight matrices -> S8 (one launch; they change after every Adam step) — at the
+       update's first minibatch only: the optimizer tail (lgx_ppo_tail's Adam launch) writes the
+       updated weights' S8 copies itself (tail_table)
     2  forward, one grouped launch per level: {priv, scan, est, critic} layers 0..2, then the
        critic's last layer beside the actor's first, then the actor (actor_critic.py:82-107,
        support_networks.py:25-80). Every epilogue writes its output in S8 (the next GEMMs'
@@ -211,6 +213,46 @@ class S8Minibatch:
                 self.wsplit.append(S.split_packed_job(W.detach(), Wp))
         self._fwd_levels = None  # built per minibatch offset (input row pointers)
         self._shapes = shapes
+        # the same S8 destinations as optimizer-tail entries (lgx_tail_s8_seg): the Adam launch
+        # writes each updated weight's S8 copies itself, so only an update's first minibatch needs
+        # the split launch (prepare); None where a weight is not a view of the flat parameters
+        self.tail_segs = self._tail_segments()
+        self._tail_dev = None
+
+    def _tail_segments(self):
+        """[(p0, N, K, c0, w, dst, ld, packed)] of every S8 weight copy (include/lgx_mlp.h
+        lgx_tail_s8_seg), or None."""
+        pb = getattr(self.alg, "params_buf", None)
+        if pb is None or not H.TAIL_S8 or pb.dtype != torch.float32:
+            return None
+        base, end = pb.data_ptr(), pb.data_ptr() + 4 * pb.numel()
+        segs = []
+        for p in self.parts:
+            for l, W in enumerate(p.W):
+                a = W.data_ptr()
+                if not (base <= a < end) or (a - base) % 4 or not W.is_contiguous():
+                    return None
+                N, K = W.shape
+                Ws = p.Ws[l]
+                if p is self.actor and l == 0:
+                    for (c, s8, w) in self.spans:
+                        if w:
+                            segs.append(((a - base) // 4, N, K, c, w, S.group_ptr(Ws, s8), Ws.shape[1], 0))
+                else:
+                    segs.append(((a - base) // 4, N, K, 0, K, Ws.data_ptr(), Ws.shape[1], 0))
+        for p in ((self.priv, self.scan) if self.enc_chain else ()):
+            for W, Wp in zip(p.W, p.Wp):
+                N, K = W.shape
+                segs.append(((W.data_ptr() - base) // 4, N, K, 0, K, Wp.data_ptr(), (K + 31) // 32, 1))
+        return segs if len(segs) <= H.TAIL_S8_MAX else None
+
+    def tail_table(self):
+        """(host table, count) for lgx_ppo_tail, or None (the split then runs per minibatch)."""
+        if self.tail_segs is None:
+            return None
+        if self._tail_dev is None:
+            self._tail_dev = H.tail_s8_table(self.tail_segs)
+        return self._tail_dev, len(self.tail_segs)
 
     def _fwd(self, p, l, A_ptr, lda, K, C=None, ldc=0, C32=None, ldc32=0, elu=True, n0=0, n1=None):
         """Layer l's forward GemmArgs; n0, n1: only output columns [n0, n1) (C already offset)."""
@@ -236,7 +278,8 @@ class S8Minibatch:
                 S.split_job(critic, self.crin.data_ptr(), self.crin.shape[1], idx=perm, rows=self.rows),
                 S.split_job(priv, self.prin.data_ptr(), self.prin.shape[1], idx=perm, rows=self.rows),
                 S.split_job(scan, self.scin.data_ptr(), self.scin.shape[1], idx=perm, rows=self.rows)]
-        S.split(jobs)
+        # with tail_segs the update's weights too (the optimizer tail keeps the copies current)
+        S.split(jobs + (self.wsplit if self.tail_segs is not None else []))
 
     # ------------------------------------------------------------------ one minibatch
     def run(self, i, shuf, adapt_latent, head_out, aux_out, kl_dst):
@@ -248,8 +291,9 @@ class S8Minibatch:
         a, pr, sc, es, cr = self.actor, self.priv, self.scan, self.est, self.critic
         row = lambda buf, col=0: S.group_ptr(buf, col) + 4 * r0 * buf.shape[1]  # noqa: E731
         lda_ain = self.ain.shape[1]
-        # 1. weights -> S8
-        S.split(self.wsplit)
+        # 1. weights -> S8 (with tail_segs: once per update in prepare, then by the optimizer tail)
+        if self.tail_segs is None:
+            S.split(self.wsplit)
         # 2. forward
         ins = {"priv": (row(self.prin), self.prin.shape[1], pr.W[0].shape[1]),
                "scan": (row(self.scin), self.scin.shape[1], sc.W[0].shape[1]),

@@ -20,7 +20,7 @@ import torch.nn as nn
 _LIB_PATH = os.environ.get("LGX_MLP_LIB") or os.path.join(
     os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))), "lib", "liblgx_mlp.so")
 _lib = None
-ABI_VERSION = 10
+ABI_VERSION = 11
 EPI_BIAS, EPI_ELU, EPI_DELU, EPI_ACCUM = 1, 2, 4, 8
 EXPORTED = ["lgx_mlp_abi_version", "lgx_mlp_sizeof_gemm_args", "lgx_mlp_pick_split", "lgx_gemm",
             "lgx_mlp_last_error", "lgx_adam_step", "lgx_ppo_head_forward", "lgx_ppo_head_backward",
@@ -29,8 +29,12 @@ EXPORTED = ["lgx_mlp_abi_version", "lgx_mlp_sizeof_gemm_args", "lgx_mlp_pick_spl
             "lgx_mlp_pick_split_group", "lgx_gae", "lgx_normalize_advantages",
             "lgx_gather_rows", "lgx_transpose_batch", "lgx_loss_heads_forward", "lgx_loss_heads_backward",
             "lgx_track_episodes", "lgx_chain", "lgx_adaptation_forward", "lgx_loss_heads_fused",
-            "lgx_loss_heads_tail", "lgx_adaptation_train", "lgx_clip_adam"]
+            "lgx_loss_heads_tail", "lgx_adaptation_train", "lgx_clip_adam", "lgx_post_step"]
 TAIL_MAX_LOSSES = 8
+TAIL_S8_MAX = 32
+# dev knob: LGX_TAIL_S8=0 keeps the per-minibatch weight split launch (the optimizer tail then
+# writes no S8 copies)
+TAIL_S8 = os.environ.get("LGX_TAIL_S8", "1") != "0"
 COPY_MAX = 16
 SPLITK_MAX = 24
 GROUP_MAX = 20
@@ -110,7 +114,21 @@ class TailArgs(C.Structure):
                                          "est_lr")] + \
                [("desired_kl", C.c_double), ("lr64", C.c_void_p), ("lr32", C.c_void_p), ("step_main", C.c_void_p),
                 ("step_est", C.c_void_p), ("loss_ptrs", C.c_void_p * TAIL_MAX_LOSSES), ("sums", C.c_void_p),
-                ("nloss", C.c_int32), ("ws", C.c_void_p), ("counter", C.c_void_p)]
+                ("nloss", C.c_int32), ("ws", C.c_void_p), ("counter", C.c_void_p), ("s8", C.c_void_p),
+                ("n_s8", C.c_int32)]
+
+
+class TailS8Seg(C.Structure):
+    """Mirror of lgx_tail_s8_seg."""
+    _fields_ = [("p0", C.c_int64), ("N", C.c_int32), ("K", C.c_int32), ("c0", C.c_int32), ("w", C.c_int32),
+                ("dst", C.c_void_p), ("ld", C.c_int32), ("packed", C.c_int32)]
+
+
+def tail_s8_table(segs):
+    """[(p0, N, K, c0, w, dst, ld, packed)] -> the host table lgx_ppo_tail reads (sorted by p0,
+    a weight's entries consecutive)."""
+    segs = sorted(segs, key=lambda q: q[0])
+    return (TailS8Seg * len(segs))(*[TailS8Seg(*q) for q in segs])
 
 
 class CopyDesc(C.Structure):
@@ -408,21 +426,29 @@ def act_head(mean, std, eps, actions, mu, sigma, logp, actions_copy=None, noise=
     _check(lib().lgx_act_head(C.byref(args), _stream()), "lgx_act_head")
 
 
-def store_transition(rewards, dones, time_outs, values, rewards_out, dones_out, values_out, gamma):
+def store_transition(rewards, dones, time_outs, values, rewards_out, dones_out, values_out, gamma, track=None):
+    """lgx_store_transition, or with `track` (track_episodes(..., launch=False)'s arguments) the
+    step's transition and episode bookkeeping in one lgx_post_step launch."""
     args = TransitionArgs(rewards.data_ptr(), dones.data_ptr(), None if time_outs is None else time_outs.data_ptr(),
                           values.data_ptr(), rewards_out.data_ptr(), dones_out.data_ptr(), values_out.data_ptr(),
                           float(gamma), rewards.shape[0])
+    if track is not None:
+        _check(lib().lgx_post_step(C.byref(args), C.byref(track), _stream()), "lgx_post_step")
+        return
     _check(lib().lgx_store_transition(C.byref(args), _stream()), "lgx_store_transition")
 
 
-def track_episodes(rewards, dones, st, ep_a=None, ep_b=None):
-    """lgx_track_episodes on the runner's stats dict (on_policy_runner.py:160-170)."""
+def track_episodes(rewards, dones, st, ep_a=None, ep_b=None, launch=True):
+    """lgx_track_episodes on the runner's stats dict (on_policy_runner.py:160-170); with
+    launch=False the arguments only (for store_transition's one-launch form)."""
     p = lambda t: None if t is None else t.data_ptr()  # noqa: E731
     args = TrackArgs(rewards.data_ptr(), dones.data_ptr(), st["cur_rew"].data_ptr(), st["cur_len"].data_ptr(),
                      st["rew_ring"].data_ptr(), st["len_ring"].data_ptr(), st["ptr"].data_ptr(), st["n"].data_ptr(),
                      p(ep_a), p(ep_b), p(st["ep_sum"] if ep_a is not None or ep_b is not None else None),
                      p(st["ep_cnt"] if ep_a is not None or ep_b is not None else None), rewards.shape[0],
                      0 if ep_a is None else ep_a.numel(), 0 if ep_b is None else ep_b.numel())
+    if not launch:
+        return args
     _check(lib().lgx_track_episodes(C.byref(args), _stream()), "lgx_track_episodes")
 
 
@@ -1506,9 +1532,11 @@ def loss_heads(mu, value, std, actions, old_logp, adv, target_values, returns, o
 
 
 def ppo_tail(grads, params, exp_avg, exp_avg_sq, main, est, adapt, kl_index, max_norm, betas_main, eps_main,
-             betas_est, eps_est, est_lr, desired_kl, lr64, lr32, step_main, step_est, loss_ptrs, sums, ws, counter):
+             betas_est, eps_est, est_lr, desired_kl, lr64, lr32, step_main, step_est, loss_ptrs, sums, ws, counter,
+             s8=None):
     """lgx_ppo_tail: clip + Adam of both optimizers, the KL schedule and the loss sums
-    (one minibatch's optimizer tail, two launches). main/est/adapt: (lo, hi) element ranges."""
+    (one minibatch's optimizer tail, two launches). main/est/adapt: (lo, hi) element ranges.
+    s8: optional (table from tail_s8_table, count): the updated weights' S8 copies."""
     a = TailArgs(grads=grads.data_ptr(), params=params.data_ptr(), exp_avg=exp_avg.data_ptr(),
                  exp_avg_sq=exp_avg_sq.data_ptr(), main_lo=main[0], main_hi=main[1], est_lo=est[0], est_hi=est[1],
                  adapt_lo=adapt[0], adapt_hi=adapt[1], kl_index=kl_index, max_norm=max_norm,
@@ -1519,4 +1547,6 @@ def ppo_tail(grads, params, exp_avg, exp_avg_sq, main, est, adapt, kl_index, max
                  counter=counter.data_ptr())
     for k, t in enumerate(loss_ptrs):
         a.loss_ptrs[k] = t.data_ptr()
+    if s8 is not None:
+        a.s8, a.n_s8 = C.addressof(s8[0]), s8[1]
     _check(lib().lgx_ppo_tail(C.byref(a), _stream()), "lgx_ppo_tail")

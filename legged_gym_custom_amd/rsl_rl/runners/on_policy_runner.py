@@ -158,10 +158,11 @@ class OnPolicyRunner:
             st["ep_sum"] += torch.stack([ep[key].reshape(()).to(self.device).float() for key in st["ep_keys"]])
             st["ep_cnt"] += 1
 
-    def _track_native(self, rewards, dones, infos):
+    def _track_native(self, rewards, dones, infos, launch=True):
         """One lgx_track_episodes launch for the whole bookkeeping when the buffers allow it
         (HIP device, fp32 rewards, bool/uint8 dones, infos['episode'] values laid out as at most
-        two contiguous fp32 runs, e.g. the env's episode means and its terrain-level mean)."""
+        two contiguous fp32 runs, e.g. the env's episode means and its terrain-level mean).
+        launch=False: its arguments (the post-step launch's), or False."""
         st = self._stats
         if not (rewards.is_cuda and rewards.dtype == torch.float32 and dones.dtype in (torch.bool, torch.uint8)
                 and rewards.is_contiguous() and dones.is_contiguous()):
@@ -181,8 +182,8 @@ class OnPolicyRunner:
                 return False
         from legged_gym_custom_amd.rsl_rl.modules import hip_mlp as H
         a, b = (runs + [None, None])[:2] if runs else (None, None)
-        H.track_episodes(rewards, dones.view(torch.uint8), st, a, b)
-        return True
+        args = H.track_episodes(rewards, dones.view(torch.uint8), st, a, b, launch=launch)
+        return args if not launch else True
 
     @staticmethod
     def _ep_runs(vals):
@@ -212,8 +213,12 @@ class OnPolicyRunner:
             if dst.data_ptr() != src.data_ptr():
                 dst.copy_(src)
         rewards, dones = rewards.to(self.device), dones.to(self.device)
-        self.alg.process_env_step(rewards, dones, infos)
-        if track:
+        # the transition row and the episode bookkeeping as one launch where both are native
+        targs = None
+        if track and getattr(self.alg, "post_step_fusable", lambda: False)():
+            targs = self._track_native(rewards, dones, infos, launch=False) or None
+        self.alg.process_env_step(rewards, dones, infos, track=targs)
+        if track and targs is None:
             self._track_episodes(rewards, dones, infos)
 
     def _graphable(self, adaptation_mode):

@@ -193,3 +193,51 @@ def test_native_episode_tracking_matches_torch_statement(n):
         assert torch.equal(sa[key], sb[key]), key
     for key in ("rew_ring", "len_ring"):
         assert torch.equal(sa[key][:100], sb[key][:100]), key
+
+
+@pytest.mark.parametrize("n", [4096, 100, 12289])
+def test_post_step_launch_equals_transition_and_tracking(n):
+    """lgx_post_step (the transition row and the episode bookkeeping in one launch) ==
+    lgx_store_transition then lgx_track_episodes, bitwise: storage rows and every tracking buffer."""
+    import types
+    import torch
+    from legged_gym_custom_amd.rsl_rl.modules import hip_mlp
+    from legged_gym_custom_amd.rsl_rl.runners.on_policy_runner import OnPolicyRunner
+    dev = "cuda"
+
+    def stats():
+        z = lambda *sh: torch.zeros(*sh, device=dev)  # noqa: E731
+        return {"cur_rew": z(n), "cur_len": z(n), "rew_ring": z(101), "len_ring": z(101),
+                "ptr": torch.zeros((), dtype=torch.long, device=dev), "n": torch.zeros((), dtype=torch.long, device=dev),
+                "ep_keys": None, "ep_sum": None, "ep_cnt": z(())}
+    means, level = torch.zeros(15, device=dev), torch.zeros((), device=dev)
+    infos = {"episode": {**{f"rew_{i}": means[i] for i in range(15)}, "terrain_level": level}}
+    runs = [types.SimpleNamespace(_stats=stats(), device=dev, _ep_runs=OnPolicyRunner._ep_runs) for _ in range(2)]
+    rows = [[torch.zeros(n, device=dev), torch.zeros(n, dtype=torch.uint8, device=dev), torch.zeros(n, device=dev)]
+            for _ in range(2)]
+    g = torch.Generator(device=dev).manual_seed(5)
+    for k in range(40):
+        p = 0.05 if k % 3 == 0 else 0.004
+        rew = torch.randn(n, device=dev, generator=g)
+        dones = torch.rand(n, device=dev, generator=g) < p
+        tout = (torch.rand(n, device=dev, generator=g) < 0.5) & dones
+        vals = torch.randn(n, device=dev, generator=g)
+        means.copy_(torch.randn(15, device=dev, generator=g))
+        level.fill_(float(k))
+        for fused, (r, (ro, do, vo)) in enumerate(zip(runs, rows)):
+            if fused:
+                targs = OnPolicyRunner._track_native(r, rew, dones, infos, launch=False)
+                assert targs
+                hip_mlp.store_transition(rew, dones.view(torch.uint8), tout.view(torch.uint8), vals, ro, do, vo, 0.99,
+                                         track=targs)
+            else:
+                hip_mlp.store_transition(rew, dones.view(torch.uint8), tout.view(torch.uint8), vals, ro, do, vo, 0.99)
+                assert OnPolicyRunner._track_native(r, rew, dones, infos)
+        torch.cuda.synchronize()
+        for x, y in zip(rows[0], rows[1]):
+            assert torch.equal(x, y)
+    sa, sb = runs[0]._stats, runs[1]._stats
+    for key in ("cur_rew", "cur_len", "ptr", "n", "ep_sum", "ep_cnt"):
+        assert torch.equal(sa[key], sb[key]), key
+    for key in ("rew_ring", "len_ring"):
+        assert torch.equal(sa[key][:100], sb[key][:100]), key

@@ -70,3 +70,30 @@ def test_s8_update_graph_equals_eager():
         torch.cuda.synchronize()
         outs.append(torch.cat([p.detach().reshape(-1) for _n, p in R.named_params(alg)]))
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("graphs", [False, True])
+def test_tail_writes_the_weight_split(graphs):
+    """The optimizer tail's S8 copies of the updated weights (lgx_ppo_tail with the S8 table,
+    include/lgx_mlp.h lgx_tail_s8_seg) equal a weight split launch of the same weights bit for
+    bit, every row-major copy (the actor's segmented first layer included) and the encoders'
+    fragment-packed ones, after updates whose minibatches ran no per-minibatch split."""
+    from legged_gym_custom_amd.rsl_rl.modules import hip_s8 as S
+    case = "go2"
+    alg = R.build(case, dev, use_graphs=graphs)
+    res = {}
+    perm = torch.from_numpy(LC.permutation(case, 1)).to(dev)
+    alg._next_perm = lambda n, p=perm: p
+    for _ in range(2):
+        R.rollout(alg, case, 1, res, False, dev)
+        alg.total_updates = LC.TOTAL_UPDATES
+        alg.update()
+    s8 = alg._s8
+    assert s8 is not None and s8.tail_segs is not None and s8.tail_table() is not None
+    bufs = [Ws for p in s8.parts for Ws in p.Ws] + [Wp for p in s8.parts for Wp in getattr(p, "Wp", [])]
+    torch.cuda.synchronize()
+    got = [b.clone() for b in bufs]
+    S.split(s8.wsplit)
+    torch.cuda.synchronize()
+    for k, (g, b) in enumerate(zip(got, bufs)):
+        assert torch.equal(g, b), f"S8 copy {k} differs from the split of the updated weights"

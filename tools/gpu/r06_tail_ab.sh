@@ -1,0 +1,5 @@
+set -o pipefail
+R=$GRAFT_REPO_ROOT; cd $R
+for L in "" $R/legged_gym_custom_amd/lib/dev/liblgx_mlp_noemit.so "" $R/legged_gym_custom_amd/lib/dev/liblgx_mlp_noemit.so; do
+  LGX_MLP_LIB=$L PYTHONPATH=$R:$R/tests timeout -k 10 200 python tools/tail_ab.py 2>&1 | tail -1 || exit 1
+done
