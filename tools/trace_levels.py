@@ -1,5 +1,6 @@
 """Per-launch medians of the update's minibatch sequence from a rocprofv3 kernel trace (dev tool):
-the launches between consecutive s8_split_kernel dispatches (one minibatch of tools/s8_mb_ab.py),
+the launches between consecutive minibatch-start dispatches (the encoder chain launch, lgxc::chain_kernel,
+since round 6 the first launch of a minibatch: the weight split runs once per update),
 position by position, and the median span of a minibatch.
 Usage: python tools/trace_levels.py <run_kernel_trace.csv> [...]"""
 import collections
@@ -13,7 +14,7 @@ def levels(path):
     seqs, cur = [], None
     for r in rows:
         short = r["Kernel_Name"].split("(")[0].replace("void ", "")
-        if "s8_split_kernel" in short:
+        if "lgxc::chain_kernel" in short:
             if cur:
                 seqs.append(cur)
             cur = []
