@@ -2082,9 +2082,8 @@ __device__ __forceinline__ void ppo_tail_body(const lgx_ppo_head_args& p, const 
   extern __shared__ __align__(16) float tl[];
   __shared__ float stdv[HMAXA], lstd[HMAXA];
   // the head rows' inputs (act | old_sigma | old_mu | old_logp adv tv R), later their sums
-  __shared__ float hin_[TR * (3 * NA + 4 > NV + 1 ? 3 * NA + 4 : NV + 1)];
+  __shared__ float hin_[TR * (3 * NA + 4)];
   float(*hin)[3 * NA + 4] = reinterpret_cast<float(*)[3 * NA + 4]>(hin_);
-  float(*vred)[NV + 1] = reinterpret_cast<float(*)[NV + 1]>(hin_);
   const int H = t.H, Hc = t.Hc, PH = tail_pitch(H), PC = tail_pitch(Hc), A = p.A;
   float* ys = tl;                   // [TR][PH]
   float* yc = ys + TR * PH;         // [TR][PC]
@@ -2203,35 +2202,105 @@ __device__ __forceinline__ void ppo_tail_body(const lgx_ppo_head_args& p, const 
   __syncthreads();
   TCK(1);
   const float gs = p.g[0] / p.B, gv = p.g[1] / p.B, ge = p.g[2];
-  float v[NV];
-#pragma unroll
-  for (int k = 0; k < NV; ++k) v[k] = 0.f;
+  // The PPO head rows (head_fused_row's arithmetic, bit for bit) with the per-action work spread
+  // over (row, action) threads: (1) each action's log-prob and KL terms; (2) per row, their sums in
+  // action order, the ratio, the clip / max decisions, the value loss and dlogp; (3) each action's
+  // dmu and std-gradient term. The row sums are the serial sums of head_fused_row (same order).
+  __shared__ float tlp[TR][NA], tkl[TR][NA];  // log-prob / KL terms (then tvs: std-gradient terms)
+  __shared__ float rowv[TR][4];                // surrogate, value loss, KL, dlogp
+  float(*tvs)[NA] = tlp;                       // the log-prob terms are dead after the row sums
+  for (int o = tid; o < TR * NA; o += blockDim.x) {
+    const int r = o / NA, j = o % NA;
+    const float sd = stdv[j], mu = mus[r * NA + min(j, A - 1)];
+    const float d = hin[r][j] - mu;
+    tlp[r][j] = -(d * d) / (2.f * sd * sd) - lstd[j] - 0.9189385332046727f;
+    const float os = hin[r][NA + j], dm = hin[r][2 * NA + j] - mu;
+    tkl[r][j] = logf(sd / os + 1.0e-5f) + (os * os + dm * dm) / (2.f * (sd * sd)) - 0.5f;
+  }
+  __syncthreads();
   if (tid < TR) {
-    float dmu[NA], dv = 0.f;
-#pragma unroll
-    for (int j = 0; j < NA; ++j) dmu[j] = 0.f;
     const int i = r0 + tid;
+    float r4[4] = {0.f, 0.f, 0.f, 0.f}, dv = 0.f;
     if (i < p.B) {
-      float mu[NA];
-      HeadIn<NA> x;
+      float lp = 0.f;
 #pragma unroll
-      for (int j = 0; j < NA; ++j) {
-        mu[j] = mus[tid * NA + min(j, A - 1)];  // load_cols' clamped columns
-        x.act[j] = hin[tid][j];
-        x.os[j] = hin[tid][NA + j];
-        x.om[j] = hin[tid][2 * NA + j];
+      for (int j = 0; j < NA; ++j) lp = j < A ? lp + tlp[tid][j] : lp;
+      const float ratio = expf(lp - hin[tid][3 * NA]);
+      const float a = hin[tid][3 * NA + 1];
+      const float lo = 1.f - p.clip, hi = 1.f + p.clip;
+      const float s1 = -a * ratio, s2 = -a * fminf(fmaxf(ratio, lo), hi);
+      const float R = hin[tid][3 * NA + 3], val = vals[tid];
+      const float tv = p.clipped_value ? hin[tid][3 * NA + 2] : val;
+      const float vc = p.clipped_value ? tv + fminf(fmaxf(val - tv, -p.clip), p.clip) : 0.f;
+      const float l1 = (val - R) * (val - R), l2 = (vc - R) * (vc - R);
+      float w1 = s1 > s2 ? 1.f : (s1 == s2 ? 0.5f : 0.f);
+      float in = (ratio >= lo && ratio <= hi) ? 1.f : 0.f;
+      float u1 = l1 > l2 ? 1.f : (l1 == l2 ? 0.5f : 0.f);
+      float inv = (val - tv >= -p.clip && val - tv <= p.clip) ? 1.f : 0.f;
+      if (s.decisions_out)
+        s.decisions_out[i] = (uint8_t)((unsigned)(2.f * w1) | ((unsigned)in << 2) | ((unsigned)(2.f * u1) << 3) |
+                                       ((unsigned)inv << 5));
+      const bool forced = s.decisions_in != nullptr && !(s.decisions_in[i] & 0x40u);
+      if (forced) {
+        const unsigned dd = s.decisions_in[i];
+        w1 = 0.5f * (float)(dd & 3u);
+        in = (float)((dd >> 2) & 1u);
+        u1 = 0.5f * (float)((dd >> 3) & 3u);
+        inv = (float)((dd >> 5) & 1u);
       }
-      x.old_logp = hin[tid][3 * NA];
-      x.adv = hin[tid][3 * NA + 1];
-      x.tv = hin[tid][3 * NA + 2];
-      x.R = hin[tid][3 * NA + 3];
-      head_fused_row<NA>(p, s, i, stdv, lstd, mu, vals[tid], x, gs, gv, v, dmu, dv);
+      if (!forced) {
+        r4[0] = 0.f + fmaxf(s1, s2);
+        r4[1] = 0.f + (p.clipped_value ? fmaxf(l1, l2) : (R - val) * (R - val));
+      } else {
+        r4[0] = 0.f + (w1 > 0.75f ? s1 : (w1 < 0.25f ? s2 : fmaxf(s1, s2)));
+        r4[1] = 0.f + (p.clipped_value ? (u1 > 0.75f ? l1 : (u1 < 0.25f ? l2 : fmaxf(l1, l2))) : (R - val) * (R - val));
+      }
+      float kl = 0.f;
+#pragma unroll
+      for (int j = 0; j < NA; ++j) kl = j < A ? kl + tkl[tid][j] : kl;
+      r4[2] = 0.f + kl;
+      const float w2 = 1.f - w1;
+      const float dratio = gs * (w1 * -a + w2 * -a * in);
+      r4[3] = dratio * ratio;  // dlogp
+      if (p.clipped_value) dv = gv * (u1 * 2.f * (val - R) + (1.f - u1) * 2.f * (vc - R) * inv);
+      else dv = gv * 2.f * (val - R);
+      if (p.dvalue) p.dvalue[i] = dv;
+      if (s.dvalue_s8) {
+        const float q[8] = {dv, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        store_s8_group(static_cast<char*>(s.dvalue_s8) + (int64_t)i * s.ld_dvalue * 4, q);
+      }
     }
 #pragma unroll
-    for (int j = 0; j < NA; ++j) dmus[tid * NA + j] = j < A ? dmu[j] : 0.f;
+    for (int k = 0; k < 4; ++k) rowv[tid][k] = r4[k];
     dvs[tid] = dv;
   }
   __syncthreads();
+  for (int o = tid; o < TR * NA; o += blockDim.x) {
+    const int r = o / NA, j = o % NA, i = r0 + r;
+    float dmu = 0.f, vs = 0.f;
+    if (i < p.B && j < A) {
+      const float sd = stdv[j], dlogp = rowv[r][3];
+      const float d = hin[r][j] - mus[r * NA + j];
+      const float var = sd * sd;
+      dmu = dlogp * d / var;
+      if (p.dmu) p.dmu[(int64_t)i * p.A + j] = dmu;
+      vs = 0.f + dlogp * (d * d / (var * sd) - 1.f / sd);
+    }
+    dmus[r * NA + j] = dmu;
+    tvs[r][j] = vs;
+  }
+  __syncthreads();
+  if (s.dmu_s8) {  // the rows' dmu as S8 groups (columns past A zero)
+    constexpr int GN = (NA + 7) / 8;
+    for (int o = tid; o < TR * GN; o += blockDim.x) {
+      const int r = o / GN, g0 = 8 * (o % GN), i = r0 + r;
+      if (i >= p.B || g0 >= A) continue;
+      float q[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) q[e] = g0 + e < NA ? dmus[r * NA + g0 + e] : 0.f;
+      store_s8_group(static_cast<char*>(s.dmu_s8) + ((int64_t)i * s.ld_dmu + g0) * 4, q);
+    }
+  }
   TCK(2);
   // the last layers' input gradients, in place of y / y_c: (dmu W) * ELU'(y), (dvalue W_c) * ELU'(y_c)
   {
@@ -2296,14 +2365,15 @@ __device__ __forceinline__ void ppo_tail_body(const lgx_ppo_head_args& p, const 
   // dstd partial with the entropy term ge / std; the launch's totals are flat sums of these
   // (lgx_s8_reduce jobs of the caller). Block 0 writes the entropy (a constant) into out[2].
   TCK(4);
-  // the block's sums: only the TR head threads hold values; rows through LDS, summed in row order
-  if (tid < TR)
-#pragma unroll
-    for (int k = 0; k < NV; ++k) vred[tid][k] = v[k];
-  __syncthreads();
+  // the block's sums of the rows' values, summed in row order
   if (tid < NV) {
     float sum = 0.f;
-    for (int q = 0; q < TR; ++q) sum += vred[q][tid];
+    for (int q = 0; q < TR; ++q) {
+      const float x = tid < 3 ? rowv[q][tid]
+                              : (tid < 3 + NA ? tvs[q][tid - 3]
+                                              : (tid < 3 + 2 * NA ? dmus[q * NA + tid - 3 - NA] : dvs[q]));
+      sum += x;
+    }
     const float inv = 1.f / p.B;
     float* w = p.ws + (int64_t)bx * (3 + HMAXA);
     if (tid < 3) w[tid] = sum * inv;
