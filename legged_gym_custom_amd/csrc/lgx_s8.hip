@@ -1069,7 +1069,9 @@ int32_t lgx_s8_pick_split(const int32_t* M, const int32_t* N, const int32_t* K, 
     tiles += (int64_t)cdiv(M[i], lgxs::Cfg::BM) * cdiv(N[i], lgxs::BN);
     kmax = std::max<int64_t>(kmax, K[i]);
   }
-  const int64_t s = std::max<int64_t>(1, tiles ? 512 / tiles : 1);
+  int64_t slots = 512;  // 2 blocks per CU x 256 CUs
+  if (const char* e = LGX_DEV_KNOB("LGX_S8_DW_SLOTS")) slots = std::max(1, atoi(e));  // dev knob
+  const int64_t s = std::max<int64_t>(1, tiles ? slots / tiles : 1);
   const int64_t chunk = ((kmax + s - 1) / s + lgxs::BK - 1) / lgxs::BK * lgxs::BK;
   for (int i = 0; i < n; ++i) out[i] = std::max(1, cdiv(K[i], (int)std::max<int64_t>(chunk, lgxs::BK)));
   return 0;
