@@ -1,8 +1,8 @@
-"""Phase clocks of lgx_loss_heads_tail (dev tool, GPU): LGX_MLP_LIB=exp/mlp_clock.so (lgx_mlp.hip
+"""Phase clocks of lgx_loss_heads_tail (dev tool, GPU): LGX_MLP_LIB=legged_gym_custom_amd/lib/dev/liblgx_mlp_clock.so (lgx_mlp.hip
 built with -DLGX_TAIL_CLOCK) runs the launch at the go2 minibatch size (24,576 rows, A 12, H 128)
 and prints per-block cycles of: input loads | last layers' forward | PPO head rows | input
 gradients | column sums | block sum | total, plus the launch time (HIP events).
-Usage: LGX_MLP_LIB=exp/mlp_clock.so PYTHONPATH=. python tools/tail_clock.py"""
+Usage: LGX_MLP_LIB=legged_gym_custom_amd/lib/dev/liblgx_mlp_clock.so PYTHONPATH=. python tools/tail_clock.py"""
 import ctypes as C
 
 import numpy as np
