@@ -3266,8 +3266,7 @@ int32_t lgx_ppo_tail(const lgx_ppo_tail_args* a, void* stream) {
 #define LGX_TAIL_ELEMS 1024
 #endif
     constexpr int64_t TAIL_ELEMS = LGX_TAIL_ELEMS;  // elements per block (one float4 per thread)
-    static lgxm::TailK k;
-    k = lgxm::TailK{};
+    lgxm::TailK k{};  // ~3.4 KB, copied into the launch's argument segment by the launch
     k.p = *a;
     for (int i = 0; i < a->n_s8; ++i) {
       const lgx_tail_s8_seg& q = a->s8[i];
